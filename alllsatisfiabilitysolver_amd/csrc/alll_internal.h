@@ -1,0 +1,79 @@
+// alll_internal.h -- shared between the HIP kernels (alll_kernels.hip) and the host runtime
+// (alll_runtime.cpp).  Not part of the public ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace alll {
+
+// Clauses per tile.  A tile is the unit of evaluation (one 256-thread workgroup), of the
+// violated-clause staging lists and of the LFMIS round kernels.
+constexpr uint32_t TILE = 4096;
+constexpr uint32_t TILE_WORDS = TILE / 64;   // violated-bitmask words per tile
+constexpr uint32_t CHUNK = 256;              // clauses per transposed literal chunk
+constexpr int EVAL_THREADS = 256;
+constexpr int ROUND_THREADS = 256;
+constexpr int TAIL_THREADS = 1024;
+constexpr int MAX_FIXED_K = 8;
+
+// Device-resident loop state.  Written only by the single-block reduce / tail kernels,
+// read by every other kernel at entry (kernel boundaries order the accesses).
+struct DevState {
+    uint64_t n_iter;       // eval passes executed (Statistics::n_iterations)
+    uint64_t limit_eval;   // eval passes allowed (kernels skip once n_iter >= limit_eval)
+    uint64_t limit_nores;  // an eval pass with n_iter == limit_nores does not resample
+    uint64_t u_total;      // violated clauses of the last eval pass
+    uint64_t count_out;    // standalone eval count (verify / bench_eval)
+    uint32_t done;         // 0 running, 1 solved, 2 stopped at limit_nores
+    uint32_t active;       // the current iteration runs MIS + resample
+    uint32_t stamp;        // cover stamp of the current iteration (never 0)
+    uint32_t round_base;   // owner-key epoch of grid round 0 of the current iteration
+    uint32_t round_next;   // first unused epoch
+    uint32_t tail_rounds;  // rounds the tail kernel needed in the last iteration
+    uint32_t max_rounds;   // max total rounds seen in one iteration
+    uint32_t pad;
+};
+
+// Clause storage on the device.
+struct ClauseView {
+    const uint32_t* offs;   // generic CSR: m+1 offsets (uint32); nullptr in fixed-k layout
+    const uint32_t* lits;   // AoS literals (CSR order; fixed-k: lits[c*k + j])
+    const uint32_t* lits_t; // fixed-k only: chunk-transposed [c/256][j][c%256]
+    uint64_t m;             // clauses
+    uint32_t k;             // fixed width, 0 = generic CSR
+};
+
+struct LoopBuffers {
+    uint32_t* A;            // bit-packed assignment, ceil(n/32) words
+    uint64_t* vmask;        // violated bitmask, n_tiles_padded * TILE_WORDS words
+    uint32_t* tile_cnt;     // undecided violated entries per tile
+    uint32_t* stage;        // per tile: TILE slots of undecided violated clause ids
+    uint32_t* mis_cnt;      // MIS entries per tile (current iteration)
+    uint32_t* mis;          // per tile: TILE slots of MIS clause ids
+    unsigned long long* owner; // per variable 64-bit owner key (epoch-tagged, never reset)
+    uint32_t* cover;        // per variable: stamp of the iteration whose MIS covers it
+    unsigned long long* tile_stats; // per tile: [2t] sum |MIS|, [2t+1] sum resampled literals
+    uint32_t* delta;        // allreduce exchange: per-iteration assignment XOR delta
+    DevState* state;
+    uint32_t n_vars;
+    uint32_t n_words;
+    uint32_t n_tiles;       // tiles covering [0, m)
+    uint64_t seed;
+};
+
+// Launchers (alll_kernels.hip).  All asynchronous on `s`.
+hipError_t launch_init_assignment(const LoopBuffers& b, hipStream_t s);
+hipError_t launch_init_state(const LoopBuffers& b, hipStream_t s);
+hipError_t launch_eval(const ClauseView& cv, const LoopBuffers& b, uint32_t tile_begin,
+                       uint32_t tile_end, bool gated, hipStream_t s);
+hipError_t launch_collect(const ClauseView& cv, const LoopBuffers& b, uint32_t own_begin,
+                          uint32_t own_end, hipStream_t s);
+hipError_t launch_reduce(const LoopBuffers& b, int mode, hipStream_t s);
+hipError_t launch_round(const ClauseView& cv, const LoopBuffers& b, uint32_t r, hipStream_t s);
+hipError_t launch_tail(const ClauseView& cv, const LoopBuffers& b, uint32_t first_round,
+                       hipStream_t s);
+hipError_t launch_resample(const ClauseView& cv, const LoopBuffers& b, uint32_t tile_begin,
+                           uint32_t tile_end, bool to_delta, hipStream_t s);
+hipError_t launch_apply_delta(const LoopBuffers& b, hipStream_t s);
+
+}  // namespace alll

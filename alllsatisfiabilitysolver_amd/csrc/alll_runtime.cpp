@@ -1,0 +1,602 @@
+// alll_runtime.cpp -- host side of the C-ABI (include/alll.h): device memory layout,
+// the per-iteration launch sequence (captured once into a hipGraph), the RCCL exchange of
+// the clause-sharded multi-GPU mode, statistics.
+//
+// Reference correspondence: alll_create ~ SATInstance(var_arr, n_threads) +
+// VariablesArray(n_vars) (SATInstance.h:51-56, VariablesArray.h:23-34); alll_solve ~
+// SATInstance::solve -> parallel_solve (SATInstance.h:60-66, 217-320); alll_verify ~
+// verify_validity (SATInstance.h:156-173).
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "alll.h"
+#include "alll_internal.h"
+
+using namespace alll;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                    \
+    do {                                                                                 \
+        hipError_t _e = (expr);                                                          \
+        if (_e != hipSuccess)                                                            \
+            return fail(ALLL_ERR_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), \
+                        __FILE__, __LINE__);                                             \
+    } while (0)
+
+#define NCCL_TRY(expr)                                                                    \
+    do {                                                                                  \
+        ncclResult_t _r = (expr);                                                         \
+        if (_r != ncclSuccess)                                                            \
+            return fail(ALLL_ERR_RCCL, "%s failed: %s", #expr, ncclGetErrorString(_r));  \
+    } while (0)
+
+constexpr uint32_t DEFAULT_GRID_ROUNDS = 4;
+
+}  // namespace
+
+struct alll_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    alll_options opt{};
+    uint32_t n_vars = 0;
+    uint64_t m = 0;
+    uint64_t n_lits = 0;
+    ClauseView cv{};
+    LoopBuffers b{};
+    uint32_t tiles_per_rank = 0, own_begin = 0, own_end = 0, n_tiles_padded = 0;
+    uint32_t grid_rounds = DEFAULT_GRID_ROUNDS;
+    int rank = 0, world = 1;
+    bool allreduce = false;
+    ncclComm_t comm = nullptr;
+    // device allocations
+    std::vector<void*> allocs;
+    DevState* h_state = nullptr;  // pinned mirror
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t graph_exec = nullptr;
+    bool use_graph = true;
+    hipEvent_t ev[8] = {};
+};
+
+namespace {
+
+template <typename T>
+int dalloc(alll_ctx* c, T** p, size_t count, int fill = 0) {
+    size_t bytes = std::max<size_t>(count * sizeof(T), 16);
+    void* q = nullptr;
+    hipError_t e = hipMalloc(&q, bytes);
+    if (e != hipSuccess)
+        return fail(ALLL_ERR_OOM, "hipMalloc(%zu bytes) failed: %s", bytes, hipGetErrorString(e));
+    c->allocs.push_back(q);
+    e = hipMemsetAsync(q, fill, bytes, c->stream);
+    if (e != hipSuccess) return fail(ALLL_ERR_HIP, "hipMemsetAsync failed: %s", hipGetErrorString(e));
+    *p = static_cast<T*>(q);
+    return ALLL_OK;
+}
+
+int read_state(alll_ctx* c) {
+    HIP_TRY(hipMemcpyAsync(c->h_state, c->b.state, sizeof(DevState), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return ALLL_OK;
+}
+
+int write_limits(alll_ctx* c, uint64_t limit_eval, uint64_t limit_nores) {
+    // called only with the stream drained (after read_state)
+    c->h_state->limit_eval = limit_eval;
+    c->h_state->limit_nores = limit_nores;
+    if (c->h_state->done == 2) c->h_state->done = 0;
+    HIP_TRY(hipMemcpyAsync(c->b.state, c->h_state, sizeof(DevState), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return ALLL_OK;
+}
+
+// The launch sequence of one iteration (SATInstance.h:260-311).  Every kernel is gated on
+// the device state, so replaying it after convergence is a no-op.
+int enqueue_iteration(alll_ctx* c, hipEvent_t* marks) {
+    hipStream_t s = c->stream;
+    if (marks) HIP_TRY(hipEventRecord(marks[0], s));
+    HIP_TRY(launch_eval(c->cv, c->b, c->own_begin, c->own_end, true, s));
+    if (marks) HIP_TRY(hipEventRecord(marks[1], s));
+    if (c->world > 1) {
+        const size_t words = (size_t)c->tiles_per_rank * TILE_WORDS;
+        NCCL_TRY(ncclAllGather(c->b.vmask + (size_t)c->rank * words, c->b.vmask, words, ncclUint64,
+                               c->comm, s));
+        HIP_TRY(launch_collect(c->cv, c->b, c->own_begin, c->own_end, s));
+    }
+    if (marks) HIP_TRY(hipEventRecord(marks[2], s));
+    HIP_TRY(launch_reduce(c->b, 0, s));
+    for (uint32_t r = 0; r < c->grid_rounds; ++r) HIP_TRY(launch_round(c->cv, c->b, r, s));
+    HIP_TRY(launch_tail(c->cv, c->b, c->grid_rounds, s));
+    if (marks) HIP_TRY(hipEventRecord(marks[3], s));
+    if (c->allreduce && c->world > 1) {
+        HIP_TRY(launch_resample(c->cv, c->b, c->own_begin, c->own_end, true, s));
+        NCCL_TRY(ncclAllReduce(c->b.delta, c->b.delta, c->b.n_words, ncclUint32, ncclSum, c->comm, s));
+        HIP_TRY(launch_apply_delta(c->b, s));
+    } else {
+        HIP_TRY(launch_resample(c->cv, c->b, c->own_begin, c->own_end, false, s));
+    }
+    if (marks) HIP_TRY(hipEventRecord(marks[4], s));
+    return ALLL_OK;
+}
+
+int ensure_graph(alll_ctx* c) {
+    if (!c->use_graph || c->graph_exec) return ALLL_OK;
+    hipError_t e = hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal);
+    if (e != hipSuccess) { c->use_graph = false; return ALLL_OK; }
+    int rc = enqueue_iteration(c, nullptr);
+    hipGraph_t g = nullptr;
+    e = hipStreamEndCapture(c->stream, &g);
+    if (rc != ALLL_OK || e != hipSuccess || !g) {
+        if (g) (void)hipGraphDestroy(g);
+        (void)hipGetLastError();
+        c->use_graph = false;  // fall back to eager launches
+        return ALLL_OK;
+    }
+    e = hipGraphInstantiate(&c->graph_exec, g, nullptr, nullptr, 0);
+    if (e != hipSuccess) {
+        (void)hipGraphDestroy(g);
+        c->graph_exec = nullptr;
+        c->use_graph = false;
+        return ALLL_OK;
+    }
+    c->graph = g;
+    return ALLL_OK;
+}
+
+int launch_iterations(alll_ctx* c, uint64_t n) {
+    int rc = ensure_graph(c);
+    if (rc) return rc;
+    for (uint64_t i = 0; i < n; ++i) {
+        if (c->use_graph) {
+            HIP_TRY(hipGraphLaunch(c->graph_exec, c->stream));
+        } else {
+            rc = enqueue_iteration(c, nullptr);
+            if (rc) return rc;
+        }
+    }
+    return ALLL_OK;
+}
+
+int fill_stats(alll_ctx* c, alll_stats* st) {
+    int rc = read_state(c);
+    if (rc) return rc;
+    std::vector<unsigned long long> ts(2 * (size_t)c->b.n_tiles);
+    if (!ts.empty())
+        HIP_TRY(hipMemcpy(ts.data(), c->b.tile_stats, ts.size() * 8, hipMemcpyDeviceToHost));
+    memset(st, 0, sizeof(*st));
+    st->n_iterations = c->h_state->n_iter;
+    for (uint32_t t = 0; t < c->b.n_tiles; ++t) {
+        st->sum_mis_size += ts[2 * t];
+        st->n_resamples += ts[2 * t + 1];
+        const uint32_t r = c->tiles_per_rank ? t / c->tiles_per_rank : 0;
+        if (r < ALLL_MAX_GPU_STATS) st->gpu_resamples[r] += ts[2 * t + 1];
+    }
+    st->avg_mis_size = st->n_iterations ? st->sum_mis_size / st->n_iterations : 0;
+    st->n_violated = c->h_state->u_total;
+    st->solved = (c->h_state->done == 1) ? 1 : 0;
+    st->n_gpus = c->world;
+    return ALLL_OK;
+}
+
+bool is_gfx950(int dev) {
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, dev) != hipSuccess) return false;
+    return strncmp(p.gcnArchName, "gfx950", 6) == 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* alll_version(void) { return "alll-mi355x 0.1.0 (abi 1, gfx950)"; }
+const char* alll_last_error(void) { return g_err.c_str(); }
+void alll_internal_set_error(const char* msg) { g_err = msg ? msg : ""; }
+
+void alll_default_options(alll_options* o) {
+    if (!o) return;
+    memset(o, 0, sizeof(*o));
+    o->seed = 1;
+    o->max_iters = 0;
+    o->device = -1;
+    o->n_threads = 1;
+    o->rank = 0;
+    o->world = 1;
+    o->flags = 0;
+    o->grid_rounds = 0;
+}
+
+int alll_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    return n;
+}
+
+int alll_comm_unique_id(uint8_t out[128]) {
+    if (!out) return fail(ALLL_ERR_INVALID_ARG, "null output");
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    ncclUniqueId id;
+    NCCL_TRY(ncclGetUniqueId(&id));
+    memcpy(out, &id, 128);
+    return ALLL_OK;
+}
+
+int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx** out) {
+    if (!prob || !out) return fail(ALLL_ERR_INVALID_ARG, "null argument");
+    *out = nullptr;
+    alll_options opt;
+    if (opt_in) opt = *opt_in; else alll_default_options(&opt);
+    if (opt.world < 1 || opt.rank < 0 || opt.rank >= opt.world)
+        return fail(ALLL_ERR_INVALID_ARG, "bad rank %d / world %d", opt.rank, opt.world);
+    if (opt.world > ALLL_MAX_GPU_STATS) return fail(ALLL_ERR_UNSUPPORTED, "world > %d", ALLL_MAX_GPU_STATS);
+    const uint64_t m = prob->n_clauses;
+    if (m && (!prob->offsets)) return fail(ALLL_ERR_INVALID_ARG, "null offsets");
+    if (m >= 0xFFFFFFFFull - TILE) return fail(ALLL_ERR_UNSUPPORTED, "more than 2^32-4097 clauses");
+    // ---- validate the CSR on the host (the reference has UB here: Clause.h:40)
+    const uint64_t L = m ? prob->offsets[m] : 0;
+    if (m && prob->offsets[0] != 0) return fail(ALLL_ERR_BAD_INPUT, "offsets[0] != 0");
+    if (L && !prob->literals) return fail(ALLL_ERR_INVALID_ARG, "null literals");
+    if (L >= 0xFFFFFFFFull) return fail(ALLL_ERR_UNSUPPORTED, "more than 2^32-1 literals");
+    int fixed_k = -1;
+    for (uint64_t c = 0; c < m; ++c) {
+        if (prob->offsets[c + 1] < prob->offsets[c]) return fail(ALLL_ERR_BAD_INPUT, "offsets decrease at %llu", (unsigned long long)c);
+        const int64_t w = (int64_t)(prob->offsets[c + 1] - prob->offsets[c]);
+        if (fixed_k == -1) fixed_k = (int)std::min<int64_t>(w, 1 << 30);
+        else if (fixed_k != w) fixed_k = 0;
+    }
+    if (fixed_k < 1 || fixed_k > MAX_FIXED_K || (opt.flags & ALLL_FLAG_GENERIC_CSR)) fixed_k = 0;
+    const uint64_t lim = 2ull * prob->n_vars;
+    for (uint64_t j = 0; j < L; ++j)
+        if (prob->literals[j] >= lim)
+            return fail(ALLL_ERR_LITERAL_RANGE, "literal %u at position %llu exceeds n_vars %u",
+                        prob->literals[j], (unsigned long long)j, prob->n_vars);
+
+    // ---- device
+    int ndev = alll_device_count();
+    if (ndev <= 0) return fail(ALLL_ERR_NO_DEVICE, "no HIP device visible");
+    int dev = opt.device;
+    if (dev < 0) { if (hipGetDevice(&dev) != hipSuccess) dev = 0; }
+    if (dev >= ndev) return fail(ALLL_ERR_NO_DEVICE, "device %d not visible (%d devices)", dev, ndev);
+    if (!is_gfx950(dev)) return fail(ALLL_ERR_NO_DEVICE, "device %d is not gfx950 (MI355X)", dev);
+    HIP_TRY(hipSetDevice(dev));
+
+    alll_ctx* c = new (std::nothrow) alll_ctx();
+    if (!c) return fail(ALLL_ERR_OOM, "host allocation failed");
+    c->device = dev;
+    c->opt = opt;
+    c->n_vars = prob->n_vars;
+    c->m = m;
+    c->n_lits = L;
+    c->rank = opt.rank;
+    c->world = opt.world;
+    c->allreduce = (opt.flags & ALLL_FLAG_EXCHANGE_ALLREDUCE) != 0;
+    c->use_graph = (opt.flags & ALLL_FLAG_NO_GRAPH) == 0;
+    c->grid_rounds = opt.grid_rounds ? opt.grid_rounds : DEFAULT_GRID_ROUNDS;
+    auto bail = [&](int rc) { alll_destroy(c); return rc; };
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+        return bail(fail(ALLL_ERR_HIP, "hipStreamCreate failed"));
+    for (auto& e : c->ev)
+        if (hipEventCreate(&e) != hipSuccess) return bail(fail(ALLL_ERR_HIP, "hipEventCreate failed"));
+    if (hipHostMalloc((void**)&c->h_state, sizeof(DevState), 0) != hipSuccess)
+        return bail(fail(ALLL_ERR_OOM, "hipHostMalloc failed"));
+
+    // ---- tiles and shards (contiguous clause ranges; concatenation = clause order)
+    const uint32_t n_tiles = (uint32_t)((m + TILE - 1) / TILE);
+    c->tiles_per_rank = (n_tiles + c->world - 1) / c->world;
+    if (c->tiles_per_rank == 0) c->tiles_per_rank = 1;
+    c->n_tiles_padded = c->tiles_per_rank * c->world;
+    c->own_begin = std::min<uint32_t>(n_tiles, (uint32_t)c->rank * c->tiles_per_rank);
+    c->own_end = std::min<uint32_t>(n_tiles, c->own_begin + c->tiles_per_rank);
+
+    int rc;
+    LoopBuffers& b = c->b;
+    b.n_vars = c->n_vars;
+    b.n_words = (c->n_vars + 31) / 32;
+    b.n_tiles = n_tiles;
+    b.seed = opt.seed;
+    if ((rc = dalloc(c, &b.A, b.n_words))) return bail(rc);
+    if ((rc = dalloc(c, &b.vmask, (size_t)c->n_tiles_padded * TILE_WORDS))) return bail(rc);
+    if ((rc = dalloc(c, &b.tile_cnt, n_tiles))) return bail(rc);
+    if ((rc = dalloc(c, &b.mis_cnt, n_tiles))) return bail(rc);
+    if ((rc = dalloc(c, &b.stage, (size_t)n_tiles * TILE))) return bail(rc);
+    if ((rc = dalloc(c, &b.mis, (size_t)n_tiles * TILE))) return bail(rc);
+    if ((rc = dalloc(c, &b.owner, c->n_vars, 0xFF))) return bail(rc);
+    if ((rc = dalloc(c, &b.cover, c->n_vars))) return bail(rc);
+    if ((rc = dalloc(c, &b.tile_stats, 2 * (size_t)n_tiles))) return bail(rc);
+    if ((rc = dalloc(c, &b.delta, b.n_words))) return bail(rc);
+    if ((rc = dalloc(c, &b.state, 1))) return bail(rc);
+    // ---- clause storage allocations, then drain the zero-fills before synchronous uploads
+    ClauseView& cv = c->cv;
+    cv.m = m;
+    cv.k = (uint32_t)fixed_k;
+    uint32_t *d_lits = nullptr, *d_t = nullptr, *d_o = nullptr;
+    const uint64_t real_chunks = (m + CHUNK - 1) / CHUNK;
+    if ((rc = dalloc(c, &d_lits, L))) return bail(rc);
+    if (fixed_k > 0) {
+        if ((rc = dalloc(c, &d_t, real_chunks * CHUNK * fixed_k))) return bail(rc);
+    } else {
+        if ((rc = dalloc(c, &d_o, m + 1))) return bail(rc);
+    }
+    if (hipStreamSynchronize(c->stream) != hipSuccess) return bail(fail(ALLL_ERR_HIP, "memset drain failed"));
+
+    // ---- clauses: AoS literals (+ offsets or a chunk-transposed copy for fixed width k)
+    if (L && hipMemcpy(d_lits, prob->literals, L * 4, hipMemcpyHostToDevice) != hipSuccess)
+        return bail(fail(ALLL_ERR_HIP, "literal upload failed"));
+    cv.lits = d_lits;
+    if (fixed_k > 0) {
+        std::vector<uint32_t> t(real_chunks * CHUNK * fixed_k, 0u);
+        for (uint64_t cl = 0; cl < m; ++cl) {
+            const uint64_t g = cl / CHUNK, r = cl % CHUNK;
+            for (int j = 0; j < fixed_k; ++j)
+                t[(g * fixed_k + j) * CHUNK + r] = prob->literals[cl * fixed_k + j];
+        }
+        if (!t.empty() && hipMemcpy(d_t, t.data(), t.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+            return bail(fail(ALLL_ERR_HIP, "transposed literal upload failed"));
+        cv.lits_t = d_t;
+        cv.offs = nullptr;
+    } else {
+        std::vector<uint32_t> o32(m + 1);
+        for (uint64_t i = 0; i <= m; ++i) o32[i] = m ? (uint32_t)prob->offsets[i] : 0u;
+        if (hipMemcpy(d_o, o32.data(), (m + 1) * 4, hipMemcpyHostToDevice) != hipSuccess)
+            return bail(fail(ALLL_ERR_HIP, "offset upload failed"));
+        cv.offs = d_o;
+    }
+
+    // ---- state + initial assignment
+    memset(c->h_state, 0, sizeof(DevState));
+    c->h_state->limit_eval = ~0ull;
+    c->h_state->limit_nores = ~0ull;
+    c->h_state->round_next = 1;
+    if (hipMemcpyAsync(b.state, c->h_state, sizeof(DevState), hipMemcpyHostToDevice, c->stream) != hipSuccess)
+        return bail(fail(ALLL_ERR_HIP, "state upload failed"));
+    if (launch_init_assignment(b, c->stream) != hipSuccess)
+        return bail(fail(ALLL_ERR_HIP, "init kernel launch failed"));
+
+    // ---- RCCL communicator (clause-sharded mode)
+    if (c->world > 1) {
+        ncclUniqueId id;
+        memcpy(&id, opt.comm_id, 128);
+        ncclResult_t r = ncclCommInitRank(&c->comm, c->world, id, c->rank);
+        if (r != ncclSuccess) return bail(fail(ALLL_ERR_RCCL, "ncclCommInitRank: %s", ncclGetErrorString(r)));
+    }
+    if (hipStreamSynchronize(c->stream) != hipSuccess)
+        return bail(fail(ALLL_ERR_HIP, "create: stream sync failed: %s", hipGetErrorString(hipGetLastError())));
+    *out = c;
+    return ALLL_OK;
+}
+
+int alll_destroy(alll_ctx* c) {
+    if (!c) return ALLL_OK;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->graph_exec) (void)hipGraphExecDestroy(c->graph_exec);
+    if (c->graph) (void)hipGraphDestroy(c->graph);
+    if (c->comm) ncclCommDestroy(c->comm);
+    for (void* p : c->allocs) (void)hipFree(p);
+    for (auto& e : c->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->h_state) (void)hipHostFree(c->h_state);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return ALLL_OK;
+}
+
+int alll_solve(alll_ctx* c, alll_stats* st) {
+    if (!c) return fail(ALLL_ERR_INVALID_ARG, "null context");
+    HIP_TRY(hipSetDevice(c->device));
+    int rc = read_state(c);
+    if (rc) return rc;
+    const uint64_t cap = c->opt.max_iters ? c->opt.max_iters : ~0ull;
+    if (c->h_state->done != 1) {
+        if ((rc = write_limits(c, cap, cap))) return rc;
+        uint64_t batch = 1;
+        for (;;) {
+            if ((rc = launch_iterations(c, batch))) return rc;
+            if ((rc = read_state(c))) return rc;
+            if (c->h_state->done || c->h_state->n_iter >= cap) break;
+            batch = std::min<uint64_t>(batch * 2, 64);
+        }
+    }
+    alll_stats tmp;
+    if ((rc = fill_stats(c, st ? st : &tmp))) return rc;
+    if (c->h_state->done != 1)
+        return fail(ALLL_ERR_MAX_ITERS, "not solved after %llu eval passes (%llu clauses violated)",
+                    (unsigned long long)c->h_state->n_iter, (unsigned long long)c->h_state->u_total);
+    return ALLL_OK;
+}
+
+int alll_run(alll_ctx* c, uint64_t n_iters, alll_stats* st) {
+    if (!c) return fail(ALLL_ERR_INVALID_ARG, "null context");
+    HIP_TRY(hipSetDevice(c->device));
+    int rc = read_state(c);
+    if (rc) return rc;
+    if (c->h_state->done != 1 && n_iters) {
+        if ((rc = write_limits(c, c->h_state->n_iter + n_iters, ~0ull))) return rc;
+        if ((rc = launch_iterations(c, n_iters))) return rc;
+    }
+    if (st) return fill_stats(c, st);
+    return ALLL_OK;
+}
+
+int alll_get_stats(alll_ctx* c, alll_stats* st) {
+    if (!c || !st) return fail(ALLL_ERR_INVALID_ARG, "null argument");
+    HIP_TRY(hipSetDevice(c->device));
+    return fill_stats(c, st);
+}
+
+int alll_synchronize(alll_ctx* c) {
+    if (!c) return fail(ALLL_ERR_INVALID_ARG, "null context");
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return ALLL_OK;
+}
+
+int alll_verify(alll_ctx* c, int* valid, uint64_t* n_violated) {
+    if (!c) return fail(ALLL_ERR_INVALID_ARG, "null context");
+    HIP_TRY(hipSetDevice(c->device));
+    // every rank holds the full clause set and the full assignment: evaluate all tiles
+    HIP_TRY(launch_eval(c->cv, c->b, 0, c->b.n_tiles, false, c->stream));
+    HIP_TRY(launch_reduce(c->b, 1, c->stream));
+    int rc = read_state(c);
+    if (rc) return rc;
+    if (valid) *valid = c->h_state->count_out == 0;
+    if (n_violated) *n_violated = c->h_state->count_out;
+    return ALLL_OK;
+}
+
+int alll_get_assignment_words(alll_ctx* c, uint32_t* out, uint64_t n_words) {
+    if (!c || (!out && c->b.n_words)) return fail(ALLL_ERR_INVALID_ARG, "null argument");
+    if (n_words < c->b.n_words) return fail(ALLL_ERR_INVALID_ARG, "need %u words", c->b.n_words);
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->b.n_words) HIP_TRY(hipMemcpy(out, c->b.A, c->b.n_words * 4ull, hipMemcpyDeviceToHost));
+    return ALLL_OK;
+}
+
+int alll_set_assignment_words(alll_ctx* c, const uint32_t* in, uint64_t n_words) {
+    if (!c || (!in && c->b.n_words)) return fail(ALLL_ERR_INVALID_ARG, "null argument");
+    if (n_words < c->b.n_words) return fail(ALLL_ERR_INVALID_ARG, "need %u words", c->b.n_words);
+    HIP_TRY(hipSetDevice(c->device));
+    std::vector<uint32_t> w(in, in + c->b.n_words);
+    if (!w.empty() && (c->n_vars & 31)) w.back() &= (1u << (c->n_vars & 31)) - 1u;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->b.n_words) HIP_TRY(hipMemcpy(c->b.A, w.data(), c->b.n_words * 4ull, hipMemcpyHostToDevice));
+    return ALLL_OK;
+}
+
+int alll_get_assignment(alll_ctx* c, uint8_t* out, uint64_t n) {
+    if (!c || (!out && c->n_vars)) return fail(ALLL_ERR_INVALID_ARG, "null argument");
+    if (n < c->n_vars) return fail(ALLL_ERR_INVALID_ARG, "need %u bytes", c->n_vars);
+    std::vector<uint32_t> w(c->b.n_words);
+    int rc = alll_get_assignment_words(c, w.data(), w.size());
+    if (rc) return rc;
+    for (uint32_t v = 0; v < c->n_vars; ++v) out[v] = (w[v >> 5] >> (v & 31)) & 1u;
+    return ALLL_OK;
+}
+
+int alll_set_assignment(alll_ctx* c, const uint8_t* in, uint64_t n) {
+    if (!c || (!in && c->n_vars)) return fail(ALLL_ERR_INVALID_ARG, "null argument");
+    if (n < c->n_vars) return fail(ALLL_ERR_INVALID_ARG, "need %u bytes", c->n_vars);
+    std::vector<uint32_t> w(c->b.n_words, 0u);
+    for (uint32_t v = 0; v < c->n_vars; ++v)
+        if (in[v]) w[v >> 5] |= 1u << (v & 31);
+    return alll_set_assignment_words(c, w.data(), w.size());
+}
+
+int alll_get_violated_mask(alll_ctx* c, uint64_t* out, uint64_t n_words) {
+    if (!c) return fail(ALLL_ERR_INVALID_ARG, "null context");
+    const uint64_t need = (c->m + 63) / 64;
+    if (n_words < need || (!out && need)) return fail(ALLL_ERR_INVALID_ARG, "need %llu words", (unsigned long long)need);
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (need) HIP_TRY(hipMemcpy(out, c->b.vmask, need * 8, hipMemcpyDeviceToHost));
+    if (c->m & 63) out[need - 1] &= (1ull << (c->m & 63)) - 1ull;
+    return ALLL_OK;
+}
+
+int alll_get_mis(alll_ctx* c, uint32_t* out, uint64_t cap, uint64_t* n_out) {
+    if (!c || !n_out) return fail(ALLL_ERR_INVALID_ARG, "null argument");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    const uint32_t nt = c->b.n_tiles;
+    std::vector<uint32_t> cnt(nt);
+    if (nt) HIP_TRY(hipMemcpy(cnt.data(), c->b.mis_cnt, nt * 4ull, hipMemcpyDeviceToHost));
+    std::vector<uint32_t> all;
+    std::vector<uint32_t> buf;
+    for (uint32_t t = 0; t < nt; ++t) {
+        if (!cnt[t]) continue;
+        buf.resize(cnt[t]);
+        HIP_TRY(hipMemcpy(buf.data(), c->b.mis + (size_t)t * TILE, cnt[t] * 4ull, hipMemcpyDeviceToHost));
+        all.insert(all.end(), buf.begin(), buf.end());
+    }
+    std::sort(all.begin(), all.end());
+    *n_out = all.size();
+    if (out) {
+        if (cap < all.size()) return fail(ALLL_ERR_INVALID_ARG, "need capacity %zu", all.size());
+        std::copy(all.begin(), all.end(), out);
+    }
+    return ALLL_OK;
+}
+
+int alll_bench_eval(alll_ctx* c, int reps, double* avg_ms, uint64_t* n_violated) {
+    if (!c || reps < 1) return fail(ALLL_ERR_INVALID_ARG, "bad argument");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(launch_eval(c->cv, c->b, c->own_begin, c->own_end, false, c->stream));  // warm
+    HIP_TRY(hipEventRecord(c->ev[0], c->stream));
+    for (int i = 0; i < reps; ++i)
+        HIP_TRY(launch_eval(c->cv, c->b, c->own_begin, c->own_end, false, c->stream));
+    HIP_TRY(hipEventRecord(c->ev[1], c->stream));
+    HIP_TRY(hipEventSynchronize(c->ev[1]));
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+    if (avg_ms) *avg_ms = ms / reps;
+    if (n_violated) {
+        int valid = 0;
+        int rc = alll_verify(c, &valid, n_violated);
+        if (rc) return rc;
+    }
+    return ALLL_OK;
+}
+
+int alll_profile(alll_ctx* c, uint64_t n_iters, alll_phase_times* out) {
+    if (!c || !out) return fail(ALLL_ERR_INVALID_ARG, "null argument");
+    HIP_TRY(hipSetDevice(c->device));
+    memset(out, 0, sizeof(*out));
+    int rc = read_state(c);
+    if (rc) return rc;
+    if (c->h_state->done == 1) return ALLL_OK;
+    if ((rc = write_limits(c, c->h_state->n_iter + n_iters, ~0ull))) return rc;
+    double acc[4] = {0, 0, 0, 0};
+    for (uint64_t i = 0; i < n_iters; ++i) {
+        if ((rc = enqueue_iteration(c, c->ev))) return rc;
+        HIP_TRY(hipEventSynchronize(c->ev[4]));
+        float t;
+        for (int p = 0; p < 4; ++p) {
+            HIP_TRY(hipEventElapsedTime(&t, c->ev[p], c->ev[p + 1]));
+            acc[p] += t;
+        }
+    }
+    out->iterations = n_iters;
+    out->eval_ms = acc[0] / n_iters;
+    out->exchange_ms = acc[1] / n_iters;
+    out->mis_ms = acc[2] / n_iters;
+    out->resample_ms = acc[3] / n_iters;
+    out->total_ms = (acc[0] + acc[1] + acc[2] + acc[3]) / n_iters;
+    return ALLL_OK;
+}
+
+uint64_t alll_eval_bytes(alll_ctx* c) {
+    // B_eval = 4 L + 4 (m+1) [CSR offsets only] + ceil(n/8) + ceil(m/8),
+    // for this rank's clause shard.
+    if (!c) return 0;
+    const uint64_t cb = (uint64_t)c->own_begin * TILE;
+    const uint64_t ce = std::min<uint64_t>(c->m, (uint64_t)c->own_end * TILE);
+    const uint64_t ms = ce > cb ? ce - cb : 0;
+    const uint64_t lits = c->cv.k ? ms * c->cv.k : (c->m ? (c->n_lits * ms) / c->m : 0);
+    return 4 * lits + (c->cv.k ? 0 : 4 * (ms + 1)) + (c->n_vars + 7) / 8 + (ms + 7) / 8;
+}
+
+int alll_layout(alll_ctx* c) { return c ? (int)c->cv.k : -1; }
+
+}  // extern "C"

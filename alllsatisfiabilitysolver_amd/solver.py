@@ -1,0 +1,268 @@
+"""Host-side Python front-end of the MI355X solver (over the C-ABI, liballl.so).
+
+Two layers:
+  * `Solver` -- a thin owner of one `alll_ctx` with numpy in/out (tests, bench, CLI).
+  * `SATInstance` / `VariablesArray` / `Clause` / `Statistics` -- the reference's API shape
+    (library/include/SATInstance.h:25-66, :156-173; VariablesArray.h:17-35; Clause.h:17-28)
+    for Python callers.  C++ callers use include/alll_compat/SATInstance.h instead.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import _native as N
+
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+
+
+def _p(a, t):
+    return a.ctypes.data_as(t)
+
+
+# ------------------------------------------------------------------ instance helpers
+def generate_ksat(gen_seed: int, n_vars: int, n_clauses: int, k: int, kind: int = 0,
+                  c_begin: int = 0, c_end: Optional[int] = None):
+    """Random k-SAT, k distinct variables per clause (kind 0 uniform, 1 power-law).
+    Returns (offsets uint64[m+1], literals uint32[m*k]) for clauses [c_begin, c_end)."""
+    c_end = n_clauses if c_end is None else c_end
+    lits = np.empty((c_end - c_begin) * k, np.uint32)
+    N.check(N.lib().alll_generate_ksat(gen_seed, n_vars, n_clauses, k, kind, c_begin, c_end,
+                                       _p(lits, _u32p)), "generate_ksat")
+    offs = np.arange(c_end - c_begin + 1, dtype=np.uint64) * np.uint64(k)
+    return offs, lits
+
+
+def parse_dimacs(text: bytes):
+    """DIMACS text -> (n_vars, offsets, literals) with the reference loader semantics."""
+    L = N.lib()
+    v, c, ln = ctypes.c_uint32(), ctypes.c_uint64(), ctypes.c_uint64()
+    rc = L.alll_dimacs_parse(text, len(text), ctypes.byref(v), ctypes.byref(c), None, None,
+                             ctypes.byref(ln))
+    if rc == N.ALLL_ERR_BAD_INPUT:
+        N.check(rc, "dimacs")
+    offs = np.zeros(c.value + 1, np.uint64)
+    lits = np.zeros(max(1, ln.value), np.uint32)
+    N.check(L.alll_dimacs_parse(text, len(text), ctypes.byref(v), ctypes.byref(c), _p(offs, _u64p),
+                                _p(lits, _u32p), ctypes.byref(ln)), "dimacs")
+    return int(v.value), offs, lits[: ln.value]
+
+
+def read_dimacs(path: str):
+    L = N.lib()
+    v, c, ln = ctypes.c_uint32(), ctypes.c_uint64(), ctypes.c_uint64()
+    bp = os.fsencode(path)
+    rc = L.alll_dimacs_read(bp, ctypes.byref(v), ctypes.byref(c), None, None, ctypes.byref(ln))
+    if rc in (N.ALLL_ERR_BAD_INPUT, N.ALLL_ERR_IO):
+        N.check(rc, f"dimacs {path}")
+    offs = np.zeros(c.value + 1, np.uint64)
+    lits = np.zeros(max(1, ln.value), np.uint32)
+    N.check(L.alll_dimacs_read(bp, ctypes.byref(v), ctypes.byref(c), _p(offs, _u64p),
+                               _p(lits, _u32p), ctypes.byref(ln)), f"dimacs {path}")
+    return int(v.value), offs, lits[: ln.value]
+
+
+# ----------------------------------------------------------------------------- Solver
+class Solver:
+    """Owns one device solver context (alll_ctx)."""
+
+    def __init__(self, n_vars: int, offsets, literals, seed: int = 1, max_iters: int = 0,
+                 device: int = -1, n_threads: int = 1, rank: int = 0, world: int = 1,
+                 comm_id: Optional[bytes] = None, flags: int = 0, grid_rounds: int = 0):
+        self._L = N.lib()
+        self.n_vars = int(n_vars)
+        self.offsets = np.ascontiguousarray(offsets, np.uint64)
+        self.literals = np.ascontiguousarray(literals, np.uint32)
+        self.m = self.offsets.size - 1
+        prob = N.Problem(self.n_vars, 0, self.m, _p(self.offsets, _u64p), _p(self.literals, _u32p))
+        opt = N.Options()
+        self._L.alll_default_options(ctypes.byref(opt))
+        opt.seed, opt.max_iters, opt.device = seed, max_iters, device
+        opt.n_threads, opt.rank, opt.world = n_threads, rank, world
+        opt.flags, opt.grid_rounds = flags, grid_rounds
+        if comm_id is not None:
+            ctypes.memmove(opt.comm_id, comm_id, 128)
+        self._ctx = ctypes.c_void_p()
+        N.check(self._L.alll_create(ctypes.byref(prob), ctypes.byref(opt), ctypes.byref(self._ctx)),
+                "alll_create")
+        self.world = world
+        self.rank = rank
+
+    # lifecycle
+    def close(self):
+        if getattr(self, "_ctx", None) and self._ctx.value:
+            self._L.alll_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # loop
+    def solve(self) -> dict:
+        st = N.Stats()
+        rc = self._L.alll_solve(self._ctx, ctypes.byref(st))
+        if rc not in (N.ALLL_OK, N.ALLL_ERR_MAX_ITERS):
+            N.check(rc, "alll_solve")
+        return st.as_dict()
+
+    def run(self, n_iters: int, sync: bool = True) -> Optional[dict]:
+        if sync:
+            st = N.Stats()
+            N.check(self._L.alll_run(self._ctx, n_iters, ctypes.byref(st)), "alll_run")
+            return st.as_dict()
+        N.check(self._L.alll_run(self._ctx, n_iters, None), "alll_run")
+        return None
+
+    def synchronize(self):
+        N.check(self._L.alll_synchronize(self._ctx), "alll_synchronize")
+
+    def stats(self) -> dict:
+        st = N.Stats()
+        N.check(self._L.alll_get_stats(self._ctx, ctypes.byref(st)), "alll_get_stats")
+        return st.as_dict()
+
+    def verify(self):
+        ok = ctypes.c_int()
+        nv = ctypes.c_uint64()
+        N.check(self._L.alll_verify(self._ctx, ctypes.byref(ok), ctypes.byref(nv)), "alll_verify")
+        return bool(ok.value), int(nv.value)
+
+    # state access
+    def assignment_words(self) -> np.ndarray:
+        w = np.zeros((self.n_vars + 31) // 32, np.uint32)
+        N.check(self._L.alll_get_assignment_words(self._ctx, _p(w, _u32p), w.size), "get_assignment")
+        return w
+
+    def set_assignment_words(self, w):
+        w = np.ascontiguousarray(w, np.uint32)
+        N.check(self._L.alll_set_assignment_words(self._ctx, _p(w, _u32p), w.size), "set_assignment")
+
+    def assignment(self) -> np.ndarray:
+        a = np.zeros(max(1, self.n_vars), np.uint8)
+        N.check(self._L.alll_get_assignment(self._ctx, _p(a, _u8p), a.size), "get_assignment")
+        return a[: self.n_vars]
+
+    def set_assignment(self, a):
+        a = np.ascontiguousarray(a, np.uint8)
+        N.check(self._L.alll_set_assignment(self._ctx, _p(a, _u8p), a.size), "set_assignment")
+
+    def violated_mask(self) -> np.ndarray:
+        w = np.zeros(max(1, (self.m + 63) // 64), np.uint64)
+        N.check(self._L.alll_get_violated_mask(self._ctx, _p(w, _u64p), w.size), "violated_mask")
+        return w
+
+    def mis(self) -> np.ndarray:
+        n = ctypes.c_uint64()
+        N.check(self._L.alll_get_mis(self._ctx, None, 0, ctypes.byref(n)), "get_mis")
+        out = np.zeros(max(1, n.value), np.uint32)
+        N.check(self._L.alll_get_mis(self._ctx, _p(out, _u32p), out.size, ctypes.byref(n)), "get_mis")
+        return out[: n.value]
+
+    # measurement
+    def bench_eval(self, reps: int = 20):
+        ms = ctypes.c_double()
+        nv = ctypes.c_uint64()
+        N.check(self._L.alll_bench_eval(self._ctx, reps, ctypes.byref(ms), ctypes.byref(nv)), "bench_eval")
+        return float(ms.value), int(nv.value)
+
+    def profile(self, n_iters: int) -> dict:
+        pt = N.PhaseTimes()
+        N.check(self._L.alll_profile(self._ctx, n_iters, ctypes.byref(pt)), "profile")
+        return pt.as_dict()
+
+    def eval_bytes(self) -> int:
+        return int(self._L.alll_eval_bytes(self._ctx))
+
+    def layout(self) -> int:
+        return int(self._L.alll_layout(self._ctx))
+
+
+def device_count() -> int:
+    return int(N.lib().alll_device_count())
+
+
+def comm_unique_id() -> bytes:
+    buf = (ctypes.c_uint8 * 128)()
+    N.check(N.lib().alll_comm_unique_id(buf), "comm_unique_id")
+    return bytes(buf)
+
+
+# ------------------------------------------------- reference-shaped API (SATInstance.h)
+class Clause:
+    """Clause<T> (Clause.h:17-28): encoded literals + the chunk id t_id."""
+
+    def __init__(self, literals: Sequence[int], t_id: int = 0):
+        self.literals = list(literals)
+        self.t_id = t_id
+
+    def is_not_satisfied(self, vars_) -> bool:  # Clause.h:34-46
+        return not any((not vars_[l >> 1]) if (l & 1) else vars_[l >> 1] for l in self.literals)
+
+
+class VariablesArray:
+    """VariablesArray<T> (VariablesArray.h:17-35).  The initial values come from the device
+    solver's Philox stream (seeded), not std::random_device."""
+
+    def __init__(self, n_vars: int):
+        self.n_vars = int(n_vars)
+        self.vars = np.zeros(self.n_vars, np.bool_)
+
+
+@dataclass
+class Statistics:
+    """Statistics (SATInstance.h:25-32)."""
+    n_iterations: int = 0
+    n_resamples: int = 0
+    avg_mis_size: int = 0
+    n_thread_resamples: List[int] = field(default_factory=list)
+
+
+class SATInstance:
+    """SATInstance<T> (SATInstance.h:39-452) over the MI355X solver.  `seed` and `device`
+    are additive keyword arguments; existing call shapes are unchanged."""
+
+    def __init__(self, var_arr: VariablesArray, n_threads: int, seed: int = 1, device: int = -1,
+                 max_iters: int = 0):
+        self.var_arr = var_arr
+        self.n_vars = var_arr.n_vars
+        self.n_clauses = 0
+        self.n_threads = max(1, int(n_threads))
+        self._seed, self._device, self._max_iters = seed, device, max_iters
+
+    @staticmethod
+    def _flatten(clauses):
+        flat = [cl for chunk in clauses for cl in chunk]
+        offs = np.zeros(len(flat) + 1, np.uint64)
+        offs[1:] = np.cumsum([len(c.literals) for c in flat])
+        lits = np.fromiter((l for c in flat for l in c.literals), np.uint32, int(offs[-1]))
+        return offs, lits
+
+    def solve(self, clauses) -> Statistics:  # SATInstance.h:60-66
+        self.n_clauses += sum(len(c) for c in clauses)
+        offs, lits = self._flatten(clauses)
+        with Solver(self.n_vars, offs, lits, seed=self._seed, device=self._device,
+                    n_threads=self.n_threads, max_iters=self._max_iters) as s:
+            d = s.solve()
+            self.var_arr.vars[:] = s.assignment().astype(np.bool_)
+        thr = [0] * self.n_threads
+        thr[0] = d["n_resamples"]
+        return Statistics(d["n_iterations"], d["n_resamples"], d["avg_mis_size"], thr)
+
+    def verify_validity(self, clauses) -> bool:  # SATInstance.h:156-173
+        v = self.var_arr.vars
+        return not any(cl.is_not_satisfied(v) for chunk in clauses for cl in chunk)

@@ -1,0 +1,239 @@
+"""Benchmark of the MI355X Moser-Tardos resample loop (BASELINE.json metric:
+"clause-evals/sec + resample iters/sec, random 3-SAT 10M clauses, 1/2/4/8 GPUs").
+
+A step is one resample iteration of SATInstance::parallel_solve (reference
+SATInstance.h:260-311) over the whole instance: evaluate all m clauses, compact the violated
+ones, exact LFMIS, Philox resample.  Ratio-4 random 3-SAT never converges under this
+algorithm, so K fixed iterations are timed.
+
+  value            = m * K / t  (clause-evals/s of the full loop, whole job)
+  resample_iters_s = K / t
+Inputs are resident in HBM before the timed region.  N>1: one process per GPU (torchrun),
+clauses sharded across ranks, per-iteration RCCL all-gather of the violated bitmask; the
+instance size is fixed (strong scaling).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config M|C2|C3|C4|C5]
+"""
+import argparse
+import json
+import os
+import platform
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    # name: (n_vars, n_clauses, k, kind, description)
+    "M": (2_500_000, 10_000_000, 3, 0, "random 3-SAT ratio 4, 2.5M vars / 10M clauses (metric anchor)"),
+    "C2": (1_000_000, 4_000_000, 3, 0, "random 3-SAT ratio 4, 1M vars / 4M clauses"),
+    "C3": (4_000_000, 6_000_000, 8, 0, "random 8-SAT m/n 1.5, 4M vars / 6M clauses"),
+    "C4": (32_000_000, 128_000_000, 3, 0, "random 3-SAT ratio 4, 32M vars / 128M clauses"),
+    "C5": (2_500_000, 10_000_000, 3, 1, "power-law (beta 0.8) 3-SAT, 2.5M vars / 10M clauses"),
+}
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(cfg, budget_s):
+    """The reference's own -p OpenMP path (oracle/_ref/ref_probe, compiled from the
+    reference sources) on the host cores: full resample iterations on a bounded sample, plus
+    the eval-phase rate at the full configuration size."""
+    n, m, k, kind, _ = CONFIGS[cfg]
+    threads = max(1, min(16, os.cpu_count() or 1))  # the GPU box's CPU share is 16
+    probe = os.path.join(ROOT, "oracle", "_ref", "ref_probe")
+    if os.path.exists(probe):
+        # bounded full-loop sample: 1/100 of the instance (same ratio, same generator)
+        ns, ms = max(k, n // 100), m // 100
+        cmd = [probe, "bench-gen", str(ns), str(ms), str(k), str(kind), "1", str(threads),
+               str(budget_s), "0"]
+        r = json.loads(subprocess.run(cmd, check=True, capture_output=True, text=True).stdout)
+        loop_rate = ms * r["iters"] / r["iters_s"] if r["iters"] else 0.0
+        # eval phase (P1, SATInstance.h:273-280) at the full size, best of 3
+        cmd = [probe, "bench-gen", str(n), str(m), str(k), str(kind), "1", str(threads), "0", "3"]
+        e = json.loads(subprocess.run(cmd, check=True, capture_output=True, text=True).stdout)
+        return {
+            "value": loop_rate,
+            "unit": "clause-evals/s",
+            "cores": threads,
+            "kind": "reference",
+            "sample": (f"reference -p path (T={threads}) full resample loop, {r['iters']} iterations in "
+                       f"{r['iters_s']:.1f}s on a 1/100 sample (n={ns}, m={ms}, same generator); "
+                       f"eval phase alone at full size m={m}: {e['eval_clause_evals_per_s']:.3e} "
+                       f"clause-evals/s; the reference MIS is quadratic in |U| so the full-size loop "
+                       f"is ~1e3 s/iteration (SURVEY.md §6); host {cpu_model()}"),
+            "resample_iters_per_s": r["iters"] / r["iters_s"] if r["iters_s"] else 0.0,
+            "eval_phase_clause_evals_per_s": e["eval_clause_evals_per_s"],
+        }
+    # fallback: the oracle's serial restatement (port)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+
+    ns, ms = max(k, n // 100), m // 100
+    offs, lits = oracle.generate_ksat(1, ns, ms, k, kind)
+    t0 = time.perf_counter()
+    it = 0
+    while time.perf_counter() - t0 < budget_s:
+        oracle.solve(ns, offs, lits, seed=1 + it, max_iters=10)
+        it += 10
+    dt = time.perf_counter() - t0
+    return {"value": ms * it / dt, "unit": "clause-evals/s", "cores": 1, "kind": "port",
+            "sample": f"oracle serial restatement, {it} iterations on n={ns}, m={ms}; host {cpu_model()}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="M", choices=list(CONFIGS))
+    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--exchange", default="allgather", choices=["allgather", "allreduce"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--profile-iters", type=int, default=10)
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_eval_traffic.json"))
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+
+    import torch
+
+    from alllsatisfiabilitysolver_amd import Solver, comm_unique_id, generate_ksat
+    from alllsatisfiabilitysolver_amd import _native as N
+
+    dist = None
+    comm_id = None
+    if world > 1:
+        import torch.distributed as dist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        obj = [comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        comm_id = obj[0]
+
+    n, m, k, kind, desc = CONFIGS[args.config]
+    t0 = time.perf_counter()
+    offs, lits = generate_ksat(1, n, m, k, kind)
+    t_gen = time.perf_counter() - t0
+    flags = N.FLAG_EXCHANGE_ALLREDUCE if args.exchange == "allreduce" else 0
+    t0 = time.perf_counter()
+    s = Solver(n, offs, lits, seed=args.seed, device=local_rank, rank=rank, world=world,
+               comm_id=comm_id, flags=flags)
+    del offs, lits
+    t_create = time.perf_counter() - t0
+    log(f"[rank {rank}] generated {m} clauses in {t_gen:.2f}s, uploaded in {t_create:.2f}s, layout k={s.layout()}")
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    # warmup (untimed)
+    s.run(args.warmup, sync=False)
+    s.synchronize()
+    torch.cuda.synchronize(local_rank)
+
+    barrier()
+    torch.cuda.synchronize(local_rank)
+    t0 = time.perf_counter()
+    s.run(args.steps, sync=False)
+    s.synchronize()
+    torch.cuda.synchronize(local_rank)
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        tt = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+    st = s.stats()
+    steps_done = args.steps  # converged runs would stop early; ratio-4 instances do not
+    value = m * steps_done / dt
+    iters_s = steps_done / dt
+
+    # per-phase device time with HIP events on the solver's stream (eager replay of the same
+    # kernel sequence); the eval kernel's average duration prices the roofline
+    pt = s.profile(args.profile_iters)
+    eval_bytes = s.eval_bytes()
+    eval_ms = pt["eval_ms"]
+    achieved = eval_bytes / (eval_ms * 1e-3) / 1e9 if eval_ms > 0 else 0.0
+    ev_ms, _ = s.bench_eval(20)
+    traffic = None
+    try:
+        tj = json.load(open(args.traffic_json))
+        if tj.get("config") == args.config and tj.get("n_gpus", 1) == world:
+            traffic = tj.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+
+    out = None
+    if rank == 0:
+        out = {
+            "metric": "clause-evals/sec + resample iters/sec, random 3-SAT 10M clauses, 1/2/4/8 GPUs",
+            "value": value,
+            "unit": "clause-evals/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt * 1e3 / args.steps,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (seeded counter-based random k-SAT generator, gen_seed=1)",
+            "config": {"workload": f"{args.config}: {desc}", "n_vars": n, "n_clauses": m, "k": k,
+                       "solve_seed": args.seed, "exchange": args.exchange if world > 1 else "none",
+                       "parallelism": f"clause-shard x{world}"},
+            "resample_iters_per_s": iters_s,
+            "violated_last": st["n_violated"],
+            "avg_mis_size": st["avg_mis_size"],
+            "phase_ms": {k2: pt[k2] for k2 in ("eval_ms", "exchange_ms", "mis_ms", "resample_ms", "total_ms")},
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "kernel": f"k_eval_fixed<{k}>" if s.layout() else "k_eval_csr",
+                "algorithmic_bytes_per_launch": eval_bytes,
+                "eval_ms_in_loop": eval_ms,
+                "eval_ms_back_to_back": ev_ms,
+            },
+        }
+    s.close()
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            out["cpu_baseline"] = cpu_baseline(args.config, args.cpu_budget)
+        except Exception as e:  # reported, never fatal for the GPU number
+            out["cpu_baseline"] = {"value": None, "error": str(e)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,175 @@
+/*
+ * alll.h -- C-ABI of the MI355X-native Moser-Tardos (ALLL) resample loop.
+ *
+ * This is the drop-in boundary for the reference's hot path.  The reference exposes a
+ * header-only C++ API (xmif1/ALLLSatisfiabilitySolver, library/include/SATInstance.h);
+ * the compatibility headers in include/alll_compat/ keep that API and call the entry
+ * points below.  Every entry point cites the reference interface it replaces.
+ *
+ * Conventions: plain pointers and sizes only; no exceptions cross this boundary; every
+ * function returns an alll_status (0 = ok) and alll_last_error() describes the last
+ * failure on the calling thread.  Literals use the reference encoding of
+ * example/main.cpp:168: DIMACS x>0 -> 2(x-1), -x -> 2(x-1)+1 (variable = l >> 1).
+ */
+#ifndef ALLL_H
+#define ALLL_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ALLL_ABI_VERSION 1
+
+typedef enum alll_status {
+    ALLL_OK = 0,
+    ALLL_ERR_INVALID_ARG = 1,   /* null pointer, bad size, bad option */
+    ALLL_ERR_BAD_INPUT = 2,     /* malformed CSR or DIMACS (header, missing clauses) */
+    ALLL_ERR_LITERAL_RANGE = 3, /* literal variable >= n_vars (reference: UB, Clause.h:40) */
+    ALLL_ERR_HIP = 4,           /* HIP runtime failure */
+    ALLL_ERR_RCCL = 5,          /* RCCL failure */
+    ALLL_ERR_MAX_ITERS = 6,     /* max_iters eval passes done, instance not solved */
+    ALLL_ERR_NO_DEVICE = 7,     /* no usable gfx950 device */
+    ALLL_ERR_OOM = 8,           /* device or host allocation failed */
+    ALLL_ERR_IO = 9,            /* file could not be opened / read */
+    ALLL_ERR_UNSUPPORTED = 10   /* size beyond the implementation limits */
+} alll_status;
+
+/* Instance in CSR form (replaces vector<ClauseArray*> of Clause<T>*, Clause.h:17-28;
+ * the chunking of example/main.cpp:149-178 is irrelevant to the T=1 semantics). */
+typedef struct alll_problem {
+    uint32_t n_vars;            /* VariablesArray<T>::n_vars (VariablesArray.h:20) */
+    uint32_t pad;
+    uint64_t n_clauses;
+    const uint64_t* offsets;    /* n_clauses+1, offsets[0] = 0, non-decreasing */
+    const uint32_t* literals;   /* offsets[n_clauses] encoded literals */
+} alll_problem;
+
+/* flags */
+#define ALLL_FLAG_NO_GRAPH          (1u << 0) /* launch eagerly instead of replaying a hipGraph */
+#define ALLL_FLAG_EXCHANGE_ALLREDUCE (1u << 1) /* multi-GPU: shard resample + allreduce of the
+                                                 bit-packed assignment delta (north_star form) */
+#define ALLL_FLAG_GENERIC_CSR       (1u << 2) /* disable the fixed-width clause layout */
+
+typedef struct alll_options {
+    uint64_t seed;          /* Philox4x32-10 key; replaces std::random_device (SATInstance.h:346) */
+    uint64_t max_iters;     /* cap on eval passes (n_iterations); 0 = unlimited like the reference */
+    int32_t device;         /* HIP device ordinal; -1 = current device */
+    int32_t n_threads;      /* length of the per-thread resample vector reported (>= 1) */
+    int32_t rank;           /* clause shard of this process (0 .. world-1) */
+    int32_t world;          /* number of GPUs the clauses are sharded over (1 = single GPU) */
+    uint8_t comm_id[128];   /* RCCL unique id from alll_comm_unique_id() on rank 0 (world > 1) */
+    uint32_t flags;         /* ALLL_FLAG_* */
+    uint32_t grid_rounds;   /* full-grid LFMIS rounds before the tail kernel (0 = default) */
+} alll_options;
+
+#define ALLL_MAX_GPU_STATS 64
+
+/* Replaces struct Statistics (SATInstance.h:25-32). */
+typedef struct alll_stats {
+    uint64_t n_iterations;   /* eval passes, including the final zero-violation pass */
+    uint64_t n_resamples;    /* sum of clause lengths over every MIS clause */
+    uint64_t avg_mis_size;   /* floor(sum |MIS_i| / n_iterations) (SATInstance.h:317) */
+    uint64_t sum_mis_size;
+    uint64_t n_violated;     /* violated clauses found by the last eval pass */
+    int32_t solved;          /* 1 if the last eval pass found no violated clause */
+    int32_t n_gpus;          /* entries used in gpu_resamples */
+    uint64_t gpu_resamples[ALLL_MAX_GPU_STATS]; /* per clause-shard share of n_resamples */
+} alll_stats;
+
+/* Per-phase device time (ms, averaged over the profiled iterations), from HIP events on
+ * the solver's stream. */
+typedef struct alll_phase_times {
+    double eval_ms;          /* clause evaluation + compaction kernel */
+    double exchange_ms;      /* RCCL collectives + collect (0 on one GPU) */
+    double mis_ms;           /* count reduction + LFMIS rounds + tail */
+    double resample_ms;      /* Philox resample kernel */
+    double total_ms;         /* whole iteration */
+    uint64_t iterations;
+} alll_phase_times;
+
+typedef struct alll_ctx alll_ctx;
+
+const char* alll_version(void);
+const char* alll_last_error(void);
+void alll_default_options(alll_options* opt);
+
+/* Number of visible HIP devices (0 without a GPU; never fails). */
+int alll_device_count(void);
+
+/* RCCL unique id for a multi-GPU solver (rank 0 creates it, all ranks pass it in
+ * alll_options.comm_id). */
+int alll_comm_unique_id(uint8_t out[128]);
+
+/* Replaces SATInstance<T>(VariablesArray<T>*, int n_threads) (SATInstance.h:51-56) plus the
+ * random initial assignment of VariablesArray<T>(n_vars) (VariablesArray.h:23-34).  Copies
+ * the caller's CSR to the device; keeps no caller pointer. */
+int alll_create(const alll_problem* prob, const alll_options* opt, alll_ctx** out);
+int alll_destroy(alll_ctx* ctx);
+
+/* Replaces Statistics* SATInstance::solve(vector<ClauseArray*>*) (SATInstance.h:60-66 ->
+ * parallel_solve :217-320).  Runs until no clause is violated (ALLL_OK) or max_iters
+ * eval passes were done (ALLL_ERR_MAX_ITERS).  Statistics accumulate over calls. */
+int alll_solve(alll_ctx* ctx, alll_stats* stats);
+
+/* Fixed-iteration mode (benchmarks, step-by-step parity tests): run n_iters more full
+ * iterations (eval + MIS + resample); stops early only when an eval pass finds no
+ * violated clause.  Asynchronous unless stats != NULL. */
+int alll_run(alll_ctx* ctx, uint64_t n_iters, alll_stats* stats);
+
+int alll_get_stats(alll_ctx* ctx, alll_stats* stats);
+
+/* Replaces bool SATInstance::verify_validity(vector<ClauseArray*>*) const
+ * (SATInstance.h:156-173): one device eval pass over the current assignment. */
+int alll_verify(alll_ctx* ctx, int* valid, uint64_t* n_violated);
+
+/* Current assignment as n_vars bytes of 0/1 (the bool vars[] of VariablesArray.h:21). */
+int alll_get_assignment(alll_ctx* ctx, uint8_t* out, uint64_t n);
+int alll_set_assignment(alll_ctx* ctx, const uint8_t* in, uint64_t n);
+/* Bit-packed form: ceil(n_vars/32) words, bit v%32 of word v/32. */
+int alll_get_assignment_words(alll_ctx* ctx, uint32_t* out, uint64_t n_words);
+int alll_set_assignment_words(alll_ctx* ctx, const uint32_t* in, uint64_t n_words);
+
+/* Introspection of the last iteration (parity tests): violated bitmask of the last eval
+ * pass (ceil(n_clauses/64) words) and the MIS picked from it (ascending clause order). */
+int alll_get_violated_mask(alll_ctx* ctx, uint64_t* out, uint64_t n_words);
+int alll_get_mis(alll_ctx* ctx, uint32_t* out, uint64_t cap, uint64_t* n_out);
+
+/* Benchmark helpers.  eval-only launches time the evaluation kernel alone on the current
+ * assignment; profile runs n_iters iterations eagerly with HIP events around each phase. */
+int alll_bench_eval(alll_ctx* ctx, int reps, double* avg_ms, uint64_t* n_violated);
+int alll_profile(alll_ctx* ctx, uint64_t n_iters, alll_phase_times* out);
+/* Block the host until all work queued on the solver's stream finished. */
+int alll_synchronize(alll_ctx* ctx);
+/* Bytes the evaluation kernel reads/writes per pass (algorithmic). */
+uint64_t alll_eval_bytes(alll_ctx* ctx);
+/* Layout in use: 0 generic CSR, k>0 fixed-width-k transposed layout. */
+int alll_layout(alll_ctx* ctx);
+
+/* ---- host-side helpers (no GPU needed) ---------------------------------------------- */
+
+/* DIMACS loader with the clause semantics of example/cnf_io (cnf_header_read
+ * cnf_io.cpp:487-705 + cnf_data_read :126-328) and the encoding of main.cpp:157-178.
+ * Two calls: first with offsets/literals NULL to get the sizes, then with buffers. */
+int alll_dimacs_parse(const char* buf, uint64_t len, uint32_t* n_vars, uint64_t* n_clauses,
+                      uint64_t* offsets, uint32_t* literals, uint64_t* n_literals);
+/* Same from a file path (mmap). */
+int alll_dimacs_read(const char* path, uint32_t* n_vars, uint64_t* n_clauses, uint64_t* offsets,
+                     uint32_t* literals, uint64_t* n_literals);
+
+/* The solver's initial assignment for `seed` as n_vars bytes of 0/1 (word w of the packed
+ * form = Philox4x32-10(key=seed, ctr={w, 0, 0xFFFFFFFF, 0}).x); used by the compatibility
+ * VariablesArray (replaces the random_device fill of VariablesArray.h:23-34). */
+int alll_initial_assignment(uint64_t seed, uint32_t n_vars, uint8_t* out);
+
+/* Synthetic random k-SAT with k distinct variables per clause (kind 0 uniform, kind 1
+ * power-law P(v) ~ (v+1)^-0.8); clauses [c_begin, c_end) of the instance, fixed width k. */
+int alll_generate_ksat(uint64_t gen_seed, uint32_t n_vars, uint64_t n_clauses, uint32_t k,
+                       int kind, uint64_t c_begin, uint64_t c_end, uint32_t* literals);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ALLL_H */

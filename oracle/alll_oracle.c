@@ -1,0 +1,392 @@
+/*
+ * alll_oracle.c -- TEST INFRASTRUCTURE ONLY.
+ *
+ * Plain-C CPU restatement of the reference's serial Moser-Tardos resample loop
+ * (xmif1/ALLLSatisfiabilitySolver).  It is the parity checker for the HIP product
+ * path and must never be linked into, or called by, the product
+ * (alllsatisfiabilitysolver_amd/).  Only tests/, __graft_entry__.smoke() and
+ * bench.py's cpu_baseline leg may load it.
+ *
+ * Parity pinning: every deterministic function here (eval, LFMIS, round-robin
+ * MIS, chunking, statistics arithmetic, DIMACS semantics) is checked against
+ * golden vectors produced by the reference's own code (oracle/ref_probe.cpp
+ * compiled from /root/reference sources, fixtures in tests/golden/).  The RNG is
+ * not pinned: the reference draws from std::random_device, so the build replaces
+ * it with Philox4x32-10 (pinned against the Random123 known-answer vectors).
+ *
+ * Citations are to files under the reference repository.
+ */
+#include "alll_oracle.h"
+
+#include <stdlib.h>
+#include <string.h>
+
+/* ------------------------------------------------------------------------- */
+/* Philox4x32-10 (Salmon et al., SC'11; Random123 reference constants).      */
+/* Replaces RBG<default_random_engine>::sample (RandomBoolGenerator.h:35-44). */
+/* ------------------------------------------------------------------------- */
+void orc_philox4x32_10(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]) {
+    uint32_t c0 = ctr[0], c1 = ctr[1], c2 = ctr[2], c3 = ctr[3];
+    uint32_t k0 = key[0], k1 = key[1];
+    for (int r = 0; r < 10; ++r) {
+        uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+        uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+        uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+        uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+        uint32_t n0 = hi1 ^ c1 ^ k0;
+        uint32_t n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+/* A0 word w (variables 32w..32w+31) = Philox(key=seed, ctr={w, 0, 0xFFFFFFFF, 0}).x.
+ * Replaces the random_device-seeded fill of VariablesArray (VariablesArray.h:23-34). */
+void orc_init_assignment(uint64_t seed, uint32_t n_vars, uint32_t* A) {
+    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    uint32_t nw = (n_vars + 31) / 32;
+    for (uint32_t w = 0; w < nw; ++w) {
+        uint32_t ctr[4] = {w, 0u, 0xFFFFFFFFu, 0u}, o[4];
+        orc_philox4x32_10(ctr, key, o);
+        uint32_t word = o[0];
+        if (w == nw - 1 && (n_vars & 31)) word &= (1u << (n_vars & 31)) - 1u;
+        A[w] = word;
+    }
+}
+
+/* Resampled value of variable v in resample round `iter` (0-based):
+ * Philox(key=seed, ctr={v, iter_lo, 0, iter_hi}).x & 1.
+ * Replaces `vars[l>>1] = rbg.sample()` (SATInstance.h:358-360). */
+uint32_t orc_resample_bit(uint64_t seed, uint64_t iter, uint32_t v) {
+    uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
+    uint32_t ctr[4] = {v, (uint32_t)iter, 0u, (uint32_t)(iter >> 32)}, o[4];
+    orc_philox4x32_10(ctr, key, o);
+    return o[0] & 1u;
+}
+
+/* ------------------------------------------------------------------------- */
+/* Synthetic instance generator (shared specification with the product's      */
+/* generator; both are checked equal in tests).  Counter-based per clause.     */
+/* ------------------------------------------------------------------------- */
+static inline uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+/* Draw variable index in [0,n): uniform (kind 0) or power-law P(v) ~ (v+1)^-0.8
+ * (kind 1: v = floor(n * u^5), u a 32-bit fixed-point uniform). */
+static inline uint32_t draw_var(uint64_t r, uint32_t n, int kind) {
+    uint64_t u = r >> 32;
+    if (kind == 1) {
+        uint64_t p = u;
+        for (int i = 0; i < 4; ++i) p = (p * u) >> 32;
+        u = p;
+    }
+    return (uint32_t)((u * (uint64_t)n) >> 32);
+}
+
+int orc_generate_ksat(uint64_t gen_seed, uint32_t n_vars, uint64_t n_clauses, uint32_t k,
+                      int kind, uint64_t c_begin, uint64_t c_end, uint32_t* lits) {
+    if (k == 0 || k > 64 || n_vars < k || c_end > n_clauses || c_begin > c_end) return -1;
+    for (uint64_t c = c_begin; c < c_end; ++c) {
+        uint64_t s = mix64(gen_seed ^ mix64(c + 0x632BE59BD9B4E019ull));
+        uint32_t* out = lits + (c - c_begin) * k;
+        for (uint32_t j = 0; j < k; ++j) {
+            for (;;) {
+                s += 0x9E3779B97F4A7C15ull;
+                uint64_t r = mix64(s);
+                uint32_t v = draw_var(r, n_vars, kind);
+                int dup = 0;
+                for (uint32_t q = 0; q < j; ++q) dup |= ((out[q] >> 1) == v);
+                if (!dup) { out[j] = 2u * v + (uint32_t)(r & 1u); break; }
+            }
+        }
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------------- */
+/* Clause evaluation: Clause<T>::is_not_satisfied (Clause.h:34-46); literal l   */
+/* is true iff vars[l>>1] XOR (l&1); a clause is violated iff no literal true. */
+/* ------------------------------------------------------------------------- */
+static inline uint32_t abit(const uint32_t* A, uint32_t v) { return (A[v >> 5] >> (v & 31)) & 1u; }
+
+int orc_clause_violated(const uint64_t* offs, const uint32_t* lits, const uint32_t* A, uint64_t c) {
+    for (uint64_t j = offs[c]; j < offs[c + 1]; ++j) {
+        uint32_t l = lits[j];
+        if (abit(A, l >> 1) != (l & 1u)) return 0;
+    }
+    return 1;
+}
+
+/* Violated collection (SATInstance.h:264-280) as a bitmask (bit c of word c/64). */
+uint64_t orc_eval(uint64_t m, const uint64_t* offs, const uint32_t* lits, const uint32_t* A,
+                  uint64_t* vmask) {
+    uint64_t cnt = 0, nw = (m + 63) / 64;
+    memset(vmask, 0, nw * sizeof(uint64_t));
+    for (uint64_t c = 0; c < m; ++c) {
+        if (orc_clause_violated(offs, lits, A, c)) {
+            vmask[c >> 6] |= 1ull << (c & 63);
+            ++cnt;
+        }
+    }
+    return cnt;
+}
+
+uint64_t orc_mask_to_list(uint64_t m, const uint64_t* vmask, uint32_t* U) {
+    uint64_t n = 0;
+    for (uint64_t c = 0; c < m; ++c)
+        if ((vmask[c >> 6] >> (c & 63)) & 1ull) U[n++] = (uint32_t)c;
+    return n;
+}
+
+/* ------------------------------------------------------------------------- */
+/* MIS.  T=1: populate_mis_parallel (SATInstance.h:391-451) with one set is the */
+/* lexicographically-first MIS of U in clause order under dependent_clauses    */
+/* (shares a variable, sign ignored; SATInstance.h:369-389).                   */
+/* ------------------------------------------------------------------------- */
+static int touches(const uint64_t* offs, const uint32_t* lits, const uint8_t* used, uint32_t c) {
+    for (uint64_t j = offs[c]; j < offs[c + 1]; ++j)
+        if (used[lits[j] >> 1]) return 1;
+    return 0;
+}
+static void mark(const uint64_t* offs, const uint32_t* lits, uint8_t* used, uint32_t c, uint8_t val) {
+    for (uint64_t j = offs[c]; j < offs[c + 1]; ++j) used[lits[j] >> 1] = val;
+}
+
+uint64_t orc_lfmis(uint32_t n_vars, const uint64_t* offs, const uint32_t* lits,
+                   const uint32_t* U, uint64_t nu, uint32_t* M, uint8_t* scratch_used) {
+    uint64_t nm = 0;
+    for (uint64_t i = 0; i < nu; ++i) {
+        uint32_t c = U[i];
+        if (!touches(offs, lits, scratch_used, c)) {
+            M[nm++] = c;
+            mark(offs, lits, scratch_used, c, 1);
+        }
+    }
+    for (uint64_t i = 0; i < nm; ++i) mark(offs, lits, scratch_used, M[i], 0); /* restore */
+    (void)n_vars;
+    return nm;
+}
+
+/* Chunk of clause c under example/main.cpp:149-178 (chunk_size = ceil(m/T);
+ * t advances by one whenever c > (t+1)*chunk_size -- chunk 0 holds chunk+1). */
+void orc_chunk_bounds(uint64_t m, uint32_t T, uint64_t* starts /* T+1 */) {
+    uint64_t chunk = (m + T - 1) / T; /* ceil(c_num / (double) n_threads) for int ranges */
+    uint32_t t = 0;
+    for (uint32_t q = 0; q <= T; ++q) starts[q] = m;
+    starts[0] = 0;
+    for (uint64_t c = 0; c < m; ++c) {
+        if (c > (uint64_t)(t + 1) * chunk) { t += 1; starts[t] = c; }
+    }
+    /* chunks that received no clause start at m (empty) */
+    for (uint32_t q = 1; q <= T; ++q)
+        if (starts[q] < starts[q - 1]) starts[q] = starts[q - 1];
+}
+
+/* T>1 round-robin MIS (SATInstance.h:414-447): t starts at 0; loop while sets
+ * remain: t=(t+1)%|sets|; an empty set is erased (and, because t is not
+ * decremented, its successor is skipped); otherwise its front clause is popped
+ * into M and every dependent clause is erased from every set.  Dependents are
+ * removed lazily here (skipped at the front), which yields the same fronts and
+ * the same emptiness tests as the eager vector::erase of the reference. */
+uint64_t orc_rr_mis(uint32_t n_vars, const uint64_t* offs, const uint32_t* lits,
+                    const uint32_t* U, uint64_t nu, uint32_t T, const uint64_t* chunk_starts,
+                    uint32_t* M, uint8_t* scratch_used) {
+    uint64_t* head = (uint64_t*)malloc(sizeof(uint64_t) * T);
+    uint64_t* tail = (uint64_t*)malloc(sizeof(uint64_t) * T);
+    uint32_t* live = (uint32_t*)malloc(sizeof(uint32_t) * T);
+    /* split U (sorted) into per-chunk ranges */
+    uint64_t p = 0;
+    for (uint32_t q = 0; q < T; ++q) {
+        head[q] = p;
+        while (p < nu && U[p] < chunk_starts[q + 1]) ++p;
+        tail[q] = p;
+        live[q] = q;
+    }
+    uint32_t nlive = T;
+    uint64_t nm = 0;
+    uint32_t t = 0;
+    while (nlive > 0) {
+        t = (t + 1) % nlive;
+        uint32_t s = live[t];
+        while (head[s] < tail[s] && touches(offs, lits, scratch_used, U[head[s]])) ++head[s];
+        if (head[s] == tail[s]) {
+            for (uint32_t q = t; q + 1 < nlive; ++q) live[q] = live[q + 1];
+            --nlive;
+            continue;
+        }
+        uint32_t c = U[head[s]++];
+        M[nm++] = c;
+        mark(offs, lits, scratch_used, c, 1);
+    }
+    for (uint64_t i = 0; i < nm; ++i) mark(offs, lits, scratch_used, M[i], 0);
+    free(head); free(tail); free(live);
+    (void)n_vars;
+    return nm;
+}
+
+/* ------------------------------------------------------------------------- */
+/* Serial resample loop (parallel_solve, SATInstance.h:217-320, with T=1) with */
+/* Philox resampling.  Statistics semantics (SATInstance.h:25-32, 313-317):    */
+/* n_iterations counts every eval pass including the final zero pass;          */
+/* n_resamples = sum of clause lengths over all MIS clauses; avg_mis_size =    */
+/* floor(sum|M| / n_iterations).                                               */
+/* max_iters (0 = unlimited) caps eval passes; a capped pass does not resample. */
+/* ------------------------------------------------------------------------- */
+int orc_solve(uint32_t n_vars, uint64_t m, const uint64_t* offs, const uint32_t* lits,
+              uint64_t seed, uint64_t max_iters, uint32_t* A, orc_stats* st,
+              orc_iter_cb cb, void* cb_user) {
+    uint64_t nw = (m + 63) / 64;
+    uint64_t* vmask = (uint64_t*)calloc(nw ? nw : 1, sizeof(uint64_t));
+    uint32_t* U = (uint32_t*)malloc(sizeof(uint32_t) * (m ? m : 1));
+    uint32_t* M = (uint32_t*)malloc(sizeof(uint32_t) * (m ? m : 1));
+    uint8_t* used = (uint8_t*)calloc(n_vars ? n_vars : 1, 1);
+    memset(st, 0, sizeof(*st));
+    uint64_t sum_mis = 0;
+    int solved = 0;
+    for (;;) {
+        st->n_iterations += 1;
+        uint64_t nu = orc_eval(m, offs, lits, A, vmask);
+        st->last_violated = nu;
+        if (nu == 0) { solved = 1; break; }
+        if (max_iters && st->n_iterations >= max_iters) break;
+        orc_mask_to_list(m, vmask, U);
+        uint64_t nm = orc_lfmis(n_vars, offs, lits, U, nu, M, used);
+        sum_mis += nm;
+        uint64_t dres = 0, iter = st->n_iterations - 1;
+        for (uint64_t i = 0; i < nm; ++i) {
+            uint32_t c = M[i];
+            for (uint64_t j = offs[c]; j < offs[c + 1]; ++j) {
+                uint32_t v = lits[j] >> 1;
+                uint32_t b = orc_resample_bit(seed, iter, v);
+                A[v >> 5] = (A[v >> 5] & ~(1u << (v & 31))) | (b << (v & 31));
+            }
+            dres += offs[c + 1] - offs[c];
+        }
+        st->n_resamples += dres;
+        if (cb) cb(cb_user, st->n_iterations, nu, nm, dres, A);
+    }
+    st->sum_mis_size = sum_mis;
+    st->avg_mis_size = st->n_iterations ? sum_mis / st->n_iterations : 0;
+    st->solved = solved;
+    free(vmask); free(U); free(M); free(used);
+    return solved ? 0 : 1;
+}
+
+/* ------------------------------------------------------------------------- */
+/* DIMACS semantics of cnf_header_read / cnf_data_read (example/cnf_io/        */
+/* cnf_io.cpp:487-705, 126-328) plus the encoding of example/main.cpp:157-178. */
+/* Restated over an in-memory buffer:                                          */
+/*  - lines are split at '\n'; a final line with no '\n' is dropped (getline   */
+/*    then eof -> break, cnf_io.cpp:277-281);                                  */
+/*  - lines whose first char is 'c'/'C' and lines of only ' ' are skipped;     */
+/*  - words are separated by ' ' only (s_word_extract_first, :1419-1486);      */
+/*  - s_to_i4 (:1305-1416): optional sign, digits, stops at first non-digit;   */
+/*    a word that does not start with a sign/digit ends the line;              */
+/*  - non-zero -> literal, 0 -> closes the clause.                             */
+/* Header: first non-comment non-blank line must be 'p'<ws>'cnf'<ws> V C.       */
+/* Returns 0 ok, -1 bad header, -2 fewer clauses than the header, -3 literal   */
+/* out of [1,V].                                                                */
+/* ------------------------------------------------------------------------- */
+static int is_ws(char c) { return c == ' ' || c == '\f' || c == '\n' || c == '\r' || c == '\t' || c == '\v'; }
+
+/* s_to_i4 on a word [w, we): returns 0 ok / 1 error; *val set */
+static int s_to_i4(const char* w, const char* we, long long* val) {
+    int st = 0, sgn = 1;
+    long long iv = 0;
+    for (const char* p = w;; ++p) {
+        char c = (p < we) ? *p : '\0';
+        if (st == 0) {
+            if (c == ' ') {}
+            else if (c == '-') { st = 1; sgn = -1; }
+            else if (c == '+') { st = 1; sgn = 1; }
+            else if (c >= '0' && c <= '9') { st = 2; iv = c - '0'; }
+            else return 1;
+        } else if (st == 1) {
+            if (c == ' ') {}
+            else if (c >= '0' && c <= '9') { st = 2; iv = c - '0'; }
+            else return 1;
+        } else {
+            if (c >= '0' && c <= '9') iv = 10 * iv + (c - '0');
+            else { *val = sgn * iv; return 0; }
+        }
+    }
+}
+
+int orc_dimacs_parse(const char* buf, uint64_t len, uint32_t* v_num, uint64_t* c_num,
+                     uint64_t* offs /* c_num+1, may be NULL */, uint32_t* lits /* may be NULL */,
+                     uint64_t* l_num) {
+    uint64_t pos = 0;
+    int have_header = 0;
+    long long V = 0, C = 0;
+    uint64_t nclauses = 0, nlits = 0, cur = 0;
+    int rc = 0;
+    if (offs) offs[0] = 0;
+    while (pos < len) {
+        const char* ls = buf + pos;
+        const char* nl = memchr(ls, '\n', len - pos);
+        if (!nl) break; /* last line without newline: dropped */
+        const char* le = nl;
+        pos = (uint64_t)(nl - buf) + 1;
+        uint64_t L = (uint64_t)(le - ls);
+        if (L > 0 && (ls[0] == 'c' || ls[0] == 'C')) continue;
+        /* s_len_trim: trailing ' ' only */
+        uint64_t tl = L;
+        while (tl > 0 && ls[tl - 1] == ' ') --tl;
+        if (tl == 0) continue;
+        if (!have_header) {
+            /* 'p', whitespace, adjustl, 'cnf' (case-insensitive), whitespace, V, C */
+            if (!(ls[0] == 'p' || ls[0] == 'P')) return -1;
+            if (L < 2 || !is_ws(ls[1])) return -1;
+            const char* p = ls + 2;
+            while (p < le && (*p == ' ' || *p == '\t')) ++p;
+            if (le - p < 4) return -1;
+            if (!((p[0] | 32) == 'c' && (p[1] | 32) == 'n' && (p[2] | 32) == 'f')) return -1;
+            if (!is_ws(p[3])) return -1;
+            p += 4;
+            while (p < le && (*p == ' ' || *p == '\t')) ++p;
+            /* two words separated by ' ' */
+            const char* w = p; while (w < le && *w == ' ') ++w;
+            const char* we = w; while (we < le && *we != ' ') ++we;
+            if (we == w || s_to_i4(w, we, &V)) return -1;
+            w = we; while (w < le && *w == ' ') ++w;
+            we = w; while (we < le && *we != ' ') ++we;
+            if (we == w || s_to_i4(w, we, &C)) return -1;
+            if (V < 0 || C < 0) return -1;
+            have_header = 1;
+            continue;
+        }
+        /* data line: words separated by ' ' */
+        const char* p = ls;
+        for (;;) {
+            while (p < le && *p == ' ') ++p;
+            const char* we = p; while (we < le && *we != ' ') ++we;
+            if (we == p) break;
+            long long x;
+            if (s_to_i4(p, we, &x)) break;
+            p = we;
+            if (x != 0) {
+                if (nclauses < (uint64_t)C) {
+                    if (x > V || -x > V) rc = rc ? rc : -3;
+                    if (lits) lits[nlits] = (x > 0) ? (uint32_t)(2 * x - 2) : (uint32_t)(-2 * x - 1);
+                    ++nlits;
+                }
+                ++cur;
+            } else {
+                if (nclauses < (uint64_t)C && offs) offs[nclauses + 1] = nlits;
+                ++nclauses;
+                cur = 0;
+            }
+        }
+    }
+    (void)cur;
+    if (!have_header) return -1;
+    *v_num = (uint32_t)V;
+    *c_num = (uint64_t)C;
+    if (l_num) *l_num = nlits;
+    if (nclauses < (uint64_t)C) return -2;
+    return rc;
+}

@@ -1,0 +1,258 @@
+"""TEST INFRASTRUCTURE ONLY -- numpy/ctypes front-end of the plain-C oracle.
+
+The oracle (oracle/alll_oracle.c) is a CPU restatement of the reference's serial
+Moser-Tardos loop (SATInstance.h:217-320 with one thread).  It is the parity checker
+for the HIP product path: only tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg may import this module, and never as the thing measured or shipped.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import struct
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liboracle.so")
+REF_PROBE = os.path.join(HERE, "_ref", "ref_probe")
+
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+
+
+class OrcStats(ctypes.Structure):
+    _fields_ = [
+        ("n_iterations", ctypes.c_uint64),
+        ("n_resamples", ctypes.c_uint64),
+        ("avg_mis_size", ctypes.c_uint64),
+        ("sum_mis_size", ctypes.c_uint64),
+        ("last_violated", ctypes.c_uint64),
+        ("solved", ctypes.c_int32),
+        ("pad", ctypes.c_int32),
+    ]
+
+
+ITER_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                           ctypes.c_uint64, ctypes.c_uint64, _u32p)
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE, "all"], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        L.orc_philox4x32_10.argtypes = [_u32p, _u32p, _u32p]
+        L.orc_init_assignment.argtypes = [ctypes.c_uint64, ctypes.c_uint32, _u32p]
+        L.orc_resample_bit.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32]
+        L.orc_resample_bit.restype = ctypes.c_uint32
+        L.orc_generate_ksat.argtypes = [ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
+                                        ctypes.c_uint32, ctypes.c_int, ctypes.c_uint64,
+                                        ctypes.c_uint64, _u32p]
+        L.orc_eval.argtypes = [ctypes.c_uint64, _u64p, _u32p, _u32p, _u64p]
+        L.orc_eval.restype = ctypes.c_uint64
+        L.orc_mask_to_list.argtypes = [ctypes.c_uint64, _u64p, _u32p]
+        L.orc_mask_to_list.restype = ctypes.c_uint64
+        L.orc_lfmis.argtypes = [ctypes.c_uint32, _u64p, _u32p, _u32p, ctypes.c_uint64, _u32p, _u8p]
+        L.orc_lfmis.restype = ctypes.c_uint64
+        L.orc_chunk_bounds.argtypes = [ctypes.c_uint64, ctypes.c_uint32, _u64p]
+        L.orc_rr_mis.argtypes = [ctypes.c_uint32, _u64p, _u32p, _u32p, ctypes.c_uint64,
+                                 ctypes.c_uint32, _u64p, _u32p, _u8p]
+        L.orc_rr_mis.restype = ctypes.c_uint64
+        L.orc_solve.argtypes = [ctypes.c_uint32, ctypes.c_uint64, _u64p, _u32p, ctypes.c_uint64,
+                                ctypes.c_uint64, _u32p, ctypes.POINTER(OrcStats), ITER_CB,
+                                ctypes.c_void_p]
+        L.orc_solve.restype = ctypes.c_int
+        L.orc_dimacs_parse.argtypes = [ctypes.c_char_p, ctypes.c_uint64, _u32p, _u64p, _u64p,
+                                       _u32p, _u64p]
+        L.orc_dimacs_parse.restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def _p(a, t):
+    return a.ctypes.data_as(t)
+
+
+# --------------------------------------------------------------------------- RNG
+def philox4x32_10(ctr, key):
+    c = np.asarray(ctr, np.uint32).copy()
+    k = np.asarray(key, np.uint32).copy()
+    o = np.zeros(4, np.uint32)
+    lib().orc_philox4x32_10(_p(c, _u32p), _p(k, _u32p), _p(o, _u32p))
+    return o
+
+
+def init_assignment(seed, n_vars):
+    A = np.zeros((n_vars + 31) // 32, np.uint32)
+    lib().orc_init_assignment(seed, n_vars, _p(A, _u32p))
+    return A
+
+
+def resample_bit(seed, it, v):
+    return int(lib().orc_resample_bit(seed, it, v))
+
+
+# --------------------------------------------------------------------- instances
+def generate_ksat(gen_seed, n_vars, n_clauses, k, kind=0):
+    """Uniform (kind=0) or power-law (kind=1) random k-SAT with distinct variables per
+    clause.  Returns (offsets uint64[m+1], literals uint32[m*k])."""
+    lits = np.zeros(n_clauses * k, np.uint32)
+    rc = lib().orc_generate_ksat(gen_seed, n_vars, n_clauses, k, kind, 0, n_clauses,
+                                 _p(lits, _u32p))
+    if rc != 0:
+        raise ValueError("bad generator arguments")
+    offs = np.arange(n_clauses + 1, dtype=np.uint64) * np.uint64(k)
+    return offs, lits
+
+
+def csr_from_lists(clauses):
+    """clauses: list of lists of encoded literals (2v + neg)."""
+    offs = np.zeros(len(clauses) + 1, np.uint64)
+    offs[1:] = np.cumsum([len(c) for c in clauses])
+    lits = np.array([l for c in clauses for l in c], np.uint32)
+    return offs, lits
+
+
+def to_dimacs(n_vars, offs, lits, comments=()):
+    out = [f"c {c}" for c in comments]
+    m = len(offs) - 1
+    out.append(f"p cnf {n_vars} {m}")
+    for c in range(m):
+        ls = lits[int(offs[c]):int(offs[c + 1])]
+        toks = [str(int(l >> 1) + 1) if (l & 1) == 0 else str(-(int(l >> 1) + 1)) for l in ls]
+        out.append(" ".join(toks + ["0"]))
+    return "\n".join(out) + "\n"
+
+
+# ------------------------------------------------------------------------- path
+def pack_bools(b):
+    b = np.asarray(b, np.uint8)
+    n = b.size
+    nw = (n + 31) // 32
+    pad = np.zeros(nw * 32, np.uint8)
+    pad[:n] = b
+    bits = pad.reshape(nw, 32).astype(np.uint32) << np.arange(32, dtype=np.uint32)
+    return np.bitwise_or.reduce(bits, axis=1).astype(np.uint32)
+
+
+def unpack_words(A, n):
+    A = np.asarray(A, np.uint32)
+    bits = (A[:, None] >> np.arange(32, dtype=np.uint32)) & 1
+    return bits.reshape(-1)[:n].astype(np.uint8)
+
+
+def eval_mask(offs, lits, A):
+    m = len(offs) - 1
+    vm = np.zeros(max(1, (m + 63) // 64), np.uint64)
+    n = lib().orc_eval(m, _p(offs, _u64p), _p(lits, _u32p), _p(A, _u32p), _p(vm, _u64p))
+    return int(n), vm
+
+
+def mask_to_list(m, vm):
+    U = np.zeros(max(1, m), np.uint32)
+    n = lib().orc_mask_to_list(m, _p(vm, _u64p), _p(U, _u32p))
+    return U[:n].copy()
+
+
+def lfmis(n_vars, offs, lits, U):
+    U = np.ascontiguousarray(U, np.uint32)
+    M = np.zeros(max(1, U.size), np.uint32)
+    used = np.zeros(max(1, n_vars), np.uint8)
+    n = lib().orc_lfmis(n_vars, _p(offs, _u64p), _p(lits, _u32p), _p(U, _u32p), U.size,
+                        _p(M, _u32p), _p(used, _u8p))
+    return M[:n].copy()
+
+
+def chunk_bounds(m, T):
+    s = np.zeros(T + 1, np.uint64)
+    lib().orc_chunk_bounds(m, T, _p(s, _u64p))
+    return s
+
+
+def rr_mis(n_vars, offs, lits, U, T):
+    U = np.ascontiguousarray(U, np.uint32)
+    M = np.zeros(max(1, U.size), np.uint32)
+    used = np.zeros(max(1, n_vars), np.uint8)
+    cs = chunk_bounds(len(offs) - 1, T)
+    n = lib().orc_rr_mis(n_vars, _p(offs, _u64p), _p(lits, _u32p), _p(U, _u32p), U.size, T,
+                         _p(cs, _u64p), _p(M, _u32p), _p(used, _u8p))
+    return M[:n].copy()
+
+
+def solve(n_vars, offs, lits, seed, max_iters=0, A0=None, trace=False):
+    """Serial resample loop with Philox.  Returns (stats dict, final A words, per-iter trace)."""
+    m = len(offs) - 1
+    A = init_assignment(seed, n_vars) if A0 is None else np.array(A0, np.uint32)
+    st = OrcStats()
+    rows = []
+
+    def cb(user, it, nu, nm, dres, Ap):
+        if trace:
+            rows.append((int(it), int(nu), int(nm), int(dres),
+                         np.ctypeslib.as_array(Ap, shape=(A.size,)).copy()))
+
+    cbf = ITER_CB(cb)
+    lib().orc_solve(n_vars, m, _p(offs, _u64p), _p(lits, _u32p), seed, max_iters, _p(A, _u32p),
+                    ctypes.byref(st), cbf, None)
+    stats = {k: int(getattr(st, k)) for k, _ in OrcStats._fields_ if k != "pad"}
+    return stats, A, rows
+
+
+def dimacs_parse(text: bytes):
+    v = ctypes.c_uint32()
+    c = ctypes.c_uint64()
+    ln = ctypes.c_uint64()
+    rc = lib().orc_dimacs_parse(text, len(text), ctypes.byref(v), ctypes.byref(c), None, None,
+                                ctypes.byref(ln))
+    if rc == -1:
+        return rc, None
+    offs = np.zeros(c.value + 1, np.uint64)
+    lits = np.zeros(max(1, ln.value), np.uint32)
+    rc = lib().orc_dimacs_parse(text, len(text), ctypes.byref(v), ctypes.byref(c),
+                                _p(offs, _u64p), _p(lits, _u32p), ctypes.byref(ln))
+    return rc, (int(v.value), offs, lits[:ln.value].copy())
+
+
+# ----------------------------------------------------------------- reference run
+def read_trace(path):
+    """Parse oracle/_ref/ref_probe `trace` output."""
+    with open(path, "rb") as f:
+        data = f.read()
+    assert data[:4] == b"ALRT"
+    n_vars, T = struct.unpack_from("<II", data, 4)
+    (m,) = struct.unpack_from("<Q", data, 12)
+    p = 20
+    iters = []
+    while True:
+        (it,) = struct.unpack_from("<Q", data, p)
+        p += 8
+        if it == 0xFFFFFFFFFFFFFFFF:
+            break
+        A = np.frombuffer(data, np.uint8, n_vars, p).copy()
+        p += n_vars
+        (nu,) = struct.unpack_from("<Q", data, p)
+        p += 8
+        U = np.frombuffer(data, np.uint32, nu, p).copy()
+        p += 4 * nu
+        (nm,) = struct.unpack_from("<Q", data, p)
+        p += 8
+        M = np.frombuffer(data, np.uint32, nm, p).copy()
+        p += 4 * nm
+        (dres,) = struct.unpack_from("<Q", data, p)
+        p += 8
+        iters.append(dict(it=it, A=A, U=U, M=M, dres=dres))
+    n_it, n_res, avg = struct.unpack_from("<QQQ", data, p)
+    p += 24
+    Af = np.frombuffer(data, np.uint8, n_vars, p).copy()
+    return dict(n_vars=n_vars, m=m, T=T, iters=iters,
+                stats=dict(n_iterations=n_it, n_resamples=n_res, avg_mis_size=avg), A_final=Af)

@@ -1,0 +1,311 @@
+// ref_probe.cpp -- TEST INFRASTRUCTURE ONLY.
+//
+// A driver around the reference's OWN code, compiled from the sources where they lie
+// under /root/reference (see oracle/Makefile; nothing is copied into this repo).  It
+// produces the golden vectors that pin the oracle (tests/golden/) and times the
+// reference's -p OpenMP path for bench.py's cpu_baseline leg.
+//
+//   trace <cnf> <T> <max_iters> <rd_seed> <out.bin>   per-iteration (A_i, U_i, M_i, dres)
+//   solve <cnf> <T> <rd_seed>                          real SATInstance::solve, prints stats
+//   bench <cnf> <T> <budget_s> <eval_reps>             eval-phase and full-iteration timing
+//   bench-gen <n> <m> <k> <kind> <gen_seed> <T> <budget_s> <eval_reps>   same, generated instance
+//   cnf   <cnf>                                        cnf_header_read/cnf_data_read output
+//
+// The load/encode/chunk sequence restates example/main.cpp:133-181 (main.cpp itself needs
+// Boost.program_options, absent here).  std::random_device::_M_getval is interposed by a
+// seeded LCG so VariablesArray init (VariablesArray.h:24) and every resample_clauses
+// engine seed (SATInstance.h:346) are reproducible.
+#include <chrono>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <string>
+#include <unordered_map>
+#include <vector>
+#include <set>
+#include <fstream>
+#include <iostream>
+#include <utility>
+#include <omp.h>
+
+static unsigned long long g_rd_state = 1;
+unsigned int std::random_device::_M_getval() {
+    g_rd_state = g_rd_state * 6364136223846793005ULL + 1442695040888963407ULL;
+    return (unsigned int)(g_rd_state >> 33);
+}
+
+extern "C" {
+#include "alll_oracle.h"
+}
+
+#define private public
+#include "SATInstance.h"
+#undef private
+#include "cnf_io/cnf_io.h"
+
+typedef uint32_t UINT_T;
+typedef SATInstance<UINT_T>::ClauseArray ClauseArray;
+
+struct Loaded {
+    int v_num = 0, c_num = 0, l_num = 0;
+    std::vector<ClauseArray*>* clauses = nullptr;
+    std::vector<Clause<UINT_T>*> all;  // clause index -> Clause*
+    std::unordered_map<const Clause<UINT_T>*, uint32_t> index;
+};
+
+// example/main.cpp:133-178
+static Loaded load(const std::string& path, int n_threads) {
+    Loaded L;
+    if (cnf_header_read(path, &L.v_num, &L.c_num, &L.l_num)) {
+        fprintf(stderr, "header read failed\n");
+        exit(1);
+    }
+    int* l_c_num = new int[L.c_num + 1];
+    int* l_val = new int[L.l_num + 1];
+    cnf_data_read(path, L.v_num, L.c_num, L.l_num, l_c_num, l_val);
+    int chunk_size = ceil(L.c_num / (double)n_threads);
+    L.clauses = new std::vector<ClauseArray*>();
+    for (int t = 0; t < n_threads; t++) L.clauses->push_back(new ClauseArray());
+    int c, l, l_c;
+    l = 0;
+    unsigned short int t = 0;
+    for (c = 0; c < L.c_num; c++) {
+        auto literals = new std::vector<UINT_T>;
+        for (l_c = 0; l_c < l_c_num[c]; l_c++) {
+            literals->push_back((0 < l_val[l]) ? (2 * l_val[l]) - 2 : ((-2) * l_val[l]) - 1);
+            l += 1;
+        }
+        if (c > (t + 1) * chunk_size) t += 1;
+        auto cl = new Clause<UINT_T>(literals, t);
+        L.clauses->at(t)->push_back(cl);
+        L.all.push_back(cl);
+        L.index[cl] = (uint32_t)c;
+    }
+    delete[] l_c_num;
+    delete[] l_val;
+    return L;
+}
+
+// Same chunking as load(), clauses from the oracle's generator (shared spec with the product).
+static Loaded load_gen(uint32_t n, uint64_t m, uint32_t k, int kind, uint64_t seed, int n_threads) {
+    Loaded L;
+    L.v_num = (int)n;
+    L.c_num = (int)m;
+    L.l_num = (int)(m * k);
+    std::vector<uint32_t> lits((size_t)m * k);
+    orc_generate_ksat(seed, n, m, k, kind, 0, m, lits.data());
+    int chunk_size = ceil(L.c_num / (double)n_threads);
+    L.clauses = new std::vector<ClauseArray*>();
+    for (int t = 0; t < n_threads; t++) L.clauses->push_back(new ClauseArray());
+    unsigned short int t = 0;
+    for (int c = 0; c < L.c_num; c++) {
+        auto literals = new std::vector<UINT_T>(lits.begin() + (size_t)c * k, lits.begin() + (size_t)(c + 1) * k);
+        if (c > (t + 1) * chunk_size) t += 1;
+        L.clauses->at(t)->push_back(new Clause<UINT_T>(literals, t));
+    }
+    return L;
+}
+
+static void wr(FILE* f, const void* p, size_t n) { fwrite(p, 1, n, f); }
+static void wr64(FILE* f, uint64_t x) { wr(f, &x, 8); }
+
+// The P1 eval loop of parallel_solve (SATInstance.h:264-280), same pragma.
+static std::vector<ClauseArray*>* eval_chunks(SATInstance<UINT_T>* S, std::vector<ClauseArray*>* clauses,
+                                             int n_threads) {
+    auto unsat_clauses = new std::vector<ClauseArray*>;
+    for (int t = 0; t < n_threads; t++) unsat_clauses->push_back(new ClauseArray());
+    auto var_arr = S->var_arr;
+#pragma omp parallel for schedule(static, 1) default(none) shared(clauses, unsat_clauses, n_threads, var_arr)
+    for (int t = 0; t < n_threads; t++) {
+        for (auto clause = clauses->at(t)->begin(); clause != clauses->at(t)->end(); ++clause) {
+            if ((*clause)->is_not_satisfied(var_arr->vars)) unsat_clauses->at(t)->push_back(*clause);
+        }
+    }
+    return unsat_clauses;
+}
+
+static int cmd_trace(int argc, char** argv) {
+    std::string path = argv[2];
+    int T = atoi(argv[3]);
+    uint64_t max_iters = strtoull(argv[4], 0, 10);
+    g_rd_state = strtoull(argv[5], 0, 10);
+    FILE* f = fopen(argv[6], "wb");
+    Loaded L = load(path, T);
+    auto S = new SATInstance<UINT_T>(new VariablesArray<UINT_T>(L.v_num), T);
+    for (auto c : *L.clauses) S->n_clauses += c->size();  // SATInstance.h:61-63
+    omp_set_num_threads(T);
+    wr(f, "ALRT", 4);
+    uint32_t hdr[2] = {(uint32_t)L.v_num, (uint32_t)T};
+    wr(f, hdr, 8);
+    wr64(f, (uint64_t)L.c_num);
+    // parallel_solve body (SATInstance.h:254-317) with the reference's own MIS / resample.
+    auto statistics = new Statistics;
+    for (int i = 0; i < T; i++) statistics->n_thread_resamples.push_back(0);
+    auto mis = new ClauseArray();
+    uint64_t it = 0;
+    std::vector<uint8_t> A(L.v_num);
+    while (true) {
+        statistics->n_iterations += 1;
+        for (int v = 0; v < L.v_num; ++v) A[v] = S->var_arr->vars[v] ? 1 : 0;
+        auto unsat = eval_chunks(S, L.clauses, T);
+        std::vector<uint32_t> U;
+        for (auto s : *unsat)
+            for (auto c : *s) U.push_back(L.index[c]);
+        wr64(f, statistics->n_iterations);
+        wr(f, A.data(), A.size());
+        wr64(f, U.size());
+        wr(f, U.data(), U.size() * 4);
+        if (S->check_if_noUNSAT(unsat)) {
+            wr64(f, 0);
+            wr64(f, 0);
+            break;
+        }
+        if (max_iters && statistics->n_iterations >= max_iters) {
+            // capped: record the MIS the reference would pick, but do not resample
+            S->populate_mis_parallel(unsat, mis, false);
+            wr64(f, mis->size());
+            for (auto c : *mis) { uint32_t x = L.index[c]; wr(f, &x, 4); }
+            wr64(f, 0);
+            mis->clear();
+            break;
+        }
+        S->populate_mis_parallel(unsat, mis, false);
+        statistics->avg_mis_size += mis->size();
+        wr64(f, mis->size());
+        for (auto c : *mis) { uint32_t x = L.index[c]; wr(f, &x, 4); }
+        ull before = 0;
+        for (auto x : statistics->n_thread_resamples) before += x;
+        S->resample_clauses(mis, statistics);
+        ull after = 0;
+        for (auto x : statistics->n_thread_resamples) after += x;
+        wr64(f, after - before);
+        mis->clear();
+        ++it;
+    }
+    for (int t = 0; t < T; t++) statistics->n_resamples += statistics->n_thread_resamples.at(t);
+    statistics->avg_mis_size = (ull)(statistics->avg_mis_size / statistics->n_iterations);
+    wr64(f, ~0ull);
+    wr64(f, statistics->n_iterations);
+    wr64(f, statistics->n_resamples);
+    wr64(f, statistics->avg_mis_size);
+    for (int v = 0; v < L.v_num; ++v) A[v] = S->var_arr->vars[v] ? 1 : 0;
+    wr(f, A.data(), A.size());
+    fclose(f);
+    return 0;
+}
+
+static int cmd_solve(int argc, char** argv) {
+    std::string path = argv[2];
+    int T = atoi(argv[3]);
+    g_rd_state = strtoull(argv[4], 0, 10);
+    Loaded L = load(path, T);
+    auto S = new SATInstance<UINT_T>(new VariablesArray<UINT_T>(L.v_num), T);
+    Statistics* st = S->solve(L.clauses);
+    bool ok = S->verify_validity(L.clauses);
+    printf("{\"n_iterations\": %llu, \"n_resamples\": %llu, \"avg_mis_size\": %llu, \"valid\": %d, \"assignment\": \"",
+           st->n_iterations, st->n_resamples, st->avg_mis_size, ok ? 1 : 0);
+    for (int v = 0; v < L.v_num; ++v) putchar(S->var_arr->vars[v] ? '1' : '0');
+    printf("\"}\n");
+    return 0;
+}
+
+static int cmd_cnf(int argc, char** argv) {
+    std::string path = argv[2];
+    int v = 0, c = 0, l = 0;
+    if (cnf_header_read(path, &v, &c, &l)) { printf("{\"error\": 1}\n"); return 0; }
+    std::vector<int> lc(c + 1, -1), lv(l + 1, 0);
+    cnf_data_read(path, v, c, l, lc.data(), lv.data());
+    printf("{\"v_num\": %d, \"c_num\": %d, \"l_num\": %d, \"l_c_num\": [", v, c, l);
+    for (int i = 0; i < c; ++i) printf("%s%d", i ? ", " : "", lc[i]);
+    printf("], \"l_val\": [");
+    for (int i = 0; i < l; ++i) printf("%s%d", i ? ", " : "", lv[i]);
+    printf("]}\n");
+    return 0;
+}
+
+// CPU baseline: the reference's -p path (P1 eval with its OpenMP pragma, populate_mis_parallel,
+// resample_clauses) on the node's host cores.
+static int bench_loaded(Loaded& L, int T, double budget, int eval_reps, double load_s) {
+    auto S = new SATInstance<UINT_T>(new VariablesArray<UINT_T>(L.v_num), T);
+    omp_set_num_threads(T);
+    // (a) eval phase only, best of eval_reps
+    double best = 0;
+    for (int r = 0; r < eval_reps; ++r) {
+        auto a = std::chrono::steady_clock::now();
+        auto u = eval_chunks(S, L.clauses, T);
+        double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - a).count();
+        if (r == 0 || dt < best) best = dt;
+        for (auto s : *u) delete s;
+        delete u;
+    }
+    // (b) full iterations within the wall budget
+    auto statistics = new Statistics;
+    for (int i = 0; i < T; i++) statistics->n_thread_resamples.push_back(0);
+    auto mis = new ClauseArray();
+    uint64_t iters = 0;
+    bool solved = false;
+    auto b0 = std::chrono::steady_clock::now();
+    double el = 0;
+    while (el < budget) {
+        statistics->n_iterations += 1;
+        auto unsat = eval_chunks(S, L.clauses, T);
+        if (S->check_if_noUNSAT(unsat)) { solved = true; break; }
+        S->populate_mis_parallel(unsat, mis, false);
+        statistics->avg_mis_size += mis->size();
+        S->resample_clauses(mis, statistics);
+        mis->clear();
+        ++iters;
+        el = std::chrono::duration<double>(std::chrono::steady_clock::now() - b0).count();
+    }
+    el = std::chrono::duration<double>(std::chrono::steady_clock::now() - b0).count();
+    printf("{\"threads\": %d, \"n_vars\": %d, \"n_clauses\": %d, \"load_s\": %.6f, \"eval_best_s\": %.6f, "
+           "\"eval_clause_evals_per_s\": %.6e, \"iters\": %llu, \"iters_s\": %.6f, \"solved\": %d}\n",
+           T, L.v_num, L.c_num, load_s, best, best > 0 ? L.c_num / best : 0.0, (unsigned long long)iters, el,
+           solved ? 1 : 0);
+    return 0;
+}
+
+// CPU baseline: the reference's -p path (P1 eval with its OpenMP pragma, populate_mis_parallel,
+// resample_clauses) on the node's host cores.
+static int cmd_bench(int argc, char** argv) {
+    std::string path = argv[2];
+    int T = atoi(argv[3]);
+    g_rd_state = 12345;
+    auto t0 = std::chrono::steady_clock::now();
+    Loaded L = load(path, T);
+    double load_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return bench_loaded(L, T, atof(argv[4]), atoi(argv[5]), load_s);
+}
+
+//   bench-gen <n> <m> <k> <kind> <gen_seed> <T> <budget_s> <eval_reps>
+static int cmd_bench_gen(int argc, char** argv) {
+    uint32_t n = (uint32_t)strtoul(argv[2], 0, 10);
+    uint64_t m = strtoull(argv[3], 0, 10);
+    uint32_t k = (uint32_t)strtoul(argv[4], 0, 10);
+    int kind = atoi(argv[5]);
+    uint64_t seed = strtoull(argv[6], 0, 10);
+    int T = atoi(argv[7]);
+    g_rd_state = 12345;
+    auto t0 = std::chrono::steady_clock::now();
+    Loaded L = load_gen(n, m, k, kind, seed, T);
+    double load_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return bench_loaded(L, T, atof(argv[8]), atoi(argv[9]), load_s);
+}
+
+int main(int argc, char** argv) {
+    if (argc < 3) {
+        fprintf(stderr, "usage: ref_probe trace|solve|bench|cnf ...\n");
+        return 2;
+    }
+    std::string cmd = argv[1];
+    if (cmd == "trace" && argc >= 7) return cmd_trace(argc, argv);
+    if (cmd == "solve" && argc >= 5) return cmd_solve(argc, argv);
+    if (cmd == "bench" && argc >= 6) return cmd_bench(argc, argv);
+    if (cmd == "bench-gen" && argc >= 10) return cmd_bench_gen(argc, argv);
+    if (cmd == "cnf") return cmd_cnf(argc, argv);
+    fprintf(stderr, "bad arguments\n");
+    return 2;
+}

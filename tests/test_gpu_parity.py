@@ -1,0 +1,286 @@
+"""GPU parity: the HIP path through the C-ABI against the reference golden vectors and the
+oracle (CPU restatement of the serial path), bit-exact.
+
+  * reference maps on the GPU: for every T=1 golden trajectory, the device evaluates
+    A_i -> U_i and picks M_i exactly as the reference did (SATInstance.h:264-280, 391-451);
+  * full trajectories with Philox vs the oracle: assignment after every iteration,
+    violated count, MIS, final Statistics (SATInstance.h:25-32, 313-317);
+  * BASELINE sizes (10M clauses 3-SAT, 8-SAT 6M, power-law 10M): per-iteration bit-exact
+    steps against the oracle for a few iterations;
+  * edge cases: empty instance, empty clause (never solvable -> max_iters), tautologies,
+    duplicate variables, unit / wide clauses, max_iters cap semantics.
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+T1_FIXTURES = sorted(p for p in glob.glob(os.path.join(GOLDEN, "*_T1.npz")))
+LAYOUTS = {"fixed": 0, "csr": 1 << 2}
+
+
+@pytest.fixture(scope="module")
+def gpu(native):
+    from alllsatisfiabilitysolver_amd import device_count
+
+    if device_count() == 0:
+        pytest.fail("no GPU visible: the gpu tests must run on an MI355X")
+    return True
+
+
+def mask_to_list(vm, m):
+    bits = np.unpackbits(vm.view(np.uint8), bitorder="little")[:m]
+    return np.nonzero(bits)[0].astype(np.uint32)
+
+
+@pytest.mark.parametrize("layout", list(LAYOUTS))
+@pytest.mark.parametrize("path", T1_FIXTURES, ids=lambda p: os.path.basename(p)[:-4])
+def test_reference_maps_on_gpu(gpu, path, layout):
+    from alllsatisfiabilitysolver_amd import Solver
+
+    f = dict(np.load(path, allow_pickle=False))
+    n, offs, lits = int(f["n_vars"]), f["offs"], f["lits"]
+    m = offs.size - 1
+    with Solver(n, offs, lits, seed=3, flags=LAYOUTS[layout]) as s:
+        for i in range(f["A"].shape[0]):
+            s.set_assignment_words(f["A"][i])
+            before = s.stats()
+            s.run(1)
+            U_ref = f["U"][int(f["U_ptr"][i]):int(f["U_ptr"][i + 1])]
+            np.testing.assert_array_equal(mask_to_list(s.violated_mask(), m), U_ref, err_msg=f"U_{i}")
+            after = s.stats()
+            if U_ref.size == 0:
+                assert after["solved"] == 1
+                break
+            M_ref = f["M"][int(f["M_ptr"][i]):int(f["M_ptr"][i + 1])]
+            np.testing.assert_array_equal(s.mis(), np.sort(M_ref), err_msg=f"M_{i}")
+            if int(f["dres"][i]):
+                assert after["n_resamples"] - before["n_resamples"] == int(f["dres"][i])
+            assert after["sum_mis_size"] - before["sum_mis_size"] == M_ref.size
+
+
+def _instances():
+    from alllsatisfiabilitysolver_amd import generate_ksat
+
+    out = {}
+    for name, (n, m, k, kind) in {
+        "c1_ratio4": (200, 800, 3, 0),
+        "u2500_ratio4": (2500, 10000, 3, 0),
+        "ratio2_solves": (200, 400, 3, 0),
+        "k8": (4000, 6000, 8, 0),
+        "powerlaw": (2000, 8000, 3, 1),
+        "k5_multi_tile": (30000, 60000, 5, 0),
+    }.items():
+        out[name] = (n,) + generate_ksat(1, n, m, k, kind)
+    f = dict(np.load(os.path.join(GOLDEN, "edge_T1.npz")))
+    out["edge"] = (int(f["n_vars"]), f["offs"], f["lits"])
+    # ragged widths across several tiles
+    rng = np.random.default_rng(5)
+    w = rng.integers(1, 12, 20000)
+    offs = np.zeros(w.size + 1, np.uint64)
+    offs[1:] = np.cumsum(w)
+    lits = rng.integers(0, 2 * 9000, int(offs[-1])).astype(np.uint32)
+    out["ragged"] = (9000, offs, lits)
+    return out
+
+
+INSTANCES = None
+
+
+def instances():
+    global INSTANCES
+    if INSTANCES is None:
+        INSTANCES = _instances()
+    return INSTANCES
+
+
+@pytest.mark.parametrize("layout", list(LAYOUTS))
+@pytest.mark.parametrize("name", ["c1_ratio4", "u2500_ratio4", "ratio2_solves", "k8", "powerlaw",
+                                  "k5_multi_tile", "edge", "ragged"])
+def test_trajectory_matches_oracle(gpu, oracle_mod, name, layout):
+    from alllsatisfiabilitysolver_amd import Solver
+
+    o = oracle_mod
+    n, offs, lits = instances()[name]
+    seed, K = 12345, 40
+    st_o, A_o, rows = o.solve(n, offs, lits, seed, max_iters=K, trace=True)
+    with Solver(n, offs, lits, seed=seed, flags=LAYOUTS[layout]) as s:
+        np.testing.assert_array_equal(s.assignment_words(), o.init_assignment(seed, n))
+        for it, nu, nm, dres, A_after in rows:
+            before = s.stats()
+            s.run(1)
+            after = s.stats()
+            assert after["n_violated"] == nu, f"iter {it}"
+            assert after["sum_mis_size"] - before["sum_mis_size"] == nm, f"iter {it}"
+            assert after["n_resamples"] - before["n_resamples"] == dres, f"iter {it}"
+            np.testing.assert_array_equal(s.assignment_words(), A_after, err_msg=f"A after iter {it}")
+    # whole solve with the same cap: identical Statistics and assignment
+    with Solver(n, offs, lits, seed=seed, max_iters=K, flags=LAYOUTS[layout]) as s:
+        st = s.solve()
+        for k in ("n_iterations", "n_resamples", "avg_mis_size", "sum_mis_size", "solved"):
+            assert st[k] == st_o[k], k
+        np.testing.assert_array_equal(s.assignment_words(), A_o)
+
+
+def test_solve_converges_and_verifies(gpu, oracle_mod):
+    from alllsatisfiabilitysolver_amd import Solver, generate_ksat
+
+    n, m = 25000, 50000  # ratio 2: converges in ~100 iterations
+    offs, lits = generate_ksat(2, n, m, 3)
+    st_o, A_o, _ = oracle_mod.solve(n, offs, lits, 99)
+    assert st_o["solved"] == 1
+    with Solver(n, offs, lits, seed=99) as s:
+        st = s.solve()
+        assert st["solved"] == 1
+        for k in ("n_iterations", "n_resamples", "avg_mis_size"):
+            assert st[k] == st_o[k]
+        np.testing.assert_array_equal(s.assignment_words(), A_o)
+        ok, nv = s.verify()
+        assert ok and nv == 0
+        nu, _ = oracle_mod.eval_mask(offs, lits, s.assignment_words())
+        assert nu == 0
+
+
+def test_max_iters_and_unsolvable(gpu, oracle_mod):
+    from alllsatisfiabilitysolver_amd import Solver
+
+    # empty clause: always violated (reference loops forever; here max_iters ends it)
+    offs = np.array([0, 2, 2, 3], np.uint64)
+    lits = np.array([0, 3, 4], np.uint32)
+    st_o, A_o, _ = oracle_mod.solve(3, offs, lits, 5, max_iters=9)
+    with Solver(3, offs, lits, seed=5, max_iters=9) as s:
+        st = s.solve()
+        assert st["solved"] == 0 and st["n_iterations"] == 9
+        for k in ("n_iterations", "n_resamples", "avg_mis_size"):
+            assert st[k] == st_o[k]
+        ok, nv = s.verify()
+        assert not ok and nv >= 1
+
+
+def test_empty_instance(gpu):
+    from alllsatisfiabilitysolver_amd import Solver
+
+    with Solver(10, np.zeros(1, np.uint64), np.zeros(0, np.uint32), seed=1) as s:
+        st = s.solve()
+        assert st["solved"] == 1 and st["n_iterations"] == 1 and st["n_resamples"] == 0
+
+
+@pytest.mark.parametrize("grid_rounds", [1, 2, 3, 8])
+def test_grid_round_split_is_invisible(gpu, oracle_mod, grid_rounds):
+    """The split between full-grid LFMIS rounds and the single-workgroup tail changes
+    nothing: same trajectory as the oracle."""
+    from alllsatisfiabilitysolver_amd import Solver
+
+    n, offs, lits = instances()["k5_multi_tile"]
+    st_o, A_o, rows = oracle_mod.solve(n, offs, lits, 77, max_iters=12, trace=True)
+    with Solver(n, offs, lits, seed=77, max_iters=12, grid_rounds=grid_rounds) as s:
+        st = s.solve()
+        assert st["n_resamples"] == st_o["n_resamples"]
+        np.testing.assert_array_equal(s.assignment_words(), A_o)
+
+
+def _oracle_step(o, n, offs, lits, A, seed, it):
+    """One serial iteration (eval -> LFMIS -> Philox resample) on the CPU."""
+    m = offs.size - 1
+    nu, vm = o.eval_mask(offs, lits, A)
+    U = o.mask_to_list(m, vm)
+    M = o.lfmis(n, offs, lits, U)
+    A2 = A.copy()
+    k = int(offs[1] - offs[0]) if m else 0
+    fixed = m and np.all(np.diff(offs) == k)
+    if fixed:
+        vs = np.unique((lits.reshape(-1, k)[M.astype(np.int64)] >> 1).ravel())
+    else:
+        vs = np.unique(np.concatenate([lits[offs[c]:offs[c + 1]] for c in M]) >> 1)
+    bits = np.array([o.resample_bit(seed, it, int(v)) for v in vs], np.uint32) if vs.size < 50000 else None
+    if bits is None:  # vectorised Philox for big MIS sets
+        bits = philox_bits(seed, it, vs)
+    w = vs >> 5
+    sh = (vs & 31).astype(np.uint32)
+    np.bitwise_and.at(A2, w, ~(np.uint32(1) << sh))
+    np.bitwise_or.at(A2, w, bits.astype(np.uint32) << sh)
+    return nu, vm, M, A2
+
+
+def philox_bits(seed, it, vs):
+    """numpy Philox4x32-10 (x word & 1) for ctr={v, it_lo, 0, it_hi}; pinned to the C oracle
+    in test_numpy_philox_matches_oracle."""
+    M0, M1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)
+    c0 = vs.astype(np.uint64)
+    c1 = np.full_like(c0, it & 0xFFFFFFFF)
+    c2 = np.zeros_like(c0)
+    c3 = np.full_like(c0, it >> 32)
+    k0, k1 = np.uint64(seed & 0xFFFFFFFF), np.uint64(seed >> 32)
+    mask = np.uint64(0xFFFFFFFF)
+    for _ in range(10):
+        p0 = M0 * c0
+        p1 = M1 * c2
+        hi0, lo0 = p0 >> np.uint64(32), p0 & mask
+        hi1, lo1 = p1 >> np.uint64(32), p1 & mask
+        c0, c1, c2, c3 = (hi1 ^ c1 ^ k0) & mask, lo1, (hi0 ^ c3 ^ k1) & mask, lo0
+        k0 = (k0 + np.uint64(0x9E3779B9)) & mask
+        k1 = (k1 + np.uint64(0xBB67AE85)) & mask
+    return (c0 & np.uint64(1)).astype(np.uint32)
+
+
+def test_numpy_philox_matches_oracle(oracle_mod):
+    vs = np.arange(0, 3000, 7, dtype=np.uint32)
+    for seed, it in [(1, 0), (12345, 77), ((7 << 32) | 9, (3 << 32) | 5)]:
+        ref = np.array([oracle_mod.resample_bit(seed, it, int(v)) for v in vs], np.uint32)
+        np.testing.assert_array_equal(philox_bits(seed, it, vs), ref)
+
+
+BIG = {
+    "M_3sat_10M": (2_500_000, 10_000_000, 3, 0),
+    "C2_3sat_4M": (1_000_000, 4_000_000, 3, 0),
+    "C3_8sat_6M": (4_000_000, 6_000_000, 8, 0),
+    "C5_powerlaw_10M": (2_500_000, 10_000_000, 3, 1),
+}
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("name", list(BIG))
+def test_baseline_sizes_bit_exact_steps(gpu, oracle_mod, name):
+    from alllsatisfiabilitysolver_amd import Solver, generate_ksat
+
+    n, m, k, kind = BIG[name]
+    offs, lits = generate_ksat(1, n, m, k, kind)
+    seed = 1
+    with Solver(n, offs, lits, seed=seed) as s:
+        A = s.assignment_words()
+        np.testing.assert_array_equal(A, oracle_mod.init_assignment(seed, n))
+        for it in range(2):
+            nu, vm, M, A_next = _oracle_step(oracle_mod, n, offs, lits, A, seed, it)
+            before = s.stats()
+            s.run(1)
+            after = s.stats()
+            assert after["n_violated"] == nu
+            np.testing.assert_array_equal(s.violated_mask(), vm[: (m + 63) // 64])
+            np.testing.assert_array_equal(s.mis(), M)
+            assert after["sum_mis_size"] - before["sum_mis_size"] == M.size
+            A = s.assignment_words()
+            np.testing.assert_array_equal(A, A_next)
+        # size-independent properties on the device path
+        ok, nv = s.verify()
+        assert nv == oracle_mod.eval_mask(offs, lits, A)[0]
+
+
+def test_bench_helpers(gpu, oracle_mod):
+    from alllsatisfiabilitysolver_amd import Solver, generate_ksat
+
+    n, m = 50000, 200000
+    offs, lits = generate_ksat(1, n, m, 3)
+    with Solver(n, offs, lits, seed=4) as s:
+        ms, nv = s.bench_eval(5)
+        assert ms > 0
+        assert nv == oracle_mod.eval_mask(offs, lits, s.assignment_words())[0]
+        assert s.eval_bytes() == 12 * m + (n + 7) // 8 + (m + 7) // 8
+        pt = s.profile(3)
+        assert pt["iterations"] == 3 and pt["eval_ms"] > 0 and pt["total_ms"] >= pt["eval_ms"]
+        st = s.stats()
+        assert st["n_iterations"] == 3

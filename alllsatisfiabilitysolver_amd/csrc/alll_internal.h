@@ -15,6 +15,9 @@ constexpr int EVAL_THREADS = 256;
 constexpr int ROUND_THREADS = 256;
 constexpr int TAIL_THREADS = 1024;
 constexpr int MAX_FIXED_K = 8;
+// Every LFMIS round decides at least the lowest undecided clause, so rounds <= |U|; the cap
+// only bounds a kernel that would otherwise run away on a bug or an adversarial chain.
+constexpr uint32_t MAX_TAIL_ROUNDS = 1u << 20;
 
 // Device-resident loop state.  Written only by the single-block reduce / tail kernels,
 // read by every other kernel at entry (kernel boundaries order the accesses).
@@ -31,7 +34,7 @@ struct DevState {
     uint32_t round_next;   // first unused epoch
     uint32_t tail_rounds;  // rounds the tail kernel needed in the last iteration
     uint32_t max_rounds;   // max total rounds seen in one iteration
-    uint32_t pad;
+    uint32_t error;        // 1: LFMIS exceeded MAX_TAIL_ROUNDS (loop stopped, done = 3)
 };
 
 // Clause storage on the device.

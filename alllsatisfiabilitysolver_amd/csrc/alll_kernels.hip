@@ -404,6 +404,10 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail(ClauseView cv, LoopBuffer
         ++rounds;
         ++epoch;
         if (left == 0) break;
+        if (rounds >= MAX_TAIL_ROUNDS) {
+            if (threadIdx.x == 0) { st->error = 1; st->done = 3; }
+            break;
+        }
         __syncthreads();
     }
     if (threadIdx.x == 0) {

@@ -97,6 +97,8 @@ int dalloc(alll_ctx* c, T** p, size_t count, int fill = 0) {
 int read_state(alll_ctx* c) {
     HIP_TRY(hipMemcpyAsync(c->h_state, c->b.state, sizeof(DevState), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->h_state->error)
+        return fail(ALLL_ERR_UNSUPPORTED, "LFMIS needed more than %u rounds in one iteration", MAX_TAIL_ROUNDS);
     return ALLL_OK;
 }
 

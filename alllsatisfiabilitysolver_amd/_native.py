@@ -28,6 +28,7 @@ ALLL_ERR_UNSUPPORTED = 10
 FLAG_NO_GRAPH = 1 << 0
 FLAG_EXCHANGE_ALLREDUCE = 1 << 1
 FLAG_GENERIC_CSR = 1 << 2
+FLAG_NO_RANGED = 1 << 3
 
 MAX_GPU_STATS = 64
 
@@ -38,7 +39,7 @@ EXPORTED = [
     "alll_get_stats", "alll_verify", "alll_get_assignment", "alll_set_assignment",
     "alll_get_assignment_words", "alll_set_assignment_words", "alll_get_violated_mask",
     "alll_get_mis", "alll_bench_eval", "alll_profile", "alll_synchronize", "alll_eval_bytes",
-    "alll_layout", "alll_initial_assignment", "alll_dimacs_parse", "alll_dimacs_read", "alll_generate_ksat",
+    "alll_layout", "alll_eval_kernel", "alll_initial_assignment", "alll_shard_plan", "alll_dimacs_parse", "alll_dimacs_read", "alll_generate_ksat",
 ]
 
 
@@ -132,6 +133,8 @@ _SIGS = {
     "alll_synchronize": ([_vp], ctypes.c_int),
     "alll_eval_bytes": ([_vp], ctypes.c_uint64),
     "alll_layout": ([_vp], ctypes.c_int),
+    "alll_eval_kernel": ([_vp], ctypes.c_char_p),
+    "alll_shard_plan": ([ctypes.c_uint64, ctypes.c_int, ctypes.c_int, _u64p, _u64p, _u64p], ctypes.c_int),
     "alll_initial_assignment": ([ctypes.c_uint64, ctypes.c_uint32, _u8p], ctypes.c_int),
     "alll_dimacs_parse": ([ctypes.c_char_p, ctypes.c_uint64, _u32p, _u64p, _u64p, _u32p, _u64p], ctypes.c_int),
     "alll_dimacs_read": ([ctypes.c_char_p, _u32p, _u64p, _u64p, _u32p, _u64p], ctypes.c_int),

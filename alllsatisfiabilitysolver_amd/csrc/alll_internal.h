@@ -15,6 +15,12 @@ constexpr int EVAL_THREADS = 256;
 constexpr int ROUND_THREADS = 256;
 constexpr int TAIL_THREADS = 1024;
 constexpr int MAX_FIXED_K = 8;
+// Range-partitioned evaluation: the assignment words of one variable range live in LDS.
+constexpr uint32_t RANGE_WORDS = 38912;            // 152 KiB of LDS per range
+constexpr uint32_t RANGE_VARS = RANGE_WORDS * 32;  // 1,245,184 variables
+constexpr int MAX_RANGES = 4;
+constexpr int RANGED_THREADS = 1024;
+constexpr uint32_t RANGED_MAX_TILES = 16;          // tiles per block pass (64-bit sat mask/lane)
 // Every LFMIS round decides at least the lowest undecided clause, so rounds <= |U|; the cap
 // only bounds a kernel that would otherwise run away on a bug or an adversarial chain.
 constexpr uint32_t MAX_TAIL_ROUNDS = 1u << 20;
@@ -35,6 +41,8 @@ struct DevState {
     uint32_t tail_rounds;  // rounds the tail kernel needed in the last iteration
     uint32_t max_rounds;   // max total rounds seen in one iteration
     uint32_t error;        // 1: LFMIS exceeded MAX_TAIL_ROUNDS (loop stopped, done = 3)
+    uint32_t left_cnt;     // undecided entries handed from the last grid round to the tail
+    uint32_t tmis_cnt;     // MIS entries decided by the tail kernel (list b.tmis)
 };
 
 // Clause storage on the device.
@@ -44,6 +52,11 @@ struct ClauseView {
     const uint32_t* lits_t; // fixed-k only: chunk-transposed [c/256][j][c%256]
     uint64_t m;             // clauses
     uint32_t k;             // fixed width, 0 = generic CSR
+    // variable-range-partitioned layout (fixed k, n <= RANGE_VARS * MAX_RANGES):
+    uint32_t n_ranges;      // 0 = not built
+    const uint32_t* rlits[MAX_RANGES];  // literals whose variable is in range r, clause order
+    const uint32_t* rcnt[MAX_RANGES];   // 4-bit count per clause (8 clauses per word)
+    const uint32_t* rbase[MAX_RANGES];  // per 64-clause group: offset of its first literal
 };
 
 struct LoopBuffers {
@@ -53,6 +66,8 @@ struct LoopBuffers {
     uint32_t* stage;        // per tile: TILE slots of undecided violated clause ids
     uint32_t* mis_cnt;      // MIS entries per tile (current iteration)
     uint32_t* mis;          // per tile: TILE slots of MIS clause ids
+    uint32_t* left;         // compact list of undecided clauses handed to the tail kernel
+    uint32_t* tmis;         // MIS clauses decided by the tail kernel
     unsigned long long* owner; // per variable 64-bit owner key (epoch-tagged, never reset)
     uint32_t* cover;        // per variable: stamp of the iteration whose MIS covers it
     unsigned long long* tile_stats; // per tile: [2t] sum |MIS|, [2t+1] sum resampled literals
@@ -69,10 +84,13 @@ hipError_t launch_init_assignment(const LoopBuffers& b, hipStream_t s);
 hipError_t launch_init_state(const LoopBuffers& b, hipStream_t s);
 hipError_t launch_eval(const ClauseView& cv, const LoopBuffers& b, uint32_t tile_begin,
                        uint32_t tile_end, bool gated, hipStream_t s);
+hipError_t launch_eval_ranged(const ClauseView& cv, const LoopBuffers& b, uint32_t tile_begin,
+                              uint32_t tile_end, bool gated, int n_cu, hipStream_t s);
 hipError_t launch_collect(const ClauseView& cv, const LoopBuffers& b, uint32_t own_begin,
                           uint32_t own_end, hipStream_t s);
 hipError_t launch_reduce(const LoopBuffers& b, int mode, hipStream_t s);
-hipError_t launch_round(const ClauseView& cv, const LoopBuffers& b, uint32_t r, hipStream_t s);
+hipError_t launch_round(const ClauseView& cv, const LoopBuffers& b, uint32_t r, bool last,
+                        hipStream_t s);
 hipError_t launch_tail(const ClauseView& cv, const LoopBuffers& b, uint32_t first_round,
                        hipStream_t s);
 hipError_t launch_resample(const ClauseView& cv, const LoopBuffers& b, uint32_t tile_begin,

@@ -15,9 +15,24 @@
 //   k_resample Philox4x32-10 per-variable resampling of every MIS clause
 //              (resample_clauses, SATInstance.h:340-365).
 // Integer / bit work only: no MFMA.  HBM-bound on the literal stream of k_eval.
+#include <algorithm>
+
 #include "alll_internal.h"
 
 namespace alll {
+
+#define ALLL_DISPATCH_K(KV, CALL)                      \
+    switch (KV) {                                      \
+        case 1: { constexpr int K = 1; CALL; } break;  \
+        case 2: { constexpr int K = 2; CALL; } break;  \
+        case 3: { constexpr int K = 3; CALL; } break;  \
+        case 4: { constexpr int K = 4; CALL; } break;  \
+        case 5: { constexpr int K = 5; CALL; } break;  \
+        case 6: { constexpr int K = 6; CALL; } break;  \
+        case 7: { constexpr int K = 7; CALL; } break;  \
+        case 8: { constexpr int K = 8; CALL; } break;  \
+        default: { constexpr int K = 0; CALL; } break; \
+    }
 
 // ------------------------------------------------------------------------------------
 // Philox4x32-10, identical constants to oracle/alll_oracle.c (Random123 KAT-pinned).
@@ -146,6 +161,91 @@ __global__ __launch_bounds__(EVAL_THREADS) void k_eval_fixed(ClauseView cv, Loop
     publish_tile(b, tile, s_idx, s_wcnt, wcount, lane, wave);
 }
 
+// Clause evaluation, fixed width K, variable-range-partitioned (P <= MAX_RANGES phases).
+// Persistent: one 1024-thread workgroup per CU owns a contiguous run of tiles.  Phase r
+// stages the assignment words of variable range r in LDS (RANGE_WORDS) and streams the
+// literals of that range (compacted, clause order, 4-bit per-clause counts), so every
+// assignment lookup is an LDS read instead of an L2 request.  Each lane keeps the
+// "satisfied" bits of its clauses in a 64-bit register across phases; wave w evaluates the
+// 64-clause groups w, w+16, ... of the pass.  After the last phase the violated bits are
+// ballot-compacted into the per-tile lists exactly like k_eval_fixed.
+template <int K>
+__global__ __launch_bounds__(RANGED_THREADS) void k_eval_ranged(ClauseView cv, LoopBuffers b,
+                                                               uint32_t tile_begin, uint32_t tile_end,
+                                                               int gated) {
+    if (gated && eval_gate_closed(b.state)) return;
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_A[];
+    __shared__ uint32_t s_tcnt[RANGED_MAX_TILES];
+    const uint32_t nblk = gridDim.x;
+    const uint32_t ntiles = tile_end - tile_begin;
+    const uint32_t t0 = tile_begin + (uint32_t)(((uint64_t)ntiles * blockIdx.x) / nblk);
+    const uint32_t t1 = tile_begin + (uint32_t)(((uint64_t)ntiles * (blockIdx.x + 1)) / nblk);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    const uint64_t m = cv.m;
+    const uint32_t P = cv.n_ranges;
+    for (uint32_t pt = t0; pt < t1; pt += RANGED_MAX_TILES) {
+        const uint32_t pe = min(t1, pt + RANGED_MAX_TILES);
+        const uint32_t ngroups = (pe - pt) * TILE_WORDS;      // 64-clause groups of this pass
+        const uint64_t g0 = (uint64_t)pt * TILE_WORDS;
+        uint64_t sat = 0;
+        for (uint32_t r = 0; r < P; ++r) {
+            __syncthreads();
+            const uint32_t w_lo = r * RANGE_WORDS;
+            const uint32_t w_hi = min(b.n_words, w_lo + RANGE_WORDS);
+            for (uint32_t w = w_lo + threadIdx.x; w < w_hi; w += RANGED_THREADS) s_A[w - w_lo] = b.A[w];
+            __syncthreads();
+            const uint32_t* __restrict__ rl = cv.rlits[r];
+            const uint32_t* __restrict__ rc = cv.rcnt[r];
+            const uint32_t* __restrict__ rb = cv.rbase[r];
+            const uint32_t v_lo = r * RANGE_VARS;
+            const uint32_t n_i = ngroups > (uint32_t)wave ? (ngroups - wave + 15u) / 16u : 0u;
+            for (uint32_t i = 0; i < n_i; ++i) {
+                const uint64_t g = g0 + wave + 16u * i;
+                const uint32_t nib = (rc[g * 8 + (lane >> 3)] >> ((lane & 7) * 4)) & 15u;
+                uint32_t pre = 0;
+#pragma unroll
+                for (int t = 0; t < K; ++t) pre += __popcll(__ballot(nib > (uint32_t)t) & lt);
+                const uint32_t off = rb[g] + pre;
+                uint32_t sb = 0;
+#pragma unroll
+                for (int t = 0; t < K; ++t) {
+                    if ((uint32_t)t < nib) {
+                        const uint32_t l = rl[off + t];
+                        const uint32_t v = (l >> 1) - v_lo;
+                        sb |= ((s_A[v >> 5] >> (v & 31u)) & 1u) ^ (l & 1u);
+                    }
+                }
+                sat |= (uint64_t)sb << i;
+            }
+        }
+        // compaction into the per-tile lists
+        if (threadIdx.x < RANGED_MAX_TILES) s_tcnt[threadIdx.x] = 0;
+        __syncthreads();
+        for (uint32_t i = 0; i < 64; ++i) {
+            const uint32_t gl = wave + 16u * i;
+            if (gl >= ngroups) break;
+            const uint64_t g = g0 + gl;
+            const uint64_t c = g * 64 + lane;
+            const bool viol = !((sat >> i) & 1ull) && c < m;
+            const uint64_t mask = __ballot(viol);
+            if (lane == 0) b.vmask[g] = mask;
+            if (mask) {
+                const uint32_t tile = (uint32_t)(g / TILE_WORDS);
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(&s_tcnt[tile - pt], (uint32_t)__popcll(mask));
+                base = __shfl(base, 0, 64);
+                if (viol) b.stage[(uint64_t)tile * TILE + base + __popcll(mask & lt)] = (uint32_t)c;
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x < pe - pt) {
+            b.tile_cnt[pt + threadIdx.x] = s_tcnt[threadIdx.x];
+            b.mis_cnt[pt + threadIdx.x] = 0;
+        }
+    }
+}
+
 // Clause evaluation, generic CSR (ragged widths): lane per clause, 64 consecutive
 // clauses per wave step, 16 steps per wave.
 __global__ __launch_bounds__(EVAL_THREADS) void k_eval_csr(ClauseView cv, LoopBuffers b,
@@ -226,6 +326,8 @@ __global__ __launch_bounds__(1024) void k_reduce(LoopBuffers b, int mode) {
     if (mode == 1) { st->count_out = u; return; }
     st->n_iter += 1;
     st->u_total = u;
+    st->left_cnt = 0;
+    st->tmis_cnt = 0;
     st->stamp = (uint32_t)st->n_iter ? (uint32_t)st->n_iter : 1u;
     st->round_base = st->round_next;
     if (u == 0) { st->done = 1; st->active = 0; }
@@ -273,10 +375,11 @@ __global__ __launch_bounds__(ROUND_THREADS) void k_claim(ClauseView cv, LoopBuff
 
 // Phase JOIN: a clause that owns all of its variables has no undecided lower-index
 // neighbour, and every decided lower neighbour is out, so it is in the LFMIS: mark its
-// variables covered and append it to the tile's MIS list.
+// variables covered and append it to the tile's MIS list.  In the last grid round the
+// still-undecided clauses move to one compact list for the tail kernel.
 template <int K>
-__global__ __launch_bounds__(ROUND_THREADS) void k_join(ClauseView cv, LoopBuffers b, uint32_t r) {
-    const DevState* st = b.state;
+__global__ __launch_bounds__(ROUND_THREADS) void k_join(ClauseView cv, LoopBuffers b, uint32_t r, int last) {
+    DevState* st = b.state;
     if (!st->active) return;
     const uint32_t tile = blockIdx.x;
     const uint32_t cnt = b.tile_cnt[tile];
@@ -284,7 +387,8 @@ __global__ __launch_bounds__(ROUND_THREADS) void k_join(ClauseView cv, LoopBuffe
     const uint32_t stamp = st->stamp;
     const unsigned long long keyhi = (unsigned long long)(~(st->round_base + r)) << 32;
     __shared__ uint32_t s_e[TILE];
-    __shared__ uint32_t s_wp, s_mp;
+    __shared__ uint32_t s_keep[TILE];
+    __shared__ uint32_t s_wp, s_mp, s_base;
     uint32_t* list = b.stage + (uint64_t)tile * TILE;
     uint32_t* mis = b.mis + (uint64_t)tile * TILE + b.mis_cnt[tile];
     for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) s_e[i] = list[i];
@@ -301,118 +405,106 @@ __global__ __launch_bounds__(ROUND_THREADS) void k_join(ClauseView cv, LoopBuffe
             for (uint64_t j = lb; j < le; ++j) b.cover[cv.lits[j] >> 1] = stamp;
             mis[atomicAdd(&s_mp, 1u)] = c;
         } else {
-            list[atomicAdd(&s_wp, 1u)] = c;
+            s_keep[atomicAdd(&s_wp, 1u)] = c;
         }
     }
     __syncthreads();
+    const uint32_t kept = s_wp;
+    uint32_t* dst = list;
+    if (last && kept) {
+        if (threadIdx.x == 0) s_base = atomicAdd(&st->left_cnt, kept);
+        __syncthreads();
+        dst = b.left + s_base;
+    }
+    for (uint32_t i = threadIdx.x; i < kept; i += blockDim.x) dst[i] = s_keep[i];
     if (threadIdx.x == 0) {
-        b.tile_cnt[tile] = s_wp;
+        b.tile_cnt[tile] = last ? 0u : kept;
         b.mis_cnt[tile] += s_mp;
     }
 }
 
-// Tail: one workgroup finishes the LFMIS (rounds until no undecided clause is left).  Each
-// wave owns the tiles t = wave (mod 16) in both phases; owner / cover / counts are accessed
-// with agent-scope relaxed atomics so no stale L1 line is read across the barriers.
+// Tail: one workgroup finishes the LFMIS over the compact list handed over by the last grid
+// round (rounds until no undecided clause is left).  Entries are processed in chunks of one
+// per thread; survivors are compacted in place (a write position never passes the chunk being
+// read).  owner / cover are accessed with agent-scope relaxed atomics so no stale L1 line is
+// read across the barriers.
 template <int K>
 __global__ __launch_bounds__(TAIL_THREADS) void k_tail(ClauseView cv, LoopBuffers b, uint32_t first_round) {
     DevState* st = b.state;
     if (!st->active) return;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
     const uint32_t stamp = st->stamp;
-    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-    __shared__ uint32_t s_left;
+    __shared__ uint32_t s_wp, s_tm;
+    uint32_t n = st->left_cnt;
     uint32_t epoch = st->round_base + first_round;
     uint32_t rounds = 0;
-    for (;;) {
-        if (threadIdx.x == 0) s_left = 0;
-        __syncthreads();
+    if (threadIdx.x == 0) s_tm = 0;
+    uint32_t* left = b.left;
+    while (n > 0) {
         const unsigned long long keyhi = (unsigned long long)(~epoch) << 32;
         // CLAIM (with the kill test)
-        for (uint32_t t = wave; t < b.n_tiles; t += nwaves) {
-            const uint32_t cnt = __hip_atomic_load(&b.tile_cnt[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (cnt == 0) continue;
-            uint32_t* list = b.stage + (uint64_t)t * TILE;
-            uint32_t wp = 0;
-            for (uint32_t i0 = 0; i0 < cnt; i0 += 64) {
-                const uint32_t i = i0 + lane;
-                bool keep = false;
-                uint32_t c = 0;
-                if (i < cnt) {
-                    c = list[i];
-                    uint64_t lb, le;
-                    clause_range<K>(cv, c, lb, le);
-                    bool killed = false;
-                    for (uint64_t j = lb; j < le; ++j)
-                        killed |= (__hip_atomic_load(&b.cover[cv.lits[j] >> 1], __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT) == stamp);
-                    if (!killed) {
-                        keep = true;
-                        const unsigned long long key = keyhi | c;
-                        for (uint64_t j = lb; j < le; ++j) atomicMin(&b.owner[cv.lits[j] >> 1], key);
-                    }
+        if (threadIdx.x == 0) s_wp = 0;
+        __syncthreads();
+        for (uint32_t base = 0; base < n; base += blockDim.x) {
+            const uint32_t i = base + threadIdx.x;
+            const uint32_t c = (i < n) ? left[i] : 0u;
+            __syncthreads();
+            if (i < n) {
+                uint64_t lb, le;
+                clause_range<K>(cv, c, lb, le);
+                bool killed = false;
+                for (uint64_t j = lb; j < le; ++j)
+                    killed |= (__hip_atomic_load(&b.cover[cv.lits[j] >> 1], __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT) == stamp);
+                if (!killed) {
+                    const unsigned long long key = keyhi | c;
+                    for (uint64_t j = lb; j < le; ++j) atomicMin(&b.owner[cv.lits[j] >> 1], key);
+                    left[atomicAdd(&s_wp, 1u)] = c;
                 }
-                const uint64_t km = __ballot(keep);
-                if (keep) list[wp + __popcll(km & lt)] = c;
-                wp += __popcll(km);
             }
-            if (lane == 0) __hip_atomic_store(&b.tile_cnt[t], wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+        __syncthreads();
+        n = s_wp;
         __syncthreads();
         // JOIN
-        for (uint32_t t = wave; t < b.n_tiles; t += nwaves) {
-            const uint32_t cnt = __hip_atomic_load(&b.tile_cnt[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (cnt == 0) continue;
-            uint32_t* list = b.stage + (uint64_t)t * TILE;
-            uint32_t mc = __hip_atomic_load(&b.mis_cnt[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            uint32_t* mis = b.mis + (uint64_t)t * TILE;
-            uint32_t wp = 0;
-            for (uint32_t i0 = 0; i0 < cnt; i0 += 64) {
-                const uint32_t i = i0 + lane;
-                bool keep = false, own = false;
-                uint32_t c = 0;
-                if (i < cnt) {
-                    c = list[i];
-                    uint64_t lb, le;
-                    clause_range<K>(cv, c, lb, le);
-                    const unsigned long long key = keyhi | c;
-                    own = true;
+        if (threadIdx.x == 0) s_wp = 0;
+        __syncthreads();
+        for (uint32_t base = 0; base < n; base += blockDim.x) {
+            const uint32_t i = base + threadIdx.x;
+            const uint32_t c = (i < n) ? left[i] : 0u;
+            __syncthreads();
+            if (i < n) {
+                uint64_t lb, le;
+                clause_range<K>(cv, c, lb, le);
+                const unsigned long long key = keyhi | c;
+                bool own = true;
+                for (uint64_t j = lb; j < le; ++j)
+                    own &= (__hip_atomic_load(&b.owner[cv.lits[j] >> 1], __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT) == key);
+                if (own) {
                     for (uint64_t j = lb; j < le; ++j)
-                        own &= (__hip_atomic_load(&b.owner[cv.lits[j] >> 1], __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT) == key);
-                    if (own) {
-                        for (uint64_t j = lb; j < le; ++j)
-                            __hip_atomic_store(&b.cover[cv.lits[j] >> 1], stamp, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-                    }
-                    keep = !own;
+                        __hip_atomic_store(&b.cover[cv.lits[j] >> 1], stamp, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                    b.tmis[atomicAdd(&s_tm, 1u)] = c;
+                } else {
+                    left[atomicAdd(&s_wp, 1u)] = c;
                 }
-                const uint64_t km = __ballot(keep), om = __ballot(own);
-                if (keep) list[wp + __popcll(km & lt)] = c;
-                if (own) mis[mc + __popcll(om & lt)] = c;
-                wp += __popcll(km);
-                mc += __popcll(om);
-            }
-            if (lane == 0) {
-                __hip_atomic_store(&b.tile_cnt[t], wp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(&b.mis_cnt[t], mc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (wp) atomicAdd(&s_left, wp);
             }
         }
         __syncthreads();
-        const uint32_t left = s_left;
+        n = s_wp;
         ++rounds;
         ++epoch;
-        if (left == 0) break;
-        if (rounds >= MAX_TAIL_ROUNDS) {
+        if (rounds >= MAX_TAIL_ROUNDS && n > 0) {
             if (threadIdx.x == 0) { st->error = 1; st->done = 3; }
             break;
         }
         __syncthreads();
     }
+    __syncthreads();
     if (threadIdx.x == 0) {
         st->round_next = epoch;
         st->tail_rounds = rounds;
+        st->tmis_cnt = s_tm;
         const uint32_t total = first_round + rounds;
         if (total > st->max_rounds) st->max_rounds = total;
     }
@@ -425,29 +517,11 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail(ClauseView cv, LoopBuffer
 // variable-disjoint).  A variable repeated inside one clause is applied once (its draws
 // are equal anyway); n_resamples still counts every literal (SATInstance.h:363).
 template <int K>
-__global__ __launch_bounds__(ROUND_THREADS) void k_resample(ClauseView cv, LoopBuffers b,
-                                                            uint32_t own_begin, uint32_t own_end,
-                                                            int to_delta) {
-    const DevState* st = b.state;
-    if (!st->active) return;
-    const uint32_t tile = blockIdx.x;
-    const uint32_t cnt = b.mis_cnt[tile];
-    if (cnt == 0) return;
-    const uint64_t it = st->n_iter - 1;
-    const uint32_t k0 = (uint32_t)b.seed, k1 = (uint32_t)(b.seed >> 32);
-    const bool apply = !to_delta || (tile >= own_begin && tile < own_end);
-    uint32_t* target = to_delta ? b.delta : b.A;
-    __shared__ unsigned long long s_res;
-    if (threadIdx.x == 0) s_res = 0;
-    __syncthreads();
-    const uint32_t* mis = b.mis + (uint64_t)tile * TILE;
-    unsigned long long res = 0;
-    for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
-        const uint32_t c = mis[i];
-        uint64_t lb, le;
-        clause_range<K>(cv, c, lb, le);
-        res += le - lb;
-        if (!apply) continue;
+__device__ __forceinline__ uint64_t resample_clause(const ClauseView& cv, uint32_t* target, uint32_t c,
+                                                    uint64_t it, uint32_t k0, uint32_t k1, bool apply) {
+    uint64_t lb, le;
+    clause_range<K>(cv, c, lb, le);
+    if (apply) {
         for (uint64_t j = lb; j < le; ++j) {
             const uint32_t l = cv.lits[j], v = l >> 1;
             bool dup = false;
@@ -457,12 +531,48 @@ __global__ __launch_bounds__(ROUND_THREADS) void k_resample(ClauseView cv, LoopB
             if (nb != (l & 1u)) atomicXor(&target[v >> 5], 1u << (v & 31u));
         }
     }
+    return le - lb;
+}
+
+template <int K>
+__global__ __launch_bounds__(ROUND_THREADS) void k_resample(ClauseView cv, LoopBuffers b,
+                                                            uint32_t own_begin, uint32_t own_end,
+                                                            int to_delta) {
+    const DevState* st = b.state;
+    if (!st->active) return;
+    const uint32_t tile = blockIdx.x;
+    const uint64_t it = st->n_iter - 1;
+    const uint32_t k0 = (uint32_t)b.seed, k1 = (uint32_t)(b.seed >> 32);
+    uint32_t* target = to_delta ? b.delta : b.A;
+    if (tile == b.n_tiles) {
+        // MIS clauses decided by the tail kernel (few): per-clause statistics to their tile
+        const uint32_t cnt = st->tmis_cnt;
+        for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
+            const uint32_t c = b.tmis[i];
+            const uint32_t t = c / TILE;
+            const bool apply = !to_delta || (t >= own_begin && t < own_end);
+            const uint64_t len = resample_clause<K>(cv, target, c, it, k0, k1, apply);
+            atomicAdd(&b.tile_stats[2 * t], 1ull);
+            atomicAdd(&b.tile_stats[2 * t + 1], (unsigned long long)len);
+        }
+        return;
+    }
+    const uint32_t cnt = b.mis_cnt[tile];
+    if (cnt == 0) return;
+    const bool apply = !to_delta || (tile >= own_begin && tile < own_end);
+    __shared__ unsigned long long s_res;
+    if (threadIdx.x == 0) s_res = 0;
+    __syncthreads();
+    const uint32_t* mis = b.mis + (uint64_t)tile * TILE;
+    unsigned long long res = 0;
+    for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x)
+        res += resample_clause<K>(cv, target, mis[i], it, k0, k1, apply);
     for (int o = 32; o > 0; o >>= 1) res += __shfl_down(res, o, 64);
     if ((threadIdx.x & 63) == 0) atomicAdd(&s_res, res);
     __syncthreads();
     if (threadIdx.x == 0) {
-        b.tile_stats[2 * tile] += cnt;
-        b.tile_stats[2 * tile + 1] += s_res;
+        atomicAdd(&b.tile_stats[2 * tile], (unsigned long long)cnt);
+        atomicAdd(&b.tile_stats[2 * tile + 1], s_res);
     }
 }
 
@@ -501,6 +611,35 @@ hipError_t launch_eval(const ClauseView& cv, const LoopBuffers& b, uint32_t tile
     return hipGetLastError();
 }
 
+hipError_t launch_eval_ranged(const ClauseView& cv, const LoopBuffers& b, uint32_t tile_begin,
+                              uint32_t tile_end, bool gated, int n_cu, hipStream_t s) {
+    if (tile_end <= tile_begin) return hipSuccess;
+    const uint32_t nt = tile_end - tile_begin;
+    const dim3 grid(std::min<uint32_t>(nt, (uint32_t)n_cu));
+    const size_t lds = RANGE_WORDS * sizeof(uint32_t);
+    const int g = gated ? 1 : 0;
+    static bool attr_set[MAX_FIXED_K + 1] = {};
+    if (cv.k >= 1 && cv.k <= (uint32_t)MAX_FIXED_K && !attr_set[cv.k]) {
+        hipError_t e = hipSuccess;
+        ALLL_DISPATCH_K(cv.k, (e = hipFuncSetAttribute((const void*)k_eval_ranged<(K > 0 ? K : 1)>,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)));
+        if (e != hipSuccess) return e;
+        attr_set[cv.k] = true;
+    }
+    switch (cv.k) {
+        case 1: k_eval_ranged<1><<<grid, RANGED_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g); break;
+        case 2: k_eval_ranged<2><<<grid, RANGED_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g); break;
+        case 3: k_eval_ranged<3><<<grid, RANGED_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g); break;
+        case 4: k_eval_ranged<4><<<grid, RANGED_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g); break;
+        case 5: k_eval_ranged<5><<<grid, RANGED_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g); break;
+        case 6: k_eval_ranged<6><<<grid, RANGED_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g); break;
+        case 7: k_eval_ranged<7><<<grid, RANGED_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g); break;
+        case 8: k_eval_ranged<8><<<grid, RANGED_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_collect(const ClauseView& cv, const LoopBuffers& b, uint32_t own_begin,
                           uint32_t own_end, hipStream_t s) {
     if (b.n_tiles == 0) return hipSuccess;
@@ -513,25 +652,15 @@ hipError_t launch_reduce(const LoopBuffers& b, int mode, hipStream_t s) {
     return hipGetLastError();
 }
 
-#define ALLL_DISPATCH_K(KV, CALL)                      \
-    switch (KV) {                                      \
-        case 1: { constexpr int K = 1; CALL; } break;  \
-        case 2: { constexpr int K = 2; CALL; } break;  \
-        case 3: { constexpr int K = 3; CALL; } break;  \
-        case 4: { constexpr int K = 4; CALL; } break;  \
-        case 5: { constexpr int K = 5; CALL; } break;  \
-        case 6: { constexpr int K = 6; CALL; } break;  \
-        case 7: { constexpr int K = 7; CALL; } break;  \
-        case 8: { constexpr int K = 8; CALL; } break;  \
-        default: { constexpr int K = 0; CALL; } break; \
-    }
 
-hipError_t launch_round(const ClauseView& cv, const LoopBuffers& b, uint32_t r, hipStream_t s) {
+hipError_t launch_round(const ClauseView& cv, const LoopBuffers& b, uint32_t r, bool last,
+                        hipStream_t s) {
     if (b.n_tiles == 0) return hipSuccess;
     ALLL_DISPATCH_K(cv.k, (k_claim<K><<<b.n_tiles, ROUND_THREADS, 0, s>>>(cv, b, r)));
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    ALLL_DISPATCH_K(cv.k, (k_join<K><<<b.n_tiles, ROUND_THREADS, 0, s>>>(cv, b, r)));
+    const int l = last ? 1 : 0;
+    ALLL_DISPATCH_K(cv.k, (k_join<K><<<b.n_tiles, ROUND_THREADS, 0, s>>>(cv, b, r, l)));
     return hipGetLastError();
 }
 
@@ -544,7 +673,7 @@ hipError_t launch_resample(const ClauseView& cv, const LoopBuffers& b, uint32_t 
                            uint32_t own_end, bool to_delta, hipStream_t s) {
     if (b.n_tiles == 0) return hipSuccess;
     const int td = to_delta ? 1 : 0;
-    ALLL_DISPATCH_K(cv.k, (k_resample<K><<<b.n_tiles, ROUND_THREADS, 0, s>>>(cv, b, own_begin, own_end, td)));
+    ALLL_DISPATCH_K(cv.k, (k_resample<K><<<b.n_tiles + 1, ROUND_THREADS, 0, s>>>(cv, b, own_begin, own_end, td)));
     return hipGetLastError();
 }
 

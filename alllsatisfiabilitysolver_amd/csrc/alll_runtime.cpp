@@ -76,6 +76,8 @@ struct alll_ctx {
     hipGraphExec_t graph_exec = nullptr;
     bool use_graph = true;
     hipEvent_t ev[8] = {};
+    int n_cu = 256;
+    std::string eval_name;
 };
 
 namespace {
@@ -112,12 +114,17 @@ int write_limits(alll_ctx* c, uint64_t limit_eval, uint64_t limit_nores) {
     return ALLL_OK;
 }
 
+hipError_t eval_launch(alll_ctx* c, uint32_t tb, uint32_t te, bool gated) {
+    if (c->cv.n_ranges) return launch_eval_ranged(c->cv, c->b, tb, te, gated, c->n_cu, c->stream);
+    return launch_eval(c->cv, c->b, tb, te, gated, c->stream);
+}
+
 // The launch sequence of one iteration (SATInstance.h:260-311).  Every kernel is gated on
 // the device state, so replaying it after convergence is a no-op.
 int enqueue_iteration(alll_ctx* c, hipEvent_t* marks) {
     hipStream_t s = c->stream;
     if (marks) HIP_TRY(hipEventRecord(marks[0], s));
-    HIP_TRY(launch_eval(c->cv, c->b, c->own_begin, c->own_end, true, s));
+    HIP_TRY(eval_launch(c, c->own_begin, c->own_end, true));
     if (marks) HIP_TRY(hipEventRecord(marks[1], s));
     if (c->world > 1) {
         const size_t words = (size_t)c->tiles_per_rank * TILE_WORDS;
@@ -127,7 +134,8 @@ int enqueue_iteration(alll_ctx* c, hipEvent_t* marks) {
     }
     if (marks) HIP_TRY(hipEventRecord(marks[2], s));
     HIP_TRY(launch_reduce(c->b, 0, s));
-    for (uint32_t r = 0; r < c->grid_rounds; ++r) HIP_TRY(launch_round(c->cv, c->b, r, s));
+    for (uint32_t r = 0; r < c->grid_rounds; ++r)
+        HIP_TRY(launch_round(c->cv, c->b, r, r + 1 == c->grid_rounds, s));
     HIP_TRY(launch_tail(c->cv, c->b, c->grid_rounds, s));
     if (marks) HIP_TRY(hipEventRecord(marks[3], s));
     if (c->allreduce && c->world > 1) {
@@ -324,6 +332,8 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     if ((rc = dalloc(c, &b.mis_cnt, n_tiles))) return bail(rc);
     if ((rc = dalloc(c, &b.stage, (size_t)n_tiles * TILE))) return bail(rc);
     if ((rc = dalloc(c, &b.mis, (size_t)n_tiles * TILE))) return bail(rc);
+    if ((rc = dalloc(c, &b.left, (size_t)n_tiles * TILE))) return bail(rc);
+    if ((rc = dalloc(c, &b.tmis, (size_t)n_tiles * TILE))) return bail(rc);
     if ((rc = dalloc(c, &b.owner, c->n_vars, 0xFF))) return bail(rc);
     if ((rc = dalloc(c, &b.cover, c->n_vars))) return bail(rc);
     if ((rc = dalloc(c, &b.tile_stats, 2 * (size_t)n_tiles))) return bail(rc);
@@ -358,6 +368,47 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
             return bail(fail(ALLL_ERR_HIP, "transposed literal upload failed"));
         cv.lits_t = d_t;
         cv.offs = nullptr;
+        // variable-range-partitioned copy for the LDS evaluation kernel
+        const uint32_t P = (b.n_words + RANGE_WORDS - 1) / RANGE_WORDS;
+        if (!(opt.flags & ALLL_FLAG_NO_RANGED) && P >= 1 && P <= (uint32_t)MAX_RANGES && m > 0) {
+            const uint64_t groups = (uint64_t)n_tiles * TILE_WORDS;
+            std::vector<uint32_t> rl;
+            rl.reserve(L);
+            std::vector<uint32_t> rcv(groups * 8), rbv(groups);
+            uint64_t roff[MAX_RANGES];
+            for (uint32_t r = 0; r < P; ++r) {
+                roff[r] = rl.size();
+                std::fill(rcv.begin(), rcv.end(), 0u);
+                const uint32_t vlo = r * RANGE_VARS, vhi = vlo + RANGE_VARS;
+                for (uint64_t g = 0; g < groups; ++g) {
+                    rbv[g] = (uint32_t)(rl.size() - roff[r]);
+                    const uint64_t ce = std::min<uint64_t>(m, (g + 1) * 64);
+                    for (uint64_t cl = g * 64; cl < ce; ++cl) {
+                        uint32_t cnt = 0;
+                        for (int j = 0; j < fixed_k; ++j) {
+                            const uint32_t l = prob->literals[cl * fixed_k + j], v = l >> 1;
+                            if (v >= vlo && v < vhi) { rl.push_back(l); ++cnt; }
+                        }
+                        rcv[cl >> 3] |= cnt << ((cl & 7) * 4);
+                    }
+                }
+                uint32_t *d_rc = nullptr, *d_rb = nullptr;
+                if ((rc = dalloc(c, &d_rc, rcv.size())) || (rc = dalloc(c, &d_rb, rbv.size()))) return bail(rc);
+                cv.rcnt[r] = d_rc;
+                cv.rbase[r] = d_rb;
+                if (hipStreamSynchronize(c->stream) != hipSuccess ||
+                    hipMemcpy(d_rc, rcv.data(), rcv.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+                    hipMemcpy(d_rb, rbv.data(), rbv.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+                    return bail(fail(ALLL_ERR_HIP, "range layout upload failed"));
+            }
+            uint32_t* d_rl = nullptr;
+            if ((rc = dalloc(c, &d_rl, rl.size()))) return bail(rc);
+            if (hipStreamSynchronize(c->stream) != hipSuccess ||
+                (!rl.empty() && hipMemcpy(d_rl, rl.data(), rl.size() * 4, hipMemcpyHostToDevice) != hipSuccess))
+                return bail(fail(ALLL_ERR_HIP, "range literal upload failed"));
+            for (uint32_t r = 0; r < P; ++r) cv.rlits[r] = d_rl + roff[r];
+            cv.n_ranges = P;
+        }
     } else {
         std::vector<uint32_t> o32(m + 1);
         for (uint64_t i = 0; i <= m; ++i) o32[i] = m ? (uint32_t)prob->offsets[i] : 0u;
@@ -385,6 +436,16 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     }
     if (hipStreamSynchronize(c->stream) != hipSuccess)
         return bail(fail(ALLL_ERR_HIP, "create: stream sync failed: %s", hipGetErrorString(hipGetLastError())));
+    {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0)
+            c->n_cu = prop.multiProcessorCount;
+    }
+    char nm[64];
+    if (cv.n_ranges) snprintf(nm, sizeof nm, "k_eval_ranged<%u>", cv.k);
+    else if (cv.k) snprintf(nm, sizeof nm, "k_eval_fixed<%u>", cv.k);
+    else snprintf(nm, sizeof nm, "k_eval_csr");
+    c->eval_name = nm;
     *out = c;
     return ALLL_OK;
 }
@@ -458,7 +519,7 @@ int alll_verify(alll_ctx* c, int* valid, uint64_t* n_violated) {
     if (!c) return fail(ALLL_ERR_INVALID_ARG, "null context");
     HIP_TRY(hipSetDevice(c->device));
     // every rank holds the full clause set and the full assignment: evaluate all tiles
-    HIP_TRY(launch_eval(c->cv, c->b, 0, c->b.n_tiles, false, c->stream));
+    HIP_TRY(eval_launch(c, 0, c->b.n_tiles, false));
     HIP_TRY(launch_reduce(c->b, 1, c->stream));
     int rc = read_state(c);
     if (rc) return rc;
@@ -520,7 +581,8 @@ int alll_get_violated_mask(alll_ctx* c, uint64_t* out, uint64_t n_words) {
 int alll_get_mis(alll_ctx* c, uint32_t* out, uint64_t cap, uint64_t* n_out) {
     if (!c || !n_out) return fail(ALLL_ERR_INVALID_ARG, "null argument");
     HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipStreamSynchronize(c->stream));
+    int rc = read_state(c);
+    if (rc) return rc;
     const uint32_t nt = c->b.n_tiles;
     std::vector<uint32_t> cnt(nt);
     if (nt) HIP_TRY(hipMemcpy(cnt.data(), c->b.mis_cnt, nt * 4ull, hipMemcpyDeviceToHost));
@@ -530,6 +592,11 @@ int alll_get_mis(alll_ctx* c, uint32_t* out, uint64_t cap, uint64_t* n_out) {
         if (!cnt[t]) continue;
         buf.resize(cnt[t]);
         HIP_TRY(hipMemcpy(buf.data(), c->b.mis + (size_t)t * TILE, cnt[t] * 4ull, hipMemcpyDeviceToHost));
+        all.insert(all.end(), buf.begin(), buf.end());
+    }
+    if (c->h_state->tmis_cnt) {
+        buf.resize(c->h_state->tmis_cnt);
+        HIP_TRY(hipMemcpy(buf.data(), c->b.tmis, buf.size() * 4ull, hipMemcpyDeviceToHost));
         all.insert(all.end(), buf.begin(), buf.end());
     }
     std::sort(all.begin(), all.end());
@@ -544,10 +611,9 @@ int alll_get_mis(alll_ctx* c, uint32_t* out, uint64_t cap, uint64_t* n_out) {
 int alll_bench_eval(alll_ctx* c, int reps, double* avg_ms, uint64_t* n_violated) {
     if (!c || reps < 1) return fail(ALLL_ERR_INVALID_ARG, "bad argument");
     HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(launch_eval(c->cv, c->b, c->own_begin, c->own_end, false, c->stream));  // warm
+    HIP_TRY(eval_launch(c, c->own_begin, c->own_end, false));  // warm
     HIP_TRY(hipEventRecord(c->ev[0], c->stream));
-    for (int i = 0; i < reps; ++i)
-        HIP_TRY(launch_eval(c->cv, c->b, c->own_begin, c->own_end, false, c->stream));
+    for (int i = 0; i < reps; ++i) HIP_TRY(eval_launch(c, c->own_begin, c->own_end, false));
     HIP_TRY(hipEventRecord(c->ev[1], c->stream));
     HIP_TRY(hipEventSynchronize(c->ev[1]));
     float ms = 0;
@@ -588,6 +654,20 @@ int alll_profile(alll_ctx* c, uint64_t n_iters, alll_phase_times* out) {
     return ALLL_OK;
 }
 
+int alll_shard_plan(uint64_t n_clauses, int world, int rank, uint64_t* clause_begin,
+                    uint64_t* clause_end, uint64_t* mask_words_per_rank) {
+    if (world < 1 || rank < 0 || rank >= world) return fail(ALLL_ERR_INVALID_ARG, "bad rank/world");
+    const uint64_t n_tiles = (n_clauses + TILE - 1) / TILE;
+    uint64_t tpr = (n_tiles + world - 1) / world;
+    if (tpr == 0) tpr = 1;
+    const uint64_t tb = std::min<uint64_t>(n_tiles, (uint64_t)rank * tpr);
+    const uint64_t te = std::min<uint64_t>(n_tiles, tb + tpr);
+    if (clause_begin) *clause_begin = std::min<uint64_t>(n_clauses, tb * TILE);
+    if (clause_end) *clause_end = std::min<uint64_t>(n_clauses, te * TILE);
+    if (mask_words_per_rank) *mask_words_per_rank = tpr * TILE_WORDS;
+    return ALLL_OK;
+}
+
 uint64_t alll_eval_bytes(alll_ctx* c) {
     // B_eval = 4 L + 4 (m+1) [CSR offsets only] + ceil(n/8) + ceil(m/8),
     // for this rank's clause shard.
@@ -600,5 +680,7 @@ uint64_t alll_eval_bytes(alll_ctx* c) {
 }
 
 int alll_layout(alll_ctx* c) { return c ? (int)c->cv.k : -1; }
+
+const char* alll_eval_kernel(alll_ctx* c) { return c ? c->eval_name.c_str() : ""; }
 
 }  // extern "C"

@@ -191,9 +191,20 @@ class Solver:
     def layout(self) -> int:
         return int(self._L.alll_layout(self._ctx))
 
+    def eval_kernel(self) -> str:
+        return self._L.alll_eval_kernel(self._ctx).decode()
+
 
 def device_count() -> int:
     return int(N.lib().alll_device_count())
+
+
+def shard_plan(n_clauses: int, world: int, rank: int):
+    """(clause_begin, clause_end, mask_words_per_rank) of `rank` in the clause-sharded mode."""
+    b, e, w = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+    N.check(N.lib().alll_shard_plan(n_clauses, world, rank, ctypes.byref(b), ctypes.byref(e),
+                                    ctypes.byref(w)), "shard_plan")
+    return int(b.value), int(e.value), int(w.value)
 
 
 def comm_unique_id() -> bytes:

@@ -106,6 +106,7 @@ def main():
     ap.add_argument("--config", default="M", choices=list(CONFIGS))
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--exchange", default="allgather", choices=["allgather", "allreduce"])
+    ap.add_argument("--no-ranged", action="store_true", help="use the L2-gather eval kernel")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--profile-iters", type=int, default=10)
@@ -139,12 +140,15 @@ def main():
     offs, lits = generate_ksat(1, n, m, k, kind)
     t_gen = time.perf_counter() - t0
     flags = N.FLAG_EXCHANGE_ALLREDUCE if args.exchange == "allreduce" else 0
+    if args.no_ranged:
+        flags |= N.FLAG_NO_RANGED
     t0 = time.perf_counter()
     s = Solver(n, offs, lits, seed=args.seed, device=local_rank, rank=rank, world=world,
                comm_id=comm_id, flags=flags)
     del offs, lits
     t_create = time.perf_counter() - t0
-    log(f"[rank {rank}] generated {m} clauses in {t_gen:.2f}s, uploaded in {t_create:.2f}s, layout k={s.layout()}")
+    log(f"[rank {rank}] generated {m} clauses in {t_gen:.2f}s, uploaded in {t_create:.2f}s, "
+        f"layout k={s.layout()}, eval kernel {s.eval_kernel()}")
 
     def barrier():
         if dist is not None:
@@ -216,7 +220,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": f"k_eval_fixed<{k}>" if s.layout() else "k_eval_csr",
+                "kernel": s.eval_kernel(),
                 "algorithmic_bytes_per_launch": eval_bytes,
                 "eval_ms_in_loop": eval_ms,
                 "eval_ms_back_to_back": ev_ms,

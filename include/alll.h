@@ -52,6 +52,7 @@ typedef struct alll_problem {
 #define ALLL_FLAG_EXCHANGE_ALLREDUCE (1u << 1) /* multi-GPU: shard resample + allreduce of the
                                                  bit-packed assignment delta (north_star form) */
 #define ALLL_FLAG_GENERIC_CSR       (1u << 2) /* disable the fixed-width clause layout */
+#define ALLL_FLAG_NO_RANGED         (1u << 3) /* disable the LDS variable-range evaluation kernel */
 
 typedef struct alll_options {
     uint64_t seed;          /* Philox4x32-10 key; replaces std::random_device (SATInstance.h:346) */
@@ -145,8 +146,10 @@ int alll_profile(alll_ctx* ctx, uint64_t n_iters, alll_phase_times* out);
 int alll_synchronize(alll_ctx* ctx);
 /* Bytes the evaluation kernel reads/writes per pass (algorithmic). */
 uint64_t alll_eval_bytes(alll_ctx* ctx);
-/* Layout in use: 0 generic CSR, k>0 fixed-width-k transposed layout. */
+/* Layout in use: 0 generic CSR, k>0 fixed-width-k layout. */
 int alll_layout(alll_ctx* ctx);
+/* Name of the evaluation kernel the loop launches (e.g. "k_eval_ranged<3>"). */
+const char* alll_eval_kernel(alll_ctx* ctx);
 
 /* ---- host-side helpers (no GPU needed) ---------------------------------------------- */
 
@@ -158,6 +161,13 @@ int alll_dimacs_parse(const char* buf, uint64_t len, uint32_t* n_vars, uint64_t*
 /* Same from a file path (mmap). */
 int alll_dimacs_read(const char* path, uint32_t* n_vars, uint64_t* n_clauses, uint64_t* offsets,
                      uint32_t* literals, uint64_t* n_literals);
+
+/* Clause sharding of the multi-GPU mode (host-only): rank `rank` of `world` owns the clause
+ * range [*clause_begin, *clause_end) (contiguous, 4096-clause tile aligned, so rank-major
+ * concatenation is clause order) and contributes *mask_words_per_rank 64-bit words to the
+ * per-iteration all-gather of the violated bitmask. */
+int alll_shard_plan(uint64_t n_clauses, int world, int rank, uint64_t* clause_begin,
+                    uint64_t* clause_end, uint64_t* mask_words_per_rank);
 
 /* The solver's initial assignment for `seed` as n_vars bytes of 0/1 (word w of the packed
  * form = Philox4x32-10(key=seed, ctr={w, 0, 0xFFFFFFFF, 0}).x); used by the compatibility

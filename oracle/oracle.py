@@ -134,6 +134,45 @@ def to_dimacs(n_vars, offs, lits, comments=()):
     return "\n".join(out) + "\n"
 
 
+def philox_bits(seed, it, vs):
+    """Vectorised Philox4x32-10 (x & 1) for ctr={v, it_lo, 0, it_hi}, key=seed; equals
+    resample_bit() elementwise (checked in tests/test_oracle.py)."""
+    M0, M1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)
+    mask = np.uint64(0xFFFFFFFF)
+    c0 = np.asarray(vs).astype(np.uint64)
+    c1 = np.full_like(c0, it & 0xFFFFFFFF)
+    c2 = np.zeros_like(c0)
+    c3 = np.full_like(c0, it >> 32)
+    k0, k1 = np.uint64(seed & 0xFFFFFFFF), np.uint64(seed >> 32)
+    for _ in range(10):
+        p0 = M0 * c0
+        p1 = M1 * c2
+        c0, c1, c2, c3 = ((p1 >> np.uint64(32)) ^ c1 ^ k0) & mask, p1 & mask, \
+            ((p0 >> np.uint64(32)) ^ c3 ^ k1) & mask, p0 & mask
+        k0 = (k0 + np.uint64(0x9E3779B9)) & mask
+        k1 = (k1 + np.uint64(0xBB67AE85)) & mask
+    return (c0 & np.uint64(1)).astype(np.uint32)
+
+
+def resample_words(A, seed, it, vs):
+    """Set bit v of A (uint32 words) to Philox(seed, it, v) for every v in vs (in place)."""
+    vs = np.unique(np.asarray(vs, np.uint32))
+    bits = philox_bits(seed, it, vs)
+    w = (vs >> 5).astype(np.int64)
+    sh = (vs & 31).astype(np.uint32)
+    np.bitwise_and.at(A, w, ~(np.uint32(1) << sh))
+    np.bitwise_or.at(A, w, bits << sh)
+    return A
+
+
+def clause_vars(offs, lits, C):
+    C = np.asarray(C, np.int64)
+    if C.size == 0:
+        return np.zeros(0, np.uint32)
+    idx = np.concatenate([np.arange(offs[c], offs[c + 1], dtype=np.int64) for c in C])
+    return (lits[idx] >> 1).astype(np.uint32)
+
+
 # ------------------------------------------------------------------------- path
 def pack_bools(b):
     b = np.asarray(b, np.uint8)

@@ -21,7 +21,7 @@ from conftest import GOLDEN
 pytestmark = pytest.mark.gpu
 
 T1_FIXTURES = sorted(p for p in glob.glob(os.path.join(GOLDEN, "*_T1.npz")))
-LAYOUTS = {"fixed": 0, "csr": 1 << 2}
+LAYOUTS = {"ranged": 0, "fixed": 1 << 3, "csr": 1 << 2}
 
 
 @pytest.fixture(scope="module")
@@ -190,49 +190,8 @@ def _oracle_step(o, n, offs, lits, A, seed, it):
     nu, vm = o.eval_mask(offs, lits, A)
     U = o.mask_to_list(m, vm)
     M = o.lfmis(n, offs, lits, U)
-    A2 = A.copy()
-    k = int(offs[1] - offs[0]) if m else 0
-    fixed = m and np.all(np.diff(offs) == k)
-    if fixed:
-        vs = np.unique((lits.reshape(-1, k)[M.astype(np.int64)] >> 1).ravel())
-    else:
-        vs = np.unique(np.concatenate([lits[offs[c]:offs[c + 1]] for c in M]) >> 1)
-    bits = np.array([o.resample_bit(seed, it, int(v)) for v in vs], np.uint32) if vs.size < 50000 else None
-    if bits is None:  # vectorised Philox for big MIS sets
-        bits = philox_bits(seed, it, vs)
-    w = vs >> 5
-    sh = (vs & 31).astype(np.uint32)
-    np.bitwise_and.at(A2, w, ~(np.uint32(1) << sh))
-    np.bitwise_or.at(A2, w, bits.astype(np.uint32) << sh)
+    A2 = o.resample_words(A.copy(), seed, it, o.clause_vars(offs, lits, M))
     return nu, vm, M, A2
-
-
-def philox_bits(seed, it, vs):
-    """numpy Philox4x32-10 (x word & 1) for ctr={v, it_lo, 0, it_hi}; pinned to the C oracle
-    in test_numpy_philox_matches_oracle."""
-    M0, M1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)
-    c0 = vs.astype(np.uint64)
-    c1 = np.full_like(c0, it & 0xFFFFFFFF)
-    c2 = np.zeros_like(c0)
-    c3 = np.full_like(c0, it >> 32)
-    k0, k1 = np.uint64(seed & 0xFFFFFFFF), np.uint64(seed >> 32)
-    mask = np.uint64(0xFFFFFFFF)
-    for _ in range(10):
-        p0 = M0 * c0
-        p1 = M1 * c2
-        hi0, lo0 = p0 >> np.uint64(32), p0 & mask
-        hi1, lo1 = p1 >> np.uint64(32), p1 & mask
-        c0, c1, c2, c3 = (hi1 ^ c1 ^ k0) & mask, lo1, (hi0 ^ c3 ^ k1) & mask, lo0
-        k0 = (k0 + np.uint64(0x9E3779B9)) & mask
-        k1 = (k1 + np.uint64(0xBB67AE85)) & mask
-    return (c0 & np.uint64(1)).astype(np.uint32)
-
-
-def test_numpy_philox_matches_oracle(oracle_mod):
-    vs = np.arange(0, 3000, 7, dtype=np.uint32)
-    for seed, it in [(1, 0), (12345, 77), ((7 << 32) | 9, (3 << 32) | 5)]:
-        ref = np.array([oracle_mod.resample_bit(seed, it, int(v)) for v in vs], np.uint32)
-        np.testing.assert_array_equal(philox_bits(seed, it, vs), ref)
 
 
 BIG = {

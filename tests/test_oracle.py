@@ -154,3 +154,11 @@ def test_oracle_generator_distinct(oracle_mod):
         v = (lits >> 1).reshape(-1, 8)
         assert all(len(set(r)) == 8 for r in v.tolist())
         assert v.max() < 50
+
+
+def test_numpy_philox_matches_c_oracle(oracle_mod):
+    o = oracle_mod
+    vs = np.arange(0, 3000, 7, dtype=np.uint32)
+    for seed, it in [(1, 0), (12345, 77), ((7 << 32) | 9, (3 << 32) | 5)]:
+        ref = np.array([o.resample_bit(seed, it, int(v)) for v in vs], np.uint32)
+        np.testing.assert_array_equal(o.philox_bits(seed, it, vs), ref)

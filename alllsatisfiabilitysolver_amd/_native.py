@@ -82,6 +82,8 @@ class Stats(ctypes.Structure):
         ("n_violated", ctypes.c_uint64),
         ("solved", ctypes.c_int32),
         ("n_gpus", ctypes.c_int32),
+        ("lfmis_rounds_max", ctypes.c_uint32),
+        ("lfmis_tail_rounds", ctypes.c_uint32),
         ("gpu_resamples", ctypes.c_uint64 * MAX_GPU_STATS),
     ]
 

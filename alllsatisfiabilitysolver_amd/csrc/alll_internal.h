@@ -15,11 +15,14 @@ constexpr int EVAL_THREADS = 256;
 constexpr int ROUND_THREADS = 256;
 constexpr int TAIL_THREADS = 1024;
 constexpr int MAX_FIXED_K = 8;
-// Range-partitioned evaluation: the assignment words of one variable range live in LDS.
-constexpr uint32_t RANGE_WORDS = 38912;            // 152 KiB of LDS per range
-constexpr uint32_t RANGE_VARS = RANGE_WORDS * 32;  // 1,245,184 variables
-constexpr int MAX_RANGES = 4;
-constexpr int RANGED_THREADS = 1024;
+// Persistent hybrid evaluation: assignment words of the first LDS_VARS variables in LDS.
+constexpr uint32_t LDS_WORDS = 38912;              // 152 KiB of LDS
+constexpr uint32_t LDS_VARS = LDS_WORDS * 32;      // 1,245,184 variables
+constexpr int HYB_THREADS = 1024;
+constexpr uint32_t HYB_MAX_TILES = 256;            // per-tile LDS counters per pass
+// Hot variables (skewed degree): at most HOT_MAX are flagged; LDS hash slots per claim block.
+constexpr uint32_t HOT_MAX = 512;
+constexpr uint32_t HOT_SLOTS = 1024;
 constexpr uint32_t RANGED_MAX_TILES = 16;          // tiles per block pass (64-bit sat mask/lane)
 // Every LFMIS round decides at least the lowest undecided clause, so rounds <= |U|; the cap
 // only bounds a kernel that would otherwise run away on a bug or an adversarial chain.
@@ -52,11 +55,7 @@ struct ClauseView {
     const uint32_t* lits_t; // fixed-k only: chunk-transposed [c/256][j][c%256]
     uint64_t m;             // clauses
     uint32_t k;             // fixed width, 0 = generic CSR
-    // variable-range-partitioned layout (fixed k, n <= RANGE_VARS * MAX_RANGES):
-    uint32_t n_ranges;      // 0 = not built
-    const uint32_t* rlits[MAX_RANGES];  // literals whose variable is in range r, clause order
-    const uint32_t* rcnt[MAX_RANGES];   // 4-bit count per clause (8 clauses per word)
-    const uint32_t* rbase[MAX_RANGES];  // per 64-clause group: offset of its first literal
+    uint32_t n_hot;         // variables flagged hot (bit 31 of their literals in `lits`)
 };
 
 struct LoopBuffers {
@@ -84,8 +83,8 @@ hipError_t launch_init_assignment(const LoopBuffers& b, hipStream_t s);
 hipError_t launch_init_state(const LoopBuffers& b, hipStream_t s);
 hipError_t launch_eval(const ClauseView& cv, const LoopBuffers& b, uint32_t tile_begin,
                        uint32_t tile_end, bool gated, hipStream_t s);
-hipError_t launch_eval_ranged(const ClauseView& cv, const LoopBuffers& b, uint32_t tile_begin,
-                              uint32_t tile_end, bool gated, int n_cu, hipStream_t s);
+hipError_t launch_eval_hybrid(const ClauseView& cv, const LoopBuffers& b, uint32_t tile_begin,
+                              uint32_t tile_end, bool gated, int n_blocks, hipStream_t s);
 hipError_t launch_collect(const ClauseView& cv, const LoopBuffers& b, uint32_t own_begin,
                           uint32_t own_end, hipStream_t s);
 hipError_t launch_reduce(const LoopBuffers& b, int mode, hipStream_t s);

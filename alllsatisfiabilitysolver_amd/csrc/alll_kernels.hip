@@ -50,6 +50,14 @@ __device__ __forceinline__ uint32_t philox_x(uint32_t c0, uint32_t c1, uint32_t 
     return c0;
 }
 
+// The AoS literal copy used by the LFMIS / resample kernels carries a "hot variable" flag in
+// bit 31 (set by the host for the highest-degree variables of skewed instances).
+constexpr uint32_t LIT_MASK = 0x7FFFFFFFu;
+constexpr uint32_t LIT_HOT = 0x80000000u;
+__device__ __forceinline__ uint32_t lvar(const ClauseView& cv, uint64_t j) {
+    return (cv.lits[j] & LIT_MASK) >> 1;
+}
+
 __device__ __forceinline__ uint32_t abit(const uint32_t* __restrict__ A, uint32_t v) {
     return (A[v >> 5] >> (v & 31u)) & 1u;
 }
@@ -161,81 +169,95 @@ __global__ __launch_bounds__(EVAL_THREADS) void k_eval_fixed(ClauseView cv, Loop
     publish_tile(b, tile, s_idx, s_wcnt, wcount, lane, wave);
 }
 
-// Clause evaluation, fixed width K, variable-range-partitioned (P <= MAX_RANGES phases).
-// Persistent: one 1024-thread workgroup per CU owns a contiguous run of tiles.  Phase r
-// stages the assignment words of variable range r in LDS (RANGE_WORDS) and streams the
-// literals of that range (compacted, clause order, 4-bit per-clause counts), so every
-// assignment lookup is an LDS read instead of an L2 request.  Each lane keeps the
-// "satisfied" bits of its clauses in a 64-bit register across phases; wave w evaluates the
-// 64-clause groups w, w+16, ... of the pass.  After the last phase the violated bits are
-// ballot-compacted into the per-tile lists exactly like k_eval_fixed.
+// Clause evaluation, fixed width K, persistent hybrid (the loop's default for fixed k).
+// One 1024-thread workgroup per CU owns a contiguous run of tiles.  The assignment words of
+// the first min(n, LDS_VARS) variables are staged once in LDS by LDS-DMA; a literal whose
+// variable lies there is looked up in LDS, the others in L2 (the whole bit-packed assignment
+// stays L2-resident).  Lanes evaluate 4 clauses of a 256-clause chunk with one 16-byte load
+// per literal slot from the chunk-transposed layout (as k_eval_fixed), so the literal stream
+// is read once, perfectly coalesced.  Violated clauses go to the per-tile lists through
+// per-tile LDS counters.
 template <int K>
-__global__ __launch_bounds__(RANGED_THREADS) void k_eval_ranged(ClauseView cv, LoopBuffers b,
-                                                               uint32_t tile_begin, uint32_t tile_end,
-                                                               int gated) {
+__global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, LoopBuffers b,
+                                                             uint32_t tile_begin, uint32_t tile_end,
+                                                             int gated) {
     if (gated && eval_gate_closed(b.state)) return;
     extern __shared__ __attribute__((aligned(16))) uint32_t s_A[];
-    __shared__ uint32_t s_tcnt[RANGED_MAX_TILES];
+    __shared__ uint32_t s_tcnt[HYB_MAX_TILES];
     const uint32_t nblk = gridDim.x;
     const uint32_t ntiles = tile_end - tile_begin;
     const uint32_t t0 = tile_begin + (uint32_t)(((uint64_t)ntiles * blockIdx.x) / nblk);
     const uint32_t t1 = tile_begin + (uint32_t)(((uint64_t)ntiles * (blockIdx.x + 1)) / nblk);
+    if (t0 >= t1) return;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     const uint64_t m = cv.m;
-    const uint32_t P = cv.n_ranges;
-    for (uint32_t pt = t0; pt < t1; pt += RANGED_MAX_TILES) {
-        const uint32_t pe = min(t1, pt + RANGED_MAX_TILES);
-        const uint32_t ngroups = (pe - pt) * TILE_WORDS;      // 64-clause groups of this pass
-        const uint64_t g0 = (uint64_t)pt * TILE_WORDS;
-        uint64_t sat = 0;
-        for (uint32_t r = 0; r < P; ++r) {
-            __syncthreads();
-            const uint32_t w_lo = r * RANGE_WORDS;
-            const uint32_t w_hi = min(b.n_words, w_lo + RANGE_WORDS);
-            for (uint32_t w = w_lo + threadIdx.x; w < w_hi; w += RANGED_THREADS) s_A[w - w_lo] = b.A[w];
-            __syncthreads();
-            const uint32_t* __restrict__ rl = cv.rlits[r];
-            const uint32_t* __restrict__ rc = cv.rcnt[r];
-            const uint32_t* __restrict__ rb = cv.rbase[r];
-            const uint32_t v_lo = r * RANGE_VARS;
-            const uint32_t n_i = ngroups > (uint32_t)wave ? (ngroups - wave + 15u) / 16u : 0u;
-            for (uint32_t i = 0; i < n_i; ++i) {
-                const uint64_t g = g0 + wave + 16u * i;
-                const uint32_t nib = (rc[g * 8 + (lane >> 3)] >> ((lane & 7) * 4)) & 15u;
-                uint32_t pre = 0;
+    const uint32_t lds_words = min(b.n_words, LDS_WORDS);
+    const uint32_t lds_vars = lds_words * 32u;
+    {
+        // LDS-DMA fill (global_load_lds_dwordx4: no VGPR round trip; A padded to 4 words)
+        const uint32_t n4 = (lds_words + 3) / 4;
+        const uint4* src = reinterpret_cast<const uint4*>(b.A);
+        const uint32_t wbase = __builtin_amdgcn_readfirstlane(wave * 64);
+        for (uint32_t q0 = 0; q0 < n4; q0 += HYB_THREADS) {
+            const uint32_t q = q0 + threadIdx.x;
+            if (q < n4)
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void*)(src + q),
+                    (__attribute__((address_space(3))) void*)(reinterpret_cast<uint4*>(s_A) + q0 + wbase),
+                    16, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    const uint32_t* __restrict__ A = b.A;
+    for (uint32_t pt = t0; pt < t1; pt += HYB_MAX_TILES) {
+        const uint32_t pe = min(t1, pt + HYB_MAX_TILES);
+        if (threadIdx.x < HYB_MAX_TILES) s_tcnt[threadIdx.x] = 0;
+        __syncthreads();  // also publishes the LDS fill
+        const uint64_t gbeg = (uint64_t)pt * (TILE / CHUNK), gend = (uint64_t)pe * (TILE / CHUNK);
+        for (uint64_t g = gbeg + wave; g < gend; g += HYB_THREADS / 64) {
+            const uint64_t cb = g * CHUNK;
+            uint32_t sat[4] = {0u, 0u, 0u, 0u};
+            if (cb < m) {
+                const uint4* src = reinterpret_cast<const uint4*>(cv.lits_t + cb * K) + lane;
+                uint4 x[K];
 #pragma unroll
-                for (int t = 0; t < K; ++t) pre += __popcll(__ballot(nib > (uint32_t)t) & lt);
-                const uint32_t off = rb[g] + pre;
-                uint32_t sb = 0;
+                for (int j = 0; j < K; ++j) x[j] = src[j * 64];
 #pragma unroll
-                for (int t = 0; t < K; ++t) {
-                    if ((uint32_t)t < nib) {
-                        const uint32_t l = rl[off + t];
-                        const uint32_t v = (l >> 1) - v_lo;
-                        sb |= ((s_A[v >> 5] >> (v & 31u)) & 1u) ^ (l & 1u);
+                for (int j = 0; j < K; ++j) {
+                    const uint32_t xs[4] = {x[j].x, x[j].y, x[j].z, x[j].w};
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const uint32_t v = xs[q] >> 1;
+                        const uint32_t w = (v < lds_vars) ? s_A[v >> 5] : A[v >> 5];
+                        sat[q] |= ((w >> (v & 31u)) & 1u) ^ (xs[q] & 1u);
                     }
                 }
-                sat |= (uint64_t)sb << i;
             }
-        }
-        // compaction into the per-tile lists
-        if (threadIdx.x < RANGED_MAX_TILES) s_tcnt[threadIdx.x] = 0;
-        __syncthreads();
-        for (uint32_t i = 0; i < 64; ++i) {
-            const uint32_t gl = wave + 16u * i;
-            if (gl >= ngroups) break;
-            const uint64_t g = g0 + gl;
-            const uint64_t c = g * 64 + lane;
-            const bool viol = !((sat >> i) & 1ull) && c < m;
-            const uint64_t mask = __ballot(viol);
-            if (lane == 0) b.vmask[g] = mask;
-            if (mask) {
-                const uint32_t tile = (uint32_t)(g / TILE_WORDS);
+            const uint64_t c0 = cb + 4u * lane;
+            const bool v0 = !sat[0] && c0 < m, v1 = !sat[1] && c0 + 1 < m;
+            const bool v2 = !sat[2] && c0 + 2 < m, v3 = !sat[3] && c0 + 3 < m;
+            const uint64_t b0 = __ballot(v0), b1 = __ballot(v1), b2 = __ballot(v2), b3 = __ballot(v3);
+            if (lane < 4) {
+                const int sh = 16 * lane;
+                const uint64_t w = spread4(b0 >> sh) | (spread4(b1 >> sh) << 1) |
+                                   (spread4(b2 >> sh) << 2) | (spread4(b3 >> sh) << 3);
+                b.vmask[g * 4 + lane] = w;
+            }
+            const uint32_t tot = __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
+            if (tot) {
+                const uint32_t tile = (uint32_t)(g / (TILE / CHUNK));
                 uint32_t base = 0;
-                if (lane == 0) base = atomicAdd(&s_tcnt[tile - pt], (uint32_t)__popcll(mask));
+                if (lane == 0) base = atomicAdd(&s_tcnt[tile - pt], tot);
                 base = __shfl(base, 0, 64);
-                if (viol) b.stage[(uint64_t)tile * TILE + base + __popcll(mask & lt)] = (uint32_t)c;
+                const uint32_t pre = __popcll(b0 & lt) + __popcll(b1 & lt) + __popcll(b2 & lt) +
+                                     __popcll(b3 & lt);
+                uint32_t* dst = b.stage + (uint64_t)tile * TILE + base + pre;
+                uint32_t q = 0;
+                if (v0) dst[q++] = (uint32_t)c0;
+                if (v1) dst[q++] = (uint32_t)(c0 + 1);
+                if (v2) dst[q++] = (uint32_t)(c0 + 2);
+                if (v3) dst[q++] = (uint32_t)(c0 + 3);
             }
         }
         __syncthreads();
@@ -269,7 +291,7 @@ __global__ __launch_bounds__(EVAL_THREADS) void k_eval_csr(ClauseView cv, LoopBu
             const uint32_t o0 = offs[c], o1 = offs[c + 1];
             uint32_t sat = 0;
             for (uint32_t j = o0; j < o1; ++j) {
-                const uint32_t l = lits[j];
+                const uint32_t l = lits[j] & LIT_MASK;
                 sat |= abit(A, l >> 1) ^ (l & 1u);
             }
             viol = !sat;
@@ -352,8 +374,15 @@ __global__ __launch_bounds__(ROUND_THREADS) void k_claim(ClauseView cv, LoopBuff
     const unsigned long long keyhi = (unsigned long long)(~(st->round_base + r)) << 32;
     __shared__ uint32_t s_e[TILE];
     __shared__ uint32_t s_wp;
+    // claims on hot variables are first reduced in an LDS hash table (one global atomic per
+    // hot variable per block instead of one per clause: power-law hubs)
+    __shared__ uint32_t s_hk[HOT_SLOTS];
+    __shared__ unsigned long long s_hv[HOT_SLOTS];
+    const bool hot = cv.n_hot != 0;
     uint32_t* list = b.stage + (uint64_t)tile * TILE;
     for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) s_e[i] = list[i];
+    if (hot)
+        for (uint32_t i = threadIdx.x; i < HOT_SLOTS; i += blockDim.x) { s_hk[i] = 0xFFFFFFFFu; s_hv[i] = ~0ull; }
     if (threadIdx.x == 0) s_wp = 0;
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
@@ -362,14 +391,31 @@ __global__ __launch_bounds__(ROUND_THREADS) void k_claim(ClauseView cv, LoopBuff
         clause_range<K>(cv, c, lb, le);
         bool killed = false;
         if (r > 0)
-            for (uint64_t j = lb; j < le; ++j) killed |= (b.cover[cv.lits[j] >> 1] == stamp);
+            for (uint64_t j = lb; j < le; ++j) killed |= (b.cover[lvar(cv, j)] == stamp);
         if (!killed) {
             const unsigned long long key = keyhi | c;
-            for (uint64_t j = lb; j < le; ++j) atomicMin(&b.owner[cv.lits[j] >> 1], key);
+            for (uint64_t j = lb; j < le; ++j) {
+                const uint32_t raw = cv.lits[j];
+                const uint32_t v = (raw & LIT_MASK) >> 1;
+                if (raw & LIT_HOT) {
+                    uint32_t h = (v * 2654435761u) & (HOT_SLOTS - 1);
+                    for (;;) {
+                        const uint32_t prev = atomicCAS(&s_hk[h], 0xFFFFFFFFu, v);
+                        if (prev == 0xFFFFFFFFu || prev == v) break;
+                        h = (h + 1) & (HOT_SLOTS - 1);
+                    }
+                    atomicMin(&s_hv[h], key);
+                } else {
+                    atomicMin(&b.owner[v], key);
+                }
+            }
             list[atomicAdd(&s_wp, 1u)] = c;
         }
     }
     __syncthreads();
+    if (hot)
+        for (uint32_t i = threadIdx.x; i < HOT_SLOTS; i += blockDim.x)
+            if (s_hk[i] != 0xFFFFFFFFu) atomicMin(&b.owner[s_hk[i]], s_hv[i]);
     if (threadIdx.x == 0) b.tile_cnt[tile] = s_wp;
 }
 
@@ -400,9 +446,9 @@ __global__ __launch_bounds__(ROUND_THREADS) void k_join(ClauseView cv, LoopBuffe
         clause_range<K>(cv, c, lb, le);
         const unsigned long long key = keyhi | c;
         bool own = true;
-        for (uint64_t j = lb; j < le; ++j) own &= (b.owner[cv.lits[j] >> 1] == key);
+        for (uint64_t j = lb; j < le; ++j) own &= (b.owner[lvar(cv, j)] == key);
         if (own) {
-            for (uint64_t j = lb; j < le; ++j) b.cover[cv.lits[j] >> 1] = stamp;
+            for (uint64_t j = lb; j < le; ++j) b.cover[lvar(cv, j)] = stamp;
             mis[atomicAdd(&s_mp, 1u)] = c;
         } else {
             s_keep[atomicAdd(&s_wp, 1u)] = c;
@@ -453,11 +499,11 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail(ClauseView cv, LoopBuffer
                 clause_range<K>(cv, c, lb, le);
                 bool killed = false;
                 for (uint64_t j = lb; j < le; ++j)
-                    killed |= (__hip_atomic_load(&b.cover[cv.lits[j] >> 1], __ATOMIC_RELAXED,
+                    killed |= (__hip_atomic_load(&b.cover[lvar(cv, j)], __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT) == stamp);
                 if (!killed) {
                     const unsigned long long key = keyhi | c;
-                    for (uint64_t j = lb; j < le; ++j) atomicMin(&b.owner[cv.lits[j] >> 1], key);
+                    for (uint64_t j = lb; j < le; ++j) atomicMin(&b.owner[lvar(cv, j)], key);
                     left[atomicAdd(&s_wp, 1u)] = c;
                 }
             }
@@ -478,11 +524,11 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail(ClauseView cv, LoopBuffer
                 const unsigned long long key = keyhi | c;
                 bool own = true;
                 for (uint64_t j = lb; j < le; ++j)
-                    own &= (__hip_atomic_load(&b.owner[cv.lits[j] >> 1], __ATOMIC_RELAXED,
+                    own &= (__hip_atomic_load(&b.owner[lvar(cv, j)], __ATOMIC_RELAXED,
                                               __HIP_MEMORY_SCOPE_AGENT) == key);
                 if (own) {
                     for (uint64_t j = lb; j < le; ++j)
-                        __hip_atomic_store(&b.cover[cv.lits[j] >> 1], stamp, __ATOMIC_RELAXED,
+                        __hip_atomic_store(&b.cover[lvar(cv, j)], stamp, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
                     b.tmis[atomicAdd(&s_tm, 1u)] = c;
                 } else {
@@ -523,9 +569,9 @@ __device__ __forceinline__ uint64_t resample_clause(const ClauseView& cv, uint32
     clause_range<K>(cv, c, lb, le);
     if (apply) {
         for (uint64_t j = lb; j < le; ++j) {
-            const uint32_t l = cv.lits[j], v = l >> 1;
+            const uint32_t l = cv.lits[j] & LIT_MASK, v = l >> 1;
             bool dup = false;
-            for (uint64_t q = lb; q < j; ++q) dup |= ((cv.lits[q] >> 1) == v);
+            for (uint64_t q = lb; q < j; ++q) dup |= (lvar(cv, q) == v);
             if (dup) continue;
             const uint32_t nb = philox_x(v, (uint32_t)it, 0u, (uint32_t)(it >> 32), k0, k1) & 1u;
             if (nb != (l & 1u)) atomicXor(&target[v >> 5], 1u << (v & 31u));
@@ -611,30 +657,31 @@ hipError_t launch_eval(const ClauseView& cv, const LoopBuffers& b, uint32_t tile
     return hipGetLastError();
 }
 
-hipError_t launch_eval_ranged(const ClauseView& cv, const LoopBuffers& b, uint32_t tile_begin,
-                              uint32_t tile_end, bool gated, int n_cu, hipStream_t s) {
+hipError_t launch_eval_hybrid(const ClauseView& cv, const LoopBuffers& b, uint32_t tile_begin,
+                              uint32_t tile_end, bool gated, int n_blocks, hipStream_t s) {
     if (tile_end <= tile_begin) return hipSuccess;
     const uint32_t nt = tile_end - tile_begin;
-    const dim3 grid(std::min<uint32_t>(nt, (uint32_t)n_cu));
-    const size_t lds = RANGE_WORDS * sizeof(uint32_t);
+    const dim3 grid(std::min<uint32_t>(nt, (uint32_t)std::max(1, n_blocks)));
+    const size_t lds = (size_t)std::max<uint32_t>(4, (std::min(b.n_words, LDS_WORDS) + 3) / 4 * 4) * 4;
     const int g = gated ? 1 : 0;
     static bool attr_set[MAX_FIXED_K + 1] = {};
     if (cv.k >= 1 && cv.k <= (uint32_t)MAX_FIXED_K && !attr_set[cv.k]) {
         hipError_t e = hipSuccess;
-        ALLL_DISPATCH_K(cv.k, (e = hipFuncSetAttribute((const void*)k_eval_ranged<(K > 0 ? K : 1)>,
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)));
+        ALLL_DISPATCH_K(cv.k, (e = hipFuncSetAttribute((const void*)k_eval_hybrid<(K > 0 ? K : 1)>,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       (int)(LDS_WORDS * 4))));
         if (e != hipSuccess) return e;
         attr_set[cv.k] = true;
     }
     switch (cv.k) {
-        case 1: k_eval_ranged<1><<<grid, RANGED_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g); break;
-        case 2: k_eval_ranged<2><<<grid, RANGED_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g); break;
-        case 3: k_eval_ranged<3><<<grid, RANGED_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g); break;
-        case 4: k_eval_ranged<4><<<grid, RANGED_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g); break;
-        case 5: k_eval_ranged<5><<<grid, RANGED_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g); break;
-        case 6: k_eval_ranged<6><<<grid, RANGED_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g); break;
-        case 7: k_eval_ranged<7><<<grid, RANGED_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g); break;
-        case 8: k_eval_ranged<8><<<grid, RANGED_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g); break;
+        case 1: k_eval_hybrid<1><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g); break;
+        case 2: k_eval_hybrid<2><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g); break;
+        case 3: k_eval_hybrid<3><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g); break;
+        case 4: k_eval_hybrid<4><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g); break;
+        case 5: k_eval_hybrid<5><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g); break;
+        case 6: k_eval_hybrid<6><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g); break;
+        case 7: k_eval_hybrid<7><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g); break;
+        case 8: k_eval_hybrid<8><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <new>
@@ -77,6 +78,7 @@ struct alll_ctx {
     bool use_graph = true;
     hipEvent_t ev[8] = {};
     int n_cu = 256;
+    bool hybrid = false;
     std::string eval_name;
 };
 
@@ -115,7 +117,11 @@ int write_limits(alll_ctx* c, uint64_t limit_eval, uint64_t limit_nores) {
 }
 
 hipError_t eval_launch(alll_ctx* c, uint32_t tb, uint32_t te, bool gated) {
-    if (c->cv.n_ranges) return launch_eval_ranged(c->cv, c->b, tb, te, gated, c->n_cu, c->stream);
+    if (c->hybrid) {
+        int grid = c->n_cu;
+        if (const char* e = getenv("ALLL_EVAL_GRID")) grid = atoi(e);  // tuning experiments
+        return launch_eval_hybrid(c->cv, c->b, tb, te, gated, grid, c->stream);
+    }
     return launch_eval(c->cv, c->b, tb, te, gated, c->stream);
 }
 
@@ -205,6 +211,8 @@ int fill_stats(alll_ctx* c, alll_stats* st) {
     st->n_violated = c->h_state->u_total;
     st->solved = (c->h_state->done == 1) ? 1 : 0;
     st->n_gpus = c->world;
+    st->lfmis_rounds_max = c->h_state->max_rounds;
+    st->lfmis_tail_rounds = c->h_state->tail_rounds;
     return ALLL_OK;
 }
 
@@ -326,7 +334,7 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     b.n_words = (c->n_vars + 31) / 32;
     b.n_tiles = n_tiles;
     b.seed = opt.seed;
-    if ((rc = dalloc(c, &b.A, b.n_words))) return bail(rc);
+    if ((rc = dalloc(c, &b.A, b.n_words + 4))) return bail(rc);  // +4: 16-byte tail loads
     if ((rc = dalloc(c, &b.vmask, (size_t)c->n_tiles_padded * TILE_WORDS))) return bail(rc);
     if ((rc = dalloc(c, &b.tile_cnt, n_tiles))) return bail(rc);
     if ((rc = dalloc(c, &b.mis_cnt, n_tiles))) return bail(rc);
@@ -354,8 +362,31 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     if (hipStreamSynchronize(c->stream) != hipSuccess) return bail(fail(ALLL_ERR_HIP, "memset drain failed"));
 
     // ---- clauses: AoS literals (+ offsets or a chunk-transposed copy for fixed width k)
-    if (L && hipMemcpy(d_lits, prob->literals, L * 4, hipMemcpyHostToDevice) != hipSuccess)
-        return bail(fail(ALLL_ERR_HIP, "literal upload failed"));
+    {
+        // hot variables: degree >= max(1024, 32 x mean degree), at most HOT_MAX of the highest
+        std::vector<uint32_t> flagged;
+        if (L && c->n_vars && c->n_vars < (1u << 30)) {
+            std::vector<uint32_t> deg(c->n_vars, 0u);
+            for (uint64_t j = 0; j < L; ++j) ++deg[prob->literals[j] >> 1];
+            const uint64_t thr = std::max<uint64_t>(1024, 32 * (L / c->n_vars + 1));
+            std::vector<std::pair<uint32_t, uint32_t>> hot;
+            for (uint32_t v = 0; v < c->n_vars; ++v)
+                if (deg[v] >= thr) hot.push_back({deg[v], v});
+            if (!hot.empty()) {
+                std::sort(hot.rbegin(), hot.rend());
+                if (hot.size() > HOT_MAX) hot.resize(HOT_MAX);
+                std::vector<uint8_t> is_hot(c->n_vars, 0);
+                for (auto& h : hot) is_hot[h.second] = 1;
+                flagged.assign(prob->literals, prob->literals + L);
+                for (auto& l : flagged)
+                    if (is_hot[l >> 1]) l |= 0x80000000u;
+                cv.n_hot = (uint32_t)hot.size();
+            }
+        }
+        const uint32_t* src = flagged.empty() ? prob->literals : flagged.data();
+        if (L && hipMemcpy(d_lits, src, L * 4, hipMemcpyHostToDevice) != hipSuccess)
+            return bail(fail(ALLL_ERR_HIP, "literal upload failed"));
+    }
     cv.lits = d_lits;
     if (fixed_k > 0) {
         std::vector<uint32_t> t(real_chunks * CHUNK * fixed_k, 0u);
@@ -368,47 +399,6 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
             return bail(fail(ALLL_ERR_HIP, "transposed literal upload failed"));
         cv.lits_t = d_t;
         cv.offs = nullptr;
-        // variable-range-partitioned copy for the LDS evaluation kernel
-        const uint32_t P = (b.n_words + RANGE_WORDS - 1) / RANGE_WORDS;
-        if (!(opt.flags & ALLL_FLAG_NO_RANGED) && P >= 1 && P <= (uint32_t)MAX_RANGES && m > 0) {
-            const uint64_t groups = (uint64_t)n_tiles * TILE_WORDS;
-            std::vector<uint32_t> rl;
-            rl.reserve(L);
-            std::vector<uint32_t> rcv(groups * 8), rbv(groups);
-            uint64_t roff[MAX_RANGES];
-            for (uint32_t r = 0; r < P; ++r) {
-                roff[r] = rl.size();
-                std::fill(rcv.begin(), rcv.end(), 0u);
-                const uint32_t vlo = r * RANGE_VARS, vhi = vlo + RANGE_VARS;
-                for (uint64_t g = 0; g < groups; ++g) {
-                    rbv[g] = (uint32_t)(rl.size() - roff[r]);
-                    const uint64_t ce = std::min<uint64_t>(m, (g + 1) * 64);
-                    for (uint64_t cl = g * 64; cl < ce; ++cl) {
-                        uint32_t cnt = 0;
-                        for (int j = 0; j < fixed_k; ++j) {
-                            const uint32_t l = prob->literals[cl * fixed_k + j], v = l >> 1;
-                            if (v >= vlo && v < vhi) { rl.push_back(l); ++cnt; }
-                        }
-                        rcv[cl >> 3] |= cnt << ((cl & 7) * 4);
-                    }
-                }
-                uint32_t *d_rc = nullptr, *d_rb = nullptr;
-                if ((rc = dalloc(c, &d_rc, rcv.size())) || (rc = dalloc(c, &d_rb, rbv.size()))) return bail(rc);
-                cv.rcnt[r] = d_rc;
-                cv.rbase[r] = d_rb;
-                if (hipStreamSynchronize(c->stream) != hipSuccess ||
-                    hipMemcpy(d_rc, rcv.data(), rcv.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
-                    hipMemcpy(d_rb, rbv.data(), rbv.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
-                    return bail(fail(ALLL_ERR_HIP, "range layout upload failed"));
-            }
-            uint32_t* d_rl = nullptr;
-            if ((rc = dalloc(c, &d_rl, rl.size()))) return bail(rc);
-            if (hipStreamSynchronize(c->stream) != hipSuccess ||
-                (!rl.empty() && hipMemcpy(d_rl, rl.data(), rl.size() * 4, hipMemcpyHostToDevice) != hipSuccess))
-                return bail(fail(ALLL_ERR_HIP, "range literal upload failed"));
-            for (uint32_t r = 0; r < P; ++r) cv.rlits[r] = d_rl + roff[r];
-            cv.n_ranges = P;
-        }
     } else {
         std::vector<uint32_t> o32(m + 1);
         for (uint64_t i = 0; i <= m; ++i) o32[i] = m ? (uint32_t)prob->offsets[i] : 0u;
@@ -441,8 +431,9 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
         if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0)
             c->n_cu = prop.multiProcessorCount;
     }
+    c->hybrid = cv.k > 0 && !(opt.flags & ALLL_FLAG_NO_RANGED);
     char nm[64];
-    if (cv.n_ranges) snprintf(nm, sizeof nm, "k_eval_ranged<%u>", cv.k);
+    if (c->hybrid) snprintf(nm, sizeof nm, "k_eval_hybrid<%u>", cv.k);
     else if (cv.k) snprintf(nm, sizeof nm, "k_eval_fixed<%u>", cv.k);
     else snprintf(nm, sizeof nm, "k_eval_csr");
     c->eval_name = nm;

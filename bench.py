@@ -212,6 +212,7 @@ def main():
             "resample_iters_per_s": iters_s,
             "violated_last": st["n_violated"],
             "avg_mis_size": st["avg_mis_size"],
+            "lfmis_rounds_max": st["lfmis_rounds_max"],
             "phase_ms": {k2: pt[k2] for k2 in ("eval_ms", "exchange_ms", "mis_ms", "resample_ms", "total_ms")},
             "roofline": {
                 "bound": "hbm",

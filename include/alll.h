@@ -52,7 +52,8 @@ typedef struct alll_problem {
 #define ALLL_FLAG_EXCHANGE_ALLREDUCE (1u << 1) /* multi-GPU: shard resample + allreduce of the
                                                  bit-packed assignment delta (north_star form) */
 #define ALLL_FLAG_GENERIC_CSR       (1u << 2) /* disable the fixed-width clause layout */
-#define ALLL_FLAG_NO_RANGED         (1u << 3) /* disable the LDS variable-range evaluation kernel */
+#define ALLL_FLAG_NO_RANGED         (1u << 3) /* use the L2-gather eval kernel instead of the
+                                                 persistent LDS/L2 hybrid */
 
 typedef struct alll_options {
     uint64_t seed;          /* Philox4x32-10 key; replaces std::random_device (SATInstance.h:346) */
@@ -77,6 +78,8 @@ typedef struct alll_stats {
     uint64_t n_violated;     /* violated clauses found by the last eval pass */
     int32_t solved;          /* 1 if the last eval pass found no violated clause */
     int32_t n_gpus;          /* entries used in gpu_resamples */
+    uint32_t lfmis_rounds_max;  /* most LFMIS rounds one iteration needed (grid + tail) */
+    uint32_t lfmis_tail_rounds; /* rounds run by the tail kernel in the last iteration */
     uint64_t gpu_resamples[ALLL_MAX_GPU_STATS]; /* per clause-shard share of n_resamples */
 } alll_stats;
 

@@ -21,7 +21,7 @@ from conftest import GOLDEN
 pytestmark = pytest.mark.gpu
 
 T1_FIXTURES = sorted(p for p in glob.glob(os.path.join(GOLDEN, "*_T1.npz")))
-LAYOUTS = {"ranged": 0, "fixed": 1 << 3, "csr": 1 << 2}
+LAYOUTS = {"hybrid": 0, "fixed": 1 << 3, "csr": 1 << 2}
 
 
 @pytest.fixture(scope="module")
@@ -75,6 +75,7 @@ def _instances():
         "k8": (4000, 6000, 8, 0),
         "powerlaw": (2000, 8000, 3, 1),
         "k5_multi_tile": (30000, 60000, 5, 0),
+        "powerlaw_hot": (20000, 80000, 3, 1),   # hub variables -> LDS-aggregated claims
     }.items():
         out[name] = (n,) + generate_ksat(1, n, m, k, kind)
     f = dict(np.load(os.path.join(GOLDEN, "edge_T1.npz")))
@@ -101,7 +102,7 @@ def instances():
 
 @pytest.mark.parametrize("layout", list(LAYOUTS))
 @pytest.mark.parametrize("name", ["c1_ratio4", "u2500_ratio4", "ratio2_solves", "k8", "powerlaw",
-                                  "k5_multi_tile", "edge", "ragged"])
+                                  "k5_multi_tile", "powerlaw_hot", "edge", "ragged"])
 def test_trajectory_matches_oracle(gpu, oracle_mod, name, layout):
     from alllsatisfiabilitysolver_amd import Solver
 

@@ -56,13 +56,15 @@ struct ClauseView {
     uint64_t m;             // clauses
     uint32_t k;             // fixed width, 0 = generic CSR
     uint32_t n_hot;         // variables flagged hot (bit 31 of their literals in `lits`)
+    const uint32_t* perm;   // fixed-k: evaluation position -> clause id (nullptr = identity)
 };
 
 struct LoopBuffers {
     uint32_t* A;            // bit-packed assignment, ceil(n/32) words
-    uint64_t* vmask;        // violated bitmask, n_tiles_padded * TILE_WORDS words
+    uint64_t* vmask;        // violated bitmask in evaluation order, n_tiles_padded * TILE_WORDS words
     uint32_t* tile_cnt;     // undecided violated entries per tile
-    uint32_t* stage;        // per tile: TILE slots of undecided violated clause ids
+    uint32_t* stage;        // per tile: TILE slots of undecided violated clauses (evaluation
+                            // positions until LFMIS round 0 translates them to clause ids)
     uint32_t* mis_cnt;      // MIS entries per tile (current iteration)
     uint32_t* mis;          // per tile: TILE slots of MIS clause ids
     uint32_t* left;         // compact list of undecided clauses handed to the tail kernel

@@ -385,8 +385,9 @@ __global__ __launch_bounds__(ROUND_THREADS) void k_claim(ClauseView cv, LoopBuff
         for (uint32_t i = threadIdx.x; i < HOT_SLOTS; i += blockDim.x) { s_hk[i] = 0xFFFFFFFFu; s_hv[i] = ~0ull; }
     if (threadIdx.x == 0) s_wp = 0;
     __syncthreads();
+    const bool translate = (r == 0) && cv.perm != nullptr;
     for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
-        const uint32_t c = s_e[i];
+        const uint32_t c = translate ? cv.perm[s_e[i]] : s_e[i];
         uint64_t lb, le;
         clause_range<K>(cv, c, lb, le);
         bool killed = false;

@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstring>
 #include <new>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -79,6 +80,7 @@ struct alll_ctx {
     hipEvent_t ev[8] = {};
     int n_cu = 256;
     bool hybrid = false;
+    std::vector<uint32_t> perm;  // evaluation position -> clause id (fixed-k layout)
     std::string eval_name;
 };
 
@@ -389,14 +391,55 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     }
     cv.lits = d_lits;
     if (fixed_k > 0) {
+        // Locality order for evaluation (results do not depend on it: the violated set is a
+        // set and the LFMIS priorities are the original clause ids).  Inside every shard the
+        // clauses are evaluated sorted by (largest, second largest) variable and each clause's
+        // literals are stored by descending variable, so the gathers of slot 0 (and mostly
+        // slot 1) of a wave hit a few cache lines.  perm[p] = original id of position p.
+        std::vector<uint32_t>& perm = c->perm;
+        perm.resize(m);
+        {
+            const int K = fixed_k;
+            auto key_of = [&](uint64_t cl) -> uint64_t {
+                uint32_t a = 0, b2 = 0;
+                for (int j = 0; j < K; ++j) {
+                    const uint32_t v = prob->literals[cl * K + j] >> 1;
+                    if (v > a) { b2 = a; a = v; }
+                    else if (v > b2) b2 = v;
+                }
+                return ((uint64_t)a << 32) | b2;
+            };
+            auto sort_range = [&](uint64_t cb0, uint64_t ce0) {
+                std::vector<std::pair<uint64_t, uint32_t>> kv(ce0 - cb0);
+                for (uint64_t cl = cb0; cl < ce0; ++cl) kv[cl - cb0] = {key_of(cl), (uint32_t)cl};
+                std::sort(kv.begin(), kv.end());
+                for (uint64_t i = 0; i < kv.size(); ++i) perm[cb0 + i] = kv[i].second;
+            };
+            std::vector<std::thread> th;
+            for (int r = 0; r < c->world; ++r) {
+                const uint64_t cb0 = std::min<uint64_t>(m, (uint64_t)r * c->tiles_per_rank * TILE);
+                const uint64_t ce0 = std::min<uint64_t>(m, cb0 + (uint64_t)c->tiles_per_rank * TILE);
+                if (ce0 > cb0) th.emplace_back(sort_range, cb0, ce0);
+            }
+            for (auto& t : th) t.join();
+        }
         std::vector<uint32_t> t(real_chunks * CHUNK * fixed_k, 0u);
-        for (uint64_t cl = 0; cl < m; ++cl) {
-            const uint64_t g = cl / CHUNK, r = cl % CHUNK;
-            for (int j = 0; j < fixed_k; ++j)
-                t[(g * fixed_k + j) * CHUNK + r] = prob->literals[cl * fixed_k + j];
+        std::vector<uint32_t> tmp(fixed_k);
+        for (uint64_t p2 = 0; p2 < m; ++p2) {
+            const uint64_t cl = perm[p2];
+            for (int j = 0; j < fixed_k; ++j) tmp[j] = prob->literals[cl * fixed_k + j];
+            std::sort(tmp.begin(), tmp.end(), [](uint32_t x, uint32_t y) { return (x >> 1) > (y >> 1); });
+            const uint64_t g = p2 / CHUNK, r = p2 % CHUNK;
+            for (int j = 0; j < fixed_k; ++j) t[(g * fixed_k + j) * CHUNK + r] = tmp[j];
         }
         if (!t.empty() && hipMemcpy(d_t, t.data(), t.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
             return bail(fail(ALLL_ERR_HIP, "transposed literal upload failed"));
+        uint32_t* d_perm = nullptr;
+        if ((rc = dalloc(c, &d_perm, m))) return bail(rc);
+        if (hipStreamSynchronize(c->stream) != hipSuccess ||
+            hipMemcpy(d_perm, perm.data(), m * 4, hipMemcpyHostToDevice) != hipSuccess)
+            return bail(fail(ALLL_ERR_HIP, "permutation upload failed"));
+        cv.perm = d_perm;
         cv.lits_t = d_t;
         cv.offs = nullptr;
     } else {
@@ -566,6 +609,12 @@ int alll_get_violated_mask(alll_ctx* c, uint64_t* out, uint64_t n_words) {
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (need) HIP_TRY(hipMemcpy(out, c->b.vmask, need * 8, hipMemcpyDeviceToHost));
     if (c->m & 63) out[need - 1] &= (1ull << (c->m & 63)) - 1ull;
+    if (!c->perm.empty()) {  // device bits are in evaluation order
+        std::vector<uint64_t> ev(out, out + need);
+        std::fill(out, out + need, 0ull);
+        for (uint64_t p = 0; p < c->m; ++p)
+            if ((ev[p >> 6] >> (p & 63)) & 1ull) out[c->perm[p] >> 6] |= 1ull << (c->perm[p] & 63);
+    }
     return ALLL_OK;
 }
 

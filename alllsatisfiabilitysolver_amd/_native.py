@@ -35,7 +35,7 @@ MAX_GPU_STATS = 64
 # Every symbol include/alll.h declares (checked by tests/test_abi.py).
 EXPORTED = [
     "alll_version", "alll_last_error", "alll_default_options", "alll_device_count",
-    "alll_comm_unique_id", "alll_create", "alll_destroy", "alll_solve", "alll_run",
+    "alll_comm_unique_id", "alll_create", "alll_destroy", "alll_set_host_exchange", "alll_solve", "alll_run",
     "alll_get_stats", "alll_verify", "alll_get_assignment", "alll_set_assignment",
     "alll_get_assignment_words", "alll_set_assignment_words", "alll_get_violated_mask",
     "alll_get_mis", "alll_bench_eval", "alll_profile", "alll_synchronize", "alll_eval_bytes",
@@ -112,6 +112,11 @@ _u32p = ctypes.POINTER(ctypes.c_uint32)
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 _vp = ctypes.c_void_p
 
+EXCHANGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                               ctypes.c_uint64)
+XCHG_ALLGATHER = 0
+XCHG_ALLREDUCE_SUM_U32 = 1
+
 _SIGS = {
     "alll_version": ([], ctypes.c_char_p),
     "alll_last_error": ([], ctypes.c_char_p),
@@ -120,6 +125,7 @@ _SIGS = {
     "alll_comm_unique_id": ([ctypes.POINTER(ctypes.c_uint8)], ctypes.c_int),
     "alll_create": ([ctypes.POINTER(Problem), ctypes.POINTER(Options), ctypes.POINTER(_vp)], ctypes.c_int),
     "alll_destroy": ([_vp], ctypes.c_int),
+    "alll_set_host_exchange": ([_vp, EXCHANGE_FN, _vp], ctypes.c_int),
     "alll_solve": ([_vp, ctypes.POINTER(Stats)], ctypes.c_int),
     "alll_run": ([_vp, ctypes.c_uint64, ctypes.POINTER(Stats)], ctypes.c_int),
     "alll_get_stats": ([_vp, ctypes.POINTER(Stats)], ctypes.c_int),

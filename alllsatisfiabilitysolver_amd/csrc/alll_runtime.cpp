@@ -80,6 +80,9 @@ struct alll_ctx {
     hipEvent_t ev[8] = {};
     int n_cu = 256;
     bool hybrid = false;
+    alll_exchange_fn xfn = nullptr;  // host-staged exchange (instead of RCCL)
+    void* xuser = nullptr;
+    std::vector<uint8_t> xbuf;
     std::vector<uint32_t> perm;  // evaluation position -> clause id (fixed-k layout)
     std::string eval_name;
 };
@@ -127,6 +130,23 @@ hipError_t eval_launch(alll_ctx* c, uint32_t tb, uint32_t te, bool gated) {
     return launch_eval(c->cv, c->b, tb, te, gated, c->stream);
 }
 
+// Host-staged collective: drain the stream, move the device buffer through host memory and
+// the user's exchange function.  Allgather: `bytes` per rank, own piece at `own_off`.
+int host_exchange(alll_ctx* c, int op, void* dev, size_t bytes, size_t own_off) {
+    if (!c->xfn) return fail(ALLL_ERR_INVALID_ARG, "world > 1 without RCCL needs alll_set_host_exchange");
+    const size_t total = op == ALLL_XCHG_ALLGATHER ? bytes * c->world : bytes;
+    c->xbuf.resize(total);
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (op == ALLL_XCHG_ALLGATHER)
+        HIP_TRY(hipMemcpy(c->xbuf.data() + own_off, (uint8_t*)dev + own_off, bytes, hipMemcpyDeviceToHost));
+    else
+        HIP_TRY(hipMemcpy(c->xbuf.data(), dev, bytes, hipMemcpyDeviceToHost));
+    if (c->xfn(c->xuser, op, c->xbuf.data(), bytes) != 0)
+        return fail(ALLL_ERR_RCCL, "host exchange callback failed");
+    HIP_TRY(hipMemcpy(dev, c->xbuf.data(), total, hipMemcpyHostToDevice));
+    return ALLL_OK;
+}
+
 // The launch sequence of one iteration (SATInstance.h:260-311).  Every kernel is gated on
 // the device state, so replaying it after convergence is a no-op.
 int enqueue_iteration(alll_ctx* c, hipEvent_t* marks) {
@@ -136,8 +156,13 @@ int enqueue_iteration(alll_ctx* c, hipEvent_t* marks) {
     if (marks) HIP_TRY(hipEventRecord(marks[1], s));
     if (c->world > 1) {
         const size_t words = (size_t)c->tiles_per_rank * TILE_WORDS;
-        NCCL_TRY(ncclAllGather(c->b.vmask + (size_t)c->rank * words, c->b.vmask, words, ncclUint64,
-                               c->comm, s));
+        if (c->comm) {
+            NCCL_TRY(ncclAllGather(c->b.vmask + (size_t)c->rank * words, c->b.vmask, words, ncclUint64,
+                                   c->comm, s));
+        } else {
+            int rc = host_exchange(c, ALLL_XCHG_ALLGATHER, c->b.vmask, words * 8, (size_t)c->rank * words * 8);
+            if (rc) return rc;
+        }
         HIP_TRY(launch_collect(c->cv, c->b, c->own_begin, c->own_end, s));
     }
     if (marks) HIP_TRY(hipEventRecord(marks[2], s));
@@ -148,7 +173,12 @@ int enqueue_iteration(alll_ctx* c, hipEvent_t* marks) {
     if (marks) HIP_TRY(hipEventRecord(marks[3], s));
     if (c->allreduce && c->world > 1) {
         HIP_TRY(launch_resample(c->cv, c->b, c->own_begin, c->own_end, true, s));
-        NCCL_TRY(ncclAllReduce(c->b.delta, c->b.delta, c->b.n_words, ncclUint32, ncclSum, c->comm, s));
+        if (c->comm) {
+            NCCL_TRY(ncclAllReduce(c->b.delta, c->b.delta, c->b.n_words, ncclUint32, ncclSum, c->comm, s));
+        } else {
+            int rc = host_exchange(c, ALLL_XCHG_ALLREDUCE_SUM_U32, c->b.delta, (size_t)c->b.n_words * 4, 0);
+            if (rc) return rc;
+        }
         HIP_TRY(launch_apply_delta(c->b, s));
     } else {
         HIP_TRY(launch_resample(c->cv, c->b, c->own_begin, c->own_end, false, s));
@@ -462,10 +492,16 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
 
     // ---- RCCL communicator (clause-sharded mode)
     if (c->world > 1) {
-        ncclUniqueId id;
-        memcpy(&id, opt.comm_id, 128);
-        ncclResult_t r = ncclCommInitRank(&c->comm, c->world, id, c->rank);
-        if (r != ncclSuccess) return bail(fail(ALLL_ERR_RCCL, "ncclCommInitRank: %s", ncclGetErrorString(r)));
+        bool zero = true;
+        for (int i = 0; i < 128; ++i) zero &= opt.comm_id[i] == 0;
+        if (!zero) {
+            ncclUniqueId id;
+            memcpy(&id, opt.comm_id, 128);
+            ncclResult_t r = ncclCommInitRank(&c->comm, c->world, id, c->rank);
+            if (r != ncclSuccess) return bail(fail(ALLL_ERR_RCCL, "ncclCommInitRank: %s", ncclGetErrorString(r)));
+        } else {
+            c->use_graph = false;  // host-staged exchange: eager launches
+        }
     }
     if (hipStreamSynchronize(c->stream) != hipSuccess)
         return bail(fail(ALLL_ERR_HIP, "create: stream sync failed: %s", hipGetErrorString(hipGetLastError())));
@@ -497,6 +533,14 @@ int alll_destroy(alll_ctx* c) {
     if (c->h_state) (void)hipHostFree(c->h_state);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
+    return ALLL_OK;
+}
+
+int alll_set_host_exchange(alll_ctx* c, alll_exchange_fn fn, void* user) {
+    if (!c) return fail(ALLL_ERR_INVALID_ARG, "null context");
+    c->xfn = fn;
+    c->xuser = user;
+    c->use_graph = false;
     return ALLL_OK;
 }
 

@@ -74,7 +74,8 @@ class Solver:
 
     def __init__(self, n_vars: int, offsets, literals, seed: int = 1, max_iters: int = 0,
                  device: int = -1, n_threads: int = 1, rank: int = 0, world: int = 1,
-                 comm_id: Optional[bytes] = None, flags: int = 0, grid_rounds: int = 0):
+                 comm_id: Optional[bytes] = None, flags: int = 0, grid_rounds: int = 0,
+                 exchange=None):
         self._L = N.lib()
         self.n_vars = int(n_vars)
         self.offsets = np.ascontiguousarray(offsets, np.uint64)
@@ -93,6 +94,29 @@ class Solver:
                 "alll_create")
         self.world = world
         self.rank = rank
+        self._xfn = None
+        if exchange is not None:
+            self.set_host_exchange(exchange)
+
+    def set_host_exchange(self, exchange):
+        """exchange(op, buf: numpy uint8 view, bytes_per_rank_or_total) -> None; see
+        include/alll.h (ALLL_XCHG_*).  Used instead of RCCL (e.g. several ranks on one GPU)."""
+        world = self.world
+
+        def fn(user, op, buf, nbytes):
+            try:
+                total = nbytes * world if op == N.XCHG_ALLGATHER else nbytes
+                arr = np.ctypeslib.as_array((ctypes.c_uint8 * total).from_address(buf))
+                exchange(op, arr, nbytes)
+                return 0
+            except Exception:  # reported as ALLL_ERR_RCCL by the library
+                import traceback
+
+                traceback.print_exc()
+                return 1
+
+        self._xfn = N.EXCHANGE_FN(fn)
+        N.check(self._L.alll_set_host_exchange(self._ctx, self._xfn, None), "set_host_exchange")
 
     # lifecycle
     def close(self):
@@ -205,6 +229,27 @@ def shard_plan(n_clauses: int, world: int, rank: int):
     N.check(N.lib().alll_shard_plan(n_clauses, world, rank, ctypes.byref(b), ctypes.byref(e),
                                     ctypes.byref(w)), "shard_plan")
     return int(b.value), int(e.value), int(w.value)
+
+
+def gloo_exchange(group=None):
+    """Host exchange over torch.distributed (gloo) for Solver(exchange=...)."""
+    import torch
+    import torch.distributed as dist
+
+    def ex(op, arr, nbytes):
+        world = dist.get_world_size(group)
+        if op == N.XCHG_ALLGATHER:
+            rank = dist.get_rank(group)
+            mine = torch.from_numpy(arr[rank * nbytes:(rank + 1) * nbytes].copy())
+            parts = [torch.empty(nbytes, dtype=torch.uint8) for _ in range(world)]
+            dist.all_gather(parts, mine, group=group)
+            arr[:] = torch.cat(parts).numpy()
+        else:
+            t = torch.from_numpy(arr.view(np.uint32).astype(np.int64))
+            dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
+            arr.view(np.uint32)[:] = (t.numpy() & 0xFFFFFFFF).astype(np.uint32)
+
+    return ex
 
 
 def comm_unique_id() -> bytes:

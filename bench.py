@@ -143,8 +143,20 @@ def main():
     if args.no_ranged:
         flags |= N.FLAG_NO_RANGED
     t0 = time.perf_counter()
-    s = Solver(n, offs, lits, seed=args.seed, device=local_rank, rank=rank, world=world,
-               comm_id=comm_id, flags=flags)
+    exchange_impl = "rccl" if world > 1 else "none"
+    try:
+        s = Solver(n, offs, lits, seed=args.seed, device=local_rank, rank=rank, world=world,
+                   comm_id=comm_id, flags=flags)
+    except N.AlllError as e:
+        if world == 1 or e.code != N.ALLL_ERR_RCCL:
+            raise
+        # RCCL communicator unavailable: same kernels, host-staged exchange over gloo
+        from alllsatisfiabilitysolver_amd import gloo_exchange
+
+        log(f"[rank {rank}] RCCL init failed ({e}); using the host-staged gloo exchange")
+        exchange_impl = "host-gloo"
+        s = Solver(n, offs, lits, seed=args.seed, device=local_rank, rank=rank, world=world,
+                   flags=flags, exchange=gloo_exchange())
     del offs, lits
     t_create = time.perf_counter() - t0
     log(f"[rank {rank}] generated {m} clauses in {t_gen:.2f}s, uploaded in {t_create:.2f}s, "
@@ -207,7 +219,8 @@ def main():
             "dtype": "u32",
             "data": "synthetic (seeded counter-based random k-SAT generator, gen_seed=1)",
             "config": {"workload": f"{args.config}: {desc}", "n_vars": n, "n_clauses": m, "k": k,
-                       "solve_seed": args.seed, "exchange": args.exchange if world > 1 else "none",
+                       "solve_seed": args.seed,
+                       "exchange": f"{args.exchange}/{exchange_impl}" if world > 1 else "none",
                        "parallelism": f"clause-shard x{world}"},
             "resample_iters_per_s": iters_s,
             "violated_last": st["n_violated"],

@@ -62,7 +62,8 @@ typedef struct alll_options {
     int32_t n_threads;      /* length of the per-thread resample vector reported (>= 1) */
     int32_t rank;           /* clause shard of this process (0 .. world-1) */
     int32_t world;          /* number of GPUs the clauses are sharded over (1 = single GPU) */
-    uint8_t comm_id[128];   /* RCCL unique id from alll_comm_unique_id() on rank 0 (world > 1) */
+    uint8_t comm_id[128];   /* RCCL unique id from alll_comm_unique_id() on rank 0 (world > 1);
+                               all zero: no RCCL, alll_set_host_exchange() is required */
     uint32_t flags;         /* ALLL_FLAG_* */
     uint32_t grid_rounds;   /* full-grid LFMIS rounds before the tail kernel (0 = default) */
 } alll_options;
@@ -107,11 +108,23 @@ int alll_device_count(void);
  * alll_options.comm_id). */
 int alll_comm_unique_id(uint8_t out[128]);
 
+/* Host-staged exchange for the clause-sharded mode (alternative to RCCL, e.g. several
+ * ranks sharing one GPU, or CPU-side collectives): op ALLL_XCHG_ALLGATHER -- `buf` holds
+ * world * `bytes` bytes, this rank's piece at rank * bytes is filled, gather the others in
+ * place; op ALLL_XCHG_ALLREDUCE_SUM_U32 -- element-wise sum of `bytes`/4 uint32 in place.
+ * Return 0 on success. */
+#define ALLL_XCHG_ALLGATHER 0
+#define ALLL_XCHG_ALLREDUCE_SUM_U32 1
+typedef int (*alll_exchange_fn)(void* user, int op, void* buf, uint64_t bytes);
+
 /* Replaces SATInstance<T>(VariablesArray<T>*, int n_threads) (SATInstance.h:51-56) plus the
  * random initial assignment of VariablesArray<T>(n_vars) (VariablesArray.h:23-34).  Copies
  * the caller's CSR to the device; keeps no caller pointer. */
 int alll_create(const alll_problem* prob, const alll_options* opt, alll_ctx** out);
 int alll_destroy(alll_ctx* ctx);
+
+/* Use a host-staged exchange instead of RCCL (world > 1; create with an all-zero comm_id). */
+int alll_set_host_exchange(alll_ctx* ctx, alll_exchange_fn fn, void* user);
 
 /* Replaces Statistics* SATInstance::solve(vector<ClauseArray*>*) (SATInstance.h:60-66 ->
  * parallel_solve :217-320).  Runs until no clause is violated (ALLL_OK) or max_iters

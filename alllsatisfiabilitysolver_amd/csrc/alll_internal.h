@@ -63,13 +63,15 @@ struct LoopBuffers {
     uint32_t* A;            // bit-packed assignment, ceil(n/32) words
     uint64_t* vmask;        // violated bitmask in evaluation order, n_tiles_padded * TILE_WORDS words
     uint32_t* tile_cnt;     // undecided violated entries per tile
-    uint32_t* stage;        // per tile: TILE slots of undecided violated clauses (evaluation
-                            // positions until LFMIS round 0 translates them to clause ids)
+    uint32_t* stage[2];     // per tile: TILE entries of undecided violated clauses, double
+                            // buffered across LFMIS rounds.  Entry = {id, K literals} (fixed
+                            // width K) or {id} (CSR); id = evaluation position until round 0
+                            // translates it to the clause id
     uint32_t* mis_cnt;      // MIS entries per tile (current iteration)
     uint32_t* mis;          // per tile: TILE slots of MIS clause ids
-    uint32_t* left;         // compact list of undecided clauses handed to the tail kernel
+    uint32_t* left;         // compact list of undecided entries handed to the tail kernel
     uint32_t* tmis;         // MIS clauses decided by the tail kernel
-    unsigned long long* owner; // per variable 64-bit owner key (epoch-tagged, never reset)
+    unsigned long long* owner; // 2 x n_vars 64-bit owner keys, array = epoch parity (never reset)
     uint32_t* cover;        // per variable: stamp of the iteration whose MIS covers it
     unsigned long long* tile_stats; // per tile: [2t] sum |MIS|, [2t+1] sum resampled literals
     uint32_t* delta;        // allreduce exchange: per-iteration assignment XOR delta

@@ -3,17 +3,16 @@
 // One iteration of SATInstance<T>::parallel_solve (reference SATInstance.h:260-311) is
 //   k_eval_*   clause evaluation (Clause.h:34-46) over the clause shard + violated-clause
 //              compaction (SATInstance.h:264-280) via wave ballots: writes the violated
-//              bitmask and per-tile lists of violated clause ids.
+//              bitmask and per-tile lists of violated-clause entries {id, literals}.
 //   k_collect  (multi-GPU) rebuilds the per-tile lists of the other shards from the
 //              all-gathered bitmask.
 //   k_reduce   violated count + termination test (check_if_noUNSAT, SATInstance.h:326-338)
 //              and the loop state update.
-//   k_claim / k_join (x R)  round-synchronous exact lexicographically-first MIS of the
-//              violated clauses in clause order (populate_mis_parallel with one set,
+//   k_claim0, k_round x G, k_tail   round-synchronous exact lexicographically-first MIS of
+//              the violated clauses in clause order (populate_mis_parallel with one set,
 //              SATInstance.h:391-451; dependency = shared variable, :369-389).
-//   k_tail     single-workgroup rounds until every violated clause is decided.
-//   k_resample Philox4x32-10 per-variable resampling of every MIS clause
-//              (resample_clauses, SATInstance.h:340-365).
+//   k_resample_vars  Philox4x32-10 resampling of every variable of every MIS clause
+//              (resample_clauses, SATInstance.h:340-365), one pass over the variables.
 // Integer / bit work only: no MFMA.  HBM-bound on the literal stream of k_eval.
 #include <algorithm>
 
@@ -76,12 +75,51 @@ __device__ __forceinline__ bool eval_gate_closed(const DevState* st) {
     return st->done != 0 || st->n_iter >= st->limit_eval;
 }
 
-// Number of literals / variables of clause c.
+// ------------------------------------------------------------------------------------
+// Violated-clause entries.  Fixed width K: {clause id, K literals} (K+1 words, so a round
+// kernel never re-reads the clause store); generic CSR (K = 0): {clause id}, literals from
+// the CSR arrays.  Literals keep the hot-variable flag (bit 31).
 template <int K>
-__device__ __forceinline__ void clause_range(const ClauseView& cv, uint32_t c, uint64_t& b, uint64_t& e) {
-    if constexpr (K > 0) { b = (uint64_t)c * K; e = b + K; }
-    else { b = cv.offs[c]; e = cv.offs[c + 1]; }
+struct Ent {
+    static constexpr int S = K > 0 ? K + 1 : 1;
+    uint32_t w[S];
+};
+
+template <int K>
+__device__ __forceinline__ void load_ent(Ent<K>& e, const uint32_t* p) {
+    if constexpr (K == 3) {
+        const uint4 x = *reinterpret_cast<const uint4*>(p);
+        e.w[0] = x.x; e.w[1] = x.y; e.w[2] = x.z; e.w[3] = x.w;
+    } else {
+#pragma unroll
+        for (int i = 0; i < Ent<K>::S; ++i) e.w[i] = p[i];
+    }
 }
+
+template <int K>
+__device__ __forceinline__ void store_ent(uint32_t* p, const Ent<K>& e) {
+    if constexpr (K == 3) {
+        *reinterpret_cast<uint4*>(p) = make_uint4(e.w[0], e.w[1], e.w[2], e.w[3]);
+    } else {
+#pragma unroll
+        for (int i = 0; i < Ent<K>::S; ++i) p[i] = e.w[i];
+    }
+}
+
+// Literal range of the entry's clause: fixed K -> the entry itself; CSR -> offsets.
+template <int K>
+__device__ __forceinline__ uint32_t ent_len(const ClauseView& cv, const Ent<K>& e, uint64_t& lb) {
+    if constexpr (K > 0) { lb = 0; return K; }
+    else { lb = cv.offs[e.w[0]]; return cv.offs[e.w[0] + 1] - (uint32_t)lb; }
+}
+
+template <int K>
+__device__ __forceinline__ uint32_t ent_lit(const ClauseView& cv, const Ent<K>& e, uint64_t lb, uint32_t j) {
+    if constexpr (K > 0) return e.w[1 + j];
+    else return cv.lits[lb + j];
+}
+
+__device__ __forceinline__ uint32_t lit_var(uint32_t raw) { return (raw & LIT_MASK) >> 1; }
 
 // ------------------------------------------------------------------------------------
 // Initial assignment: word w = Philox(seed, {w, 0, 0xFFFFFFFF, 0}).x (VariablesArray.h:23-34).
@@ -93,80 +131,88 @@ __global__ void k_init_assignment(uint32_t* A, uint32_t n_words, uint32_t n_vars
     A[w] = x;
 }
 
-// Common epilogue of eval / collect: per-wave LDS lists -> contiguous tile list.
-__device__ __forceinline__ void publish_tile(const LoopBuffers& b, uint32_t tile, uint32_t* s_idx,
-                                             uint32_t* s_wcnt, uint32_t wcount, int lane, int wave) {
-    if (lane == 0) s_wcnt[wave] = wcount;
-    __syncthreads();
-    uint32_t off = 0, tot = 0;
+// Writes the violated clauses of lane `lane` (four consecutive evaluation positions c0..c0+3,
+// literals x[j] component q) as entries into tile `tile`'s list at base + rank.
+template <int K>
+__device__ __forceinline__ void emit4(uint32_t* list, uint32_t pos, uint64_t c0, const bool v[4],
+                                      const uint4 (&x)[K]) {
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
-        const uint32_t cw = s_wcnt[w];
-        off += (w < wave) ? cw : 0u;
-        tot += cw;
-    }
-    uint32_t* dst = b.stage + (uint64_t)tile * TILE + off;
-    const uint32_t* src = s_idx + wave * (TILE / 4);
-    for (uint32_t i = lane; i < wcount; i += 64) dst[i] = src[i];
-    if (threadIdx.x == 0) {
-        b.tile_cnt[tile] = tot;
-        b.mis_cnt[tile] = 0;
+    for (int q = 0; q < 4; ++q) {
+        if (!v[q]) continue;
+        Ent<K> e;
+        e.w[0] = (uint32_t)(c0 + q);
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const uint32_t xs[4] = {x[j].x, x[j].y, x[j].z, x[j].w};
+            e.w[1 + j] = xs[q];
+        }
+        store_ent<K>(list + (uint64_t)pos * Ent<K>::S, e);
+        ++pos;
     }
 }
 
 // ------------------------------------------------------------------------------------
-// Clause evaluation, fixed width K, chunk-transposed literals: lane i of a wave evaluates
-// clauses 4i..4i+3 of a 256-clause chunk with one 16-byte load per literal slot
-// (1 KiB per wave-instruction).  4 chunks per wave, 16 per 256-thread workgroup (= TILE).
+// Clause evaluation, fixed width K, chunk-transposed literals, one tile per 256-thread
+// workgroup: lane i of a wave evaluates clauses 4i..4i+3 of a 256-clause chunk with one
+// 16-byte load per literal slot (1 KiB per wave-instruction); every lookup of the
+// assignment is an L2 gather.  (Alternative to k_eval_hybrid, ALLL_FLAG_NO_RANGED.)
 template <int K>
 __global__ __launch_bounds__(EVAL_THREADS) void k_eval_fixed(ClauseView cv, LoopBuffers b,
                                                              uint32_t tile_begin, int gated) {
     if (gated && eval_gate_closed(b.state)) return;
-    __shared__ uint32_t s_idx[TILE];
-    __shared__ uint32_t s_wcnt[4];
+    __shared__ uint32_t s_cnt;
     const uint32_t tile = tile_begin + blockIdx.x;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t m = cv.m;
     const uint32_t* __restrict__ A = b.A;
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-    uint32_t wcount = 0;
-#pragma unroll 2
+    uint32_t* list = b.stage[0] + (uint64_t)tile * TILE * Ent<K>::S;
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
     for (int s = 0; s < 4; ++s) {
         const uint64_t g = (uint64_t)tile * (TILE / CHUNK) + wave * 4 + s;
         const uint64_t cb = g * CHUNK;
-        uint32_t s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+        uint32_t sat[4] = {0u, 0u, 0u, 0u};
+        uint4 x[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) x[j] = make_uint4(0u, 0u, 0u, 0u);
         if (cb < m) {
             const uint4* src = reinterpret_cast<const uint4*>(cv.lits_t + cb * K) + lane;
 #pragma unroll
+            for (int j = 0; j < K; ++j) x[j] = src[j * 64];
+#pragma unroll
             for (int j = 0; j < K; ++j) {
-                const uint4 x = src[j * 64];
-                s0 |= abit(A, x.x >> 1) ^ (x.x & 1u);
-                s1 |= abit(A, x.y >> 1) ^ (x.y & 1u);
-                s2 |= abit(A, x.z >> 1) ^ (x.z & 1u);
-                s3 |= abit(A, x.w >> 1) ^ (x.w & 1u);
+                const uint32_t xs[4] = {x[j].x, x[j].y, x[j].z, x[j].w};
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t l = xs[q] & LIT_MASK;
+                    sat[q] |= abit(A, l >> 1) ^ (l & 1u);
+                }
             }
         }
         const uint64_t c0 = cb + 4u * lane;
-        const bool v0 = !s0 && c0 < m, v1 = !s1 && c0 + 1 < m;
-        const bool v2 = !s2 && c0 + 2 < m, v3 = !s3 && c0 + 3 < m;
-        const uint64_t b0 = __ballot(v0), b1 = __ballot(v1), b2 = __ballot(v2), b3 = __ballot(v3);
+        const bool v[4] = {!sat[0] && c0 < m, !sat[1] && c0 + 1 < m, !sat[2] && c0 + 2 < m,
+                           !sat[3] && c0 + 3 < m};
+        const uint64_t b0 = __ballot(v[0]), b1 = __ballot(v[1]), b2 = __ballot(v[2]), b3 = __ballot(v[3]);
         if (lane < 4) {
             const int sh = 16 * lane;
-            const uint64_t w = spread4(b0 >> sh) | (spread4(b1 >> sh) << 1) |
-                               (spread4(b2 >> sh) << 2) | (spread4(b3 >> sh) << 3);
-            b.vmask[g * 4 + lane] = w;
+            b.vmask[g * 4 + lane] = spread4(b0 >> sh) | (spread4(b1 >> sh) << 1) |
+                                    (spread4(b2 >> sh) << 2) | (spread4(b3 >> sh) << 3);
         }
-        const uint32_t pre = __popcll(b0 & lt) + __popcll(b1 & lt) + __popcll(b2 & lt) +
-                             __popcll(b3 & lt);
-        uint32_t* dst = s_idx + wave * (TILE / 4) + wcount + pre;
-        uint32_t q = 0;
-        if (v0) dst[q++] = (uint32_t)c0;
-        if (v1) dst[q++] = (uint32_t)(c0 + 1);
-        if (v2) dst[q++] = (uint32_t)(c0 + 2);
-        if (v3) dst[q++] = (uint32_t)(c0 + 3);
-        wcount += __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
+        const uint32_t tot = __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
+        if (tot) {
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(&s_cnt, tot);
+            base = __shfl(base, 0, 64);
+            const uint32_t pre = __popcll(b0 & lt) + __popcll(b1 & lt) + __popcll(b2 & lt) + __popcll(b3 & lt);
+            emit4<K>(list, base + pre, c0, v, x);
+        }
     }
-    publish_tile(b, tile, s_idx, s_wcnt, wcount, lane, wave);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        b.tile_cnt[tile] = s_cnt;
+        b.mis_cnt[tile] = 0;
+    }
 }
 
 // Clause evaluation, fixed width K, persistent hybrid (the loop's default for fixed k).
@@ -218,9 +264,11 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
         for (uint64_t g = gbeg + wave; g < gend; g += HYB_THREADS / 64) {
             const uint64_t cb = g * CHUNK;
             uint32_t sat[4] = {0u, 0u, 0u, 0u};
+            uint4 x[K];
+#pragma unroll
+            for (int j = 0; j < K; ++j) x[j] = make_uint4(0u, 0u, 0u, 0u);
             if (cb < m) {
                 const uint4* src = reinterpret_cast<const uint4*>(cv.lits_t + cb * K) + lane;
-                uint4 x[K];
 #pragma unroll
                 for (int j = 0; j < K; ++j) x[j] = src[j * 64];
 #pragma unroll
@@ -228,21 +276,20 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
                     const uint32_t xs[4] = {x[j].x, x[j].y, x[j].z, x[j].w};
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
-                        const uint32_t v = xs[q] >> 1;
+                        const uint32_t v = (xs[q] & LIT_MASK) >> 1;
                         const uint32_t w = (v < lds_vars) ? s_A[v >> 5] : A[v >> 5];
                         sat[q] |= ((w >> (v & 31u)) & 1u) ^ (xs[q] & 1u);
                     }
                 }
             }
             const uint64_t c0 = cb + 4u * lane;
-            const bool v0 = !sat[0] && c0 < m, v1 = !sat[1] && c0 + 1 < m;
-            const bool v2 = !sat[2] && c0 + 2 < m, v3 = !sat[3] && c0 + 3 < m;
-            const uint64_t b0 = __ballot(v0), b1 = __ballot(v1), b2 = __ballot(v2), b3 = __ballot(v3);
+            const bool v[4] = {!sat[0] && c0 < m, !sat[1] && c0 + 1 < m, !sat[2] && c0 + 2 < m,
+                               !sat[3] && c0 + 3 < m};
+            const uint64_t b0 = __ballot(v[0]), b1 = __ballot(v[1]), b2 = __ballot(v[2]), b3 = __ballot(v[3]);
             if (lane < 4) {
                 const int sh = 16 * lane;
-                const uint64_t w = spread4(b0 >> sh) | (spread4(b1 >> sh) << 1) |
-                                   (spread4(b2 >> sh) << 2) | (spread4(b3 >> sh) << 3);
-                b.vmask[g * 4 + lane] = w;
+                b.vmask[g * 4 + lane] = spread4(b0 >> sh) | (spread4(b1 >> sh) << 1) |
+                                        (spread4(b2 >> sh) << 2) | (spread4(b3 >> sh) << 3);
             }
             const uint32_t tot = __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
             if (tot) {
@@ -252,12 +299,7 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
                 base = __shfl(base, 0, 64);
                 const uint32_t pre = __popcll(b0 & lt) + __popcll(b1 & lt) + __popcll(b2 & lt) +
                                      __popcll(b3 & lt);
-                uint32_t* dst = b.stage + (uint64_t)tile * TILE + base + pre;
-                uint32_t q = 0;
-                if (v0) dst[q++] = (uint32_t)c0;
-                if (v1) dst[q++] = (uint32_t)(c0 + 1);
-                if (v2) dst[q++] = (uint32_t)(c0 + 2);
-                if (v3) dst[q++] = (uint32_t)(c0 + 3);
+                emit4<K>(b.stage[0] + (uint64_t)tile * TILE * Ent<K>::S, base + pre, c0, v, x);
             }
         }
         __syncthreads();
@@ -269,12 +311,11 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
 }
 
 // Clause evaluation, generic CSR (ragged widths): lane per clause, 64 consecutive
-// clauses per wave step, 16 steps per wave.
+// clauses per wave step, 16 steps per wave, one tile per workgroup.
 __global__ __launch_bounds__(EVAL_THREADS) void k_eval_csr(ClauseView cv, LoopBuffers b,
                                                            uint32_t tile_begin, int gated) {
     if (gated && eval_gate_closed(b.state)) return;
-    __shared__ uint32_t s_idx[TILE];
-    __shared__ uint32_t s_wcnt[4];
+    __shared__ uint32_t s_cnt;
     const uint32_t tile = tile_begin + blockIdx.x;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t m = cv.m;
@@ -282,8 +323,9 @@ __global__ __launch_bounds__(EVAL_THREADS) void k_eval_csr(ClauseView cv, LoopBu
     const uint32_t* __restrict__ offs = cv.offs;
     const uint32_t* __restrict__ lits = cv.lits;
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-    uint32_t wcount = 0;
-#pragma unroll 4
+    uint32_t* list = b.stage[0] + (uint64_t)tile * TILE;
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
     for (int s = 0; s < 16; ++s) {
         const uint64_t c = (uint64_t)tile * TILE + wave * (TILE / 4) + s * 64 + lane;
         bool viol = false;
@@ -298,33 +340,59 @@ __global__ __launch_bounds__(EVAL_THREADS) void k_eval_csr(ClauseView cv, LoopBu
         }
         const uint64_t mask = __ballot(viol);
         if (lane == 0) b.vmask[c >> 6] = mask;
-        if (viol) s_idx[wave * (TILE / 4) + wcount + __popcll(mask & lt)] = (uint32_t)c;
-        wcount += __popcll(mask);
+        if (mask) {
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(&s_cnt, (uint32_t)__popcll(mask));
+            base = __shfl(base, 0, 64);
+            if (viol) list[base + __popcll(mask & lt)] = (uint32_t)c;
+        }
     }
-    publish_tile(b, tile, s_idx, s_wcnt, wcount, lane, wave);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        b.tile_cnt[tile] = s_cnt;
+        b.mis_cnt[tile] = 0;
+    }
 }
 
 // Multi-GPU: tiles owned by other ranks get their violated lists from the all-gathered
-// bitmask (same order and format as k_eval_*).
+// bitmask (evaluation positions; fixed K fetches the literals from the transposed store).
+template <int K>
 __global__ __launch_bounds__(EVAL_THREADS) void k_collect(ClauseView cv, LoopBuffers b,
                                                           uint32_t own_begin, uint32_t own_end) {
     if (eval_gate_closed(b.state)) return;
     const uint32_t tile = blockIdx.x;
     if (tile >= own_begin && tile < own_end) return;
-    __shared__ uint32_t s_idx[TILE];
-    __shared__ uint32_t s_wcnt[4];
+    __shared__ uint32_t s_cnt;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     const uint64_t m = cv.m;
-    uint32_t wcount = 0;
+    uint32_t* list = b.stage[0] + (uint64_t)tile * TILE * Ent<K>::S;
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
     for (int s = 0; s < 16; ++s) {
         const uint64_t c = (uint64_t)tile * TILE + wave * (TILE / 4) + s * 64 + lane;
         const uint64_t mask = b.vmask[c >> 6];  // uniform load
         const bool viol = ((mask >> lane) & 1ull) && c < m;
-        if (viol) s_idx[wave * (TILE / 4) + wcount + __popcll(mask & lt)] = (uint32_t)c;
-        wcount += __popcll(mask);
+        if (!mask) continue;
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(&s_cnt, (uint32_t)__popcll(mask));
+        base = __shfl(base, 0, 64);
+        if (viol) {
+            Ent<K> e;
+            e.w[0] = (uint32_t)c;
+            if constexpr (K > 0) {
+                const uint32_t* t = cv.lits_t + (c / CHUNK) * CHUNK * K + (c % CHUNK);
+#pragma unroll
+                for (int j = 0; j < K; ++j) e.w[1 + j] = t[j * CHUNK];
+            }
+            store_ent<K>(list + (uint64_t)(base + __popcll(mask & lt)) * Ent<K>::S, e);
+        }
     }
-    publish_tile(b, tile, s_idx, s_wcnt, wcount, lane, wave);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        b.tile_cnt[tile] = s_cnt;
+        b.mis_cnt[tile] = 0;
+    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -352,133 +420,179 @@ __global__ __launch_bounds__(1024) void k_reduce(LoopBuffers b, int mode) {
     st->tmis_cnt = 0;
     st->stamp = (uint32_t)st->n_iter ? (uint32_t)st->n_iter : 1u;
     st->round_base = st->round_next;
+    st->round_next = st->round_base + 1;  // the tail advances it past every epoch it used
     if (u == 0) { st->done = 1; st->active = 0; }
     else if (st->n_iter >= st->limit_nores) { st->done = 2; st->active = 0; }
     else st->active = 1;
 }
 
 // ------------------------------------------------------------------------------------
-// LFMIS round r, phase CLAIM: every undecided violated clause first drops out if a
-// variable is covered by a clause that joined the MIS in an earlier round of this
-// iteration (it depends on an MIS clause), otherwise it claims each of its variables with
-// atomicMin(owner[v], key), key = (~epoch << 32) | clause: keys of later rounds/iterations
-// are always smaller than stale ones, so owner[] is never reset.
+// LFMIS (exact lexicographically-first MIS of the violated clauses in clause order).
+// Round r = CLAIM then JOIN, each its own kernel (the kernel boundary orders them):
+//   CLAIM(r): an undecided clause touching a variable covered by a clause that already
+//     joined in this iteration is out (it depends on an MIS clause); otherwise it claims each
+//     of its variables with atomicMin(owner[v], key_r(c)), key_r(c) = (~(round_base+r) << 32)
+//     | c, so keys of later rounds / iterations are always smaller than stale ones and
+//     owner[] is never reset.
+//   JOIN(r): a clause that holds every variable it claimed has no undecided lower-index
+//     neighbour, and every decided lower neighbour is out, so it is in the LFMIS: its
+//     variables are covered (cover[v] = stamp) and it leaves the list.
+// Lists are double buffered: each kernel reads one buffer and compacts the survivors into
+// the other.  Claims on hot variables (high-degree, flagged by the host) are reduced in an
+// LDS hash table first: one global atomic per hot variable per workgroup (power-law hubs).
+struct HotTable {
+    uint32_t* k;
+    unsigned long long* v;
+    __device__ void init() {
+        for (uint32_t i = threadIdx.x; i < HOT_SLOTS; i += blockDim.x) { k[i] = 0xFFFFFFFFu; v[i] = ~0ull; }
+    }
+    __device__ void claim(uint32_t var, unsigned long long key) {
+        uint32_t h = (var * 2654435761u) & (HOT_SLOTS - 1);
+        for (;;) {
+            const uint32_t prev = atomicCAS(&k[h], 0xFFFFFFFFu, var);
+            if (prev == 0xFFFFFFFFu || prev == var) break;
+            h = (h + 1) & (HOT_SLOTS - 1);
+        }
+        atomicMin(&v[h], key);
+    }
+    __device__ void flush(unsigned long long* owner) {
+        for (uint32_t i = threadIdx.x; i < HOT_SLOTS; i += blockDim.x)
+            if (k[i] != 0xFFFFFFFFu) atomicMin(&owner[k[i]], v[i]);
+    }
+};
+
+// Claims of epoch e go to owner array e & 1 (kept separate so that a future fused
+// join(r)+claim(r+1) kernel never reads an array it writes).
+__device__ __forceinline__ unsigned long long* owner_of(const LoopBuffers& b, uint32_t epoch) {
+    return b.owner + (uint64_t)(epoch & 1u) * b.n_vars;
+}
+
 template <int K>
-__global__ __launch_bounds__(ROUND_THREADS) void k_claim(ClauseView cv, LoopBuffers b, uint32_t r) {
+__device__ __forceinline__ void claim_all(const ClauseView& cv, const Ent<K>& e, uint64_t lb, uint32_t len,
+                                          unsigned long long key, unsigned long long* owner, HotTable& ht,
+                                          bool hot) {
+    for (uint32_t j = 0; j < len; ++j) {
+        const uint32_t raw = ent_lit<K>(cv, e, lb, j);
+        if (hot && (raw & LIT_HOT)) ht.claim(lit_var(raw), key);
+        else atomicMin(&owner[lit_var(raw)], key);
+    }
+}
+
+// CLAIM(r).  r == 0: every violated clause claims, in place (evaluation positions become
+// clause ids here).  r > 0: kill test, claim, survivors compacted from `in` to `out`.
+template <int K>
+__global__ __launch_bounds__(ROUND_THREADS) void k_claim(ClauseView cv, LoopBuffers b, uint32_t r,
+                                                         uint32_t* in, uint32_t* out) {
     const DevState* st = b.state;
     if (!st->active) return;
     const uint32_t tile = blockIdx.x;
     const uint32_t cnt = b.tile_cnt[tile];
     if (cnt == 0) return;
-    const uint32_t stamp = st->stamp;
-    const unsigned long long keyhi = (unsigned long long)(~(st->round_base + r)) << 32;
-    __shared__ uint32_t s_e[TILE];
-    __shared__ uint32_t s_wp;
-    // claims on hot variables are first reduced in an LDS hash table (one global atomic per
-    // hot variable per block instead of one per clause: power-law hubs)
+    constexpr int S = Ent<K>::S;
     __shared__ uint32_t s_hk[HOT_SLOTS];
     __shared__ unsigned long long s_hv[HOT_SLOTS];
+    __shared__ uint32_t s_keep;
+    HotTable ht{s_hk, s_hv};
     const bool hot = cv.n_hot != 0;
-    uint32_t* list = b.stage + (uint64_t)tile * TILE;
-    for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) s_e[i] = list[i];
-    if (hot)
-        for (uint32_t i = threadIdx.x; i < HOT_SLOTS; i += blockDim.x) { s_hk[i] = 0xFFFFFFFFu; s_hv[i] = ~0ull; }
-    if (threadIdx.x == 0) s_wp = 0;
+    if (hot) ht.init();
+    if (threadIdx.x == 0) s_keep = 0;
     __syncthreads();
-    const bool translate = (r == 0) && cv.perm != nullptr;
+    const uint32_t stamp = st->stamp;
+    const unsigned long long keyhi = (unsigned long long)(~(st->round_base + r)) << 32;
+    unsigned long long* owner = owner_of(b, st->round_base + r);
+    uint32_t* lin = in + (uint64_t)tile * TILE * S;
+    uint32_t* lout = out + (uint64_t)tile * TILE * S;
     for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
-        const uint32_t c = translate ? cv.perm[s_e[i]] : s_e[i];
-        uint64_t lb, le;
-        clause_range<K>(cv, c, lb, le);
-        bool killed = false;
-        if (r > 0)
-            for (uint64_t j = lb; j < le; ++j) killed |= (b.cover[lvar(cv, j)] == stamp);
-        if (!killed) {
-            const unsigned long long key = keyhi | c;
-            for (uint64_t j = lb; j < le; ++j) {
-                const uint32_t raw = cv.lits[j];
-                const uint32_t v = (raw & LIT_MASK) >> 1;
-                if (raw & LIT_HOT) {
-                    uint32_t h = (v * 2654435761u) & (HOT_SLOTS - 1);
-                    for (;;) {
-                        const uint32_t prev = atomicCAS(&s_hk[h], 0xFFFFFFFFu, v);
-                        if (prev == 0xFFFFFFFFu || prev == v) break;
-                        h = (h + 1) & (HOT_SLOTS - 1);
-                    }
-                    atomicMin(&s_hv[h], key);
-                } else {
-                    atomicMin(&b.owner[v], key);
-                }
-            }
-            list[atomicAdd(&s_wp, 1u)] = c;
+        Ent<K> e;
+        load_ent<K>(e, lin + (uint64_t)i * S);
+        if (r == 0 && cv.perm) {
+            e.w[0] = cv.perm[e.w[0]];
+            lin[(uint64_t)i * S] = e.w[0];
         }
+        uint64_t lb;
+        const uint32_t len = ent_len<K>(cv, e, lb);
+        if (r > 0) {
+            bool killed = false;
+            for (uint32_t j = 0; j < len; ++j) killed |= b.cover[lit_var(ent_lit<K>(cv, e, lb, j))] == stamp;
+            if (killed) continue;
+        }
+        claim_all<K>(cv, e, lb, len, keyhi | e.w[0], owner, ht, hot);
+        if (r > 0) store_ent<K>(lout + (uint64_t)atomicAdd(&s_keep, 1u) * S, e);
     }
     __syncthreads();
-    if (hot)
-        for (uint32_t i = threadIdx.x; i < HOT_SLOTS; i += blockDim.x)
-            if (s_hk[i] != 0xFFFFFFFFu) atomicMin(&b.owner[s_hk[i]], s_hv[i]);
-    if (threadIdx.x == 0) b.tile_cnt[tile] = s_wp;
+    if (hot) ht.flush(owner);
+    if (r > 0 && threadIdx.x == 0) b.tile_cnt[tile] = s_keep;
 }
 
-// Phase JOIN: a clause that owns all of its variables has no undecided lower-index
-// neighbour, and every decided lower neighbour is out, so it is in the LFMIS: mark its
-// variables covered and append it to the tile's MIS list.  In the last grid round the
-// still-undecided clauses move to one compact list for the tail kernel.
+// JOIN(r): survivors compacted from `in` to `out`; in the last grid round they go to the
+// tail kernel's compact list instead.
 template <int K>
-__global__ __launch_bounds__(ROUND_THREADS) void k_join(ClauseView cv, LoopBuffers b, uint32_t r, int last) {
+__global__ __launch_bounds__(ROUND_THREADS) void k_join(ClauseView cv, LoopBuffers b, uint32_t r,
+                                                        const uint32_t* __restrict__ in, uint32_t* out,
+                                                        int last) {
     DevState* st = b.state;
     if (!st->active) return;
     const uint32_t tile = blockIdx.x;
     const uint32_t cnt = b.tile_cnt[tile];
     if (cnt == 0) return;
+    constexpr int S = Ent<K>::S;
     const uint32_t stamp = st->stamp;
     const unsigned long long keyhi = (unsigned long long)(~(st->round_base + r)) << 32;
-    __shared__ uint32_t s_e[TILE];
-    __shared__ uint32_t s_keep[TILE];
-    __shared__ uint32_t s_wp, s_mp, s_base;
-    uint32_t* list = b.stage + (uint64_t)tile * TILE;
-    uint32_t* mis = b.mis + (uint64_t)tile * TILE + b.mis_cnt[tile];
-    for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) s_e[i] = list[i];
-    if (threadIdx.x == 0) { s_wp = 0; s_mp = 0; }
+    const unsigned long long* owner = owner_of(b, st->round_base + r);
+    __shared__ uint32_t s_keep, s_join, s_base;
+    __shared__ unsigned long long s_lits;
+    if (threadIdx.x == 0) { s_keep = 0; s_join = 0; s_lits = 0; }
     __syncthreads();
+    const uint32_t* lin = in + (uint64_t)tile * TILE * S;
+    uint32_t* lout = out + (uint64_t)tile * TILE * S;
+    uint32_t* mis = b.mis + (uint64_t)tile * TILE + b.mis_cnt[tile];
+    unsigned long long my_lits = 0;
     for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
-        const uint32_t c = s_e[i];
-        uint64_t lb, le;
-        clause_range<K>(cv, c, lb, le);
-        const unsigned long long key = keyhi | c;
+        Ent<K> e;
+        load_ent<K>(e, lin + (uint64_t)i * S);
+        const uint32_t c = e.w[0];
+        uint64_t lb;
+        const uint32_t len = ent_len<K>(cv, e, lb);
         bool own = true;
-        for (uint64_t j = lb; j < le; ++j) own &= (b.owner[lvar(cv, j)] == key);
+        for (uint32_t j = 0; j < len; ++j) own &= owner[lit_var(ent_lit<K>(cv, e, lb, j))] == (keyhi | c);
         if (own) {
-            for (uint64_t j = lb; j < le; ++j) b.cover[lvar(cv, j)] = stamp;
-            mis[atomicAdd(&s_mp, 1u)] = c;
+            for (uint32_t j = 0; j < len; ++j) b.cover[lit_var(ent_lit<K>(cv, e, lb, j))] = stamp;
+            mis[atomicAdd(&s_join, 1u)] = c;
+            my_lits += len;
         } else {
-            s_keep[atomicAdd(&s_wp, 1u)] = c;
+            store_ent<K>(lout + (uint64_t)atomicAdd(&s_keep, 1u) * S, e);
         }
     }
+    for (int o = 32; o > 0; o >>= 1) my_lits += __shfl_down(my_lits, o, 64);
+    if ((threadIdx.x & 63) == 0 && my_lits) atomicAdd(&s_lits, my_lits);
     __syncthreads();
-    const uint32_t kept = s_wp;
-    uint32_t* dst = list;
+    const uint32_t kept = s_keep;
     if (last && kept) {
         if (threadIdx.x == 0) s_base = atomicAdd(&st->left_cnt, kept);
         __syncthreads();
-        dst = b.left + s_base;
+        uint32_t* dst = b.left + (uint64_t)s_base * S;
+        for (uint32_t i = threadIdx.x; i < kept * S; i += blockDim.x) dst[i] = lout[i];
     }
-    for (uint32_t i = threadIdx.x; i < kept; i += blockDim.x) dst[i] = s_keep[i];
     if (threadIdx.x == 0) {
         b.tile_cnt[tile] = last ? 0u : kept;
-        b.mis_cnt[tile] += s_mp;
+        b.mis_cnt[tile] += s_join;
+        if (s_join) {
+            atomicAdd(&b.tile_stats[2 * tile], (unsigned long long)s_join);
+            atomicAdd(&b.tile_stats[2 * tile + 1], s_lits);
+        }
     }
 }
 
 // Tail: one workgroup finishes the LFMIS over the compact list handed over by the last grid
-// round (rounds until no undecided clause is left).  Entries are processed in chunks of one
-// per thread; survivors are compacted in place (a write position never passes the chunk being
-// read).  owner / cover are accessed with agent-scope relaxed atomics so no stale L1 line is
-// read across the barriers.
+// round (CLAIM / barrier / JOIN passes until no undecided clause is left).  Entries are
+// processed in chunks of one per thread; survivors are compacted in place (a write position
+// never passes the chunk being read).  owner / cover are accessed with agent-scope relaxed
+// atomics so no stale L1 line is read across the barriers.
 template <int K>
 __global__ __launch_bounds__(TAIL_THREADS) void k_tail(ClauseView cv, LoopBuffers b, uint32_t first_round) {
     DevState* st = b.state;
     if (!st->active) return;
+    constexpr int S = Ent<K>::S;
     const uint32_t stamp = st->stamp;
     __shared__ uint32_t s_wp, s_tm;
     uint32_t n = st->left_cnt;
@@ -488,24 +602,26 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail(ClauseView cv, LoopBuffer
     uint32_t* left = b.left;
     while (n > 0) {
         const unsigned long long keyhi = (unsigned long long)(~epoch) << 32;
+        unsigned long long* owner = owner_of(b, epoch);
         // CLAIM (with the kill test)
         if (threadIdx.x == 0) s_wp = 0;
         __syncthreads();
         for (uint32_t base = 0; base < n; base += blockDim.x) {
             const uint32_t i = base + threadIdx.x;
-            const uint32_t c = (i < n) ? left[i] : 0u;
+            Ent<K> e;
+            if (i < n) load_ent<K>(e, left + (uint64_t)i * S);
             __syncthreads();
             if (i < n) {
-                uint64_t lb, le;
-                clause_range<K>(cv, c, lb, le);
+                uint64_t lb;
+                const uint32_t len = ent_len<K>(cv, e, lb);
                 bool killed = false;
-                for (uint64_t j = lb; j < le; ++j)
-                    killed |= (__hip_atomic_load(&b.cover[lvar(cv, j)], __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT) == stamp);
+                for (uint32_t j = 0; j < len; ++j)
+                    killed |= __hip_atomic_load(&b.cover[lit_var(ent_lit<K>(cv, e, lb, j))], __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT) == stamp;
                 if (!killed) {
-                    const unsigned long long key = keyhi | c;
-                    for (uint64_t j = lb; j < le; ++j) atomicMin(&b.owner[lvar(cv, j)], key);
-                    left[atomicAdd(&s_wp, 1u)] = c;
+                    for (uint32_t j = 0; j < len; ++j)
+                        atomicMin(&owner[lit_var(ent_lit<K>(cv, e, lb, j))], keyhi | e.w[0]);
+                    store_ent<K>(left + (uint64_t)atomicAdd(&s_wp, 1u) * S, e);
                 }
             }
         }
@@ -517,23 +633,26 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail(ClauseView cv, LoopBuffer
         __syncthreads();
         for (uint32_t base = 0; base < n; base += blockDim.x) {
             const uint32_t i = base + threadIdx.x;
-            const uint32_t c = (i < n) ? left[i] : 0u;
+            Ent<K> e;
+            if (i < n) load_ent<K>(e, left + (uint64_t)i * S);
             __syncthreads();
             if (i < n) {
-                uint64_t lb, le;
-                clause_range<K>(cv, c, lb, le);
-                const unsigned long long key = keyhi | c;
+                const uint32_t c = e.w[0];
+                uint64_t lb;
+                const uint32_t len = ent_len<K>(cv, e, lb);
                 bool own = true;
-                for (uint64_t j = lb; j < le; ++j)
-                    own &= (__hip_atomic_load(&b.owner[lvar(cv, j)], __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT) == key);
+                for (uint32_t j = 0; j < len; ++j)
+                    own &= __hip_atomic_load(&owner[lit_var(ent_lit<K>(cv, e, lb, j))], __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT) == (keyhi | c);
                 if (own) {
-                    for (uint64_t j = lb; j < le; ++j)
-                        __hip_atomic_store(&b.cover[lvar(cv, j)], stamp, __ATOMIC_RELAXED,
+                    for (uint32_t j = 0; j < len; ++j)
+                        __hip_atomic_store(&b.cover[lit_var(ent_lit<K>(cv, e, lb, j))], stamp, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
                     b.tmis[atomicAdd(&s_tm, 1u)] = c;
+                    atomicAdd(&b.tile_stats[2 * (c / TILE)], 1ull);
+                    atomicAdd(&b.tile_stats[2 * (c / TILE) + 1], (unsigned long long)len);
                 } else {
-                    left[atomicAdd(&s_wp, 1u)] = c;
+                    store_ent<K>(left + (uint64_t)atomicAdd(&s_wp, 1u) * S, e);
                 }
             }
         }
@@ -549,7 +668,7 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail(ClauseView cv, LoopBuffer
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        st->round_next = epoch;
+        if (epoch > st->round_next) st->round_next = epoch;
         st->tail_rounds = rounds;
         st->tmis_cnt = s_tm;
         const uint32_t total = first_round + rounds;
@@ -558,69 +677,75 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail(ClauseView cv, LoopBuffer
 }
 
 // ------------------------------------------------------------------------------------
-// Resample: every variable of every MIS clause gets Philox(seed, {v, it_lo, 0, it_hi}).x & 1
-// with it = resample round (n_iter - 1).  A violated clause has every literal false, so the
-// old value of v is l & 1 and only differing bits are flipped (atomicXor; MIS clauses are
-// variable-disjoint).  A variable repeated inside one clause is applied once (its draws
-// are equal anyway); n_resamples still counts every literal (SATInstance.h:363).
-template <int K>
-__device__ __forceinline__ uint64_t resample_clause(const ClauseView& cv, uint32_t* target, uint32_t c,
-                                                    uint64_t it, uint32_t k0, uint32_t k1, bool apply) {
-    uint64_t lb, le;
-    clause_range<K>(cv, c, lb, le);
-    if (apply) {
-        for (uint64_t j = lb; j < le; ++j) {
-            const uint32_t l = cv.lits[j] & LIT_MASK, v = l >> 1;
-            bool dup = false;
-            for (uint64_t q = lb; q < j; ++q) dup |= (lvar(cv, q) == v);
-            if (dup) continue;
-            const uint32_t nb = philox_x(v, (uint32_t)it, 0u, (uint32_t)(it >> 32), k0, k1) & 1u;
-            if (nb != (l & 1u)) atomicXor(&target[v >> 5], 1u << (v & 31u));
+// Resample (resample_clauses, SATInstance.h:340-365): the variables of the MIS clauses are
+// exactly those with cover[v] == stamp, so one pass over the variables gives each of them
+// Philox(seed, {v, it_lo, 0, it_hi}).x & 1 (it = resample round n_iter - 1) with plain word
+// stores: no per-clause atomics, a variable repeated inside a clause is drawn once (its
+// draws are equal anyway).  n_resamples counts every literal (SATInstance.h:363) in k_round.
+__global__ __launch_bounds__(256) void k_resample_vars(LoopBuffers b) {
+    const DevState* st = b.state;
+    if (!st->active) return;
+    const uint32_t stamp = st->stamp;
+    const uint64_t it = st->n_iter - 1;
+    const uint32_t k0 = (uint32_t)b.seed, k1 = (uint32_t)(b.seed >> 32);
+    const int lane = threadIdx.x & 63;
+    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v - lane < b.n_vars;
+         v += (uint64_t)gridDim.x * blockDim.x) {
+        const bool cov = v < b.n_vars && b.cover[v] == stamp;
+        uint32_t nb = 0;
+        if (cov) nb = philox_x((uint32_t)v, (uint32_t)it, 0u, (uint32_t)(it >> 32), k0, k1) & 1u;
+        const uint64_t mc = __ballot(cov), mb = __ballot(nb != 0);
+        if ((lane & 31) == 0 && v < b.n_vars) {
+            const int sh = lane;  // 0 or 32
+            const uint32_t cm = (uint32_t)(mc >> sh), bm = (uint32_t)(mb >> sh);
+            if (cm) {
+                uint32_t* w = &b.A[v >> 5];
+                *w = (*w & ~cm) | bm;
+            }
         }
     }
-    return le - lb;
+}
+
+// Allreduce exchange (ALLL_FLAG_EXCHANGE_ALLREDUCE): each rank resamples only the MIS clauses
+// of its own shard into the XOR delta (old value of v is l & 1 because the clause is
+// violated; MIS clauses are variable-disjoint); the delta is summed over ranks.
+template <int K>
+__device__ __forceinline__ void delta_clause(const ClauseView& cv, uint32_t* delta, uint32_t c, uint64_t it,
+                                             uint32_t k0, uint32_t k1) {
+    uint64_t lb, le;
+    if constexpr (K > 0) { lb = (uint64_t)c * K; le = lb + K; }
+    else { lb = cv.offs[c]; le = cv.offs[c + 1]; }
+    for (uint64_t j = lb; j < le; ++j) {
+        const uint32_t l = cv.lits[j] & LIT_MASK, v = l >> 1;
+        bool dup = false;
+        for (uint64_t q = lb; q < j; ++q) dup |= (lvar(cv, q) == v);
+        if (dup) continue;
+        const uint32_t nb = philox_x(v, (uint32_t)it, 0u, (uint32_t)(it >> 32), k0, k1) & 1u;
+        if (nb != (l & 1u)) atomicXor(&delta[v >> 5], 1u << (v & 31u));
+    }
 }
 
 template <int K>
-__global__ __launch_bounds__(ROUND_THREADS) void k_resample(ClauseView cv, LoopBuffers b,
-                                                            uint32_t own_begin, uint32_t own_end,
-                                                            int to_delta) {
+__global__ __launch_bounds__(ROUND_THREADS) void k_resample_delta(ClauseView cv, LoopBuffers b,
+                                                                  uint32_t own_begin, uint32_t own_end) {
     const DevState* st = b.state;
     if (!st->active) return;
-    const uint32_t tile = blockIdx.x;
     const uint64_t it = st->n_iter - 1;
     const uint32_t k0 = (uint32_t)b.seed, k1 = (uint32_t)(b.seed >> 32);
-    uint32_t* target = to_delta ? b.delta : b.A;
+    const uint32_t tile = blockIdx.x;
     if (tile == b.n_tiles) {
-        // MIS clauses decided by the tail kernel (few): per-clause statistics to their tile
         const uint32_t cnt = st->tmis_cnt;
         for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
             const uint32_t c = b.tmis[i];
             const uint32_t t = c / TILE;
-            const bool apply = !to_delta || (t >= own_begin && t < own_end);
-            const uint64_t len = resample_clause<K>(cv, target, c, it, k0, k1, apply);
-            atomicAdd(&b.tile_stats[2 * t], 1ull);
-            atomicAdd(&b.tile_stats[2 * t + 1], (unsigned long long)len);
+            if (t >= own_begin && t < own_end) delta_clause<K>(cv, b.delta, c, it, k0, k1);
         }
         return;
     }
+    if (tile < own_begin || tile >= own_end) return;
     const uint32_t cnt = b.mis_cnt[tile];
-    if (cnt == 0) return;
-    const bool apply = !to_delta || (tile >= own_begin && tile < own_end);
-    __shared__ unsigned long long s_res;
-    if (threadIdx.x == 0) s_res = 0;
-    __syncthreads();
     const uint32_t* mis = b.mis + (uint64_t)tile * TILE;
-    unsigned long long res = 0;
-    for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x)
-        res += resample_clause<K>(cv, target, mis[i], it, k0, k1, apply);
-    for (int o = 32; o > 0; o >>= 1) res += __shfl_down(res, o, 64);
-    if ((threadIdx.x & 63) == 0) atomicAdd(&s_res, res);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        atomicAdd(&b.tile_stats[2 * tile], (unsigned long long)cnt);
-        atomicAdd(&b.tile_stats[2 * tile + 1], s_res);
-    }
+    for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) delta_clause<K>(cv, b.delta, mis[i], it, k0, k1);
 }
 
 __global__ void k_apply_delta(LoopBuffers b) {
@@ -644,16 +769,10 @@ hipError_t launch_eval(const ClauseView& cv, const LoopBuffers& b, uint32_t tile
     if (tile_end <= tile_begin) return hipSuccess;
     const dim3 grid(tile_end - tile_begin);
     const int g = gated ? 1 : 0;
-    switch (cv.k) {
-        case 1: k_eval_fixed<1><<<grid, EVAL_THREADS, 0, s>>>(cv, b, tile_begin, g); break;
-        case 2: k_eval_fixed<2><<<grid, EVAL_THREADS, 0, s>>>(cv, b, tile_begin, g); break;
-        case 3: k_eval_fixed<3><<<grid, EVAL_THREADS, 0, s>>>(cv, b, tile_begin, g); break;
-        case 4: k_eval_fixed<4><<<grid, EVAL_THREADS, 0, s>>>(cv, b, tile_begin, g); break;
-        case 5: k_eval_fixed<5><<<grid, EVAL_THREADS, 0, s>>>(cv, b, tile_begin, g); break;
-        case 6: k_eval_fixed<6><<<grid, EVAL_THREADS, 0, s>>>(cv, b, tile_begin, g); break;
-        case 7: k_eval_fixed<7><<<grid, EVAL_THREADS, 0, s>>>(cv, b, tile_begin, g); break;
-        case 8: k_eval_fixed<8><<<grid, EVAL_THREADS, 0, s>>>(cv, b, tile_begin, g); break;
-        default: k_eval_csr<<<grid, EVAL_THREADS, 0, s>>>(cv, b, tile_begin, g); break;
+    if (cv.k == 0) {
+        k_eval_csr<<<grid, EVAL_THREADS, 0, s>>>(cv, b, tile_begin, g);
+    } else {
+        ALLL_DISPATCH_K(cv.k, (k_eval_fixed<(K > 0 ? K : 1)><<<grid, EVAL_THREADS, 0, s>>>(cv, b, tile_begin, g)));
     }
     return hipGetLastError();
 }
@@ -691,7 +810,7 @@ hipError_t launch_eval_hybrid(const ClauseView& cv, const LoopBuffers& b, uint32
 hipError_t launch_collect(const ClauseView& cv, const LoopBuffers& b, uint32_t own_begin,
                           uint32_t own_end, hipStream_t s) {
     if (b.n_tiles == 0) return hipSuccess;
-    k_collect<<<b.n_tiles, EVAL_THREADS, 0, s>>>(cv, b, own_begin, own_end);
+    ALLL_DISPATCH_K(cv.k, (k_collect<K><<<b.n_tiles, EVAL_THREADS, 0, s>>>(cv, b, own_begin, own_end)));
     return hipGetLastError();
 }
 
@@ -700,15 +819,18 @@ hipError_t launch_reduce(const LoopBuffers& b, int mode, hipStream_t s) {
     return hipGetLastError();
 }
 
-
 hipError_t launch_round(const ClauseView& cv, const LoopBuffers& b, uint32_t r, bool last,
                         hipStream_t s) {
+    // buffers: eval -> stage[0]; CLAIM(0) in place; JOIN(r) stage[0] -> stage[1];
+    // CLAIM(r>0) stage[1] -> stage[0]
     if (b.n_tiles == 0) return hipSuccess;
-    ALLL_DISPATCH_K(cv.k, (k_claim<K><<<b.n_tiles, ROUND_THREADS, 0, s>>>(cv, b, r)));
+    uint32_t* s0 = b.stage[0];
+    uint32_t* s1 = b.stage[1];
+    ALLL_DISPATCH_K(cv.k, (k_claim<K><<<b.n_tiles, ROUND_THREADS, 0, s>>>(cv, b, r, r == 0 ? s0 : s1, s0)));
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const int l = last ? 1 : 0;
-    ALLL_DISPATCH_K(cv.k, (k_join<K><<<b.n_tiles, ROUND_THREADS, 0, s>>>(cv, b, r, l)));
+    ALLL_DISPATCH_K(cv.k, (k_join<K><<<b.n_tiles, ROUND_THREADS, 0, s>>>(cv, b, r, s0, s1, l)));
     return hipGetLastError();
 }
 
@@ -719,9 +841,14 @@ hipError_t launch_tail(const ClauseView& cv, const LoopBuffers& b, uint32_t firs
 
 hipError_t launch_resample(const ClauseView& cv, const LoopBuffers& b, uint32_t own_begin,
                            uint32_t own_end, bool to_delta, hipStream_t s) {
-    if (b.n_tiles == 0) return hipSuccess;
-    const int td = to_delta ? 1 : 0;
-    ALLL_DISPATCH_K(cv.k, (k_resample<K><<<b.n_tiles + 1, ROUND_THREADS, 0, s>>>(cv, b, own_begin, own_end, td)));
+    if (to_delta) {
+        if (b.n_tiles == 0) return hipSuccess;
+        ALLL_DISPATCH_K(cv.k, (k_resample_delta<K><<<b.n_tiles + 1, ROUND_THREADS, 0, s>>>(cv, b, own_begin, own_end)));
+        return hipGetLastError();
+    }
+    if (b.n_vars == 0) return hipSuccess;
+    const uint32_t blocks = std::min<uint32_t>((b.n_vars + 255) / 256, 4096);
+    k_resample_vars<<<blocks, 256, 0, s>>>(b);
     return hipGetLastError();
 }
 

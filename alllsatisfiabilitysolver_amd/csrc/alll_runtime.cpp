@@ -370,11 +370,13 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     if ((rc = dalloc(c, &b.vmask, (size_t)c->n_tiles_padded * TILE_WORDS))) return bail(rc);
     if ((rc = dalloc(c, &b.tile_cnt, n_tiles))) return bail(rc);
     if ((rc = dalloc(c, &b.mis_cnt, n_tiles))) return bail(rc);
-    if ((rc = dalloc(c, &b.stage, (size_t)n_tiles * TILE))) return bail(rc);
+    const size_t ent_words = (fixed_k > 0 ? (size_t)fixed_k + 1 : 1);
+    if ((rc = dalloc(c, &b.stage[0], (size_t)n_tiles * TILE * ent_words))) return bail(rc);
+    if ((rc = dalloc(c, &b.stage[1], (size_t)n_tiles * TILE * ent_words))) return bail(rc);
     if ((rc = dalloc(c, &b.mis, (size_t)n_tiles * TILE))) return bail(rc);
-    if ((rc = dalloc(c, &b.left, (size_t)n_tiles * TILE))) return bail(rc);
+    if ((rc = dalloc(c, &b.left, (size_t)n_tiles * TILE * ent_words))) return bail(rc);
     if ((rc = dalloc(c, &b.tmis, (size_t)n_tiles * TILE))) return bail(rc);
-    if ((rc = dalloc(c, &b.owner, c->n_vars, 0xFF))) return bail(rc);
+    if ((rc = dalloc(c, &b.owner, 2 * (size_t)c->n_vars, 0xFF))) return bail(rc);
     if ((rc = dalloc(c, &b.cover, c->n_vars))) return bail(rc);
     if ((rc = dalloc(c, &b.tile_stats, 2 * (size_t)n_tiles))) return bail(rc);
     if ((rc = dalloc(c, &b.delta, b.n_words))) return bail(rc);
@@ -394,9 +396,10 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     if (hipStreamSynchronize(c->stream) != hipSuccess) return bail(fail(ALLL_ERR_HIP, "memset drain failed"));
 
     // ---- clauses: AoS literals (+ offsets or a chunk-transposed copy for fixed width k)
+    // hot variables: degree >= max(1024, 32 x mean degree), at most HOT_MAX of the highest;
+    // flagged in bit 31 of every literal copy the device uses
+    std::vector<uint32_t> flagged;
     {
-        // hot variables: degree >= max(1024, 32 x mean degree), at most HOT_MAX of the highest
-        std::vector<uint32_t> flagged;
         if (L && c->n_vars && c->n_vars < (1u << 30)) {
             std::vector<uint32_t> deg(c->n_vars, 0u);
             for (uint64_t j = 0; j < L; ++j) ++deg[prob->literals[j] >> 1];
@@ -457,7 +460,8 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
         std::vector<uint32_t> tmp(fixed_k);
         for (uint64_t p2 = 0; p2 < m; ++p2) {
             const uint64_t cl = perm[p2];
-            for (int j = 0; j < fixed_k; ++j) tmp[j] = prob->literals[cl * fixed_k + j];
+            for (int j = 0; j < fixed_k; ++j)
+                tmp[j] = flagged.empty() ? prob->literals[cl * fixed_k + j] : flagged[cl * fixed_k + j];
             std::sort(tmp.begin(), tmp.end(), [](uint32_t x, uint32_t y) { return (x >> 1) > (y >> 1); });
             const uint64_t g = p2 / CHUNK, r = p2 % CHUNK;
             for (int j = 0; j < fixed_k; ++j) t[(g * fixed_k + j) * CHUNK + r] = tmp[j];

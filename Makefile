@@ -30,7 +30,7 @@ $(LIB): $(OBJS)
 cli: tools/alll_main
 
 tools/alll_main: tools/alll_main.cpp $(LIB) include/alll_compat/SATInstance.h
-	g++ -O2 -std=c++17 -Iinclude/alll_compat -Iinclude -o $@ tools/alll_main.cpp \
+	g++ -O2 -std=c++17 -fopenmp -Iinclude/alll_compat -Iinclude -o $@ tools/alll_main.cpp \
 	    -L$(PKG) -lalll -Wl,-rpath,'$$ORIGIN/../$(PKG)'
 
 oracle:

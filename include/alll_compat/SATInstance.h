@@ -13,6 +13,8 @@
 #include <string>
 #include <vector>
 
+#include <omp.h>  // main.cpp calls omp_get_num_procs() through this header
+
 #include "Clause.h"
 #include "RandomBoolGenerator.h"
 #include "VariablesArray.h"

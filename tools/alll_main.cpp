@@ -50,7 +50,7 @@ int main(int argc, char* argv[]) {
     int n_threads = 1;
     bool dump = false;
     string cnf_fpath;
-    const int procs = (int)std::thread::hardware_concurrency();
+    const int procs = omp_get_num_procs();  // main.cpp:77
     for (int i = 1; i < argc; ++i) {
         string a = argv[i];
         auto need = [&](const char* what) -> string {

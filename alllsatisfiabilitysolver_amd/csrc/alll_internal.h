@@ -27,6 +27,11 @@ constexpr uint32_t RANGED_MAX_TILES = 16;          // tiles per block pass (64-b
 // Every LFMIS round decides at least the lowest undecided clause, so rounds <= |U|; the cap
 // only bounds a kernel that would otherwise run away on a bug or an adversarial chain.
 constexpr uint32_t MAX_TAIL_ROUNDS = 1u << 20;
+// In-loop kernel timing (ALLL_FLAG_KERNEL_TIMING): per iteration i, slot i % TIME_SLOTS holds
+// device wall-clock stamps (s_memrealtime) {eval start (min over workgroups), eval end (max),
+// reduce start, LFMIS tail end}.
+constexpr uint32_t TIME_SLOTS = 4096;
+constexpr uint32_t TIME_FIELDS = 4;
 
 // Device-resident loop state.  Written only by the single-block reduce / tail kernels,
 // read by every other kernel at entry (kernel boundaries order the accesses).
@@ -76,6 +81,7 @@ struct LoopBuffers {
     unsigned long long* tile_stats; // per tile: [2t] sum |MIS|, [2t+1] sum resampled literals
     uint32_t* delta;        // allreduce exchange: per-iteration assignment XOR delta
     DevState* state;
+    unsigned long long* ktime; // TIME_SLOTS x TIME_FIELDS stamps, nullptr = timing off
     uint32_t n_vars;
     uint32_t n_words;
     uint32_t n_tiles;       // tiles covering [0, m)

@@ -75,6 +75,21 @@ __device__ __forceinline__ bool eval_gate_closed(const DevState* st) {
     return st->done != 0 || st->n_iter >= st->limit_eval;
 }
 
+// In-loop timing stamps (ALLL_FLAG_KERNEL_TIMING): slot of iteration n_iter (see TIME_SLOTS).
+__device__ __forceinline__ unsigned long long* time_slot(const LoopBuffers& b, uint64_t it) {
+    return b.ktime + (it % TIME_SLOTS) * TIME_FIELDS;
+}
+__device__ __forceinline__ unsigned long long wall_now() {
+    return (unsigned long long)__builtin_amdgcn_s_memrealtime();
+}
+// one stamp per workgroup (thread 0); only loop evaluations (gated) are timed
+__device__ __forceinline__ void stamp_eval_begin(const LoopBuffers& b, int gated) {
+    if (gated && b.ktime && threadIdx.x == 0) atomicMin(time_slot(b, b.state->n_iter), wall_now());
+}
+__device__ __forceinline__ void stamp_eval_end(const LoopBuffers& b, int gated) {
+    if (gated && b.ktime && threadIdx.x == 0) atomicMax(time_slot(b, b.state->n_iter) + 1, wall_now());
+}
+
 // ------------------------------------------------------------------------------------
 // Violated-clause entries.  Fixed width K: {clause id, K literals} (K+1 words, so a round
 // kernel never re-reads the clause store); generic CSR (K = 0): {clause id}, literals from
@@ -160,6 +175,7 @@ template <int K>
 __global__ __launch_bounds__(EVAL_THREADS) void k_eval_fixed(ClauseView cv, LoopBuffers b,
                                                              uint32_t tile_begin, int gated) {
     if (gated && eval_gate_closed(b.state)) return;
+    stamp_eval_begin(b, gated);
     __shared__ uint32_t s_cnt;
     const uint32_t tile = tile_begin + blockIdx.x;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -213,6 +229,7 @@ __global__ __launch_bounds__(EVAL_THREADS) void k_eval_fixed(ClauseView cv, Loop
         b.tile_cnt[tile] = s_cnt;
         b.mis_cnt[tile] = 0;
     }
+    stamp_eval_end(b, gated);
 }
 
 // Clause evaluation, fixed width K, persistent hybrid (the loop's default for fixed k).
@@ -235,6 +252,7 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
     const uint32_t t0 = tile_begin + (uint32_t)(((uint64_t)ntiles * blockIdx.x) / nblk);
     const uint32_t t1 = tile_begin + (uint32_t)(((uint64_t)ntiles * (blockIdx.x + 1)) / nblk);
     if (t0 >= t1) return;
+    stamp_eval_begin(b, gated);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     const uint64_t m = cv.m;
@@ -308,6 +326,7 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
             b.mis_cnt[pt + threadIdx.x] = 0;
         }
     }
+    stamp_eval_end(b, gated);
 }
 
 // Clause evaluation, generic CSR (ragged widths): lane per clause, 64 consecutive
@@ -316,6 +335,7 @@ __global__ __launch_bounds__(EVAL_THREADS) void k_eval_csr(ClauseView cv, LoopBu
                                                            uint32_t tile_begin, int gated) {
     if (gated && eval_gate_closed(b.state)) return;
     __shared__ uint32_t s_cnt;
+    stamp_eval_begin(b, gated);
     const uint32_t tile = tile_begin + blockIdx.x;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t m = cv.m;
@@ -352,6 +372,7 @@ __global__ __launch_bounds__(EVAL_THREADS) void k_eval_csr(ClauseView cv, LoopBu
         b.tile_cnt[tile] = s_cnt;
         b.mis_cnt[tile] = 0;
     }
+    stamp_eval_end(b, gated);
 }
 
 // Multi-GPU: tiles owned by other ranks get their violated lists from the all-gathered
@@ -403,6 +424,7 @@ __global__ __launch_bounds__(1024) void k_reduce(LoopBuffers b, int mode) {
         if (threadIdx.x == 0) st->active = 0;
         return;
     }
+    const unsigned long long reduce_t0 = wall_now();
     __shared__ unsigned long long s_sum;
     if (threadIdx.x == 0) s_sum = 0;
     __syncthreads();
@@ -414,6 +436,12 @@ __global__ __launch_bounds__(1024) void k_reduce(LoopBuffers b, int mode) {
     if (threadIdx.x != 0) return;
     const unsigned long long u = s_sum;
     if (mode == 1) { st->count_out = u; return; }
+    if (b.ktime) {
+        unsigned long long* ts = time_slot(b, st->n_iter);
+        ts[2] = reduce_t0;
+        unsigned long long* nx = time_slot(b, st->n_iter + 1);  // next iteration's slot
+        nx[0] = ~0ull; nx[1] = 0; nx[2] = 0; nx[3] = 0;
+    }
     st->n_iter += 1;
     st->u_total = u;
     st->left_cnt = 0;
@@ -673,6 +701,7 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail(ClauseView cv, LoopBuffer
         st->tmis_cnt = s_tm;
         const uint32_t total = first_round + rounds;
         if (total > st->max_rounds) st->max_rounds = total;
+        if (b.ktime) time_slot(b, st->n_iter - 1)[3] = wall_now();
     }
 }
 

@@ -85,6 +85,7 @@ struct alll_ctx {
     std::vector<uint8_t> xbuf;
     std::vector<uint32_t> perm;  // evaluation position -> clause id (fixed-k layout)
     std::string eval_name;
+    int wall_khz = 100000;       // s_memrealtime rate (ALLL_FLAG_KERNEL_TIMING)
 };
 
 namespace {
@@ -381,6 +382,17 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     if ((rc = dalloc(c, &b.tile_stats, 2 * (size_t)n_tiles))) return bail(rc);
     if ((rc = dalloc(c, &b.delta, b.n_words))) return bail(rc);
     if ((rc = dalloc(c, &b.state, 1))) return bail(rc);
+    if (opt.flags & ALLL_FLAG_KERNEL_TIMING) {
+        if ((rc = dalloc(c, &b.ktime, (size_t)TIME_SLOTS * TIME_FIELDS))) return bail(rc);
+        std::vector<unsigned long long> init((size_t)TIME_SLOTS * TIME_FIELDS, 0ull);
+        for (uint32_t i = 0; i < TIME_SLOTS; ++i) init[(size_t)i * TIME_FIELDS] = ~0ull;
+        if (hipStreamSynchronize(c->stream) != hipSuccess ||
+            hipMemcpy(b.ktime, init.data(), init.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
+            return bail(fail(ALLL_ERR_HIP, "timing buffer upload failed"));
+        int khz = 0;
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) == hipSuccess && khz > 0)
+            c->wall_khz = khz;
+    }
     // ---- clause storage allocations, then drain the zero-fills before synchronous uploads
     ClauseView& cv = c->cv;
     cv.m = m;
@@ -739,6 +751,50 @@ int alll_profile(alll_ctx* c, uint64_t n_iters, alll_phase_times* out) {
     out->mis_ms = acc[2] / n_iters;
     out->resample_ms = acc[3] / n_iters;
     out->total_ms = (acc[0] + acc[1] + acc[2] + acc[3]) / n_iters;
+    return ALLL_OK;
+}
+
+int alll_loop_times(alll_ctx* c, uint64_t first_iter, uint64_t n_iters, alll_phase_times* out) {
+    if (!c || !out) return fail(ALLL_ERR_INVALID_ARG, "null argument");
+    memset(out, 0, sizeof(*out));
+    if (!c->b.ktime) return fail(ALLL_ERR_INVALID_ARG, "created without ALLL_FLAG_KERNEL_TIMING");
+    HIP_TRY(hipSetDevice(c->device));
+    int rc = read_state(c);
+    if (rc) return rc;
+    const uint64_t done = c->h_state->n_iter;  // slots of iterations < done are complete
+    if (first_iter + n_iters > done) n_iters = done > first_iter ? done - first_iter : 0;
+    if (done > TIME_SLOTS && first_iter < done - TIME_SLOTS) {
+        const uint64_t lo = done - TIME_SLOTS;
+        n_iters = first_iter + n_iters > lo ? first_iter + n_iters - lo : 0;
+        first_iter = lo;
+    }
+    if (n_iters == 0) return ALLL_OK;
+    std::vector<unsigned long long> t((size_t)TIME_SLOTS * TIME_FIELDS);
+    HIP_TRY(hipMemcpy(t.data(), c->b.ktime, t.size() * 8, hipMemcpyDeviceToHost));
+    const double tick_ms = 1.0 / c->wall_khz;
+    auto slot = [&](uint64_t i) { return &t[(size_t)(i % TIME_SLOTS) * TIME_FIELDS]; };
+    double se = 0, sx = 0, sm = 0, sr = 0, st = 0;
+    uint64_t ne = 0, nm = 0, nt = 0;
+    for (uint64_t i = first_iter; i < first_iter + n_iters; ++i) {
+        const unsigned long long* a = slot(i);
+        if (a[0] == ~0ull || a[1] < a[0]) continue;  // not evaluated (converged / gated)
+        se += (a[1] - a[0]) * tick_ms; ++ne;
+        if (a[2] >= a[1]) sx += (a[2] - a[1]) * tick_ms;
+        if (a[3] && a[3] >= a[2]) {
+            sm += (a[3] - a[2]) * tick_ms; ++nm;
+            // resample + launch gaps: LFMIS end to the next iteration's evaluation start
+            const unsigned long long* z = slot(i + 1);
+            if (i + 1 < done && z[0] != ~0ull && z[0] >= a[3]) {
+                sr += (z[0] - a[3]) * tick_ms;
+                st += (z[0] - a[0]) * tick_ms;
+                ++nt;
+            }
+        }
+    }
+    out->iterations = ne;
+    if (ne) { out->eval_ms = se / ne; out->exchange_ms = sx / ne; }
+    if (nm) out->mis_ms = sm / nm;
+    if (nt) { out->resample_ms = sr / nt; out->total_ms = st / nt; }
     return ALLL_OK;
 }
 

@@ -209,6 +209,13 @@ class Solver:
         N.check(self._L.alll_profile(self._ctx, n_iters, ctypes.byref(pt)), "profile")
         return pt.as_dict()
 
+    def loop_times(self, first_iter: int, n_iters: int) -> dict:
+        """In-loop phase times of iterations [first_iter, first_iter+n_iters) from the kernels'
+        own wall-clock stamps (needs flags |= FLAG_KERNEL_TIMING)."""
+        pt = N.PhaseTimes()
+        N.check(self._L.alll_loop_times(self._ctx, first_iter, n_iters, ctypes.byref(pt)), "loop_times")
+        return pt.as_dict()
+
     def eval_bytes(self) -> int:
         return int(self._L.alll_eval_bytes(self._ctx))
 

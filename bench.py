@@ -109,7 +109,10 @@ def main():
     ap.add_argument("--no-ranged", action="store_true", help="use the L2-gather eval kernel")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
-    ap.add_argument("--profile-iters", type=int, default=10)
+    ap.add_argument("--event-iters", type=int, default=10,
+                    help="iterations replayed eagerly with HIP events around each phase (cross-check)")
+    ap.add_argument("--eval-b2b", type=int, default=0,
+                    help="also time N back-to-back eval-only launches (reported separately)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_eval_traffic.json"))
     args = ap.parse_args()
 
@@ -139,7 +142,9 @@ def main():
     t0 = time.perf_counter()
     offs, lits = generate_ksat(1, n, m, k, kind)
     t_gen = time.perf_counter() - t0
-    flags = N.FLAG_EXCHANGE_ALLREDUCE if args.exchange == "allreduce" else 0
+    flags = N.FLAG_KERNEL_TIMING  # kernels stamp device wall-clock times of every iteration
+    if args.exchange == "allreduce":
+        flags |= N.FLAG_EXCHANGE_ALLREDUCE
     if args.no_ranged:
         flags |= N.FLAG_NO_RANGED
     t0 = time.perf_counter()
@@ -173,6 +178,7 @@ def main():
 
     barrier()
     torch.cuda.synchronize(local_rank)
+    it0 = s.stats()["n_iterations"]
     t0 = time.perf_counter()
     s.run(args.steps, sync=False)
     s.synchronize()
@@ -188,13 +194,16 @@ def main():
     value = m * steps_done / dt
     iters_s = steps_done / dt
 
-    # per-phase device time with HIP events on the solver's stream (eager replay of the same
-    # kernel sequence); the eval kernel's average duration prices the roofline
-    pt = s.profile(args.profile_iters)
+    # in-loop phase times of exactly the K timed iterations, from the kernels' own device
+    # wall-clock stamps (the graph replays as timed; eval = first workgroup start to last
+    # workgroup end); the eval kernel's average duration prices the roofline
+    pt = s.loop_times(it0, args.steps)
     eval_bytes = s.eval_bytes()
     eval_ms = pt["eval_ms"]
     achieved = eval_bytes / (eval_ms * 1e-3) / 1e9 if eval_ms > 0 else 0.0
-    ev_ms, _ = s.bench_eval(20)
+    # cross-check with HIP events on the solver's stream: the same iteration replayed eagerly
+    pe = s.profile(args.event_iters) if args.event_iters > 0 else None
+    ev_ms = s.bench_eval(args.eval_b2b)[0] if args.eval_b2b > 0 else None
     traffic = None
     try:
         tj = json.load(open(args.traffic_json))
@@ -227,6 +236,7 @@ def main():
             "avg_mis_size": st["avg_mis_size"],
             "lfmis_rounds_max": st["lfmis_rounds_max"],
             "phase_ms": {k2: pt[k2] for k2 in ("eval_ms", "exchange_ms", "mis_ms", "resample_ms", "total_ms")},
+            "phase_iters": pt["iterations"],
             "roofline": {
                 "bound": "hbm",
                 "achieved": achieved,
@@ -237,6 +247,8 @@ def main():
                 "kernel": s.eval_kernel(),
                 "algorithmic_bytes_per_launch": eval_bytes,
                 "eval_ms_in_loop": eval_ms,
+                "timing": "device wall-clock stamps inside the timed region (s_memrealtime)",
+                "eval_ms_hip_events": pe["eval_ms"] if pe else None,
                 "eval_ms_back_to_back": ev_ms,
             },
         }

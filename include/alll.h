@@ -54,6 +54,8 @@ typedef struct alll_problem {
 #define ALLL_FLAG_GENERIC_CSR       (1u << 2) /* disable the fixed-width clause layout */
 #define ALLL_FLAG_NO_RANGED         (1u << 3) /* use the L2-gather eval kernel instead of the
                                                  persistent LDS/L2 hybrid */
+#define ALLL_FLAG_KERNEL_TIMING     (1u << 4) /* stamp every loop iteration with device wall-clock
+                                                 times (alll_loop_times) */
 
 typedef struct alll_options {
     uint64_t seed;          /* Philox4x32-10 key; replaces std::random_device (SATInstance.h:346) */
@@ -158,6 +160,14 @@ int alll_get_mis(alll_ctx* ctx, uint32_t* out, uint64_t cap, uint64_t* n_out);
  * assignment; profile runs n_iters iterations eagerly with HIP events around each phase. */
 int alll_bench_eval(alll_ctx* ctx, int reps, double* avg_ms, uint64_t* n_violated);
 int alll_profile(alll_ctx* ctx, uint64_t n_iters, alll_phase_times* out);
+/* In-loop phase times of iterations [first_iter, first_iter + n_iters) as they ran (graph
+ * replay included), from device wall-clock stamps taken by the kernels themselves; needs
+ * ALLL_FLAG_KERNEL_TIMING at create.  eval_ms = evaluation kernel (first workgroup start to
+ * last workgroup end); exchange_ms = evaluation end to reduce start (collectives + collect on
+ * several GPUs, a launch gap on one); mis_ms = reduce start to LFMIS tail end; resample_ms =
+ * tail end to the next evaluation start; total_ms = evaluation start to the next one.  Only
+ * the last 4096 iterations are kept.  (No reference counterpart: measurement) */
+int alll_loop_times(alll_ctx* ctx, uint64_t first_iter, uint64_t n_iters, alll_phase_times* out);
 /* Block the host until all work queued on the solver's stream finished. */
 int alll_synchronize(alll_ctx* ctx);
 /* Bytes the evaluation kernel reads/writes per pass (algorithmic). */

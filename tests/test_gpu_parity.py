@@ -244,3 +244,28 @@ def test_bench_helpers(gpu, oracle_mod):
         assert pt["iterations"] == 3 and pt["eval_ms"] > 0 and pt["total_ms"] >= pt["eval_ms"]
         st = s.stats()
         assert st["n_iterations"] == 3
+
+
+def test_loop_times_stamps_leave_trajectory_unchanged(gpu, oracle_mod):
+    """ALLL_FLAG_KERNEL_TIMING: kernels stamp each iteration; results stay bit-exact."""
+    from alllsatisfiabilitysolver_amd import Solver, generate_ksat
+    from alllsatisfiabilitysolver_amd import _native as N
+
+    n, m = 30000, 120000
+    offs, lits = generate_ksat(6, n, m, 3)
+    st_o, A_o, _ = oracle_mod.solve(n, offs, lits, 21, max_iters=13, trace=True)
+    for flags in (N.FLAG_KERNEL_TIMING, N.FLAG_KERNEL_TIMING | N.FLAG_NO_RANGED):
+        with Solver(n, offs, lits, seed=21, flags=flags) as s:
+            s.run(4)
+            it0 = s.stats()["n_iterations"]
+            s.run(8)
+            np.testing.assert_array_equal(s.assignment_words(), oracle_mod.solve(n, offs, lits, 21, max_iters=13)[1])
+            pt = s.loop_times(it0, 8)
+            assert pt["iterations"] == 8
+            assert 0 < pt["eval_ms"] < 50
+            assert pt["mis_ms"] > 0 and pt["total_ms"] >= pt["eval_ms"] + pt["mis_ms"]
+            # out-of-range requests are clipped, never read garbage
+            assert s.loop_times(it0 + 8, 5)["iterations"] == 0
+    with Solver(n, offs, lits, seed=21) as s:
+        with pytest.raises(Exception):
+            s.loop_times(0, 1)

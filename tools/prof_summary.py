@@ -10,6 +10,7 @@ import statistics
 import sys
 
 d = sys.argv[1]
+config = sys.argv[2] if len(sys.argv) > 2 else "M"
 
 
 def rows(pattern):
@@ -45,4 +46,17 @@ for k, v in res.items():
     if "TCC_HIT_sum" in v:
         v["l2_hit_rate"] = v["TCC_HIT_sum"] / max(1.0, v["TCC_HIT_sum"] + v["TCC_MISS_sum"])
         print(f"   L2 hit rate {v['l2_hit_rate']:.3f}")
-json.dump(res, open(os.path.join(d, "pmc_eval_traffic.json"), "w"), indent=1)
+# bench-format record (bench.py --traffic-json): the dominant eval kernel of this config
+out = {"config": config, "n_gpus": 1, "per_kernel": res}
+main = [k for k in res if "hbm_bytes_per_launch" in res[k]]
+if main:
+    k = max(main, key=lambda k: res[k]["hbm_bytes_per_launch"])
+    out.update(kernel=k, hbm_bytes_per_launch=res[k]["hbm_bytes_per_launch"],
+               fetch_bytes=2 * res[k]["FETCH_SIZE"] * 1024, write_bytes=res[k]["WRITE_SIZE"] * 1024,
+               correction="FETCH_SIZE x2 (gfx950 wide-stream undercount), KiB units")
+    for r in stats:
+        if r["Name"].startswith(k.split("(")[0]):
+            out["trace_avg_ns"] = float(r["AverageNs"])
+            out["trace_calls"] = int(r["Calls"])
+json.dump(out, open(os.path.join(d, "pmc_eval_traffic.json"), "w"), indent=1)
+print(json.dumps({k: v for k, v in out.items() if k != "per_kernel"}))

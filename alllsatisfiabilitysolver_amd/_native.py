@@ -30,6 +30,7 @@ FLAG_EXCHANGE_ALLREDUCE = 1 << 1
 FLAG_GENERIC_CSR = 1 << 2
 FLAG_NO_RANGED = 1 << 3
 FLAG_KERNEL_TIMING = 1 << 4
+FLAG_ATOMIC_CLAIMS = 1 << 5
 
 MAX_GPU_STATS = 64
 

@@ -27,6 +27,16 @@ constexpr uint32_t RANGED_MAX_TILES = 16;          // tiles per block pass (64-b
 // Every LFMIS round decides at least the lowest undecided clause, so rounds <= |U|; the cap
 // only bounds a kernel that would otherwise run away on a bug or an adversarial chain.
 constexpr uint32_t MAX_TAIL_ROUNDS = 1u << 20;
+// Bucketed LFMIS round 0 (fixed width K): every claim of round 0 becomes a 64-bit pair
+// {clause id:32 | lose:1 | entry index in its run:16 | variable offset in its bucket:15},
+// written grouped by variable bucket (2^bkt_shift variables) inside its run (run_tiles
+// consecutive tiles); per-bucket minima are then resolved in LDS instead of by global atomics.
+constexpr uint32_t BKT_MAX = 4096;            // buckets (LDS histogram of k_bscatter)
+constexpr uint32_t BKT_SHIFT_MIN = 10;
+constexpr uint32_t BKT_SHIFT_MAX = 15;        // LDS minima of k_bresolve: 4 << 15 = 128 KiB
+constexpr uint32_t RUN_TILES_MAX = 16;        // entry index within a run < 16 * TILE = 2^16
+constexpr int BKT_THREADS = 512;
+constexpr unsigned long long PAIR_LOSE = 1ull << 31;
 // In-loop kernel timing (ALLL_FLAG_KERNEL_TIMING): per iteration i, slot i % TIME_SLOTS holds
 // device wall-clock stamps (s_memrealtime) {eval start (min over workgroups), eval end (max),
 // reduce start, LFMIS tail end}.
@@ -82,6 +92,13 @@ struct LoopBuffers {
     uint32_t* delta;        // allreduce exchange: per-iteration assignment XOR delta
     DevState* state;
     unsigned long long* ktime; // TIME_SLOTS x TIME_FIELDS stamps, nullptr = timing off
+    unsigned long long* pairs;  // bucketed round 0: n_runs x run_tiles*TILE*K pairs (nullptr = atomics)
+    unsigned long long* runtab; // [bucket][run]: start | count << 32 of the bucket's pairs in the run
+    uint32_t* run_pairs;        // pairs per run
+    uint32_t bkt_shift;         // bucket = variable >> bkt_shift
+    uint32_t n_bkt;
+    uint32_t run_tiles;
+    uint32_t n_runs;
     uint32_t n_vars;
     uint32_t n_words;
     uint32_t n_tiles;       // tiles covering [0, m)
@@ -100,6 +117,7 @@ hipError_t launch_collect(const ClauseView& cv, const LoopBuffers& b, uint32_t o
 hipError_t launch_reduce(const LoopBuffers& b, int mode, hipStream_t s);
 hipError_t launch_round(const ClauseView& cv, const LoopBuffers& b, uint32_t r, bool last,
                         hipStream_t s);
+hipError_t launch_round0_buckets(const ClauseView& cv, const LoopBuffers& b, bool last, hipStream_t s);
 hipError_t launch_tail(const ClauseView& cv, const LoopBuffers& b, uint32_t first_round,
                        hipStream_t s);
 hipError_t launch_resample(const ClauseView& cv, const LoopBuffers& b, uint32_t tile_begin,

@@ -552,21 +552,15 @@ __global__ __launch_bounds__(ROUND_THREADS) void k_claim(ClauseView cv, LoopBuff
     if (r > 0 && threadIdx.x == 0) b.tile_cnt[tile] = s_keep;
 }
 
-// JOIN(r): survivors compacted from `in` to `out`; in the last grid round they go to the
-// tail kernel's compact list instead.
-template <int K>
-__global__ __launch_bounds__(ROUND_THREADS) void k_join(ClauseView cv, LoopBuffers b, uint32_t r,
-                                                        const uint32_t* __restrict__ in, uint32_t* out,
-                                                        int last) {
+// Join one tile's undecided entries: own(e, i) says whether entry i holds every variable it
+// claimed; such a clause is in the LFMIS (cover + MIS list + statistics), the others are
+// compacted from `in` to `out` (in the last grid round: into the tail kernel's compact list).
+template <int K, typename OwnFn>
+__device__ __forceinline__ void join_tile(const ClauseView& cv, const LoopBuffers& b, uint32_t tile, uint32_t cnt,
+                                          const uint32_t* __restrict__ in, uint32_t* out, int last,
+                                          uint32_t stamp, OwnFn own) {
     DevState* st = b.state;
-    if (!st->active) return;
-    const uint32_t tile = blockIdx.x;
-    const uint32_t cnt = b.tile_cnt[tile];
-    if (cnt == 0) return;
     constexpr int S = Ent<K>::S;
-    const uint32_t stamp = st->stamp;
-    const unsigned long long keyhi = (unsigned long long)(~(st->round_base + r)) << 32;
-    const unsigned long long* owner = owner_of(b, st->round_base + r);
     __shared__ uint32_t s_keep, s_join, s_base;
     __shared__ unsigned long long s_lits;
     if (threadIdx.x == 0) { s_keep = 0; s_join = 0; s_lits = 0; }
@@ -581,9 +575,7 @@ __global__ __launch_bounds__(ROUND_THREADS) void k_join(ClauseView cv, LoopBuffe
         const uint32_t c = e.w[0];
         uint64_t lb;
         const uint32_t len = ent_len<K>(cv, e, lb);
-        bool own = true;
-        for (uint32_t j = 0; j < len; ++j) own &= owner[lit_var(ent_lit<K>(cv, e, lb, j))] == (keyhi | c);
-        if (own) {
+        if (own(e, i, lb, len)) {
             for (uint32_t j = 0; j < len; ++j) b.cover[lit_var(ent_lit<K>(cv, e, lb, j))] = stamp;
             mis[atomicAdd(&s_join, 1u)] = c;
             my_lits += len;
@@ -607,6 +599,445 @@ __global__ __launch_bounds__(ROUND_THREADS) void k_join(ClauseView cv, LoopBuffe
         if (s_join) {
             atomicAdd(&b.tile_stats[2 * tile], (unsigned long long)s_join);
             atomicAdd(&b.tile_stats[2 * tile + 1], s_lits);
+        }
+    }
+    __syncthreads();  // the shared counters are reused by the next tile
+}
+
+// JOIN(r): a clause joins iff owner[v] holds its round-r key for every variable.
+template <int K>
+__global__ __launch_bounds__(ROUND_THREADS) void k_join(ClauseView cv, LoopBuffers b, uint32_t r,
+                                                        const uint32_t* __restrict__ in, uint32_t* out,
+                                                        int last) {
+    const DevState* st = b.state;
+    if (!st->active) return;
+    const uint32_t tile = blockIdx.x;
+    const uint32_t cnt = b.tile_cnt[tile];
+    if (cnt == 0) return;
+    const unsigned long long keyhi = (unsigned long long)(~(st->round_base + r)) << 32;
+    const unsigned long long* owner = owner_of(b, st->round_base + r);
+    join_tile<K>(cv, b, tile, cnt, in, out, last, st->stamp,
+                 [&](const Ent<K>& e, uint32_t, uint64_t lb, uint32_t len) {
+                     bool own = true;
+                     for (uint32_t j = 0; j < len; ++j)
+                         own &= owner[lit_var(ent_lit<K>(cv, e, lb, j))] == (keyhi | e.w[0]);
+                     return own;
+                 });
+}
+
+// ------------------------------------------------------------------------------------
+// Bucketed round 0 (fixed width K; same decisions as CLAIM(0) + JOIN(0)).  Round 0 claims
+// ~k|U| random variables, which as global atomicMin runs at the chip's memory-side atomic
+// rate; here the claims are grouped by variable bucket instead and each bucket's minima are
+// taken in LDS:
+//   k_bscatter (workgroup per run of run_tiles tiles): translates evaluation positions to
+//     clause ids, histograms the run's claims by bucket, writes them as pairs grouped by
+//     bucket into the run's area, and the per-bucket (start, count) into runtab[bucket][run].
+//     Hot-variable claims are reduced in the LDS hash table and go to owner[] as before.
+//   k_bresolve (workgroup per bucket): LDS minimum per variable over the bucket's pairs of
+//     every run, then marks the pairs that are not the minimum (PAIR_LOSE).
+//   k_bjoin (workgroup per run): a clause joins iff none of its pairs lost and it owns its hot
+//     variables; joins and compaction as JOIN(0).
+__device__ __forceinline__ unsigned long long make_pair(uint32_t c, uint32_t el, uint32_t vl) {
+    return ((unsigned long long)c << 32) | ((unsigned long long)el << 15) | vl;
+}
+
+// Run-local entry index f -> (tile of the run, index in that tile); pre = prefix of the
+// run's tile counts (<= RUN_TILES_MAX + 1 entries, in LDS).
+__device__ __forceinline__ uint32_t run_tile_of(const uint32_t* pre, uint32_t nt, uint32_t f) {
+    uint32_t tt = 0;
+    while (tt + 1 < nt && pre[tt + 1] <= f) ++tt;
+    return tt;
+}
+
+// Loops below are unrolled by BKT_UNROLL independent items per thread so that their global
+// loads are in flight together.  When a run's entries fit in one unrolled sweep of the
+// workgroup (the common case: ~2.5k entries per run at 10M clauses), they stay in registers
+// between the phases of a kernel instead of being re-read.
+constexpr int BKT_UNROLL = 4;
+constexpr int BSC_THREADS = 1024;
+constexpr uint32_t BKT_STAGE = 12288;  // pairs staged in LDS by k_bscatter (96 KiB)
+
+// Tile counts of run r -> LDS prefix (nt + 1 entries); returns the run's entry count.
+__device__ __forceinline__ uint32_t run_prefix(const LoopBuffers& b, uint32_t t0, uint32_t nt, uint32_t* s_tc,
+                                               uint32_t* s_pre) {
+    if (threadIdx.x < nt) s_tc[threadIdx.x] = b.tile_cnt[t0 + threadIdx.x];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (uint32_t tt = 0; tt < nt; ++tt) { s_pre[tt] = acc; acc += s_tc[tt]; }
+        s_pre[nt] = acc;
+    }
+    __syncthreads();
+    return s_pre[nt];
+}
+
+// Load the U entries f0 + u * blockDim.x of the run (ok[u] = exists; tt/idx = its tile / slot).
+template <int K, int U>
+__device__ __forceinline__ void load_run_entries(const uint32_t* list, uint32_t t0, uint32_t nt, const uint32_t* s_pre,
+                                                 uint32_t E, uint32_t f0, Ent<K>* e, bool* ok, uint32_t* tt,
+                                                 uint32_t* idx) {
+    constexpr int S = Ent<K>::S;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint32_t f = f0 + u * blockDim.x;
+        ok[u] = f < E;
+        if (ok[u]) {
+            tt[u] = run_tile_of(s_pre, nt, f);
+            idx[u] = f - s_pre[tt[u]];
+            load_ent<K>(e[u], list + ((uint64_t)(t0 + tt[u]) * TILE + idx[u]) * S);
+        }
+    }
+}
+
+template <int K>
+__global__ __launch_bounds__(BSC_THREADS) void k_bscatter(ClauseView cv, LoopBuffers b, uint32_t* list) {
+    const DevState* st = b.state;
+    if (!st->active) return;
+    constexpr int S = Ent<K>::S;
+    constexpr int U = BKT_UNROLL;
+    const uint32_t r = blockIdx.x;
+    const uint32_t t0 = r * b.run_tiles, nt = min(b.run_tiles, b.n_tiles - t0);
+    __shared__ uint32_t s_hist[BKT_MAX];
+    __shared__ uint32_t s_hk[HOT_SLOTS];
+    __shared__ unsigned long long s_hv[HOT_SLOTS];
+    __shared__ uint32_t s_tc[RUN_TILES_MAX], s_pre[RUN_TILES_MAX + 1];
+    __shared__ uint32_t s_wsum[BSC_THREADS / 64];
+    extern __shared__ unsigned long long s_pairs[];  // BKT_STAGE pairs
+    HotTable ht{s_hk, s_hv};
+    const bool hot = cv.n_hot != 0;
+    if (hot) ht.init();
+    const uint32_t nb = b.n_bkt, sh = b.bkt_shift;
+    for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) s_hist[i] = 0;
+    const uint32_t E = run_prefix(b, t0, nt, s_tc, s_pre);
+    const bool single = E <= blockDim.x * U;
+    const unsigned long long keyhi = (unsigned long long)(~st->round_base) << 32;
+    Ent<K> e[U];
+    bool ok[U];
+    uint32_t tts[U], idx[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) ok[u] = false;  // threads past the last entry emit nothing
+    // pass 1: clause ids (written back), bucket histogram, hot claims
+    for (uint32_t f0 = threadIdx.x; f0 < E; f0 += blockDim.x * U) {
+        load_run_entries<K, U>(list, t0, nt, s_pre, E, f0, e, ok, tts, idx);
+        if (cv.perm) {
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (ok[u]) e[u].w[0] = cv.perm[e[u].w[0]];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (ok[u]) list[((uint64_t)(t0 + tts[u]) * TILE + idx[u]) * S] = e[u].w[0];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!ok[u]) continue;
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                const uint32_t raw = e[u].w[1 + j];
+                if (hot && (raw & LIT_HOT)) ht.claim(lit_var(raw), keyhi | e[u].w[0]);
+                else atomicAdd(&s_hist[lit_var(raw) >> sh], 1u);
+            }
+        }
+    }
+    __syncthreads();
+    if (hot) ht.flush(owner_of(b, st->round_base));
+    // exclusive scan of the histogram: run-local start of every bucket
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t per = (nb + blockDim.x - 1) / blockDim.x;
+    const uint32_t b0 = min(nb, threadIdx.x * per), b1 = min(nb, b0 + per);
+    uint32_t sum = 0;
+    for (uint32_t k = b0; k < b1; ++k) sum += s_hist[k];
+    uint32_t incl = sum;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) s_wsum[wave] = incl;
+    __syncthreads();
+    uint32_t wbase = 0, total = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+        if (w < wave) wbase += s_wsum[w];
+        total += s_wsum[w];
+    }
+    uint32_t run = wbase + incl - sum;
+    for (uint32_t k = b0; k < b1; ++k) {
+        const uint32_t c = s_hist[k];
+        b.runtab[(uint64_t)k * b.n_runs + r] = run | ((unsigned long long)c << 32);
+        s_hist[k] = run;
+        run += c;
+    }
+    if (threadIdx.x == 0) b.run_pairs[r] = total;
+    __syncthreads();
+    // pass 2: pairs grouped by bucket, staged in LDS when they fit so that the run's area is
+    // written with whole-line stores
+    unsigned long long* gpr = b.pairs + (uint64_t)r * b.run_tiles * TILE * K;
+    const bool staged = total <= BKT_STAGE;
+    const uint32_t vmask = (1u << sh) - 1u;
+    auto emit = [&]() {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!ok[u]) continue;
+            const uint32_t el = tts[u] * TILE + idx[u];
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                const uint32_t raw = e[u].w[1 + j];
+                if (hot && (raw & LIT_HOT)) continue;
+                const uint32_t v = lit_var(raw);
+                const uint32_t pos = atomicAdd(&s_hist[v >> sh], 1u);
+                const unsigned long long x = make_pair(e[u].w[0], el, v & vmask);
+                if (staged) s_pairs[pos] = x;
+                else gpr[pos] = x;
+            }
+        }
+    };
+    if (single) {
+        emit();  // this thread's entries are still in registers
+    } else {
+        for (uint32_t f0 = threadIdx.x; f0 < E; f0 += blockDim.x * U) {
+            load_run_entries<K, U>(list, t0, nt, s_pre, E, f0, e, ok, tts, idx);
+            emit();
+        }
+    }
+    if (staged) {
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < total; i += blockDim.x) gpr[i] = s_pairs[i];
+    }
+}
+
+// Workgroup per bucket.  The run table column is processed in batches of BKT_RUN_BATCH runs:
+// segment starts and a prefix of segment lengths in LDS make the batch's pairs one flat index
+// space; a wave takes 64 consecutive items per step (coalesced loads: a segment is contiguous)
+// and each lane finds its item's run by a fixed-depth binary search, BKT_UNROLL items
+// interleaved.  When the bucket's pairs fit the LDS stage (one batch, stage_cap items), the
+// pairs and their positions stay in LDS for the marking pass; otherwise it re-reads them.
+constexpr uint32_t BKT_RUN_BATCH = 1024;
+
+struct ResolveLds {
+    uint32_t* min;          // 1 << bkt_shift
+    unsigned long long* sx; // stage: pairs
+    uint32_t* sp;           // stage: positions in b.pairs
+    uint32_t* start;        // batch: segment start in the run area
+    uint32_t* pre;          // batch: exclusive prefix of segment lengths (pre[nr] = total)
+    uint32_t* wsum;
+};
+
+// Batch setup: segments of runs [rb, rb+nr) of this bucket; returns the batch's pair count.
+__device__ __forceinline__ uint32_t resolve_batch(const LoopBuffers& b, const ResolveLds& L, uint32_t rb, uint32_t nr) {
+    const unsigned long long* tab = b.runtab + (uint64_t)blockIdx.x * b.n_runs;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t per = (nr + blockDim.x - 1) / blockDim.x;
+    const uint32_t q0 = min(nr, threadIdx.x * per), q1 = min(nr, q0 + per);
+    uint32_t sum = 0;
+    for (uint32_t q = q0; q < q1; ++q) {
+        const unsigned long long t = tab[rb + q];
+        L.start[q] = (uint32_t)t;
+        L.pre[q] = (uint32_t)(t >> 32);
+        sum += (uint32_t)(t >> 32);
+    }
+    uint32_t incl = sum;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) L.wsum[wave] = incl;
+    __syncthreads();
+    uint32_t run = incl - sum, total = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+        if (w < wave) run += L.wsum[w];
+        total += L.wsum[w];
+    }
+    for (uint32_t q = q0; q < q1; ++q) {
+        const uint32_t c = L.pre[q];
+        L.pre[q] = run;
+        run += c;
+    }
+    if (threadIdx.x == 0) L.pre[nr] = total;
+    __syncthreads();
+    return total;
+}
+
+// Position of flat item f of the batch: largest q with pre[q] <= f (fixed depth: log2 nr steps;
+// a run with an empty segment shares its prefix with the next one, and the largest wins).
+__device__ __forceinline__ uint64_t resolve_pos(const ResolveLds& L, uint32_t rb, uint32_t nr, uint32_t f,
+                                                uint64_t run_cap) {
+    uint32_t lo = 0;
+    for (uint32_t half = 1u << (31 - __clz(nr)); half; half >>= 1) {
+        const uint32_t mid = lo + half;
+        if (mid < nr && L.pre[mid] <= f) lo = mid;
+    }
+    return (uint64_t)(rb + lo) * run_cap + L.start[lo] + (f - L.pre[lo]);
+}
+
+__global__ __launch_bounds__(BKT_THREADS) void k_bresolve(LoopBuffers b, uint64_t run_cap, uint32_t stage_cap) {
+    if (!b.state->active) return;
+    constexpr int U = BKT_UNROLL;
+    extern __shared__ unsigned long long s_dyn[];
+    __shared__ uint32_t s_start[BKT_RUN_BATCH], s_pre[BKT_RUN_BATCH + 1];
+    __shared__ uint32_t s_wsum[BKT_THREADS / 64];
+    const uint32_t bv = 1u << b.bkt_shift;
+    ResolveLds L;
+    L.sx = s_dyn;
+    L.sp = reinterpret_cast<uint32_t*>(s_dyn + stage_cap);
+    L.min = L.sp + stage_cap;
+    L.start = s_start; L.pre = s_pre; L.wsum = s_wsum;
+    for (uint32_t i = threadIdx.x; i < bv; i += blockDim.x) L.min[i] = ~0u;
+    __syncthreads();
+    const uint32_t stride = blockDim.x * U;
+    for (uint32_t rb = 0; rb < b.n_runs; rb += BKT_RUN_BATCH) {
+        const uint32_t nr = min(BKT_RUN_BATCH, b.n_runs - rb);
+        const uint32_t np = resolve_batch(b, L, rb, nr);
+        const bool staged = rb == 0 && nr == b.n_runs && np <= stage_cap;
+        // items of a wave: base + lane + 64 u, base = wave * 64 U (+ stride per step)
+        for (uint32_t f0 = (threadIdx.x >> 6) * 64 * U + (threadIdx.x & 63); f0 < np; f0 += stride) {
+            uint64_t pos[U];
+            unsigned long long x[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t f = f0 + 64 * u;
+                if (f < np) pos[u] = resolve_pos(L, rb, nr, f, run_cap);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (f0 + 64 * u < np) x[u] = b.pairs[pos[u]];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t f = f0 + 64 * u;
+                if (f >= np) continue;
+                atomicMin(&L.min[(uint32_t)x[u] & 0x7FFFu], (uint32_t)(x[u] >> 32));
+                if (staged) { L.sx[f] = x[u]; L.sp[f] = (uint32_t)pos[u]; }
+            }
+        }
+        __syncthreads();
+        if (staged) {
+            for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) {
+                const unsigned long long x = L.sx[i];
+                if (L.min[(uint32_t)x & 0x7FFFu] != (uint32_t)(x >> 32)) b.pairs[L.sp[i]] = x | PAIR_LOSE;
+            }
+            return;
+        }
+    }
+    // marking pass, re-reading the pairs
+    for (uint32_t rb = 0; rb < b.n_runs; rb += BKT_RUN_BATCH) {
+        const uint32_t nr = min(BKT_RUN_BATCH, b.n_runs - rb);
+        const uint32_t np = resolve_batch(b, L, rb, nr);
+        for (uint32_t f0 = (threadIdx.x >> 6) * 64 * U + (threadIdx.x & 63); f0 < np; f0 += stride) {
+            uint64_t pos[U];
+            unsigned long long x[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t f = f0 + 64 * u;
+                if (f < np) pos[u] = resolve_pos(L, rb, nr, f, run_cap);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (f0 + 64 * u < np) x[u] = b.pairs[pos[u]];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (f0 + 64 * u < np && L.min[(uint32_t)x[u] & 0x7FFFu] != (uint32_t)(x[u] >> 32))
+                    b.pairs[pos[u]] = x[u] | PAIR_LOSE;
+        }
+        __syncthreads();
+    }
+}
+
+// Workgroup per run: lose marks -> LDS byte per entry; then every entry of the run's tiles in
+// one flat loop: join (cover, MIS list of its tile) or survive (compacted into its tile's
+// list in `out`, or the tail's compact list when `last`).
+template <int K>
+__global__ __launch_bounds__(BKT_THREADS) void k_bjoin(ClauseView cv, LoopBuffers b, const uint32_t* in,
+                                                       uint32_t* out, int last) {
+    DevState* st = b.state;
+    if (!st->active) return;
+    constexpr int S = Ent<K>::S;
+    constexpr int U = 2 * BKT_UNROLL;
+    const uint32_t r = blockIdx.x;
+    const uint32_t t0 = r * b.run_tiles, nt = min(b.run_tiles, b.n_tiles - t0);
+    extern __shared__ uint32_t s_lost[];  // one byte per entry slot of the run's tiles
+    __shared__ uint32_t s_tc[RUN_TILES_MAX], s_pre[RUN_TILES_MAX + 1], s_keep[RUN_TILES_MAX],
+        s_join[RUN_TILES_MAX], s_mis0[RUN_TILES_MAX], s_base[RUN_TILES_MAX];
+    __shared__ unsigned long long s_lits[RUN_TILES_MAX];
+    for (uint32_t i = threadIdx.x; i < nt * TILE / 4; i += blockDim.x) s_lost[i] = 0;
+    if (threadIdx.x < nt) {
+        s_keep[threadIdx.x] = 0;
+        s_join[threadIdx.x] = 0;
+        s_lits[threadIdx.x] = 0;
+        s_mis0[threadIdx.x] = b.mis_cnt[t0 + threadIdx.x];
+    }
+    const uint32_t E = run_prefix(b, t0, nt, s_tc, s_pre);
+    const bool single = E <= blockDim.x * U;
+    Ent<K> e[U];
+    bool ok[U];
+    uint32_t tts[U], idx[U];
+    if (single) load_run_entries<K, U>(in, t0, nt, s_pre, E, threadIdx.x, e, ok, tts, idx);
+    uint8_t* lost = reinterpret_cast<uint8_t*>(s_lost);
+    const unsigned long long* pr = b.pairs + (uint64_t)r * b.run_tiles * TILE * K;
+    const uint32_t np = b.run_pairs[r];
+    for (uint32_t i0 = threadIdx.x; i0 < np; i0 += blockDim.x * U) {
+        unsigned long long x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t i = i0 + u * blockDim.x;
+            x[u] = i < np ? pr[i] : 0ull;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (x[u] & PAIR_LOSE) lost[(x[u] >> 15) & 0xFFFFu] = 1;
+    }
+    __syncthreads();
+    const bool hot = cv.n_hot != 0;
+    const unsigned long long keyhi = (unsigned long long)(~st->round_base) << 32;
+    const unsigned long long* owner = owner_of(b, st->round_base);
+    const uint32_t stamp = st->stamp;
+    auto decide = [&]() {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!ok[u]) continue;
+            const uint32_t tt = tts[u], tile = t0 + tt;
+            bool own = !lost[tt * TILE + idx[u]];
+            if (hot) {
+#pragma unroll
+                for (int j = 0; j < K; ++j) {
+                    const uint32_t raw = e[u].w[1 + j];
+                    if (raw & LIT_HOT) own &= owner[lit_var(raw)] == (keyhi | e[u].w[0]);
+                }
+            }
+            if (own) {
+#pragma unroll
+                for (int j = 0; j < K; ++j) b.cover[lit_var(e[u].w[1 + j])] = stamp;
+                b.mis[(uint64_t)tile * TILE + s_mis0[tt] + atomicAdd(&s_join[tt], 1u)] = e[u].w[0];
+                atomicAdd(&s_lits[tt], (unsigned long long)K);
+            } else {
+                store_ent<K>(out + ((uint64_t)tile * TILE + atomicAdd(&s_keep[tt], 1u)) * S, e[u]);
+            }
+        }
+    };
+    if (single) {
+        decide();
+    } else {
+        for (uint32_t f0 = threadIdx.x; f0 < E; f0 += blockDim.x * U) {
+            load_run_entries<K, U>(in, t0, nt, s_pre, E, f0, e, ok, tts, idx);
+            decide();
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < nt) {
+        const uint32_t tt = threadIdx.x, tile = t0 + tt, kept = s_keep[tt];
+        if (last && kept) s_base[tt] = atomicAdd(&st->left_cnt, kept);
+        b.tile_cnt[tile] = last ? 0u : kept;
+        b.mis_cnt[tile] = s_mis0[tt] + s_join[tt];
+        if (s_join[tt]) {
+            atomicAdd(&b.tile_stats[2 * tile], (unsigned long long)s_join[tt]);
+            atomicAdd(&b.tile_stats[2 * tile + 1], s_lits[tt]);
+        }
+    }
+    if (last) {
+        __syncthreads();
+        for (uint32_t tt = 0; tt < nt; ++tt) {
+            const uint32_t kept = s_keep[tt];
+            if (!kept) continue;
+            const uint32_t* src = out + (uint64_t)(t0 + tt) * TILE * S;
+            uint32_t* dst = b.left + (uint64_t)s_base[tt] * S;
+            for (uint32_t i = threadIdx.x; i < kept * S; i += blockDim.x) dst[i] = src[i];
         }
     }
 }
@@ -860,6 +1291,44 @@ hipError_t launch_round(const ClauseView& cv, const LoopBuffers& b, uint32_t r, 
     if (e != hipSuccess) return e;
     const int l = last ? 1 : 0;
     ALLL_DISPATCH_K(cv.k, (k_join<K><<<b.n_tiles, ROUND_THREADS, 0, s>>>(cv, b, r, s0, s1, l)));
+    return hipGetLastError();
+}
+
+hipError_t launch_round0_buckets(const ClauseView& cv, const LoopBuffers& b, bool last, hipStream_t s) {
+    // buffers as CLAIM(0) + JOIN(0): eval -> stage[0] (ids translated in place); JOIN stage[0] -> stage[1]
+    if (b.n_tiles == 0 || cv.k == 0 || !b.pairs) return hipErrorInvalidValue;
+    const uint64_t run_cap = (uint64_t)b.run_tiles * TILE * cv.k;
+    // k_bresolve LDS: minima (4 << shift) + a stage of 12-byte slots within ~150 KiB in all
+    const uint32_t min_bytes = 4u << b.bkt_shift;
+    const uint32_t static_bytes = 2 * BKT_RUN_BATCH * 4 + 64;
+    const uint32_t budget = 76u * 1024u;  // two workgroups per CU
+    uint32_t stage_cap = budget > min_bytes + static_bytes ? (budget - min_bytes - static_bytes) / 12 : 0;
+    stage_cap = std::min<uint32_t>(stage_cap, 8192);
+    const size_t lds = (size_t)min_bytes + (size_t)stage_cap * 12;
+    static bool attr_set[MAX_FIXED_K + 1] = {};
+    if (!attr_set[cv.k]) {
+        hipError_t e = hipFuncSetAttribute((const void*)k_bresolve, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)(budget - static_bytes));
+        if (e != hipSuccess) return e;
+        ALLL_DISPATCH_K(cv.k, (e = hipFuncSetAttribute((const void*)k_bscatter<(K > 0 ? K : 1)>,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       (int)(BKT_STAGE * 8))));
+        if (e != hipSuccess) return e;
+        ALLL_DISPATCH_K(cv.k, (e = hipFuncSetAttribute((const void*)k_bjoin<(K > 0 ? K : 1)>,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       (int)(RUN_TILES_MAX * TILE))));
+        if (e != hipSuccess) return e;
+        attr_set[cv.k] = true;
+    }
+    ALLL_DISPATCH_K(cv.k, (k_bscatter<(K > 0 ? K : 1)><<<b.n_runs, BSC_THREADS, BKT_STAGE * 8, s>>>(cv, b, b.stage[0])));
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    k_bresolve<<<b.n_bkt, BKT_THREADS, lds, s>>>(b, run_cap, stage_cap);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const int l = last ? 1 : 0;
+    ALLL_DISPATCH_K(cv.k, (k_bjoin<(K > 0 ? K : 1)><<<b.n_runs, BKT_THREADS, (size_t)b.run_tiles * TILE, s>>>(
+                              cv, b, b.stage[0], b.stage[1], l)));
     return hipGetLastError();
 }
 

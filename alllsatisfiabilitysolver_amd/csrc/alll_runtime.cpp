@@ -168,8 +168,10 @@ int enqueue_iteration(alll_ctx* c, hipEvent_t* marks) {
     }
     if (marks) HIP_TRY(hipEventRecord(marks[2], s));
     HIP_TRY(launch_reduce(c->b, 0, s));
-    for (uint32_t r = 0; r < c->grid_rounds; ++r)
-        HIP_TRY(launch_round(c->cv, c->b, r, r + 1 == c->grid_rounds, s));
+    for (uint32_t r = 0; r < c->grid_rounds; ++r) {
+        if (r == 0 && c->b.pairs) HIP_TRY(launch_round0_buckets(c->cv, c->b, c->grid_rounds == 1, s));
+        else HIP_TRY(launch_round(c->cv, c->b, r, r + 1 == c->grid_rounds, s));
+    }
     HIP_TRY(launch_tail(c->cv, c->b, c->grid_rounds, s));
     if (marks) HIP_TRY(hipEventRecord(marks[3], s));
     if (c->allreduce && c->world > 1) {
@@ -392,6 +394,23 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
         int khz = 0;
         if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) == hipSuccess && khz > 0)
             c->wall_khz = khz;
+    }
+    // ---- bucketed LFMIS round 0 (fixed width): ~768 buckets, runs of up to 16 tiles
+    if (fixed_k > 0 && !(opt.flags & ALLL_FLAG_ATOMIC_CLAIMS) && n_tiles > 0 && c->n_vars > 0) {
+        uint32_t shift = BKT_SHIFT_MIN;
+        while (shift < BKT_SHIFT_MAX && ((uint64_t)c->n_vars >> shift) > 768) ++shift;
+        const uint64_t nb = ((uint64_t)c->n_vars + (1u << shift) - 1) >> shift;
+        if (nb <= BKT_MAX) {
+            b.bkt_shift = shift;
+            b.n_bkt = (uint32_t)nb;
+            // about one run per CU (k_bscatter holds one 1024-thread workgroup per CU)
+            b.run_tiles = std::max<uint32_t>(1, std::min<uint32_t>(RUN_TILES_MAX, (n_tiles + 255) / 256));
+            b.n_runs = (n_tiles + b.run_tiles - 1) / b.run_tiles;
+            const size_t run_cap = (size_t)b.run_tiles * TILE * fixed_k;
+            if ((rc = dalloc(c, &b.pairs, (size_t)b.n_runs * run_cap))) return bail(rc);
+            if ((rc = dalloc(c, &b.runtab, (size_t)b.n_bkt * b.n_runs))) return bail(rc);
+            if ((rc = dalloc(c, &b.run_pairs, b.n_runs))) return bail(rc);
+        }
     }
     // ---- clause storage allocations, then drain the zero-fills before synchronous uploads
     ClauseView& cv = c->cv;

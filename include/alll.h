@@ -56,6 +56,8 @@ typedef struct alll_problem {
                                                  persistent LDS/L2 hybrid */
 #define ALLL_FLAG_KERNEL_TIMING     (1u << 4) /* stamp every loop iteration with device wall-clock
                                                  times (alll_loop_times) */
+#define ALLL_FLAG_ATOMIC_CLAIMS     (1u << 5) /* LFMIS round 0 by global atomicMin claims instead of
+                                                 the variable-bucketed LDS resolution */
 
 typedef struct alll_options {
     uint64_t seed;          /* Philox4x32-10 key; replaces std::random_device (SATInstance.h:346) */

@@ -21,7 +21,7 @@ from conftest import GOLDEN
 pytestmark = pytest.mark.gpu
 
 T1_FIXTURES = sorted(p for p in glob.glob(os.path.join(GOLDEN, "*_T1.npz")))
-LAYOUTS = {"hybrid": 0, "fixed": 1 << 3, "csr": 1 << 2}
+LAYOUTS = {"hybrid": 0, "fixed": 1 << 3, "csr": 1 << 2, "atomic_claims": 1 << 5}
 
 
 @pytest.fixture(scope="module")

@@ -99,6 +99,7 @@ struct LoopBuffers {
     uint32_t n_bkt;
     uint32_t run_tiles;
     uint32_t n_runs;
+    uint32_t resolve_lds;       // LDS budget of a k_bresolve workgroup (bytes)
     uint32_t n_vars;
     uint32_t n_words;
     uint32_t n_tiles;       // tiles covering [0, m)

@@ -1301,14 +1301,15 @@ hipError_t launch_round0_buckets(const ClauseView& cv, const LoopBuffers& b, boo
     // k_bresolve LDS: minima (4 << shift) + a stage of 12-byte slots within ~150 KiB in all
     const uint32_t min_bytes = 4u << b.bkt_shift;
     const uint32_t static_bytes = 2 * BKT_RUN_BATCH * 4 + 64;
-    const uint32_t budget = 76u * 1024u;  // two workgroups per CU
+    const uint32_t budget = b.resolve_lds;
     uint32_t stage_cap = budget > min_bytes + static_bytes ? (budget - min_bytes - static_bytes) / 12 : 0;
+    if (min_bytes + static_bytes + stage_cap * 12 > 150u * 1024u) stage_cap = 0;
     stage_cap = std::min<uint32_t>(stage_cap, 8192);
     const size_t lds = (size_t)min_bytes + (size_t)stage_cap * 12;
     static bool attr_set[MAX_FIXED_K + 1] = {};
     if (!attr_set[cv.k]) {
         hipError_t e = hipFuncSetAttribute((const void*)k_bresolve, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)(budget - static_bytes));
+                                           (int)(150u * 1024u - static_bytes));
         if (e != hipSuccess) return e;
         ALLL_DISPATCH_K(cv.k, (e = hipFuncSetAttribute((const void*)k_bscatter<(K > 0 ? K : 1)>,
                                                        hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -399,12 +399,18 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     if (fixed_k > 0 && !(opt.flags & ALLL_FLAG_ATOMIC_CLAIMS) && n_tiles > 0 && c->n_vars > 0) {
         uint32_t shift = BKT_SHIFT_MIN;
         while (shift < BKT_SHIFT_MAX && ((uint64_t)c->n_vars >> shift) > 768) ++shift;
+        if (const char* e = getenv("ALLL_BKT_SHIFT"))  // tuning experiments
+            shift = std::min<uint32_t>(BKT_SHIFT_MAX, std::max<uint32_t>(BKT_SHIFT_MIN, (uint32_t)atoi(e)));
         const uint64_t nb = ((uint64_t)c->n_vars + (1u << shift) - 1) >> shift;
         if (nb <= BKT_MAX) {
             b.bkt_shift = shift;
             b.n_bkt = (uint32_t)nb;
             // about one run per CU (k_bscatter holds one 1024-thread workgroup per CU)
             b.run_tiles = std::max<uint32_t>(1, std::min<uint32_t>(RUN_TILES_MAX, (n_tiles + 255) / 256));
+            if (const char* e = getenv("ALLL_RUN_TILES"))  // tuning experiments
+                b.run_tiles = std::max<uint32_t>(1, std::min<uint32_t>(RUN_TILES_MAX, (uint32_t)atoi(e)));
+            b.resolve_lds = 40u * 1024u;  // k_bresolve: stage only small buckets, 3 workgroups per CU
+            if (const char* e = getenv("ALLL_RESOLVE_LDS")) b.resolve_lds = (uint32_t)atoi(e) * 1024u;
             b.n_runs = (n_tiles + b.run_tiles - 1) / b.run_tiles;
             const size_t run_cap = (size_t)b.run_tiles * TILE * fixed_k;
             if ((rc = dalloc(c, &b.pairs, (size_t)b.n_runs * run_cap))) return bail(rc);

@@ -107,6 +107,8 @@ def main():
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--exchange", default="allgather", choices=["allgather", "allreduce"])
     ap.add_argument("--no-ranged", action="store_true", help="use the L2-gather eval kernel")
+    ap.add_argument("--atomic-claims", action="store_true", help="LFMIS round 0 by global atomics")
+    ap.add_argument("--grid-rounds", type=int, default=0, help="full-grid LFMIS rounds (0 = default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--event-iters", type=int, default=10,
@@ -147,11 +149,13 @@ def main():
         flags |= N.FLAG_EXCHANGE_ALLREDUCE
     if args.no_ranged:
         flags |= N.FLAG_NO_RANGED
+    if args.atomic_claims:
+        flags |= N.FLAG_ATOMIC_CLAIMS
     t0 = time.perf_counter()
     exchange_impl = "rccl" if world > 1 else "none"
     try:
         s = Solver(n, offs, lits, seed=args.seed, device=local_rank, rank=rank, world=world,
-                   comm_id=comm_id, flags=flags)
+                   comm_id=comm_id, flags=flags, grid_rounds=args.grid_rounds)
     except N.AlllError as e:
         if world == 1 or e.code != N.ALLL_ERR_RCCL:
             raise
@@ -161,7 +165,7 @@ def main():
         log(f"[rank {rank}] RCCL init failed ({e}); using the host-staged gloo exchange")
         exchange_impl = "host-gloo"
         s = Solver(n, offs, lits, seed=args.seed, device=local_rank, rank=rank, world=world,
-                   flags=flags, exchange=gloo_exchange())
+                   flags=flags, grid_rounds=args.grid_rounds, exchange=gloo_exchange())
     del offs, lits
     t_create = time.perf_counter() - t0
     log(f"[rank {rank}] generated {m} clauses in {t_gen:.2f}s, uploaded in {t_create:.2f}s, "

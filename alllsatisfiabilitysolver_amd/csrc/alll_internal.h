@@ -42,6 +42,8 @@ constexpr unsigned long long PAIR_LOSE = 1ull << 31;
 // reduce start, LFMIS tail end}.
 constexpr uint32_t TIME_SLOTS = 4096;
 constexpr uint32_t TIME_FIELDS = 4;
+// Diagnostics: DBG_KERNELS regions x DBG_BLOCKS workgroups x DBG_FIELDS phase stamps (last iteration).
+constexpr uint32_t DBG_KERNELS = 4, DBG_BLOCKS = 8192, DBG_FIELDS = 8;
 
 // Device-resident loop state.  Written only by the single-block reduce / tail kernels,
 // read by every other kernel at entry (kernel boundaries order the accesses).
@@ -99,7 +101,8 @@ struct LoopBuffers {
     uint32_t n_bkt;
     uint32_t run_tiles;
     uint32_t n_runs;
-    uint32_t resolve_lds;       // LDS budget of a k_bresolve workgroup (bytes)
+    unsigned long long* kdbg;   // diagnostics (env ALLL_DEBUG_PHASES): per-workgroup phase stamps
+    uint32_t experiment;        // diagnostics (env ALLL_EXPERIMENT): timing-only variants, results invalid
     uint32_t n_vars;
     uint32_t n_words;
     uint32_t n_tiles;       // tiles covering [0, m)

@@ -82,6 +82,11 @@ __device__ __forceinline__ unsigned long long* time_slot(const LoopBuffers& b, u
 __device__ __forceinline__ unsigned long long wall_now() {
     return (unsigned long long)__builtin_amdgcn_s_memrealtime();
 }
+// diagnostics: phase stamp of this workgroup (thread 0) in kernel region `kr`
+__device__ __forceinline__ void dbg_stamp(const LoopBuffers& b, uint32_t kr, uint32_t phase) {
+    if (b.kdbg && threadIdx.x == 0 && blockIdx.x < DBG_BLOCKS)
+        b.kdbg[((uint64_t)kr * DBG_BLOCKS + blockIdx.x) * DBG_FIELDS + phase] = wall_now();
+}
 // one stamp per workgroup (thread 0); only loop evaluations (gated) are timed
 __device__ __forceinline__ void stamp_eval_begin(const LoopBuffers& b, int gated) {
     if (gated && b.ktime && threadIdx.x == 0) atomicMin(time_slot(b, b.state->n_iter), wall_now());
@@ -709,7 +714,9 @@ __global__ __launch_bounds__(BSC_THREADS) void k_bscatter(ClauseView cv, LoopBuf
     if (hot) ht.init();
     const uint32_t nb = b.n_bkt, sh = b.bkt_shift;
     for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) s_hist[i] = 0;
+    dbg_stamp(b, 0, 0);
     const uint32_t E = run_prefix(b, t0, nt, s_tc, s_pre);
+    dbg_stamp(b, 0, 1);
     const bool single = E <= blockDim.x * U;
     const unsigned long long keyhi = (unsigned long long)(~st->round_base) << 32;
     Ent<K> e[U];
@@ -739,7 +746,9 @@ __global__ __launch_bounds__(BSC_THREADS) void k_bscatter(ClauseView cv, LoopBuf
             }
         }
     }
+    dbg_stamp(b, 0, 2);
     __syncthreads();
+    dbg_stamp(b, 0, 3);
     if (hot) ht.flush(owner_of(b, st->round_base));
     // exclusive scan of the histogram: run-local start of every bucket
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -768,6 +777,7 @@ __global__ __launch_bounds__(BSC_THREADS) void k_bscatter(ClauseView cv, LoopBuf
     }
     if (threadIdx.x == 0) b.run_pairs[r] = total;
     __syncthreads();
+    dbg_stamp(b, 0, 4);
     // pass 2: pairs grouped by bucket, staged in LDS when they fit so that the run's area is
     // written with whole-line stores
     unsigned long long* gpr = b.pairs + (uint64_t)r * b.run_tiles * TILE * K;
@@ -798,24 +808,28 @@ __global__ __launch_bounds__(BSC_THREADS) void k_bscatter(ClauseView cv, LoopBuf
             emit();
         }
     }
+    dbg_stamp(b, 0, 5);
     if (staged) {
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < total; i += blockDim.x) gpr[i] = s_pairs[i];
     }
+    dbg_stamp(b, 0, 6);
 }
 
 // Workgroup per bucket.  The run table column is processed in batches of BKT_RUN_BATCH runs:
 // segment starts and a prefix of segment lengths in LDS make the batch's pairs one flat index
 // space; a wave takes 64 consecutive items per step (coalesced loads: a segment is contiguous)
-// and each lane finds its item's run by a fixed-depth binary search, BKT_UNROLL items
-// interleaved.  When the bucket's pairs fit the LDS stage (one batch, stage_cap items), the
-// pairs and their positions stay in LDS for the marking pass; otherwise it re-reads them.
+// and each lane finds its item's run by a fixed-depth branch-free binary search, BRS_UNROLL
+// items interleaved.  When the bucket's pairs fit one unrolled sweep of the workgroup (the
+// common case), they stay in registers between the minimum and the marking pass; otherwise
+// the marking pass re-reads them.  Every pair is written back, with PAIR_LOSE set when it is
+// not its variable's minimum: a segment's pairs are contiguous, so these are whole-line stores.
 constexpr uint32_t BKT_RUN_BATCH = 1024;
+constexpr int BRS_THREADS = 512;
+constexpr int BRS_UNROLL = 16;  // one sweep covers 8192 pairs (~7.4k per bucket at 10M clauses)
 
 struct ResolveLds {
     uint32_t* min;          // 1 << bkt_shift
-    unsigned long long* sx; // stage: pairs
-    uint32_t* sp;           // stage: positions in b.pairs
     uint32_t* start;        // batch: segment start in the run area
     uint32_t* pre;          // batch: exclusive prefix of segment lengths (pre[nr] = total)
     uint32_t* wsum;
@@ -856,100 +870,103 @@ __device__ __forceinline__ uint32_t resolve_batch(const LoopBuffers& b, const Re
     return total;
 }
 
-// Position of flat item f of the batch: largest q with pre[q] <= f (fixed depth: log2 nr steps;
-// a run with an empty segment shares its prefix with the next one, and the largest wins).
-__device__ __forceinline__ uint64_t resolve_pos(const ResolveLds& L, uint32_t rb, uint32_t nr, uint32_t f,
-                                                uint64_t run_cap) {
+// Position of flat item f of the batch: largest q with pre[q] <= f (fixed depth, branch-free:
+// BKT_RUN_BATCH = 2^10 runs at most; a run with an empty segment shares its prefix with the
+// next one, and the largest wins).
+__device__ __forceinline__ uint32_t resolve_pos(const ResolveLds& L, uint32_t rb, uint32_t nr, uint32_t f,
+                                                uint32_t run_cap) {
     uint32_t lo = 0;
-    for (uint32_t half = 1u << (31 - __clz(nr)); half; half >>= 1) {
-        const uint32_t mid = lo + half;
-        if (mid < nr && L.pre[mid] <= f) lo = mid;
+#pragma unroll
+    for (int step = 9; step >= 0; --step) {
+        const uint32_t mid = lo + (1u << step);
+        lo = (mid < nr && L.pre[min(mid, nr)] <= f) ? mid : lo;
     }
-    return (uint64_t)(rb + lo) * run_cap + L.start[lo] + (f - L.pre[lo]);
+    return (rb + lo) * run_cap + L.start[lo] + (f - L.pre[lo]);
 }
 
-__global__ __launch_bounds__(BKT_THREADS) void k_bresolve(LoopBuffers b, uint64_t run_cap, uint32_t stage_cap) {
+// One unrolled sweep over the batch items f0 + 64 u (u < BRS_UNROLL): positions and pairs
+// (items past np load the batch's last pair again; callers ignore them).
+__device__ __forceinline__ void resolve_load(const LoopBuffers& b, const ResolveLds& L, uint32_t rb, uint32_t nr,
+                                             uint32_t np, uint32_t f0, uint32_t run_cap, uint32_t* pos,
+                                             unsigned long long* x) {
+#pragma unroll
+    for (int u = 0; u < BRS_UNROLL; ++u) pos[u] = resolve_pos(L, rb, nr, min(f0 + 64 * u, np - 1), run_cap);
+#pragma unroll
+    for (int u = 0; u < BRS_UNROLL; ++u) x[u] = b.pairs[pos[u]];
+}
+
+__device__ __forceinline__ unsigned long long resolve_mark(const ResolveLds& L, unsigned long long x) {
+    return L.min[(uint32_t)x & 0x7FFFu] != (uint32_t)(x >> 32) ? (x | PAIR_LOSE) : x;
+}
+
+__global__ __launch_bounds__(BRS_THREADS, 2) void k_bresolve(LoopBuffers b, uint32_t run_cap) {
     if (!b.state->active) return;
-    constexpr int U = BKT_UNROLL;
-    extern __shared__ unsigned long long s_dyn[];
+    constexpr int U = BRS_UNROLL;
+    extern __shared__ uint32_t s_min[];
     __shared__ uint32_t s_start[BKT_RUN_BATCH], s_pre[BKT_RUN_BATCH + 1];
-    __shared__ uint32_t s_wsum[BKT_THREADS / 64];
+    __shared__ uint32_t s_wsum[BRS_THREADS / 64];
     const uint32_t bv = 1u << b.bkt_shift;
-    ResolveLds L;
-    L.sx = s_dyn;
-    L.sp = reinterpret_cast<uint32_t*>(s_dyn + stage_cap);
-    L.min = L.sp + stage_cap;
-    L.start = s_start; L.pre = s_pre; L.wsum = s_wsum;
+    ResolveLds L{s_min, s_start, s_pre, s_wsum};
+    dbg_stamp(b, 1, 0);
     for (uint32_t i = threadIdx.x; i < bv; i += blockDim.x) L.min[i] = ~0u;
-    __syncthreads();
+    // items of a wave: f0 + 64 u, f0 = wave * 64 U + lane (+ stride per sweep)
+    const uint32_t first = (threadIdx.x >> 6) * 64 * U + (threadIdx.x & 63);
     const uint32_t stride = blockDim.x * U;
-    for (uint32_t rb = 0; rb < b.n_runs; rb += BKT_RUN_BATCH) {
-        const uint32_t nr = min(BKT_RUN_BATCH, b.n_runs - rb);
-        const uint32_t np = resolve_batch(b, L, rb, nr);
-        const bool staged = rb == 0 && nr == b.n_runs && np <= stage_cap;
-        // items of a wave: base + lane + 64 u, base = wave * 64 U (+ stride per step)
-        for (uint32_t f0 = (threadIdx.x >> 6) * 64 * U + (threadIdx.x & 63); f0 < np; f0 += stride) {
-            uint64_t pos[U];
-            unsigned long long x[U];
+    uint32_t pos[U];  // pair positions (the pair area holds < 2^32 pairs, checked at create)
+    unsigned long long x[U];
+    if (b.n_runs <= BKT_RUN_BATCH) {
+        const uint32_t np = resolve_batch(b, L, 0, b.n_runs);  // (its barriers also publish L.min)
+        dbg_stamp(b, 1, 1);
+        if (np <= stride) {
+            if (np > 0) {
+                resolve_load(b, L, 0, b.n_runs, np, first, run_cap, pos, x);
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint32_t f = f0 + 64 * u;
-                if (f < np) pos[u] = resolve_pos(L, rb, nr, f, run_cap);
+                for (int u = 0; u < U; ++u)  // a clamped duplicate of the last pair is harmless
+                    atomicMin(&L.min[(uint32_t)x[u] & 0x7FFFu], (uint32_t)(x[u] >> 32));
             }
+            dbg_stamp(b, 1, 2);
+            __syncthreads();
+            dbg_stamp(b, 1, 3);
+            if (np > 0) {
 #pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (f0 + 64 * u < np) x[u] = b.pairs[pos[u]];
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint32_t f = f0 + 64 * u;
-                if (f >= np) continue;
-                atomicMin(&L.min[(uint32_t)x[u] & 0x7FFFu], (uint32_t)(x[u] >> 32));
-                if (staged) { L.sx[f] = x[u]; L.sp[f] = (uint32_t)pos[u]; }
+                for (int u = 0; u < U; ++u)
+                    if (first + 64 * u < np) b.pairs[pos[u]] = resolve_mark(L, x[u]);
             }
-        }
-        __syncthreads();
-        if (staged) {
-            for (uint32_t i = threadIdx.x; i < np; i += blockDim.x) {
-                const unsigned long long x = L.sx[i];
-                if (L.min[(uint32_t)x & 0x7FFFu] != (uint32_t)(x >> 32)) b.pairs[L.sp[i]] = x | PAIR_LOSE;
-            }
+            dbg_stamp(b, 1, 4);
             return;
         }
     }
-    // marking pass, re-reading the pairs
-    for (uint32_t rb = 0; rb < b.n_runs; rb += BKT_RUN_BATCH) {
-        const uint32_t nr = min(BKT_RUN_BATCH, b.n_runs - rb);
-        const uint32_t np = resolve_batch(b, L, rb, nr);
-        for (uint32_t f0 = (threadIdx.x >> 6) * 64 * U + (threadIdx.x & 63); f0 < np; f0 += stride) {
-            uint64_t pos[U];
-            unsigned long long x[U];
+    __syncthreads();
+    for (int pass = 0; pass < 2; ++pass) {
+        for (uint32_t rb = 0; rb < b.n_runs; rb += BKT_RUN_BATCH) {
+            const uint32_t nr = min(BKT_RUN_BATCH, b.n_runs - rb);
+            const uint32_t np = resolve_batch(b, L, rb, nr);
+            for (uint32_t f0 = first; f0 < np; f0 += stride) {
+                resolve_load(b, L, rb, nr, np, f0, run_cap, pos, x);
 #pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint32_t f = f0 + 64 * u;
-                if (f < np) pos[u] = resolve_pos(L, rb, nr, f, run_cap);
+                for (int u = 0; u < U; ++u) {
+                    if (pass == 0) atomicMin(&L.min[(uint32_t)x[u] & 0x7FFFu], (uint32_t)(x[u] >> 32));
+                    else if (f0 + 64 * u < np) b.pairs[pos[u]] = resolve_mark(L, x[u]);
+                }
             }
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (f0 + 64 * u < np) x[u] = b.pairs[pos[u]];
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (f0 + 64 * u < np && L.min[(uint32_t)x[u] & 0x7FFFu] != (uint32_t)(x[u] >> 32))
-                    b.pairs[pos[u]] = x[u] | PAIR_LOSE;
+            __syncthreads();  // batch arrays are rewritten next; after pass 0: L.min is final
         }
-        __syncthreads();
     }
+    dbg_stamp(b, 1, 4);
 }
 
 // Workgroup per run: lose marks -> LDS byte per entry; then every entry of the run's tiles in
 // one flat loop: join (cover, MIS list of its tile) or survive (compacted into its tile's
 // list in `out`, or the tail's compact list when `last`).
+constexpr int BJN_THREADS = 1024;
+
 template <int K>
-__global__ __launch_bounds__(BKT_THREADS) void k_bjoin(ClauseView cv, LoopBuffers b, const uint32_t* in,
+__global__ __launch_bounds__(BJN_THREADS) void k_bjoin(ClauseView cv, LoopBuffers b, const uint32_t* in,
                                                        uint32_t* out, int last) {
     DevState* st = b.state;
     if (!st->active) return;
     constexpr int S = Ent<K>::S;
-    constexpr int U = 2 * BKT_UNROLL;
+    constexpr int U = K <= 4 ? 2 * BKT_UNROLL : BKT_UNROLL;
     const uint32_t r = blockIdx.x;
     const uint32_t t0 = r * b.run_tiles, nt = min(b.run_tiles, b.n_tiles - t0);
     extern __shared__ uint32_t s_lost[];  // one byte per entry slot of the run's tiles
@@ -963,7 +980,9 @@ __global__ __launch_bounds__(BKT_THREADS) void k_bjoin(ClauseView cv, LoopBuffer
         s_lits[threadIdx.x] = 0;
         s_mis0[threadIdx.x] = b.mis_cnt[t0 + threadIdx.x];
     }
+    dbg_stamp(b, 2, 0);
     const uint32_t E = run_prefix(b, t0, nt, s_tc, s_pre);
+    dbg_stamp(b, 2, 1);
     const bool single = E <= blockDim.x * U;
     Ent<K> e[U];
     bool ok[U];
@@ -972,18 +991,21 @@ __global__ __launch_bounds__(BKT_THREADS) void k_bjoin(ClauseView cv, LoopBuffer
     uint8_t* lost = reinterpret_cast<uint8_t*>(s_lost);
     const unsigned long long* pr = b.pairs + (uint64_t)r * b.run_tiles * TILE * K;
     const uint32_t np = b.run_pairs[r];
-    for (uint32_t i0 = threadIdx.x; i0 < np; i0 += blockDim.x * U) {
-        unsigned long long x[U];
+    constexpr int PU = 16;  // pairs per thread per sweep (~3 per clause: one sweep at 10M clauses)
+    for (uint32_t i0 = threadIdx.x; i0 < np; i0 += blockDim.x * PU) {
+        unsigned long long x[PU];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
+        for (int u = 0; u < PU; ++u) {
             const uint32_t i = i0 + u * blockDim.x;
             x[u] = i < np ? pr[i] : 0ull;
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u)
+        for (int u = 0; u < PU; ++u)
             if (x[u] & PAIR_LOSE) lost[(x[u] >> 15) & 0xFFFFu] = 1;
     }
+    dbg_stamp(b, 2, 2);
     __syncthreads();
+    dbg_stamp(b, 2, 3);
     const bool hot = cv.n_hot != 0;
     const unsigned long long keyhi = (unsigned long long)(~st->round_base) << 32;
     const unsigned long long* owner = owner_of(b, st->round_base);
@@ -1019,6 +1041,7 @@ __global__ __launch_bounds__(BKT_THREADS) void k_bjoin(ClauseView cv, LoopBuffer
             decide();
         }
     }
+    dbg_stamp(b, 2, 4);
     __syncthreads();
     if (threadIdx.x < nt) {
         const uint32_t tt = threadIdx.x, tile = t0 + tt, kept = s_keep[tt];
@@ -1040,6 +1063,7 @@ __global__ __launch_bounds__(BKT_THREADS) void k_bjoin(ClauseView cv, LoopBuffer
             for (uint32_t i = threadIdx.x; i < kept * S; i += blockDim.x) dst[i] = src[i];
         }
     }
+    dbg_stamp(b, 2, 5);
 }
 
 // Tail: one workgroup finishes the LFMIS over the compact list handed over by the last grid
@@ -1298,18 +1322,11 @@ hipError_t launch_round0_buckets(const ClauseView& cv, const LoopBuffers& b, boo
     // buffers as CLAIM(0) + JOIN(0): eval -> stage[0] (ids translated in place); JOIN stage[0] -> stage[1]
     if (b.n_tiles == 0 || cv.k == 0 || !b.pairs) return hipErrorInvalidValue;
     const uint64_t run_cap = (uint64_t)b.run_tiles * TILE * cv.k;
-    // k_bresolve LDS: minima (4 << shift) + a stage of 12-byte slots within ~150 KiB in all
-    const uint32_t min_bytes = 4u << b.bkt_shift;
-    const uint32_t static_bytes = 2 * BKT_RUN_BATCH * 4 + 64;
-    const uint32_t budget = b.resolve_lds;
-    uint32_t stage_cap = budget > min_bytes + static_bytes ? (budget - min_bytes - static_bytes) / 12 : 0;
-    if (min_bytes + static_bytes + stage_cap * 12 > 150u * 1024u) stage_cap = 0;
-    stage_cap = std::min<uint32_t>(stage_cap, 8192);
-    const size_t lds = (size_t)min_bytes + (size_t)stage_cap * 12;
+    const size_t lds = (size_t)4 << b.bkt_shift;  // k_bresolve minima
     static bool attr_set[MAX_FIXED_K + 1] = {};
     if (!attr_set[cv.k]) {
         hipError_t e = hipFuncSetAttribute((const void*)k_bresolve, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)(150u * 1024u - static_bytes));
+                                           (int)(4u << BKT_SHIFT_MAX));
         if (e != hipSuccess) return e;
         ALLL_DISPATCH_K(cv.k, (e = hipFuncSetAttribute((const void*)k_bscatter<(K > 0 ? K : 1)>,
                                                        hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1324,11 +1341,11 @@ hipError_t launch_round0_buckets(const ClauseView& cv, const LoopBuffers& b, boo
     ALLL_DISPATCH_K(cv.k, (k_bscatter<(K > 0 ? K : 1)><<<b.n_runs, BSC_THREADS, BKT_STAGE * 8, s>>>(cv, b, b.stage[0])));
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    k_bresolve<<<b.n_bkt, BKT_THREADS, lds, s>>>(b, run_cap, stage_cap);
+    k_bresolve<<<b.n_bkt, BRS_THREADS, lds, s>>>(b, (uint32_t)run_cap);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     const int l = last ? 1 : 0;
-    ALLL_DISPATCH_K(cv.k, (k_bjoin<(K > 0 ? K : 1)><<<b.n_runs, BKT_THREADS, (size_t)b.run_tiles * TILE, s>>>(
+    ALLL_DISPATCH_K(cv.k, (k_bjoin<(K > 0 ? K : 1)><<<b.n_runs, BJN_THREADS, (size_t)b.run_tiles * TILE, s>>>(
                               cv, b, b.stage[0], b.stage[1], l)));
     return hipGetLastError();
 }

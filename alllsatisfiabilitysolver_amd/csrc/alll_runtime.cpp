@@ -391,26 +391,32 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
         if (hipStreamSynchronize(c->stream) != hipSuccess ||
             hipMemcpy(b.ktime, init.data(), init.size() * 8, hipMemcpyHostToDevice) != hipSuccess)
             return bail(fail(ALLL_ERR_HIP, "timing buffer upload failed"));
+    }
+    {
         int khz = 0;
         if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) == hipSuccess && khz > 0)
             c->wall_khz = khz;
     }
-    // ---- bucketed LFMIS round 0 (fixed width): ~768 buckets, runs of up to 16 tiles
+    if (const char* e = getenv("ALLL_EXPERIMENT")) b.experiment = (uint32_t)atoi(e);  // diagnostics only
+    if (getenv("ALLL_DEBUG_PHASES")) {  // diagnostics only
+        if ((rc = dalloc(c, &b.kdbg, (size_t)DBG_KERNELS * DBG_BLOCKS * DBG_FIELDS))) return bail(rc);
+    }
+    // ---- bucketed LFMIS round 0 (fixed width): ~300 buckets, runs of up to 16 tiles
     if (fixed_k > 0 && !(opt.flags & ALLL_FLAG_ATOMIC_CLAIMS) && n_tiles > 0 && c->n_vars > 0) {
         uint32_t shift = BKT_SHIFT_MIN;
-        while (shift < BKT_SHIFT_MAX && ((uint64_t)c->n_vars >> shift) > 768) ++shift;
+        while (shift < BKT_SHIFT_MAX && ((uint64_t)c->n_vars >> shift) > 384) ++shift;
         if (const char* e = getenv("ALLL_BKT_SHIFT"))  // tuning experiments
             shift = std::min<uint32_t>(BKT_SHIFT_MAX, std::max<uint32_t>(BKT_SHIFT_MIN, (uint32_t)atoi(e)));
         const uint64_t nb = ((uint64_t)c->n_vars + (1u << shift) - 1) >> shift;
-        if (nb <= BKT_MAX) {
+        // about one run per CU (k_bscatter holds one 1024-thread workgroup per CU)
+        uint32_t rt = std::max<uint32_t>(1, std::min<uint32_t>(RUN_TILES_MAX, (n_tiles + 255) / 256));
+        if (const char* e = getenv("ALLL_RUN_TILES"))  // tuning experiments
+            rt = std::max<uint32_t>(1, std::min<uint32_t>(RUN_TILES_MAX, (uint32_t)atoi(e)));
+        const uint64_t area = (uint64_t)((n_tiles + rt - 1) / rt) * rt * TILE * fixed_k;  // pairs
+        if (nb <= BKT_MAX && area < (1ull << 32)) {  // pair positions are 32-bit in k_bresolve
             b.bkt_shift = shift;
             b.n_bkt = (uint32_t)nb;
-            // about one run per CU (k_bscatter holds one 1024-thread workgroup per CU)
-            b.run_tiles = std::max<uint32_t>(1, std::min<uint32_t>(RUN_TILES_MAX, (n_tiles + 255) / 256));
-            if (const char* e = getenv("ALLL_RUN_TILES"))  // tuning experiments
-                b.run_tiles = std::max<uint32_t>(1, std::min<uint32_t>(RUN_TILES_MAX, (uint32_t)atoi(e)));
-            b.resolve_lds = 40u * 1024u;  // k_bresolve: stage only small buckets, 3 workgroups per CU
-            if (const char* e = getenv("ALLL_RESOLVE_LDS")) b.resolve_lds = (uint32_t)atoi(e) * 1024u;
+            b.run_tiles = rt;
             b.n_runs = (n_tiles + b.run_tiles - 1) / b.run_tiles;
             const size_t run_cap = (size_t)b.run_tiles * TILE * fixed_k;
             if ((rc = dalloc(c, &b.pairs, (size_t)b.n_runs * run_cap))) return bail(rc);
@@ -820,6 +826,17 @@ int alll_loop_times(alll_ctx* c, uint64_t first_iter, uint64_t n_iters, alll_pha
     if (ne) { out->eval_ms = se / ne; out->exchange_ms = sx / ne; }
     if (nm) out->mis_ms = sm / nm;
     if (nt) { out->resample_ms = sr / nt; out->total_ms = st / nt; }
+    return ALLL_OK;
+}
+
+int alll_debug_phases(alll_ctx* c, uint64_t* out, uint64_t n, int* wall_khz) {
+    if (!c || !out) return fail(ALLL_ERR_INVALID_ARG, "null argument");
+    if (!c->b.kdbg) return fail(ALLL_ERR_INVALID_ARG, "created without ALLL_DEBUG_PHASES in the environment");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    n = std::min<uint64_t>(n, (uint64_t)DBG_KERNELS * DBG_BLOCKS * DBG_FIELDS);
+    HIP_TRY(hipMemcpy(out, c->b.kdbg, n * 8, hipMemcpyDeviceToHost));
+    if (wall_khz) *wall_khz = c->wall_khz;
     return ALLL_OK;
 }
 

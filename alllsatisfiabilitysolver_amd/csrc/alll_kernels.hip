@@ -202,10 +202,11 @@ __global__ __launch_bounds__(EVAL_THREADS) void k_eval_fixed(ClauseView cv, Loop
 #pragma unroll
             for (int j = 0; j < K; ++j) x[j] = src[j * 64];
 #pragma unroll
-            for (int j = 0; j < K; ++j) {
+            for (int j = 0; j < K; ++j) {  // satisfied clauses skip their remaining lookups
                 const uint32_t xs[4] = {x[j].x, x[j].y, x[j].z, x[j].w};
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
+                    if (j > 0 && sat[q]) continue;
                     const uint32_t l = xs[q] & LIT_MASK;
                     sat[q] |= abit(A, l >> 1) ^ (l & 1u);
                 }
@@ -294,11 +295,14 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
                 const uint4* src = reinterpret_cast<const uint4*>(cv.lits_t + cb * K) + lane;
 #pragma unroll
                 for (int j = 0; j < K; ++j) x[j] = src[j * 64];
+                // slot by slot (largest variable first): a clause already satisfied skips the
+                // lookups of its remaining literals (half of them after slot 0, 3/4 after slot 1)
 #pragma unroll
                 for (int j = 0; j < K; ++j) {
                     const uint32_t xs[4] = {x[j].x, x[j].y, x[j].z, x[j].w};
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
+                        if (j > 0 && sat[q]) continue;
                         const uint32_t v = (xs[q] & LIT_MASK) >> 1;
                         const uint32_t w = (v < lds_vars) ? s_A[v >> 5] : A[v >> 5];
                         sat[q] |= ((w >> (v & 31u)) & 1u) ^ (xs[q] & 1u);
@@ -357,7 +361,7 @@ __global__ __launch_bounds__(EVAL_THREADS) void k_eval_csr(ClauseView cv, LoopBu
         if (c < m) {
             const uint32_t o0 = offs[c], o1 = offs[c + 1];
             uint32_t sat = 0;
-            for (uint32_t j = o0; j < o1; ++j) {
+            for (uint32_t j = o0; j < o1 && !sat; ++j) {
                 const uint32_t l = lits[j] & LIT_MASK;
                 sat |= abit(A, l >> 1) ^ (l & 1u);
             }

@@ -74,9 +74,11 @@ struct alll_ctx {
     // device allocations
     std::vector<void*> allocs;
     DevState* h_state = nullptr;  // pinned mirror
-    hipGraph_t graph = nullptr;
-    hipGraphExec_t graph_exec = nullptr;
+    // one captured iteration per LFMIS round-0 variant (0: atomic claims, 1: bucketed)
+    hipGraph_t graph[2] = {};
+    hipGraphExec_t graph_exec[2] = {};
     bool use_graph = true;
+    uint64_t bucket_min_u = 0;  // bucketed round 0 when the last pass found at least this many
     hipEvent_t ev[8] = {};
     int n_cu = 256;
     bool hybrid = false;
@@ -150,7 +152,15 @@ int host_exchange(alll_ctx* c, int op, void* dev, size_t bytes, size_t own_off) 
 
 // The launch sequence of one iteration (SATInstance.h:260-311).  Every kernel is gated on
 // the device state, so replaying it after convergence is a no-op.
-int enqueue_iteration(alll_ctx* c, hipEvent_t* marks) {
+// Round-0 variant for the next iterations, from the last state read: the bucketed kernels
+// have a fixed cost that only pays off on large violated sets (and they are not built for
+// skewed instances, see create).
+int round0_variant(const alll_ctx* c) {
+    if (!c->b.pairs) return 0;
+    return (c->h_state->n_iter == 0 || c->h_state->u_total >= c->bucket_min_u) ? 1 : 0;
+}
+
+int enqueue_iteration(alll_ctx* c, hipEvent_t* marks, int variant) {
     hipStream_t s = c->stream;
     if (marks) HIP_TRY(hipEventRecord(marks[0], s));
     HIP_TRY(eval_launch(c, c->own_begin, c->own_end, true));
@@ -169,7 +179,7 @@ int enqueue_iteration(alll_ctx* c, hipEvent_t* marks) {
     if (marks) HIP_TRY(hipEventRecord(marks[2], s));
     HIP_TRY(launch_reduce(c->b, 0, s));
     for (uint32_t r = 0; r < c->grid_rounds; ++r) {
-        if (r == 0 && c->b.pairs) HIP_TRY(launch_round0_buckets(c->cv, c->b, c->grid_rounds == 1, s));
+        if (r == 0 && variant == 1) HIP_TRY(launch_round0_buckets(c->cv, c->b, c->grid_rounds == 1, s));
         else HIP_TRY(launch_round(c->cv, c->b, r, r + 1 == c->grid_rounds, s));
     }
     HIP_TRY(launch_tail(c->cv, c->b, c->grid_rounds, s));
@@ -190,11 +200,11 @@ int enqueue_iteration(alll_ctx* c, hipEvent_t* marks) {
     return ALLL_OK;
 }
 
-int ensure_graph(alll_ctx* c) {
-    if (!c->use_graph || c->graph_exec) return ALLL_OK;
+int ensure_graph(alll_ctx* c, int variant) {
+    if (!c->use_graph || c->graph_exec[variant]) return ALLL_OK;
     hipError_t e = hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal);
     if (e != hipSuccess) { c->use_graph = false; return ALLL_OK; }
-    int rc = enqueue_iteration(c, nullptr);
+    int rc = enqueue_iteration(c, nullptr, variant);
     hipGraph_t g = nullptr;
     e = hipStreamEndCapture(c->stream, &g);
     if (rc != ALLL_OK || e != hipSuccess || !g) {
@@ -203,25 +213,26 @@ int ensure_graph(alll_ctx* c) {
         c->use_graph = false;  // fall back to eager launches
         return ALLL_OK;
     }
-    e = hipGraphInstantiate(&c->graph_exec, g, nullptr, nullptr, 0);
+    e = hipGraphInstantiate(&c->graph_exec[variant], g, nullptr, nullptr, 0);
     if (e != hipSuccess) {
         (void)hipGraphDestroy(g);
-        c->graph_exec = nullptr;
+        c->graph_exec[variant] = nullptr;
         c->use_graph = false;
         return ALLL_OK;
     }
-    c->graph = g;
+    c->graph[variant] = g;
     return ALLL_OK;
 }
 
 int launch_iterations(alll_ctx* c, uint64_t n) {
-    int rc = ensure_graph(c);
+    const int variant = round0_variant(c);
+    int rc = ensure_graph(c, variant);
     if (rc) return rc;
     for (uint64_t i = 0; i < n; ++i) {
         if (c->use_graph) {
-            HIP_TRY(hipGraphLaunch(c->graph_exec, c->stream));
+            HIP_TRY(hipGraphLaunch(c->graph_exec[variant], c->stream));
         } else {
-            rc = enqueue_iteration(c, nullptr);
+            rc = enqueue_iteration(c, nullptr, variant);
             if (rc) return rc;
         }
     }
@@ -408,12 +419,23 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
         if (const char* e = getenv("ALLL_BKT_SHIFT"))  // tuning experiments
             shift = std::min<uint32_t>(BKT_SHIFT_MAX, std::max<uint32_t>(BKT_SHIFT_MIN, (uint32_t)atoi(e)));
         const uint64_t nb = ((uint64_t)c->n_vars + (1u << shift) - 1) >> shift;
+        // skewed literal distribution (power-law hubs): the fullest bucket's workgroup would
+        // serialise the round; such instances keep the atomic claims (with hot-variable
+        // aggregation), which handle skew better
+        bool skewed = false;
+        if (nb <= BKT_MAX) {
+            std::vector<uint64_t> load(nb, 0);
+            const uint64_t L_all = prob->offsets[m];
+            for (uint64_t j = 0; j < L_all; ++j) ++load[(prob->literals[j] >> 1) >> shift];
+            const uint64_t mx = *std::max_element(load.begin(), load.end());
+            skewed = mx > 4 * (L_all / nb + 1);
+        }
         // about one run per CU (k_bscatter holds one 1024-thread workgroup per CU)
         uint32_t rt = std::max<uint32_t>(1, std::min<uint32_t>(RUN_TILES_MAX, (n_tiles + 255) / 256));
         if (const char* e = getenv("ALLL_RUN_TILES"))  // tuning experiments
             rt = std::max<uint32_t>(1, std::min<uint32_t>(RUN_TILES_MAX, (uint32_t)atoi(e)));
         const uint64_t area = (uint64_t)((n_tiles + rt - 1) / rt) * rt * TILE * fixed_k;  // pairs
-        if (nb <= BKT_MAX && area < (1ull << 32)) {  // pair positions are 32-bit in k_bresolve
+        if (nb <= BKT_MAX && !skewed && area < (1ull << 32)) {  // pair positions are 32-bit in k_bresolve
             b.bkt_shift = shift;
             b.n_bkt = (uint32_t)nb;
             b.run_tiles = rt;
@@ -422,6 +444,9 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
             if ((rc = dalloc(c, &b.pairs, (size_t)b.n_runs * run_cap))) return bail(rc);
             if ((rc = dalloc(c, &b.runtab, (size_t)b.n_bkt * b.n_runs))) return bail(rc);
             if ((rc = dalloc(c, &b.run_pairs, b.n_runs))) return bail(rc);
+            // below this many violated clauses the atomic round 0 is cheaper (fixed costs)
+            c->bucket_min_u = std::max<uint64_t>(65536, m / 64);
+            if (const char* e = getenv("ALLL_BUCKET_MIN_U")) c->bucket_min_u = strtoull(e, nullptr, 10);
         }
     }
     // ---- clause storage allocations, then drain the zero-fills before synchronous uploads
@@ -571,8 +596,10 @@ int alll_destroy(alll_ctx* c) {
     if (!c) return ALLL_OK;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    if (c->graph_exec) (void)hipGraphExecDestroy(c->graph_exec);
-    if (c->graph) (void)hipGraphDestroy(c->graph);
+    for (int v = 0; v < 2; ++v) {
+        if (c->graph_exec[v]) (void)hipGraphExecDestroy(c->graph_exec[v]);
+        if (c->graph[v]) (void)hipGraphDestroy(c->graph[v]);
+    }
     if (c->comm) ncclCommDestroy(c->comm);
     for (void* p : c->allocs) (void)hipFree(p);
     for (auto& e : c->ev)
@@ -768,7 +795,7 @@ int alll_profile(alll_ctx* c, uint64_t n_iters, alll_phase_times* out) {
     if ((rc = write_limits(c, c->h_state->n_iter + n_iters, ~0ull))) return rc;
     double acc[4] = {0, 0, 0, 0};
     for (uint64_t i = 0; i < n_iters; ++i) {
-        if ((rc = enqueue_iteration(c, c->ev))) return rc;
+        if ((rc = enqueue_iteration(c, c->ev, round0_variant(c)))) return rc;
         HIP_TRY(hipEventSynchronize(c->ev[4]));
         float t;
         for (int p = 0; p < 4; ++p) {

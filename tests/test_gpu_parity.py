@@ -21,7 +21,22 @@ from conftest import GOLDEN
 pytestmark = pytest.mark.gpu
 
 T1_FIXTURES = sorted(p for p in glob.glob(os.path.join(GOLDEN, "*_T1.npz")))
-LAYOUTS = {"hybrid": 0, "fixed": 1 << 3, "csr": 1 << 2, "atomic_claims": 1 << 5}
+# name -> (flags, environment at create): the default policy picks the bucketed LFMIS round 0
+# only for large violated sets, "buckets" forces it for every iteration
+LAYOUTS = {"hybrid": (0, {}), "fixed": (1 << 3, {}), "csr": (1 << 2, {}), "atomic_claims": (1 << 5, {}),
+           "buckets": (0, {"ALLL_BUCKET_MIN_U": "0"})}
+
+
+def make_solver(layout, monkeypatch, *args, **kw):
+    from alllsatisfiabilitysolver_amd import Solver
+
+    flags, env = LAYOUTS[layout]
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    s = Solver(*args, flags=flags, **kw)
+    for k in env:
+        monkeypatch.delenv(k)
+    return s
 
 
 @pytest.fixture(scope="module")
@@ -40,13 +55,11 @@ def mask_to_list(vm, m):
 
 @pytest.mark.parametrize("layout", list(LAYOUTS))
 @pytest.mark.parametrize("path", T1_FIXTURES, ids=lambda p: os.path.basename(p)[:-4])
-def test_reference_maps_on_gpu(gpu, path, layout):
-    from alllsatisfiabilitysolver_amd import Solver
-
+def test_reference_maps_on_gpu(gpu, path, layout, monkeypatch):
     f = dict(np.load(path, allow_pickle=False))
     n, offs, lits = int(f["n_vars"]), f["offs"], f["lits"]
     m = offs.size - 1
-    with Solver(n, offs, lits, seed=3, flags=LAYOUTS[layout]) as s:
+    with make_solver(layout, monkeypatch, n, offs, lits, seed=3) as s:
         for i in range(f["A"].shape[0]):
             s.set_assignment_words(f["A"][i])
             before = s.stats()
@@ -103,14 +116,12 @@ def instances():
 @pytest.mark.parametrize("layout", list(LAYOUTS))
 @pytest.mark.parametrize("name", ["c1_ratio4", "u2500_ratio4", "ratio2_solves", "k8", "powerlaw",
                                   "k5_multi_tile", "powerlaw_hot", "edge", "ragged"])
-def test_trajectory_matches_oracle(gpu, oracle_mod, name, layout):
-    from alllsatisfiabilitysolver_amd import Solver
-
+def test_trajectory_matches_oracle(gpu, oracle_mod, name, layout, monkeypatch):
     o = oracle_mod
     n, offs, lits = instances()[name]
     seed, K = 12345, 40
     st_o, A_o, rows = o.solve(n, offs, lits, seed, max_iters=K, trace=True)
-    with Solver(n, offs, lits, seed=seed, flags=LAYOUTS[layout]) as s:
+    with make_solver(layout, monkeypatch, n, offs, lits, seed=seed) as s:
         np.testing.assert_array_equal(s.assignment_words(), o.init_assignment(seed, n))
         for it, nu, nm, dres, A_after in rows:
             before = s.stats()
@@ -121,7 +132,7 @@ def test_trajectory_matches_oracle(gpu, oracle_mod, name, layout):
             assert after["n_resamples"] - before["n_resamples"] == dres, f"iter {it}"
             np.testing.assert_array_equal(s.assignment_words(), A_after, err_msg=f"A after iter {it}")
     # whole solve with the same cap: identical Statistics and assignment
-    with Solver(n, offs, lits, seed=seed, max_iters=K, flags=LAYOUTS[layout]) as s:
+    with make_solver(layout, monkeypatch, n, offs, lits, seed=seed, max_iters=K) as s:
         st = s.solve()
         for k in ("n_iterations", "n_resamples", "avg_mis_size", "sum_mis_size", "solved"):
             assert st[k] == st_o[k], k
@@ -172,13 +183,14 @@ def test_empty_instance(gpu):
 
 
 @pytest.mark.parametrize("grid_rounds", [1, 2, 3, 8])
-def test_grid_round_split_is_invisible(gpu, oracle_mod, grid_rounds):
+def test_grid_round_split_is_invisible(gpu, oracle_mod, grid_rounds, monkeypatch):
     """The split between full-grid LFMIS rounds and the single-workgroup tail changes
     nothing: same trajectory as the oracle."""
     from alllsatisfiabilitysolver_amd import Solver
 
     n, offs, lits = instances()["k5_multi_tile"]
     st_o, A_o, rows = oracle_mod.solve(n, offs, lits, 77, max_iters=12, trace=True)
+    monkeypatch.setenv("ALLL_BUCKET_MIN_U", "0")  # round 0 bucketed (incl. last-round hand-off at G=1)
     with Solver(n, offs, lits, seed=77, max_iters=12, grid_rounds=grid_rounds) as s:
         st = s.solve()
         assert st["n_resamples"] == st_o["n_resamples"]

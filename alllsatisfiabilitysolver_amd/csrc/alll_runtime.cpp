@@ -54,6 +54,7 @@ int fail(int code, const char* fmt, ...) {
     } while (0)
 
 constexpr uint32_t DEFAULT_GRID_ROUNDS = 4;
+constexpr uint32_t SKEWED_GRID_ROUNDS = 6;  // instances with hot variables
 
 }  // namespace
 
@@ -484,6 +485,9 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
                 for (auto& l : flagged)
                     if (is_hot[l >> 1]) l |= 0x80000000u;
                 cv.n_hot = (uint32_t)hot.size();
+                // skewed instances need more rounds before the leftovers are few enough for
+                // the single-workgroup tail (power-law 3-SAT at 10M clauses: 10 rounds)
+                if (!opt.grid_rounds) c->grid_rounds = SKEWED_GRID_ROUNDS;
             }
         }
         const uint32_t* src = flagged.empty() ? prob->literals : flagged.data();

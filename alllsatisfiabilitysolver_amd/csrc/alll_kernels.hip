@@ -296,16 +296,40 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
 #pragma unroll
                 for (int j = 0; j < K; ++j) x[j] = src[j * 64];
                 // slot by slot (largest variable first): a clause already satisfied skips the
-                // lookups of its remaining literals (half of them after slot 0, 3/4 after slot 1)
+                // lookups of its remaining literals (half of them after slot 0, 3/4 after slot 1).
+                // Per slot, the global loads (words past the LDS range) of the lane's 4 clauses
+                // are issued first, then the LDS reads, into separate registers, and only then
+                // consumed: no load waits for another one.
 #pragma unroll
-                for (int j = 0; j < K; ++j) {
+                for (int jj = 0; jj < K; ++jj) {
+                    // phase 1: slots 0 and K-1 together (largest variable: coalesced; smallest:
+                    // mostly in LDS); then the middle slots, each only for unsatisfied clauses
+                    const int j = jj == 0 ? 0 : (jj == 1 ? K - 1 : jj - 1);
+                    const bool first = jj == 0 || jj == 1;
                     const uint32_t xs[4] = {x[j].x, x[j].y, x[j].z, x[j].w};
+                    uint32_t wi[4], gw[4], lw[4];
+                    bool need[4], useg[4];
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
-                        if (j > 0 && sat[q]) continue;
-                        const uint32_t v = (xs[q] & LIT_MASK) >> 1;
-                        const uint32_t w = (v < lds_vars) ? s_A[v >> 5] : A[v >> 5];
-                        sat[q] |= ((w >> (v & 31u)) & 1u) ^ (xs[q] & 1u);
+                        wi[q] = (xs[q] & LIT_MASK) >> 6;
+                        need[q] = first || !sat[q];
+                        useg[q] = need[q] && wi[q] >= lds_words;
+                    }
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        gw[q] = 0;
+                        if (useg[q]) gw[q] = A[wi[q]];
+                    }
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        lw[q] = 0;
+                        if (need[q] && !useg[q]) lw[q] = s_A[wi[q]];
+                    }
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const uint32_t w = gw[q] | lw[q];  // (both live: never one shared register)
+                        const uint32_t bit = ((w >> ((xs[q] >> 1) & 31u)) & 1u) ^ (xs[q] & 1u);
+                        sat[q] |= need[q] ? bit : 0u;
                     }
                 }
             }

@@ -514,7 +514,9 @@ struct HotTable {
             if (prev == 0xFFFFFFFFu || prev == var) break;
             h = (h + 1) & (HOT_SLOTS - 1);
         }
-        atomicMin(&v[h], key);
+        // workgroup scope: an LDS atomic (a different scope from the global claims keeps the
+        // compiler from merging the two into one flat atomic through a selected pointer)
+        __hip_atomic_fetch_min(&v[h], key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     __device__ void flush(unsigned long long* owner) {
         for (uint32_t i = threadIdx.x; i < HOT_SLOTS; i += blockDim.x)
@@ -535,7 +537,7 @@ __device__ __forceinline__ void claim_all(const ClauseView& cv, const Ent<K>& e,
     for (uint32_t j = 0; j < len; ++j) {
         const uint32_t raw = ent_lit<K>(cv, e, lb, j);
         if (hot && (raw & LIT_HOT)) ht.claim(lit_var(raw), key);
-        else atomicMin(&owner[lit_var(raw)], key);
+        else __hip_atomic_fetch_min(&owner[lit_var(raw)], key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 

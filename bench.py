@@ -121,6 +121,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("ALLL_BENCH_SAME_DEVICE"):  # rehearsal of the N>1 path on a 1-GPU box
+        local_rank = 0
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
 
@@ -175,9 +177,35 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    # warmup (untimed)
-    s.run(args.warmup, sync=False)
-    s.synchronize()
+    # warmup (untimed).  With RCCL, every rank reports whether its warmup went through; if any
+    # failed, all ranks rebuild the solver with the host-staged gloo exchange (same kernels)
+    failed = 0
+    try:
+        s.run(args.warmup, sync=False)
+        s.synchronize()
+    except N.AlllError as e:
+        if world == 1:
+            raise
+        log(f"[rank {rank}] warmup failed ({e})")
+        failed = 1
+    if world > 1 and exchange_impl == "rccl":
+        flag = torch.tensor([failed], dtype=torch.int32)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+        if int(flag.item()):
+            from alllsatisfiabilitysolver_amd import gloo_exchange
+
+            log(f"[rank {rank}] RCCL exchange failed on some rank; using the host-staged gloo exchange")
+            try:
+                s.close()
+            except N.AlllError:
+                pass
+            offs, lits = generate_ksat(1, n, m, k, kind)
+            s = Solver(n, offs, lits, seed=args.seed, device=local_rank, rank=rank, world=world,
+                       flags=flags, grid_rounds=args.grid_rounds, exchange=gloo_exchange())
+            del offs, lits
+            exchange_impl = "host-gloo"
+            s.run(args.warmup, sync=False)
+            s.synchronize()
     torch.cuda.synchronize(local_rank)
 
     barrier()

@@ -277,6 +277,98 @@ int orc_solve(uint32_t n_vars, uint64_t m, const uint64_t* offs, const uint32_t*
 }
 
 /* ------------------------------------------------------------------------- */
+/* Streaming solve, SATInstance::solve(getEnumeratedClause, n_clauses,       */
+/* batch_size) (SATInstance.h:70-153) with one thread.                        */
+/*  - ClauseGenerator (ClauseGenerator.h:33-70) yields clause indices         */
+/*    c <- (c + P) % m, P = 9223372036854775783, c starting at 0 and never    */
+/*    reset: over the whole run the yield sequence is s_j = j*P mod m,        */
+/*    j = 1, 2, ...;                                                           */
+/*  - iteration 1 takes m steps.  The end-of-iteration check (:130-147) calls */
+/*    yieldNextClause() for clauses 0, 1, ... in index order only until the   */
+/*    first violated one (later loop turns `continue`), which leaves the      */
+/*    generator at n_yielded = k0 = (first violated index) + 1 with           */
+/*    finished = false; the next iteration therefore takes only m - k0 steps  */
+/*    (all m when k0 == m: the generator finished and resets).  Clauses       */
+/*    outside that window of the sequence are not yielded at all;             */
+/*  - batches of batch_size steps from the window start (the last shorter);   */
+/*    the violated clauses of a batch extend the MIS greedily in yield order  */
+/*    (populate_mis_parallel with the current MIS, :391-451); the MIS is      */
+/*    resampled after the last batch (parallel_solve, resample =              */
+/*    finishedYielding, :217-320);                                            */
+/*  - avg_mis_size accumulates the MIS size after EVERY batch (:113-114), and */
+/*    is divided by n_iterations at the end;                                  */
+/*  - an already satisfied start still counts one iteration.                  */
+/* Restated with Philox resampling (iteration i uses round i-1).  max_iters   */
+/* caps the number of iterations (the reference has no cap).                  */
+/* ------------------------------------------------------------------------- */
+#define ORC_STREAM_P 9223372036854775783ULL
+
+void orc_stream_order(uint64_t m, uint32_t* order) {
+    uint64_t c = 0;
+    for (uint64_t k = 0; k < m; ++k) {
+        c = (c + ORC_STREAM_P) % m;  /* ClauseGenerator.h:47 (c < m, no overflow) */
+        order[k] = (uint32_t)c;
+    }
+}
+
+int orc_solve_stream(uint32_t n_vars, uint64_t m, const uint64_t* offs, const uint32_t* lits, uint64_t seed,
+                     uint64_t max_iters, uint64_t batch, uint32_t* A, orc_stats* st, orc_iter_cb cb,
+                     void* cb_user) {
+    uint32_t* M = (uint32_t*)malloc(sizeof(uint32_t) * (m ? m : 1));
+    uint8_t* used = (uint8_t*)calloc(n_vars ? n_vars : 1, 1);
+    uint64_t nw = (m + 63) / 64;
+    uint64_t* vmask = (uint64_t*)calloc(nw ? nw : 1, sizeof(uint64_t));
+    memset(st, 0, sizeof(*st));
+    if (batch == 0) batch = 1;
+    uint64_t weighted = 0, c = 0, window = m;
+    int solved = 0;
+    uint64_t nu = orc_eval(m, offs, lits, A, vmask);
+    for (;;) {
+        st->n_iterations += 1;
+        st->last_violated = nu;
+        /* greedy MIS over the window's violated clauses in yield order; a clause picked in
+           batch b counts in the cumulative sizes of batches b .. nb-1 */
+        const uint64_t nb = window ? (window + batch - 1) / batch : 0;
+        uint64_t nm = 0;
+        for (uint64_t k = 0; k < window; ++k) {
+            c = m ? (c + ORC_STREAM_P) % m : 0;
+            if (!((vmask[c >> 6] >> (c & 63)) & 1)) continue;
+            int dep = 0;
+            for (uint64_t j = offs[c]; j < offs[c + 1]; ++j) dep |= used[lits[j] >> 1];
+            if (dep) continue;
+            for (uint64_t j = offs[c]; j < offs[c + 1]; ++j) used[lits[j] >> 1] = 1;
+            M[nm++] = (uint32_t)c;
+            weighted += nb - k / batch;
+        }
+        uint64_t dres = 0;
+        const uint64_t iter = st->n_iterations - 1;
+        for (uint64_t i = 0; i < nm; ++i) {
+            const uint32_t cl = M[i];
+            for (uint64_t j = offs[cl]; j < offs[cl + 1]; ++j) {
+                const uint32_t v = lits[j] >> 1;
+                const uint32_t b = orc_resample_bit(seed, iter, v);
+                A[v >> 5] = (A[v >> 5] & ~(1u << (v & 31))) | (b << (v & 31));
+                used[v] = 0;
+            }
+            dres += offs[cl + 1] - offs[cl];
+        }
+        st->n_resamples += dres;
+        if (cb) cb(cb_user, st->n_iterations, nu, nm, dres, A);
+        nu = orc_eval(m, offs, lits, A, vmask);
+        if (nu == 0) { solved = 1; st->last_violated = 0; break; }
+        if (max_iters && st->n_iterations >= max_iters) { st->last_violated = nu; break; }
+        uint64_t first = 0;  /* first violated index: the check stops there */
+        while (!((vmask[first >> 6] >> (first & 63)) & 1)) ++first;
+        window = (first + 1 == m) ? m : m - (first + 1);
+    }
+    st->sum_mis_size = weighted;
+    st->avg_mis_size = st->n_iterations ? weighted / st->n_iterations : 0;
+    st->solved = solved;
+    free(M); free(used); free(vmask);
+    return solved ? 0 : 1;
+}
+
+/* ------------------------------------------------------------------------- */
 /* DIMACS semantics of cnf_header_read / cnf_data_read (example/cnf_io/        */
 /* cnf_io.cpp:487-705, 126-328) plus the encoding of example/main.cpp:157-178. */
 /* Restated over an in-memory buffer:                                          */

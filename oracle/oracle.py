@@ -72,6 +72,12 @@ def lib():
                                 ctypes.c_uint64, _u32p, ctypes.POINTER(OrcStats), ITER_CB,
                                 ctypes.c_void_p]
         L.orc_solve.restype = ctypes.c_int
+        L.orc_stream_order.argtypes = [ctypes.c_uint64, _u32p]
+        L.orc_stream_order.restype = None
+        L.orc_solve_stream.argtypes = [ctypes.c_uint32, ctypes.c_uint64, _u64p, _u32p, ctypes.c_uint64,
+                                       ctypes.c_uint64, ctypes.c_uint64, _u32p, ctypes.POINTER(OrcStats),
+                                       ITER_CB, ctypes.c_void_p]
+        L.orc_solve_stream.restype = ctypes.c_int
         L.orc_dimacs_parse.argtypes = [ctypes.c_char_p, ctypes.c_uint64, _u32p, _u64p, _u64p,
                                        _u32p, _u64p]
         L.orc_dimacs_parse.restype = ctypes.c_int
@@ -247,6 +253,51 @@ def solve(n_vars, offs, lits, seed, max_iters=0, A0=None, trace=False):
     return stats, A, rows
 
 
+def stream_order(m):
+    """Yield order of the reference's ClauseGenerator over m clauses (ClauseGenerator.h:47)."""
+    order = np.zeros(max(1, m), np.uint32)
+    lib().orc_stream_order(m, _p(order, _u32p))
+    return order[:m]
+
+
+def solve_stream(n_vars, offs, lits, seed, batch, max_iters=0, A0=None, trace=False):
+    """Streaming solve (SATInstance.h:70-153, one thread) with Philox.  Returns (stats dict,
+    final A words, per-iteration rows (it, |U|, |M|, dres, A after))."""
+    m = len(offs) - 1
+    A = init_assignment(seed, n_vars) if A0 is None else np.array(A0, np.uint32)
+    st = OrcStats()
+    rows = []
+
+    def cb(user, it, nu, nm, dres, Ap):
+        if trace:
+            rows.append((int(it), int(nu), int(nm), int(dres),
+                         np.ctypeslib.as_array(Ap, shape=(A.size,)).copy()))
+
+    cbf = ITER_CB(cb)
+    lib().orc_solve_stream(n_vars, m, _p(offs, _u64p), _p(lits, _u32p), seed, max_iters, batch,
+                           _p(A, _u32p), ctypes.byref(st), cbf, None)
+    stats = {k: int(getattr(st, k)) for k, _ in OrcStats._fields_ if k != "pad"}
+    return stats, A, rows
+
+
+def stream_mis(n_vars, offs, lits, A, order):
+    """Greedy MIS of the violated clauses in the given order (pick order)."""
+    nu, vm = eval_mask(offs, lits, A)
+    bits = np.unpackbits(vm.view(np.uint8), bitorder="little")
+    used = np.zeros(n_vars, bool)
+    M = []
+    for c in order:
+        c = int(c)
+        if not bits[c]:
+            continue
+        vs = lits[int(offs[c]):int(offs[c + 1])] >> 1
+        if used[vs].any():
+            continue
+        used[vs] = True
+        M.append(c)
+    return np.array(M, np.uint32)
+
+
 def dimacs_parse(text: bytes):
     v = ctypes.c_uint32()
     c = ctypes.c_uint64()
@@ -260,6 +311,48 @@ def dimacs_parse(text: bytes):
     rc = lib().orc_dimacs_parse(text, len(text), ctypes.byref(v), ctypes.byref(c),
                                 _p(offs, _u64p), _p(lits, _u32p), ctypes.byref(ln))
     return rc, (int(v.value), offs, lits[:ln.value].copy())
+
+
+# ----------------------------------------------------------------- reference run
+def read_stream_trace(path):
+    """Parse oracle/_ref/ref_probe `stream` output."""
+    with open(path, "rb") as f:
+        data = f.read()
+    assert data[:4] == b"ALRS"
+    n_vars, batch = struct.unpack_from("<II", data, 4)
+    (m,) = struct.unpack_from("<Q", data, 12)
+    p = 20
+    iters = []
+
+    def arr(dtype, p):
+        (n,) = struct.unpack_from("<Q", data, p)
+        p += 8
+        a = np.frombuffer(data, dtype, n, p).copy()
+        return a, p + a.nbytes
+
+    while True:
+        (it,) = struct.unpack_from("<Q", data, p)
+        p += 8
+        if it == 0xFFFFFFFFFFFFFFFF:
+            break
+        A = np.frombuffer(data, np.uint8, n_vars, p).copy()
+        p += n_vars
+        U, p = arr(np.uint32, p)
+        M, p = arr(np.uint32, p)
+        cum, p = arr(np.uint32, p)
+        (dres,) = struct.unpack_from("<Q", data, p)
+        p += 8
+        iters.append(dict(it=it, A=A, U=U, M=M, cum=cum, dres=dres))
+    n_it, n_res, avg = struct.unpack_from("<QQQ", data, p)
+    p += 24
+    Af = np.frombuffer(data, np.uint8, n_vars, p).copy()
+    p += n_vars
+    s_it, s_res, s_avg = struct.unpack_from("<QQQ", data, p)
+    p += 24
+    As = np.frombuffer(data, np.uint8, n_vars, p).copy()
+    return dict(n_vars=n_vars, m=m, batch=batch, iters=iters,
+                stats=dict(n_iterations=n_it, n_resamples=n_res, avg_mis_size=avg), A_final=Af,
+                solve_stats=dict(n_iterations=s_it, n_resamples=s_res, avg_mis_size=s_avg), solve_A=As)
 
 
 # ----------------------------------------------------------------- reference run

@@ -10,6 +10,10 @@
 //   bench <cnf> <T> <budget_s> <eval_reps>             eval-phase and full-iteration timing
 //   bench-gen <n> <m> <k> <kind> <gen_seed> <T> <budget_s> <eval_reps>   same, generated instance
 //   cnf   <cnf>                                        cnf_header_read/cnf_data_read output
+//   stream <cnf> <batch> <rd_seed> <out.bin>           streaming solve (SATInstance.h:70-153), T=1:
+//                                                      per-iteration (A_i, U_i in yield order, M_i in
+//                                                      pick order, per-batch MIS sizes), final stats,
+//                                                      and the real solve(getEnumeratedClause, ...)
 //
 // The load/encode/chunk sequence restates example/main.cpp:133-181 (main.cpp itself needs
 // Boost.program_options, absent here).  std::random_device::_M_getval is interposed by a
@@ -295,6 +299,117 @@ static int cmd_bench_gen(int argc, char** argv) {
     return bench_loaded(L, T, atof(argv[8]), atoi(argv[9]), load_s);
 }
 
+// ---- streaming solve (SATInstance.h:70-153) with T = 1 -------------------------------------
+// The clause callback returns a fresh copy of clause idx (the solver deletes what it yields);
+// every copy is registered so yielded clauses can be mapped back to their index.
+static Loaded* g_stream = nullptr;
+static std::unordered_map<const Clause<UINT_T>*, uint32_t> g_copy_index;
+static Clause<UINT_T>* stream_clause(UINT_T idx, unsigned short t_id) {
+    if (!g_stream || idx >= (UINT_T)g_stream->all.size()) return nullptr;
+    auto cl = new Clause<UINT_T>(new std::vector<UINT_T>(*g_stream->all[idx]->literals), t_id);
+    g_copy_index[cl] = (uint32_t)idx;
+    return cl;
+}
+
+static int cmd_stream(int argc, char** argv) {
+    std::string path = argv[2];
+    const UINT_T batch = (UINT_T)strtoul(argv[3], 0, 10);
+    const unsigned long long rd_seed = strtoull(argv[4], 0, 10);
+    FILE* f = fopen(argv[5], "wb");
+    Loaded L = load(path, 1);
+    g_stream = &L;
+    const UINT_T n_clauses = (UINT_T)L.c_num;
+    wr(f, "ALRS", 4);
+    uint32_t hdr[2] = {(uint32_t)L.v_num, (uint32_t)batch};
+    wr(f, hdr, 8);
+    wr64(f, (uint64_t)L.c_num);
+    // (1) the loop of SATInstance::solve(getEnumeratedClause, n_clauses, batch_size) with T = 1,
+    //     the reference's own ClauseGenerator, populate_mis_parallel and resample_clauses,
+    //     recording each iteration
+    g_rd_state = rd_seed;
+    auto S = new SATInstance<UINT_T>(new VariablesArray<UINT_T>(L.v_num), 1);
+    omp_set_num_threads(1);
+    auto statistics = new Statistics;
+    statistics->n_thread_resamples.push_back(0);
+    S->n_clauses = n_clauses;
+    auto gen = new ClauseGenerator<UINT_T>(stream_clause, 0, n_clauses, 0, batch);
+    std::vector<uint8_t> A(L.v_num);
+    bool solved = false;
+    while (!solved) {
+        solved = true;
+        statistics->n_iterations += 1;
+        for (int v = 0; v < L.v_num; ++v) A[v] = S->var_arr->vars[v] ? 1 : 0;
+        auto mis = new ClauseArray();
+        std::vector<uint32_t> U, M, cum;
+        bool finished = false;
+        ull dres = 0;
+        while (!finished) {
+            auto clauses = new std::vector<ClauseArray*>;
+            clauses->push_back(gen->yieldRandomUNSATClauseBatch(S->var_arr->vars));
+            for (auto c : *clauses->at(0)) U.push_back(g_copy_index[c]);
+            finished = gen->has_finished_yielding();
+            // parallel_solve(clauses, mis, stream = true, resample = finished), SATInstance.h:217-320
+            auto result = new Statistics;
+            result->n_thread_resamples.push_back(0);
+            result->n_iterations = 1;
+            S->populate_mis_parallel(clauses, mis, true);
+            result->avg_mis_size += mis->size();
+            cum.push_back((uint32_t)mis->size());
+            if (finished) {
+                for (auto c : *mis) M.push_back(g_copy_index[c]);
+                S->resample_clauses(mis, result);
+                mis->clear();  // (the reference also frees the clauses; ids recorded above)
+            }
+            result->n_resamples += result->n_thread_resamples.at(0);
+            statistics->avg_mis_size += result->avg_mis_size;
+            statistics->n_resamples += result->n_resamples;
+            statistics->n_thread_resamples.at(0) += result->n_thread_resamples.at(0);
+            dres += result->n_resamples;
+            delete result;
+        }
+        delete mis;
+        for (UINT_T k = 0; k < n_clauses; k++) {  // SATInstance.h:130-147
+            if (!solved) continue;
+            auto c = gen->yieldNextClause();
+            if (c->is_not_satisfied(S->var_arr->vars)) solved = false;
+            delete c->literals;
+            delete c;
+        }
+        wr64(f, statistics->n_iterations);
+        wr(f, A.data(), A.size());
+        wr64(f, U.size());
+        wr(f, U.data(), U.size() * 4);
+        wr64(f, M.size());
+        wr(f, M.data(), M.size() * 4);
+        wr64(f, cum.size());
+        wr(f, cum.data(), cum.size() * 4);
+        wr64(f, dres);
+        if (statistics->n_iterations >= 100000) break;  // (probe safety cap)
+    }
+    statistics->avg_mis_size /= statistics->n_iterations;
+    wr64(f, ~0ull);
+    wr64(f, statistics->n_iterations);
+    wr64(f, statistics->n_resamples);
+    wr64(f, statistics->avg_mis_size);
+    for (int v = 0; v < L.v_num; ++v) A[v] = S->var_arr->vars[v] ? 1 : 0;
+    wr(f, A.data(), A.size());
+    // (2) the real SATInstance::solve(getEnumeratedClause, ...) with the same interposed RNG
+    g_rd_state = rd_seed;
+    auto S2 = new SATInstance<UINT_T>(new VariablesArray<UINT_T>(L.v_num), 1);
+    std::streambuf* saved = std::cout.rdbuf();
+    std::ofstream devnull("/dev/null");
+    std::cout.rdbuf(devnull.rdbuf());  // it prints "New solve iteration..." every iteration
+    Statistics* st = S2->solve(stream_clause, (ull)n_clauses, batch);
+    std::cout.rdbuf(saved);
+    wr64(f, st->n_iterations);
+    wr64(f, st->n_resamples);
+    wr64(f, st->avg_mis_size);
+    for (int v = 0; v < L.v_num; ++v) A[v] = S2->var_arr->vars[v] ? 1 : 0;
+    wr(f, A.data(), A.size());
+    fclose(f);
+    return 0;
+}
+
 int main(int argc, char** argv) {
     if (argc < 3) {
         fprintf(stderr, "usage: ref_probe trace|solve|bench|cnf ...\n");
@@ -306,6 +421,7 @@ int main(int argc, char** argv) {
     if (cmd == "bench" && argc >= 6) return cmd_bench(argc, argv);
     if (cmd == "bench-gen" && argc >= 10) return cmd_bench_gen(argc, argv);
     if (cmd == "cnf") return cmd_cnf(argc, argv);
+    if (cmd == "stream" && argc >= 6) return cmd_stream(argc, argv);
     fprintf(stderr, "bad arguments\n");
     return 2;
 }

@@ -8,7 +8,8 @@ Runs oracle/_ref/ref_probe (compiled by oracle/Makefile from the reference sourc
     interposed random_device (pins the probe's per-iteration loop to parallel_solve),
   * DIMACS loader edge cases with the reference cnf_header_read/cnf_data_read output.
 
-Usage:  python tests/golden/make_golden.py     (needs /root/reference; not run on the GPU box)
+Usage:  python tests/golden/make_golden.py [--stream-only]
+        (needs /root/reference; not run on the GPU box)
 """
 import json
 import os
@@ -79,7 +80,59 @@ def pack_fixture(name, n_vars, offs, lits, T, tr, solve_json=None):
                         A_final=o.pack_bools(tr["A_final"]), **extra)
 
 
+def stream_fixtures(tmp):
+    """Streaming solve (SATInstance::solve(getEnumeratedClause, n, batch), T=1): per-iteration
+    (A_i, violated clauses in yield order, MIS in pick order, MIS size after every batch, delta
+    n_resamples), final Statistics of the probe loop and of the real solve (same RNG)."""
+    specs = [
+        # name, instance, batch sizes
+        ("r2_3sat_200_400", (200, 400, 3, 0), [1, 64, 1000]),
+        ("r2_3sat_2000_4000", (2000, 4000, 3, 0), [256]),
+        ("edge", None, [5]),
+    ]
+    out = []
+    for name, inst, batches in specs:
+        if inst is None:
+            n, (offs, lits) = edge_instance()
+        else:
+            n, m, k, kind = inst
+            offs, lits = o.generate_ksat(1, n, m, k, kind)
+        cnf = os.path.join(tmp, name + "_s.cnf")
+        with open(cnf, "w") as f:
+            f.write(o.to_dimacs(n, offs, lits))
+        for bs in batches:
+            path = os.path.join(tmp, "s.bin")
+            subprocess.run([o.REF_PROBE, "stream", cnf, str(bs), str(RD_SEED), path], check=True)
+            tr = o.read_stream_trace(path)
+            it = tr["iters"]
+            ptr = lambda key: np.cumsum([0] + [r[key].size for r in it]).astype(np.uint64)
+            cat = lambda key: np.concatenate([r[key] for r in it]).astype(np.uint32)
+            st, ss = tr["stats"], tr["solve_stats"]
+            fx = f"stream_{name}_b{bs}"
+            np.savez_compressed(
+                os.path.join(HERE, fx + ".npz"), n_vars=np.uint32(n), offs=offs, lits=lits,
+                batch=np.uint64(bs), A=np.stack([o.pack_bools(r["A"]) for r in it]),
+                U=cat("U"), U_ptr=ptr("U"), M=cat("M"), M_ptr=ptr("M"), cum=cat("cum"),
+                cum_ptr=ptr("cum"), dres=np.array([r["dres"] for r in it], np.uint64),
+                stats=np.array([st["n_iterations"], st["n_resamples"], st["avg_mis_size"]], np.uint64),
+                A_final=o.pack_bools(tr["A_final"]),
+                solve_stats=np.array([ss["n_iterations"], ss["n_resamples"], ss["avg_mis_size"]], np.uint64),
+                solve_A=o.pack_bools(tr["solve_A"]))
+            out.append(dict(fixture=fx, n_vars=n, n_clauses=len(offs) - 1, batch=bs, iters=len(it)))
+    return out
+
+
 def main():
+    if "--stream-only" in sys.argv:
+        tmp = tempfile.mkdtemp()
+        sm = stream_fixtures(tmp)
+        mf = os.path.join(HERE, "manifest.json")
+        man = json.load(open(mf))
+        man["stream_fixtures"] = sm
+        with open(mf, "w") as f:
+            json.dump(man, f, indent=1)
+        print("wrote", len(sm), "streaming fixtures")
+        return
     if not os.path.exists(o.REF_PROBE):
         subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "ref"], check=True)
     tmp = tempfile.mkdtemp()
@@ -150,9 +203,10 @@ def main():
         loader[key] = dict(text=text, ref=json.loads(out))
     with open(os.path.join(HERE, "dimacs_cases.json"), "w") as f:
         json.dump(loader, f, indent=1)
+    sm = stream_fixtures(tmp)
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
         json.dump(dict(rd_seed=RD_SEED, generator="oracle.generate_ksat(gen_seed=1, ...)",
-                       fixtures=manifest), f, indent=1)
+                       fixtures=manifest, stream_fixtures=sm), f, indent=1)
     print("wrote", len(manifest), "trajectory fixtures and", len(loader), "loader cases")
 
 

@@ -16,7 +16,9 @@ import pytest
 
 from conftest import GOLDEN
 
-FIXTURES = sorted(glob.glob(os.path.join(GOLDEN, "*.npz")))
+FIXTURES = sorted(p for p in glob.glob(os.path.join(GOLDEN, "*.npz"))
+                  if not os.path.basename(p).startswith("stream_"))
+STREAM_FIXTURES = sorted(glob.glob(os.path.join(GOLDEN, "stream_*.npz")))
 
 
 def load(path):
@@ -162,3 +164,124 @@ def test_numpy_philox_matches_c_oracle(oracle_mod):
     for seed, it in [(1, 0), (12345, 77), ((7 << 32) | 9, (3 << 32) | 5)]:
         ref = np.array([o.resample_bit(seed, it, int(v)) for v in vs], np.uint32)
         np.testing.assert_array_equal(o.philox_bits(seed, it, vs), ref)
+
+
+# ---------------------------------------------------------------------------------------------
+# Streaming solve (SATInstance::solve(getEnumeratedClause, n_clauses, batch), SATInstance.h:70-153,
+# one thread): fixtures from the reference's own ClauseGenerator / populate_mis_parallel /
+# resample_clauses (ref_probe `stream`).
+
+
+def test_stream_fixtures_present():
+    assert len(STREAM_FIXTURES) >= 4
+
+
+def test_stream_order_is_the_generator_lcg():
+    """ClauseGenerator.h:47: c <- (c + P) % m from c = 0, P = 9223372036854775783."""
+    from conftest import ROOT  # noqa: F401
+    import oracle as o
+
+    P = 9223372036854775783
+    for m in (1, 7, 10, 400, 4000, 99991):
+        c, ref = 0, []
+        for _ in range(m):
+            c = (c + P) % m
+            ref.append(c)
+        np.testing.assert_array_equal(o.stream_order(m), np.array(ref, np.uint32))
+
+
+@pytest.mark.parametrize("path", STREAM_FIXTURES, ids=lambda p: os.path.basename(p)[:-4])
+def test_oracle_matches_reference_stream(oracle_mod, path):
+    """Per iteration the reference yields a window of the generator's sequence: all m steps in
+    the first iteration, then m - k0 steps, k0 = first violated clause index + 1 (where its
+    end-of-iteration check stopped; all m again when k0 == m)."""
+    o = oracle_mod
+    f = load(path)
+    n, offs, lits, bs = int(f["n_vars"]), f["offs"], f["lits"], int(f["batch"])
+    m = offs.size - 1
+    period = o.stream_order(m)          # s_1 .. s_m; the sequence repeats with period m
+    S, window = 0, m                    # steps taken before this iteration, window length
+    n_it = f["A"].shape[0]
+    total_w = 0
+    for i in range(n_it):
+        A = f["A"][i]
+        U_ref = f["U"][int(f["U_ptr"][i]):int(f["U_ptr"][i + 1])]
+        M_ref = f["M"][int(f["M_ptr"][i]):int(f["M_ptr"][i + 1])]
+        cum = f["cum"][int(f["cum_ptr"][i]):int(f["cum_ptr"][i + 1])]
+        order = period[(S + np.arange(window)) % m]
+        _, vm = o.eval_mask(offs, lits, A)
+        bits = np.unpackbits(vm.view(np.uint8), bitorder="little")[:m]
+        np.testing.assert_array_equal(order[bits[order] == 1], U_ref, err_msg=f"U_{i} in yield order")
+        M = o.stream_mis(n, offs, lits, A, order)
+        np.testing.assert_array_equal(M, M_ref, err_msg=f"M_{i} (pick order)")
+        nb = -(-window // bs)
+        pos = {int(c): k for k, c in enumerate(order)}
+        b_of = np.array([pos[int(c)] // bs for c in M], np.int64)
+        assert cum.size == nb
+        np.testing.assert_array_equal(cum, [(b_of <= b).sum() for b in range(nb)])
+        w = int((nb - b_of).sum())
+        assert w == int(cum.sum())
+        total_w += w
+        assert int(f["dres"][i]) == int(np.sum(offs[M.astype(np.int64) + 1] - offs[M.astype(np.int64)]))
+        if i + 1 < n_it:
+            a0 = o.unpack_words(A, n)
+            a1 = o.unpack_words(f["A"][i + 1], n)
+            changed = np.nonzero(a0 != a1)[0]
+            idx = [np.arange(offs[c], offs[c + 1]) for c in M] or [np.zeros(0, np.int64)]
+            vars_m = np.unique(lits[np.concatenate(idx).astype(np.int64)] >> 1)
+            assert np.isin(changed, vars_m).all()
+            # next window: where the reference's check stopped under the new assignment
+            _, vm1 = o.eval_mask(offs, lits, f["A"][i + 1])
+            bits1 = np.unpackbits(vm1.view(np.uint8), bitorder="little")[:m]
+            k0 = int(np.nonzero(bits1)[0][0]) + 1
+            S += window
+            window = m if k0 == m else m - k0
+    st = f["stats"]
+    assert int(st[0]) == n_it
+    assert int(st[1]) == int(f["dres"].sum())
+    assert int(st[2]) == total_w // n_it
+    # the probe's loop is the real streaming solve (same interposed random_device)
+    np.testing.assert_array_equal(f["solve_stats"], st)
+    np.testing.assert_array_equal(f["solve_A"], f["A_final"])
+
+
+def test_oracle_solve_stream_semantics(oracle_mod):
+    """Philox restatement: converges; stats consistent with the per-iteration rows."""
+    o = oracle_mod
+    offs, lits = o.generate_ksat(3, 500, 1000, 3)
+    for bs in (1, 37, 5000):
+        st, A, rows = o.solve_stream(500, offs, lits, 11, bs, trace=True)
+        assert st["solved"] == 1 and o.eval_mask(offs, lits, A)[0] == 0
+        assert st["n_iterations"] == len(rows)
+        assert st["n_resamples"] == sum(r[3] for r in rows)
+        assert st["avg_mis_size"] == st["sum_mis_size"] // st["n_iterations"]
+    # the C restatement follows the same windows / MIS as the fixture-checked maps above
+    m = offs.size - 1
+    period = o.stream_order(m)
+    for bs in (1, 50):
+        st, A_end, rows = o.solve_stream(500, offs, lits, 13, bs, trace=True)
+        A = o.init_assignment(13, 500)
+        S, window, w_total = 0, m, 0
+        for it, nu, nm, dres, A_after in rows:
+            order = period[(S + np.arange(window)) % m]
+            M = o.stream_mis(500, offs, lits, A, order)
+            assert (nu, nm) == (o.eval_mask(offs, lits, A)[0], M.size)
+            assert dres == int(np.sum(offs[M.astype(np.int64) + 1] - offs[M.astype(np.int64)]))
+            pos = {int(c): k for k, c in enumerate(order)}
+            nb = -(-window // bs)
+            w_total += sum(nb - pos[int(c)] // bs for c in M)
+            np.testing.assert_array_equal(
+                o.resample_words(A.copy(), 13, it - 1, o.clause_vars(offs, lits, M)), A_after)
+            A = A_after
+            nu1, vm1 = o.eval_mask(offs, lits, A)
+            if nu1:
+                k0 = int(np.nonzero(np.unpackbits(vm1.view(np.uint8), bitorder="little")[:m])[0][0]) + 1
+                S += window
+                window = m if k0 == m else m - k0
+        assert st["sum_mis_size"] == w_total
+    # already satisfied: one iteration, nothing resampled
+    offs1 = np.array([0, 1], np.uint64)
+    A0 = o.init_assignment(2, 4)
+    lit = np.array([0 if (A0[0] & 1) else 1], np.uint32)  # the literal of variable 0 that is true
+    st, A, rows = o.solve_stream(4, offs1, lit, 2, 8, trace=True)
+    assert st == {**st, "n_iterations": 1, "n_resamples": 0, "avg_mis_size": 0, "solved": 1}

@@ -72,6 +72,7 @@ class Options(ctypes.Structure):
         ("comm_id", ctypes.c_uint8 * 128),
         ("flags", ctypes.c_uint32),
         ("grid_rounds", ctypes.c_uint32),
+        ("stream_batch", ctypes.c_uint64),
     ]
 
 

@@ -63,6 +63,8 @@ struct DevState {
     uint32_t error;        // 1: LFMIS exceeded MAX_TAIL_ROUNDS (loop stopped, done = 3)
     uint32_t left_cnt;     // undecided entries handed from the last grid round to the tail
     uint32_t tmis_cnt;     // MIS entries decided by the tail kernel (list b.tmis)
+    uint64_t win_start;    // streaming solve: generator steps taken before this iteration
+    uint64_t win_len;      // streaming solve: steps (clauses yielded) in this iteration
 };
 
 // Clause storage on the device.
@@ -103,6 +105,11 @@ struct LoopBuffers {
     uint32_t n_runs;
     unsigned long long* kdbg;   // diagnostics (env ALLL_DEBUG_PHASES): per-workgroup phase stamps
     uint32_t experiment;        // diagnostics (env ALLL_EXPERIMENT): timing-only variants, results invalid
+    // streaming solve (SATInstance::solve(getEnumeratedClause, ...), T = 1): LFMIS priority =
+    // position in the clause generator's yield window (alll_options.stream_batch > 0)
+    uint64_t m;                 // clauses
+    uint64_t stream_batch;      // 0: clause-order LFMIS
+    uint64_t stream_pinv;       // inverse of P mod m (P = 9223372036854775783, ClauseGenerator.h:110)
     uint32_t n_vars;
     uint32_t n_words;
     uint32_t n_tiles;       // tiles covering [0, m)

@@ -75,6 +75,27 @@ __device__ __forceinline__ bool eval_gate_closed(const DevState* st) {
     return st->done != 0 || st->n_iter >= st->limit_eval;
 }
 
+// Streaming solve priorities (b.stream_batch > 0).  The reference's clause generator yields
+// clause s_j = j*P mod m at step j (ClauseGenerator.h:47), so clause c comes at the steps
+// j = pos(c) (mod m), pos(c) = c * P^-1 mod m in [1, m].  The iteration's window is steps
+// (win_start, win_start + win_len]; the LFMIS key of c is its offset in the window + 1, or ~0
+// when the window does not yield it.  Without streaming the key is the clause id.
+__device__ __forceinline__ uint32_t prio(const LoopBuffers& b, const DevState* st, uint32_t c) {
+    if (!b.stream_batch) return c;
+    const uint64_t m = b.m;
+    uint64_t pos = ((uint64_t)c * b.stream_pinv) % m;  // both factors < 2^32
+    if (pos == 0) pos = m;
+    const uint64_t off = (pos - 1 + m - st->win_start % m) % m;
+    return off < st->win_len ? (uint32_t)(off + 1) : ~0u;
+}
+// Contribution of an MIS clause to the MIS-size statistic: 1, or in the streaming solve the
+// number of batches after which it is counted (its batch and every later one, SATInstance.h:113)
+__device__ __forceinline__ unsigned long long mis_weight(const LoopBuffers& b, const DevState* st, uint32_t key) {
+    if (!b.stream_batch) return 1ull;
+    const uint64_t nb = (st->win_len + b.stream_batch - 1) / b.stream_batch;
+    return nb - (uint64_t)(key - 1) / b.stream_batch;
+}
+
 // In-loop timing stamps (ALLL_FLAG_KERNEL_TIMING): slot of iteration n_iter (see TIME_SLOTS).
 __device__ __forceinline__ unsigned long long* time_slot(const LoopBuffers& b, uint64_t it) {
     return b.ktime + (it % TIME_SLOTS) * TIME_FIELDS;
@@ -459,10 +480,17 @@ __global__ __launch_bounds__(1024) void k_reduce(LoopBuffers b, int mode) {
     }
     const unsigned long long reduce_t0 = wall_now();
     __shared__ unsigned long long s_sum;
-    if (threadIdx.x == 0) s_sum = 0;
+    __shared__ uint32_t s_first;  // first tile with a violated clause (streaming window)
+    if (threadIdx.x == 0) { s_sum = 0; s_first = ~0u; }
     __syncthreads();
     unsigned long long acc = 0;
-    for (uint32_t t = threadIdx.x; t < b.n_tiles; t += blockDim.x) acc += b.tile_cnt[t];
+    uint32_t first = ~0u;
+    for (uint32_t t = threadIdx.x; t < b.n_tiles; t += blockDim.x) {
+        const uint32_t cnt = b.tile_cnt[t];
+        acc += cnt;
+        if (cnt && t < first) first = t;
+    }
+    if (b.stream_batch && first != ~0u) atomicMin(&s_first, first);
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
     if ((threadIdx.x & 63) == 0) atomicAdd(&s_sum, acc);
     __syncthreads();
@@ -485,6 +513,26 @@ __global__ __launch_bounds__(1024) void k_reduce(LoopBuffers b, int mode) {
     if (u == 0) { st->done = 1; st->active = 0; }
     else if (st->n_iter >= st->limit_nores) { st->done = 2; st->active = 0; }
     else st->active = 1;
+    if (b.stream_batch && u) {
+        // streaming window of this iteration: the first one takes all m steps; later ones
+        // m - k0, k0 = first violated clause index + 1 (where the reference's end-of-iteration
+        // check stopped), or m again when k0 == m (SATInstance.h:130-147, ClauseGenerator.h:73-90).
+        // Streaming uses the clause-order (CSR) layout, so the bitmask is in clause order.
+        if (st->n_iter == 1) {
+            st->win_start = 0;
+            st->win_len = b.m;
+        } else {
+            const uint32_t t = s_first;
+            uint64_t first_c = (uint64_t)t * TILE;
+            for (uint32_t w = 0; w < TILE_WORDS; ++w) {
+                const uint64_t x = b.vmask[(uint64_t)t * TILE_WORDS + w];
+                if (x) { first_c += 64u * w + (uint32_t)__builtin_ctzll(x); break; }
+            }
+            const uint64_t k0 = first_c + 1;
+            st->win_start += st->win_len;
+            st->win_len = (k0 == b.m) ? b.m : b.m - k0;
+        }
+    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -574,12 +622,14 @@ __global__ __launch_bounds__(ROUND_THREADS) void k_claim(ClauseView cv, LoopBuff
         }
         uint64_t lb;
         const uint32_t len = ent_len<K>(cv, e, lb);
+        const uint32_t key = prio(b, st, e.w[0]);
+        if (key == ~0u) continue;  // streaming: not yielded this iteration (dropped by JOIN(0))
         if (r > 0) {
             bool killed = false;
             for (uint32_t j = 0; j < len; ++j) killed |= b.cover[lit_var(ent_lit<K>(cv, e, lb, j))] == stamp;
             if (killed) continue;
         }
-        claim_all<K>(cv, e, lb, len, keyhi | e.w[0], owner, ht, hot);
+        claim_all<K>(cv, e, lb, len, keyhi | key, owner, ht, hot);
         if (r > 0) store_ent<K>(lout + (uint64_t)atomicAdd(&s_keep, 1u) * S, e);
     }
     __syncthreads();
@@ -597,29 +647,38 @@ __device__ __forceinline__ void join_tile(const ClauseView& cv, const LoopBuffer
     DevState* st = b.state;
     constexpr int S = Ent<K>::S;
     __shared__ uint32_t s_keep, s_join, s_base;
-    __shared__ unsigned long long s_lits;
-    if (threadIdx.x == 0) { s_keep = 0; s_join = 0; s_lits = 0; }
+    __shared__ unsigned long long s_lits, s_w;
+    if (threadIdx.x == 0) { s_keep = 0; s_join = 0; s_lits = 0; s_w = 0; }
     __syncthreads();
     const uint32_t* lin = in + (uint64_t)tile * TILE * S;
     uint32_t* lout = out + (uint64_t)tile * TILE * S;
     uint32_t* mis = b.mis + (uint64_t)tile * TILE + b.mis_cnt[tile];
-    unsigned long long my_lits = 0;
+    unsigned long long my_lits = 0, my_w = 0;
     for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
         Ent<K> e;
         load_ent<K>(e, lin + (uint64_t)i * S);
         const uint32_t c = e.w[0];
+        const uint32_t key = prio(b, st, c);
+        if (key == ~0u) continue;  // streaming: not yielded this iteration, leaves the list
         uint64_t lb;
         const uint32_t len = ent_len<K>(cv, e, lb);
         if (own(e, i, lb, len)) {
             for (uint32_t j = 0; j < len; ++j) b.cover[lit_var(ent_lit<K>(cv, e, lb, j))] = stamp;
             mis[atomicAdd(&s_join, 1u)] = c;
             my_lits += len;
+            my_w += mis_weight(b, st, key);
         } else {
             store_ent<K>(lout + (uint64_t)atomicAdd(&s_keep, 1u) * S, e);
         }
     }
-    for (int o = 32; o > 0; o >>= 1) my_lits += __shfl_down(my_lits, o, 64);
-    if ((threadIdx.x & 63) == 0 && my_lits) atomicAdd(&s_lits, my_lits);
+    for (int o = 32; o > 0; o >>= 1) {
+        my_lits += __shfl_down(my_lits, o, 64);
+        my_w += __shfl_down(my_w, o, 64);
+    }
+    if ((threadIdx.x & 63) == 0 && my_w) {  // (an empty clause joins with no literals)
+        atomicAdd(&s_lits, my_lits);
+        atomicAdd(&s_w, my_w);
+    }
     __syncthreads();
     const uint32_t kept = s_keep;
     if (last && kept) {
@@ -632,7 +691,7 @@ __device__ __forceinline__ void join_tile(const ClauseView& cv, const LoopBuffer
         b.tile_cnt[tile] = last ? 0u : kept;
         b.mis_cnt[tile] += s_join;
         if (s_join) {
-            atomicAdd(&b.tile_stats[2 * tile], (unsigned long long)s_join);
+            atomicAdd(&b.tile_stats[2 * tile], s_w);  // = s_join unless streaming
             atomicAdd(&b.tile_stats[2 * tile + 1], s_lits);
         }
     }
@@ -654,8 +713,8 @@ __global__ __launch_bounds__(ROUND_THREADS) void k_join(ClauseView cv, LoopBuffe
     join_tile<K>(cv, b, tile, cnt, in, out, last, st->stamp,
                  [&](const Ent<K>& e, uint32_t, uint64_t lb, uint32_t len) {
                      bool own = true;
-                     for (uint32_t j = 0; j < len; ++j)
-                         own &= owner[lit_var(ent_lit<K>(cv, e, lb, j))] == (keyhi | e.w[0]);
+                     const unsigned long long key = keyhi | prio(b, st, e.w[0]);
+                     for (uint32_t j = 0; j < len; ++j) own &= owner[lit_var(ent_lit<K>(cv, e, lb, j))] == key;
                      return own;
                  });
 }
@@ -1132,8 +1191,10 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail(ClauseView cv, LoopBuffer
                     killed |= __hip_atomic_load(&b.cover[lit_var(ent_lit<K>(cv, e, lb, j))], __ATOMIC_RELAXED,
                                                 __HIP_MEMORY_SCOPE_AGENT) == stamp;
                 if (!killed) {
+                    const unsigned long long key = keyhi | prio(b, st, e.w[0]);
                     for (uint32_t j = 0; j < len; ++j)
-                        atomicMin(&owner[lit_var(ent_lit<K>(cv, e, lb, j))], keyhi | e.w[0]);
+                        __hip_atomic_fetch_min(&owner[lit_var(ent_lit<K>(cv, e, lb, j))], key, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
                     store_ent<K>(left + (uint64_t)atomicAdd(&s_wp, 1u) * S, e);
                 }
             }
@@ -1151,18 +1212,19 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail(ClauseView cv, LoopBuffer
             __syncthreads();
             if (i < n) {
                 const uint32_t c = e.w[0];
+                const uint32_t kc = prio(b, st, c);
                 uint64_t lb;
                 const uint32_t len = ent_len<K>(cv, e, lb);
                 bool own = true;
                 for (uint32_t j = 0; j < len; ++j)
                     own &= __hip_atomic_load(&owner[lit_var(ent_lit<K>(cv, e, lb, j))], __ATOMIC_RELAXED,
-                                             __HIP_MEMORY_SCOPE_AGENT) == (keyhi | c);
+                                             __HIP_MEMORY_SCOPE_AGENT) == (keyhi | kc);
                 if (own) {
                     for (uint32_t j = 0; j < len; ++j)
                         __hip_atomic_store(&b.cover[lit_var(ent_lit<K>(cv, e, lb, j))], stamp, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
                     b.tmis[atomicAdd(&s_tm, 1u)] = c;
-                    atomicAdd(&b.tile_stats[2 * (c / TILE)], 1ull);
+                    atomicAdd(&b.tile_stats[2 * (c / TILE)], mis_weight(b, st, kc));
                     atomicAdd(&b.tile_stats[2 * (c / TILE) + 1], (unsigned long long)len);
                 } else {
                     store_ent<K>(left + (uint64_t)atomicAdd(&s_wp, 1u) * S, e);

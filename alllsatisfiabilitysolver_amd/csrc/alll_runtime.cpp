@@ -254,6 +254,14 @@ int fill_stats(alll_ctx* c, alll_stats* st) {
         const uint32_t r = c->tiles_per_rank ? t / c->tiles_per_rank : 0;
         if (r < ALLL_MAX_GPU_STATS) st->gpu_resamples[r] += ts[2 * t + 1];
     }
+    if (c->b.stream_batch && st->n_iterations) {
+        // a stream iteration is evaluation + MIS + resample + the full check (SATInstance.h:
+        // 91-147); the check is the next evaluation pass, so the stream iterations are the
+        // resample rounds: every pass but a final non-resampling one (solved or capped), and
+        // at least one (a start that is already satisfied)
+        const uint64_t rounds = st->n_iterations - (c->h_state->done ? 1 : 0);
+        st->n_iterations = rounds ? rounds : 1;
+    }
     st->avg_mis_size = st->n_iterations ? st->sum_mis_size / st->n_iterations : 0;
     st->n_violated = c->h_state->u_total;
     st->solved = (c->h_state->done == 1) ? 1 : 0;
@@ -331,7 +339,10 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
         if (fixed_k == -1) fixed_k = (int)std::min<int64_t>(w, 1 << 30);
         else if (fixed_k != w) fixed_k = 0;
     }
-    if (fixed_k < 1 || fixed_k > MAX_FIXED_K || (opt.flags & ALLL_FLAG_GENERIC_CSR)) fixed_k = 0;
+    // the streaming solve keeps the clause-order (CSR) layout: its window rule needs the first
+    // violated clause index, read from a clause-order bitmask
+    if (fixed_k < 1 || fixed_k > MAX_FIXED_K || (opt.flags & ALLL_FLAG_GENERIC_CSR) || opt.stream_batch)
+        fixed_k = 0;
     const uint64_t lim = 2ull * prob->n_vars;
     for (uint64_t j = 0; j < L; ++j)
         if (prob->literals[j] >= lim)
@@ -380,6 +391,22 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     b.n_vars = c->n_vars;
     b.n_words = (c->n_vars + 31) / 32;
     b.n_tiles = n_tiles;
+    b.m = m;
+    if (opt.stream_batch && m) {
+        // key of the streaming solve: position in the generator sequence j*P mod m, so the
+        // inverse of P mod m (P is prime, so it exists for every m < P)
+        const uint64_t p = 9223372036854775783ull % m;
+        int64_t r0 = (int64_t)m, r1 = (int64_t)p, t0 = 0, t1 = 1;
+        while (r1) {
+            const int64_t q = r0 / r1;
+            int64_t x = r0 - q * r1; r0 = r1; r1 = x;
+            x = t0 - q * t1; t0 = t1; t1 = x;
+        }
+        if (m > 1 && r0 != 1) return bail(fail(ALLL_ERR_UNSUPPORTED, "generator step not invertible mod %llu",
+                                                (unsigned long long)m));
+        b.stream_pinv = m > 1 ? (uint64_t)((t0 % (int64_t)m + (int64_t)m) % (int64_t)m) : 0;
+        b.stream_batch = opt.stream_batch;
+    }
     b.seed = opt.seed;
     if ((rc = dalloc(c, &b.A, b.n_words + 4))) return bail(rc);  // +4: 16-byte tail loads
     if ((rc = dalloc(c, &b.vmask, (size_t)c->n_tiles_padded * TILE_WORDS))) return bail(rc);
@@ -627,7 +654,9 @@ int alll_solve(alll_ctx* c, alll_stats* st) {
     HIP_TRY(hipSetDevice(c->device));
     int rc = read_state(c);
     if (rc) return rc;
-    const uint64_t cap = c->opt.max_iters ? c->opt.max_iters : ~0ull;
+    // (streaming solve: max_iters counts stream iterations; the last one's check is one more
+    // evaluation pass, which does not resample)
+    const uint64_t cap = c->opt.max_iters ? c->opt.max_iters + (c->b.stream_batch ? 1 : 0) : ~0ull;
     if (c->h_state->done != 1) {
         if ((rc = write_limits(c, cap, cap))) return rc;
         uint64_t batch = 1;

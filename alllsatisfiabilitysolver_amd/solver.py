@@ -75,7 +75,7 @@ class Solver:
     def __init__(self, n_vars: int, offsets, literals, seed: int = 1, max_iters: int = 0,
                  device: int = -1, n_threads: int = 1, rank: int = 0, world: int = 1,
                  comm_id: Optional[bytes] = None, flags: int = 0, grid_rounds: int = 0,
-                 exchange=None):
+                 exchange=None, stream_batch: int = 0):
         self._L = N.lib()
         self.n_vars = int(n_vars)
         self.offsets = np.ascontiguousarray(offsets, np.uint64)
@@ -87,6 +87,7 @@ class Solver:
         opt.seed, opt.max_iters, opt.device = seed, max_iters, device
         opt.n_threads, opt.rank, opt.world = n_threads, rank, world
         opt.flags, opt.grid_rounds = flags, grid_rounds
+        opt.stream_batch = stream_batch  # > 0: streaming solve semantics (alll.h)
         if comm_id is not None:
             ctypes.memmove(opt.comm_id, comm_id, 128)
         self._ctx = ctypes.c_void_p()

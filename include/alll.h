@@ -70,6 +70,13 @@ typedef struct alll_options {
                                all zero: no RCCL, alll_set_host_exchange() is required */
     uint32_t flags;         /* ALLL_FLAG_* */
     uint32_t grid_rounds;   /* full-grid LFMIS rounds before the tail kernel (0 = default) */
+    uint64_t stream_batch;  /* 0: SATInstance::solve(vector<ClauseArray*>*) semantics.  > 0: the
+                               streaming solve SATInstance::solve(getEnumeratedClause, n_clauses,
+                               batch_size) (SATInstance.h:70-153) with one thread and this batch
+                               size: the MIS follows the clause generator's yield order
+                               (ClauseGenerator.h:33-70) and alll_stats reports its statistics
+                               (n_iterations = stream iterations, avg_mis_size summed per batch);
+                               max_iters then caps stream iterations */
 } alll_options;
 
 #define ALLL_MAX_GPU_STATS 64

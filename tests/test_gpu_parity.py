@@ -281,3 +281,60 @@ def test_loop_times_stamps_leave_trajectory_unchanged(gpu, oracle_mod):
     with Solver(n, offs, lits, seed=21) as s:
         with pytest.raises(Exception):
             s.loop_times(0, 1)
+
+
+# ---------------------------------------------------------------------------------------------
+# Streaming solve (SATInstance::solve(getEnumeratedClause, n, batch), T=1; oracle.solve_stream is
+# pinned to the reference by tests/test_oracle.py::test_oracle_matches_reference_stream)
+
+STREAM_CASES = {
+    "r2_200_400_b64": (200, 400, 3, 64),
+    "r2_200_400_b1": (200, 400, 3, 1),
+    "r2_5000_10000_b777": (5000, 10000, 3, 777),   # several tiles, ragged last batch
+    "r2_30000_60000_b4096": (30000, 60000, 3, 4096),
+}
+
+
+@pytest.mark.parametrize("name", list(STREAM_CASES))
+def test_stream_trajectory_matches_oracle(gpu, oracle_mod, name):
+    from alllsatisfiabilitysolver_amd import Solver, generate_ksat
+
+    n, m, k, bs = STREAM_CASES[name]
+    offs, lits = generate_ksat(2, n, m, k)
+    seed = 31
+    st_o, A_o, rows = oracle_mod.solve_stream(n, offs, lits, seed, bs, trace=True)
+    assert st_o["solved"] == 1
+    with Solver(n, offs, lits, seed=seed, stream_batch=bs) as s:
+        for it, nu, nm, dres, A_after in rows:
+            before = s.stats()
+            s.run(1)
+            after = s.stats()
+            assert after["n_violated"] == nu, f"iter {it}"
+            assert after["n_resamples"] - before["n_resamples"] == dres, f"iter {it}"
+            np.testing.assert_array_equal(s.assignment_words(), A_after, err_msg=f"A after iter {it}")
+        assert len(s.mis()) == rows[-1][2]
+    with Solver(n, offs, lits, seed=seed, stream_batch=bs) as s:
+        st = s.solve()
+        for key in ("n_iterations", "n_resamples", "avg_mis_size", "sum_mis_size", "solved"):
+            assert st[key] == st_o[key], key
+        np.testing.assert_array_equal(s.assignment_words(), A_o)
+
+
+def test_stream_cap_and_satisfied_start(gpu, oracle_mod):
+    from alllsatisfiabilitysolver_amd import Solver, generate_ksat
+
+    n, m = 2000, 8000  # ratio 4: not solved within the cap
+    offs, lits = generate_ksat(4, n, m, 3)
+    st_o, A_o, _ = oracle_mod.solve_stream(n, offs, lits, 9, 100, max_iters=6)
+    assert st_o["solved"] == 0 and st_o["n_iterations"] == 6
+    with Solver(n, offs, lits, seed=9, max_iters=6, stream_batch=100) as s:
+        st = s.solve()
+        for key in ("n_iterations", "n_resamples", "avg_mis_size", "solved"):
+            assert st[key] == st_o[key], key
+        np.testing.assert_array_equal(s.assignment_words(), A_o)
+    # one clause, satisfied by the initial assignment: one iteration, nothing resampled
+    A0 = oracle_mod.init_assignment(2, 4)
+    lit = np.array([0 if (A0[0] & 1) else 1], np.uint32)
+    with Solver(4, np.array([0, 1], np.uint64), lit, seed=2, stream_batch=8) as s:
+        st = s.solve()
+        assert (st["n_iterations"], st["n_resamples"], st["avg_mis_size"], st["solved"]) == (1, 0, 0, 1)

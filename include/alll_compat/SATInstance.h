@@ -1,10 +1,12 @@
 // SATInstance.h -- compatibility header: the reference's public API
-// (library/include/SATInstance.h:25-66, 156-173) over the MI355X solver's C-ABI
+// (library/include/SATInstance.h:25-203: both solve overloads, verify_validity, writeDIMACS)
+// over the MI355X solver's C-ABI
 // (include/alll.h).  Existing call sites (example/main.cpp) compile unchanged; the device,
 // seed and iteration cap are additive settings (env ALLL_DEVICE, ALLL_SEED, ALLL_MAX_ITERS).
 #ifndef ALLL_COMPAT_SATINSTANCE_H
 #define ALLL_COMPAT_SATINSTANCE_H
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
 #include <fstream>
@@ -54,6 +56,63 @@ class SATInstance {
                 for (auto l : *cl->literals) lits.push_back((uint32_t)l);
                 offs.push_back(lits.size());
             }
+        return run_solver(offs, lits, 0);
+    }
+
+    // Streaming solve (reference SATInstance.h:70-153): clauses come from a callback by index.
+    // With 288 GB of HBM the instance is materialised once (callback order and t_id as the
+    // reference's per-thread generators would use) and the GPU runs the streaming semantics of
+    // one thread: the MIS follows the generator's yield order, batch by batch
+    // (alll_options.stream_batch); a batch size of 0 is taken as 1.
+    Statistics* solve(Clause<T>* (*getEnumeratedClause)(T, unsigned short int), ull n_clauses, T batch_size) {
+        this->n_clauses = n_clauses;
+        vector<uint64_t> offs(1, 0);
+        vector<uint32_t> lits;
+        const int nt = n_threads_ > 0 ? n_threads_ : 1;
+        const ull per = n_clauses / (ull)nt;
+        for (ull i = 0; i < n_clauses; ++i) {
+            const unsigned short t = (unsigned short)(per ? std::min<ull>(i / per, (ull)nt - 1) : 0);
+            Clause<T>* cl = getEnumeratedClause((T)i, t);
+            if (!cl) throw std::runtime_error("alll: clause generator returned nullptr");
+            for (auto l : *cl->literals) lits.push_back((uint32_t)l);
+            offs.push_back(lits.size());
+            delete cl->literals;
+            delete cl;
+        }
+        return run_solver(offs, lits, batch_size > 0 ? (uint64_t)batch_size : 1);
+    }
+
+    // DIMACS export of a generated instance (reference SATInstance.h:175-203, same layout).
+    void writeDIMACS(Clause<T>* (*getEnumeratedClause)(T, unsigned short int), ull n_clauses, ofstream* out_f) {
+        this->n_clauses = n_clauses;
+        *out_f << "p cnf " << n_vars << " " << n_clauses << endl;
+        for (ull i = 0; i < n_clauses; i++) {
+            Clause<T>* clause = getEnumeratedClause((T)i, 0);
+            if (!clause) throw std::runtime_error("alll: clause generator returned nullptr");
+            for (auto& l : *(clause->literals)) {
+                if (l & 1) *out_f << " " << to_string(-((intmax_t)(l >> 1)) - 1);
+                else *out_f << " " << to_string((l >> 1) + 1);
+            }
+            *out_f << " 0" << endl;
+            delete clause->literals;
+            delete clause;
+            if (i % 1000 == 0) out_f->flush();
+        }
+        out_f->flush();
+    }
+
+    // Host check over var_arr->vars, like the reference.
+    bool verify_validity(vector<ClauseArray*>* clauses) const {
+        for (auto chunk : *clauses)
+            for (auto cl : *chunk)
+                if (cl->is_not_satisfied(var_arr->vars)) return false;
+        return true;
+    }
+
+   private:
+    int n_threads_{};
+
+    Statistics* run_solver(const vector<uint64_t>& offs, const vector<uint32_t>& lits, uint64_t stream_batch) {
         alll_problem p{(uint32_t)n_vars, 0, offs.size() - 1, offs.data(), lits.data()};
         alll_options o;
         alll_default_options(&o);
@@ -61,6 +120,7 @@ class SATInstance {
         o.max_iters = alll_compat::env_u64("ALLL_MAX_ITERS", 0);
         o.device = (int32_t)alll_compat::env_u64("ALLL_DEVICE", (uint64_t)-1);
         o.n_threads = n_threads_ > 0 ? n_threads_ : 1;
+        o.stream_batch = stream_batch;
         alll_ctx* ctx = nullptr;
         check(alll_create(&p, &o, &ctx));
         vector<uint8_t> a(n_vars > 0 ? n_vars : 1);
@@ -84,17 +144,6 @@ class SATInstance {
         for (int g = 0; g < st.n_gpus && g < ALLL_MAX_GPU_STATS; ++g) s->n_thread_resamples[g] = st.gpu_resamples[g];
         return s;
     }
-
-    // Host check over var_arr->vars, like the reference.
-    bool verify_validity(vector<ClauseArray*>* clauses) const {
-        for (auto chunk : *clauses)
-            for (auto cl : *chunk)
-                if (cl->is_not_satisfied(var_arr->vars)) return false;
-        return true;
-    }
-
-   private:
-    int n_threads_{};
 
     static void check(int rc) {
         if (rc != ALLL_OK) throw std::runtime_error(std::string("alll: ") + alll_last_error());

@@ -1,6 +1,7 @@
 """The drop-in surface above the C-ABI: the CMake package (find_package + target, as the
 reference's example/CMakeLists.txt consumes it), the SATInstance compatibility headers and the
 Boost-free CLI with the flags and output of example/main.cpp (-h, -o, -p N, --sat)."""
+import json
 import os
 import shutil
 import subprocess
@@ -72,3 +73,63 @@ def test_cli_unsolvable_cap_exit_code(native, tmp_path):
     assert r.returncode == 1
     assert "ERROR: Solver converged to an invalid solution!" in r.stdout
     assert "# Iterations\t= 50" in r.stdout
+
+
+# ---- compatibility API: streaming solve(getEnumeratedClause, n, batch) and writeDIMACS ---------
+STREAM_DRIVER_SRC = os.path.join(ROOT, "tests", "cpp", "stream_compat.cpp")
+
+
+def _build_stream_driver(tmp_path):
+    exe = str(tmp_path / "stream_compat")
+    lib_dir = os.path.join(ROOT, "alllsatisfiabilitysolver_amd")
+    r = subprocess.run(["g++", "-std=c++20", "-O2", "-fopenmp", "-I" + os.path.join(ROOT, "include", "alll_compat"),
+                        "-I" + os.path.join(ROOT, "include"), "-o", exe, STREAM_DRIVER_SRC, "-L" + lib_dir, "-lalll",
+                        "-Wl,-rpath," + lib_dir], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    return exe
+
+
+def test_compat_stream_api_compiles(native, tmp_path):
+    """The compatibility SATInstance exposes both solve overloads and writeDIMACS."""
+    _build_stream_driver(tmp_path)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("batch", [1, 50, 100000])
+def test_compat_stream_solve_matches_oracle(oracle_mod, native, tmp_path, batch):
+    o = oracle_mod
+    exe = _build_stream_driver(tmp_path)
+    n, m, seed = 300, 600, 17
+    offs, lits = o.generate_ksat(5, n, m, 3)
+    cnf = tmp_path / "x.cnf"
+    cnf.write_text(o.to_dimacs(n, offs, lits))
+    out = tmp_path / "w.cnf"
+    env = dict(os.environ, ALLL_SEED=str(seed))
+    r = subprocess.run([exe, str(cnf), str(batch), str(out)], capture_output=True, text=True, env=env)
+    assert r.returncode == 0, r.stderr
+    got = json.loads(r.stdout)
+    st, A, _ = o.solve_stream(n, offs, lits, seed, batch)
+    assert st["solved"] == 1
+    for key in ("n_iterations", "n_resamples", "avg_mis_size"):
+        assert got[key] == st[key], key
+    bits = np.frombuffer(got["assignment"].encode(), np.uint8) - 48
+    np.testing.assert_array_equal(o.pack_bools(bits), A)
+    # writeDIMACS wrote the same instance
+    rc, parsed = o.dimacs_parse(out.read_bytes())
+    assert rc == 0
+    v, offs2, lits2 = parsed
+    assert v == n
+    np.testing.assert_array_equal(offs2, offs)
+    np.testing.assert_array_equal(lits2, lits)
+
+
+def test_compat_clause_generator_order(oracle_mod, native, tmp_path):
+    """The compatibility ClauseGenerator walks clauses in the reference generator's order
+    (ClauseGenerator.h:47), continuing across passes."""
+    exe = _build_stream_driver(tmp_path)
+    for m, batch in [(1, 1), (10, 3), (400, 64), (4099, 1000)]:
+        r = subprocess.run([exe, "order", str(m), str(batch)], capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr
+        got = json.loads(r.stdout)
+        order = oracle_mod.stream_order(m)
+        np.testing.assert_array_equal(got, np.concatenate([order, order]))

@@ -17,6 +17,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -156,6 +157,202 @@ int parse(const char* buf, uint64_t len, Parsed& P) {
     return P.rc;
 }
 
+// ---- parallel loader (large inputs) ------------------------------------------------------
+// Same semantics as parse(): the header is found serially; the data lines after it (up to the
+// last '\n': an unterminated last line is dropped) are cut at line starts into one chunk per
+// thread.  Every line's words are independent of other lines, so pass 1 counts the numbers
+// per chunk (literals, clause-closing zeros), a prefix over the chunks gives each chunk its
+// first clause index and literal position, and pass 2 writes literals and clause ends in
+// place.  Clauses beyond the header's count are ignored as in parse().
+
+// Calls f(value) for every number word of the data lines in [b, e); e[-1] is a '\n', which
+// serves as the sentinel of every scan.  One pass per byte, fusing the line, word and number
+// rules of parse()/read_word().
+inline bool is_digit(char ch) { return (unsigned)(ch - '0') <= 9u; }
+
+template <typename F>
+inline void for_each_number(const char* b, const char* e, F&& f) {
+    const char* p = b;
+    while (p < e) {
+        if (*p == 'c' || *p == 'C') {  // comment line
+            p = static_cast<const char*>(memchr(p, '\n', (size_t)(e - p))) + 1;
+            continue;
+        }
+        for (;;) {
+            while (*p == ' ') ++p;
+            const char ch = *p;
+            if (ch == '\n') {
+                ++p;
+                break;
+            }
+            const char* q = p;
+            long long sign = 1;
+            if (ch == '-' || ch == '+') {
+                sign = (ch == '-') ? -1 : 1;
+                ++q;
+            }
+            if (!is_digit(*q)) {  // not a number: the rest of the line is ignored
+                p = static_cast<const char*>(memchr(p, '\n', (size_t)(e - p))) + 1;
+                break;
+            }
+            long long v = 0;
+            do {
+                v = v * 10 + (*q - '0');
+                if (v > (1ll << 40)) v = 1ll << 40;
+                ++q;
+            } while (is_digit(*q));
+            while (*q != ' ' && *q != '\n') ++q;  // trailing non-digits of the word
+            p = q;
+            if (!f(sign * v)) return;
+        }
+    }
+}
+
+struct ChunkCount {
+    const char* b;
+    const char* e;
+    uint64_t lits = 0, zeros = 0;
+    uint64_t tail = 0;     // literals after the chunk's last zero
+    uint64_t bad = ~0ull;  // clause (counted within the chunk) of the first out-of-range literal
+};
+
+// returns ALLL_OK / ALLL_ERR_BAD_INPUT / ALLL_ERR_LITERAL_RANGE; offsets/literals may be null
+int parse_parallel(const char* buf, uint64_t len, unsigned nt, uint32_t* n_vars, uint64_t* n_clauses,
+                   uint64_t* offsets, uint32_t* literals, uint64_t* n_literals) {
+    // header: first line that is neither a comment nor blank
+    const char* end = buf + len;
+    const char* p = buf;
+    long long V = 0, C = 0;
+    bool header = false;
+    while (p < end) {
+        const char* le = static_cast<const char*>(memchr(p, '\n', (size_t)(end - p)));
+        if (!le) break;
+        const char* ls = p;
+        p = le + 1;
+        if (le > ls && (ls[0] == 'c' || ls[0] == 'C')) continue;
+        const char* t = le;
+        while (t > ls && t[-1] == ' ') --t;
+        if (t == ls) continue;
+        if (!parse_header(ls, le, V, C)) {
+            g_host_err = "DIMACS: first non-comment line is not a valid 'p cnf V C' header";
+            return ALLL_ERR_BAD_INPUT;
+        }
+        header = true;
+        break;
+    }
+    if (!header) {
+        g_host_err = "DIMACS: no 'p cnf' header";
+        return ALLL_ERR_BAD_INPUT;
+    }
+    // data: [p, data_end), data_end just after the last '\n'
+    const char* data_end = p;
+    for (const char* q = end; q > p; --q)
+        if (q[-1] == '\n') { data_end = q; break; }
+    std::vector<ChunkCount> ch;
+    const uint64_t span = (uint64_t)(data_end - p);
+    const char* cb = p;
+    for (unsigned i = 1; i <= nt && cb < data_end; ++i) {
+        const char* ce = (i == nt) ? data_end : p + span * i / nt;
+        if (ce < cb) ce = cb;
+        if (ce < data_end) {
+            const char* nl = static_cast<const char*>(memchr(ce, '\n', (size_t)(data_end - ce)));
+            ce = nl ? nl + 1 : data_end;
+        }
+        ch.push_back({cb, ce});
+        cb = ce;
+    }
+    auto run = [&](auto&& body) {
+        std::vector<std::thread> th;
+        for (size_t i = 0; i < ch.size(); ++i) th.emplace_back(body, i);
+        for (auto& t : th) t.join();
+    };
+    run([&](size_t i) {
+        ChunkCount& c = ch[i];
+        for_each_number(c.b, c.e, [&](long long v) {
+            if (v == 0) {
+                ++c.zeros;
+                c.tail = 0;
+            } else if (v <= V && -v <= V) {  // out-of-range literals are skipped, as in parse()
+                ++c.lits;
+                ++c.tail;
+            } else if (c.bad == ~0ull) {
+                c.bad = c.zeros;
+            }
+            return true;
+        });
+    });
+    std::vector<uint64_t> cl_base(ch.size() + 1, 0), lit_base(ch.size() + 1, 0);
+    for (size_t i = 0; i < ch.size(); ++i) {
+        cl_base[i + 1] = cl_base[i] + ch[i].zeros;
+        lit_base[i + 1] = lit_base[i] + ch[i].lits;
+    }
+    if (cl_base[ch.size()] < (uint64_t)C) {
+        g_host_err = "DIMACS: header announces " + std::to_string(C) + " clauses, found " +
+                     std::to_string(cl_base[ch.size()]);
+        return ALLL_ERR_BAD_INPUT;
+    }
+    // literals of the first C clauses: up to the C-th zero
+    uint64_t nlits = 0;
+    if (C > 0 && cl_base[ch.size()] == (uint64_t)C) {  // all literals but those after the last zero
+        nlits = lit_base[ch.size()];
+        for (size_t i = ch.size(); i-- > 0;) {
+            nlits -= ch[i].tail;
+            if (ch[i].zeros) break;
+        }
+    } else if (C > 0) {  // clauses past the header's count: find where the C-th ends
+        size_t t = 0;
+        while (cl_base[t + 1] < (uint64_t)C) ++t;
+        uint64_t cl = cl_base[t], lp = lit_base[t];
+        for_each_number(ch[t].b, ch[t].e, [&](long long v) {
+            if (v) {
+                lp += (v <= V && -v <= V);
+                return true;
+            }
+            return ++cl < (uint64_t)C;
+        });
+        nlits = lp;
+    }
+    // pass 2: literals and clause ends in place
+    if (offsets || literals) {
+        if (offsets) offsets[0] = 0;
+        run([&](size_t i) {
+            uint64_t cl = cl_base[i], lp = lit_base[i];
+            if (cl >= (uint64_t)C) return;
+            for_each_number(ch[i].b, ch[i].e, [&](long long x) {
+                if (x != 0) {
+                    if (x <= V && -x <= V) {
+                        if (literals) literals[lp] = x > 0 ? (uint32_t)(2 * x - 2) : (uint32_t)(-2 * x - 1);
+                        ++lp;
+                    }
+                    return true;
+                }
+                if (offsets) offsets[cl + 1] = lp;
+                return ++cl < (uint64_t)C;
+            });
+        });
+    }
+    if (n_vars) *n_vars = (uint32_t)V;
+    if (n_clauses) *n_clauses = (uint64_t)C;
+    if (n_literals) *n_literals = nlits;
+    uint64_t first_bad = ~0ull;  // the first out-of-range literal among the first C clauses
+    for (size_t i = 0; i < ch.size() && first_bad == ~0ull; ++i)
+        if (ch[i].bad != ~0ull && cl_base[i] + ch[i].bad < (uint64_t)C) first_bad = cl_base[i] + ch[i].bad;
+    if (first_bad != ~0ull) {
+        g_host_err = "DIMACS: literal outside [1, V] in clause " + std::to_string(first_bad);
+        return ALLL_ERR_LITERAL_RANGE;
+    }
+    return ALLL_OK;
+}
+
+unsigned loader_threads(uint64_t len) {
+    uint64_t min_parallel = 8ull << 20;  // below this the serial parse is as fast
+    if (const char* e = getenv("ALLL_DIMACS_MIN_PARALLEL")) min_parallel = strtoull(e, nullptr, 10);
+    if (len < min_parallel) return 1;
+    unsigned nt = std::min(32u, std::thread::hardware_concurrency());
+    if (const char* e = getenv("ALLL_DIMACS_THREADS")) nt = (unsigned)std::max(1l, std::min(256l, strtol(e, nullptr, 10)));
+    return std::max(2u, nt);
+}
+
 int deliver(const Parsed& P, uint32_t* n_vars, uint64_t* n_clauses, uint64_t* offsets,
             uint32_t* literals, uint64_t* n_literals) {
     if (n_vars) *n_vars = (uint32_t)P.V;
@@ -237,6 +434,8 @@ int alll_initial_assignment(uint64_t seed, uint32_t n_vars, uint8_t* out) {
 int alll_dimacs_parse(const char* buf, uint64_t len, uint32_t* n_vars, uint64_t* n_clauses,
                       uint64_t* offsets, uint32_t* literals, uint64_t* n_literals) {
     if (!buf && len) return ALLL_ERR_INVALID_ARG;
+    const unsigned nt = loader_threads(len);
+    if (nt > 1) return parse_parallel(buf, len, nt, n_vars, n_clauses, offsets, literals, n_literals);
     Parsed P;
     int rc = parse(buf, len, P);
     if (rc == ALLL_ERR_BAD_INPUT) return rc;

@@ -119,6 +119,117 @@ def test_product_dimacs_roundtrip_file(native, oracle_mod, tmp_path):
     np.testing.assert_array_equal(lits, lits3)
 
 
+def _messy_dimacs(rng, n_vars, n_clauses, bad=None):
+    """DIMACS text exercising the loader's line rules: comments, blank lines, clauses split
+    over lines and several clauses on one line, trailing words after a non-number, extra
+    clauses past the header count, and optionally an out-of-range literal."""
+    lines = ["c generated", "", "p cnf %d %d" % (n_vars, n_clauses)]
+    cur = []
+    for c in range(n_clauses + 5):
+        k = int(rng.integers(0, 6))
+        lits = [int(v) * (1 if rng.integers(0, 2) else -1) for v in rng.integers(1, n_vars + 1, k)]
+        if bad is not None and c == bad:
+            lits.append(n_vars + 3)
+        toks = [str(x) for x in lits] + ["0"]
+        r = rng.integers(0, 10)
+        if r == 0:
+            lines.append("c " + " ".join(toks))
+        if r == 1:
+            lines.append("   ")
+        if r == 2 and len(toks) > 1:       # clause split over two lines
+            cur += toks[:1]
+            lines.append(" ".join(cur))
+            cur = toks[1:]
+        else:
+            cur += toks
+        if r != 3:                         # r == 3: next clause shares the line
+            if r == 4:
+                cur.append("x 7 0")        # a non-number word ends the line
+            lines.append("  ".join(cur))
+            cur = []
+    lines.append(" ".join(cur + ["1", "0"]))
+    return ("\n".join(lines) + "\n").encode()
+
+
+@pytest.fixture
+def force_parallel_loader(monkeypatch):
+    monkeypatch.setenv("ALLL_DIMACS_MIN_PARALLEL", "0")
+
+
+def test_parallel_dimacs_matches_reference_loader(native, force_parallel_loader):
+    test_product_dimacs_matches_reference_loader(native)
+
+
+def test_parallel_dimacs_errors(native, force_parallel_loader, tmp_path):
+    test_product_dimacs_errors(native, tmp_path)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_parallel_dimacs_matches_oracle(native, oracle_mod, monkeypatch, seed):
+    from alllsatisfiabilitysolver_amd import parse_dimacs
+
+    rng = np.random.default_rng(seed)
+    text = _messy_dimacs(rng, 500, 20000)
+    rc, (v0, o0, l0) = oracle_mod.dimacs_parse(text)
+    assert rc == 0
+    for thresh in ["0", str(1 << 40)]:     # parallel, serial
+        monkeypatch.setenv("ALLL_DIMACS_MIN_PARALLEL", thresh)
+        v, offs, lits = parse_dimacs(text)
+        assert v == v0
+        np.testing.assert_array_equal(offs, o0)
+        np.testing.assert_array_equal(lits, l0)
+
+
+@pytest.mark.parametrize("text", [
+    b"p cnf 3 1\n1 0\n2\n",                 # literals after the last zero
+    b"p cnf 3 1\n1 0 2 3\n",
+    b"p cnf 3 2\n1 0 2 0 3 0\n-1\n",        # clauses past the header's count
+    b"p cnf 3 0\n1 2\n",
+    b"p cnf 3 0\n",
+    b"c x\n\n  \np cnf 3 2\n+1 2x 0 -3\n\n2\t0 -\n0\n",  # signs, trailing non-digits, tabs
+])
+def test_parallel_dimacs_edge_cases(native, oracle_mod, monkeypatch, text):
+    from alllsatisfiabilitysolver_amd import parse_dimacs
+
+    rc, (v0, o0, l0) = oracle_mod.dimacs_parse(text)
+    assert rc == 0
+    for nt in ["2", "3", "64"]:
+        monkeypatch.setenv("ALLL_DIMACS_MIN_PARALLEL", "0")
+        monkeypatch.setenv("ALLL_DIMACS_THREADS", nt)
+        v, offs, lits = parse_dimacs(text)
+        assert v == v0
+        np.testing.assert_array_equal(offs, o0)
+        np.testing.assert_array_equal(lits, l0)
+
+
+def test_parallel_dimacs_literal_range(native, monkeypatch):
+    """Out-of-range literals: same error code, clause index in the message and skipped
+    literals as the serial loader."""
+    L = native.lib()
+    rng = np.random.default_rng(7)
+    for bad in [0, 777, 19999, 20002]:    # 20002 is past the header count: not an error
+        text = _messy_dimacs(rng, 300, 20000, bad=bad)
+        res = []
+        for thresh in ["0", str(1 << 40)]:
+            monkeypatch.setenv("ALLL_DIMACS_MIN_PARALLEL", thresh)
+            v, c, ln = ctypes.c_uint32(), ctypes.c_uint64(), ctypes.c_uint64()
+            rc = L.alll_dimacs_parse(text, len(text), ctypes.byref(v), ctypes.byref(c), None, None,
+                                     ctypes.byref(ln))
+            msg = native.last_error()
+            offs = np.zeros(c.value + 1, np.uint64)
+            lits = np.zeros(max(1, ln.value), np.uint32)
+            rc2 = L.alll_dimacs_parse(text, len(text), ctypes.byref(v), ctypes.byref(c),
+                                      offs.ctypes.data_as(native._u64p), lits.ctypes.data_as(native._u32p),
+                                      ctypes.byref(ln))
+            res.append((rc, rc2, msg if rc else "", offs, lits))
+        (p_rc, p_rc2, p_msg, p_o, p_l), (s_rc, s_rc2, s_msg, s_o, s_l) = res
+        assert (p_rc, p_rc2) == (s_rc, s_rc2)
+        assert p_rc == (native.ALLL_ERR_LITERAL_RANGE if bad < 20000 else native.ALLL_OK)
+        assert p_msg == s_msg and (bad >= 20000 or f"clause {bad}" in p_msg)
+        np.testing.assert_array_equal(p_o, s_o)
+        np.testing.assert_array_equal(p_l, s_l)
+
+
 @pytest.mark.parametrize("kind", [0, 1])
 def test_product_generator_matches_oracle(native, oracle_mod, kind):
     from alllsatisfiabilitysolver_amd import generate_ksat

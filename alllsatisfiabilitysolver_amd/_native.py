@@ -31,6 +31,7 @@ FLAG_GENERIC_CSR = 1 << 2
 FLAG_NO_RANGED = 1 << 3
 FLAG_KERNEL_TIMING = 1 << 4
 FLAG_ATOMIC_CLAIMS = 1 << 5
+FLAG_LFMIS = 1 << 6
 
 MAX_GPU_STATS = 64
 
@@ -73,6 +74,7 @@ class Options(ctypes.Structure):
         ("flags", ctypes.c_uint32),
         ("grid_rounds", ctypes.c_uint32),
         ("stream_batch", ctypes.c_uint64),
+        ("set_starts", ctypes.POINTER(ctypes.c_uint64)),
     ]
 
 

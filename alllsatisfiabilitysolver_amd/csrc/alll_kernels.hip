@@ -1333,6 +1333,355 @@ __global__ void k_apply_delta(LoopBuffers b) {
 }
 
 // ------------------------------------------------------------------------------------
+// Round-robin MIS of T > 1 clause chunks (populate_mis_parallel with T sets,
+// SATInstance.h:414-447).  The reference keeps one list U_q of violated clauses per chunk q
+// and a list of live sets; turn after turn, t <- (t + 1) % |sets|: an empty set is erased
+// (t is not decremented, so its successor is skipped), otherwise the set's front clause joins
+// the MIS and every clause sharing a variable with it is erased from every set.  A clause is
+// erased exactly when one of its variables is covered by an MIS clause, so a set is a pointer
+// into its sorted list, the front is the first clause at or after it with no covered variable,
+// and the sequence of turns is the whole algorithm.
+//
+// One 1024-thread workgroup runs the turns in speculative batches.  B = min(|sets|, groups)
+// consecutive sets get a lane group each; when every live set has a group, each group also
+// runs D levels (its set's next D turns).  A group scans its list, GS clauses per step, and
+// picks its next fronts greedily, assuming that only its own picks and the covered variables
+// matter.  Turn l*B + g belongs to group g, level l.  The batch is exact up to the first turn
+// whose pick shares a variable with a pick of an earlier turn of the batch (an LDS hash keeps
+// the earliest turn per variable) and up to the first turn a group could not decide; those
+// turns are committed (cover + MIS), and the first undecided turn of an exhausted set is its
+// erasure.  Skipped clauses before a group's first uncommitted pick are erased for certain
+// (covered by committed picks), so no scan is repeated.
+constexpr int RR_THREADS = 1024;
+constexpr uint32_t RR_HASH = 4096;      // LDS hash slots (variable -> earliest turn)
+constexpr uint32_t RR_VCAP = 2048;      // variables of the picks of one batch
+constexpr uint32_t RR_CMAX = 1024;      // picks of one batch
+constexpr uint32_t RR_DMAX = 32;        // levels per group
+constexpr uint32_t RR_KR = 8;           // clause variables kept in registers while scanning
+constexpr uint32_t RR_SCAN_STEPS = 4;   // scan steps per group per batch
+
+struct RRLds {
+    uint32_t hkey[RR_HASH];
+    uint32_t hmin[RR_HASH];
+    uint32_t var[RR_VCAP];     // group g: [g*vpg, g*vpg + nvar[g])
+    uint32_t vtau[RR_VCAP];    // turn of the pick the variable belongs to
+    uint32_t cc[RR_CMAX];      // group g: [g*cpg, g*cpg + ncand[g]) picked clause ids
+    uint32_t cpos[RR_CMAX];    // their positions in U
+    uint32_t cw[RR_CMAX];      // their widths
+    uint32_t ptr[RR_TMAX];     // per set: position in U of the first clause not known erased
+    uint32_t end[RR_TMAX];     // per set: end of its clauses in U
+    uint16_t live[RR_TMAX];    // live sets in the reference's vector order
+    uint32_t ncand[64], nvar[64], scan_end[64], exh[64];
+    uint32_t n_live, t, trunc, tm, wide;
+};
+
+__device__ __forceinline__ uint32_t rr_hash(uint32_t v) { return (v * 0x9E3779B1u) >> (32 - 12); }
+
+__global__ __launch_bounds__(RR_THREADS) void k_rr_mis(ClauseView cv, LoopBuffers b) {
+    DevState* st = b.state;
+    if (!st->active) return;
+    extern __shared__ __align__(16) unsigned char rr_lds_raw[];
+    RRLds& L = *reinterpret_cast<RRLds*>(rr_lds_raw);
+    const uint32_t stamp = st->stamp;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63;
+    const uint32_t T = b.rr_T;
+    const uint64_t m = cv.m;
+    uint32_t* U = b.rr_u;
+
+    // ---- U: violated clause ids in clause order (the bitmask is in clause order: CSR layout)
+    __shared__ uint32_t s_wsum[RR_THREADS / 64];
+    __shared__ uint32_t s_base;
+    if (tid == 0) s_base = 0;
+    __syncthreads();
+    const uint64_t nw = (m + 63) / 64;
+    for (uint64_t w0 = 0; w0 < nw; w0 += RR_THREADS) {
+        const uint64_t w = w0 + tid;
+        uint64_t x = w < nw ? b.vmask[w] : 0ull;
+        if (w == nw - 1 && (m & 63)) x &= (1ull << (m & 63)) - 1ull;
+        const uint32_t cnt = (uint32_t)__popcll(x);
+        uint32_t incl = cnt;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o, 64);
+            if ((int)lane >= o) incl += y;
+        }
+        if (lane == 63) s_wsum[tid >> 6] = incl;
+        __syncthreads();
+        uint32_t wave_off = 0, total = 0;
+        for (uint32_t q = 0; q < RR_THREADS / 64; ++q) {
+            const uint32_t v = s_wsum[q];
+            if (q < (tid >> 6)) wave_off += v;
+            total += v;
+        }
+        uint32_t o = s_base + wave_off + incl - cnt;
+        while (x) {
+            U[o++] = (uint32_t)(w * 64 + (uint32_t)__builtin_ctzll(x));
+            x &= x - 1;
+        }
+        __threadfence();
+        __syncthreads();
+        if (tid == 0) s_base += total;
+        __syncthreads();
+    }
+    const uint32_t nu = s_base;
+    // ---- sets: [lower_bound(start q), lower_bound(start q+1)) of U
+    for (uint32_t q = tid; q < T; q += RR_THREADS) {
+        uint32_t bnd[2];
+        for (int e = 0; e < 2; ++e) {
+            const uint32_t key = b.rr_sets[q + e];
+            uint32_t lo = 0, hi = nu;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (U[mid] < key) lo = mid + 1; else hi = mid;
+            }
+            bnd[e] = lo;
+        }
+        L.ptr[q] = bnd[0];
+        L.end[q] = bnd[1];
+        L.live[q] = (uint16_t)q;
+    }
+    if (tid == 0) { L.n_live = T; L.t = 0; L.tm = 0; L.wide = 0; }
+    __threadfence();
+    __syncthreads();
+
+    uint32_t batches = 0;
+    while (true) {
+        const uint32_t n_live = L.n_live;
+        if (n_live == 0) break;
+        // every batch commits a turn, erases a set or advances set 0's scan by a full budget
+        if (++batches > 2 * nu + 2 * T + 64) {
+            if (tid == 0) { st->error = 1; st->done = 3; }
+            break;
+        }
+        const uint32_t GS = n_live <= RR_THREADS / 64 ? 64u : 16u;  // lanes per group
+        const uint32_t NG = RR_THREADS / GS;
+        const uint32_t B = n_live < NG ? n_live : NG;
+        const uint32_t vpg = RR_VCAP / NG, cpg = RR_CMAX / NG;
+        const uint32_t D = (B == n_live) ? (cpg < RR_DMAX ? cpg : RR_DMAX) : 1u;
+        const uint32_t t0 = L.t;
+        // ---- scan: group g decides the next D turns of set live[(t + 1 + g) % n_live]
+        {
+            const uint32_t g = tid / GS, gl = tid % GS;
+            const uint32_t gshift = lane & ~(GS - 1);
+            const uint64_t gmask = GS == 64 ? ~0ull : ((1ull << GS) - 1ull);
+            if (g < B) {
+                const uint32_t s = L.live[(t0 + 1 + g) % n_live];
+                uint32_t pos = L.ptr[s];
+                const uint32_t end = L.end[s];
+                uint32_t nc = 0, nv = 0, scan_end = pos, exhausted = 0;
+                const uint32_t vb = g * vpg, cb = g * cpg;
+                for (uint32_t step = 0;; ++step) {
+                    if (pos >= end) { exhausted = 1; scan_end = end; break; }
+                    if (step == RR_SCAN_STEPS) { scan_end = pos; break; }
+                    const uint32_t i = pos + gl;
+                    const bool valid = i < end;
+                    uint32_t c = 0, lb = 0, w = 0;
+                    if (valid) {
+                        c = U[i];
+                        lb = cv.offs[c];
+                        w = cv.offs[c + 1] - lb;
+                    }
+                    uint32_t rv[RR_KR];
+                    bool alive = valid;
+#pragma unroll
+                    for (uint32_t j = 0; j < RR_KR; ++j) {
+                        rv[j] = 0xFFFFFFFFu;
+                        if (j < w) {
+                            rv[j] = lit_var(cv.lits[lb + j]);
+                            alive &= __hip_atomic_load(&b.cover[rv[j]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != stamp;
+                        }
+                    }
+                    for (uint32_t j = RR_KR; j < w; ++j)
+                        alive &= __hip_atomic_load(&b.cover[lit_var(cv.lits[lb + j])], __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT) != stamp;
+                    // variables of this group's earlier picks in the batch
+                    if (alive) {
+                        for (uint32_t q = 0; q < nv && alive; ++q) {
+                            const uint32_t ov = L.var[vb + q];
+#pragma unroll
+                            for (uint32_t j = 0; j < RR_KR; ++j) alive &= rv[j] != ov;
+                            for (uint32_t j = RR_KR; j < w; ++j) alive &= lit_var(cv.lits[lb + j]) != ov;
+                        }
+                    }
+                    uint64_t gm = (__ballot(alive) >> gshift) & gmask;
+                    bool stop = false;
+                    while (gm) {
+                        const uint32_t i0 = (uint32_t)__builtin_ctzll(gm);
+                        const uint32_t src = gshift + i0;
+                        const uint32_t w0 = __shfl(w, (int)src, 64);
+                        if (nc == D) { stop = true; scan_end = pos + i0; break; }
+                        if (nv + w0 > vpg) {
+                            stop = true;
+                            scan_end = pos + i0;
+                            if (nc == 0 && g == 0) {
+                                // turn 0 is always exact: a pick too wide to record is
+                                // committed alone (its variables are covered from memory)
+                                if (gl == i0) {
+                                    L.cc[cb] = c;
+                                    L.cpos[cb] = i;
+                                    L.cw[cb] = w;
+                                    L.wide = 1;
+                                }
+                                nc = 1;
+                                scan_end = pos + i0 + 1;
+                            }
+                            break;
+                        }
+                        const uint32_t lb0 = __shfl(lb, (int)src, 64);
+                        const uint32_t tau = nc * B + g;
+                        if (gl == i0) {
+                            L.cc[cb + nc] = c;
+                            L.cpos[cb + nc] = i;
+                            L.cw[cb + nc] = w;
+                        }
+                        // the pick's variables: record them, and drop later lanes sharing one
+#pragma unroll
+                        for (uint32_t j0 = 0; j0 < RR_KR; ++j0) {
+                            if (j0 < w0) {
+                                const uint32_t v0 = __shfl(rv[j0], (int)src, 64);
+                                if (gl == i0) { L.var[vb + nv + j0] = v0; L.vtau[vb + nv + j0] = tau; }
+                                if (gl > i0 && alive) {
+#pragma unroll
+                                    for (uint32_t j = 0; j < RR_KR; ++j) alive &= rv[j] != v0;
+                                    for (uint32_t j = RR_KR; j < w; ++j) alive &= lit_var(cv.lits[lb + j]) != v0;
+                                }
+                            }
+                        }
+                        for (uint32_t j0 = RR_KR; j0 < w0; ++j0) {
+                            const uint32_t v0 = lit_var(cv.lits[lb0 + j0]);
+                            if (gl == i0) { L.var[vb + nv + j0] = v0; L.vtau[vb + nv + j0] = tau; }
+                            if (gl > i0 && alive) {
+#pragma unroll
+                                for (uint32_t j = 0; j < RR_KR; ++j) alive &= rv[j] != v0;
+                                for (uint32_t j = RR_KR; j < w; ++j) alive &= lit_var(cv.lits[lb + j]) != v0;
+                            }
+                        }
+                        nv += w0;
+                        ++nc;
+                        gm = (__ballot(alive && gl > i0) >> gshift) & gmask;
+                        if (nc == D) {
+                            stop = true;
+                            scan_end = gm ? pos + (uint32_t)__builtin_ctzll(gm) : (pos + GS < end ? pos + GS : end);
+                            break;
+                        }
+                    }
+                    if (stop) break;
+                    pos += GS;
+                }
+                if (gl == 0) {
+                    L.ncand[g] = nc;
+                    L.nvar[g] = nv;
+                    L.scan_end[g] = scan_end;
+                    L.exh[g] = exhausted;
+                }
+            }
+        }
+        for (uint32_t i = tid; i < RR_HASH; i += RR_THREADS) { L.hkey[i] = 0xFFFFFFFFu; L.hmin[i] = 0xFFFFFFFFu; }
+        if (tid == 0) L.trunc = L.wide ? 1u : D * B;
+        __syncthreads();
+        // ---- earliest turn per variable, then the first turn that conflicts with an earlier one
+        for (uint32_t e = tid; e < B * vpg; e += RR_THREADS) {
+            const uint32_t g = e / vpg;
+            if (e - g * vpg >= L.nvar[g]) continue;
+            const uint32_t v = L.var[e], tau = L.vtau[e];
+            uint32_t h = rr_hash(v);
+            while (true) {
+                const uint32_t k = atomicCAS(&L.hkey[h], 0xFFFFFFFFu, v);
+                if (k == 0xFFFFFFFFu || k == v) { atomicMin(&L.hmin[h], tau); break; }
+                h = (h + 1) & (RR_HASH - 1);
+            }
+        }
+        if (tid < B) {
+            const uint32_t nc = L.ncand[tid];
+            if (nc < D) atomicMin(&L.trunc, nc * B + tid);  // first turn the group did not decide
+        }
+        __syncthreads();
+        for (uint32_t e = tid; e < B * vpg; e += RR_THREADS) {
+            const uint32_t g = e / vpg;
+            if (e - g * vpg >= L.nvar[g]) continue;
+            const uint32_t v = L.var[e], tau = L.vtau[e];
+            uint32_t h = rr_hash(v);
+            while (L.hkey[h] != v) h = (h + 1) & (RR_HASH - 1);
+            if (L.hmin[h] < tau) atomicMin(&L.trunc, tau);
+        }
+        __syncthreads();
+        const uint32_t trunc = L.trunc;
+        // ---- commit turns < trunc
+        for (uint32_t e = tid; e < B * vpg; e += RR_THREADS) {
+            const uint32_t g = e / vpg;
+            if (e - g * vpg >= L.nvar[g] || L.vtau[e] >= trunc) continue;
+            __hip_atomic_store(&b.cover[L.var[e]], stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (L.wide) {
+            const uint32_t c = L.cc[0], lb = cv.offs[c], w = L.cw[0];
+            for (uint32_t j = tid; j < w; j += RR_THREADS)
+                __hip_atomic_store(&b.cover[lit_var(cv.lits[lb + j])], stamp, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+        for (uint32_t e = tid; e < B * cpg; e += RR_THREADS) {
+            const uint32_t g = e / cpg, l = e - g * cpg;
+            if (l >= L.ncand[g] || l * B + g >= trunc) continue;
+            const uint32_t c = L.cc[e];
+            b.tmis[atomicAdd(&L.tm, 1u)] = c;
+            atomicAdd(&b.tile_stats[2 * (c / TILE)], 1ull);
+            atomicAdd(&b.tile_stats[2 * (c / TILE) + 1], (unsigned long long)L.cw[e]);
+        }
+        uint32_t new_ptr = 0, ptr_set = 0xFFFFFFFFu;
+        if (tid < B) {
+            const uint32_t g = tid, nc = L.ncand[g];
+            uint32_t a = trunc > g ? (trunc - g + B - 1) / B : 0;
+            if (a > nc) a = nc;
+            ptr_set = L.live[(t0 + 1 + g) % n_live];
+            new_ptr = a < nc ? L.cpos[g * cpg + a] : L.scan_end[g];
+        }
+        __threadfence();
+        __syncthreads();
+        if (ptr_set != 0xFFFFFFFFu) L.ptr[ptr_set] = new_ptr;
+        // ---- erasure at turn trunc, or the next turn index
+        bool erase = false;
+        uint32_t idx_e = 0;
+        if (trunc < D * B) {
+            const uint32_t ge = trunc % B, le = trunc / B;
+            erase = (le == L.ncand[ge]) && L.exh[ge];
+            idx_e = (t0 + 1 + trunc) % n_live;
+        }
+        uint16_t moved = 0;
+        if (erase && tid >= idx_e && tid + 1 < n_live) moved = L.live[tid + 1];
+        uint16_t moved2[RR_TMAX / RR_THREADS - 1];
+#pragma unroll
+        for (uint32_t r = 1; r < RR_TMAX / RR_THREADS; ++r) {
+            const uint32_t i = tid + r * RR_THREADS;
+            moved2[r - 1] = (erase && i >= idx_e && i + 1 < n_live) ? L.live[i + 1] : 0;
+        }
+        __syncthreads();
+        if (erase) {
+            if (tid >= idx_e && tid + 1 < n_live) L.live[tid] = moved;
+#pragma unroll
+            for (uint32_t r = 1; r < RR_TMAX / RR_THREADS; ++r) {
+                const uint32_t i = tid + r * RR_THREADS;
+                if (i >= idx_e && i + 1 < n_live) L.live[i] = moved2[r - 1];
+            }
+        }
+        if (tid == 0) {
+            L.wide = 0;
+            if (erase) {
+                L.n_live = n_live - 1;
+                L.t = idx_e;  // t is not decremented: the next turn skips the moved-up set
+            } else {
+                L.t = (t0 + trunc) % n_live;
+            }
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        st->tmis_cnt = L.tm;
+        st->tail_rounds = batches;
+        if (batches > st->max_rounds) st->max_rounds = batches;
+        if (b.ktime) time_slot(b, st->n_iter - 1)[3] = wall_now();
+    }
+}
+
+// ------------------------------------------------------------------------------------
 // Launchers.
 hipError_t launch_init_assignment(const LoopBuffers& b, hipStream_t s) {
     if (b.n_words == 0) return hipSuccess;
@@ -1444,6 +1793,19 @@ hipError_t launch_round0_buckets(const ClauseView& cv, const LoopBuffers& b, boo
 
 hipError_t launch_tail(const ClauseView& cv, const LoopBuffers& b, uint32_t first_round, hipStream_t s) {
     ALLL_DISPATCH_K(cv.k, (k_tail<K><<<1, TAIL_THREADS, 0, s>>>(cv, b, first_round)));
+    return hipGetLastError();
+}
+
+hipError_t launch_rr_mis(const ClauseView& cv, const LoopBuffers& b, hipStream_t s) {
+    if (cv.k != 0 || !b.rr_u || b.rr_T < 2 || b.rr_T > RR_TMAX) return hipErrorInvalidValue;
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void*)k_rr_mis, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)sizeof(RRLds));
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    k_rr_mis<<<1, RR_THREADS, sizeof(RRLds), s>>>(cv, b);
     return hipGetLastError();
 }
 

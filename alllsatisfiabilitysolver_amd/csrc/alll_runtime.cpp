@@ -111,7 +111,9 @@ int read_state(alll_ctx* c) {
     HIP_TRY(hipMemcpyAsync(c->h_state, c->b.state, sizeof(DevState), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (c->h_state->error)
-        return fail(ALLL_ERR_UNSUPPORTED, "LFMIS needed more than %u rounds in one iteration", MAX_TAIL_ROUNDS);
+        return fail(ALLL_ERR_UNSUPPORTED, c->b.rr_T ? "round-robin MIS exceeded its batch cap in one iteration"
+                                                    : "LFMIS needed more than %u rounds in one iteration",
+                    MAX_TAIL_ROUNDS);
     return ALLL_OK;
 }
 
@@ -179,11 +181,15 @@ int enqueue_iteration(alll_ctx* c, hipEvent_t* marks, int variant) {
     }
     if (marks) HIP_TRY(hipEventRecord(marks[2], s));
     HIP_TRY(launch_reduce(c->b, 0, s));
-    for (uint32_t r = 0; r < c->grid_rounds; ++r) {
-        if (r == 0 && variant == 1) HIP_TRY(launch_round0_buckets(c->cv, c->b, c->grid_rounds == 1, s));
-        else HIP_TRY(launch_round(c->cv, c->b, r, r + 1 == c->grid_rounds, s));
+    if (c->b.rr_T) {
+        HIP_TRY(launch_rr_mis(c->cv, c->b, s));
+    } else {
+        for (uint32_t r = 0; r < c->grid_rounds; ++r) {
+            if (r == 0 && variant == 1) HIP_TRY(launch_round0_buckets(c->cv, c->b, c->grid_rounds == 1, s));
+            else HIP_TRY(launch_round(c->cv, c->b, r, r + 1 == c->grid_rounds, s));
+        }
+        HIP_TRY(launch_tail(c->cv, c->b, c->grid_rounds, s));
     }
-    HIP_TRY(launch_tail(c->cv, c->b, c->grid_rounds, s));
     if (marks) HIP_TRY(hipEventRecord(marks[3], s));
     if (c->allreduce && c->world > 1) {
         HIP_TRY(launch_resample(c->cv, c->b, c->own_begin, c->own_end, true, s));
@@ -341,7 +347,32 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     }
     // the streaming solve keeps the clause-order (CSR) layout: its window rule needs the first
     // violated clause index, read from a clause-order bitmask
-    if (fixed_k < 1 || fixed_k > MAX_FIXED_K || (opt.flags & ALLL_FLAG_GENERIC_CSR) || opt.stream_batch)
+    // the round-robin MIS of T > 1 chunks (the reference's n_threads > 1) walks clause-order
+    // lists of violated clauses: CSR layout too
+    const uint32_t rr_T = (opt.n_threads > 1 && !(opt.flags & ALLL_FLAG_LFMIS) && !opt.stream_batch)
+                              ? (uint32_t)opt.n_threads : 0u;
+    if (rr_T > RR_TMAX) return fail(ALLL_ERR_UNSUPPORTED, "n_threads %u > %u chunks", rr_T, RR_TMAX);
+    std::vector<uint32_t> rr_sets;
+    if (rr_T) {
+        rr_sets.resize(rr_T + 1);
+        if (opt.set_starts) {
+            if (opt.set_starts[0] != 0 || opt.set_starts[rr_T] != m)
+                return fail(ALLL_ERR_INVALID_ARG, "set_starts must run from 0 to n_clauses");
+            for (uint32_t q = 0; q <= rr_T; ++q) {
+                if (q && opt.set_starts[q] < opt.set_starts[q - 1])
+                    return fail(ALLL_ERR_INVALID_ARG, "set_starts decrease at %u", q);
+                rr_sets[q] = (uint32_t)opt.set_starts[q];
+            }
+        } else {
+            // example/main.cpp:149-178: chunk_size = ceil(m / T); clause c moves to the next
+            // chunk when c > (t + 1) * chunk_size, so chunk q >= 1 starts at q * chunk_size + 1
+            const uint64_t chunk = (m + rr_T - 1) / rr_T;
+            rr_sets[0] = 0;
+            for (uint32_t q = 1; q <= rr_T; ++q) rr_sets[q] = (uint32_t)std::min<uint64_t>(m, q * chunk + 1);
+            rr_sets[rr_T] = (uint32_t)m;
+        }
+    }
+    if (fixed_k < 1 || fixed_k > MAX_FIXED_K || (opt.flags & ALLL_FLAG_GENERIC_CSR) || opt.stream_batch || rr_T)
         fixed_k = 0;
     const uint64_t lim = 2ull * prob->n_vars;
     for (uint64_t j = 0; j < L; ++j)
@@ -408,6 +439,16 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
         b.stream_batch = opt.stream_batch;
     }
     b.seed = opt.seed;
+    if (rr_T) {
+        uint32_t* d_sets = nullptr;
+        if ((rc = dalloc(c, &b.rr_u, m))) return bail(rc);
+        if ((rc = dalloc(c, &d_sets, rr_T + 1))) return bail(rc);
+        if (hipStreamSynchronize(c->stream) != hipSuccess ||
+            hipMemcpy(d_sets, rr_sets.data(), (rr_T + 1) * 4ull, hipMemcpyHostToDevice) != hipSuccess)
+            return bail(fail(ALLL_ERR_HIP, "chunk upload failed"));
+        b.rr_sets = d_sets;
+        b.rr_T = rr_T;
+    }
     if ((rc = dalloc(c, &b.A, b.n_words + 4))) return bail(rc);  // +4: 16-byte tail loads
     if ((rc = dalloc(c, &b.vmask, (size_t)c->n_tiles_padded * TILE_WORDS))) return bail(rc);
     if ((rc = dalloc(c, &b.tile_cnt, n_tiles))) return bail(rc);

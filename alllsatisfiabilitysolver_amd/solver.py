@@ -75,7 +75,7 @@ class Solver:
     def __init__(self, n_vars: int, offsets, literals, seed: int = 1, max_iters: int = 0,
                  device: int = -1, n_threads: int = 1, rank: int = 0, world: int = 1,
                  comm_id: Optional[bytes] = None, flags: int = 0, grid_rounds: int = 0,
-                 exchange=None, stream_batch: int = 0):
+                 exchange=None, stream_batch: int = 0, set_starts=None):
         self._L = N.lib()
         self.n_vars = int(n_vars)
         self.offsets = np.ascontiguousarray(offsets, np.uint64)
@@ -88,6 +88,11 @@ class Solver:
         opt.n_threads, opt.rank, opt.world = n_threads, rank, world
         opt.flags, opt.grid_rounds = flags, grid_rounds
         opt.stream_batch = stream_batch  # > 0: streaming solve semantics (alll.h)
+        # n_threads > 1: round-robin MIS over n_threads chunks (alll.h); set_starts = the
+        # n_threads + 1 chunk boundaries, None = the example/main.cpp chunking
+        if set_starts is not None:
+            self._set_starts = np.ascontiguousarray(set_starts, np.uint64)
+            opt.set_starts = _p(self._set_starts, _u64p)
         if comm_id is not None:
             ctypes.memmove(opt.comm_id, comm_id, 128)
         self._ctx = ctypes.c_void_p()
@@ -319,8 +324,14 @@ class SATInstance:
     def solve(self, clauses) -> Statistics:  # SATInstance.h:60-66
         self.n_clauses += sum(len(c) for c in clauses)
         offs, lits = self._flatten(clauses)
+        starts = None
+        if self.n_threads > 1:  # the MIS works on the caller's chunks (SATInstance.h:270-276, 414-447)
+            if len(clauses) != self.n_threads:
+                raise ValueError(f"{self.n_threads} threads need {self.n_threads} clause chunks, got {len(clauses)}")
+            starts = np.zeros(self.n_threads + 1, np.uint64)
+            starts[1:] = np.cumsum([len(c) for c in clauses])
         with Solver(self.n_vars, offs, lits, seed=self._seed, device=self._device,
-                    n_threads=self.n_threads, max_iters=self._max_iters) as s:
+                    n_threads=self.n_threads, max_iters=self._max_iters, set_starts=starts) as s:
             d = s.solve()
             self.var_arr.vars[:] = s.assignment().astype(np.bool_)
         thr = [0] * self.n_threads

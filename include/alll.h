@@ -58,12 +58,17 @@ typedef struct alll_problem {
                                                  times (alll_loop_times) */
 #define ALLL_FLAG_ATOMIC_CLAIMS     (1u << 5) /* LFMIS round 0 by global atomicMin claims instead of
                                                  the variable-bucketed LDS resolution */
+#define ALLL_FLAG_LFMIS             (1u << 6) /* n_threads > 1: keep the one-set MIS (the
+                                                 lexicographically-first MIS in clause order, fast)
+                                                 instead of the reference's T-set round robin */
 
 typedef struct alll_options {
     uint64_t seed;          /* Philox4x32-10 key; replaces std::random_device (SATInstance.h:346) */
     uint64_t max_iters;     /* cap on eval passes (n_iterations); 0 = unlimited like the reference */
     int32_t device;         /* HIP device ordinal; -1 = current device */
-    int32_t n_threads;      /* length of the per-thread resample vector reported (>= 1) */
+    int32_t n_threads;      /* the reference's n_threads T (SATInstance.h:51): T > 1 makes the MIS
+                               the round-robin greedy over T clause chunks (populate_mis_parallel,
+                               SATInstance.h:414-447; at most 4096 chunks) unless ALLL_FLAG_LFMIS */
     int32_t rank;           /* clause shard of this process (0 .. world-1) */
     int32_t world;          /* number of GPUs the clauses are sharded over (1 = single GPU) */
     uint8_t comm_id[128];   /* RCCL unique id from alll_comm_unique_id() on rank 0 (world > 1);
@@ -77,6 +82,11 @@ typedef struct alll_options {
                                (ClauseGenerator.h:33-70) and alll_stats reports its statistics
                                (n_iterations = stream iterations, avg_mis_size summed per batch);
                                max_iters then caps stream iterations */
+    const uint64_t* set_starts; /* n_threads > 1: n_threads + 1 non-decreasing clause indices,
+                               chunk q = [set_starts[q], set_starts[q+1]), set_starts[0] = 0,
+                               set_starts[n_threads] = n_clauses (the sizes of the caller's
+                               vector<ClauseArray*>); NULL = the chunking of example/main.cpp:
+                               149-178.  Read by alll_create only */
 } alll_options;
 
 #define ALLL_MAX_GPU_STATS 64

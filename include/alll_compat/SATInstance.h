@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <fstream>
 #include <iostream>
 #include <stdexcept>
@@ -56,7 +57,16 @@ class SATInstance {
                 for (auto l : *cl->literals) lits.push_back((uint32_t)l);
                 offs.push_back(lits.size());
             }
-        return run_solver(offs, lits, 0);
+        // n_threads > 1: the MIS is the reference's round robin over these chunks
+        // (SATInstance.h:270-276, 414-447), one chunk per thread
+        vector<uint64_t> starts;
+        if (n_threads_ > 1) {
+            if (clauses->size() != (size_t)n_threads_)
+                throw std::runtime_error("alll: n_threads clause chunks expected");
+            starts.push_back(0);
+            for (auto chunk : *clauses) starts.push_back(starts.back() + chunk->size());
+        }
+        return run_solver(offs, lits, 0, starts.empty() ? nullptr : starts.data());
     }
 
     // Streaming solve (reference SATInstance.h:70-153): clauses come from a callback by index.
@@ -112,7 +122,8 @@ class SATInstance {
    private:
     int n_threads_{};
 
-    Statistics* run_solver(const vector<uint64_t>& offs, const vector<uint32_t>& lits, uint64_t stream_batch) {
+    Statistics* run_solver(const vector<uint64_t>& offs, const vector<uint32_t>& lits, uint64_t stream_batch,
+                           const uint64_t* set_starts = nullptr) {
         alll_problem p{(uint32_t)n_vars, 0, offs.size() - 1, offs.data(), lits.data()};
         alll_options o;
         alll_default_options(&o);
@@ -121,6 +132,10 @@ class SATInstance {
         o.device = (int32_t)alll_compat::env_u64("ALLL_DEVICE", (uint64_t)-1);
         o.n_threads = n_threads_ > 0 ? n_threads_ : 1;
         o.stream_batch = stream_batch;
+        o.set_starts = set_starts;
+        // ALLL_MIS=lfmis: keep the one-set MIS for n_threads > 1 (faster, a different valid MIS)
+        if (const char* e = std::getenv("ALLL_MIS"))
+            if (std::string(e) == "lfmis") o.flags |= ALLL_FLAG_LFMIS;
         alll_ctx* ctx = nullptr;
         check(alll_create(&p, &o, &ctx));
         vector<uint8_t> a(n_vars > 0 ? n_vars : 1);

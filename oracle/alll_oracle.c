@@ -229,16 +229,16 @@ uint64_t orc_rr_mis(uint32_t n_vars, const uint64_t* offs, const uint32_t* lits,
 }
 
 /* ------------------------------------------------------------------------- */
-/* Serial resample loop (parallel_solve, SATInstance.h:217-320, with T=1) with */
+/* Resample loop (parallel_solve, SATInstance.h:217-320; T=1 or T chunks) with */
 /* Philox resampling.  Statistics semantics (SATInstance.h:25-32, 313-317):    */
 /* n_iterations counts every eval pass including the final zero pass;          */
 /* n_resamples = sum of clause lengths over all MIS clauses; avg_mis_size =    */
 /* floor(sum|M| / n_iterations).                                               */
 /* max_iters (0 = unlimited) caps eval passes; a capped pass does not resample. */
 /* ------------------------------------------------------------------------- */
-int orc_solve(uint32_t n_vars, uint64_t m, const uint64_t* offs, const uint32_t* lits,
-              uint64_t seed, uint64_t max_iters, uint32_t* A, orc_stats* st,
-              orc_iter_cb cb, void* cb_user) {
+static int solve_sets(uint32_t n_vars, uint64_t m, const uint64_t* offs, const uint32_t* lits,
+                      uint64_t seed, uint64_t max_iters, uint32_t T, const uint64_t* chunk_starts,
+                      uint32_t* A, orc_stats* st, orc_iter_cb cb, void* cb_user) {
     uint64_t nw = (m + 63) / 64;
     uint64_t* vmask = (uint64_t*)calloc(nw ? nw : 1, sizeof(uint64_t));
     uint32_t* U = (uint32_t*)malloc(sizeof(uint32_t) * (m ? m : 1));
@@ -254,7 +254,8 @@ int orc_solve(uint32_t n_vars, uint64_t m, const uint64_t* offs, const uint32_t*
         if (nu == 0) { solved = 1; break; }
         if (max_iters && st->n_iterations >= max_iters) break;
         orc_mask_to_list(m, vmask, U);
-        uint64_t nm = orc_lfmis(n_vars, offs, lits, U, nu, M, used);
+        uint64_t nm = T > 1 ? orc_rr_mis(n_vars, offs, lits, U, nu, T, chunk_starts, M, used)
+                            : orc_lfmis(n_vars, offs, lits, U, nu, M, used);
         sum_mis += nm;
         uint64_t dres = 0, iter = st->n_iterations - 1;
         for (uint64_t i = 0; i < nm; ++i) {
@@ -274,6 +275,21 @@ int orc_solve(uint32_t n_vars, uint64_t m, const uint64_t* offs, const uint32_t*
     st->solved = solved;
     free(vmask); free(U); free(M); free(used);
     return solved ? 0 : 1;
+}
+
+int orc_solve(uint32_t n_vars, uint64_t m, const uint64_t* offs, const uint32_t* lits,
+              uint64_t seed, uint64_t max_iters, uint32_t* A, orc_stats* st,
+              orc_iter_cb cb, void* cb_user) {
+    return solve_sets(n_vars, m, offs, lits, seed, max_iters, 1, 0, A, st, cb, cb_user);
+}
+
+/* parallel_solve with T > 1 clause chunks (chunk q = clauses [chunk_starts[q],
+ * chunk_starts[q+1])): the MIS of every iteration is the round-robin greedy of
+ * populate_mis_parallel (orc_rr_mis); everything else as orc_solve. */
+int orc_solve_rr(uint32_t n_vars, uint64_t m, const uint64_t* offs, const uint32_t* lits,
+                 uint64_t seed, uint64_t max_iters, uint32_t T, const uint64_t* chunk_starts,
+                 uint32_t* A, orc_stats* st, orc_iter_cb cb, void* cb_user) {
+    return solve_sets(n_vars, m, offs, lits, seed, max_iters, T, chunk_starts, A, st, cb, cb_user);
 }
 
 /* ------------------------------------------------------------------------- */

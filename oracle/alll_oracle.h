@@ -37,6 +37,9 @@ uint64_t orc_rr_mis(uint32_t n_vars, const uint64_t* offs, const uint32_t* lits,
                     uint8_t* scratch_used);
 int orc_solve(uint32_t n_vars, uint64_t m, const uint64_t* offs, const uint32_t* lits, uint64_t seed,
               uint64_t max_iters, uint32_t* A, orc_stats* st, orc_iter_cb cb, void* cb_user);
+int orc_solve_rr(uint32_t n_vars, uint64_t m, const uint64_t* offs, const uint32_t* lits, uint64_t seed,
+                 uint64_t max_iters, uint32_t T, const uint64_t* chunk_starts, uint32_t* A, orc_stats* st,
+                 orc_iter_cb cb, void* cb_user);
 void orc_stream_order(uint64_t m, uint32_t* order);
 int orc_solve_stream(uint32_t n_vars, uint64_t m, const uint64_t* offs, const uint32_t* lits, uint64_t seed,
                      uint64_t max_iters, uint64_t batch, uint32_t* A, orc_stats* st, orc_iter_cb cb,

@@ -72,6 +72,10 @@ def lib():
                                 ctypes.c_uint64, _u32p, ctypes.POINTER(OrcStats), ITER_CB,
                                 ctypes.c_void_p]
         L.orc_solve.restype = ctypes.c_int
+        L.orc_solve_rr.argtypes = [ctypes.c_uint32, ctypes.c_uint64, _u64p, _u32p, ctypes.c_uint64,
+                                   ctypes.c_uint64, ctypes.c_uint32, _u64p, _u32p, ctypes.POINTER(OrcStats),
+                                   ITER_CB, ctypes.c_void_p]
+        L.orc_solve_rr.restype = ctypes.c_int
         L.orc_stream_order.argtypes = [ctypes.c_uint64, _u32p]
         L.orc_stream_order.restype = None
         L.orc_solve_stream.argtypes = [ctypes.c_uint32, ctypes.c_uint64, _u64p, _u32p, ctypes.c_uint64,
@@ -224,18 +228,20 @@ def chunk_bounds(m, T):
     return s
 
 
-def rr_mis(n_vars, offs, lits, U, T):
+def rr_mis(n_vars, offs, lits, U, T, chunk_starts=None):
     U = np.ascontiguousarray(U, np.uint32)
     M = np.zeros(max(1, U.size), np.uint32)
     used = np.zeros(max(1, n_vars), np.uint8)
-    cs = chunk_bounds(len(offs) - 1, T)
+    cs = chunk_bounds(len(offs) - 1, T) if chunk_starts is None else np.ascontiguousarray(chunk_starts, np.uint64)
     n = lib().orc_rr_mis(n_vars, _p(offs, _u64p), _p(lits, _u32p), _p(U, _u32p), U.size, T,
                          _p(cs, _u64p), _p(M, _u32p), _p(used, _u8p))
     return M[:n].copy()
 
 
-def solve(n_vars, offs, lits, seed, max_iters=0, A0=None, trace=False):
-    """Serial resample loop with Philox.  Returns (stats dict, final A words, per-iter trace)."""
+def solve(n_vars, offs, lits, seed, max_iters=0, A0=None, trace=False, T=1, chunk_starts=None):
+    """Resample loop with Philox.  Returns (stats dict, final A words, per-iter trace).
+    T > 1: the MIS is the round-robin greedy over T clause chunks (orc_rr_mis), chunk
+    boundaries `chunk_starts` (T+1) or by the example/main.cpp rule."""
     m = len(offs) - 1
     A = init_assignment(seed, n_vars) if A0 is None else np.array(A0, np.uint32)
     st = OrcStats()
@@ -247,8 +253,13 @@ def solve(n_vars, offs, lits, seed, max_iters=0, A0=None, trace=False):
                          np.ctypeslib.as_array(Ap, shape=(A.size,)).copy()))
 
     cbf = ITER_CB(cb)
-    lib().orc_solve(n_vars, m, _p(offs, _u64p), _p(lits, _u32p), seed, max_iters, _p(A, _u32p),
-                    ctypes.byref(st), cbf, None)
+    if T > 1:
+        cs = chunk_bounds(m, T) if chunk_starts is None else np.ascontiguousarray(chunk_starts, np.uint64)
+        lib().orc_solve_rr(n_vars, m, _p(offs, _u64p), _p(lits, _u32p), seed, max_iters, T, _p(cs, _u64p),
+                           _p(A, _u32p), ctypes.byref(st), cbf, None)
+    else:
+        lib().orc_solve(n_vars, m, _p(offs, _u64p), _p(lits, _u32p), seed, max_iters, _p(A, _u32p),
+                        ctypes.byref(st), cbf, None)
     stats = {k: int(getattr(st, k)) for k, _ in OrcStats._fields_ if k != "pad"}
     return stats, A, rows
 

@@ -38,7 +38,7 @@ def test_version_and_options(native):
 def test_struct_layout(native):
     # must match include/alll.h on x86-64
     assert ctypes.sizeof(native.Problem) == 32
-    assert ctypes.sizeof(native.Options) == 8 + 8 + 4 * 4 + 128 + 4 + 4 + 8
+    assert ctypes.sizeof(native.Options) == 8 + 8 + 4 * 4 + 128 + 4 + 4 + 8 + 8
     assert ctypes.sizeof(native.Stats) == 5 * 8 + 8 + 8 + 64 * 8
     assert ctypes.sizeof(native.PhaseTimes) == 6 * 8
 

@@ -44,7 +44,7 @@ def test_cli_solves_and_matches_oracle(oracle_mod, native, tmp_path, threads):
     offs, lits = o.generate_ksat(2, n, m, 3)
     path = tmp_path / "inst.cnf"
     path.write_text(o.to_dimacs(n, offs, lits, comments=["cli test"]))
-    st, A, _ = o.solve(n, offs, lits, seed)
+    st, A, _ = o.solve(n, offs, lits, seed, T=threads)  # -p T: round-robin MIS over main.cpp's chunks
     assert st["solved"]
     r = subprocess.run([CLI, "-o", "-p", str(threads), "--seed", str(seed), "--sat", str(path)],
                        capture_output=True, text=True, timeout=300)

@@ -1,0 +1,197 @@
+"""GPU parity of the round-robin MIS (the reference's n_threads = T > 1: populate_mis_parallel
+with T sets, SATInstance.h:414-447, over the chunks of example/main.cpp:149-178 or the
+caller's vector<ClauseArray*>), bit-exact:
+
+  * reference maps on the GPU: for every T > 1 golden trajectory, the device evaluates
+    A_i -> U_i and picks exactly the reference's M_i;
+  * full trajectories with Philox against the oracle's T-chunk loop (orc_solve_rr, whose MIS
+    is pinned by the same fixtures): assignment after every iteration, statistics;
+  * the batch paths of the kernel: few sets (one 64-lane group per set, many levels), more
+    sets than groups (16-lane groups, one level), erasures of empty chunks, clauses too wide
+    for a group's variable buffer, caller-given chunk boundaries;
+  * ALLL_FLAG_LFMIS keeps the one-set MIS for T > 1.
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+RR_FIXTURES = sorted(p for p in glob.glob(os.path.join(GOLDEN, "*_T*.npz")) if not p.endswith("_T1.npz"))
+
+
+@pytest.fixture(scope="module")
+def gpu(native):
+    from alllsatisfiabilitysolver_amd import device_count
+
+    if device_count() == 0:
+        pytest.fail("no GPU visible: the gpu tests must run on an MI355X")
+    return True
+
+
+def mask_to_list(vm, m):
+    bits = np.unpackbits(vm.view(np.uint8), bitorder="little")[:m]
+    return np.nonzero(bits)[0].astype(np.uint32)
+
+
+def test_fixtures_present():
+    assert len(RR_FIXTURES) >= 6
+
+
+@pytest.mark.parametrize("path", RR_FIXTURES, ids=lambda p: os.path.basename(p)[:-4])
+def test_reference_rr_maps_on_gpu(gpu, path):
+    from alllsatisfiabilitysolver_amd import Solver
+
+    f = dict(np.load(path, allow_pickle=False))
+    n, offs, lits, T = int(f["n_vars"]), f["offs"], f["lits"], int(f["T"])
+    m = offs.size - 1
+    with Solver(n, offs, lits, seed=3, n_threads=T) as s:
+        for i in range(f["A"].shape[0]):
+            s.set_assignment_words(f["A"][i])
+            before = s.stats()
+            s.run(1)
+            after = s.stats()
+            U_ref = f["U"][int(f["U_ptr"][i]):int(f["U_ptr"][i + 1])]
+            np.testing.assert_array_equal(mask_to_list(s.violated_mask(), m), U_ref, err_msg=f"U_{i}")
+            if U_ref.size == 0:
+                assert after["solved"] == 1
+                break
+            M_ref = f["M"][int(f["M_ptr"][i]):int(f["M_ptr"][i + 1])]
+            np.testing.assert_array_equal(s.mis(), np.sort(M_ref), err_msg=f"M_{i}")
+            assert after["sum_mis_size"] - before["sum_mis_size"] == M_ref.size
+            if int(f["dres"][i]):
+                assert after["n_resamples"] - before["n_resamples"] == int(f["dres"][i])
+
+
+def _instance(name):
+    from alllsatisfiabilitysolver_amd import generate_ksat
+
+    if name == "ratio4":
+        n, m = 3000, 12000
+        return (n,) + generate_ksat(1, n, m, 3)
+    if name == "ratio2_solves":
+        n, m = 2000, 4000
+        return (n,) + generate_ksat(2, n, m, 3)
+    if name == "k5_multi_tile":
+        n, m = 30000, 60000
+        return (n,) + generate_ksat(1, n, m, 5)
+    if name == "powerlaw":
+        n, m = 5000, 20000
+        return (n,) + generate_ksat(1, n, m, 3, 1)
+    if name == "wide":  # clauses of up to 150 literals: wider than a group's variable buffer
+        rng = np.random.default_rng(11)
+        m, n = 3000, 4000
+        w = rng.integers(1, 8, m)
+        w[rng.choice(m, 40, replace=False)] = rng.integers(40, 150, 40)
+        offs = np.zeros(m + 1, np.uint64)
+        offs[1:] = np.cumsum(w)
+        lits = rng.integers(0, 2 * n, int(offs[-1])).astype(np.uint32)
+        return n, offs, lits
+    if name == "edge":
+        f = dict(np.load(os.path.join(GOLDEN, "edge_T1.npz")))
+        return int(f["n_vars"]), f["offs"], f["lits"]
+    raise KeyError(name)
+
+
+CASES = [("ratio4", 2), ("ratio4", 3), ("ratio4", 8), ("ratio4", 16), ("ratio4", 17), ("ratio4", 64),
+         ("ratio4", 65), ("ratio4", 300), ("ratio2_solves", 4), ("ratio2_solves", 100),
+         ("k5_multi_tile", 7), ("k5_multi_tile", 40), ("powerlaw", 5), ("powerlaw", 33),
+         ("wide", 4), ("wide", 20), ("wide", 90), ("edge", 3), ("edge", 8)]
+
+
+@pytest.mark.parametrize("name,T", CASES, ids=[f"{a}-T{b}" for a, b in CASES])
+def test_rr_trajectory_matches_oracle(gpu, oracle_mod, name, T):
+    from alllsatisfiabilitysolver_amd import Solver
+
+    o = oracle_mod
+    n, offs, lits = _instance(name)
+    seed, K = 4242, 30
+    st_o, A_o, rows = o.solve(n, offs, lits, seed, max_iters=K, trace=True, T=T)
+    with Solver(n, offs, lits, seed=seed, n_threads=T) as s:
+        for it, nu, nm, dres, A_after in rows:
+            before = s.stats()
+            s.run(1)
+            after = s.stats()
+            assert after["n_violated"] == nu, f"iter {it}"
+            assert after["sum_mis_size"] - before["sum_mis_size"] == nm, f"iter {it}"
+            assert after["n_resamples"] - before["n_resamples"] == dres, f"iter {it}"
+            np.testing.assert_array_equal(s.assignment_words(), A_after, err_msg=f"A after iter {it}")
+    with Solver(n, offs, lits, seed=seed, n_threads=T, max_iters=K) as s:
+        st = s.solve()
+        for k in ("n_iterations", "n_resamples", "avg_mis_size", "sum_mis_size", "solved"):
+            assert st[k] == st_o[k], k
+        np.testing.assert_array_equal(s.assignment_words(), A_o)
+
+
+def test_rr_caller_chunks(gpu, oracle_mod):
+    """Chunk boundaries from the caller (the sizes of its vector<ClauseArray*>), including
+    empty chunks at the front, middle and end."""
+    from alllsatisfiabilitysolver_amd import Solver
+
+    o = oracle_mod
+    n, offs, lits = _instance("ratio4")
+    m = offs.size - 1
+    starts = np.array([0, 0, 100, 100, 5000, 5001, 11999, m, m], np.uint64)
+    T = starts.size - 1
+    st_o, A_o, _ = o.solve(n, offs, lits, 8, max_iters=20, T=T, chunk_starts=starts)
+    with Solver(n, offs, lits, seed=8, n_threads=T, max_iters=20, set_starts=starts) as s:
+        st = s.solve()
+        for k in ("n_iterations", "n_resamples", "avg_mis_size"):
+            assert st[k] == st_o[k], k
+        np.testing.assert_array_equal(s.assignment_words(), A_o)
+
+
+def test_rr_converges_and_verifies(gpu, oracle_mod):
+    from alllsatisfiabilitysolver_amd import Solver, generate_ksat
+
+    n, m, T = 25000, 50000, 12
+    offs, lits = generate_ksat(2, n, m, 3)
+    st_o, A_o, _ = oracle_mod.solve(n, offs, lits, 99, T=T)
+    assert st_o["solved"] == 1
+    with Solver(n, offs, lits, seed=99, n_threads=T) as s:
+        st = s.solve()
+        assert st["solved"] == 1
+        for k in ("n_iterations", "n_resamples", "avg_mis_size"):
+            assert st[k] == st_o[k]
+        np.testing.assert_array_equal(s.assignment_words(), A_o)
+        ok, nv = s.verify()
+        assert ok and nv == 0
+
+
+def test_rr_flag_lfmis_and_limits(gpu, oracle_mod, native):
+    from alllsatisfiabilitysolver_amd import Solver, AlllError
+
+    n, offs, lits = _instance("ratio4")
+    st_o, A_o, _ = oracle_mod.solve(n, offs, lits, 5, max_iters=10)
+    with Solver(n, offs, lits, seed=5, n_threads=8, max_iters=10, flags=native.FLAG_LFMIS) as s:
+        s.solve()
+        np.testing.assert_array_equal(s.assignment_words(), A_o)
+    with pytest.raises(AlllError) as ei:
+        Solver(n, offs, lits, n_threads=5000)
+    assert ei.value.code == native.ALLL_ERR_UNSUPPORTED
+    with pytest.raises(AlllError) as ei:
+        Solver(n, offs, lits, n_threads=2, set_starts=np.array([0, 5, 7], np.uint64))
+    assert ei.value.code == native.ALLL_ERR_INVALID_ARG
+
+
+def test_rr_python_satinstance(gpu, oracle_mod):
+    """SATInstance(var_arr, n_threads).solve(chunks) runs the round robin over the chunks."""
+    from alllsatisfiabilitysolver_amd import Clause, SATInstance, VariablesArray
+
+    o = oracle_mod
+    n, offs, lits = _instance("ratio2_solves")
+    m = offs.size - 1
+    T = 3
+    starts = o.chunk_bounds(m, T)
+    chunks = [[Clause([int(x) for x in lits[offs[c]:offs[c + 1]]]) for c in range(int(starts[q]), int(starts[q + 1]))]
+              for q in range(T)]
+    va = VariablesArray(n)
+    inst = SATInstance(va, T, seed=21)
+    stats = inst.solve(chunks)
+    st_o, A_o, _ = o.solve(n, offs, lits, 21, T=T)
+    assert stats.n_iterations == st_o["n_iterations"] and stats.n_resamples == st_o["n_resamples"]
+    assert inst.verify_validity(chunks)

@@ -103,6 +103,30 @@ def test_oracle_solve_semantics(oracle_mod):
     assert st["avg_mis_size"] == sum(r[2] for r in rows) // st["n_iterations"]
 
 
+@pytest.mark.parametrize("T", [2, 5, 70])
+def test_oracle_solve_rr_replays(oracle_mod, T):
+    """T-chunk loop (orc_solve_rr): every iteration is eval -> round-robin MIS (orc_rr_mis,
+    pinned above by the reference's T>1 fixtures) -> Philox resample of the MIS variables."""
+    o = oracle_mod
+    n = 400
+    offs, lits = o.generate_ksat(4, n, 1600, 3)
+    st, A_end, rows = o.solve(n, offs, lits, seed=9, max_iters=25, trace=True, T=T)
+    A = o.init_assignment(9, n)
+    for it, nu, nm, dres, A_after in rows:
+        cnt, vm = o.eval_mask(offs, lits, A)
+        assert cnt == nu
+        M = o.rr_mis(n, offs, lits, o.mask_to_list(offs.size - 1, vm), T)
+        assert M.size == nm
+        assert dres == int(np.sum(offs[M.astype(np.int64) + 1] - offs[M.astype(np.int64)]))
+        o.resample_words(A, 9, it - 1, o.clause_vars(offs, lits, M))
+        np.testing.assert_array_equal(A, A_after, err_msg=f"iter {it}")
+    np.testing.assert_array_equal(A, A_end)
+    # T = 1 chunking and an explicit single chunk give the LFMIS loop
+    st1, A1, _ = o.solve(n, offs, lits, seed=9, max_iters=25)
+    stc, Ac, _ = o.solve(n, offs, lits, seed=9, max_iters=25, T=1, chunk_starts=[0, offs.size - 1])
+    np.testing.assert_array_equal(A1, Ac)
+
+
 def test_oracle_max_iters(oracle_mod):
     o = oracle_mod
     offs, lits = o.generate_ksat(1, 200, 800, 3)

@@ -38,7 +38,7 @@ constexpr uint32_t RUN_TILES_MAX = 16;        // entry index within a run < 16 *
 constexpr int BKT_THREADS = 512;
 constexpr unsigned long long PAIR_LOSE = 1ull << 31;
 // Round-robin MIS of T > 1 clause chunks (the reference's n_threads > 1): at most RR_TMAX sets.
-constexpr uint32_t RR_TMAX = 4096;
+constexpr uint32_t RR_TMAX = 2048;
 // In-loop kernel timing (ALLL_FLAG_KERNEL_TIMING): per iteration i, slot i % TIME_SLOTS holds
 // device wall-clock stamps (s_memrealtime) {eval start (min over workgroups), eval end (max),
 // reduce start, LFMIS tail end}.
@@ -113,9 +113,10 @@ struct LoopBuffers {
     uint64_t stream_batch;      // 0: clause-order LFMIS
     uint64_t stream_pinv;       // inverse of P mod m (P = 9223372036854775783, ClauseGenerator.h:110)
     // round-robin MIS (T = rr_T > 1 clause chunks, SATInstance.h:414-447; CSR layout)
-    uint32_t* rr_u;             // violated clause ids in clause order (m slots)
+    uint32_t* rr_u;             // violated clauses in clause order: m scan entries of 12 words
     const uint32_t* rr_sets;    // rr_T + 1 chunk starts (clause ids)
     uint32_t rr_T;
+    uint32_t rr_k;              // common clause width (<= 8), 0 = ragged
     uint32_t n_vars;
     uint32_t n_words;
     uint32_t n_tiles;       // tiles covering [0, m)

@@ -1344,39 +1344,213 @@ __global__ void k_apply_delta(LoopBuffers b) {
 //
 // One 1024-thread workgroup runs the turns in speculative batches.  B = min(|sets|, groups)
 // consecutive sets get a lane group each; when every live set has a group, each group also
-// runs D levels (its set's next D turns).  A group scans its list, GS clauses per step, and
+// runs D levels (its set's next D turns).  Turn l*B + g belongs to group g, level l.  A group
+// scans its list GS clauses per step (the loads of ST steps in flight together) and
 // picks its next fronts greedily, assuming that only its own picks and the covered variables
-// matter.  Turn l*B + g belongs to group g, level l.  The batch is exact up to the first turn
-// whose pick shares a variable with a pick of an earlier turn of the batch (an LDS hash keeps
-// the earliest turn per variable) and up to the first turn a group could not decide; those
-// turns are committed (cover + MIS), and the first undecided turn of an exhausted set is its
+// matter: a step whose live candidates share no variable (an LDS hash per step tells) is
+// taken whole, otherwise lane by lane.  Every pick enters the batch hash (variable -> earliest
+// turn, groups).  The batch is exact up to the first turn whose pick shares a variable with
+// a pick of an earlier turn, and up to the first turn a group could not decide; those turns
+// are committed (cover + MIS), and the first undecided turn of an exhausted set is its
 // erasure.  Skipped clauses before a group's first uncommitted pick are erased for certain
 // (covered by committed picks), so no scan is repeated.
 constexpr int RR_THREADS = 1024;
-constexpr uint32_t RR_HASH = 4096;      // LDS hash slots (variable -> earliest turn)
-constexpr uint32_t RR_VCAP = 2048;      // variables of the picks of one batch
-constexpr uint32_t RR_CMAX = 1024;      // picks of one batch
-constexpr uint32_t RR_DMAX = 32;        // levels per group
-constexpr uint32_t RR_KR = 8;           // clause variables kept in registers while scanning
-constexpr uint32_t RR_SCAN_STEPS = 4;   // scan steps per group per batch
+constexpr uint32_t RR_HBITS = 11;
+constexpr uint32_t RR_HASH = 1u << RR_HBITS;  // batch hash slots (variable -> earliest turn, groups)
+constexpr uint32_t RR_VCAP = RR_HASH / 2;     // variables of the picks of one batch
+constexpr uint32_t RR_CMAX = 2048;            // picks of one batch
+constexpr uint32_t RR_SHASH = 8192;           // step hash slots {variable:32 | lane:32}, split between groups
+constexpr uint32_t RR_KE = 8;                 // variables stored in a scan entry (k_rr_entries)
+constexpr uint32_t RR_ROUNDS = 2;             // rounds of ST scan steps (loads issued together) per group per batch
+constexpr uint32_t RR_EMPTY = 0xFFFFFFFFu;
+constexpr unsigned long long RR_EMPTY64 = ~0ull;
 
 struct RRLds {
     uint32_t hkey[RR_HASH];
     uint32_t hmin[RR_HASH];
-    uint32_t var[RR_VCAP];     // group g: [g*vpg, g*vpg + nvar[g])
-    uint32_t vtau[RR_VCAP];    // turn of the pick the variable belongs to
+    unsigned long long hgrp[RR_HASH];
+    unsigned long long skey[RR_SHASH];
     uint32_t cc[RR_CMAX];      // group g: [g*cpg, g*cpg + ncand[g]) picked clause ids
     uint32_t cpos[RR_CMAX];    // their positions in U
-    uint32_t cw[RR_CMAX];      // their widths
     uint32_t ptr[RR_TMAX];     // per set: position in U of the first clause not known erased
     uint32_t end[RR_TMAX];     // per set: end of its clauses in U
     uint16_t live[RR_TMAX];    // live sets in the reference's vector order
-    uint32_t ncand[64], nvar[64], scan_end[64], exh[64];
+    uint32_t ncand[64], scan_end[64], exh[64];
     uint32_t n_live, t, trunc, tm, wide;
+    uint32_t n_steps, n_rounds;  // diagnostics (ALLL_DEBUG_PHASES)
 };
 
-__device__ __forceinline__ uint32_t rr_hash(uint32_t v) { return (v * 0x9E3779B1u) >> (32 - 12); }
+__device__ __forceinline__ uint32_t rr_hash(uint32_t v, uint32_t bits) { return (v * 0x9E3779B1u) >> (32 - bits); }
 
+// batch hash: v picked at turn tau by group g
+__device__ __forceinline__ void rr_insert(RRLds& L, uint32_t v, uint32_t tau, uint32_t g) {
+    uint32_t h = rr_hash(v, RR_HBITS);
+    while (true) {
+        const uint32_t k = atomicCAS(&L.hkey[h], RR_EMPTY, v);
+        if (k == RR_EMPTY || k == v) {
+            atomicMin(&L.hmin[h], tau);
+            atomicOr(&L.hgrp[h], 1ull << g);
+            return;
+        }
+        h = (h + 1) & (RR_HASH - 1);
+    }
+}
+
+// did group g pick a clause with variable v in this batch?  (The group's own inserts precede
+// this lookup in its wave's LDS order; slots never empty within a batch.)
+__device__ __forceinline__ bool rr_own(const RRLds& L, uint32_t v, uint32_t g) {
+    uint32_t h = rr_hash(v, RR_HBITS);
+    while (true) {
+        const uint32_t k = L.hkey[h];
+        if (k == v) return (L.hgrp[h] >> g) & 1ull;
+        if (k == RR_EMPTY) return false;
+        h = (h + 1) & (RR_HASH - 1);
+    }
+}
+
+// does group g own any of the variables rv[0..n) (n <= KR) in the batch hash?  The probes
+// of the variables run interleaved so that their LDS latencies overlap.
+template <uint32_t KR>
+__device__ __forceinline__ bool rr_own_any(const RRLds& L, const uint32_t (&rv)[KR], uint32_t n, uint32_t g) {
+    uint32_t h[KR];
+    uint32_t act = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < KR; ++j) {
+        h[j] = rr_hash(rv[j], RR_HBITS);
+        if (j < n) act |= 1u << j;
+    }
+    bool own = false;
+    while (act && !own) {
+#pragma unroll
+        for (uint32_t j = 0; j < KR; ++j) {
+            if (!((act >> j) & 1u)) continue;
+            const uint32_t k = L.hkey[h[j]];
+            if (k == rv[j]) {
+                own |= (L.hgrp[h[j]] >> g) & 1ull;
+                act &= ~(1u << j);
+            } else if (k == RR_EMPTY) {
+                act &= ~(1u << j);
+            } else {
+                h[j] = (h[j] + 1) & (RR_HASH - 1);
+            }
+        }
+    }
+    return own;
+}
+
+// step hash of a group (2^sbits slots): lowest lane holding variable v; returns whether v was
+// already present (another lane of the step holds it)
+__device__ __forceinline__ bool rr_step_insert(unsigned long long* sk, uint32_t sbits, uint32_t v, uint32_t gl) {
+    const unsigned long long me = ((unsigned long long)v << 32) | gl;
+    uint32_t h = rr_hash(v, sbits);
+    while (true) {
+        unsigned long long cur = sk[h];
+        if (cur == RR_EMPTY64) {
+            cur = atomicCAS(&sk[h], RR_EMPTY64, me);
+            if (cur == RR_EMPTY64) return false;
+        }
+        if ((uint32_t)(cur >> 32) == v) { atomicMin(&sk[h], me); return true; }
+        h = (h + 1) & ((1u << sbits) - 1);
+    }
+}
+
+// lanes holding rv[0..n) in the step hash (RR_EMPTY if absent), probes interleaved
+template <uint32_t KR>
+__device__ __forceinline__ void rr_step_lanes(const unsigned long long* sk, uint32_t sbits,
+                                              const uint32_t (&rv)[KR], uint32_t n, uint32_t (&ml)[KR]) {
+    uint32_t h[KR];
+    uint32_t act = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < KR; ++j) {
+        h[j] = rr_hash(rv[j], sbits);
+        ml[j] = RR_EMPTY;
+        if (j < n) act |= 1u << j;
+    }
+    while (act) {
+#pragma unroll
+        for (uint32_t j = 0; j < KR; ++j) {
+            if (!((act >> j) & 1u)) continue;
+            const unsigned long long cur = sk[h[j]];
+            if (cur == RR_EMPTY64) {
+                act &= ~(1u << j);
+            } else if ((uint32_t)(cur >> 32) == rv[j]) {
+                ml[j] = (uint32_t)cur;
+                act &= ~(1u << j);
+            } else {
+                h[j] = (h[j] + 1) & ((1u << sbits) - 1);
+            }
+        }
+    }
+}
+
+// lane holding v in the step hash, or RR_EMPTY
+__device__ __forceinline__ uint32_t rr_step_lane(const unsigned long long* sk, uint32_t sbits, uint32_t v) {
+    uint32_t h = rr_hash(v, sbits);
+    while (true) {
+        const unsigned long long cur = sk[h];
+        if (cur == RR_EMPTY64) return RR_EMPTY;
+        if ((uint32_t)(cur >> 32) == v) return (uint32_t)cur;
+        h = (h + 1) & ((1u << sbits) - 1);
+    }
+}
+
+// Violated clauses of the iteration in clause order as scan entries {id, literal start, width,
+// variables 0..7} (one 256-thread workgroup per tile; tile offsets from the evaluation's
+// per-tile counts), so that a scan round of k_rr_mis is two dependent loads (entry, cover).
+struct RREnt {
+    uint4 a;      // {clause id, literal start, width, 0}
+    uint4 v0, v1; // variables 0..7 (RR_EMPTY past the width)
+};
+
+__global__ __launch_bounds__(256) void k_rr_entries(ClauseView cv, LoopBuffers b) {
+    if (!b.state->active) return;
+    const uint32_t tile = blockIdx.x, tid = threadIdx.x;
+    __shared__ uint32_t s_part[4], s_wpre[TILE_WORDS + 1];
+    __shared__ uint32_t s_ids[TILE];
+    uint32_t acc = 0;
+    for (uint32_t t = tid; t < tile; t += 256) acc += b.tile_cnt[t];
+    for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
+    if ((tid & 63) == 0) s_part[tid >> 6] = acc;
+    uint64_t x = 0;
+    uint32_t cnt = 0, excl = 0;
+    if (tid < TILE_WORDS) {
+        const uint64_t c0 = (uint64_t)tile * TILE + 64u * tid;
+        x = c0 < cv.m ? b.vmask[(uint64_t)tile * TILE_WORDS + tid] : 0ull;
+        if (c0 < cv.m && cv.m - c0 < 64) x &= (1ull << (cv.m - c0)) - 1ull;
+        cnt = (uint32_t)__popcll(x);
+        uint32_t incl = cnt;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o, 64);
+            if ((int)tid >= o) incl += y;
+        }
+        excl = incl - cnt;
+        if (tid == TILE_WORDS - 1) s_wpre[TILE_WORDS] = incl;
+    }
+    if (tid < TILE_WORDS) {
+        uint32_t o = excl;
+        while (x) {
+            s_ids[o++] = tile * TILE + 64u * tid + (uint32_t)__builtin_ctzll(x);
+            x &= x - 1;
+        }
+    }
+    __syncthreads();
+    const uint32_t base = s_part[0] + s_part[1] + s_part[2] + s_part[3];
+    const uint32_t n = s_wpre[TILE_WORDS];
+    RREnt* out = reinterpret_cast<RREnt*>(b.rr_u) + base;
+    for (uint32_t i = tid; i < n; i += 256) {
+        const uint32_t c = s_ids[i], lb = cv.offs[c], w = cv.offs[c + 1] - lb;
+        uint32_t v[8];
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j) v[j] = j < w ? lit_var(cv.lits[lb + j]) : RR_EMPTY;
+        RREnt e;
+        e.a = make_uint4(c, lb, w, 0u);
+        e.v0 = make_uint4(v[0], v[1], v[2], v[3]);
+        e.v1 = make_uint4(v[4], v[5], v[6], v[7]);
+        out[i] = e;
+    }
+}
+
+template <uint32_t KR, uint32_t ST>
 __global__ __launch_bounds__(RR_THREADS) void k_rr_mis(ClauseView cv, LoopBuffers b) {
     DevState* st = b.state;
     if (!st->active) return;
@@ -1387,43 +1561,11 @@ __global__ __launch_bounds__(RR_THREADS) void k_rr_mis(ClauseView cv, LoopBuffer
     const uint32_t lane = tid & 63;
     const uint32_t T = b.rr_T;
     const uint64_t m = cv.m;
-    uint32_t* U = b.rr_u;
+    const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
+    const bool prof = b.kdbg != nullptr;  // diagnostics: phase times of thread 0
+    unsigned long long tp0 = prof ? wall_now() : 0, tacc[4] = {0, 0, 0, 0};
 
-    // ---- U: violated clause ids in clause order (the bitmask is in clause order: CSR layout)
-    __shared__ uint32_t s_wsum[RR_THREADS / 64];
-    __shared__ uint32_t s_base;
-    if (tid == 0) s_base = 0;
-    __syncthreads();
-    const uint64_t nw = (m + 63) / 64;
-    for (uint64_t w0 = 0; w0 < nw; w0 += RR_THREADS) {
-        const uint64_t w = w0 + tid;
-        uint64_t x = w < nw ? b.vmask[w] : 0ull;
-        if (w == nw - 1 && (m & 63)) x &= (1ull << (m & 63)) - 1ull;
-        const uint32_t cnt = (uint32_t)__popcll(x);
-        uint32_t incl = cnt;
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(incl, o, 64);
-            if ((int)lane >= o) incl += y;
-        }
-        if (lane == 63) s_wsum[tid >> 6] = incl;
-        __syncthreads();
-        uint32_t wave_off = 0, total = 0;
-        for (uint32_t q = 0; q < RR_THREADS / 64; ++q) {
-            const uint32_t v = s_wsum[q];
-            if (q < (tid >> 6)) wave_off += v;
-            total += v;
-        }
-        uint32_t o = s_base + wave_off + incl - cnt;
-        while (x) {
-            U[o++] = (uint32_t)(w * 64 + (uint32_t)__builtin_ctzll(x));
-            x &= x - 1;
-        }
-        __threadfence();
-        __syncthreads();
-        if (tid == 0) s_base += total;
-        __syncthreads();
-    }
-    const uint32_t nu = s_base;
+    const uint32_t nu = (uint32_t)st->u_total;  // entries written by k_rr_entries
     // ---- sets: [lower_bound(start q), lower_bound(start q+1)) of U
     for (uint32_t q = tid; q < T; q += RR_THREADS) {
         uint32_t bnd[2];
@@ -1432,7 +1574,7 @@ __global__ __launch_bounds__(RR_THREADS) void k_rr_mis(ClauseView cv, LoopBuffer
             uint32_t lo = 0, hi = nu;
             while (lo < hi) {
                 const uint32_t mid = (lo + hi) >> 1;
-                if (U[mid] < key) lo = mid + 1; else hi = mid;
+                if (U[mid].a.x < key) lo = mid + 1; else hi = mid;
             }
             bnd[e] = lo;
         }
@@ -1440,11 +1582,12 @@ __global__ __launch_bounds__(RR_THREADS) void k_rr_mis(ClauseView cv, LoopBuffer
         L.end[q] = bnd[1];
         L.live[q] = (uint16_t)q;
     }
-    if (tid == 0) { L.n_live = T; L.t = 0; L.tm = 0; L.wide = 0; }
-    __threadfence();
+    if (tid == 0) { L.n_live = T; L.t = 0; L.tm = 0; L.wide = 0; L.n_steps = 0; L.n_rounds = 0; }
+    for (uint32_t i = tid; i < RR_HASH; i += RR_THREADS) { L.hkey[i] = RR_EMPTY; L.hmin[i] = RR_EMPTY; L.hgrp[i] = 0; }
     __syncthreads();
 
     uint32_t batches = 0;
+    if (prof) { const unsigned long long t1 = wall_now(); tacc[0] += t1 - tp0; tp0 = t1; }
     while (true) {
         const uint32_t n_live = L.n_live;
         if (n_live == 0) break;
@@ -1456,164 +1599,233 @@ __global__ __launch_bounds__(RR_THREADS) void k_rr_mis(ClauseView cv, LoopBuffer
         const uint32_t GS = n_live <= RR_THREADS / 64 ? 64u : 16u;  // lanes per group
         const uint32_t NG = RR_THREADS / GS;
         const uint32_t B = n_live < NG ? n_live : NG;
-        const uint32_t vpg = RR_VCAP / NG, cpg = RR_CMAX / NG;
-        const uint32_t D = (B == n_live) ? (cpg < RR_DMAX ? cpg : RR_DMAX) : 1u;
+        const uint32_t vpg = RR_VCAP / B, cpg = RR_CMAX / B;
+        const uint32_t D = (B == n_live) ? cpg : 1u;
         const uint32_t t0 = L.t;
         // ---- scan: group g decides the next D turns of set live[(t + 1 + g) % n_live]
         {
             const uint32_t g = tid / GS, gl = tid % GS;
             const uint32_t gshift = lane & ~(GS - 1);
             const uint64_t gmask = GS == 64 ? ~0ull : ((1ull << GS) - 1ull);
+            const uint64_t below = (1ull << gl) - 1ull;
+            const uint32_t sbits = GS == 64 ? 9u : 7u;  // RR_SHASH / NG slots per group
+            const uint32_t shs = 1u << sbits, wcap = shs / 2;
+            unsigned long long* sk = L.skey + g * shs;
             if (g < B) {
                 const uint32_t s = L.live[(t0 + 1 + g) % n_live];
                 uint32_t pos = L.ptr[s];
                 const uint32_t end = L.end[s];
-                uint32_t nc = 0, nv = 0, scan_end = pos, exhausted = 0;
-                const uint32_t vb = g * vpg, cb = g * cpg;
-                for (uint32_t step = 0;; ++step) {
-                    if (pos >= end) { exhausted = 1; scan_end = end; break; }
-                    if (step == RR_SCAN_STEPS) { scan_end = pos; break; }
-                    const uint32_t i = pos + gl;
-                    const bool valid = i < end;
-                    uint32_t c = 0, lb = 0, w = 0;
-                    if (valid) {
-                        c = U[i];
-                        lb = cv.offs[c];
-                        w = cv.offs[c + 1] - lb;
-                    }
-                    uint32_t rv[RR_KR];
-                    bool alive = valid;
+                uint32_t nc = 0, nv = 0, scan_end = pos, exhausted = 0, n_steps = 0, n_rounds = 0;
+                const uint32_t cb = g * cpg;
+                bool stop = false;
+                for (uint32_t round = 0; round < RR_ROUNDS && !stop; ++round) {
+                    // loads of ST steps: clause, width, variables, covered test
+                    uint32_t c[ST], lb[ST], w[ST], rv[ST][KR];
+                    bool alive[ST];
 #pragma unroll
-                    for (uint32_t j = 0; j < RR_KR; ++j) {
-                        rv[j] = 0xFFFFFFFFu;
-                        if (j < w) {
-                            rv[j] = lit_var(cv.lits[lb + j]);
-                            alive &= __hip_atomic_load(&b.cover[rv[j]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != stamp;
-                        }
-                    }
-                    for (uint32_t j = RR_KR; j < w; ++j)
-                        alive &= __hip_atomic_load(&b.cover[lit_var(cv.lits[lb + j])], __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT) != stamp;
-                    // variables of this group's earlier picks in the batch
-                    if (alive) {
-                        for (uint32_t q = 0; q < nv && alive; ++q) {
-                            const uint32_t ov = L.var[vb + q];
+                    for (uint32_t u = 0; u < ST; ++u) {
+                        const uint32_t i = pos + u * GS + gl;
+                        alive[u] = i < end;
+                        RREnt e;
+                        if (alive[u]) e = U[i];
+                        else { e.a = make_uint4(0u, 0u, 0u, 0u); e.v0 = e.v1 = make_uint4(RR_EMPTY, RR_EMPTY, RR_EMPTY, RR_EMPTY); }
+                        c[u] = e.a.x; lb[u] = e.a.y; w[u] = e.a.z;
+                        const uint32_t ev[8] = {e.v0.x, e.v0.y, e.v0.z, e.v0.w, e.v1.x, e.v1.y, e.v1.z, e.v1.w};
 #pragma unroll
-                            for (uint32_t j = 0; j < RR_KR; ++j) alive &= rv[j] != ov;
-                            for (uint32_t j = RR_KR; j < w; ++j) alive &= lit_var(cv.lits[lb + j]) != ov;
-                        }
+                        for (uint32_t j = 0; j < KR; ++j) rv[u][j] = ev[j];
                     }
-                    uint64_t gm = (__ballot(alive) >> gshift) & gmask;
-                    bool stop = false;
-                    while (gm) {
-                        const uint32_t i0 = (uint32_t)__builtin_ctzll(gm);
-                        const uint32_t src = gshift + i0;
-                        const uint32_t w0 = __shfl(w, (int)src, 64);
-                        if (nc == D) { stop = true; scan_end = pos + i0; break; }
-                        if (nv + w0 > vpg) {
+#pragma unroll
+                    for (uint32_t u = 0; u < ST; ++u) {
+#pragma unroll
+                        for (uint32_t j = 0; j < KR; ++j)
+                            if (j < w[u])
+                                alive[u] &= __hip_atomic_load(&b.cover[rv[u][j]], __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_AGENT) != stamp;
+                        for (uint32_t j = KR; j < w[u]; ++j)
+                            alive[u] &= __hip_atomic_load(&b.cover[lit_var(cv.lits[lb[u] + j])], __ATOMIC_RELAXED,
+                                                          __HIP_MEMORY_SCOPE_AGENT) != stamp;
+                    }
+#pragma unroll
+                    for (uint32_t u = 0; u < ST; ++u) {
+                        if (stop) break;
+                        const uint32_t pu = pos + u * GS;
+                        if (pu >= end) { exhausted = 1; scan_end = end; stop = true; break; }
+                        const uint32_t i = pu + gl;
+                        bool al = alive[u];
+                        auto var_of = [&](uint32_t j) -> uint32_t {
+                            return j < KR ? rv[u][j] : lit_var(cv.lits[lb[u] + j]);
+                        };
+                        // erased by an earlier pick of this group in the batch
+                        if (al && nc) {
+                            al = !rr_own_any(L, rv[u], w[u] < KR ? w[u] : KR, g);
+                            for (uint32_t j = KR; al && j < w[u]; ++j)
+                                if (rr_own(L, var_of(j), g)) al = false;
+                        }
+                        uint64_t und = (__ballot(al) >> gshift) & gmask;
+                        if (!und) continue;
+                        ++n_steps;
+                        // greedy (lane order) subset S of the live candidates, by rounds: a lane that
+                        // holds the lowest undecided lane index on every variable is in S, the lanes
+                        // sharing a variable with it are out
+                        uint64_t S = 0;
+                        while (und) {
+                            ++n_rounds;
+                            const bool me = (und >> gl) & 1ull;
+                            uint32_t wsum = me ? w[u] : 0u;
+                            if (b.rr_k) {
+                                wsum = me ? b.rr_k * ((uint32_t)__popcll(und & below) + 1u) : 0u;
+                            } else {
+                                for (uint32_t o = 1; o < GS; o <<= 1) {
+                                    const uint32_t y = __shfl_up(wsum, o, GS);
+                                    if (gl >= o) wsum += y;
+                                }
+                            }
+                            const bool inwin = me && wsum <= wcap;  // lanes whose variables fit the step hash
+                            const uint32_t first = (uint32_t)__builtin_ctzll(und);
+                            bool win = false, dead = false;
+                            const bool wide_first = !((__ballot(inwin) >> gshift >> first) & 1ull);
+                            if (wide_first) {
+                                // the first undecided lane alone is too wide: it is in S; the others
+                                // compare their variables with its variables in memory
+                                win = gl == first;
+                                const uint32_t lb0 = __shfl(lb[u], (int)(gshift + first), 64);
+                                const uint32_t w0 = __shfl(w[u], (int)(gshift + first), 64);
+                                for (uint32_t j0 = 0; j0 < w0; ++j0) {
+                                    const uint32_t v0 = lit_var(cv.lits[lb0 + j0]);
+                                    if (me && !win && !dead)
+                                        for (uint32_t j = 0; j < w[u]; ++j) dead |= var_of(j) == v0;
+                                }
+                            }
+                            uint64_t W;
+                            if (wide_first) {
+                                W = (__ballot(win) >> gshift) & gmask;
+                            } else {
+                                for (uint32_t q = gl; q < shs; q += GS) sk[q] = RR_EMPTY64;
+                                __builtin_amdgcn_wave_barrier();
+                                bool dup = false;
+                                if (inwin)
+                                    for (uint32_t j = 0; j < w[u]; ++j) dup |= rr_step_insert(sk, sbits, var_of(j), gl);
+                                __builtin_amdgcn_wave_barrier();
+                                const uint64_t wm = (__ballot(inwin) >> gshift) & gmask;
+                                if (!((__ballot(dup) >> gshift) & gmask) && wm == und) {
+                                    // no variable shared inside the step: every candidate is in S
+                                    win = me;
+                                    W = und;
+                                } else {
+                                    uint32_t ml[KR];
+                                    rr_step_lanes(sk, sbits, rv[u], me ? (w[u] < KR ? w[u] : KR) : 0u, ml);
+                                    win = inwin;
+#pragma unroll
+                                    for (uint32_t j = 0; j < KR; ++j) win &= j >= w[u] || ml[j] == gl;
+                                    for (uint32_t j = KR; win && j < w[u]; ++j) win = rr_step_lane(sk, sbits, var_of(j)) == gl;
+                                    W = (__ballot(win) >> gshift) & gmask;
+                                    if (me && !win) {
+#pragma unroll
+                                        for (uint32_t j = 0; j < KR; ++j)
+                                            dead |= j < w[u] && ml[j] != RR_EMPTY && ((W >> ml[j]) & 1ull);
+                                        for (uint32_t j = KR; !dead && j < w[u]; ++j) {
+                                            const uint32_t q = rr_step_lane(sk, sbits, var_of(j));
+                                            dead = q != RR_EMPTY && ((W >> q) & 1ull);
+                                        }
+                                    }
+                                }
+                            }
+                            const uint64_t Dm = (__ballot(dead) >> gshift) & gmask;
+                            S |= W;
+                            und &= ~(W | Dm);
+                        }
+                        // S in lane order, up to the level and variable capacities
+                        const bool inS = (S >> gl) & 1ull;
+                        const uint32_t rank = (uint32_t)__popcll(S & below);
+                        uint32_t wincl = inS ? w[u] : 0u;
+                        if (b.rr_k) {
+                            wincl = inS ? b.rr_k * (rank + 1u) : 0u;
+                        } else {
+                            for (uint32_t o = 1; o < GS; o <<= 1) {
+                                const uint32_t y = __shfl_up(wincl, o, GS);
+                                if (gl >= o) wincl += y;
+                            }
+                        }
+                        const bool picked = inS && nc + rank < D && nv + wincl <= vpg;
+                        const uint64_t pm = (__ballot(picked) >> gshift) & gmask;
+                        if (picked) {
+                            const uint32_t idx = nc + rank, tau = idx * B + g;
+                            L.cc[cb + idx] = c[u];
+                            L.cpos[cb + idx] = i;
+                            for (uint32_t j = 0; j < w[u]; ++j) rr_insert(L, var_of(j), tau, g);
+                        }
+                        const uint32_t np = (uint32_t)__popcll(pm);
+                        if (np) {
+                            const uint32_t lastp = 63u - (uint32_t)__builtin_clzll(pm);
+                            nv += __shfl(wincl, (int)(gshift + lastp), 64);
+                        }
+                        nc += np;
+                        const uint64_t rest = S & ~pm;
+                        if (rest) {
+                            const uint32_t i0 = (uint32_t)__builtin_ctzll(rest);
                             stop = true;
-                            scan_end = pos + i0;
-                            if (nc == 0 && g == 0) {
-                                // turn 0 is always exact: a pick too wide to record is
-                                // committed alone (its variables are covered from memory)
+                            scan_end = pu + i0;
+                            if (np == 0 && nc == 0 && g == 0) {
+                                // turn 0 is always exact: a pick too wide to record is committed
+                                // alone (its variables are covered from memory)
                                 if (gl == i0) {
-                                    L.cc[cb] = c;
+                                    L.cc[cb] = c[u];
                                     L.cpos[cb] = i;
-                                    L.cw[cb] = w;
                                     L.wide = 1;
                                 }
                                 nc = 1;
-                                scan_end = pos + i0 + 1;
+                                scan_end = pu + i0 + 1;
                             }
-                            break;
-                        }
-                        const uint32_t lb0 = __shfl(lb, (int)src, 64);
-                        const uint32_t tau = nc * B + g;
-                        if (gl == i0) {
-                            L.cc[cb + nc] = c;
-                            L.cpos[cb + nc] = i;
-                            L.cw[cb + nc] = w;
-                        }
-                        // the pick's variables: record them, and drop later lanes sharing one
-#pragma unroll
-                        for (uint32_t j0 = 0; j0 < RR_KR; ++j0) {
-                            if (j0 < w0) {
-                                const uint32_t v0 = __shfl(rv[j0], (int)src, 64);
-                                if (gl == i0) { L.var[vb + nv + j0] = v0; L.vtau[vb + nv + j0] = tau; }
-                                if (gl > i0 && alive) {
-#pragma unroll
-                                    for (uint32_t j = 0; j < RR_KR; ++j) alive &= rv[j] != v0;
-                                    for (uint32_t j = RR_KR; j < w; ++j) alive &= lit_var(cv.lits[lb + j]) != v0;
-                                }
-                            }
-                        }
-                        for (uint32_t j0 = RR_KR; j0 < w0; ++j0) {
-                            const uint32_t v0 = lit_var(cv.lits[lb0 + j0]);
-                            if (gl == i0) { L.var[vb + nv + j0] = v0; L.vtau[vb + nv + j0] = tau; }
-                            if (gl > i0 && alive) {
-#pragma unroll
-                                for (uint32_t j = 0; j < RR_KR; ++j) alive &= rv[j] != v0;
-                                for (uint32_t j = RR_KR; j < w; ++j) alive &= lit_var(cv.lits[lb + j]) != v0;
-                            }
-                        }
-                        nv += w0;
-                        ++nc;
-                        gm = (__ballot(alive && gl > i0) >> gshift) & gmask;
-                        if (nc == D) {
+                        } else if (nc == D) {
                             stop = true;
-                            scan_end = gm ? pos + (uint32_t)__builtin_ctzll(gm) : (pos + GS < end ? pos + GS : end);
-                            break;
+                            scan_end = pu + GS < end ? pu + GS : end;
                         }
                     }
-                    if (stop) break;
-                    pos += GS;
+                    if (!stop) { pos += ST * GS; scan_end = pos; }
                 }
+                if (!stop && pos >= end) { exhausted = 1; scan_end = end; }
                 if (gl == 0) {
                     L.ncand[g] = nc;
-                    L.nvar[g] = nv;
                     L.scan_end[g] = scan_end;
                     L.exh[g] = exhausted;
+                    if (prof) { atomicAdd(&L.n_steps, n_steps); atomicAdd(&L.n_rounds, n_rounds); }
                 }
             }
         }
-        for (uint32_t i = tid; i < RR_HASH; i += RR_THREADS) { L.hkey[i] = 0xFFFFFFFFu; L.hmin[i] = 0xFFFFFFFFu; }
         if (tid == 0) L.trunc = L.wide ? 1u : D * B;
         __syncthreads();
-        // ---- earliest turn per variable, then the first turn that conflicts with an earlier one
-        for (uint32_t e = tid; e < B * vpg; e += RR_THREADS) {
-            const uint32_t g = e / vpg;
-            if (e - g * vpg >= L.nvar[g]) continue;
-            const uint32_t v = L.var[e], tau = L.vtau[e];
-            uint32_t h = rr_hash(v);
-            while (true) {
-                const uint32_t k = atomicCAS(&L.hkey[h], 0xFFFFFFFFu, v);
-                if (k == 0xFFFFFFFFu || k == v) { atomicMin(&L.hmin[h], tau); break; }
-                h = (h + 1) & (RR_HASH - 1);
-            }
-        }
+        if (prof) { const unsigned long long t1 = wall_now(); tacc[1] += t1 - tp0; tp0 = t1; }
+        // ---- the first turn a group did not decide, and the first pick that shares a variable
+        // with a pick of an earlier turn
         if (tid < B) {
             const uint32_t nc = L.ncand[tid];
-            if (nc < D) atomicMin(&L.trunc, nc * B + tid);  // first turn the group did not decide
+            if (nc < D) atomicMin(&L.trunc, nc * B + tid);
+        }
+        for (uint32_t e = tid; e < B * cpg; e += RR_THREADS) {
+            const uint32_t g = e / cpg, l = e - g * cpg;
+            if (l >= L.ncand[g] || (L.wide && e == 0)) continue;
+            const uint32_t tau = l * B + g, c = L.cc[e], lb = cv.offs[c], w = cv.offs[c + 1] - lb;
+            for (uint32_t j = 0; j < w; ++j) {
+                const uint32_t v = lit_var(cv.lits[lb + j]);
+                uint32_t h = rr_hash(v, RR_HBITS);
+                while (L.hkey[h] != v) h = (h + 1) & (RR_HASH - 1);
+                if (L.hmin[h] < tau) { atomicMin(&L.trunc, tau); break; }
+            }
         }
         __syncthreads();
-        for (uint32_t e = tid; e < B * vpg; e += RR_THREADS) {
-            const uint32_t g = e / vpg;
-            if (e - g * vpg >= L.nvar[g]) continue;
-            const uint32_t v = L.var[e], tau = L.vtau[e];
-            uint32_t h = rr_hash(v);
-            while (L.hkey[h] != v) h = (h + 1) & (RR_HASH - 1);
-            if (L.hmin[h] < tau) atomicMin(&L.trunc, tau);
-        }
-        __syncthreads();
+        if (prof) { const unsigned long long t1 = wall_now(); tacc[2] += t1 - tp0; tp0 = t1; }
         const uint32_t trunc = L.trunc;
-        // ---- commit turns < trunc
-        for (uint32_t e = tid; e < B * vpg; e += RR_THREADS) {
-            const uint32_t g = e / vpg;
-            if (e - g * vpg >= L.nvar[g] || L.vtau[e] >= trunc) continue;
-            __hip_atomic_store(&b.cover[L.var[e]], stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // ---- commit turns < trunc: covers, MIS, statistics; reset the batch hash
+        for (uint32_t i = tid; i < RR_HASH; i += RR_THREADS) {
+            const uint32_t k = L.hkey[i];
+            if (k != RR_EMPTY && L.hmin[i] < trunc)
+                __hip_atomic_store(&b.cover[k], stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            L.hkey[i] = RR_EMPTY;
+            L.hmin[i] = RR_EMPTY;
+            L.hgrp[i] = 0;
         }
         if (L.wide) {
-            const uint32_t c = L.cc[0], lb = cv.offs[c], w = L.cw[0];
+            const uint32_t c = L.cc[0], lb = cv.offs[c], w = cv.offs[c + 1] - lb;
             for (uint32_t j = tid; j < w; j += RR_THREADS)
                 __hip_atomic_store(&b.cover[lit_var(cv.lits[lb + j])], stamp, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
@@ -1621,12 +1833,9 @@ __global__ __launch_bounds__(RR_THREADS) void k_rr_mis(ClauseView cv, LoopBuffer
         for (uint32_t e = tid; e < B * cpg; e += RR_THREADS) {
             const uint32_t g = e / cpg, l = e - g * cpg;
             if (l >= L.ncand[g] || l * B + g >= trunc) continue;
-            const uint32_t c = L.cc[e];
-            b.tmis[atomicAdd(&L.tm, 1u)] = c;
-            atomicAdd(&b.tile_stats[2 * (c / TILE)], 1ull);
-            atomicAdd(&b.tile_stats[2 * (c / TILE) + 1], (unsigned long long)L.cw[e]);
+            b.tmis[atomicAdd(&L.tm, 1u)] = L.cc[e];
         }
-        uint32_t new_ptr = 0, ptr_set = 0xFFFFFFFFu;
+        uint32_t new_ptr = 0, ptr_set = RR_EMPTY;
         if (tid < B) {
             const uint32_t g = tid, nc = L.ncand[g];
             uint32_t a = trunc > g ? (trunc - g + B - 1) / B : 0;
@@ -1636,7 +1845,7 @@ __global__ __launch_bounds__(RR_THREADS) void k_rr_mis(ClauseView cv, LoopBuffer
         }
         __threadfence();
         __syncthreads();
-        if (ptr_set != 0xFFFFFFFFu) L.ptr[ptr_set] = new_ptr;
+        if (ptr_set != RR_EMPTY) L.ptr[ptr_set] = new_ptr;
         // ---- erasure at turn trunc, or the next turn index
         bool erase = false;
         uint32_t idx_e = 0;
@@ -1645,21 +1854,18 @@ __global__ __launch_bounds__(RR_THREADS) void k_rr_mis(ClauseView cv, LoopBuffer
             erase = (le == L.ncand[ge]) && L.exh[ge];
             idx_e = (t0 + 1 + trunc) % n_live;
         }
-        uint16_t moved = 0;
-        if (erase && tid >= idx_e && tid + 1 < n_live) moved = L.live[tid + 1];
-        uint16_t moved2[RR_TMAX / RR_THREADS - 1];
+        uint16_t moved[RR_TMAX / RR_THREADS];
 #pragma unroll
-        for (uint32_t r = 1; r < RR_TMAX / RR_THREADS; ++r) {
+        for (uint32_t r = 0; r < RR_TMAX / RR_THREADS; ++r) {
             const uint32_t i = tid + r * RR_THREADS;
-            moved2[r - 1] = (erase && i >= idx_e && i + 1 < n_live) ? L.live[i + 1] : 0;
+            moved[r] = (erase && i >= idx_e && i + 1 < n_live) ? L.live[i + 1] : 0;
         }
         __syncthreads();
         if (erase) {
-            if (tid >= idx_e && tid + 1 < n_live) L.live[tid] = moved;
 #pragma unroll
-            for (uint32_t r = 1; r < RR_TMAX / RR_THREADS; ++r) {
+            for (uint32_t r = 0; r < RR_TMAX / RR_THREADS; ++r) {
                 const uint32_t i = tid + r * RR_THREADS;
-                if (i >= idx_e && i + 1 < n_live) L.live[i] = moved2[r - 1];
+                if (i >= idx_e && i + 1 < n_live) L.live[i] = moved[r];
             }
         }
         if (tid == 0) {
@@ -1672,10 +1878,34 @@ __global__ __launch_bounds__(RR_THREADS) void k_rr_mis(ClauseView cv, LoopBuffer
             }
         }
         __syncthreads();
+        if (prof) { const unsigned long long t1 = wall_now(); tacc[3] += t1 - tp0; tp0 = t1; }
+    }
+    // statistics of the MIS (per tile, like the LFMIS kernels): |M| and resampled literals
+    const uint32_t tm = L.tm;
+    for (uint32_t i0 = 0; i0 < tm; i0 += 4 * RR_THREADS) {
+        uint32_t cs[4], ws[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t i = i0 + q * RR_THREADS + tid;
+            cs[q] = i < tm ? b.tmis[i] : RR_EMPTY;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ws[q] = cs[q] != RR_EMPTY ? cv.offs[cs[q] + 1] - cv.offs[cs[q]] : 0u;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (cs[q] == RR_EMPTY) continue;
+            atomicAdd(&b.tile_stats[2 * (cs[q] / TILE)], 1ull);
+            atomicAdd(&b.tile_stats[2 * (cs[q] / TILE) + 1], (unsigned long long)ws[q]);
+        }
     }
     if (tid == 0) {
         st->tmis_cnt = L.tm;
         st->tail_rounds = batches;
+        if (prof) {
+            unsigned long long* d = b.kdbg + (uint64_t)3 * DBG_BLOCKS * DBG_FIELDS;
+            d[0] = tacc[0]; d[1] = tacc[1]; d[2] = tacc[2]; d[3] = tacc[3];
+            d[4] = batches; d[5] = L.n_steps; d[6] = L.n_rounds; d[7] = L.tm;
+        }
         if (batches > st->max_rounds) st->max_rounds = batches;
         if (b.ktime) time_slot(b, st->n_iter - 1)[3] = wall_now();
     }
@@ -1800,12 +2030,18 @@ hipError_t launch_rr_mis(const ClauseView& cv, const LoopBuffers& b, hipStream_t
     if (cv.k != 0 || !b.rr_u || b.rr_T < 2 || b.rr_T > RR_TMAX) return hipErrorInvalidValue;
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_rr_mis, hipFuncAttributeMaxDynamicSharedMemorySize,
+        hipError_t e = hipFuncSetAttribute((const void*)k_rr_mis<4, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)sizeof(RRLds));
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute((const void*)k_rr_mis<8, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)sizeof(RRLds));
         if (e != hipSuccess) return e;
         attr_set = true;
     }
-    k_rr_mis<<<1, RR_THREADS, sizeof(RRLds), s>>>(cv, b);
+    if (b.n_tiles) k_rr_entries<<<b.n_tiles, 256, 0, s>>>(cv, b);
+    // clause variables held in registers while scanning: 4 for instances of width <= 4
+    if (b.rr_k >= 1 && b.rr_k <= 4) k_rr_mis<4, 4><<<1, RR_THREADS, sizeof(RRLds), s>>>(cv, b);
+    else k_rr_mis<8, 2><<<1, RR_THREADS, sizeof(RRLds), s>>>(cv, b);
     return hipGetLastError();
 }
 

@@ -372,6 +372,7 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
             rr_sets[rr_T] = (uint32_t)m;
         }
     }
+    const int rr_width = fixed_k;  // common clause width (-1: no clauses, 0: ragged)
     if (fixed_k < 1 || fixed_k > MAX_FIXED_K || (opt.flags & ALLL_FLAG_GENERIC_CSR) || opt.stream_batch || rr_T)
         fixed_k = 0;
     const uint64_t lim = 2ull * prob->n_vars;
@@ -441,13 +442,14 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     b.seed = opt.seed;
     if (rr_T) {
         uint32_t* d_sets = nullptr;
-        if ((rc = dalloc(c, &b.rr_u, m))) return bail(rc);
+        if ((rc = dalloc(c, &b.rr_u, 12 * (size_t)m))) return bail(rc);  // scan entries (k_rr_entries)
         if ((rc = dalloc(c, &d_sets, rr_T + 1))) return bail(rc);
         if (hipStreamSynchronize(c->stream) != hipSuccess ||
             hipMemcpy(d_sets, rr_sets.data(), (rr_T + 1) * 4ull, hipMemcpyHostToDevice) != hipSuccess)
             return bail(fail(ALLL_ERR_HIP, "chunk upload failed"));
         b.rr_sets = d_sets;
         b.rr_T = rr_T;
+        b.rr_k = (rr_width >= 1 && rr_width <= 8) ? (uint32_t)rr_width : 0u;
     }
     if ((rc = dalloc(c, &b.A, b.n_words + 4))) return bail(rc);  // +4: 16-byte tail loads
     if ((rc = dalloc(c, &b.vmask, (size_t)c->n_tiles_padded * TILE_WORDS))) return bail(rc);

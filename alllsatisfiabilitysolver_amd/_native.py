@@ -12,6 +12,8 @@ import subprocess
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG_DIR)
 LIB_PATH = os.path.join(PKG_DIR, "liballl.so")
+if os.environ.get("ALLL_LIB_AB"):  # development A/B timing of two builds (tools/ab_bench.sh)
+    LIB_PATH = os.path.abspath(os.environ["ALLL_LIB_AB"])
 
 ALLL_OK = 0
 ALLL_ERR_INVALID_ARG = 1

@@ -82,7 +82,10 @@ struct ClauseView {
 
 struct LoopBuffers {
     uint32_t* A;            // bit-packed assignment, ceil(n/32) words
-    uint64_t* vmask;        // violated bitmask in evaluation order, n_tiles_padded * TILE_WORDS words
+    uint64_t* vmask;        // violated bitmask in evaluation order, n_tiles_padded * TILE_WORDS words:
+                            // CSR: bit i of word w = position 64w + i; fixed width: word w = the
+                            // ballot of slot w % 4 of chunk w / 4, bit i = position
+                            // (w / 4) * CHUNK + 4i + w % 4
     uint32_t* tile_cnt;     // undecided violated entries per tile
     uint32_t* stage[2];     // per tile: TILE entries of undecided violated clauses, double
                             // buffered across LFMIS rounds.  Entry = {id, K literals} (fixed

@@ -61,16 +61,6 @@ __device__ __forceinline__ uint32_t abit(const uint32_t* __restrict__ A, uint32_
     return (A[v >> 5] >> (v & 31u)) & 1u;
 }
 
-// bits 0..15 of x -> bit positions 0,4,...,60 (4-way Morton spread)
-__device__ __forceinline__ uint64_t spread4(uint64_t x) {
-    x &= 0xFFFFull;
-    x = (x | (x << 24)) & 0x000000FF000000FFull;
-    x = (x | (x << 12)) & 0x000F000F000F000Full;
-    x = (x | (x << 6)) & 0x0303030303030303ull;
-    x = (x | (x << 3)) & 0x1111111111111111ull;
-    return x;
-}
-
 __device__ __forceinline__ bool eval_gate_closed(const DevState* st) {
     return st->done != 0 || st->n_iter >= st->limit_eval;
 }
@@ -237,11 +227,7 @@ __global__ __launch_bounds__(EVAL_THREADS) void k_eval_fixed(ClauseView cv, Loop
         const bool v[4] = {!sat[0] && c0 < m, !sat[1] && c0 + 1 < m, !sat[2] && c0 + 2 < m,
                            !sat[3] && c0 + 3 < m};
         const uint64_t b0 = __ballot(v[0]), b1 = __ballot(v[1]), b2 = __ballot(v[2]), b3 = __ballot(v[3]);
-        if (lane < 4) {
-            const int sh = 16 * lane;
-            b.vmask[g * 4 + lane] = spread4(b0 >> sh) | (spread4(b1 >> sh) << 1) |
-                                    (spread4(b2 >> sh) << 2) | (spread4(b3 >> sh) << 3);
-        }
+        if (lane < 4) b.vmask[g * 4 + lane] = lane == 0 ? b0 : lane == 1 ? b1 : lane == 2 ? b2 : b3;
         const uint32_t tot = __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
         if (tot) {
             uint32_t base = 0;
@@ -284,7 +270,6 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     const uint64_t m = cv.m;
     const uint32_t lds_words = min(b.n_words, LDS_WORDS);
-    const uint32_t lds_vars = lds_words * 32u;
     {
         // LDS-DMA fill (global_load_lds_dwordx4: no VGPR round trip; A padded to 4 words)
         const uint32_t n4 = (lds_words + 3) / 4;
@@ -358,11 +343,7 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
             const bool v[4] = {!sat[0] && c0 < m, !sat[1] && c0 + 1 < m, !sat[2] && c0 + 2 < m,
                                !sat[3] && c0 + 3 < m};
             const uint64_t b0 = __ballot(v[0]), b1 = __ballot(v[1]), b2 = __ballot(v[2]), b3 = __ballot(v[3]);
-            if (lane < 4) {
-                const int sh = 16 * lane;
-                b.vmask[g * 4 + lane] = spread4(b0 >> sh) | (spread4(b1 >> sh) << 1) |
-                                        (spread4(b2 >> sh) << 2) | (spread4(b3 >> sh) << 3);
-            }
+            if (lane < 4) b.vmask[g * 4 + lane] = lane == 0 ? b0 : lane == 1 ? b1 : lane == 2 ? b2 : b3;
             const uint32_t tot = __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
             if (tot) {
                 const uint32_t tile = (uint32_t)(g / (TILE / CHUNK));
@@ -447,16 +428,20 @@ __global__ __launch_bounds__(EVAL_THREADS) void k_collect(ClauseView cv, LoopBuf
     for (int s = 0; s < 16; ++s) {
         const uint64_t c = (uint64_t)tile * TILE + wave * (TILE / 4) + s * 64 + lane;
         const uint64_t mask = b.vmask[c >> 6];  // uniform load
-        const bool viol = ((mask >> lane) & 1ull) && c < m;
+        const bool viol = ((mask >> lane) & 1ull) && (K > 0 || c < m);  // (fixed K: bits past m are 0)
         if (!mask) continue;
         uint32_t base = 0;
         if (lane == 0) base = atomicAdd(&s_cnt, (uint32_t)__popcll(mask));
         base = __shfl(base, 0, 64);
         if (viol) {
+            // fixed K: word w of the bitmask holds positions (w / 4) * 256 + 4 * bit + w % 4
+            // (k_eval_* store their four ballots as they are); CSR: positions 64 * w + bit
+            const uint64_t w = c >> 6;
+            const uint64_t p = K > 0 ? (w >> 2) * CHUNK + 4u * lane + (w & 3u) : c;
             Ent<K> e;
-            e.w[0] = (uint32_t)c;
+            e.w[0] = (uint32_t)p;
             if constexpr (K > 0) {
-                const uint32_t* t = cv.lits_t + (c / CHUNK) * CHUNK * K + (c % CHUNK);
+                const uint32_t* t = cv.lits_t + (p / CHUNK) * CHUNK * K + (p % CHUNK);
 #pragma unroll
                 for (int j = 0; j < K; ++j) e.w[1 + j] = t[j * CHUNK];
             }

@@ -801,13 +801,17 @@ int alll_get_violated_mask(alll_ctx* c, uint64_t* out, uint64_t n_words) {
     if (n_words < need || (!out && need)) return fail(ALLL_ERR_INVALID_ARG, "need %llu words", (unsigned long long)need);
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    if (need) HIP_TRY(hipMemcpy(out, c->b.vmask, need * 8, hipMemcpyDeviceToHost));
-    if (c->m & 63) out[need - 1] &= (1ull << (c->m & 63)) - 1ull;
-    if (!c->perm.empty()) {  // device bits are in evaluation order
-        std::vector<uint64_t> ev(out, out + need);
+    if (!c->perm.empty()) {  // fixed width: device bits are chunk ballots in evaluation order
+        std::vector<uint64_t> ev((c->m + CHUNK - 1) / CHUNK * 4);
+        HIP_TRY(hipMemcpy(ev.data(), c->b.vmask, ev.size() * 8, hipMemcpyDeviceToHost));
         std::fill(out, out + need, 0ull);
-        for (uint64_t p = 0; p < c->m; ++p)
-            if ((ev[p >> 6] >> (p & 63)) & 1ull) out[c->perm[p] >> 6] |= 1ull << (c->perm[p] & 63);
+        for (uint64_t p = 0; p < c->m; ++p) {
+            const uint64_t w = (p / CHUNK) * 4 + (p & 3), bit = (p % CHUNK) >> 2;
+            if ((ev[w] >> bit) & 1ull) out[c->perm[p] >> 6] |= 1ull << (c->perm[p] & 63);
+        }
+    } else {
+        if (need) HIP_TRY(hipMemcpy(out, c->b.vmask, need * 8, hipMemcpyDeviceToHost));
+        if (c->m & 63) out[need - 1] &= (1ull << (c->m & 63)) - 1ull;
     }
     return ALLL_OK;
 }

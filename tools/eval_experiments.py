@@ -1,5 +1,5 @@
 """Timing-only eval-kernel variants (ALLL_EXPERIMENT, results invalid): back-to-back
-alll_bench_eval on config M.  3 = every lookup from LDS, 4 = no lookups, 5 = no entry lists."""
+alll_bench_eval on config M.  1 = no lookups, 2 = no entry lists, 3 = no LDS fill, 4 = 1+2, 5 = 1+2+3."""
 import os
 import statistics
 import sys
@@ -11,7 +11,7 @@ from alllsatisfiabilitysolver_amd import Solver, generate_ksat  # noqa: E402
 n, m, k = 2_500_000, 10_000_000, 3
 offs, lits = generate_ksat(1, n, m, k, 0)
 solvers = {}
-for x in os.environ.get("EXPS", "0,3,4,5").split(","):
+for x in os.environ.get("EXPS", "0,1,2,3,4,5").split(","):
     os.environ["ALLL_EXPERIMENT"] = x
     solvers[x] = Solver(n, offs, lits, seed=1)
 os.environ.pop("ALLL_EXPERIMENT")

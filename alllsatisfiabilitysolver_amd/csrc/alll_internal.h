@@ -109,7 +109,6 @@ struct LoopBuffers {
     uint32_t run_tiles;
     uint32_t n_runs;
     unsigned long long* kdbg;   // diagnostics (env ALLL_DEBUG_PHASES): per-workgroup phase stamps
-    uint32_t experiment;        // diagnostics (env ALLL_EXPERIMENT): timing-only variants, results invalid
     // streaming solve (SATInstance::solve(getEnumeratedClause, ...), T = 1): LFMIS priority =
     // position in the clause generator's yield window (alll_options.stream_batch > 0)
     uint64_t m;                 // clauses

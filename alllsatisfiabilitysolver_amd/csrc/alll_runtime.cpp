@@ -479,7 +479,6 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
         if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) == hipSuccess && khz > 0)
             c->wall_khz = khz;
     }
-    if (const char* e = getenv("ALLL_EXPERIMENT")) b.experiment = (uint32_t)atoi(e);  // diagnostics only
     if (getenv("ALLL_DEBUG_PHASES")) {  // diagnostics only
         if ((rc = dalloc(c, &b.kdbg, (size_t)DBG_KERNELS * DBG_BLOCKS * DBG_FIELDS))) return bail(rc);
     }

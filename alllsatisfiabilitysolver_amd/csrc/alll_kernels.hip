@@ -1239,32 +1239,36 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail(ClauseView cv, LoopBuffer
 
 // ------------------------------------------------------------------------------------
 // Resample (resample_clauses, SATInstance.h:340-365): the variables of the MIS clauses are
-// exactly those with cover[v] == stamp, so one pass over the variables gives each of them
-// Philox(seed, {v, it_lo, 0, it_hi}).x & 1 (it = resample round n_iter - 1) with plain word
-// stores: no per-clause atomics, a variable repeated inside a clause is drawn once (its
-// draws are equal anyway).  n_resamples counts every literal (SATInstance.h:363) in k_round.
+// exactly those with cover[v] == stamp.  Their new values come from one Philox draw per
+// assignment word: variable v takes bit v % 32 of Philox(seed, {v / 32, it_lo, 0, it_hi}).x
+// (it = resample round n_iter - 1; a variable repeated inside a clause is drawn once).  A lane
+// reads the stamps of 4 variables (one 16-byte load), 8 lanes OR their nibbles into a word's
+// covered mask, and the first of them draws and writes the word: no per-clause atomics.
+// n_resamples counts every literal (SATInstance.h:363) in the joins.
+__device__ __forceinline__ uint32_t resample_word(uint64_t seed, uint64_t it, uint32_t w) {
+    return philox_x(w, (uint32_t)it, 0u, (uint32_t)(it >> 32), (uint32_t)seed, (uint32_t)(seed >> 32));
+}
+
 __global__ __launch_bounds__(256) void k_resample_vars(LoopBuffers b) {
     const DevState* st = b.state;
     if (!st->active) return;
     const uint32_t stamp = st->stamp;
     const uint64_t it = st->n_iter - 1;
-    const uint32_t k0 = (uint32_t)b.seed, k1 = (uint32_t)(b.seed >> 32);
     const int lane = threadIdx.x & 63;
-    for (uint64_t v = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; v - lane < b.n_vars;
-         v += (uint64_t)gridDim.x * blockDim.x) {
-        const bool cov = v < b.n_vars && b.cover[v] == stamp;
-        uint32_t nb = 0;
-        if (cov) nb = philox_x((uint32_t)v, (uint32_t)it, 0u, (uint32_t)(it >> 32), k0, k1) & 1u;
-        const uint64_t mc = __ballot(cov), mb = __ballot(nb != 0);
-        if ((lane & 31) == 0 && v < b.n_vars) {
-            const int sh = lane;  // 0 or 32
-            const uint32_t cm = (uint32_t)(mc >> sh), bm = (uint32_t)(mb >> sh);
-            if (cm) {
-                uint32_t* w = &b.A[v >> 5];
-                *w = (*w & ~cm) | bm;
-            }
-        }
-    }
+    const bool lead = (lane & 7) == 0;
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // variables 4t .. 4t+3
+    const uint32_t w = (uint32_t)(t >> 3);
+    const bool live = w < b.n_words;  // (cover is padded to whole words with zeros)
+    uint32_t a = 0;
+    if (lead && live) a = b.A[w];
+    uint4 c = make_uint4(0u, 0u, 0u, 0u);
+    if (live) c = reinterpret_cast<const uint4*>(b.cover)[t];
+    uint32_t cm = ((uint32_t)(c.x == stamp) | ((uint32_t)(c.y == stamp) << 1) | ((uint32_t)(c.z == stamp) << 2) |
+                   ((uint32_t)(c.w == stamp) << 3)) << (4 * (lane & 7));
+    cm |= __shfl_xor(cm, 1, 64);
+    cm |= __shfl_xor(cm, 2, 64);
+    cm |= __shfl_xor(cm, 4, 64);
+    if (lead && cm) b.A[w] = (a & ~cm) | (resample_word(b.seed, it, w) & cm);
 }
 
 // Allreduce exchange (ALLL_FLAG_EXCHANGE_ALLREDUCE): each rank resamples only the MIS clauses
@@ -1281,7 +1285,7 @@ __device__ __forceinline__ void delta_clause(const ClauseView& cv, uint32_t* del
         bool dup = false;
         for (uint64_t q = lb; q < j; ++q) dup |= (lvar(cv, q) == v);
         if (dup) continue;
-        const uint32_t nb = philox_x(v, (uint32_t)it, 0u, (uint32_t)(it >> 32), k0, k1) & 1u;
+        const uint32_t nb = (philox_x(v >> 5, (uint32_t)it, 0u, (uint32_t)(it >> 32), k0, k1) >> (v & 31u)) & 1u;
         if (nb != (l & 1u)) atomicXor(&delta[v >> 5], 1u << (v & 31u));
     }
 }
@@ -1484,8 +1488,9 @@ __device__ __forceinline__ uint32_t rr_step_lane(const unsigned long long* sk, u
 // per-tile counts), so that a scan round of k_rr_mis is two dependent loads (entry, cover).
 struct RREnt {
     uint4 a;      // {clause id, literal start, width, 0}
-    uint4 v0, v1; // variables 0..7 (RR_EMPTY past the width)
+    uint4 v0, v1; // variables 0..RR_KE-1 (RR_EMPTY past the width)
 };
+static_assert(sizeof(RREnt) == 16 + 4 * RR_KE, "scan entry = header + RR_KE variables");
 
 __global__ __launch_bounds__(256) void k_rr_entries(ClauseView cv, LoopBuffers b) {
     if (!b.state->active) return;
@@ -1545,7 +1550,6 @@ __global__ __launch_bounds__(RR_THREADS) void k_rr_mis(ClauseView cv, LoopBuffer
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63;
     const uint32_t T = b.rr_T;
-    const uint64_t m = cv.m;
     const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
     const bool prof = b.kdbg != nullptr;  // diagnostics: phase times of thread 0
     unsigned long long tp0 = prof ? wall_now() : 0, tacc[4] = {0, 0, 0, 0};
@@ -2038,8 +2042,9 @@ hipError_t launch_resample(const ClauseView& cv, const LoopBuffers& b, uint32_t 
         return hipGetLastError();
     }
     if (b.n_vars == 0) return hipSuccess;
-    const uint32_t blocks = std::min<uint32_t>((b.n_vars + 255) / 256, 4096);
-    k_resample_vars<<<blocks, 256, 0, s>>>(b);
+    const uint64_t blocks = ((uint64_t)b.n_words * 8 + 255) / 256;  // a thread per 4 variables
+    if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    k_resample_vars<<<(uint32_t)blocks, 256, 0, s>>>(b);
     return hipGetLastError();
 }
 

@@ -55,14 +55,15 @@ void orc_init_assignment(uint64_t seed, uint32_t n_vars, uint32_t* A) {
     }
 }
 
-/* Resampled value of variable v in resample round `iter` (0-based):
- * Philox(key=seed, ctr={v, iter_lo, 0, iter_hi}).x & 1.
+/* Resampled value of variable v in resample round `iter` (0-based): bit v % 32 of
+ * Philox(key=seed, ctr={v / 32, iter_lo, 0, iter_hi}).x -- one draw per assignment word and
+ * round, like the initial assignment (ctr c2 = 0 here, 0xFFFFFFFF there: disjoint streams).
  * Replaces `vars[l>>1] = rbg.sample()` (SATInstance.h:358-360). */
 uint32_t orc_resample_bit(uint64_t seed, uint64_t iter, uint32_t v) {
     uint32_t key[2] = {(uint32_t)seed, (uint32_t)(seed >> 32)};
-    uint32_t ctr[4] = {v, (uint32_t)iter, 0u, (uint32_t)(iter >> 32)}, o[4];
+    uint32_t ctr[4] = {v >> 5, (uint32_t)iter, 0u, (uint32_t)(iter >> 32)}, o[4];
     orc_philox4x32_10(ctr, key, o);
-    return o[0] & 1u;
+    return (o[0] >> (v & 31u)) & 1u;
 }
 
 /* ------------------------------------------------------------------------- */

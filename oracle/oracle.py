@@ -145,11 +145,12 @@ def to_dimacs(n_vars, offs, lits, comments=()):
 
 
 def philox_bits(seed, it, vs):
-    """Vectorised Philox4x32-10 (x & 1) for ctr={v, it_lo, 0, it_hi}, key=seed; equals
-    resample_bit() elementwise (checked in tests/test_oracle.py)."""
+    """Vectorised resample bits: bit v % 32 of Philox4x32-10(key=seed, ctr={v / 32, it_lo, 0,
+    it_hi}).x; equals resample_bit() elementwise (checked in tests/test_oracle.py)."""
     M0, M1 = np.uint64(0xD2511F53), np.uint64(0xCD9E8D57)
     mask = np.uint64(0xFFFFFFFF)
-    c0 = np.asarray(vs).astype(np.uint64)
+    v = np.asarray(vs).astype(np.uint64)
+    c0 = v >> np.uint64(5)
     c1 = np.full_like(c0, it & 0xFFFFFFFF)
     c2 = np.zeros_like(c0)
     c3 = np.full_like(c0, it >> 32)
@@ -161,7 +162,7 @@ def philox_bits(seed, it, vs):
             ((p0 >> np.uint64(32)) ^ c3 ^ k1) & mask, p0 & mask
         k0 = (k0 + np.uint64(0x9E3779B9)) & mask
         k1 = (k1 + np.uint64(0xBB67AE85)) & mask
-    return (c0 & np.uint64(1)).astype(np.uint32)
+    return ((c0 >> (v & np.uint64(31))) & np.uint64(1)).astype(np.uint32)
 
 
 def resample_words(A, seed, it, vs):

@@ -979,6 +979,7 @@ __global__ __launch_bounds__(BRS_THREADS, 2) void k_bresolve(LoopBuffers b, uint
     extern __shared__ uint32_t s_min[];
     __shared__ uint32_t s_start[BKT_RUN_BATCH], s_pre[BKT_RUN_BATCH + 1];
     __shared__ uint32_t s_wsum[BRS_THREADS / 64];
+    __shared__ uint16_t s_seg[BRS_THREADS * BRS_UNROLL];  // single sweep: item -> segment
     const uint32_t bv = 1u << b.bkt_shift;
     ResolveLds L{s_min, s_start, s_pre, s_wsum};
     dbg_stamp(b, 1, 0);
@@ -993,7 +994,19 @@ __global__ __launch_bounds__(BRS_THREADS, 2) void k_bresolve(LoopBuffers b, uint
         dbg_stamp(b, 1, 1);
         if (np <= stride) {
             if (np > 0) {
-                resolve_load(b, L, 0, b.n_runs, np, first, run_cap, pos, x);
+                // item -> segment table (one LDS read per item instead of a binary search):
+                // a thread fills the items of its segments
+                for (uint32_t q = threadIdx.x; q < b.n_runs; q += blockDim.x)
+                    for (uint32_t f = L.pre[q]; f < L.pre[q + 1]; ++f) s_seg[f] = (uint16_t)q;
+                __syncthreads();
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const uint32_t f = min(first + 64 * u, np - 1);
+                    const uint32_t q = s_seg[f];
+                    pos[u] = q * run_cap + L.start[q] + (f - L.pre[q]);
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) x[u] = b.pairs[pos[u]];
 #pragma unroll
                 for (int u = 0; u < U; ++u)  // a clamped duplicate of the last pair is harmless
                     atomicMin(&L.min[(uint32_t)x[u] & 0x7FFFu], (uint32_t)(x[u] >> 32));

@@ -412,45 +412,54 @@ __global__ __launch_bounds__(EVAL_THREADS) void k_eval_csr(ClauseView cv, LoopBu
 
 // Multi-GPU: tiles owned by other ranks get their violated lists from the all-gathered
 // bitmask (evaluation positions; fixed K fetches the literals from the transposed store).
+// Thread t takes 16 bits of word t / 4 of the tile: all bitmask loads are issued at once, a
+// workgroup scan of the bit counts places every entry (ascending positions), and each thread's
+// literal loads follow -- two dependent load rounds per tile instead of one per word.
 template <int K>
 __global__ __launch_bounds__(EVAL_THREADS) void k_collect(ClauseView cv, LoopBuffers b,
                                                           uint32_t own_begin, uint32_t own_end) {
+    static_assert(EVAL_THREADS * 16 == TILE, "a thread per 16 positions of the tile");
     if (eval_gate_closed(b.state)) return;
     const uint32_t tile = blockIdx.x;
     if (tile >= own_begin && tile < own_end) return;
-    __shared__ uint32_t s_cnt;
+    __shared__ uint32_t s_wsum[EVAL_THREADS / 64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-    const uint64_t m = cv.m;
-    uint32_t* list = b.stage[0] + (uint64_t)tile * TILE * Ent<K>::S;
-    if (threadIdx.x == 0) s_cnt = 0;
-    __syncthreads();
-    for (int s = 0; s < 16; ++s) {
-        const uint64_t c = (uint64_t)tile * TILE + wave * (TILE / 4) + s * 64 + lane;
-        const uint64_t mask = b.vmask[c >> 6];  // uniform load
-        const bool viol = ((mask >> lane) & 1ull) && (K > 0 || c < m);  // (fixed K: bits past m are 0)
-        if (!mask) continue;
-        uint32_t base = 0;
-        if (lane == 0) base = atomicAdd(&s_cnt, (uint32_t)__popcll(mask));
-        base = __shfl(base, 0, 64);
-        if (viol) {
-            // fixed K: word w of the bitmask holds positions (w / 4) * 256 + 4 * bit + w % 4
-            // (k_eval_* store their four ballots as they are); CSR: positions 64 * w + bit
-            const uint64_t w = c >> 6;
-            const uint64_t p = K > 0 ? (w >> 2) * CHUNK + 4u * lane + (w & 3u) : c;
-            Ent<K> e;
-            e.w[0] = (uint32_t)p;
-            if constexpr (K > 0) {
-                const uint32_t* t = cv.lits_t + (p / CHUNK) * CHUNK * K + (p % CHUNK);
-#pragma unroll
-                for (int j = 0; j < K; ++j) e.w[1 + j] = t[j * CHUNK];
-            }
-            store_ent<K>(list + (uint64_t)(base + __popcll(mask & lt)) * Ent<K>::S, e);
-        }
+    const uint64_t w = (uint64_t)tile * TILE_WORDS + (threadIdx.x >> 2);
+    const uint32_t sl = (threadIdx.x & 3u) * 16u;
+    // (bits past m are 0: the evaluation kernels never set them)
+    uint32_t bits = (uint32_t)(b.vmask[w] >> sl) & 0xFFFFu;
+    const uint32_t cnt = (uint32_t)__popc(bits);
+    uint32_t incl = cnt;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
     }
+    if (lane == 63) s_wsum[wave] = incl;
     __syncthreads();
+    uint32_t pos = incl - cnt, total = 0;
+    for (int v = 0; v < EVAL_THREADS / 64; ++v) {
+        if (v < wave) pos += s_wsum[v];
+        total += s_wsum[v];
+    }
+    uint32_t* list = b.stage[0] + (uint64_t)tile * TILE * Ent<K>::S;
+    while (bits) {
+        const uint32_t i = sl + (uint32_t)__ffs(bits) - 1u;
+        bits &= bits - 1u;
+        // fixed K: word w of the bitmask holds positions (w / 4) * 256 + 4 * bit + w % 4
+        // (k_eval_* store their four ballots as they are); CSR: positions 64 * w + bit
+        const uint64_t p = K > 0 ? (w >> 2) * CHUNK + 4u * i + (w & 3u) : w * 64 + i;
+        Ent<K> e;
+        e.w[0] = (uint32_t)p;
+        if constexpr (K > 0) {
+            const uint32_t* t = cv.lits_t + (p / CHUNK) * CHUNK * K + (p % CHUNK);
+#pragma unroll
+            for (int j = 0; j < K; ++j) e.w[1 + j] = t[j * CHUNK];
+        }
+        store_ent<K>(list + (uint64_t)pos * Ent<K>::S, e);
+        ++pos;
+    }
     if (threadIdx.x == 0) {
-        b.tile_cnt[tile] = s_cnt;
+        b.tile_cnt[tile] = total;
         b.mis_cnt[tile] = 0;
     }
 }

@@ -14,6 +14,7 @@ constexpr uint32_t CHUNK = 256;              // clauses per transposed literal c
 constexpr int EVAL_THREADS = 256;
 constexpr int ROUND_THREADS = 256;
 constexpr int TAIL_THREADS = 1024;
+constexpr uint32_t WAVE_ROUND_MIN = 2;       // grid rounds from here on run a wave per tile
 constexpr int MAX_FIXED_K = 8;
 // Persistent hybrid evaluation: assignment words of the first LDS_VARS variables in LDS.
 constexpr uint32_t LDS_WORDS = 38912;              // 152 KiB of LDS

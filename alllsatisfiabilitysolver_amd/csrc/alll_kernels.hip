@@ -713,6 +713,128 @@ __global__ __launch_bounds__(ROUND_THREADS) void k_join(ClauseView cv, LoopBuffe
                  });
 }
 
+// Late rounds (r >= 2: ~60k undecided clauses of 1.25M at M, a few dozen per tile): the same
+// CLAIM / JOIN over the same per-tile lists with a wave per tile instead of a workgroup per
+// tile (a quarter of the workgroups to dispatch, no idle waves); positions in a tile's output
+// and MIS lists come from the wave's ballots.  `last`: survivors go to the tail's list (one
+// atomic per wave step that has survivors).
+__device__ __forceinline__ uint32_t wave_tile() {
+    return __builtin_amdgcn_readfirstlane(blockIdx.x * (ROUND_THREADS / 64) + (threadIdx.x >> 6));
+}
+
+template <int K>
+__global__ __launch_bounds__(ROUND_THREADS) void k_wclaim(ClauseView cv, LoopBuffers b, uint32_t r,
+                                                          const uint32_t* __restrict__ in, uint32_t* out) {
+    const DevState* st = b.state;
+    if (!st->active) return;
+    constexpr int S = Ent<K>::S;
+    const uint32_t tile = wave_tile();
+    if (tile >= b.n_tiles) return;
+    const uint32_t cnt = __builtin_amdgcn_readfirstlane(b.tile_cnt[tile]);
+    if (cnt == 0) return;
+    const int lane = threadIdx.x & 63;
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    const uint32_t stamp = st->stamp;
+    const unsigned long long keyhi = (unsigned long long)(~(st->round_base + r)) << 32;
+    unsigned long long* owner = owner_of(b, st->round_base + r);
+    const uint32_t* lin = in + (uint64_t)tile * TILE * S;
+    uint32_t* lout = out + (uint64_t)tile * TILE * S;
+    uint32_t kept = 0;
+    for (uint32_t i0 = 0; i0 < cnt; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        Ent<K> e;
+        bool keep = false;
+        if (i < cnt) {
+            load_ent<K>(e, lin + (uint64_t)i * S);
+            uint64_t lb;
+            const uint32_t len = ent_len<K>(cv, e, lb);
+            const uint32_t key = prio(b, st, e.w[0]);
+            if (key != ~0u) {
+                bool killed = false;
+                for (uint32_t j = 0; j < len; ++j) killed |= b.cover[lit_var(ent_lit<K>(cv, e, lb, j))] == stamp;
+                if (!killed) {
+                    for (uint32_t j = 0; j < len; ++j)
+                        __hip_atomic_fetch_min(&owner[lit_var(ent_lit<K>(cv, e, lb, j))], keyhi | key,
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    keep = true;
+                }
+            }
+        }
+        const uint64_t km = __ballot(keep);
+        if (keep) store_ent<K>(lout + (uint64_t)(kept + __popcll(km & lt)) * S, e);
+        kept += (uint32_t)__popcll(km);
+    }
+    if (lane == 0) b.tile_cnt[tile] = kept;
+}
+
+template <int K>
+__global__ __launch_bounds__(ROUND_THREADS) void k_wjoin(ClauseView cv, LoopBuffers b, uint32_t r,
+                                                         const uint32_t* __restrict__ in, uint32_t* out, int last) {
+    DevState* st = b.state;
+    if (!st->active) return;
+    constexpr int S = Ent<K>::S;
+    const uint32_t tile = wave_tile();
+    if (tile >= b.n_tiles) return;
+    const uint32_t cnt = __builtin_amdgcn_readfirstlane(b.tile_cnt[tile]);
+    if (cnt == 0) return;
+    const int lane = threadIdx.x & 63;
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    const uint32_t stamp = st->stamp;
+    const unsigned long long keyhi = (unsigned long long)(~(st->round_base + r)) << 32;
+    const unsigned long long* owner = owner_of(b, st->round_base + r);
+    const uint32_t* lin = in + (uint64_t)tile * TILE * S;
+    uint32_t* lout = out + (uint64_t)tile * TILE * S;
+    const uint32_t m0 = __builtin_amdgcn_readfirstlane(b.mis_cnt[tile]);
+    uint32_t* mis = b.mis + (uint64_t)tile * TILE + m0;
+    uint32_t kept = 0, joined = 0;
+    unsigned long long lits = 0, w = 0;
+    for (uint32_t i0 = 0; i0 < cnt; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        Ent<K> e;
+        bool own = false, keep = false;
+        if (i < cnt) {
+            load_ent<K>(e, lin + (uint64_t)i * S);
+            uint64_t lb;
+            const uint32_t len = ent_len<K>(cv, e, lb);
+            const uint32_t kc = prio(b, st, e.w[0]);
+            if (kc != ~0u) {  // (streaming: a clause not yielded this iteration leaves the list)
+                own = true;
+                for (uint32_t j = 0; j < len; ++j) own &= owner[lit_var(ent_lit<K>(cv, e, lb, j))] == (keyhi | kc);
+                keep = !own;
+                if (own) {
+                    for (uint32_t j = 0; j < len; ++j) b.cover[lit_var(ent_lit<K>(cv, e, lb, j))] = stamp;
+                    lits += len;
+                    w += mis_weight(b, st, kc);
+                }
+            }
+        }
+        const uint64_t jm = __ballot(own), km = __ballot(keep);
+        if (own) mis[joined + __popcll(jm & lt)] = e.w[0];
+        if (last) {  // survivors straight into the tail's list
+            uint32_t base = 0;
+            if (km && lane == 0) base = atomicAdd(&st->left_cnt, (uint32_t)__popcll(km));
+            base = __shfl(base, 0, 64);
+            if (keep) store_ent<K>(b.left + (uint64_t)(base + __popcll(km & lt)) * S, e);
+        } else if (keep) {
+            store_ent<K>(lout + (uint64_t)(kept + __popcll(km & lt)) * S, e);
+        }
+        joined += (uint32_t)__popcll(jm);
+        kept += (uint32_t)__popcll(km);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        lits += __shfl_down(lits, o, 64);
+        w += __shfl_down(w, o, 64);
+    }
+    if (lane == 0) {
+        b.tile_cnt[tile] = last ? 0u : kept;
+        b.mis_cnt[tile] = m0 + joined;
+        if (joined) {  // (the wave owns the tile: no other writer in this kernel)
+            b.tile_stats[2 * tile] += w;
+            b.tile_stats[2 * tile + 1] += lits;
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------
 // Bucketed round 0 (fixed width K; same decisions as CLAIM(0) + JOIN(0)).  Round 0 claims
 // ~k|U| random variables, which as global atomicMin runs at the chip's memory-side atomic
@@ -1992,10 +2114,18 @@ hipError_t launch_round(const ClauseView& cv, const LoopBuffers& b, uint32_t r, 
     if (b.n_tiles == 0) return hipSuccess;
     uint32_t* s0 = b.stage[0];
     uint32_t* s1 = b.stage[1];
+    const int l = last ? 1 : 0;
+    if (r >= WAVE_ROUND_MIN) {  // late rounds: a wave per tile
+        const uint32_t grid = (b.n_tiles + ROUND_THREADS / 64 - 1) / (ROUND_THREADS / 64);
+        ALLL_DISPATCH_K(cv.k, (k_wclaim<K><<<grid, ROUND_THREADS, 0, s>>>(cv, b, r, s1, s0)));
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        ALLL_DISPATCH_K(cv.k, (k_wjoin<K><<<grid, ROUND_THREADS, 0, s>>>(cv, b, r, s0, s1, l)));
+        return hipGetLastError();
+    }
     ALLL_DISPATCH_K(cv.k, (k_claim<K><<<b.n_tiles, ROUND_THREADS, 0, s>>>(cv, b, r, r == 0 ? s0 : s1, s0)));
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    const int l = last ? 1 : 0;
     ALLL_DISPATCH_K(cv.k, (k_join<K><<<b.n_tiles, ROUND_THREADS, 0, s>>>(cv, b, r, s0, s1, l)));
     return hipGetLastError();
 }

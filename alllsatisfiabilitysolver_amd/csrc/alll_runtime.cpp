@@ -54,6 +54,7 @@ int fail(int code, const char* fmt, ...) {
     } while (0)
 
 constexpr uint32_t DEFAULT_GRID_ROUNDS = 4;
+constexpr uint32_t GRAPH_UNROLL = 8;  // iterations per captured graph for long batches
 constexpr uint32_t SKEWED_GRID_ROUNDS = 6;  // instances with hot variables
 
 }  // namespace
@@ -75,9 +76,10 @@ struct alll_ctx {
     // device allocations
     std::vector<void*> allocs;
     DevState* h_state = nullptr;  // pinned mirror
-    // one captured iteration per LFMIS round-0 variant (0: atomic claims, 1: bucketed)
-    hipGraph_t graph[2] = {};
-    hipGraphExec_t graph_exec[2] = {};
+    // captured iterations per LFMIS round-0 variant (0: atomic claims, 1: bucketed): [v][0] one
+    // iteration, [v][1] GRAPH_UNROLL iterations (one launch gap per GRAPH_UNROLL iterations)
+    hipGraph_t graph[2][2] = {};
+    hipGraphExec_t graph_exec[2][2] = {};
     bool use_graph = true;
     uint64_t bucket_min_u = 0;  // bucketed round 0 when the last pass found at least this many
     hipEvent_t ev[8] = {};
@@ -207,11 +209,12 @@ int enqueue_iteration(alll_ctx* c, hipEvent_t* marks, int variant) {
     return ALLL_OK;
 }
 
-int ensure_graph(alll_ctx* c, int variant) {
-    if (!c->use_graph || c->graph_exec[variant]) return ALLL_OK;
+int ensure_graph(alll_ctx* c, int variant, int big) {
+    if (!c->use_graph || c->graph_exec[variant][big]) return ALLL_OK;
     hipError_t e = hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal);
     if (e != hipSuccess) { c->use_graph = false; return ALLL_OK; }
-    int rc = enqueue_iteration(c, nullptr, variant);
+    int rc = ALLL_OK;
+    for (uint32_t i = 0; i < (big ? GRAPH_UNROLL : 1u) && rc == ALLL_OK; ++i) rc = enqueue_iteration(c, nullptr, variant);
     hipGraph_t g = nullptr;
     e = hipStreamEndCapture(c->stream, &g);
     if (rc != ALLL_OK || e != hipSuccess || !g) {
@@ -220,24 +223,29 @@ int ensure_graph(alll_ctx* c, int variant) {
         c->use_graph = false;  // fall back to eager launches
         return ALLL_OK;
     }
-    e = hipGraphInstantiate(&c->graph_exec[variant], g, nullptr, nullptr, 0);
+    e = hipGraphInstantiate(&c->graph_exec[variant][big], g, nullptr, nullptr, 0);
     if (e != hipSuccess) {
         (void)hipGraphDestroy(g);
-        c->graph_exec[variant] = nullptr;
+        c->graph_exec[variant][big] = nullptr;
         c->use_graph = false;
         return ALLL_OK;
     }
-    c->graph[variant] = g;
+    c->graph[variant][big] = g;
     return ALLL_OK;
 }
 
 int launch_iterations(alll_ctx* c, uint64_t n) {
     const int variant = round0_variant(c);
-    int rc = ensure_graph(c, variant);
-    if (rc) return rc;
+    int rc;
+    if (n >= GRAPH_UNROLL && (rc = ensure_graph(c, variant, 1))) return rc;
+    if ((rc = ensure_graph(c, variant, 0))) return rc;
+    while (c->use_graph && n >= GRAPH_UNROLL) {
+        HIP_TRY(hipGraphLaunch(c->graph_exec[variant][1], c->stream));
+        n -= GRAPH_UNROLL;
+    }
     for (uint64_t i = 0; i < n; ++i) {
         if (c->use_graph) {
-            HIP_TRY(hipGraphLaunch(c->graph_exec[variant], c->stream));
+            HIP_TRY(hipGraphLaunch(c->graph_exec[variant][0], c->stream));
         } else {
             rc = enqueue_iteration(c, nullptr, variant);
             if (rc) return rc;
@@ -669,10 +677,11 @@ int alll_destroy(alll_ctx* c) {
     if (!c) return ALLL_OK;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (int v = 0; v < 2; ++v) {
-        if (c->graph_exec[v]) (void)hipGraphExecDestroy(c->graph_exec[v]);
-        if (c->graph[v]) (void)hipGraphDestroy(c->graph[v]);
-    }
+    for (int v = 0; v < 2; ++v)
+        for (int u = 0; u < 2; ++u) {
+            if (c->graph_exec[v][u]) (void)hipGraphExecDestroy(c->graph_exec[v][u]);
+            if (c->graph[v][u]) (void)hipGraphDestroy(c->graph[v][u]);
+        }
     if (c->comm) ncclCommDestroy(c->comm);
     for (void* p : c->allocs) (void)hipFree(p);
     for (auto& e : c->ev)

@@ -105,6 +105,8 @@ struct LoopBuffers {
     unsigned long long* pairs;  // bucketed round 0: n_runs x run_tiles*TILE*K pairs (nullptr = atomics)
     unsigned long long* runtab; // [bucket][run]: start | count << 32 of the bucket's pairs in the run
     uint32_t* run_pairs;        // pairs per run
+    const uint32_t* win_base;   // hybrid eval: per tile, first assignment word of its LDS window
+                                // (nullptr: words [0, LDS_WORDS) for every tile)
     uint32_t bkt_shift;         // bucket = variable >> bkt_shift
     uint32_t n_bkt;
     uint32_t run_tiles;

@@ -270,10 +270,11 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     const uint64_t m = cv.m;
     const uint32_t lds_words = min(b.n_words, LDS_WORDS);
-    {
-        // LDS-DMA fill (global_load_lds_dwordx4: no VGPR round trip; A padded to 4 words)
+    // LDS-DMA fill of assignment words [wb, wb + lds_words) (global_load_lds_dwordx4: no VGPR
+    // round trip; A padded to 4 words; wb + lds_words <= n_words)
+    auto fill = [&](uint32_t wb) {
         const uint32_t n4 = (lds_words + 3) / 4;
-        const uint4* src = reinterpret_cast<const uint4*>(b.A);
+        const uint4* src = reinterpret_cast<const uint4*>(b.A + wb);
         const uint32_t wbase = __builtin_amdgcn_readfirstlane(wave * 64);
         for (uint32_t q0 = 0; q0 < n4; q0 += HYB_THREADS) {
             const uint32_t q = q0 + threadIdx.x;
@@ -284,13 +285,29 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
                     16, 0, 0);
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    };
+    // window of a tile (words; b.win_base: instances sorted by smallest-variable block, else 0)
+    auto window = [&](uint32_t t) -> uint32_t { return b.win_base ? b.win_base[t] : 0u; };
+    uint32_t wb = window(t0);
+    fill(wb);
     const uint32_t* __restrict__ A = b.A;
     for (uint32_t pt = t0; pt < t1; pt += HYB_MAX_TILES) {
         const uint32_t pe = min(t1, pt + HYB_MAX_TILES);
         if (threadIdx.x < HYB_MAX_TILES) s_tcnt[threadIdx.x] = 0;
         __syncthreads();  // also publishes the LDS fill
-        const uint64_t gbeg = (uint64_t)pt * (TILE / CHUNK), gend = (uint64_t)pe * (TILE / CHUNK);
+      // segments of tiles with one window; the LDS is refilled between them
+      for (uint32_t sa = pt; sa < pe;) {
+        const uint32_t ws = window(sa);
+        uint32_t se = sa + 1;
+        while (se < pe && window(se) == ws) ++se;
+        if (ws != wb) {
+            __syncthreads();  // every wave is done with the old window
+            fill(ws);
+            __syncthreads();
+            wb = ws;
+        }
+        const uint64_t gbeg = (uint64_t)sa * (TILE / CHUNK), gend = (uint64_t)se * (TILE / CHUNK);
+        sa = se;
         for (uint64_t g = gbeg + wave; g < gend; g += HYB_THREADS / 64) {
             const uint64_t cb = g * CHUNK;
             uint32_t sat[4] = {0u, 0u, 0u, 0u};
@@ -319,7 +336,7 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
                     for (int q = 0; q < 4; ++q) {
                         wi[q] = (xs[q] & LIT_MASK) >> 6;
                         need[q] = first || !sat[q];
-                        useg[q] = need[q] && wi[q] >= lds_words;
+                        useg[q] = need[q] && wi[q] - wb >= lds_words;  // (unsigned: below the window too)
                     }
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
@@ -329,7 +346,7 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
                         lw[q] = 0;
-                        if (need[q] && !useg[q]) lw[q] = s_A[wi[q]];
+                        if (need[q] && !useg[q]) lw[q] = s_A[wi[q] - wb];
                     }
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
@@ -355,6 +372,7 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
                 emit4<K>(b.stage[0] + (uint64_t)tile * TILE * Ent<K>::S, base + pre, c0, v, x);
             }
         }
+      }
         __syncthreads();
         if (threadIdx.x < pe - pt) {
             b.tile_cnt[pt + threadIdx.x] = s_tcnt[threadIdx.x];

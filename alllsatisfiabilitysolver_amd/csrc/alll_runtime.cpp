@@ -578,24 +578,36 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
         // clauses are evaluated sorted by (largest, second largest) variable and each clause's
         // literals are stored by descending variable, so the gathers of slot 0 (and mostly
         // slot 1) of a wave hit a few cache lines.  perm[p] = original id of position p.
+        //
+        // Windows (instances with more than LDS_VARS variables; ALLL_EVAL_WINDOWS=0/1 overrides):
+        // the hybrid evaluation's LDS holds LDS_VARS consecutive variables; clauses are first
+        // grouped by the block of their smallest variable and each tile's LDS window starts at
+        // its block, so the smallest variable (looked up by every clause) is an LDS hit.
         std::vector<uint32_t>& perm = c->perm;
         perm.resize(m);
+        bool windows = c->n_vars > LDS_VARS;
+        if (const char* e = getenv("ALLL_EVAL_WINDOWS")) windows = atoi(e) != 0;  // tuning, tests
         {
             const int K = fixed_k;
-            auto key_of = [&](uint64_t cl) -> uint64_t {
-                uint32_t a = 0, b2 = 0;
+            struct Key { uint64_t k1; uint32_t k2, id; };
+            auto key_of = [&](uint64_t cl) -> Key {
+                uint32_t a = 0, b2 = 0, lo = ~0u;
                 for (int j = 0; j < K; ++j) {
                     const uint32_t v = prob->literals[cl * K + j] >> 1;
                     if (v > a) { b2 = a; a = v; }
                     else if (v > b2) b2 = v;
+                    lo = std::min(lo, v);
                 }
-                return ((uint64_t)a << 32) | b2;
+                const uint64_t blk = windows ? lo / LDS_VARS : 0;
+                return {(blk << 32) | a, b2, (uint32_t)cl};
             };
             auto sort_range = [&](uint64_t cb0, uint64_t ce0) {
-                std::vector<std::pair<uint64_t, uint32_t>> kv(ce0 - cb0);
-                for (uint64_t cl = cb0; cl < ce0; ++cl) kv[cl - cb0] = {key_of(cl), (uint32_t)cl};
-                std::sort(kv.begin(), kv.end());
-                for (uint64_t i = 0; i < kv.size(); ++i) perm[cb0 + i] = kv[i].second;
+                std::vector<Key> kv(ce0 - cb0);
+                for (uint64_t cl = cb0; cl < ce0; ++cl) kv[cl - cb0] = key_of(cl);
+                std::sort(kv.begin(), kv.end(), [](const Key& x, const Key& y) {
+                    return x.k1 != y.k1 ? x.k1 < y.k1 : (x.k2 != y.k2 ? x.k2 < y.k2 : x.id < y.id);
+                });
+                for (uint64_t i = 0; i < kv.size(); ++i) perm[cb0 + i] = kv[i].id;
             };
             std::vector<std::thread> th;
             for (int r = 0; r < c->world; ++r) {
@@ -625,6 +637,24 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
         cv.perm = d_perm;
         cv.lits_t = d_t;
         cv.offs = nullptr;
+        if (windows && m) {  // LDS window of every tile: the block of its first clause's smallest variable
+            const uint32_t lds_words = std::min<uint32_t>(b.n_words, LDS_WORDS);
+            std::vector<uint32_t> wb(n_tiles, 0u);
+            for (uint32_t tt = 0; tt < n_tiles; ++tt) {
+                const uint64_t p = (uint64_t)tt * TILE;
+                if (p >= m) break;
+                const uint64_t cl = perm[p];
+                uint32_t lo = ~0u;
+                for (int j = 0; j < fixed_k; ++j) lo = std::min(lo, prob->literals[cl * fixed_k + j] >> 1);
+                wb[tt] = std::min<uint64_t>((uint64_t)(lo / LDS_VARS) * LDS_WORDS, b.n_words - lds_words);
+            }
+            uint32_t* d_wb = nullptr;
+            if ((rc = dalloc(c, &d_wb, n_tiles))) return bail(rc);
+            if (hipStreamSynchronize(c->stream) != hipSuccess ||
+                hipMemcpy(d_wb, wb.data(), n_tiles * 4ull, hipMemcpyHostToDevice) != hipSuccess)
+                return bail(fail(ALLL_ERR_HIP, "window upload failed"));
+            b.win_base = d_wb;
+        }
     } else {
         std::vector<uint32_t> o32(m + 1);
         for (uint64_t i = 0; i <= m; ++i) o32[i] = m ? (uint32_t)prob->offsets[i] : 0u;

@@ -24,7 +24,7 @@ T1_FIXTURES = sorted(p for p in glob.glob(os.path.join(GOLDEN, "*_T1.npz")))
 # name -> (flags, environment at create): the default policy picks the bucketed LFMIS round 0
 # only for large violated sets, "buckets" forces it for every iteration
 LAYOUTS = {"hybrid": (0, {}), "fixed": (1 << 3, {}), "csr": (1 << 2, {}), "atomic_claims": (1 << 5, {}),
-           "buckets": (0, {"ALLL_BUCKET_MIN_U": "0"})}
+           "buckets": (0, {"ALLL_BUCKET_MIN_U": "0"}), "windows": (0, {"ALLL_EVAL_WINDOWS": "1"})}
 
 
 def make_solver(layout, monkeypatch, *args, **kw):
@@ -212,15 +212,19 @@ BIG = {
     "C2_3sat_4M": (1_000_000, 4_000_000, 3, 0),
     "C3_8sat_6M": (4_000_000, 6_000_000, 8, 0),
     "C5_powerlaw_10M": (2_500_000, 10_000_000, 3, 1),
+    "W_3sat_4Mvars": (4_000_000, 2_000_000, 3, 0),  # 4 LDS blocks of variables: windowed eval
+    "M_no_windows": (2_500_000, 10_000_000, 3, 0, {"ALLL_EVAL_WINDOWS": "0"}),
 }
 
 
 @pytest.mark.slow
 @pytest.mark.parametrize("name", list(BIG))
-def test_baseline_sizes_bit_exact_steps(gpu, oracle_mod, name):
+def test_baseline_sizes_bit_exact_steps(gpu, oracle_mod, name, monkeypatch):
     from alllsatisfiabilitysolver_amd import Solver, generate_ksat
 
-    n, m, k, kind = BIG[name]
+    n, m, k, kind = BIG[name][:4]
+    for key, v in (BIG[name][4] if len(BIG[name]) > 4 else {}).items():
+        monkeypatch.setenv(key, v)
     offs, lits = generate_ksat(1, n, m, k, kind)
     seed = 1
     with Solver(n, offs, lits, seed=seed) as s:

@@ -306,15 +306,15 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
             __syncthreads();
             wb = ws;
         }
-        const uint64_t gbeg = (uint64_t)sa * (TILE / CHUNK), gend = (uint64_t)se * (TILE / CHUNK);
+        // (chunks past m are skipped: their bitmask words stay 0 from the allocation)
+        const uint64_t gbeg = (uint64_t)sa * (TILE / CHUNK);
+        const uint64_t gend = min((uint64_t)se * (TILE / CHUNK), (m + CHUNK - 1) / CHUNK);
         sa = se;
         for (uint64_t g = gbeg + wave; g < gend; g += HYB_THREADS / 64) {
             const uint64_t cb = g * CHUNK;
             uint32_t sat[4] = {0u, 0u, 0u, 0u};
             uint4 x[K];
-#pragma unroll
-            for (int j = 0; j < K; ++j) x[j] = make_uint4(0u, 0u, 0u, 0u);
-            if (cb < m) {
+            {
                 const uint4* src = reinterpret_cast<const uint4*>(cv.lits_t + cb * K) + lane;
 #pragma unroll
                 for (int j = 0; j < K; ++j) x[j] = src[j * 64];
@@ -344,21 +344,25 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
                         if (useg[q]) gw[q] = A[wi[q]];
                     }
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        lw[q] = 0;
-                        if (need[q] && !useg[q]) lw[q] = s_A[wi[q] - wb];
-                    }
+                    for (int q = 0; q < 4; ++q)  // (unconditional: lanes that need no LDS word read word 0)
+                        lw[q] = s_A[need[q] && !useg[q] ? wi[q] - wb : 0u];
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
-                        const uint32_t w = gw[q] | lw[q];  // (both live: never one shared register)
+                        const uint32_t w = useg[q] ? gw[q] : lw[q];
                         const uint32_t bit = ((w >> ((xs[q] >> 1) & 31u)) & 1u) ^ (xs[q] & 1u);
                         sat[q] |= need[q] ? bit : 0u;
                     }
                 }
             }
             const uint64_t c0 = cb + 4u * lane;
-            const bool v[4] = {!sat[0] && c0 < m, !sat[1] && c0 + 1 < m, !sat[2] && c0 + 2 < m,
-                               !sat[3] && c0 + 3 < m};
+            bool v[4];
+            if (cb + CHUNK <= m) {  // (wave-uniform: only the last chunk holds positions past m)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) v[q] = !sat[q];
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) v[q] = !sat[q] && c0 + q < m;
+            }
             const uint64_t b0 = __ballot(v[0]), b1 = __ballot(v[1]), b2 = __ballot(v[2]), b3 = __ballot(v[3]);
             if (lane < 4) b.vmask[g * 4 + lane] = lane == 0 ? b0 : lane == 1 ? b1 : lane == 2 ? b2 : b3;
             const uint32_t tot = __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);

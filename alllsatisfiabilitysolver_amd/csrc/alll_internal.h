@@ -140,7 +140,8 @@ hipError_t launch_collect(const ClauseView& cv, const LoopBuffers& b, uint32_t o
 hipError_t launch_reduce(const LoopBuffers& b, int mode, hipStream_t s);
 hipError_t launch_round(const ClauseView& cv, const LoopBuffers& b, uint32_t r, bool last,
                         hipStream_t s);
-hipError_t launch_round0_buckets(const ClauseView& cv, const LoopBuffers& b, bool last, hipStream_t s);
+hipError_t launch_round0_buckets(const ClauseView& cv, const LoopBuffers& b, bool last, bool fused_reduce,
+                                 hipStream_t s);
 hipError_t launch_tail(const ClauseView& cv, const LoopBuffers& b, uint32_t first_round,
                        hipStream_t s);
 hipError_t launch_rr_mis(const ClauseView& cv, const LoopBuffers& b, hipStream_t s);

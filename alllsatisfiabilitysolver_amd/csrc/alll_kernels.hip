@@ -487,13 +487,10 @@ __global__ __launch_bounds__(EVAL_THREADS) void k_collect(ClauseView cv, LoopBuf
 }
 
 // ------------------------------------------------------------------------------------
-// Single workgroup: violated count + loop state (mode 0) or standalone count (mode 1).
-__global__ __launch_bounds__(1024) void k_reduce(LoopBuffers b, int mode) {
+// Violated count + loop state (mode 0) or standalone count (mode 1), by one 1024-thread
+// workgroup: k_reduce, or the extra workgroup of k_bscatter (fused reduce).
+__device__ void reduce_body(const LoopBuffers& b, int mode) {
     DevState* st = b.state;
-    if (mode == 0 && eval_gate_closed(st)) {
-        if (threadIdx.x == 0) st->active = 0;
-        return;
-    }
     const unsigned long long reduce_t0 = wall_now();
     __shared__ unsigned long long s_sum;
     __shared__ uint32_t s_first;  // first tile with a violated clause (streaming window)
@@ -549,6 +546,14 @@ __global__ __launch_bounds__(1024) void k_reduce(LoopBuffers b, int mode) {
             st->win_len = (k0 == b.m) ? b.m : b.m - k0;
         }
     }
+}
+
+__global__ __launch_bounds__(1024) void k_reduce(LoopBuffers b, int mode) {
+    if (mode == 0 && eval_gate_closed(b.state)) {
+        if (threadIdx.x == 0) b.state->active = 0;
+        return;
+    }
+    reduce_body(b, mode);
 }
 
 // ------------------------------------------------------------------------------------
@@ -923,9 +928,27 @@ __device__ __forceinline__ void load_run_entries(const uint32_t* list, uint32_t 
 }
 
 template <int K>
-__global__ __launch_bounds__(BSC_THREADS) void k_bscatter(ClauseView cv, LoopBuffers b, uint32_t* list) {
+//
+// fused_reduce (one GPU, no hot variables): the loop's reduce runs in an extra workgroup
+// (blockIdx.x == n_runs) beside the runs, saving the k_reduce launch.  The run workgroups then
+// read no loop state: when this iteration turns out inactive, their pairs are simply never
+// resolved (k_bresolve and k_bjoin test st->active, which the reduce has set by then), and a
+// skipped evaluation leaves empty or unconsumed lists.
+__global__ __launch_bounds__(BSC_THREADS) void k_bscatter(ClauseView cv, LoopBuffers b, uint32_t* list,
+                                                          int fused_reduce) {
     const DevState* st = b.state;
-    if (!st->active) return;
+    if (fused_reduce) {
+        if (blockIdx.x == b.n_runs) {
+            if (eval_gate_closed(st)) {
+                if (threadIdx.x == 0) b.state->active = 0;
+            } else {
+                reduce_body(b, 0);
+            }
+            return;
+        }
+    } else if (!st->active) {
+        return;
+    }
     constexpr int S = Ent<K>::S;
     constexpr int U = BKT_UNROLL;
     const uint32_t r = blockIdx.x;
@@ -2152,7 +2175,9 @@ hipError_t launch_round(const ClauseView& cv, const LoopBuffers& b, uint32_t r, 
     return hipGetLastError();
 }
 
-hipError_t launch_round0_buckets(const ClauseView& cv, const LoopBuffers& b, bool last, hipStream_t s) {
+hipError_t launch_round0_buckets(const ClauseView& cv, const LoopBuffers& b, bool last, bool fused_reduce,
+                                 hipStream_t s) {
+    if (fused_reduce && cv.n_hot) return hipErrorInvalidValue;  // (hot claims need the epoch)
     // buffers as CLAIM(0) + JOIN(0): eval -> stage[0] (ids translated in place); JOIN stage[0] -> stage[1]
     if (b.n_tiles == 0 || cv.k == 0 || !b.pairs) return hipErrorInvalidValue;
     const uint64_t run_cap = (uint64_t)b.run_tiles * TILE * cv.k;
@@ -2172,7 +2197,9 @@ hipError_t launch_round0_buckets(const ClauseView& cv, const LoopBuffers& b, boo
         if (e != hipSuccess) return e;
         attr_set[cv.k] = true;
     }
-    ALLL_DISPATCH_K(cv.k, (k_bscatter<(K > 0 ? K : 1)><<<b.n_runs, BSC_THREADS, BKT_STAGE * 8, s>>>(cv, b, b.stage[0])));
+    const int fr = fused_reduce ? 1 : 0;
+    ALLL_DISPATCH_K(cv.k, (k_bscatter<(K > 0 ? K : 1)><<<b.n_runs + fr, BSC_THREADS, BKT_STAGE * 8, s>>>(
+                              cv, b, b.stage[0], fr)));
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     k_bresolve<<<b.n_bkt, BRS_THREADS, lds, s>>>(b, (uint32_t)run_cap);

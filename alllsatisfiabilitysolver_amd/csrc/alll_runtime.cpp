@@ -70,6 +70,7 @@ struct alll_ctx {
     LoopBuffers b{};
     uint32_t tiles_per_rank = 0, own_begin = 0, own_end = 0, n_tiles_padded = 0;
     uint32_t grid_rounds = DEFAULT_GRID_ROUNDS;
+    bool fuse_reduce = true;     // env ALLL_FUSE_REDUCE=0: separate k_reduce (tests, A/B)
     int rank = 0, world = 1;
     bool allreduce = false;
     ncclComm_t comm = nullptr;
@@ -182,12 +183,15 @@ int enqueue_iteration(alll_ctx* c, hipEvent_t* marks, int variant) {
         HIP_TRY(launch_collect(c->cv, c->b, c->own_begin, c->own_end, s));
     }
     if (marks) HIP_TRY(hipEventRecord(marks[2], s));
-    HIP_TRY(launch_reduce(c->b, 0, s));
+    // the bucketed round 0 runs the reduce in an extra k_bscatter workgroup (one GPU, no hot
+    // variables, not the round robin): one launch less
+    const bool fused = c->fuse_reduce && variant == 1 && c->world == 1 && c->cv.n_hot == 0 && !c->b.rr_T;
+    if (!fused) HIP_TRY(launch_reduce(c->b, 0, s));
     if (c->b.rr_T) {
         HIP_TRY(launch_rr_mis(c->cv, c->b, s));
     } else {
         for (uint32_t r = 0; r < c->grid_rounds; ++r) {
-            if (r == 0 && variant == 1) HIP_TRY(launch_round0_buckets(c->cv, c->b, c->grid_rounds == 1, s));
+            if (r == 0 && variant == 1) HIP_TRY(launch_round0_buckets(c->cv, c->b, c->grid_rounds == 1, fused, s));
             else HIP_TRY(launch_round(c->cv, c->b, r, r + 1 == c->grid_rounds, s));
         }
         HIP_TRY(launch_tail(c->cv, c->b, c->grid_rounds, s));
@@ -410,6 +414,7 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     c->allreduce = (opt.flags & ALLL_FLAG_EXCHANGE_ALLREDUCE) != 0;
     c->use_graph = (opt.flags & ALLL_FLAG_NO_GRAPH) == 0;
     c->grid_rounds = opt.grid_rounds ? opt.grid_rounds : DEFAULT_GRID_ROUNDS;
+    if (const char* e = getenv("ALLL_FUSE_REDUCE")) c->fuse_reduce = atoi(e) != 0;
     auto bail = [&](int rc) { alll_destroy(c); return rc; };
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
         return bail(fail(ALLL_ERR_HIP, "hipStreamCreate failed"));

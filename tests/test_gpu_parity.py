@@ -197,6 +197,36 @@ def test_grid_round_split_is_invisible(gpu, oracle_mod, grid_rounds, monkeypatch
         np.testing.assert_array_equal(s.assignment_words(), A_o)
 
 
+@pytest.mark.parametrize("fuse", ["0", "1"])
+def test_fused_reduce_is_invisible(gpu, oracle_mod, fuse, monkeypatch):
+    """The loop's reduce runs in an extra workgroup of the bucketed round 0 (default) or as its
+    own kernel (ALLL_FUSE_REDUCE=0): same trajectory, statistics, stop and cap as the oracle."""
+    from alllsatisfiabilitysolver_amd import Solver, generate_ksat
+
+    n = 20000
+    offs, lits = generate_ksat(3, n, 2 * n, 3, 0)  # ratio 2 over 10 tiles: converges
+    st_o, A_o, rows = oracle_mod.solve(n, offs, lits, 5, max_iters=400, trace=True)
+    assert st_o["solved"] == 1
+    monkeypatch.setenv("ALLL_FUSE_REDUCE", fuse)
+    monkeypatch.setenv("ALLL_BUCKET_MIN_U", "0")  # the bucketed round 0 in every iteration
+    with Solver(n, offs, lits, seed=5, max_iters=400) as s:
+        for it, nu, nm, dres, A_after in rows[:6]:
+            s.run(1)
+            assert s.stats()["n_violated"] == nu
+            np.testing.assert_array_equal(s.assignment_words(), A_after)
+        st = s.solve()
+        for key in ("n_iterations", "n_resamples", "avg_mis_size", "solved"):
+            assert st[key] == st_o[key], key
+        np.testing.assert_array_equal(s.assignment_words(), A_o)
+    # a cap that stops before convergence: the final pass evaluates without resampling
+    st_c, A_c, _ = oracle_mod.solve(n, offs, lits, 5, max_iters=7, trace=True)
+    with Solver(n, offs, lits, seed=5, max_iters=7) as s:
+        st = s.solve()
+        for key in ("n_iterations", "n_resamples", "avg_mis_size", "solved"):
+            assert st[key] == st_c[key], key
+        np.testing.assert_array_equal(s.assignment_words(), A_c)
+
+
 def _oracle_step(o, n, offs, lits, A, seed, it):
     """One serial iteration (eval -> LFMIS -> Philox resample) on the CPU."""
     m = offs.size - 1

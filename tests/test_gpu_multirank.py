@@ -68,12 +68,20 @@ def run_world(world, spec, flags):
     return sorted(res, key=lambda r: r[0])
 
 
-@pytest.mark.parametrize("world,mode", [(2, "allgather"), (2, "allreduce"), (3, "allgather"),
-                                        (3, "allreduce")])
-def test_sharded_solver_matches_oracle(oracle_mod, native, world, mode):
-    o = oracle_mod
+SPECS = {
     # 7 tiles of 4096 clauses -> uneven shards; fixed-k hybrid eval path
-    n, m, k, kind, seed, K = spec = (7000, 28000, 3, 0, 5, 8)
+    "small": (7000, 28000, 3, 0, 5, 8),
+    # more variables than one LDS window holds: windowed evaluation order inside every shard
+    "windows": (1_600_000, 40000, 3, 0, 5, 4),
+}
+
+
+@pytest.mark.parametrize("world,mode,spec_name", [(2, "allgather", "small"), (2, "allreduce", "small"),
+                                                  (3, "allgather", "small"), (3, "allreduce", "small"),
+                                                  (2, "allgather", "windows")])
+def test_sharded_solver_matches_oracle(oracle_mod, native, world, mode, spec_name):
+    o = oracle_mod
+    n, m, k, kind, seed, K = spec = SPECS[spec_name]
     flags = native.FLAG_EXCHANGE_ALLREDUCE if mode == "allreduce" else 0
     offs, lits = o.generate_ksat(1, n, m, k, kind)
     st_o, A_o, rows = o.solve(n, offs, lits, seed, max_iters=K + 1, trace=True)

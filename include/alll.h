@@ -197,7 +197,7 @@ int alll_synchronize(alll_ctx* ctx);
 uint64_t alll_eval_bytes(alll_ctx* ctx);
 /* Layout in use: 0 generic CSR, k>0 fixed-width-k layout. */
 int alll_layout(alll_ctx* ctx);
-/* Name of the evaluation kernel the loop launches (e.g. "k_eval_ranged<3>"). */
+/* Name of the evaluation kernel the loop launches (e.g. "k_eval_hybrid<3>"). */
 const char* alll_eval_kernel(alll_ctx* ctx);
 
 /* ---- host-side helpers (no GPU needed) ---------------------------------------------- */

@@ -106,7 +106,8 @@ struct LoopBuffers {
     unsigned long long* runtab; // [bucket][run]: start | count << 32 of the bucket's pairs in the run
     uint32_t* run_pairs;        // pairs per run
     const uint32_t* win_base;   // hybrid eval: per tile, first assignment word of its LDS window
-                                // (nullptr: words [0, LDS_WORDS) for every tile)
+                                // (nullptr: words [0, win_words) for every tile)
+    uint32_t win_words;         // hybrid eval: LDS window size in words (<= LDS_WORDS)
     uint32_t bkt_shift;         // bucket = variable >> bkt_shift
     uint32_t n_bkt;
     uint32_t run_tiles;

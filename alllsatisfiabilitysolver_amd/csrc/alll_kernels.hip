@@ -269,7 +269,7 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     const uint64_t m = cv.m;
-    const uint32_t lds_words = min(b.n_words, LDS_WORDS);
+    const uint32_t lds_words = min(b.n_words, b.win_words);
     // LDS-DMA fill of assignment words [wb, wb + lds_words) (global_load_lds_dwordx4: no VGPR
     // round trip; A padded to 4 words; wb + lds_words <= n_words)
     auto fill = [&](uint32_t wb) {
@@ -2115,7 +2115,7 @@ hipError_t launch_eval_hybrid(const ClauseView& cv, const LoopBuffers& b, uint32
     if (tile_end <= tile_begin) return hipSuccess;
     const uint32_t nt = tile_end - tile_begin;
     const dim3 grid(std::min<uint32_t>(nt, (uint32_t)std::max(1, n_blocks)));
-    const size_t lds = (size_t)std::max<uint32_t>(4, (std::min(b.n_words, LDS_WORDS) + 3) / 4 * 4) * 4;
+    const size_t lds = (size_t)std::max<uint32_t>(4, (std::min(b.n_words, b.win_words) + 3) / 4 * 4) * 4;
     const int g = gated ? 1 : 0;
     static bool attr_set[MAX_FIXED_K + 1] = {};
     if (cv.k >= 1 && cv.k <= (uint32_t)MAX_FIXED_K && !attr_set[cv.k]) {

@@ -85,6 +85,7 @@ struct alll_ctx {
     uint64_t bucket_min_u = 0;  // bucketed round 0 when the last pass found at least this many
     hipEvent_t ev[8] = {};
     int n_cu = 256;
+    int eval_wgs = 1;            // hybrid evaluation workgroups per CU (LDS window = LDS_WORDS / eval_wgs)
     bool hybrid = false;
     alll_exchange_fn xfn = nullptr;  // host-staged exchange (instead of RCCL)
     void* xuser = nullptr;
@@ -132,7 +133,7 @@ int write_limits(alll_ctx* c, uint64_t limit_eval, uint64_t limit_nores) {
 
 hipError_t eval_launch(alll_ctx* c, uint32_t tb, uint32_t te, bool gated) {
     if (c->hybrid) {
-        int grid = c->n_cu;
+        int grid = c->n_cu * c->eval_wgs;
         if (const char* e = getenv("ALLL_EVAL_GRID")) grid = atoi(e);  // tuning experiments
         return launch_eval_hybrid(c->cv, c->b, tb, te, gated, grid, c->stream);
     }
@@ -435,6 +436,8 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     LoopBuffers& b = c->b;
     b.n_vars = c->n_vars;
     b.n_words = (c->n_vars + 31) / 32;
+    if (const char* e = getenv("ALLL_EVAL_WGS")) c->eval_wgs = std::max(1, std::min(2, atoi(e)));  // tuning
+    b.win_words = LDS_WORDS / c->eval_wgs / 4 * 4;
     b.n_tiles = n_tiles;
     b.m = m;
     if (opt.stream_batch && m) {
@@ -584,13 +587,14 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
         // literals are stored by descending variable, so the gathers of slot 0 (and mostly
         // slot 1) of a wave hit a few cache lines.  perm[p] = original id of position p.
         //
-        // Windows (instances with more than LDS_VARS variables; ALLL_EVAL_WINDOWS=0/1 overrides):
-        // the hybrid evaluation's LDS holds LDS_VARS consecutive variables; clauses are first
+        // Windows (instances with more than win_vars variables; ALLL_EVAL_WINDOWS=0/1 overrides):
+        // the hybrid evaluation's LDS holds win_vars consecutive variables; clauses are first
         // grouped by the block of their smallest variable and each tile's LDS window starts at
         // its block, so the smallest variable (looked up by every clause) is an LDS hit.
         std::vector<uint32_t>& perm = c->perm;
         perm.resize(m);
-        bool windows = c->n_vars > LDS_VARS;
+        const uint64_t win_vars = (uint64_t)b.win_words * 32;
+        bool windows = c->n_vars > win_vars;
         if (const char* e = getenv("ALLL_EVAL_WINDOWS")) windows = atoi(e) != 0;  // tuning, tests
         {
             const int K = fixed_k;
@@ -603,7 +607,7 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
                     else if (v > b2) b2 = v;
                     lo = std::min(lo, v);
                 }
-                const uint64_t blk = windows ? lo / LDS_VARS : 0;
+                const uint64_t blk = windows ? lo / win_vars : 0;
                 return {(blk << 32) | a, b2, (uint32_t)cl};
             };
             auto sort_range = [&](uint64_t cb0, uint64_t ce0) {
@@ -643,7 +647,7 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
         cv.lits_t = d_t;
         cv.offs = nullptr;
         if (windows && m) {  // LDS window of every tile: the block of its first clause's smallest variable
-            const uint32_t lds_words = std::min<uint32_t>(b.n_words, LDS_WORDS);
+            const uint32_t lds_words = std::min<uint32_t>(b.n_words, b.win_words);
             std::vector<uint32_t> wb(n_tiles, 0u);
             for (uint32_t tt = 0; tt < n_tiles; ++tt) {
                 const uint64_t p = (uint64_t)tt * TILE;
@@ -651,7 +655,7 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
                 const uint64_t cl = perm[p];
                 uint32_t lo = ~0u;
                 for (int j = 0; j < fixed_k; ++j) lo = std::min(lo, prob->literals[cl * fixed_k + j] >> 1);
-                wb[tt] = std::min<uint64_t>((uint64_t)(lo / LDS_VARS) * LDS_WORDS, b.n_words - lds_words);
+                wb[tt] = std::min<uint64_t>((uint64_t)(lo / win_vars) * b.win_words, b.n_words - lds_words);
             }
             uint32_t* d_wb = nullptr;
             if ((rc = dalloc(c, &d_wb, n_tiles))) return bail(rc);

@@ -15,6 +15,7 @@
 //              (resample_clauses, SATInstance.h:340-365), one pass over the variables.
 // Integer / bit work only: no MFMA.  HBM-bound on the literal stream of k_eval.
 #include <algorithm>
+#include <atomic>
 
 #include "alll_internal.h"
 
@@ -2110,6 +2111,22 @@ hipError_t launch_eval(const ClauseView& cv, const LoopBuffers& b, uint32_t tile
     return hipGetLastError();
 }
 
+// Kernel attributes (dynamic LDS above the default) are per device: one bit per kernel group
+// and device records what is set (contexts on several devices may share a process).
+constexpr int ATTR_MAX_DEV = 64;
+static std::atomic<uint32_t> g_attr_done[ATTR_MAX_DEV];
+enum : uint32_t { ATTR_HYBRID = 0, ATTR_BUCKETS = 9, ATTR_RR = 18 };  // + k for per-width groups
+static bool attr_pending(uint32_t bit, int& dev) {
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= ATTR_MAX_DEV) {
+        dev = -1;
+        return true;
+    }
+    return !(g_attr_done[dev].load(std::memory_order_acquire) & (1u << bit));
+}
+static void attr_mark(uint32_t bit, int dev) {
+    if (dev >= 0) g_attr_done[dev].fetch_or(1u << bit, std::memory_order_release);
+}
+
 hipError_t launch_eval_hybrid(const ClauseView& cv, const LoopBuffers& b, uint32_t tile_begin,
                               uint32_t tile_end, bool gated, int n_blocks, hipStream_t s) {
     if (tile_end <= tile_begin) return hipSuccess;
@@ -2117,14 +2134,14 @@ hipError_t launch_eval_hybrid(const ClauseView& cv, const LoopBuffers& b, uint32
     const dim3 grid(std::min<uint32_t>(nt, (uint32_t)std::max(1, n_blocks)));
     const size_t lds = (size_t)std::max<uint32_t>(4, (std::min(b.n_words, b.win_words) + 3) / 4 * 4) * 4;
     const int g = gated ? 1 : 0;
-    static bool attr_set[MAX_FIXED_K + 1] = {};
-    if (cv.k >= 1 && cv.k <= (uint32_t)MAX_FIXED_K && !attr_set[cv.k]) {
+    int dev;
+    if (cv.k >= 1 && cv.k <= (uint32_t)MAX_FIXED_K && attr_pending(ATTR_HYBRID + cv.k, dev)) {
         hipError_t e = hipSuccess;
         ALLL_DISPATCH_K(cv.k, (e = hipFuncSetAttribute((const void*)k_eval_hybrid<(K > 0 ? K : 1)>,
                                                        hipFuncAttributeMaxDynamicSharedMemorySize,
                                                        (int)(LDS_WORDS * 4))));
         if (e != hipSuccess) return e;
-        attr_set[cv.k] = true;
+        attr_mark(ATTR_HYBRID + cv.k, dev);
     }
     switch (cv.k) {
         case 1: k_eval_hybrid<1><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g); break;
@@ -2182,8 +2199,8 @@ hipError_t launch_round0_buckets(const ClauseView& cv, const LoopBuffers& b, boo
     if (b.n_tiles == 0 || cv.k == 0 || !b.pairs) return hipErrorInvalidValue;
     const uint64_t run_cap = (uint64_t)b.run_tiles * TILE * cv.k;
     const size_t lds = (size_t)4 << b.bkt_shift;  // k_bresolve minima
-    static bool attr_set[MAX_FIXED_K + 1] = {};
-    if (!attr_set[cv.k]) {
+    int dev;
+    if (cv.k <= (uint32_t)MAX_FIXED_K && attr_pending(ATTR_BUCKETS + cv.k, dev)) {
         hipError_t e = hipFuncSetAttribute((const void*)k_bresolve, hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)(4u << BKT_SHIFT_MAX));
         if (e != hipSuccess) return e;
@@ -2195,7 +2212,7 @@ hipError_t launch_round0_buckets(const ClauseView& cv, const LoopBuffers& b, boo
                                                        hipFuncAttributeMaxDynamicSharedMemorySize,
                                                        (int)(RUN_TILES_MAX * TILE))));
         if (e != hipSuccess) return e;
-        attr_set[cv.k] = true;
+        attr_mark(ATTR_BUCKETS + cv.k, dev);
     }
     const int fr = fused_reduce ? 1 : 0;
     ALLL_DISPATCH_K(cv.k, (k_bscatter<(K > 0 ? K : 1)><<<b.n_runs + fr, BSC_THREADS, BKT_STAGE * 8, s>>>(
@@ -2218,15 +2235,15 @@ hipError_t launch_tail(const ClauseView& cv, const LoopBuffers& b, uint32_t firs
 
 hipError_t launch_rr_mis(const ClauseView& cv, const LoopBuffers& b, hipStream_t s) {
     if (cv.k != 0 || !b.rr_u || b.rr_T < 2 || b.rr_T > RR_TMAX) return hipErrorInvalidValue;
-    static bool attr_set = false;
-    if (!attr_set) {
+    int dev;
+    if (attr_pending(ATTR_RR, dev)) {
         hipError_t e = hipFuncSetAttribute((const void*)k_rr_mis<4, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                            (int)sizeof(RRLds));
         if (e == hipSuccess)
             e = hipFuncSetAttribute((const void*)k_rr_mis<8, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                     (int)sizeof(RRLds));
         if (e != hipSuccess) return e;
-        attr_set = true;
+        attr_mark(ATTR_RR, dev);
     }
     if (b.n_tiles) k_rr_entries<<<b.n_tiles, 256, 0, s>>>(cv, b);
     // clause variables held in registers while scanning: 4 for instances of width <= 4

@@ -58,7 +58,7 @@ struct DevState {
     uint64_t count_out;    // standalone eval count (verify / bench_eval)
     uint32_t done;         // 0 running, 1 solved, 2 stopped at limit_nores
     uint32_t active;       // the current iteration runs MIS + resample
-    uint32_t stamp;        // cover stamp of the current iteration (never 0)
+    uint32_t stamp;        // cover stamp of the current iteration: 1 .. 255, cycling (never 0)
     uint32_t round_base;   // owner-key epoch of grid round 0 of the current iteration
     uint32_t round_next;   // first unused epoch
     uint32_t tail_rounds;  // rounds the tail kernel needed in the last iteration
@@ -97,7 +97,8 @@ struct LoopBuffers {
     uint32_t* left;         // compact list of undecided entries handed to the tail kernel
     uint32_t* tmis;         // MIS clauses decided by the tail kernel
     unsigned long long* owner; // 2 x n_vars 64-bit owner keys, array = epoch parity (never reset)
-    uint32_t* cover;        // per variable: stamp of the iteration whose MIS covers it
+    uint8_t* cover;         // per variable: stamp of the iteration whose MIS covers it (the
+                            // reduce clears it when the stamp cycles back to 1)
     unsigned long long* tile_stats; // per tile: [2t] sum |MIS|, [2t+1] sum resampled literals
     uint32_t* delta;        // allreduce exchange: per-iteration assignment XOR delta
     DevState* state;

@@ -497,6 +497,12 @@ __device__ void reduce_body(const LoopBuffers& b, int mode) {
     __shared__ uint32_t s_first;  // first tile with a violated clause (streaming window)
     if (threadIdx.x == 0) { s_sum = 0; s_first = ~0u; }
     __syncthreads();
+    // 8-bit cover stamps cycle through 1 .. 255: when this iteration's stamp comes back to 1,
+    // the marks of the last 255 iterations are cleared first (once per 255 iterations)
+    if (mode == 0 && st->n_iter > 0 && st->n_iter % 255 == 0) {
+        uint4* cv4 = reinterpret_cast<uint4*>(b.cover);  // n_words * 32 bytes
+        for (uint32_t i = threadIdx.x; i < b.n_words * 2; i += blockDim.x) cv4[i] = make_uint4(0, 0, 0, 0);
+    }
     unsigned long long acc = 0;
     uint32_t first = ~0u;
     for (uint32_t t = threadIdx.x; t < b.n_tiles; t += blockDim.x) {
@@ -521,7 +527,7 @@ __device__ void reduce_body(const LoopBuffers& b, int mode) {
     st->u_total = u;
     st->left_cnt = 0;
     st->tmis_cnt = 0;
-    st->stamp = (uint32_t)st->n_iter ? (uint32_t)st->n_iter : 1u;
+    st->stamp = (uint32_t)((st->n_iter - 1) % 255) + 1u;
     st->round_base = st->round_next;
     st->round_next = st->round_base + 1;  // the tail advances it past every epoch it used
     if (u == 0) { st->done = 1; st->active = 0; }
@@ -685,7 +691,7 @@ __device__ __forceinline__ void join_tile(const ClauseView& cv, const LoopBuffer
         uint64_t lb;
         const uint32_t len = ent_len<K>(cv, e, lb);
         if (own(e, i, lb, len)) {
-            for (uint32_t j = 0; j < len; ++j) b.cover[lit_var(ent_lit<K>(cv, e, lb, j))] = stamp;
+            for (uint32_t j = 0; j < len; ++j) b.cover[lit_var(ent_lit<K>(cv, e, lb, j))] = (uint8_t)stamp;
             mis[atomicAdd(&s_join, 1u)] = c;
             my_lits += len;
             my_w += mis_weight(b, st, key);
@@ -830,7 +836,7 @@ __global__ __launch_bounds__(ROUND_THREADS) void k_wjoin(ClauseView cv, LoopBuff
                 for (uint32_t j = 0; j < len; ++j) own &= owner[lit_var(ent_lit<K>(cv, e, lb, j))] == (keyhi | kc);
                 keep = !own;
                 if (own) {
-                    for (uint32_t j = 0; j < len; ++j) b.cover[lit_var(ent_lit<K>(cv, e, lb, j))] = stamp;
+                    for (uint32_t j = 0; j < len; ++j) b.cover[lit_var(ent_lit<K>(cv, e, lb, j))] = (uint8_t)stamp;
                     lits += len;
                     w += mis_weight(b, st, kc);
                 }
@@ -1289,7 +1295,7 @@ __global__ __launch_bounds__(BJN_THREADS) void k_bjoin(ClauseView cv, LoopBuffer
             }
             if (own) {
 #pragma unroll
-                for (int j = 0; j < K; ++j) b.cover[lit_var(e[u].w[1 + j])] = stamp;
+                for (int j = 0; j < K; ++j) b.cover[lit_var(e[u].w[1 + j])] = (uint8_t)stamp;
                 b.mis[(uint64_t)tile * TILE + s_mis0[tt] + atomicAdd(&s_join[tt], 1u)] = e[u].w[0];
                 atomicAdd(&s_lits[tt], (unsigned long long)K);
             } else {
@@ -1396,7 +1402,7 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail(ClauseView cv, LoopBuffer
                                              __HIP_MEMORY_SCOPE_AGENT) == (keyhi | kc);
                 if (own) {
                     for (uint32_t j = 0; j < len; ++j)
-                        __hip_atomic_store(&b.cover[lit_var(ent_lit<K>(cv, e, lb, j))], stamp, __ATOMIC_RELAXED,
+                        __hip_atomic_store(&b.cover[lit_var(ent_lit<K>(cv, e, lb, j))], (uint8_t)stamp, __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_AGENT);
                     b.tmis[atomicAdd(&s_tm, 1u)] = c;
                     atomicAdd(&b.tile_stats[2 * (c / TILE)], mis_weight(b, st, kc));
@@ -1432,8 +1438,8 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail(ClauseView cv, LoopBuffer
 // exactly those with cover[v] == stamp.  Their new values come from one Philox draw per
 // assignment word: variable v takes bit v % 32 of Philox(seed, {v / 32, it_lo, 0, it_hi}).x
 // (it = resample round n_iter - 1; a variable repeated inside a clause is drawn once).  A lane
-// reads the stamps of 4 variables (one 16-byte load), 8 lanes OR their nibbles into a word's
-// covered mask, and the first of them draws and writes the word: no per-clause atomics.
+// reads the 8-bit stamps of 16 variables (one 16-byte load), 2 lanes OR their halves into a
+// word's covered mask, and the first of them draws and writes the word: no per-clause atomics.
 // n_resamples counts every literal (SATInstance.h:363) in the joins.
 __device__ __forceinline__ uint32_t resample_word(uint64_t seed, uint64_t it, uint32_t w) {
     return philox_x(w, (uint32_t)it, 0u, (uint32_t)(it >> 32), (uint32_t)seed, (uint32_t)(seed >> 32));
@@ -1445,19 +1451,20 @@ __global__ __launch_bounds__(256) void k_resample_vars(LoopBuffers b) {
     const uint32_t stamp = st->stamp;
     const uint64_t it = st->n_iter - 1;
     const int lane = threadIdx.x & 63;
-    const bool lead = (lane & 7) == 0;
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // variables 4t .. 4t+3
-    const uint32_t w = (uint32_t)(t >> 3);
+    const bool lead = (lane & 1) == 0;
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // variables 16t .. 16t+15
+    const uint32_t w = (uint32_t)(t >> 1);
     const bool live = w < b.n_words;  // (cover is padded to whole words with zeros)
     uint32_t a = 0;
     if (lead && live) a = b.A[w];
     uint4 c = make_uint4(0u, 0u, 0u, 0u);
     if (live) c = reinterpret_cast<const uint4*>(b.cover)[t];
-    uint32_t cm = ((uint32_t)(c.x == stamp) | ((uint32_t)(c.y == stamp) << 1) | ((uint32_t)(c.z == stamp) << 2) |
-                   ((uint32_t)(c.w == stamp) << 3)) << (4 * (lane & 7));
+    const uint32_t cs[4] = {c.x, c.y, c.z, c.w};
+    uint32_t cm = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) cm |= (uint32_t)(((cs[i >> 2] >> (8 * (i & 3))) & 0xFFu) == stamp) << i;
+    cm <<= 16 * (lane & 1);
     cm |= __shfl_xor(cm, 1, 64);
-    cm |= __shfl_xor(cm, 2, 64);
-    cm |= __shfl_xor(cm, 4, 64);
     if (lead && cm) b.A[w] = (a & ~cm) | (resample_word(b.seed, it, w) & cm);
 }
 
@@ -1998,7 +2005,7 @@ __global__ __launch_bounds__(RR_THREADS) void k_rr_mis(ClauseView cv, LoopBuffer
         for (uint32_t i = tid; i < RR_HASH; i += RR_THREADS) {
             const uint32_t k = L.hkey[i];
             if (k != RR_EMPTY && L.hmin[i] < trunc)
-                __hip_atomic_store(&b.cover[k], stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&b.cover[k], (uint8_t)stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             L.hkey[i] = RR_EMPTY;
             L.hmin[i] = RR_EMPTY;
             L.hgrp[i] = 0;
@@ -2006,7 +2013,7 @@ __global__ __launch_bounds__(RR_THREADS) void k_rr_mis(ClauseView cv, LoopBuffer
         if (L.wide) {
             const uint32_t c = L.cc[0], lb = cv.offs[c], w = cv.offs[c + 1] - lb;
             for (uint32_t j = tid; j < w; j += RR_THREADS)
-                __hip_atomic_store(&b.cover[lit_var(cv.lits[lb + j])], stamp, __ATOMIC_RELAXED,
+                __hip_atomic_store(&b.cover[lit_var(cv.lits[lb + j])], (uint8_t)stamp, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
         }
         for (uint32_t e = tid; e < B * cpg; e += RR_THREADS) {
@@ -2260,7 +2267,7 @@ hipError_t launch_resample(const ClauseView& cv, const LoopBuffers& b, uint32_t 
         return hipGetLastError();
     }
     if (b.n_vars == 0) return hipSuccess;
-    const uint64_t blocks = ((uint64_t)b.n_words * 8 + 255) / 256;  // a thread per 4 variables
+    const uint64_t blocks = ((uint64_t)b.n_words * 2 + 255) / 256;  // a thread per 16 variables
     if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
     k_resample_vars<<<(uint32_t)blocks, 256, 0, s>>>(b);
     return hipGetLastError();

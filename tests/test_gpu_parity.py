@@ -139,6 +139,27 @@ def test_trajectory_matches_oracle(gpu, oracle_mod, name, layout, monkeypatch):
         np.testing.assert_array_equal(s.assignment_words(), A_o)
 
 
+@pytest.mark.parametrize("layout", ["hybrid", "csr", "buckets"])
+def test_long_run_across_cover_stamp_cycles(gpu, oracle_mod, layout, monkeypatch):
+    """Cover marks are 8-bit stamps cycling through 1..255 (cleared at every wrap): a 600-
+    iteration run crosses two wraps and stays bit-exact (checkpoints around each wrap)."""
+    n, offs, lits = instances()["u2500_ratio4"]
+    seed, K = 7, 600
+    st_o, A_o, rows = oracle_mod.solve(n, offs, lits, seed, max_iters=K, trace=True)
+    assert st_o["solved"] == 0 and len(rows) >= K - 1
+    with make_solver(layout, monkeypatch, n, offs, lits, seed=seed) as s:
+        done = 0
+        for stop in (250, 254, 255, 256, 257, 509, 510, 511, 512, 599):
+            s.run(stop - done)
+            done = stop
+            np.testing.assert_array_equal(s.assignment_words(), rows[stop - 1][4], err_msg=f"A after {stop}")
+    with make_solver(layout, monkeypatch, n, offs, lits, seed=seed, max_iters=K) as s:
+        st = s.solve()
+        for k in ("n_iterations", "n_resamples", "avg_mis_size", "sum_mis_size", "solved"):
+            assert st[k] == st_o[k], k
+        np.testing.assert_array_equal(s.assignment_words(), A_o)
+
+
 def test_solve_converges_and_verifies(gpu, oracle_mod):
     from alllsatisfiabilitysolver_amd import Solver, generate_ksat
 

@@ -127,6 +127,21 @@ def test_rr_trajectory_matches_oracle(gpu, oracle_mod, name, T):
         np.testing.assert_array_equal(s.assignment_words(), A_o)
 
 
+def test_rr_long_run_across_cover_stamp_cycles(gpu, oracle_mod):
+    """600 iterations of the T = 4 round robin cross two wraps of the 8-bit cover stamps."""
+    from alllsatisfiabilitysolver_amd import Solver
+
+    n, offs, lits = _instance("ratio4")
+    seed, K, T = 31, 600, 4
+    st_o, A_o, _ = oracle_mod.solve(n, offs, lits, seed, max_iters=K, T=T)
+    assert st_o["solved"] == 0
+    with Solver(n, offs, lits, seed=seed, n_threads=T, max_iters=K) as s:
+        st = s.solve()
+        for k in ("n_iterations", "n_resamples", "avg_mis_size", "sum_mis_size", "solved"):
+            assert st[k] == st_o[k], k
+        np.testing.assert_array_equal(s.assignment_words(), A_o)
+
+
 def test_rr_caller_chunks(gpu, oracle_mod):
     """Chunk boundaries from the caller (the sizes of its vector<ClauseArray*>), including
     empty chunks at the front, middle and end."""

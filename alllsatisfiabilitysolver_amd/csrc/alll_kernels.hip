@@ -981,16 +981,14 @@ __global__ __launch_bounds__(BSC_THREADS) void k_bscatter(ClauseView cv, LoopBuf
     uint32_t tts[U], idx[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) ok[u] = false;  // threads past the last entry emit nothing
-    // pass 1: clause ids (written back), bucket histogram, hot claims
+    // pass 1: bucket histogram (variables only: it runs while the clause-id loads are in
+    // flight), clause ids (written back), hot claims
     for (uint32_t f0 = threadIdx.x; f0 < E; f0 += blockDim.x * U) {
         load_run_entries<K, U>(list, t0, nt, s_pre, E, f0, e, ok, tts, idx);
+        uint32_t id[U];
         if (cv.perm) {
 #pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (ok[u]) e[u].w[0] = cv.perm[e[u].w[0]];
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-                if (ok[u]) list[((uint64_t)(t0 + tts[u]) * TILE + idx[u]) * S] = e[u].w[0];
+            for (int u = 0; u < U; ++u) id[u] = ok[u] ? cv.perm[e[u].w[0]] : 0u;
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -998,8 +996,26 @@ __global__ __launch_bounds__(BSC_THREADS) void k_bscatter(ClauseView cv, LoopBuf
 #pragma unroll
             for (int j = 0; j < K; ++j) {
                 const uint32_t raw = e[u].w[1 + j];
-                if (hot && (raw & LIT_HOT)) ht.claim(lit_var(raw), keyhi | e[u].w[0]);
-                else atomicAdd(&s_hist[lit_var(raw) >> sh], 1u);
+                if (!(hot && (raw & LIT_HOT))) atomicAdd(&s_hist[lit_var(raw) >> sh], 1u);
+            }
+        }
+        if (cv.perm) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (!ok[u]) continue;
+                e[u].w[0] = id[u];
+                list[((uint64_t)(t0 + tts[u]) * TILE + idx[u]) * S] = id[u];
+            }
+        }
+        if (hot) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (!ok[u]) continue;
+#pragma unroll
+                for (int j = 0; j < K; ++j) {
+                    const uint32_t raw = e[u].w[1 + j];
+                    if (raw & LIT_HOT) ht.claim(lit_var(raw), keyhi | e[u].w[0]);
+                }
             }
         }
     }

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Development loop on one MI355X: parity tests, eval-kernel experiments, bench of config M.
+# Development loop on one MI355X: parity tests, then a bench line of config M.
 # usage: bash tools/gpu_iter.sh <tag> [pytest selection]
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 TAG=${1:-it}; SEL=${2:-tests/test_gpu_parity.py}
@@ -7,10 +7,6 @@ mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest $SEL -m gpu -x -q --timeout 120 --timeout-method thread \
     > gpurun_out/pytest_$TAG.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -4 gpurun_out/pytest_$TAG.log; [ $rc -eq 0 ] || exit $rc
-if [ -n "$EXPS" ]; then
-  timeout -k 10 300 python tools/eval_experiments.py > gpurun_out/evalexp_$TAG.log 2>&1
-  rc=$?; cat gpurun_out/evalexp_$TAG.log; [ $rc -eq 0 ] || exit $rc
-fi
 timeout -k 10 300 python bench.py --no-cpu-baseline > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err
 rc=$?; echo "bench rc=$rc"; python3 -c "
 import json,sys; d=json.load(open('gpurun_out/bench_$TAG.json'))

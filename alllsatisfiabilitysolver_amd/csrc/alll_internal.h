@@ -78,7 +78,14 @@ struct ClauseView {
     uint64_t m;             // clauses
     uint32_t k;             // fixed width, 0 = generic CSR
     uint32_t n_hot;         // variables flagged hot (bit 31 of their literals in `lits`)
-    const uint32_t* perm;   // fixed-k: evaluation position -> clause id (nullptr = identity)
+    const uint32_t* perm;   // fixed-k: evaluation position -> clause id (nullptr = identity or
+                            // ids packed into lits_t)
+    // Packed clause ids (fixed k): the literals of lits_t use their low id_shift bits, and
+    // slot j carries bits [j * id_bits, (j + 1) * id_bits) of the clause id above them (below
+    // the hot flag, bit 31), so that the evaluation emits clause ids without reading perm.
+    uint32_t lit_mask;      // lits_t literal bits (LIT_MASK when ids are not packed)
+    uint32_t id_shift;      // = bit width of the literals when packed
+    uint32_t id_bits;       // id bits per slot; 0 = not packed (entries carry positions)
 };
 
 struct LoopBuffers {

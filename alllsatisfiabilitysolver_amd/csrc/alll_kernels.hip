@@ -163,21 +163,43 @@ __global__ void k_init_assignment(uint32_t* A, uint32_t n_words, uint32_t n_vars
     A[w] = x;
 }
 
+// Entry of the clause at evaluation position p with lits_t slots t[0..K-1]: the clause id
+// (unpacked from the slots, or the position when ids are not packed; k_bscatter / CLAIM(0)
+// translate positions through perm) and the literals without the id bits.
+template <int K>
+__device__ __forceinline__ void make_ent(const ClauseView& cv, Ent<K>& e, uint64_t p, const uint32_t* t) {
+    if (cv.id_bits) {
+        const uint32_t fm = ((1u << cv.id_bits) - 1u) << cv.id_shift;
+        uint32_t id = 0;
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            id |= ((t[j] & fm) >> cv.id_shift) << (j * cv.id_bits);
+            e.w[1 + j] = t[j] & ~fm;
+        }
+        e.w[0] = id;
+    } else {
+        e.w[0] = (uint32_t)p;
+#pragma unroll
+        for (int j = 0; j < K; ++j) e.w[1 + j] = t[j];
+    }
+}
+
 // Writes the violated clauses of lane `lane` (four consecutive evaluation positions c0..c0+3,
 // literals x[j] component q) as entries into tile `tile`'s list at base + rank.
 template <int K>
-__device__ __forceinline__ void emit4(uint32_t* list, uint32_t pos, uint64_t c0, const bool v[4],
-                                      const uint4 (&x)[K]) {
+__device__ __forceinline__ void emit4(const ClauseView& cv, uint32_t* list, uint32_t pos, uint64_t c0,
+                                      const bool v[4], const uint4 (&x)[K]) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         if (!v[q]) continue;
-        Ent<K> e;
-        e.w[0] = (uint32_t)(c0 + q);
+        uint32_t t[K];
 #pragma unroll
         for (int j = 0; j < K; ++j) {
             const uint32_t xs[4] = {x[j].x, x[j].y, x[j].z, x[j].w};
-            e.w[1 + j] = xs[q];
+            t[j] = xs[q];
         }
+        Ent<K> e;
+        make_ent<K>(cv, e, c0 + q, t);
         store_ent<K>(list + (uint64_t)pos * Ent<K>::S, e);
         ++pos;
     }
@@ -219,7 +241,7 @@ __global__ __launch_bounds__(EVAL_THREADS) void k_eval_fixed(ClauseView cv, Loop
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     if (j > 0 && sat[q]) continue;
-                    const uint32_t l = xs[q] & LIT_MASK;
+                    const uint32_t l = xs[q] & cv.lit_mask;
                     sat[q] |= abit(A, l >> 1) ^ (l & 1u);
                 }
             }
@@ -235,7 +257,7 @@ __global__ __launch_bounds__(EVAL_THREADS) void k_eval_fixed(ClauseView cv, Loop
             if (lane == 0) base = atomicAdd(&s_cnt, tot);
             base = __shfl(base, 0, 64);
             const uint32_t pre = __popcll(b0 & lt) + __popcll(b1 & lt) + __popcll(b2 & lt) + __popcll(b3 & lt);
-            emit4<K>(list, base + pre, c0, v, x);
+            emit4<K>(cv, list, base + pre, c0, v, x);
         }
     }
     __syncthreads();
@@ -335,7 +357,7 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
                     bool need[4], useg[4];
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
-                        wi[q] = (xs[q] & LIT_MASK) >> 6;
+                        wi[q] = (xs[q] & cv.lit_mask) >> 6;
                         need[q] = first || !sat[q];
                         useg[q] = need[q] && wi[q] - wb >= lds_words;  // (unsigned: below the window too)
                     }
@@ -374,7 +396,7 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
                 base = __shfl(base, 0, 64);
                 const uint32_t pre = __popcll(b0 & lt) + __popcll(b1 & lt) + __popcll(b2 & lt) +
                                      __popcll(b3 & lt);
-                emit4<K>(b.stage[0] + (uint64_t)tile * TILE * Ent<K>::S, base + pre, c0, v, x);
+                emit4<K>(cv, b.stage[0] + (uint64_t)tile * TILE * Ent<K>::S, base + pre, c0, v, x);
             }
         }
       }
@@ -472,11 +494,14 @@ __global__ __launch_bounds__(EVAL_THREADS) void k_collect(ClauseView cv, LoopBuf
         // (k_eval_* store their four ballots as they are); CSR: positions 64 * w + bit
         const uint64_t p = K > 0 ? (w >> 2) * CHUNK + 4u * i + (w & 3u) : w * 64 + i;
         Ent<K> e;
-        e.w[0] = (uint32_t)p;
         if constexpr (K > 0) {
-            const uint32_t* t = cv.lits_t + (p / CHUNK) * CHUNK * K + (p % CHUNK);
+            const uint32_t* tp = cv.lits_t + (p / CHUNK) * CHUNK * K + (p % CHUNK);
+            uint32_t t[K];
 #pragma unroll
-            for (int j = 0; j < K; ++j) e.w[1 + j] = t[j * CHUNK];
+            for (int j = 0; j < K; ++j) t[j] = tp[j * CHUNK];
+            make_ent<K>(cv, e, p, t);
+        } else {
+            e.w[0] = (uint32_t)p;
         }
         store_ent<K>(list + (uint64_t)pos * Ent<K>::S, e);
         ++pos;

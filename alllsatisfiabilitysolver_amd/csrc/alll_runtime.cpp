@@ -539,6 +539,7 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     ClauseView& cv = c->cv;
     cv.m = m;
     cv.k = (uint32_t)fixed_k;
+    cv.lit_mask = 0x7FFFFFFFu;  // (bit 31: hot-variable flag)
     uint32_t *d_lits = nullptr, *d_t = nullptr, *d_o = nullptr;
     const uint64_t real_chunks = (m + CHUNK - 1) / CHUNK;
     if ((rc = dalloc(c, &d_lits, L))) return bail(rc);
@@ -626,24 +627,50 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
             }
             for (auto& t : th) t.join();
         }
+        // Packed clause ids: when the literals leave enough bits below the hot flag, slot j of
+        // every clause also carries bits [j * id_bits, (j + 1) * id_bits) of its clause id, so
+        // the evaluation emits clause ids and perm is never read on the device
+        // (ALLL_PACKED_IDS=0 keeps positions + perm; tuning, tests).
+        {
+            const uint64_t max_lit = 2ull * std::max<uint64_t>(c->n_vars, 1) - 1;
+            // (at least 6: the evaluation takes a variable's bit index from literal bits 1..5
+            // without masking)
+            const uint32_t lit_bits = std::max<uint32_t>(6, 64 - (uint32_t)__builtin_clzll(max_lit));
+            const uint32_t spare = lit_bits < 31 ? 31 - lit_bits : 0;
+            const uint32_t idb = m > 1 ? 64 - (uint32_t)__builtin_clzll(m - 1) : 1;
+            const uint32_t per = (idb + fixed_k - 1) / fixed_k;
+            bool pack = per <= spare;
+            if (const char* e = getenv("ALLL_PACKED_IDS")) pack = pack && atoi(e) != 0;
+            if (pack) {
+                cv.id_shift = lit_bits;
+                cv.id_bits = per;
+                cv.lit_mask = (1u << lit_bits) - 1u;
+            }
+        }
         std::vector<uint32_t> t(real_chunks * CHUNK * fixed_k, 0u);
         std::vector<uint32_t> tmp(fixed_k);
+        const uint32_t id_mask = cv.id_bits ? (1u << cv.id_bits) - 1u : 0u;
         for (uint64_t p2 = 0; p2 < m; ++p2) {
             const uint64_t cl = perm[p2];
             for (int j = 0; j < fixed_k; ++j)
                 tmp[j] = flagged.empty() ? prob->literals[cl * fixed_k + j] : flagged[cl * fixed_k + j];
             std::sort(tmp.begin(), tmp.end(), [](uint32_t x, uint32_t y) { return (x >> 1) > (y >> 1); });
             const uint64_t g = p2 / CHUNK, r = p2 % CHUNK;
-            for (int j = 0; j < fixed_k; ++j) t[(g * fixed_k + j) * CHUNK + r] = tmp[j];
+            for (int j = 0; j < fixed_k; ++j) {
+                const uint32_t idp = cv.id_bits ? ((uint32_t)(cl >> (j * cv.id_bits)) & id_mask) << cv.id_shift : 0u;
+                t[(g * fixed_k + j) * CHUNK + r] = tmp[j] | idp;
+            }
         }
         if (!t.empty() && hipMemcpy(d_t, t.data(), t.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
             return bail(fail(ALLL_ERR_HIP, "transposed literal upload failed"));
-        uint32_t* d_perm = nullptr;
-        if ((rc = dalloc(c, &d_perm, m))) return bail(rc);
-        if (hipStreamSynchronize(c->stream) != hipSuccess ||
-            hipMemcpy(d_perm, perm.data(), m * 4, hipMemcpyHostToDevice) != hipSuccess)
-            return bail(fail(ALLL_ERR_HIP, "permutation upload failed"));
-        cv.perm = d_perm;
+        if (!cv.id_bits) {
+            uint32_t* d_perm = nullptr;
+            if ((rc = dalloc(c, &d_perm, m))) return bail(rc);
+            if (hipStreamSynchronize(c->stream) != hipSuccess ||
+                hipMemcpy(d_perm, perm.data(), m * 4, hipMemcpyHostToDevice) != hipSuccess)
+                return bail(fail(ALLL_ERR_HIP, "permutation upload failed"));
+            cv.perm = d_perm;
+        }
         cv.lits_t = d_t;
         cv.offs = nullptr;
         if (windows && m) {  // LDS window of every tile: the block of its first clause's smallest variable

@@ -24,7 +24,8 @@ T1_FIXTURES = sorted(p for p in glob.glob(os.path.join(GOLDEN, "*_T1.npz")))
 # name -> (flags, environment at create): the default policy picks the bucketed LFMIS round 0
 # only for large violated sets, "buckets" forces it for every iteration
 LAYOUTS = {"hybrid": (0, {}), "fixed": (1 << 3, {}), "csr": (1 << 2, {}), "atomic_claims": (1 << 5, {}),
-           "buckets": (0, {"ALLL_BUCKET_MIN_U": "0"}), "windows": (0, {"ALLL_EVAL_WINDOWS": "1"})}
+           "buckets": (0, {"ALLL_BUCKET_MIN_U": "0"}), "windows": (0, {"ALLL_EVAL_WINDOWS": "1"}),
+           "positions": (0, {"ALLL_PACKED_IDS": "0"})}
 
 
 def make_solver(layout, monkeypatch, *args, **kw):
@@ -139,7 +140,7 @@ def test_trajectory_matches_oracle(gpu, oracle_mod, name, layout, monkeypatch):
         np.testing.assert_array_equal(s.assignment_words(), A_o)
 
 
-@pytest.mark.parametrize("layout", ["hybrid", "csr", "buckets"])
+@pytest.mark.parametrize("layout", ["hybrid", "csr", "buckets", "positions"])
 def test_long_run_across_cover_stamp_cycles(gpu, oracle_mod, layout, monkeypatch):
     """Cover marks are 8-bit stamps cycling through 1..255 (cleared at every wrap): a 600-
     iteration run crosses two wraps and stays bit-exact (checkpoints around each wrap)."""
@@ -265,6 +266,7 @@ BIG = {
     "C5_powerlaw_10M": (2_500_000, 10_000_000, 3, 1),
     "W_3sat_4Mvars": (4_000_000, 2_000_000, 3, 0),  # 4 LDS blocks of variables: windowed eval
     "M_no_windows": (2_500_000, 10_000_000, 3, 0, {"ALLL_EVAL_WINDOWS": "0"}),
+    "M_positions": (2_500_000, 10_000_000, 3, 0, {"ALLL_PACKED_IDS": "0"}),  # perm translation
 }
 
 

@@ -103,7 +103,7 @@ struct LoopBuffers {
     uint32_t* mis;          // per tile: TILE slots of MIS clause ids
     uint32_t* left;         // compact list of undecided entries handed to the tail kernel
     uint32_t* tmis;         // MIS clauses decided by the tail kernel
-    unsigned long long* owner; // 2 x n_vars 64-bit owner keys, array = epoch parity (never reset)
+    unsigned long long* owner; // n_vars 64-bit owner keys (epoch-tagged, never reset)
     uint8_t* cover;         // per variable: stamp of the iteration whose MIS covers it (the
                             // reduce clears it when the stamp cycles back to 1)
     unsigned long long* tile_stats; // per tile: [2t] sum |MIS|, [2t+1] sum resampled literals

@@ -625,10 +625,10 @@ struct HotTable {
     }
 };
 
-// Claims of epoch e go to owner array e & 1 (kept separate so that a future fused
-// join(r)+claim(r+1) kernel never reads an array it writes).
-__device__ __forceinline__ unsigned long long* owner_of(const LoopBuffers& b, uint32_t epoch) {
-    return b.owner + (uint64_t)(epoch & 1u) * b.n_vars;
+// One owner array for every epoch: JOIN(r) and CLAIM(r+1) are separated by a kernel boundary
+// (or, in the tail, a workgroup barrier), and keys of later epochs are always smaller.
+__device__ __forceinline__ unsigned long long* owner_of(const LoopBuffers& b, uint32_t /*epoch*/) {
+    return b.owner;
 }
 
 template <int K>

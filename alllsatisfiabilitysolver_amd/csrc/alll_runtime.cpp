@@ -477,7 +477,7 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     if ((rc = dalloc(c, &b.mis, (size_t)n_tiles * TILE))) return bail(rc);
     if ((rc = dalloc(c, &b.left, (size_t)n_tiles * TILE * ent_words))) return bail(rc);
     if ((rc = dalloc(c, &b.tmis, (size_t)n_tiles * TILE))) return bail(rc);
-    if ((rc = dalloc(c, &b.owner, 2 * (size_t)c->n_vars, 0xFF))) return bail(rc);
+    if ((rc = dalloc(c, &b.owner, (size_t)c->n_vars, 0xFF))) return bail(rc);
     if ((rc = dalloc(c, &b.cover, (size_t)b.n_words * 32))) return bail(rc);  // whole words, zero-padded
     if ((rc = dalloc(c, &b.tile_stats, 2 * (size_t)n_tiles))) return bail(rc);
     if ((rc = dalloc(c, &b.delta, b.n_words))) return bail(rc);

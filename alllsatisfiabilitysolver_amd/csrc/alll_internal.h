@@ -30,7 +30,7 @@ constexpr uint32_t RANGED_MAX_TILES = 16;          // tiles per block pass (64-b
 constexpr uint32_t MAX_TAIL_ROUNDS = 1u << 20;
 // Bucketed LFMIS round 0 (fixed width K): every claim of round 0 becomes a 64-bit pair
 // {clause id:32 | lose:1 | entry index in its run:16 | variable offset in its bucket:15},
-// written grouped by variable bucket (2^bkt_shift variables) inside its run (run_tiles
+// written grouped by variable bucket (bkt_width variables) inside its run (run_tiles
 // consecutive tiles); per-bucket minima are then resolved in LDS instead of by global atomics.
 constexpr uint32_t BKT_MAX = 4096;            // buckets (LDS histogram of k_bscatter)
 constexpr uint32_t BKT_SHIFT_MIN = 10;
@@ -116,7 +116,9 @@ struct LoopBuffers {
     const uint32_t* win_base;   // hybrid eval: per tile, first assignment word of its LDS window
                                 // (nullptr: words [0, win_words) for every tile)
     uint32_t win_words;         // hybrid eval: LDS window size in words (<= LDS_WORDS)
-    uint32_t bkt_shift;         // bucket = variable >> bkt_shift
+    uint32_t bkt_width;         // bucket = variable / bkt_width (<= 2^BKT_SHIFT_MAX)
+    uint32_t bkt_magic;         // floor(2^32 / bkt_width): bucket by multiply-high
+    uint32_t n_cu;              // compute units of the device
     uint32_t n_bkt;
     uint32_t run_tiles;
     uint32_t n_runs;

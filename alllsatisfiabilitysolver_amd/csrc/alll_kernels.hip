@@ -911,6 +911,16 @@ __device__ __forceinline__ unsigned long long make_pair(uint32_t c, uint32_t el,
     return ((unsigned long long)c << 32) | ((unsigned long long)el << 15) | vl;
 }
 
+// Variable bucket of the bucketed round 0: v / bkt_width by multiply-high (the estimate is
+// at most one low for v < 2^32, one correction step), and v's offset in the bucket.
+__device__ __forceinline__ uint32_t bucket_of(const LoopBuffers& b, uint32_t v, uint32_t& off) {
+    uint32_t q = __umulhi(v, b.bkt_magic);
+    uint32_t r = v - q * b.bkt_width;
+    if (r >= b.bkt_width) { ++q; r -= b.bkt_width; }
+    off = r;
+    return q;
+}
+
 // Run-local entry index f -> (tile of the run, index in that tile); pre = prefix of the
 // run's tile counts (<= RUN_TILES_MAX + 1 entries, in LDS).
 __device__ __forceinline__ uint32_t run_tile_of(const uint32_t* pre, uint32_t nt, uint32_t f) {
@@ -994,7 +1004,7 @@ __global__ __launch_bounds__(BSC_THREADS) void k_bscatter(ClauseView cv, LoopBuf
     HotTable ht{s_hk, s_hv};
     const bool hot = cv.n_hot != 0;
     if (hot) ht.init();
-    const uint32_t nb = b.n_bkt, sh = b.bkt_shift;
+    const uint32_t nb = b.n_bkt;
     for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) s_hist[i] = 0;
     dbg_stamp(b, 0, 0);
     const uint32_t E = run_prefix(b, t0, nt, s_tc, s_pre);
@@ -1021,7 +1031,8 @@ __global__ __launch_bounds__(BSC_THREADS) void k_bscatter(ClauseView cv, LoopBuf
 #pragma unroll
             for (int j = 0; j < K; ++j) {
                 const uint32_t raw = e[u].w[1 + j];
-                if (!(hot && (raw & LIT_HOT))) atomicAdd(&s_hist[lit_var(raw) >> sh], 1u);
+                uint32_t off;
+                if (!(hot && (raw & LIT_HOT))) atomicAdd(&s_hist[bucket_of(b, lit_var(raw), off)], 1u);
             }
         }
         if (cv.perm) {
@@ -1080,7 +1091,6 @@ __global__ __launch_bounds__(BSC_THREADS) void k_bscatter(ClauseView cv, LoopBuf
     // written with whole-line stores
     unsigned long long* gpr = b.pairs + (uint64_t)r * b.run_tiles * TILE * K;
     const bool staged = total <= BKT_STAGE;
-    const uint32_t vmask = (1u << sh) - 1u;
     auto emit = [&]() {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -1091,8 +1101,9 @@ __global__ __launch_bounds__(BSC_THREADS) void k_bscatter(ClauseView cv, LoopBuf
                 const uint32_t raw = e[u].w[1 + j];
                 if (hot && (raw & LIT_HOT)) continue;
                 const uint32_t v = lit_var(raw);
-                const uint32_t pos = atomicAdd(&s_hist[v >> sh], 1u);
-                const unsigned long long x = make_pair(e[u].w[0], el, v & vmask);
+                uint32_t off;
+                const uint32_t pos = atomicAdd(&s_hist[bucket_of(b, v, off)], 1u);
+                const unsigned long long x = make_pair(e[u].w[0], el, off);
                 if (staged) s_pairs[pos] = x;
                 else gpr[pos] = x;
             }
@@ -1124,10 +1135,13 @@ __global__ __launch_bounds__(BSC_THREADS) void k_bscatter(ClauseView cv, LoopBuf
 // not its variable's minimum: a segment's pairs are contiguous, so these are whole-line stores.
 constexpr uint32_t BKT_RUN_BATCH = 1024;
 constexpr int BRS_THREADS = 512;
-constexpr int BRS_UNROLL = 16;  // one sweep covers 8192 pairs (~7.4k per bucket at 10M clauses)
+// Items per thread and sweep: 20 (10240 pairs: ~8.9k per bucket at 10M clauses with one bucket
+// per CU; 150 VGPRs, one workgroup per CU), or 16 (8192 pairs; two workgroups per CU) when
+// there are more buckets than CUs.
+constexpr int BRS_UNROLL_WIDE = 20, BRS_UNROLL_NARROW = 16;
 
 struct ResolveLds {
-    uint32_t* min;          // 1 << bkt_shift
+    uint32_t* min;          // bkt_width
     uint32_t* start;        // batch: segment start in the run area
     uint32_t* pre;          // batch: exclusive prefix of segment lengths (pre[nr] = total)
     uint32_t* wsum;
@@ -1182,29 +1196,31 @@ __device__ __forceinline__ uint32_t resolve_pos(const ResolveLds& L, uint32_t rb
     return (rb + lo) * run_cap + L.start[lo] + (f - L.pre[lo]);
 }
 
-// One unrolled sweep over the batch items f0 + 64 u (u < BRS_UNROLL): positions and pairs
+// One unrolled sweep over the batch items f0 + 64 u (u < U): positions and pairs
 // (items past np load the batch's last pair again; callers ignore them).
+template <int U>
 __device__ __forceinline__ void resolve_load(const LoopBuffers& b, const ResolveLds& L, uint32_t rb, uint32_t nr,
                                              uint32_t np, uint32_t f0, uint32_t run_cap, uint32_t* pos,
                                              unsigned long long* x) {
 #pragma unroll
-    for (int u = 0; u < BRS_UNROLL; ++u) pos[u] = resolve_pos(L, rb, nr, min(f0 + 64 * u, np - 1), run_cap);
+    for (int u = 0; u < U; ++u) pos[u] = resolve_pos(L, rb, nr, min(f0 + 64 * u, np - 1), run_cap);
 #pragma unroll
-    for (int u = 0; u < BRS_UNROLL; ++u) x[u] = b.pairs[pos[u]];
+    for (int u = 0; u < U; ++u) x[u] = b.pairs[pos[u]];
 }
 
 __device__ __forceinline__ unsigned long long resolve_mark(const ResolveLds& L, unsigned long long x) {
     return L.min[(uint32_t)x & 0x7FFFu] != (uint32_t)(x >> 32) ? (x | PAIR_LOSE) : x;
 }
 
-__global__ __launch_bounds__(BRS_THREADS, 2) void k_bresolve(LoopBuffers b, uint32_t run_cap) {
+template <int U>
+__global__ __launch_bounds__(BRS_THREADS, U <= BRS_UNROLL_NARROW ? 2 : 1) void k_bresolve(LoopBuffers b,
+                                                                                          uint32_t run_cap) {
     if (!b.state->active) return;
-    constexpr int U = BRS_UNROLL;
     extern __shared__ uint32_t s_min[];
     __shared__ uint32_t s_start[BKT_RUN_BATCH], s_pre[BKT_RUN_BATCH + 1];
     __shared__ uint32_t s_wsum[BRS_THREADS / 64];
-    __shared__ uint16_t s_seg[BRS_THREADS * BRS_UNROLL];  // single sweep: item -> segment
-    const uint32_t bv = 1u << b.bkt_shift;
+    __shared__ uint16_t s_seg[BRS_THREADS * U];  // single sweep: item -> segment
+    const uint32_t bv = b.bkt_width;
     ResolveLds L{s_min, s_start, s_pre, s_wsum};
     dbg_stamp(b, 1, 0);
     for (uint32_t i = threadIdx.x; i < bv; i += blockDim.x) L.min[i] = ~0u;
@@ -1232,8 +1248,8 @@ __global__ __launch_bounds__(BRS_THREADS, 2) void k_bresolve(LoopBuffers b, uint
 #pragma unroll
                 for (int u = 0; u < U; ++u) x[u] = b.pairs[pos[u]];
 #pragma unroll
-                for (int u = 0; u < U; ++u)  // a clamped duplicate of the last pair is harmless
-                    atomicMin(&L.min[(uint32_t)x[u] & 0x7FFFu], (uint32_t)(x[u] >> 32));
+                for (int u = 0; u < U; ++u)  // (clamped duplicates of the last pair would serialise)
+                    if (first + 64 * u < np) atomicMin(&L.min[(uint32_t)x[u] & 0x7FFFu], (uint32_t)(x[u] >> 32));
             }
             dbg_stamp(b, 1, 2);
             __syncthreads();
@@ -1253,10 +1269,12 @@ __global__ __launch_bounds__(BRS_THREADS, 2) void k_bresolve(LoopBuffers b, uint
             const uint32_t nr = min(BKT_RUN_BATCH, b.n_runs - rb);
             const uint32_t np = resolve_batch(b, L, rb, nr);
             for (uint32_t f0 = first; f0 < np; f0 += stride) {
-                resolve_load(b, L, rb, nr, np, f0, run_cap, pos, x);
+                resolve_load<U>(b, L, rb, nr, np, f0, run_cap, pos, x);
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
-                    if (pass == 0) atomicMin(&L.min[(uint32_t)x[u] & 0x7FFFu], (uint32_t)(x[u] >> 32));
+                    if (pass == 0) {
+                        if (f0 + 64 * u < np) atomicMin(&L.min[(uint32_t)x[u] & 0x7FFFu], (uint32_t)(x[u] >> 32));
+                    }
                     else if (f0 + 64 * u < np) b.pairs[pos[u]] = resolve_mark(L, x[u]);
                 }
             }
@@ -2246,11 +2264,14 @@ hipError_t launch_round0_buckets(const ClauseView& cv, const LoopBuffers& b, boo
     // buffers as CLAIM(0) + JOIN(0): eval -> stage[0] (ids translated in place); JOIN stage[0] -> stage[1]
     if (b.n_tiles == 0 || cv.k == 0 || !b.pairs) return hipErrorInvalidValue;
     const uint64_t run_cap = (uint64_t)b.run_tiles * TILE * cv.k;
-    const size_t lds = (size_t)4 << b.bkt_shift;  // k_bresolve minima
+    const size_t lds = (size_t)4 * b.bkt_width;  // k_bresolve minima
     int dev;
     if (cv.k <= (uint32_t)MAX_FIXED_K && attr_pending(ATTR_BUCKETS + cv.k, dev)) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_bresolve, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)(4u << BKT_SHIFT_MAX));
+        hipError_t e = hipFuncSetAttribute((const void*)k_bresolve<BRS_UNROLL_WIDE>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)(4u << BKT_SHIFT_MAX));
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute((const void*)k_bresolve<BRS_UNROLL_NARROW>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)(4u << BKT_SHIFT_MAX));
         if (e != hipSuccess) return e;
         ALLL_DISPATCH_K(cv.k, (e = hipFuncSetAttribute((const void*)k_bscatter<(K > 0 ? K : 1)>,
                                                        hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -2267,7 +2288,8 @@ hipError_t launch_round0_buckets(const ClauseView& cv, const LoopBuffers& b, boo
                               cv, b, b.stage[0], fr)));
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    k_bresolve<<<b.n_bkt, BRS_THREADS, lds, s>>>(b, (uint32_t)run_cap);
+    if (b.n_bkt <= b.n_cu) k_bresolve<BRS_UNROLL_WIDE><<<b.n_bkt, BRS_THREADS, lds, s>>>(b, (uint32_t)run_cap);
+    else k_bresolve<BRS_UNROLL_NARROW><<<b.n_bkt, BRS_THREADS, lds, s>>>(b, (uint32_t)run_cap);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     const int l = last ? 1 : 0;

@@ -406,6 +406,11 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     alll_ctx* c = new (std::nothrow) alll_ctx();
     if (!c) return fail(ALLL_ERR_OOM, "host allocation failed");
     c->device = dev;
+    {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0)
+            c->n_cu = prop.multiProcessorCount;
+    }
     c->opt = opt;
     c->n_vars = prob->n_vars;
     c->m = m;
@@ -438,6 +443,7 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     b.n_words = (c->n_vars + 31) / 32;
     if (const char* e = getenv("ALLL_EVAL_WGS")) c->eval_wgs = std::max(1, std::min(2, atoi(e)));  // tuning
     b.win_words = LDS_WORDS / c->eval_wgs / 4 * 4;
+    b.n_cu = (uint32_t)c->n_cu;
     b.n_tiles = n_tiles;
     b.m = m;
     if (opt.stream_batch && m) {
@@ -498,13 +504,17 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     if (getenv("ALLL_DEBUG_PHASES")) {  // diagnostics only
         if ((rc = dalloc(c, &b.kdbg, (size_t)DBG_KERNELS * DBG_BLOCKS * DBG_FIELDS))) return bail(rc);
     }
-    // ---- bucketed LFMIS round 0 (fixed width): ~300 buckets, runs of up to 16 tiles
+    // ---- bucketed LFMIS round 0 (fixed width): one bucket per CU when a bucket's minima fit
+    // in LDS (else ~300-1000 power-of-2 buckets), runs of up to 16 tiles
     if (fixed_k > 0 && !(opt.flags & ALLL_FLAG_ATOMIC_CLAIMS) && n_tiles > 0 && c->n_vars > 0) {
         uint32_t shift = BKT_SHIFT_MIN;
         while (shift < BKT_SHIFT_MAX && ((uint64_t)c->n_vars >> shift) > 384) ++shift;
+        uint64_t width = ((uint64_t)c->n_vars + c->n_cu - 1) / c->n_cu;
+        width = std::max<uint64_t>(width, 1u << BKT_SHIFT_MIN);
+        if (width > (1u << BKT_SHIFT_MAX) || getenv("ALLL_BKT_POW2")) width = 1u << shift;
         if (const char* e = getenv("ALLL_BKT_SHIFT"))  // tuning experiments
-            shift = std::min<uint32_t>(BKT_SHIFT_MAX, std::max<uint32_t>(BKT_SHIFT_MIN, (uint32_t)atoi(e)));
-        const uint64_t nb = ((uint64_t)c->n_vars + (1u << shift) - 1) >> shift;
+            width = 1u << std::min<uint32_t>(BKT_SHIFT_MAX, std::max<uint32_t>(BKT_SHIFT_MIN, (uint32_t)atoi(e)));
+        const uint64_t nb = ((uint64_t)c->n_vars + width - 1) / width;
         // skewed literal distribution (power-law hubs): the fullest bucket's workgroup would
         // serialise the round; such instances keep the atomic claims (with hot-variable
         // aggregation), which handle skew better
@@ -512,7 +522,7 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
         if (nb <= BKT_MAX) {
             std::vector<uint64_t> load(nb, 0);
             const uint64_t L_all = prob->offsets[m];
-            for (uint64_t j = 0; j < L_all; ++j) ++load[(prob->literals[j] >> 1) >> shift];
+            for (uint64_t j = 0; j < L_all; ++j) ++load[(prob->literals[j] >> 1) / width];
             const uint64_t mx = *std::max_element(load.begin(), load.end());
             skewed = mx > 4 * (L_all / nb + 1);
         }
@@ -522,7 +532,8 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
             rt = std::max<uint32_t>(1, std::min<uint32_t>(RUN_TILES_MAX, (uint32_t)atoi(e)));
         const uint64_t area = (uint64_t)((n_tiles + rt - 1) / rt) * rt * TILE * fixed_k;  // pairs
         if (nb <= BKT_MAX && !skewed && area < (1ull << 32)) {  // pair positions are 32-bit in k_bresolve
-            b.bkt_shift = shift;
+            b.bkt_width = (uint32_t)width;
+            b.bkt_magic = (uint32_t)((1ull << 32) / width);
             b.n_bkt = (uint32_t)nb;
             b.run_tiles = rt;
             b.n_runs = (n_tiles + b.run_tiles - 1) / b.run_tiles;
@@ -724,11 +735,6 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     }
     if (hipStreamSynchronize(c->stream) != hipSuccess)
         return bail(fail(ALLL_ERR_HIP, "create: stream sync failed: %s", hipGetErrorString(hipGetLastError())));
-    {
-        hipDeviceProp_t prop;
-        if (hipGetDeviceProperties(&prop, dev) == hipSuccess && prop.multiProcessorCount > 0)
-            c->n_cu = prop.multiProcessorCount;
-    }
     c->hybrid = cv.k > 0 && !(opt.flags & ALLL_FLAG_NO_RANGED);
     char nm[64];
     if (c->hybrid) snprintf(nm, sizeof nm, "k_eval_hybrid<%u>", cv.k);

@@ -267,6 +267,8 @@ BIG = {
     "W_3sat_4Mvars": (4_000_000, 2_000_000, 3, 0),  # 4 LDS blocks of variables: windowed eval
     "M_no_windows": (2_500_000, 10_000_000, 3, 0, {"ALLL_EVAL_WINDOWS": "0"}),
     "M_positions": (2_500_000, 10_000_000, 3, 0, {"ALLL_PACKED_IDS": "0"}),  # perm translation
+    # 611 power-of-2 buckets (more than CUs): the narrow k_bresolve, two workgroups per CU
+    "M_pow2_buckets": (2_500_000, 10_000_000, 3, 0, {"ALLL_BKT_SHIFT": "12"}),
 }
 
 

@@ -16,7 +16,7 @@ constexpr int ROUND_THREADS = 256;
 constexpr int TAIL_THREADS = 1024;
 constexpr uint32_t WAVE_ROUND_MIN = 2;       // grid rounds from here on run a wave per tile
 constexpr int MAX_FIXED_K = 8;
-// Persistent hybrid evaluation: assignment words of the first LDS_VARS variables in LDS.
+// Persistent hybrid evaluation: LDS window of at most LDS_VARS variables' assignment words.
 constexpr uint32_t LDS_WORDS = 38912;              // 152 KiB of LDS
 constexpr uint32_t LDS_VARS = LDS_WORDS * 32;      // 1,245,184 variables
 constexpr int HYB_THREADS = 1024;

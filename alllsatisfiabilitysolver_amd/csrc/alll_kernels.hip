@@ -270,9 +270,10 @@ __global__ __launch_bounds__(EVAL_THREADS) void k_eval_fixed(ClauseView cv, Loop
 
 // Clause evaluation, fixed width K, persistent hybrid (the loop's default for fixed k).
 // One 1024-thread workgroup per CU owns a contiguous run of tiles.  The assignment words of
-// the first min(n, LDS_VARS) variables are staged once in LDS by LDS-DMA; a literal whose
-// variable lies there is looked up in LDS, the others in L2 (the whole bit-packed assignment
-// stays L2-resident).  Lanes evaluate 4 clauses of a 256-clause chunk with one 16-byte load
+// a window of win_words * 32 consecutive variables (the block of the tile's smallest
+// variables, b.win_base; refilled between tiles of different windows) are staged in LDS by
+// LDS-DMA; a literal whose variable lies there is looked up in LDS, the others in L2 (the
+// whole bit-packed assignment stays L2-resident).  Lanes evaluate 4 clauses of a 256-clause chunk with one 16-byte load
 // per literal slot from the chunk-transposed layout (as k_eval_fixed), so the literal stream
 // is read once, perfectly coalesced.  Violated clauses go to the per-tile lists through
 // per-tile LDS counters.
@@ -1128,8 +1129,8 @@ __global__ __launch_bounds__(BSC_THREADS) void k_bscatter(ClauseView cv, LoopBuf
 // Workgroup per bucket.  The run table column is processed in batches of BKT_RUN_BATCH runs:
 // segment starts and a prefix of segment lengths in LDS make the batch's pairs one flat index
 // space; a wave takes 64 consecutive items per step (coalesced loads: a segment is contiguous)
-// and each lane finds its item's run by a fixed-depth branch-free binary search, BRS_UNROLL
-// items interleaved.  When the bucket's pairs fit one unrolled sweep of the workgroup (the
+// and each lane finds its item's run by a fixed-depth branch-free binary search, U items
+// interleaved (an LDS item -> segment table instead in the single-sweep case).  When the bucket's pairs fit one unrolled sweep of the workgroup (the
 // common case), they stay in registers between the minimum and the marking pass; otherwise
 // the marking pass re-reads them.  Every pair is written back, with PAIR_LOSE set when it is
 // not its variable's minimum: a segment's pairs are contiguous, so these are whole-line stores.

@@ -13,6 +13,7 @@ constexpr uint32_t TILE_WORDS = TILE / 64;   // violated-bitmask words per tile
 constexpr uint32_t CHUNK = 256;              // clauses per transposed literal chunk
 constexpr int EVAL_THREADS = 256;
 constexpr int ROUND_THREADS = 256;
+constexpr int JOIN_THREADS = 128;  // k_join: ~230 entries per tile in round 1, all tiles resident at once
 constexpr int TAIL_THREADS = 1024;
 constexpr uint32_t WAVE_ROUND_MIN = 2;       // grid rounds from here on run a wave per tile
 constexpr int MAX_FIXED_K = 8;

@@ -754,7 +754,7 @@ __device__ __forceinline__ void join_tile(const ClauseView& cv, const LoopBuffer
 
 // JOIN(r): a clause joins iff owner[v] holds its round-r key for every variable.
 template <int K>
-__global__ __launch_bounds__(ROUND_THREADS) void k_join(ClauseView cv, LoopBuffers b, uint32_t r,
+__global__ __launch_bounds__(JOIN_THREADS) void k_join(ClauseView cv, LoopBuffers b, uint32_t r,
                                                         const uint32_t* __restrict__ in, uint32_t* out,
                                                         int last) {
     const DevState* st = b.state;
@@ -2255,7 +2255,7 @@ hipError_t launch_round(const ClauseView& cv, const LoopBuffers& b, uint32_t r, 
     ALLL_DISPATCH_K(cv.k, (k_claim<K><<<b.n_tiles, ROUND_THREADS, 0, s>>>(cv, b, r, r == 0 ? s0 : s1, s0)));
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    ALLL_DISPATCH_K(cv.k, (k_join<K><<<b.n_tiles, ROUND_THREADS, 0, s>>>(cv, b, r, s0, s1, l)));
+    ALLL_DISPATCH_K(cv.k, (k_join<K><<<b.n_tiles, JOIN_THREADS, 0, s>>>(cv, b, r, s0, s1, l)));
     return hipGetLastError();
 }
 

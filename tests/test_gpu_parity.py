@@ -161,6 +161,27 @@ def test_long_run_across_cover_stamp_cycles(gpu, oracle_mod, layout, monkeypatch
         np.testing.assert_array_equal(s.assignment_words(), A_o)
 
 
+@pytest.mark.parametrize("m", [4096, 4097])
+def test_packed_id_boundary(gpu, oracle_mod, m):
+    """k = 2 over 2^24 variables: literals need 25 bits, leaving 6 id bits per slot.  4096
+    clauses (12-bit ids) are packed exactly at the limit; 4097 (13 bits) fall back to
+    evaluation positions translated through perm.  Both are bit-exact."""
+    from alllsatisfiabilitysolver_amd import Solver, generate_ksat
+
+    n = 1 << 24
+    offs, lits = generate_ksat(3, n, m, 2, 0)
+    seed, K = 9, 12
+    _, A_o, rows = oracle_mod.solve(n, offs, lits, seed, max_iters=K, trace=True)
+    with Solver(n, offs, lits, seed=seed) as s:
+        for it, nu, nm, dres, A_after in rows:
+            before = s.stats()
+            s.run(1)
+            after = s.stats()
+            assert after["n_violated"] == nu, f"iter {it}"
+            assert after["sum_mis_size"] - before["sum_mis_size"] == nm, f"iter {it}"
+            np.testing.assert_array_equal(s.assignment_words(), A_after, err_msg=f"A after iter {it}")
+
+
 def test_solve_converges_and_verifies(gpu, oracle_mod):
     from alllsatisfiabilitysolver_amd import Solver, generate_ksat
 

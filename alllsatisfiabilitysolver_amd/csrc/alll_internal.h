@@ -143,6 +143,8 @@ struct LoopBuffers {
 // Launchers (alll_kernels.hip).  All asynchronous on `s`.
 hipError_t launch_init_assignment(const LoopBuffers& b, hipStream_t s);
 hipError_t launch_init_state(const LoopBuffers& b, hipStream_t s);
+// limit_eval = n_iter + n, limit_nores = none, a stop at limit_nores is lifted (alll_run)
+hipError_t launch_set_limits(const LoopBuffers& b, uint64_t n, hipStream_t s);
 hipError_t launch_eval(const ClauseView& cv, const LoopBuffers& b, uint32_t tile_begin,
                        uint32_t tile_end, bool gated, hipStream_t s);
 hipError_t launch_eval_hybrid(const ClauseView& cv, const LoopBuffers& b, uint32_t tile_begin,

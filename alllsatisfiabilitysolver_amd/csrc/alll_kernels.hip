@@ -2165,6 +2165,18 @@ hipError_t launch_init_assignment(const LoopBuffers& b, hipStream_t s) {
     return hipGetLastError();
 }
 
+__global__ void k_set_limits(DevState* st, uint64_t n) {
+    if (threadIdx.x != 0) return;
+    st->limit_eval = st->n_iter + n;
+    st->limit_nores = ~0ull;
+    if (st->done == 2) st->done = 0;
+}
+
+hipError_t launch_set_limits(const LoopBuffers& b, uint64_t n, hipStream_t s) {
+    k_set_limits<<<1, 64, 0, s>>>(b.state, n);
+    return hipGetLastError();
+}
+
 hipError_t launch_eval(const ClauseView& cv, const LoopBuffers& b, uint32_t tile_begin,
                        uint32_t tile_end, bool gated, hipStream_t s) {
     if (tile_end <= tile_begin) return hipSuccess;

@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstring>
 #include <new>
+#include <sched.h>
 #include <thread>
 #include <string>
 #include <vector>
@@ -54,7 +55,10 @@ int fail(int code, const char* fmt, ...) {
     } while (0)
 
 constexpr uint32_t DEFAULT_GRID_ROUNDS = 4;
-constexpr uint32_t GRAPH_UNROLL = 8;  // iterations per captured graph for long batches
+// captured graphs of 1, 2, 4 and 8 iterations: a batch of n iterations replays n / 8 eight-
+// iteration graphs and at most one of each smaller size (one launch gap per graph)
+constexpr int GRAPH_SIZES = 4;
+constexpr uint32_t GRAPH_UNROLL = 1u << (GRAPH_SIZES - 1);
 constexpr uint32_t SKEWED_GRID_ROUNDS = 6;  // instances with hot variables
 
 }  // namespace
@@ -77,10 +81,10 @@ struct alll_ctx {
     // device allocations
     std::vector<void*> allocs;
     DevState* h_state = nullptr;  // pinned mirror
-    // captured iterations per LFMIS round-0 variant (0: atomic claims, 1: bucketed): [v][0] one
-    // iteration, [v][1] GRAPH_UNROLL iterations (one launch gap per GRAPH_UNROLL iterations)
-    hipGraph_t graph[2][2] = {};
-    hipGraphExec_t graph_exec[2][2] = {};
+    // captured iterations per LFMIS round-0 variant (0: atomic claims, 1: bucketed): [v][j]
+    // holds 2^j iterations
+    hipGraph_t graph[2][GRAPH_SIZES] = {};
+    hipGraphExec_t graph_exec[2][GRAPH_SIZES] = {};
     bool use_graph = true;
     uint64_t bucket_min_u = 0;  // bucketed round 0 when the last pass found at least this many
     hipEvent_t ev[8] = {};
@@ -96,6 +100,47 @@ struct alll_ctx {
 };
 
 namespace {
+
+// Host threads for the layout work of alll_create: the process's CPU affinity, at most 16
+// (the CPU share of one GPU on the MI355X boxes) or OMP_NUM_THREADS when set.
+unsigned host_threads() {
+    unsigned n = std::max(1u, std::thread::hardware_concurrency());
+    cpu_set_t cs;
+    if (sched_getaffinity(0, sizeof cs, &cs) == 0) n = std::max(1, CPU_COUNT(&cs));
+    unsigned cap = 16;
+    if (const char* e = getenv("OMP_NUM_THREADS")) { const int v = atoi(e); if (v > 0) cap = (unsigned)v; }
+    return std::min(n, cap);
+}
+
+// Runs f(i) for i in [0, n) on up to nt threads (contiguous blocks of indices).
+template <typename F>
+void parallel_for(uint64_t n, unsigned nt, F f) {
+    nt = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(nt, n / 4096 + 1));
+    if (nt <= 1) { for (uint64_t i = 0; i < n; ++i) f(i); return; }
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; ++t)
+        th.emplace_back([&, t] { for (uint64_t i = n * t / nt; i < n * (t + 1) / nt; ++i) f(i); });
+    for (auto& x : th) x.join();
+}
+
+// std::sort of a[0, n) on nt threads: sorted blocks, then pairwise merges level by level.
+template <typename T, typename Cmp>
+void parallel_sort(T* a, size_t n, Cmp cmp, unsigned nt) {
+    if (nt <= 1 || n < (1u << 16)) { std::sort(a, a + n, cmp); return; }
+    std::vector<size_t> cut(nt + 1);
+    for (unsigned i = 0; i <= nt; ++i) cut[i] = n * i / nt;
+    {
+        std::vector<std::thread> th;
+        for (unsigned i = 0; i < nt; ++i) th.emplace_back([&, i] { std::sort(a + cut[i], a + cut[i + 1], cmp); });
+        for (auto& x : th) x.join();
+    }
+    for (unsigned w = 1; w < nt; w *= 2) {
+        std::vector<std::thread> th;
+        for (unsigned i = 0; i + w < nt; i += 2 * w)
+            th.emplace_back([&, i, w] { std::inplace_merge(a + cut[i], a + cut[i + w], a + cut[std::min(i + 2 * w, nt)], cmp); });
+        for (auto& x : th) x.join();
+    }
+}
 
 template <typename T>
 int dalloc(alll_ctx* c, T** p, size_t count, int fill = 0) {
@@ -214,12 +259,12 @@ int enqueue_iteration(alll_ctx* c, hipEvent_t* marks, int variant) {
     return ALLL_OK;
 }
 
-int ensure_graph(alll_ctx* c, int variant, int big) {
-    if (!c->use_graph || c->graph_exec[variant][big]) return ALLL_OK;
+int ensure_graph(alll_ctx* c, int variant, int j) {
+    if (!c->use_graph || c->graph_exec[variant][j]) return ALLL_OK;
     hipError_t e = hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal);
     if (e != hipSuccess) { c->use_graph = false; return ALLL_OK; }
     int rc = ALLL_OK;
-    for (uint32_t i = 0; i < (big ? GRAPH_UNROLL : 1u) && rc == ALLL_OK; ++i) rc = enqueue_iteration(c, nullptr, variant);
+    for (uint32_t i = 0; i < (1u << j) && rc == ALLL_OK; ++i) rc = enqueue_iteration(c, nullptr, variant);
     hipGraph_t g = nullptr;
     e = hipStreamEndCapture(c->stream, &g);
     if (rc != ALLL_OK || e != hipSuccess || !g) {
@@ -228,34 +273,35 @@ int ensure_graph(alll_ctx* c, int variant, int big) {
         c->use_graph = false;  // fall back to eager launches
         return ALLL_OK;
     }
-    e = hipGraphInstantiate(&c->graph_exec[variant][big], g, nullptr, nullptr, 0);
+    e = hipGraphInstantiate(&c->graph_exec[variant][j], g, nullptr, nullptr, 0);
     if (e != hipSuccess) {
         (void)hipGraphDestroy(g);
-        c->graph_exec[variant][big] = nullptr;
+        c->graph_exec[variant][j] = nullptr;
         c->use_graph = false;
         return ALLL_OK;
     }
-    c->graph[variant][big] = g;
+    c->graph[variant][j] = g;
+    (void)hipGraphUpload(c->graph_exec[variant][j], c->stream);
     return ALLL_OK;
 }
 
+// n iterations: n / 8 replays of the 8-iteration graph, then one replay per set bit of n % 8
 int launch_iterations(alll_ctx* c, uint64_t n) {
     const int variant = round0_variant(c);
     int rc;
-    if (n >= GRAPH_UNROLL && (rc = ensure_graph(c, variant, 1))) return rc;
-    if ((rc = ensure_graph(c, variant, 0))) return rc;
-    while (c->use_graph && n >= GRAPH_UNROLL) {
-        HIP_TRY(hipGraphLaunch(c->graph_exec[variant][1], c->stream));
-        n -= GRAPH_UNROLL;
+    // every size is captured, instantiated and uploaded at the variant's first launch, so a
+    // later batch never pays a capture
+    for (int j = 0; j < GRAPH_SIZES; ++j)
+        if ((rc = ensure_graph(c, variant, j))) return rc;
+    if (!c->use_graph) {
+        for (uint64_t i = 0; i < n; ++i)
+            if ((rc = enqueue_iteration(c, nullptr, variant))) return rc;
+        return ALLL_OK;
     }
-    for (uint64_t i = 0; i < n; ++i) {
-        if (c->use_graph) {
-            HIP_TRY(hipGraphLaunch(c->graph_exec[variant][0], c->stream));
-        } else {
-            rc = enqueue_iteration(c, nullptr, variant);
-            if (rc) return rc;
-        }
-    }
+    for (; n >= GRAPH_UNROLL; n -= GRAPH_UNROLL)
+        HIP_TRY(hipGraphLaunch(c->graph_exec[variant][GRAPH_SIZES - 1], c->stream));
+    for (int j = GRAPH_SIZES - 2; j >= 0; --j)
+        if ((n >> j) & 1u) HIP_TRY(hipGraphLaunch(c->graph_exec[variant][j], c->stream));
     return ALLL_OK;
 }
 
@@ -622,21 +668,20 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
                 const uint64_t blk = windows ? lo / win_vars : 0;
                 return {(blk << 32) | a, b2, (uint32_t)cl};
             };
+            const unsigned nt = host_threads();
             auto sort_range = [&](uint64_t cb0, uint64_t ce0) {
                 std::vector<Key> kv(ce0 - cb0);
-                for (uint64_t cl = cb0; cl < ce0; ++cl) kv[cl - cb0] = key_of(cl);
-                std::sort(kv.begin(), kv.end(), [](const Key& x, const Key& y) {
+                parallel_for(ce0 - cb0, nt, [&](uint64_t i) { kv[i] = key_of(cb0 + i); });
+                parallel_sort(kv.data(), kv.size(), [](const Key& x, const Key& y) {
                     return x.k1 != y.k1 ? x.k1 < y.k1 : (x.k2 != y.k2 ? x.k2 < y.k2 : x.id < y.id);
-                });
-                for (uint64_t i = 0; i < kv.size(); ++i) perm[cb0 + i] = kv[i].id;
+                }, nt);
+                parallel_for(kv.size(), nt, [&](uint64_t i) { perm[cb0 + i] = kv[i].id; });
             };
-            std::vector<std::thread> th;
-            for (int r = 0; r < c->world; ++r) {
+            for (int r = 0; r < c->world; ++r) {  // every rank lays out every shard (replicated lists)
                 const uint64_t cb0 = std::min<uint64_t>(m, (uint64_t)r * c->tiles_per_rank * TILE);
                 const uint64_t ce0 = std::min<uint64_t>(m, cb0 + (uint64_t)c->tiles_per_rank * TILE);
-                if (ce0 > cb0) th.emplace_back(sort_range, cb0, ce0);
+                if (ce0 > cb0) sort_range(cb0, ce0);
             }
-            for (auto& t : th) t.join();
         }
         // Packed clause ids: when the literals leave enough bits below the hot flag, slot j of
         // every clause also carries bits [j * id_bits, (j + 1) * id_bits) of its clause id, so
@@ -659,19 +704,19 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
             }
         }
         std::vector<uint32_t> t(real_chunks * CHUNK * fixed_k, 0u);
-        std::vector<uint32_t> tmp(fixed_k);
         const uint32_t id_mask = cv.id_bits ? (1u << cv.id_bits) - 1u : 0u;
-        for (uint64_t p2 = 0; p2 < m; ++p2) {
+        parallel_for(m, host_threads(), [&](uint64_t p2) {
+            uint32_t tmp[MAX_FIXED_K];
             const uint64_t cl = perm[p2];
             for (int j = 0; j < fixed_k; ++j)
                 tmp[j] = flagged.empty() ? prob->literals[cl * fixed_k + j] : flagged[cl * fixed_k + j];
-            std::sort(tmp.begin(), tmp.end(), [](uint32_t x, uint32_t y) { return (x >> 1) > (y >> 1); });
+            std::sort(tmp, tmp + fixed_k, [](uint32_t x, uint32_t y) { return (x >> 1) > (y >> 1); });
             const uint64_t g = p2 / CHUNK, r = p2 % CHUNK;
             for (int j = 0; j < fixed_k; ++j) {
                 const uint32_t idp = cv.id_bits ? ((uint32_t)(cl >> (j * cv.id_bits)) & id_mask) << cv.id_shift : 0u;
                 t[(g * fixed_k + j) * CHUNK + r] = tmp[j] | idp;
             }
-        }
+        });
         if (!t.empty() && hipMemcpy(d_t, t.data(), t.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
             return bail(fail(ALLL_ERR_HIP, "transposed literal upload failed"));
         if (!cv.id_bits) {
@@ -750,7 +795,7 @@ int alll_destroy(alll_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (int v = 0; v < 2; ++v)
-        for (int u = 0; u < 2; ++u) {
+        for (int u = 0; u < GRAPH_SIZES; ++u) {
             if (c->graph_exec[v][u]) (void)hipGraphExecDestroy(c->graph_exec[v][u]);
             if (c->graph[v][u]) (void)hipGraphDestroy(c->graph[v][u]);
         }
@@ -801,10 +846,11 @@ int alll_solve(alll_ctx* c, alll_stats* st) {
 int alll_run(alll_ctx* c, uint64_t n_iters, alll_stats* st) {
     if (!c) return fail(ALLL_ERR_INVALID_ARG, "null context");
     HIP_TRY(hipSetDevice(c->device));
-    int rc = read_state(c);
-    if (rc) return rc;
-    if (c->h_state->done != 1 && n_iters) {
-        if ((rc = write_limits(c, c->h_state->n_iter + n_iters, ~0ull))) return rc;
+    int rc;
+    if (n_iters) {
+        // no host round trip: the limit is set on the device (n_iter + n_iters), stream-ordered
+        // before the iterations; after convergence every kernel is gated off
+        HIP_TRY(launch_set_limits(c->b, n_iters, c->stream));
         if ((rc = launch_iterations(c, n_iters))) return rc;
     }
     if (st) return fill_stats(c, st);
@@ -1053,6 +1099,14 @@ uint64_t alll_eval_bytes(alll_ctx* c) {
 }
 
 int alll_layout(alll_ctx* c) { return c ? (int)c->cv.k : -1; }
+
+int alll_comm_size(alll_ctx* c) {
+    if (!c) return -1;
+    if (!c->comm) return c->world;
+    int n = 0;
+    if (ncclCommCount(c->comm, &n) != ncclSuccess) return -1;
+    return n;
+}
 
 const char* alll_eval_kernel(alll_ctx* c) { return c ? c->eval_name.c_str() : ""; }
 

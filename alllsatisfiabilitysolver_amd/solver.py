@@ -231,6 +231,13 @@ class Solver:
     def eval_kernel(self) -> str:
         return self._L.alll_eval_kernel(self._ctx).decode()
 
+    def comm_size(self) -> int:
+        """Ranks in the solve: the RCCL communicator's count (or world with a host exchange)."""
+        n = int(self._L.alll_comm_size(self._ctx))
+        if n < 1:
+            raise N.AlllError(N.ALLL_ERR_RCCL, "ncclCommCount failed")
+        return n
+
 
 def device_count() -> int:
     return int(N.lib().alll_device_count())

@@ -8,9 +8,11 @@ algorithm, so K fixed iterations are timed.
 
   value            = m * K / t  (clause-evals/s of the full loop, whole job)
   resample_iters_s = K / t
-Inputs are resident in HBM before the timed region.  N>1: one process per GPU (torchrun),
-clauses sharded across ranks, per-iteration RCCL all-gather of the violated bitmask; the
-instance size is fixed (strong scaling).
+Inputs are resident in HBM before the timed region.  N>1: one process per GPU, clauses
+sharded across ranks, per-iteration RCCL all-gather of the violated bitmask; the instance
+size is fixed (strong scaling).  Under torch.distributed.run the ranks come from the
+environment; `python bench.py --gpus N` alone starts the N ranks itself.  An RCCL failure is
+fatal; the host-staged gloo exchange is only used with --exchange-impl host.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config M|C2|C3|C4|C5]
 """
@@ -52,35 +54,77 @@ def cpu_model():
     return platform.processor() or "unknown"
 
 
+def cpu_threads():
+    """Host threads for the CPU baseline: the process's CPU affinity (the reference takes
+    omp_get_num_procs(), example/main.cpp:77), capped by the cgroup CPU quota and by
+    OMP_NUM_THREADS when the environment declares the job's CPU share.  Returns (threads, why)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    why = [f"affinity {n}"]
+    quota = None
+    try:  # cgroup v2
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(q) // int(per))
+    except (OSError, ValueError):
+        try:  # cgroup v1
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = max(1, q // per)
+        except (OSError, ValueError):
+            pass
+    if quota is not None:
+        why.append(f"cgroup quota {quota}")
+        n = min(n, quota)
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        why.append(f"OMP_NUM_THREADS {omp}")
+        n = min(n, int(omp))
+    return max(1, n), ", ".join(why)
+
+
+def _probe(probe, n, m, k, kind, threads, budget, eval_reps):
+    cmd = [probe, "bench-gen", str(n), str(m), str(k), str(kind), "1", str(threads), str(budget), str(eval_reps)]
+    return json.loads(subprocess.run(cmd, check=True, capture_output=True, text=True).stdout)
+
+
 def cpu_baseline(cfg, budget_s):
-    """The reference's own -p OpenMP path (oracle/_ref/ref_probe, compiled from the
-    reference sources) on the host cores: full resample iterations on a bounded sample, plus
-    the eval-phase rate at the full configuration size."""
+    """The reference's own -p OpenMP path (oracle/_ref/ref_probe, compiled from the reference
+    sources) on the host cores: full resample iterations on bounded samples of the same
+    generator (BASELINE.md "CPU-baseline plan"), plus the eval-phase rate at the full size."""
     n, m, k, kind, _ = CONFIGS[cfg]
-    threads = max(1, min(16, os.cpu_count() or 1))  # the GPU box's CPU share is 16
+    threads, why = cpu_threads()
     probe = os.path.join(ROOT, "oracle", "_ref", "ref_probe")
     if os.path.exists(probe):
-        # bounded full-loop sample: 1/100 of the instance (same ratio, same generator)
+        # headline sample: 1/100 of the instance (same ratio, same generator), budget_s of loop
         ns, ms = max(k, n // 100), m // 100
-        cmd = [probe, "bench-gen", str(ns), str(ms), str(k), str(kind), "1", str(threads),
-               str(budget_s), "0"]
-        r = json.loads(subprocess.run(cmd, check=True, capture_output=True, text=True).stdout)
+        r = _probe(probe, ns, ms, k, kind, threads, budget_s, 0)
         loop_rate = ms * r["iters"] / r["iters_s"] if r["iters"] else 0.0
+        points = {f"m={ms}": {"iters": r["iters"], "s": r["iters_s"],
+                              "iters_per_s": r["iters"] / r["iters_s"] if r["iters_s"] else 0.0}}
+        # the plan's other full-loop points: m = 10k (a few seconds of loop) and m = 1M (one
+        # iteration: the reference MIS is quadratic in |U|)
+        for frac, budget in ((1000, min(3.0, budget_s)), (10, 1e-3)):
+            if m // frac < 1000 or m // frac == ms:
+                continue
+            q = _probe(probe, max(k, n // frac), m // frac, k, kind, threads, budget, 0)
+            points[f"m={m // frac}"] = {"iters": q["iters"], "s": q["iters_s"],
+                                        "iters_per_s": q["iters"] / q["iters_s"] if q["iters_s"] else 0.0}
         # eval phase (P1, SATInstance.h:273-280) at the full size, best of 3
-        cmd = [probe, "bench-gen", str(n), str(m), str(k), str(kind), "1", str(threads), "0", "3"]
-        e = json.loads(subprocess.run(cmd, check=True, capture_output=True, text=True).stdout)
+        e = _probe(probe, n, m, k, kind, threads, 0, 3)
         return {
             "value": loop_rate,
             "unit": "clause-evals/s",
             "cores": threads,
             "kind": "reference",
-            "sample": (f"reference -p path (T={threads}) full resample loop, {r['iters']} iterations in "
+            "sample": (f"reference -p path (T={threads}; {why}) full resample loop, {r['iters']} iterations in "
                        f"{r['iters_s']:.1f}s on a 1/100 sample (n={ns}, m={ms}, same generator); "
                        f"eval phase alone at full size m={m}: {e['eval_clause_evals_per_s']:.3e} "
                        f"clause-evals/s; the reference MIS is quadratic in |U| so the full-size loop "
                        f"is ~1e3 s/iteration (SURVEY.md §6); host {cpu_model()}"),
             "resample_iters_per_s": r["iters"] / r["iters_s"] if r["iters_s"] else 0.0,
             "eval_phase_clause_evals_per_s": e["eval_clause_evals_per_s"],
+            "full_loop_points": points,
         }
     # fallback: the oracle's serial restatement (port)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -98,6 +142,20 @@ def cpu_baseline(cfg, budget_s):
             "sample": f"oracle serial restatement, {it} iterations on n={ns}, m={ms}; host {cpu_model()}"}
 
 
+def launch_ranks(args):
+    """--gpus N > 1 without a launcher: start N rank processes (one per GPU) through
+    torch.distributed.run and exit with its status.  This process never touches the GPU."""
+    import socket
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    log(f"launching {args.gpus} ranks: {' '.join(cmd)}")
+    return subprocess.run(cmd).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -106,6 +164,9 @@ def main():
     ap.add_argument("--config", default="M", choices=list(CONFIGS))
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--exchange", default="allgather", choices=["allgather", "allreduce"])
+    ap.add_argument("--exchange-impl", default="rccl", choices=["rccl", "host"],
+                    help="N>1: RCCL collectives (default; a failure is fatal) or the host-staged gloo "
+                         "exchange (rehearsal on one GPU, ALLL_BENCH_SAME_DEVICE=1)")
     ap.add_argument("--no-ranged", action="store_true", help="use the L2-gather eval kernel")
     ap.add_argument("--atomic-claims", action="store_true", help="LFMIS round 0 by global atomics")
     ap.add_argument("--grid-rounds", type=int, default=0, help="full-grid LFMIS rounds (0 = default)")
@@ -118,13 +179,15 @@ def main():
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_eval_traffic.json"))
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     if os.environ.get("ALLL_BENCH_SAME_DEVICE"):  # rehearsal of the N>1 path on a 1-GPU box
         local_rank = 0
-    if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
 
     import torch
 
@@ -133,14 +196,17 @@ def main():
 
     dist = None
     comm_id = None
+    exchange_impl = "none"
     if world > 1:
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-        obj = [comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(obj, src=0)
-        comm_id = obj[0]
+        dist.init_process_group("gloo", rank=rank, world_size=world)  # host-side control only
+        exchange_impl = args.exchange_impl
+        if exchange_impl == "rccl":
+            obj = [comm_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(obj, src=0)
+            comm_id = obj[0]
 
     n, m, k, kind, desc = CONFIGS[args.config]
     t0 = time.perf_counter()
@@ -154,59 +220,35 @@ def main():
     if args.atomic_claims:
         flags |= N.FLAG_ATOMIC_CLAIMS
     t0 = time.perf_counter()
-    exchange_impl = "rccl" if world > 1 else "none"
-    try:
-        s = Solver(n, offs, lits, seed=args.seed, device=local_rank, rank=rank, world=world,
-                   comm_id=comm_id, flags=flags, grid_rounds=args.grid_rounds)
-    except N.AlllError as e:
-        if world == 1 or e.code != N.ALLL_ERR_RCCL:
-            raise
-        # RCCL communicator unavailable: same kernels, host-staged exchange over gloo
+    kw = dict(seed=args.seed, device=local_rank, rank=rank, world=world, flags=flags, grid_rounds=args.grid_rounds)
+    if exchange_impl == "host":
         from alllsatisfiabilitysolver_amd import gloo_exchange
 
-        log(f"[rank {rank}] RCCL init failed ({e}); using the host-staged gloo exchange")
-        exchange_impl = "host-gloo"
-        s = Solver(n, offs, lits, seed=args.seed, device=local_rank, rank=rank, world=world,
-                   flags=flags, grid_rounds=args.grid_rounds, exchange=gloo_exchange())
+        s = Solver(n, offs, lits, exchange=gloo_exchange(), **kw)
+    else:
+        s = Solver(n, offs, lits, comm_id=comm_id, **kw)  # RCCL failure raises: fatal
     del offs, lits
     t_create = time.perf_counter() - t0
     log(f"[rank {rank}] generated {m} clauses in {t_gen:.2f}s, uploaded in {t_create:.2f}s, "
-        f"layout k={s.layout()}, eval kernel {s.eval_kernel()}")
+        f"layout k={s.layout()}, eval kernel {s.eval_kernel()}, exchange {exchange_impl}")
 
     def barrier():
         if dist is not None:
             dist.barrier()
 
-    # warmup (untimed).  With RCCL, every rank reports whether its warmup went through; if any
-    # failed, all ranks rebuild the solver with the host-staged gloo exchange (same kernels)
-    failed = 0
-    try:
-        s.run(args.warmup, sync=False)
-        s.synchronize()
-    except N.AlllError as e:
-        if world == 1:
-            raise
-        log(f"[rank {rank}] warmup failed ({e})")
-        failed = 1
-    if world > 1 and exchange_impl == "rccl":
-        flag = torch.tensor([failed], dtype=torch.int32)
-        dist.all_reduce(flag, op=dist.ReduceOp.MAX)
-        if int(flag.item()):
-            from alllsatisfiabilitysolver_amd import gloo_exchange
-
-            log(f"[rank {rank}] RCCL exchange failed on some rank; using the host-staged gloo exchange")
-            try:
-                s.close()
-            except N.AlllError:
-                pass
-            offs, lits = generate_ksat(1, n, m, k, kind)
-            s = Solver(n, offs, lits, seed=args.seed, device=local_rank, rank=rank, world=world,
-                       flags=flags, grid_rounds=args.grid_rounds, exchange=gloo_exchange())
-            del offs, lits
-            exchange_impl = "host-gloo"
-            s.run(args.warmup, sync=False)
-            s.synchronize()
+    # warmup (untimed); an RCCL error here is fatal too
+    s.run(args.warmup, sync=False)
+    s.synchronize()
     torch.cuda.synchronize(local_rank)
+    n_comm = s.comm_size()
+    ranks_seen = 1
+    if dist is not None:
+        t = torch.tensor([1], dtype=torch.int64)
+        dist.all_reduce(t)
+        ranks_seen = int(t.item())
+        if ranks_seen != world or n_comm != world:
+            raise SystemExit(f"rank {rank}: {ranks_seen} ranks answered, communicator holds {n_comm}, "
+                             f"expected {world}")
 
     barrier()
     torch.cuda.synchronize(local_rank)
@@ -222,20 +264,26 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     st = s.stats()
-    steps_done = args.steps  # converged runs would stop early; ratio-4 instances do not
-    value = m * steps_done / dt
-    iters_s = steps_done / dt
+    # iterations actually run: an instance that converges stops early (every kernel is gated
+    # off after the final zero-violation pass), so m * K / t would overstate the rate
+    steps_done = st["n_iterations"] - it0
+    converged = bool(st["solved"])
 
-    # in-loop phase times of exactly the K timed iterations, from the kernels' own device
+    # in-loop phase times of exactly the timed iterations, from the kernels' own device
     # wall-clock stamps (the graph replays as timed; eval = first workgroup start to last
     # workgroup end); the eval kernel's average duration prices the roofline
-    pt = s.loop_times(it0, args.steps)
+    pt = s.loop_times(it0, max(1, steps_done))
     eval_bytes = s.eval_bytes()
     eval_ms = pt["eval_ms"]
+    ev_ms = s.bench_eval(args.eval_b2b)[0] if args.eval_b2b > 0 else None
+    if converged:
+        # a converging instance's clause-eval rate is measured as repeated
+        # evaluation passes over a fixed assignment
+        ev_ms = s.bench_eval(max(args.eval_b2b, 20))[0]
+        eval_ms = ev_ms
     achieved = eval_bytes / (eval_ms * 1e-3) / 1e9 if eval_ms > 0 else 0.0
     # cross-check with HIP events on the solver's stream: the same iteration replayed eagerly
-    pe = s.profile(args.event_iters) if args.event_iters > 0 else None
-    ev_ms = s.bench_eval(args.eval_b2b)[0] if args.eval_b2b > 0 else None
+    pe = s.profile(args.event_iters) if args.event_iters > 0 and not converged else None
     traffic = None
     try:
         tj = json.load(open(args.traffic_json))
@@ -246,14 +294,22 @@ def main():
 
     out = None
     if rank == 0:
+        if steps_done == args.steps and not converged:
+            value, iters_s, ms_step, vkind = m * steps_done / dt, steps_done / dt, dt * 1e3 / steps_done, "loop"
+        else:
+            # converged before or during the timed region: no loop rate exists; report the
+            # evaluation pass rate and mark it
+            value, iters_s, ms_step, vkind = m / (eval_ms * 1e-3), None, eval_ms, "eval-only (instance converged)"
         out = {
             "metric": "clause-evals/sec + resample iters/sec, random 3-SAT 10M clauses, 1/2/4/8 GPUs",
             "value": value,
             "unit": "clause-evals/s",
-            "n_gpus": world,
+            "n_gpus": n_comm,
+            "ranks_seen": ranks_seen,
             "steps": args.steps,
+            "steps_done": steps_done,
             "warmup": args.warmup,
-            "ms_per_step": dt * 1e3 / args.steps,
+            "ms_per_step": ms_step,
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": None,
@@ -263,6 +319,7 @@ def main():
                        "solve_seed": args.seed,
                        "exchange": f"{args.exchange}/{exchange_impl}" if world > 1 else "none",
                        "parallelism": f"clause-shard x{world}"},
+            "value_kind": vkind,
             "resample_iters_per_s": iters_s,
             "violated_last": st["n_violated"],
             "avg_mis_size": st["avg_mis_size"],
@@ -278,7 +335,7 @@ def main():
                 "traffic": traffic,
                 "kernel": s.eval_kernel(),
                 "algorithmic_bytes_per_launch": eval_bytes,
-                "eval_ms_in_loop": eval_ms,
+                "eval_ms_in_loop": pt["eval_ms"],
                 "timing": "device wall-clock stamps inside the timed region (s_memrealtime)",
                 "eval_ms_hip_events": pe["eval_ms"] if pe else None,
                 "eval_ms_back_to_back": ev_ms,

@@ -199,6 +199,10 @@ uint64_t alll_eval_bytes(alll_ctx* ctx);
 int alll_layout(alll_ctx* ctx);
 /* Name of the evaluation kernel the loop launches (e.g. "k_eval_hybrid<3>"). */
 const char* alll_eval_kernel(alll_ctx* ctx);
+/* Ranks taking part in the clause-sharded solve: ncclCommCount of the RCCL communicator, or
+ * alll_options.world with a host-staged exchange (1 on one GPU); -1 on failure.  (The
+ * reference counterpart is the thread count of the -p path, example/main.cpp:76-84.) */
+int alll_comm_size(alll_ctx* ctx);
 
 /* ---- host-side helpers (no GPU needed) ---------------------------------------------- */
 

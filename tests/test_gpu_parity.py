@@ -290,6 +290,9 @@ BIG = {
     "M_positions": (2_500_000, 10_000_000, 3, 0, {"ALLL_PACKED_IDS": "0"}),  # perm translation
     # 611 power-of-2 buckets (more than CUs): the narrow k_bresolve, two workgroups per CU
     "M_pow2_buckets": (2_500_000, 10_000_000, 3, 0, {"ALLL_BKT_SHIFT": "12"}),
+    # C4 (the north star's 8-GPU instance) on one GPU: 27-bit clause ids do not fit in the
+    # literals' spare bits (26-bit literals), so evaluation positions + perm; 26 LDS windows
+    "C4_3sat_128M": (32_000_000, 128_000_000, 3, 0),
 }
 
 

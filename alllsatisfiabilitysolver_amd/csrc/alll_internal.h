@@ -15,7 +15,9 @@ constexpr int EVAL_THREADS = 256;
 constexpr int ROUND_THREADS = 256;
 constexpr int JOIN_THREADS = 128;  // k_join: ~230 entries per tile in round 1, all tiles resident at once
 constexpr int TAIL_THREADS = 1024;
-constexpr uint32_t WAVE_ROUND_MIN = 2;       // grid rounds from here on run a wave per tile
+// grid rounds from here on run a wave per tile (instances with hot variables: one round later,
+// their round 2 still holds ~10% of the violated clauses)
+constexpr uint32_t WAVE_ROUND_MIN = 2, WAVE_ROUND_MIN_HOT = 3;
 constexpr int MAX_FIXED_K = 8;
 // Persistent hybrid evaluation: LDS window of at most LDS_VARS variables' assignment words.
 constexpr uint32_t LDS_WORDS = 38912;              // 152 KiB of LDS
@@ -117,7 +119,14 @@ struct LoopBuffers {
     const uint32_t* win_base;   // hybrid eval: per tile, first assignment word of its LDS window
                                 // (nullptr: words [0, win_words) for every tile)
     uint32_t win_words;         // hybrid eval: LDS window size in words (<= LDS_WORDS)
-    uint32_t bkt_width;         // bucket = variable / bkt_width (<= 2^BKT_SHIFT_MAX)
+    // Variable spread of skewed instances (power-law hubs have the lowest ids): the owner slot
+    // and the round-0 bucket of variable v are taken from vmix(v) = (v * vmix_mul) & vmix_mask,
+    // a bijection onto [0, vmix_mask] (odd multiplier mod 2^k), so that the hubs' owner keys
+    // fall in different memory channels and their pairs in different buckets.  Identity
+    // (mul 1, mask ~0) otherwise.
+    uint32_t vmix_mul;
+    uint32_t vmix_mask;
+    uint32_t bkt_width;         // bucket = vmix(variable) / bkt_width (<= 2^BKT_SHIFT_MAX)
     uint32_t bkt_magic;         // floor(2^32 / bkt_width): bucket by multiply-high
     uint32_t n_cu;              // compute units of the device
     uint32_t n_bkt;
@@ -153,7 +162,7 @@ hipError_t launch_collect(const ClauseView& cv, const LoopBuffers& b, uint32_t o
                           uint32_t own_end, hipStream_t s);
 hipError_t launch_reduce(const LoopBuffers& b, int mode, hipStream_t s);
 hipError_t launch_round(const ClauseView& cv, const LoopBuffers& b, uint32_t r, bool last,
-                        hipStream_t s);
+                        uint32_t wave_from, hipStream_t s);
 hipError_t launch_round0_buckets(const ClauseView& cv, const LoopBuffers& b, bool last, bool fused_reduce,
                                  hipStream_t s);
 hipError_t launch_tail(const ClauseView& cv, const LoopBuffers& b, uint32_t first_round,

@@ -603,6 +603,9 @@ __global__ __launch_bounds__(1024) void k_reduce(LoopBuffers b, int mode) {
 // Lists are double buffered: each kernel reads one buffer and compacts the survivors into
 // the other.  Claims on hot variables (high-degree, flagged by the host) are reduced in an
 // LDS hash table first: one global atomic per hot variable per workgroup (power-law hubs).
+// Owner slot / bucket key of variable v (LoopBuffers::vmix_mul, identity unless skewed).
+__device__ __forceinline__ uint32_t vmix(const LoopBuffers& b, uint32_t v) { return (v * b.vmix_mul) & b.vmix_mask; }
+
 struct HotTable {
     uint32_t* k;
     unsigned long long* v;
@@ -620,9 +623,17 @@ struct HotTable {
         // compiler from merging the two into one flat atomic through a selected pointer)
         __hip_atomic_fetch_min(&v[h], key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
-    __device__ void flush(unsigned long long* owner) {
-        for (uint32_t i = threadIdx.x; i < HOT_SLOTS; i += blockDim.x)
-            if (k[i] != 0xFFFFFFFFu) atomicMin(&owner[k[i]], v[i]);
+    // One claim per hot variable per workgroup.  The claim is tested against the owner key first
+    // (agent-scope load): every workgroup of a round claims the top hubs, and memory-side
+    // atomics on one address serialise (~11 ns each), so only keys below the current minimum
+    // are sent.  A stale read is never below the true minimum (keys only decrease), so a
+    // skipped claim could not have won.
+    __device__ void flush(unsigned long long* owner, const LoopBuffers& b) {
+        for (uint32_t i = threadIdx.x; i < HOT_SLOTS; i += blockDim.x) {
+            if (k[i] == 0xFFFFFFFFu) continue;
+            unsigned long long* o = &owner[vmix(b, k[i])];
+            if (v[i] < __hip_atomic_load(o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(o, v[i]);
+        }
     }
 };
 
@@ -633,13 +644,13 @@ __device__ __forceinline__ unsigned long long* owner_of(const LoopBuffers& b, ui
 }
 
 template <int K>
-__device__ __forceinline__ void claim_all(const ClauseView& cv, const Ent<K>& e, uint64_t lb, uint32_t len,
-                                          unsigned long long key, unsigned long long* owner, HotTable& ht,
-                                          bool hot) {
+__device__ __forceinline__ void claim_all(const ClauseView& cv, const LoopBuffers& b, const Ent<K>& e, uint64_t lb,
+                                          uint32_t len, unsigned long long key, unsigned long long* owner,
+                                          HotTable& ht, bool hot) {
     for (uint32_t j = 0; j < len; ++j) {
         const uint32_t raw = ent_lit<K>(cv, e, lb, j);
         if (hot && (raw & LIT_HOT)) ht.claim(lit_var(raw), key);
-        else __hip_atomic_fetch_min(&owner[lit_var(raw)], key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else __hip_atomic_fetch_min(&owner[vmix(b, lit_var(raw))], key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -683,11 +694,11 @@ __global__ __launch_bounds__(ROUND_THREADS) void k_claim(ClauseView cv, LoopBuff
             for (uint32_t j = 0; j < len; ++j) killed |= b.cover[lit_var(ent_lit<K>(cv, e, lb, j))] == stamp;
             if (killed) continue;
         }
-        claim_all<K>(cv, e, lb, len, keyhi | key, owner, ht, hot);
+        claim_all<K>(cv, b, e, lb, len, keyhi | key, owner, ht, hot);
         if (r > 0) store_ent<K>(lout + (uint64_t)atomicAdd(&s_keep, 1u) * S, e);
     }
     __syncthreads();
-    if (hot) ht.flush(owner);
+    if (hot) ht.flush(owner, b);
     if (r > 0 && threadIdx.x == 0) b.tile_cnt[tile] = s_keep;
 }
 
@@ -768,7 +779,7 @@ __global__ __launch_bounds__(JOIN_THREADS) void k_join(ClauseView cv, LoopBuffer
                  [&](const Ent<K>& e, uint32_t, uint64_t lb, uint32_t len) {
                      bool own = true;
                      const unsigned long long key = keyhi | prio(b, st, e.w[0]);
-                     for (uint32_t j = 0; j < len; ++j) own &= owner[lit_var(ent_lit<K>(cv, e, lb, j))] == key;
+                     for (uint32_t j = 0; j < len; ++j) own &= owner[vmix(b, lit_var(ent_lit<K>(cv, e, lb, j)))] == key;
                      return own;
                  });
 }
@@ -813,9 +824,14 @@ __global__ __launch_bounds__(ROUND_THREADS) void k_wclaim(ClauseView cv, LoopBuf
                 bool killed = false;
                 for (uint32_t j = 0; j < len; ++j) killed |= b.cover[lit_var(ent_lit<K>(cv, e, lb, j))] == stamp;
                 if (!killed) {
-                    for (uint32_t j = 0; j < len; ++j)
-                        __hip_atomic_fetch_min(&owner[lit_var(ent_lit<K>(cv, e, lb, j))], keyhi | key,
-                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    for (uint32_t j = 0; j < len; ++j) {
+                        const uint32_t raw = ent_lit<K>(cv, e, lb, j);
+                        unsigned long long* o = &owner[vmix(b, lit_var(raw))];
+                        // hubs: test first (see HotTable::flush)
+                        if (!(raw & LIT_HOT) ||
+                            (keyhi | key) < __hip_atomic_load(o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                            __hip_atomic_fetch_min(o, keyhi | key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
                     keep = true;
                 }
             }
@@ -859,7 +875,7 @@ __global__ __launch_bounds__(ROUND_THREADS) void k_wjoin(ClauseView cv, LoopBuff
             const uint32_t kc = prio(b, st, e.w[0]);
             if (kc != ~0u) {  // (streaming: a clause not yielded this iteration leaves the list)
                 own = true;
-                for (uint32_t j = 0; j < len; ++j) own &= owner[lit_var(ent_lit<K>(cv, e, lb, j))] == (keyhi | kc);
+                for (uint32_t j = 0; j < len; ++j) own &= owner[vmix(b, lit_var(ent_lit<K>(cv, e, lb, j)))] == (keyhi | kc);
                 keep = !own;
                 if (own) {
                     for (uint32_t j = 0; j < len; ++j) b.cover[lit_var(ent_lit<K>(cv, e, lb, j))] = (uint8_t)stamp;
@@ -915,6 +931,7 @@ __device__ __forceinline__ unsigned long long make_pair(uint32_t c, uint32_t el,
 // Variable bucket of the bucketed round 0: v / bkt_width by multiply-high (the estimate is
 // at most one low for v < 2^32, one correction step), and v's offset in the bucket.
 __device__ __forceinline__ uint32_t bucket_of(const LoopBuffers& b, uint32_t v, uint32_t& off) {
+    v = vmix(b, v);
     uint32_t q = __umulhi(v, b.bkt_magic);
     uint32_t r = v - q * b.bkt_width;
     if (r >= b.bkt_width) { ++q; r -= b.bkt_width; }
@@ -1059,7 +1076,7 @@ __global__ __launch_bounds__(BSC_THREADS) void k_bscatter(ClauseView cv, LoopBuf
     dbg_stamp(b, 0, 2);
     __syncthreads();
     dbg_stamp(b, 0, 3);
-    if (hot) ht.flush(owner_of(b, st->round_base));
+    if (hot) ht.flush(owner_of(b, st->round_base), b);
     // exclusive scan of the histogram: run-local start of every bucket
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t per = (nb + blockDim.x - 1) / blockDim.x;
@@ -1350,7 +1367,7 @@ __global__ __launch_bounds__(BJN_THREADS) void k_bjoin(ClauseView cv, LoopBuffer
 #pragma unroll
                 for (int j = 0; j < K; ++j) {
                     const uint32_t raw = e[u].w[1 + j];
-                    if (raw & LIT_HOT) own &= owner[lit_var(raw)] == (keyhi | e[u].w[0]);
+                    if (raw & LIT_HOT) own &= owner[vmix(b, lit_var(raw))] == (keyhi | e[u].w[0]);
                 }
             }
             if (own) {
@@ -1434,7 +1451,7 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail(ClauseView cv, LoopBuffer
                 if (!killed) {
                     const unsigned long long key = keyhi | prio(b, st, e.w[0]);
                     for (uint32_t j = 0; j < len; ++j)
-                        __hip_atomic_fetch_min(&owner[lit_var(ent_lit<K>(cv, e, lb, j))], key, __ATOMIC_RELAXED,
+                        __hip_atomic_fetch_min(&owner[vmix(b, lit_var(ent_lit<K>(cv, e, lb, j)))], key, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_AGENT);
                     store_ent<K>(left + (uint64_t)atomicAdd(&s_wp, 1u) * S, e);
                 }
@@ -1458,7 +1475,7 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail(ClauseView cv, LoopBuffer
                 const uint32_t len = ent_len<K>(cv, e, lb);
                 bool own = true;
                 for (uint32_t j = 0; j < len; ++j)
-                    own &= __hip_atomic_load(&owner[lit_var(ent_lit<K>(cv, e, lb, j))], __ATOMIC_RELAXED,
+                    own &= __hip_atomic_load(&owner[vmix(b, lit_var(ent_lit<K>(cv, e, lb, j)))], __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_AGENT) == (keyhi | kc);
                 if (own) {
                     for (uint32_t j = 0; j < len; ++j)
@@ -2249,14 +2266,14 @@ hipError_t launch_reduce(const LoopBuffers& b, int mode, hipStream_t s) {
 }
 
 hipError_t launch_round(const ClauseView& cv, const LoopBuffers& b, uint32_t r, bool last,
-                        hipStream_t s) {
+                        uint32_t wave_from, hipStream_t s) {
     // buffers: eval -> stage[0]; CLAIM(0) in place; JOIN(r) stage[0] -> stage[1];
     // CLAIM(r>0) stage[1] -> stage[0]
     if (b.n_tiles == 0) return hipSuccess;
     uint32_t* s0 = b.stage[0];
     uint32_t* s1 = b.stage[1];
     const int l = last ? 1 : 0;
-    if (r >= WAVE_ROUND_MIN) {  // late rounds: a wave per tile
+    if (r >= wave_from) {  // late rounds: a wave per tile
         const uint32_t grid = (b.n_tiles + ROUND_THREADS / 64 - 1) / (ROUND_THREADS / 64);
         ALLL_DISPATCH_K(cv.k, (k_wclaim<K><<<grid, ROUND_THREADS, 0, s>>>(cv, b, r, s1, s0)));
         hipError_t e = hipGetLastError();

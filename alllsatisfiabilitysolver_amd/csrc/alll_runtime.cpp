@@ -75,6 +75,7 @@ struct alll_ctx {
     uint32_t tiles_per_rank = 0, own_begin = 0, own_end = 0, n_tiles_padded = 0;
     uint32_t grid_rounds = DEFAULT_GRID_ROUNDS;
     bool fuse_reduce = true;     // env ALLL_FUSE_REDUCE=0: separate k_reduce (tests, A/B)
+    uint32_t wave_round_min = WAVE_ROUND_MIN;  // first grid round with a wave per tile
     int rank = 0, world = 1;
     bool allreduce = false;
     ncclComm_t comm = nullptr;
@@ -238,7 +239,7 @@ int enqueue_iteration(alll_ctx* c, hipEvent_t* marks, int variant) {
     } else {
         for (uint32_t r = 0; r < c->grid_rounds; ++r) {
             if (r == 0 && variant == 1) HIP_TRY(launch_round0_buckets(c->cv, c->b, c->grid_rounds == 1, fused, s));
-            else HIP_TRY(launch_round(c->cv, c->b, r, r + 1 == c->grid_rounds, s));
+            else HIP_TRY(launch_round(c->cv, c->b, r, r + 1 == c->grid_rounds, c->wave_round_min, s));
         }
         HIP_TRY(launch_tail(c->cv, c->b, c->grid_rounds, s));
     }
@@ -440,6 +441,26 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
             return fail(ALLL_ERR_LITERAL_RANGE, "literal %u at position %llu exceeds n_vars %u",
                         prob->literals[j], (unsigned long long)j, prob->n_vars);
 
+    // ---- hot variables (skewed degree: power-law hubs): degree >= max(1024, 32 x mean degree),
+    // at most HOT_MAX of the highest; flagged in bit 31 of every literal copy the device uses
+    std::vector<uint8_t> is_hot;
+    uint32_t n_hot = 0;
+    if (L && prob->n_vars && prob->n_vars < (1u << 30)) {
+        std::vector<uint32_t> deg(prob->n_vars, 0u);
+        for (uint64_t j = 0; j < L; ++j) ++deg[prob->literals[j] >> 1];
+        const uint64_t thr = std::max<uint64_t>(1024, 32 * (L / prob->n_vars + 1));
+        std::vector<std::pair<uint32_t, uint32_t>> hot;
+        for (uint32_t v = 0; v < prob->n_vars; ++v)
+            if (deg[v] >= thr) hot.push_back({deg[v], v});
+        if (!hot.empty()) {
+            std::sort(hot.rbegin(), hot.rend());
+            if (hot.size() > HOT_MAX) hot.resize(HOT_MAX);
+            is_hot.assign(prob->n_vars, 0);
+            for (auto& h : hot) is_hot[h.second] = 1;
+            n_hot = (uint32_t)hot.size();
+        }
+    }
+
     // ---- device
     int ndev = alll_device_count();
     if (ndev <= 0) return fail(ALLL_ERR_NO_DEVICE, "no HIP device visible");
@@ -467,6 +488,7 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     c->use_graph = (opt.flags & ALLL_FLAG_NO_GRAPH) == 0;
     c->grid_rounds = opt.grid_rounds ? opt.grid_rounds : DEFAULT_GRID_ROUNDS;
     if (const char* e = getenv("ALLL_FUSE_REDUCE")) c->fuse_reduce = atoi(e) != 0;
+    if (const char* e = getenv("ALLL_WAVE_ROUND_MIN")) c->wave_round_min = (uint32_t)atoi(e);  // A/B
     auto bail = [&](int rc) { alll_destroy(c); return rc; };
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
         return bail(fail(ALLL_ERR_HIP, "hipStreamCreate failed"));
@@ -529,7 +551,17 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     if ((rc = dalloc(c, &b.mis, (size_t)n_tiles * TILE))) return bail(rc);
     if ((rc = dalloc(c, &b.left, (size_t)n_tiles * TILE * ent_words))) return bail(rc);
     if ((rc = dalloc(c, &b.tmis, (size_t)n_tiles * TILE))) return bail(rc);
-    if ((rc = dalloc(c, &b.owner, (size_t)c->n_vars, 0xFF))) return bail(rc);
+    // skewed instances (hot variables): owner slots and round-0 buckets by vmix (alll_internal.h)
+    b.vmix_mul = 1u;
+    b.vmix_mask = 0xFFFFFFFFu;
+    uint64_t vrange = c->n_vars;  // owner slots / bucketed variable keys
+    if (n_hot && !getenv("ALLL_NO_VMIX")) {
+        vrange = 1024;
+        while (vrange < c->n_vars) vrange <<= 1;
+        b.vmix_mul = 0x9E3779B1u;
+        b.vmix_mask = (uint32_t)(vrange - 1);
+    }
+    if ((rc = dalloc(c, &b.owner, (size_t)vrange, 0xFF))) return bail(rc);
     if ((rc = dalloc(c, &b.cover, (size_t)b.n_words * 32))) return bail(rc);  // whole words, zero-padded
     if ((rc = dalloc(c, &b.tile_stats, 2 * (size_t)n_tiles))) return bail(rc);
     if ((rc = dalloc(c, &b.delta, b.n_words))) return bail(rc);
@@ -554,23 +586,29 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     // in LDS (else ~300-1000 power-of-2 buckets), runs of up to 16 tiles
     if (fixed_k > 0 && !(opt.flags & ALLL_FLAG_ATOMIC_CLAIMS) && n_tiles > 0 && c->n_vars > 0) {
         uint32_t shift = BKT_SHIFT_MIN;
-        while (shift < BKT_SHIFT_MAX && ((uint64_t)c->n_vars >> shift) > 384) ++shift;
-        uint64_t width = ((uint64_t)c->n_vars + c->n_cu - 1) / c->n_cu;
+        while (shift < BKT_SHIFT_MAX && (vrange >> shift) > 384) ++shift;
+        uint64_t width = (vrange + c->n_cu - 1) / c->n_cu;
         width = std::max<uint64_t>(width, 1u << BKT_SHIFT_MIN);
         if (width > (1u << BKT_SHIFT_MAX) || getenv("ALLL_BKT_POW2")) width = 1u << shift;
         if (const char* e = getenv("ALLL_BKT_SHIFT"))  // tuning experiments
             width = 1u << std::min<uint32_t>(BKT_SHIFT_MAX, std::max<uint32_t>(BKT_SHIFT_MIN, (uint32_t)atoi(e)));
-        const uint64_t nb = ((uint64_t)c->n_vars + width - 1) / width;
-        // skewed literal distribution (power-law hubs): the fullest bucket's workgroup would
-        // serialise the round; such instances keep the atomic claims (with hot-variable
-        // aggregation), which handle skew better
+        const uint64_t nb = (vrange + width - 1) / width;
+        // skewed pair load (a literal distribution whose hubs are not all flagged hot): the
+        // fullest bucket's workgroup would serialise the round; such instances keep the atomic
+        // claims.  Hot literals never become pairs (LDS hash + owner), and vmix spreads the
+        // remaining high-degree variables of power-law instances over the buckets.
         bool skewed = false;
         if (nb <= BKT_MAX) {
             std::vector<uint64_t> load(nb, 0);
-            const uint64_t L_all = prob->offsets[m];
-            for (uint64_t j = 0; j < L_all; ++j) ++load[(prob->literals[j] >> 1) / width];
+            uint64_t L_pairs = 0;
+            for (uint64_t j = 0; j < L; ++j) {
+                const uint32_t v = prob->literals[j] >> 1;
+                if (n_hot && is_hot[v]) continue;
+                ++load[((v * b.vmix_mul) & b.vmix_mask) / width];
+                ++L_pairs;
+            }
             const uint64_t mx = *std::max_element(load.begin(), load.end());
-            skewed = mx > 4 * (L_all / nb + 1);
+            skewed = mx > 4 * (L_pairs / nb + 1);
         }
         // about one run per CU (k_bscatter holds one 1024-thread workgroup per CU)
         uint32_t rt = std::max<uint32_t>(1, std::min<uint32_t>(RUN_TILES_MAX, (n_tiles + 255) / 256));
@@ -608,30 +646,18 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     if (hipStreamSynchronize(c->stream) != hipSuccess) return bail(fail(ALLL_ERR_HIP, "memset drain failed"));
 
     // ---- clauses: AoS literals (+ offsets or a chunk-transposed copy for fixed width k)
-    // hot variables: degree >= max(1024, 32 x mean degree), at most HOT_MAX of the highest;
-    // flagged in bit 31 of every literal copy the device uses
+    // hot variables (chosen above) flagged in bit 31 of every literal copy the device uses
     std::vector<uint32_t> flagged;
     {
-        if (L && c->n_vars && c->n_vars < (1u << 30)) {
-            std::vector<uint32_t> deg(c->n_vars, 0u);
-            for (uint64_t j = 0; j < L; ++j) ++deg[prob->literals[j] >> 1];
-            const uint64_t thr = std::max<uint64_t>(1024, 32 * (L / c->n_vars + 1));
-            std::vector<std::pair<uint32_t, uint32_t>> hot;
-            for (uint32_t v = 0; v < c->n_vars; ++v)
-                if (deg[v] >= thr) hot.push_back({deg[v], v});
-            if (!hot.empty()) {
-                std::sort(hot.rbegin(), hot.rend());
-                if (hot.size() > HOT_MAX) hot.resize(HOT_MAX);
-                std::vector<uint8_t> is_hot(c->n_vars, 0);
-                for (auto& h : hot) is_hot[h.second] = 1;
-                flagged.assign(prob->literals, prob->literals + L);
-                for (auto& l : flagged)
-                    if (is_hot[l >> 1]) l |= 0x80000000u;
-                cv.n_hot = (uint32_t)hot.size();
-                // skewed instances need more rounds before the leftovers are few enough for
-                // the single-workgroup tail (power-law 3-SAT at 10M clauses: 10 rounds)
-                if (!opt.grid_rounds) c->grid_rounds = SKEWED_GRID_ROUNDS;
-            }
+        if (n_hot) {
+            flagged.assign(prob->literals, prob->literals + L);
+            for (auto& l : flagged)
+                if (is_hot[l >> 1]) l |= 0x80000000u;
+            cv.n_hot = n_hot;
+            // skewed instances need more rounds before the leftovers are few enough for
+            // the single-workgroup tail (power-law 3-SAT at 10M clauses: 10 rounds)
+            if (!opt.grid_rounds) c->grid_rounds = SKEWED_GRID_ROUNDS;
+            if (!getenv("ALLL_WAVE_ROUND_MIN")) c->wave_round_min = WAVE_ROUND_MIN_HOT;
         }
         const uint32_t* src = flagged.empty() ? prob->literals : flagged.data();
         if (L && hipMemcpy(d_lits, src, L * 4, hipMemcpyHostToDevice) != hipSuccess)

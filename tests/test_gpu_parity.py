@@ -25,7 +25,9 @@ T1_FIXTURES = sorted(p for p in glob.glob(os.path.join(GOLDEN, "*_T1.npz")))
 # only for large violated sets, "buckets" forces it for every iteration
 LAYOUTS = {"hybrid": (0, {}), "fixed": (1 << 3, {}), "csr": (1 << 2, {}), "atomic_claims": (1 << 5, {}),
            "buckets": (0, {"ALLL_BUCKET_MIN_U": "0"}), "windows": (0, {"ALLL_EVAL_WINDOWS": "1"}),
-           "positions": (0, {"ALLL_PACKED_IDS": "0"})}
+           "positions": (0, {"ALLL_PACKED_IDS": "0"}),
+           # hot-variable instances without the owner/bucket spread (identity vmix)
+           "no_vmix": (0, {"ALLL_NO_VMIX": "1", "ALLL_BUCKET_MIN_U": "0"})}
 
 
 def make_solver(layout, monkeypatch, *args, **kw):
@@ -285,6 +287,8 @@ BIG = {
     "C2_3sat_4M": (1_000_000, 4_000_000, 3, 0),
     "C3_8sat_6M": (4_000_000, 6_000_000, 8, 0),
     "C5_powerlaw_10M": (2_500_000, 10_000_000, 3, 1),
+    # power-law with the atomic round 0 (the default policy buckets it while |U| is large)
+    "C5_atomic_round0": (2_500_000, 10_000_000, 3, 1, {"ALLL_BUCKET_MIN_U": str(1 << 62)}),
     "W_3sat_4Mvars": (4_000_000, 2_000_000, 3, 0),  # 4 LDS blocks of variables: windowed eval
     "M_no_windows": (2_500_000, 10_000_000, 3, 0, {"ALLL_EVAL_WINDOWS": "0"}),
     "M_positions": (2_500_000, 10_000_000, 3, 0, {"ALLL_PACKED_IDS": "0"}),  # perm translation

@@ -163,24 +163,32 @@ __global__ void k_init_assignment(uint32_t* A, uint32_t n_words, uint32_t n_vars
     A[w] = x;
 }
 
-// Entry of the clause at evaluation position p with lits_t slots t[0..K-1]: the clause id
-// (unpacked from the slots, or the position when ids are not packed; k_bscatter / CLAIM(0)
-// translate positions through perm) and the literals without the id bits.
+// Raw entry of the clause at evaluation position p with lits_t slots t[0..K-1], as the
+// evaluation writes it (no per-clause unpacking in the streaming kernel): {p, slots with their
+// packed id bits}.  The first LFMIS round-0 kernel (k_bscatter / CLAIM(0)) turns it into the
+// entry every later kernel reads (ent_unpack): {clause id, literals without id bits}.
 template <int K>
-__device__ __forceinline__ void make_ent(const ClauseView& cv, Ent<K>& e, uint64_t p, const uint32_t* t) {
+__device__ __forceinline__ void make_ent(Ent<K>& e, uint64_t p, const uint32_t* t) {
+    e.w[0] = (uint32_t)p;
+#pragma unroll
+    for (int j = 0; j < K; ++j) e.w[1 + j] = t[j];
+}
+
+// Raw entry -> {clause id, literals}: the id from the slots' packed bits, or perm[position]
+// when ids are not packed (cv.perm; a 4-byte gather).
+template <int K>
+__device__ __forceinline__ void ent_unpack(const ClauseView& cv, Ent<K>& e) {
     if (cv.id_bits) {
         const uint32_t fm = ((1u << cv.id_bits) - 1u) << cv.id_shift;
         uint32_t id = 0;
 #pragma unroll
         for (int j = 0; j < K; ++j) {
-            id |= ((t[j] & fm) >> cv.id_shift) << (j * cv.id_bits);
-            e.w[1 + j] = t[j] & ~fm;
+            id |= ((e.w[1 + j] & fm) >> cv.id_shift) << (j * cv.id_bits);
+            e.w[1 + j] &= ~fm;
         }
         e.w[0] = id;
-    } else {
-        e.w[0] = (uint32_t)p;
-#pragma unroll
-        for (int j = 0; j < K; ++j) e.w[1 + j] = t[j];
+    } else if (cv.perm) {
+        e.w[0] = cv.perm[e.w[0]];
     }
 }
 
@@ -199,7 +207,7 @@ __device__ __forceinline__ void emit4(const ClauseView& cv, uint32_t* list, uint
             t[j] = xs[q];
         }
         Ent<K> e;
-        make_ent<K>(cv, e, c0 + q, t);
+        make_ent<K>(e, c0 + q, t);
         store_ent<K>(list + (uint64_t)pos * Ent<K>::S, e);
         ++pos;
     }
@@ -313,8 +321,18 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
     // window of a tile (words; b.win_base: instances sorted by smallest-variable block, else 0)
     auto window = [&](uint32_t t) -> uint32_t { return b.win_base ? b.win_base[t] : 0u; };
     uint32_t wb = window(t0);
+    // zero word for lanes that need no LDS word (past every word the fill writes)
+    const uint32_t zslot = (lds_words + 3) / 4 * 4;
+    if (threadIdx.x == 0) s_A[zslot] = 0u;
     fill(wb);
-    const uint32_t* __restrict__ A = b.A;
+    // L2 lookups through a buffer descriptor over the assignment: its range check returns 0
+    // for the out-of-range offsets of lanes that need no L2 word
+    const uint32_t a_lo = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)b.A);
+    const uint32_t a_hi = __builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)b.A >> 32));
+    const uint32_t a_bytes = __builtin_amdgcn_readfirstlane(b.n_words * 4u);
+    const auto rsA = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(((uintptr_t)a_hi << 32) | a_lo), (short)0, (int)a_bytes, 0x00020000);
+    const uint32_t wbits = __popc(cv.lit_mask) - 6u;  // word-index bits of a literal
     for (uint32_t pt = t0; pt < t1; pt += HYB_MAX_TILES) {
         const uint32_t pe = min(t1, pt + HYB_MAX_TILES);
         if (threadIdx.x < HYB_MAX_TILES) s_tcnt[threadIdx.x] = 0;
@@ -354,41 +372,44 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
                     const int j = jj == 0 ? 0 : (jj == 1 ? K - 1 : jj - 1);
                     const bool first = jj == 0 || jj == 1;
                     const uint32_t xs[4] = {x[j].x, x[j].y, x[j].z, x[j].w};
-                    uint32_t wi[4], gw[4], lw[4];
-                    bool need[4], useg[4];
+                    // Branch-free lookups: every lane issues one buffer load and one LDS read
+                    // per clause.  A word the lane does not need from L2 (in the window, or the
+                    // clause already satisfied) gets an out-of-range buffer offset, which the
+                    // range check turns into 0 without a memory access; a word it does not need
+                    // from LDS reads the zero word s_A[zslot].  So w = global | LDS word.  A
+                    // lane that needs no lookup is already satisfied, so its bit is ignored.
+                    uint32_t gw[4], lw[4];
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
-                        wi[q] = (xs[q] & cv.lit_mask) >> 6;
-                        need[q] = first || !sat[q];
-                        useg[q] = need[q] && wi[q] - wb >= lds_words;  // (unsigned: below the window too)
+                        const uint32_t wi = __builtin_amdgcn_ubfe(xs[q], 6u, wbits);
+                        const uint32_t d = wi - wb;  // (unsigned: below the window too)
+                        const bool need = first || !(sat[q] & 1u);
+                        const bool inl = d < lds_words;
+                        gw[q] = __builtin_amdgcn_raw_buffer_load_b32(rsA, (need && !inl) ? wi * 4u : 0x80000000u, 0, 0);
+                        lw[q] = s_A[(need && inl) ? d : zslot];
                     }
+                    // bit 0 of sat: clause satisfied (the literal's value is its variable's bit
+                    // xor the sign, bit 0 of the literal; the other bits of sat are don't-care)
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        gw[q] = 0;
-                        if (useg[q]) gw[q] = A[wi[q]];
-                    }
-#pragma unroll
-                    for (int q = 0; q < 4; ++q)  // (unconditional: lanes that need no LDS word read word 0)
-                        lw[q] = s_A[need[q] && !useg[q] ? wi[q] - wb : 0u];
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const uint32_t w = useg[q] ? gw[q] : lw[q];
-                        const uint32_t bit = ((w >> ((xs[q] >> 1) & 31u)) & 1u) ^ (xs[q] & 1u);
-                        sat[q] |= need[q] ? bit : 0u;
-                    }
+                    for (int q = 0; q < 4; ++q)
+                        sat[q] |= __builtin_amdgcn_ubfe(gw[q] | lw[q], xs[q] >> 1, 1u) ^ xs[q];
                 }
             }
             const uint64_t c0 = cb + 4u * lane;
             bool v[4];
             if (cb + CHUNK <= m) {  // (wave-uniform: only the last chunk holds positions past m)
 #pragma unroll
-                for (int q = 0; q < 4; ++q) v[q] = !sat[q];
+                for (int q = 0; q < 4; ++q) v[q] = !(sat[q] & 1u);
             } else {
 #pragma unroll
-                for (int q = 0; q < 4; ++q) v[q] = !sat[q] && c0 + q < m;
+                for (int q = 0; q < 4; ++q) v[q] = !(sat[q] & 1u) && c0 + q < m;
             }
             const uint64_t b0 = __ballot(v[0]), b1 = __ballot(v[1]), b2 = __ballot(v[2]), b3 = __ballot(v[3]);
-            if (lane < 4) b.vmask[g * 4 + lane] = lane == 0 ? b0 : lane == 1 ? b1 : lane == 2 ? b2 : b3;
+            if (lane == 0) {  // the chunk's four bitmask words, 32 aligned bytes
+                uint4* vm = reinterpret_cast<uint4*>(b.vmask + g * 4);
+                vm[0] = make_uint4((uint32_t)b0, (uint32_t)(b0 >> 32), (uint32_t)b1, (uint32_t)(b1 >> 32));
+                vm[1] = make_uint4((uint32_t)b2, (uint32_t)(b2 >> 32), (uint32_t)b3, (uint32_t)(b3 >> 32));
+            }
             const uint32_t tot = __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
             if (tot) {
                 const uint32_t tile = (uint32_t)(g / (TILE / CHUNK));
@@ -500,7 +521,7 @@ __global__ __launch_bounds__(EVAL_THREADS) void k_collect(ClauseView cv, LoopBuf
             uint32_t t[K];
 #pragma unroll
             for (int j = 0; j < K; ++j) t[j] = tp[j * CHUNK];
-            make_ent<K>(cv, e, p, t);
+            make_ent<K>(e, p, t);
         } else {
             e.w[0] = (uint32_t)p;
         }
@@ -681,9 +702,9 @@ __global__ __launch_bounds__(ROUND_THREADS) void k_claim(ClauseView cv, LoopBuff
     for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
         Ent<K> e;
         load_ent<K>(e, lin + (uint64_t)i * S);
-        if (r == 0 && cv.perm) {
-            e.w[0] = cv.perm[e.w[0]];
-            lin[(uint64_t)i * S] = e.w[0];
+        if (K > 0 && r == 0 && (cv.id_bits || cv.perm)) {  // raw entry from the evaluation
+            ent_unpack<K>(cv, e);
+            store_ent<K>(lin + (uint64_t)i * S, e);
         }
         uint64_t lb;
         const uint32_t len = ent_len<K>(cv, e, lb);
@@ -1038,8 +1059,14 @@ __global__ __launch_bounds__(BSC_THREADS) void k_bscatter(ClauseView cv, LoopBuf
     // flight), clause ids (written back), hot claims
     for (uint32_t f0 = threadIdx.x; f0 < E; f0 += blockDim.x * U) {
         load_run_entries<K, U>(list, t0, nt, s_pre, E, f0, e, ok, tts, idx);
+        // raw entries from the evaluation: packed ids are unpacked here (ALU); without packed
+        // ids the perm loads are issued first and land while the histogram runs
         uint32_t id[U];
-        if (cv.perm) {
+        if (cv.id_bits) {
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (ok[u]) ent_unpack<K>(cv, e[u]);
+        } else if (cv.perm) {
 #pragma unroll
             for (int u = 0; u < U; ++u) id[u] = ok[u] ? cv.perm[e[u].w[0]] : 0u;
         }
@@ -1053,7 +1080,11 @@ __global__ __launch_bounds__(BSC_THREADS) void k_bscatter(ClauseView cv, LoopBuf
                 if (!(hot && (raw & LIT_HOT))) atomicAdd(&s_hist[bucket_of(b, lit_var(raw), off)], 1u);
             }
         }
-        if (cv.perm) {
+        if (cv.id_bits) {  // the unpacked entries replace the raw ones (k_bjoin reads them)
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (ok[u]) store_ent<K>(list + ((uint64_t)(t0 + tts[u]) * TILE + idx[u]) * S, e[u]);
+        } else if (cv.perm) {
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 if (!ok[u]) continue;
@@ -2228,14 +2259,15 @@ hipError_t launch_eval_hybrid(const ClauseView& cv, const LoopBuffers& b, uint32
     if (tile_end <= tile_begin) return hipSuccess;
     const uint32_t nt = tile_end - tile_begin;
     const dim3 grid(std::min<uint32_t>(nt, (uint32_t)std::max(1, n_blocks)));
-    const size_t lds = (size_t)std::max<uint32_t>(4, (std::min(b.n_words, b.win_words) + 3) / 4 * 4) * 4;
+    // window words (a multiple of 4) + the zero word (a 16-byte slot)
+    const size_t lds = ((size_t)(std::min(b.n_words, b.win_words) + 3) / 4 * 4 + 4) * 4;
     const int g = gated ? 1 : 0;
     int dev;
     if (cv.k >= 1 && cv.k <= (uint32_t)MAX_FIXED_K && attr_pending(ATTR_HYBRID + cv.k, dev)) {
         hipError_t e = hipSuccess;
         ALLL_DISPATCH_K(cv.k, (e = hipFuncSetAttribute((const void*)k_eval_hybrid<(K > 0 ? K : 1)>,
                                                        hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                       (int)(LDS_WORDS * 4))));
+                                                       (int)(LDS_WORDS * 4 + 16))));
         if (e != hipSuccess) return e;
         attr_mark(ATTR_HYBRID + cv.k, dev);
     }

@@ -299,7 +299,6 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
     if (t0 >= t1) return;
     stamp_eval_begin(b, gated);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     const uint64_t m = cv.m;
     const uint32_t lds_words = min(b.n_words, b.win_words);
     // LDS-DMA fill of assignment words [wb, wb + lds_words) (global_load_lds_dwordx4: no VGPR
@@ -396,14 +395,11 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
                 }
             }
             const uint64_t c0 = cb + 4u * lane;
+            // (wave-uniform: only the last chunk holds positions past m)
+            const uint32_t lim = (uint32_t)min((uint64_t)CHUNK, m - cb);
             bool v[4];
-            if (cb + CHUNK <= m) {  // (wave-uniform: only the last chunk holds positions past m)
 #pragma unroll
-                for (int q = 0; q < 4; ++q) v[q] = !(sat[q] & 1u);
-            } else {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) v[q] = !(sat[q] & 1u) && c0 + q < m;
-            }
+            for (int q = 0; q < 4; ++q) v[q] = !(sat[q] & 1u) && 4u * lane + q < lim;
             const uint64_t b0 = __ballot(v[0]), b1 = __ballot(v[1]), b2 = __ballot(v[2]), b3 = __ballot(v[3]);
             if (lane == 0) {  // the chunk's four bitmask words, 32 aligned bytes
                 uint4* vm = reinterpret_cast<uint4*>(b.vmask + g * 4);
@@ -415,9 +411,14 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
                 const uint32_t tile = (uint32_t)(g / (TILE / CHUNK));
                 uint32_t base = 0;
                 if (lane == 0) base = atomicAdd(&s_tcnt[tile - pt], tot);
-                base = __shfl(base, 0, 64);
-                const uint32_t pre = __popcll(b0 & lt) + __popcll(b1 & lt) + __popcll(b2 & lt) +
-                                     __popcll(b3 & lt);
+                base = __builtin_amdgcn_readfirstlane(base);  // (every lane is active here)
+                // rank of the lane's first violated clause: set bits of the four ballots below
+                // the lane (mbcnt chain)
+                uint32_t pre = 0;
+                pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(b0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b0, pre));
+                pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(b1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b1, pre));
+                pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(b2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b2, pre));
+                pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(b3 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b3, pre));
                 emit4<K>(cv, b.stage[0] + (uint64_t)tile * TILE * Ent<K>::S, base + pre, c0, v, x);
             }
         }

@@ -89,6 +89,15 @@ struct ClauseView {
     uint32_t lit_mask;      // lits_t literal bits (LIT_MASK when ids are not packed)
     uint32_t id_shift;      // = bit width of the literals when packed
     uint32_t id_bits;       // id bits per slot; 0 = not packed (entries carry positions)
+    // Ragged widths (generic CSR entries, T = 1, not streaming): the evaluation reads a
+    // chunk-transposed copy instead of the CSR arrays.  Clauses are evaluated sorted by width
+    // (then by the block of their smallest variable and their largest variable; perm maps
+    // positions to clause ids), chunk g of 256 positions holds w_g = rg_off[g+1] - rg_off[g]
+    // slots [slot j][256] from word 256 * rg_off[g] of rg_lits, each clause's literals by
+    // descending variable and padded with an always-false literal (variable 32 * n_words,
+    // past the assignment: its buffer load is out of range and reads 0).  nullptr = CSR eval.
+    const uint32_t* rg_off;
+    const uint32_t* rg_lits;
 };
 
 struct LoopBuffers {
@@ -157,6 +166,8 @@ hipError_t launch_set_limits(const LoopBuffers& b, uint64_t n, hipStream_t s);
 hipError_t launch_eval(const ClauseView& cv, const LoopBuffers& b, uint32_t tile_begin,
                        uint32_t tile_end, bool gated, hipStream_t s);
 hipError_t launch_eval_hybrid(const ClauseView& cv, const LoopBuffers& b, uint32_t tile_begin,
+                              uint32_t tile_end, bool gated, int n_blocks, hipStream_t s);
+hipError_t launch_eval_ragged(const ClauseView& cv, const LoopBuffers& b, uint32_t tile_begin,
                               uint32_t tile_end, bool gated, int n_blocks, hipStream_t s);
 hipError_t launch_collect(const ClauseView& cv, const LoopBuffers& b, uint32_t own_begin,
                           uint32_t own_end, hipStream_t s);

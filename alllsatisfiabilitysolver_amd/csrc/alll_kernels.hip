@@ -432,6 +432,139 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
     stamp_eval_end(b, gated);
 }
 
+// Clause evaluation, ragged widths (ClauseView::rg_off): the persistent LDS-window structure
+// of k_eval_hybrid over the chunk-transposed ragged copy.  A chunk's width w (its widest
+// clause; clauses are evaluated sorted by width, so chunks are nearly uniform) is wave-uniform;
+// its slots are read RG_BATCH at a time (one 16-byte load per slot: 4 clauses per lane) and the
+// chunk stops early once every one of its 256 clauses is satisfied.  Violated clauses go to the
+// per-tile lists as evaluation positions (generic entries, one word); CLAIM(0) translates them
+// through perm.  The bitmask has the four-ballots-per-chunk layout of the fixed-width kernels.
+constexpr uint32_t RG_BATCH = 4;
+
+__global__ __launch_bounds__(HYB_THREADS) void k_eval_ragged(ClauseView cv, LoopBuffers b, uint32_t tile_begin,
+                                                             uint32_t tile_end, int gated) {
+    if (gated && eval_gate_closed(b.state)) return;
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_A[];
+    __shared__ uint32_t s_tcnt[HYB_MAX_TILES];
+    const uint32_t nblk = gridDim.x;
+    const uint32_t ntiles = tile_end - tile_begin;
+    const uint32_t t0 = tile_begin + (uint32_t)(((uint64_t)ntiles * blockIdx.x) / nblk);
+    const uint32_t t1 = tile_begin + (uint32_t)(((uint64_t)ntiles * (blockIdx.x + 1)) / nblk);
+    if (t0 >= t1) return;
+    stamp_eval_begin(b, gated);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint64_t m = cv.m;
+    const uint32_t lds_words = min(b.n_words, b.win_words);
+    auto fill = [&](uint32_t wb) {
+        const uint32_t n4 = (lds_words + 3) / 4;
+        const uint4* src = reinterpret_cast<const uint4*>(b.A + wb);
+        const uint32_t wbase = __builtin_amdgcn_readfirstlane(wave * 64);
+        for (uint32_t q0 = 0; q0 < n4; q0 += HYB_THREADS) {
+            const uint32_t q = q0 + threadIdx.x;
+            if (q < n4)
+                __builtin_amdgcn_global_load_lds(
+                    (const __attribute__((address_space(1))) void*)(src + q),
+                    (__attribute__((address_space(3))) void*)(reinterpret_cast<uint4*>(s_A) + q0 + wbase),
+                    16, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    };
+    auto window = [&](uint32_t t) -> uint32_t { return b.win_base ? b.win_base[t] : 0u; };
+    uint32_t wb = window(t0);
+    const uint32_t zslot = (lds_words + 3) / 4 * 4;
+    if (threadIdx.x == 0) s_A[zslot] = 0u;
+    fill(wb);
+    const uint32_t a_lo = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)b.A);
+    const uint32_t a_hi = __builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)b.A >> 32));
+    const uint32_t a_bytes = __builtin_amdgcn_readfirstlane(b.n_words * 4u);
+    const auto rsA = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(((uintptr_t)a_hi << 32) | a_lo), (short)0, (int)a_bytes, 0x00020000);
+    for (uint32_t pt = t0; pt < t1; pt += HYB_MAX_TILES) {
+        const uint32_t pe = min(t1, pt + HYB_MAX_TILES);
+        if (threadIdx.x < HYB_MAX_TILES) s_tcnt[threadIdx.x] = 0;
+        __syncthreads();
+      for (uint32_t sa = pt; sa < pe;) {
+        const uint32_t ws = window(sa);
+        uint32_t se = sa + 1;
+        while (se < pe && window(se) == ws) ++se;
+        if (ws != wb) {
+            __syncthreads();
+            fill(ws);
+            __syncthreads();
+            wb = ws;
+        }
+        const uint64_t gbeg = (uint64_t)sa * (TILE / CHUNK);
+        const uint64_t gend = min((uint64_t)se * (TILE / CHUNK), (m + CHUNK - 1) / CHUNK);
+        sa = se;
+        for (uint64_t g = gbeg + wave; g < gend; g += HYB_THREADS / 64) {
+            const uint64_t cb = g * CHUNK;
+            const uint32_t o0 = __builtin_amdgcn_readfirstlane(cv.rg_off[g]);
+            const uint32_t w = __builtin_amdgcn_readfirstlane(cv.rg_off[g + 1]) - o0;
+            const uint4* src = reinterpret_cast<const uint4*>(cv.rg_lits + (uint64_t)o0 * CHUNK) + lane;
+            uint32_t sat[4] = {0u, 0u, 0u, 0u};  // bit 0: clause satisfied (as k_eval_hybrid)
+            for (uint32_t j0 = 0; j0 < w; j0 += RG_BATCH) {
+                uint4 x[RG_BATCH];
+#pragma unroll
+                for (uint32_t u = 0; u < RG_BATCH; ++u)
+                    x[u] = j0 + u < w ? src[(j0 + u) * 64] : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+                for (uint32_t u = 0; u < RG_BATCH; ++u) {
+                    if (j0 + u >= w) break;  // (wave-uniform)
+                    const uint32_t xs[4] = {x[u].x, x[u].y, x[u].z, x[u].w};
+                    uint32_t gw[4], lw[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const uint32_t wi = __builtin_amdgcn_ubfe(xs[q], 6u, 25u);  // (bit 31: hot flag)
+                        const uint32_t d = wi - wb;
+                        const bool need = !(sat[q] & 1u);
+                        const bool inl = d < lds_words;
+                        gw[q] = __builtin_amdgcn_raw_buffer_load_b32(rsA, (need && !inl) ? wi * 4u : 0x80000000u, 0, 0);
+                        lw[q] = s_A[(need && inl) ? d : zslot];
+                    }
+#pragma unroll
+                    for (int q = 0; q < 4; ++q)
+                        sat[q] |= __builtin_amdgcn_ubfe(gw[q] | lw[q], xs[q] >> 1, 1u) ^ xs[q];
+                }
+                if (!__any(!((sat[0] & sat[1] & sat[2] & sat[3]) & 1u))) break;  // chunk satisfied
+            }
+            const uint64_t c0 = cb + 4u * lane;
+            const uint32_t lim = (uint32_t)min((uint64_t)CHUNK, m - cb);
+            bool v[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = !(sat[q] & 1u) && 4u * lane + q < lim;
+            const uint64_t b0 = __ballot(v[0]), b1 = __ballot(v[1]), b2 = __ballot(v[2]), b3 = __ballot(v[3]);
+            if (lane == 0) {
+                uint4* vm = reinterpret_cast<uint4*>(b.vmask + g * 4);
+                vm[0] = make_uint4((uint32_t)b0, (uint32_t)(b0 >> 32), (uint32_t)b1, (uint32_t)(b1 >> 32));
+                vm[1] = make_uint4((uint32_t)b2, (uint32_t)(b2 >> 32), (uint32_t)b3, (uint32_t)(b3 >> 32));
+            }
+            const uint32_t tot = __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
+            if (tot) {
+                const uint32_t tile = (uint32_t)(g / (TILE / CHUNK));
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(&s_tcnt[tile - pt], tot);
+                base = __builtin_amdgcn_readfirstlane(base);
+                uint32_t pre = 0;
+                pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(b0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b0, pre));
+                pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(b1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b1, pre));
+                pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(b2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b2, pre));
+                pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(b3 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b3, pre));
+                uint32_t* list = b.stage[0] + (uint64_t)tile * TILE + base + pre;
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+                    if (v[q]) *list++ = (uint32_t)(c0 + q);
+            }
+        }
+      }
+        __syncthreads();
+        if (threadIdx.x < pe - pt) {
+            b.tile_cnt[pt + threadIdx.x] = s_tcnt[threadIdx.x];
+            b.mis_cnt[pt + threadIdx.x] = 0;
+        }
+    }
+    stamp_eval_end(b, gated);
+}
+
 // Clause evaluation, generic CSR (ragged widths): lane per clause, 64 consecutive
 // clauses per wave step, 16 steps per wave, one tile per workgroup.
 __global__ __launch_bounds__(EVAL_THREADS) void k_eval_csr(ClauseView cv, LoopBuffers b,
@@ -513,9 +646,9 @@ __global__ __launch_bounds__(EVAL_THREADS) void k_collect(ClauseView cv, LoopBuf
     while (bits) {
         const uint32_t i = sl + (uint32_t)__ffs(bits) - 1u;
         bits &= bits - 1u;
-        // fixed K: word w of the bitmask holds positions (w / 4) * 256 + 4 * bit + w % 4
-        // (k_eval_* store their four ballots as they are); CSR: positions 64 * w + bit
-        const uint64_t p = K > 0 ? (w >> 2) * CHUNK + 4u * i + (w & 3u) : w * 64 + i;
+        // fixed K and ragged: word w of the bitmask holds positions (w / 4) * 256 + 4 * bit +
+        // w % 4 (the kernels store their four ballots as they are); CSR: positions 64 * w + bit
+        const uint64_t p = (K > 0 || cv.rg_off) ? (w >> 2) * CHUNK + 4u * i + (w & 3u) : w * 64 + i;
         Ent<K> e;
         if constexpr (K > 0) {
             const uint32_t* tp = cv.lits_t + (p / CHUNK) * CHUNK * K + (p % CHUNK);
@@ -703,7 +836,7 @@ __global__ __launch_bounds__(ROUND_THREADS) void k_claim(ClauseView cv, LoopBuff
     for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
         Ent<K> e;
         load_ent<K>(e, lin + (uint64_t)i * S);
-        if (K > 0 && r == 0 && (cv.id_bits || cv.perm)) {  // raw entry from the evaluation
+        if (r == 0 && (cv.id_bits || cv.perm)) {  // raw entry from the evaluation
             ent_unpack<K>(cv, e);
             store_ent<K>(lin + (uint64_t)i * S, e);
         }
@@ -2243,7 +2376,7 @@ hipError_t launch_eval(const ClauseView& cv, const LoopBuffers& b, uint32_t tile
 // and device records what is set (contexts on several devices may share a process).
 constexpr int ATTR_MAX_DEV = 64;
 static std::atomic<uint32_t> g_attr_done[ATTR_MAX_DEV];
-enum : uint32_t { ATTR_HYBRID = 0, ATTR_BUCKETS = 9, ATTR_RR = 18 };  // + k for per-width groups
+enum : uint32_t { ATTR_HYBRID = 0, ATTR_BUCKETS = 9, ATTR_RR = 18, ATTR_RAGGED = 30 };  // + k for per-width groups
 static bool attr_pending(uint32_t bit, int& dev) {
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= ATTR_MAX_DEV) {
         dev = -1;
@@ -2283,6 +2416,23 @@ hipError_t launch_eval_hybrid(const ClauseView& cv, const LoopBuffers& b, uint32
         case 8: k_eval_hybrid<8><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g); break;
         default: return hipErrorInvalidValue;
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_eval_ragged(const ClauseView& cv, const LoopBuffers& b, uint32_t tile_begin,
+                              uint32_t tile_end, bool gated, int n_blocks, hipStream_t s) {
+    if (tile_end <= tile_begin) return hipSuccess;
+    const uint32_t nt = tile_end - tile_begin;
+    const dim3 grid(std::min<uint32_t>(nt, (uint32_t)std::max(1, n_blocks)));
+    const size_t lds = ((size_t)(std::min(b.n_words, b.win_words) + 3) / 4 * 4 + 4) * 4;
+    int dev;
+    if (attr_pending(ATTR_RAGGED, dev)) {
+        hipError_t e = hipFuncSetAttribute((const void*)k_eval_ragged, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)(LDS_WORDS * 4 + 16));
+        if (e != hipSuccess) return e;
+        attr_mark(ATTR_RAGGED, dev);
+    }
+    k_eval_ragged<<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, gated ? 1 : 0);
     return hipGetLastError();
 }
 

@@ -157,6 +157,103 @@ int dalloc(alll_ctx* c, T** p, size_t count, int fill = 0) {
     return ALLL_OK;
 }
 
+// Ragged-width evaluation layout (ClauseView::rg_off, k_eval_ragged): inside every shard the
+// clauses are evaluated sorted by (width, block of the smallest variable, largest variable),
+// so a chunk's 256 clauses share one width and the slot-0 lookups of a wave fall on few
+// lines; every clause's literals are stored by descending variable (its smallest variable,
+// looked up last, lies in the tile's LDS window) and padded to its chunk's width with an
+// always-false literal.  perm maps positions to clause ids (CLAIM(0) translates the
+// evaluation's positions; alll_get_violated_mask reorders the bitmask on the host).
+int build_ragged(alll_ctx* c, const alll_problem* prob) {
+    const uint64_t m = c->m;
+    const uint64_t* offs = prob->offsets;
+    const uint32_t* lits = prob->literals;
+    LoopBuffers& b = c->b;
+    ClauseView& cv = c->cv;
+    const uint64_t win_vars = (uint64_t)b.win_words * 32;
+    bool windows = c->n_vars > win_vars;
+    if (const char* e = getenv("ALLL_EVAL_WINDOWS")) windows = atoi(e) != 0;
+    const unsigned nt = host_threads();
+    std::vector<uint32_t>& perm = c->perm;
+    perm.resize(m);
+    struct Key { uint64_t k1; uint32_t id; };
+    auto key_of = [&](uint64_t cl) -> Key {
+        uint32_t hi = 0, lo = ~0u;
+        for (uint64_t j = offs[cl]; j < offs[cl + 1]; ++j) {
+            const uint32_t v = lits[j] >> 1;
+            hi = std::max(hi, v);
+            lo = std::min(lo, v);
+        }
+        const uint64_t w = std::min<uint64_t>(offs[cl + 1] - offs[cl], (1u << 20) - 1);
+        const uint64_t blk = (windows && lo != ~0u) ? std::min<uint64_t>(lo / win_vars, 1023) : 0;
+        return {(w << 40) | (blk << 30) | (hi & ((1u << 30) - 1)), (uint32_t)cl};
+    };
+    for (int r = 0; r < c->world; ++r) {  // every shard sorted on its own (shards are clause ranges)
+        const uint64_t cb0 = std::min<uint64_t>(m, (uint64_t)r * c->tiles_per_rank * TILE);
+        const uint64_t ce0 = std::min<uint64_t>(m, cb0 + (uint64_t)c->tiles_per_rank * TILE);
+        if (ce0 <= cb0) continue;
+        std::vector<Key> kv(ce0 - cb0);
+        parallel_for(ce0 - cb0, nt, [&](uint64_t i) { kv[i] = key_of(cb0 + i); });
+        parallel_sort(kv.data(), kv.size(), [](const Key& x, const Key& y) {
+            return x.k1 != y.k1 ? x.k1 < y.k1 : x.id < y.id;
+        }, nt);
+        parallel_for(kv.size(), nt, [&](uint64_t i) { perm[cb0 + i] = kv[i].id; });
+    }
+    // chunk widths and offsets (units of CHUNK words)
+    const uint64_t n_chunks = (m + CHUNK - 1) / CHUNK;
+    std::vector<uint32_t> off(n_chunks + 1, 0u);
+    uint64_t acc = 0;
+    for (uint64_t g = 0; g < n_chunks; ++g) {
+        uint64_t w = 0;
+        for (uint64_t p = g * CHUNK; p < std::min<uint64_t>(m, (g + 1) * CHUNK); ++p)
+            w = std::max<uint64_t>(w, offs[perm[p] + 1] - offs[perm[p]]);
+        off[g] = (uint32_t)acc;
+        acc += w;
+        if (acc >= (1ull << 32)) return fail(ALLL_ERR_UNSUPPORTED, "ragged layout exceeds 2^32 chunk slots");
+    }
+    off[n_chunks] = (uint32_t)acc;
+    const uint32_t false_lit = 64u * b.n_words;  // variable 32 * n_words: its word is out of range
+    std::vector<uint32_t> t((size_t)acc * CHUNK, false_lit);
+    parallel_for(m, nt, [&](uint64_t p) {
+        const uint64_t cl = perm[p], g = p / CHUNK, r = p % CHUNK;
+        const uint64_t w = offs[cl + 1] - offs[cl];
+        std::vector<uint32_t> tmp(lits + offs[cl], lits + offs[cl] + w);
+        std::sort(tmp.begin(), tmp.end(), [](uint32_t x, uint32_t y) { return (x >> 1) > (y >> 1); });
+        uint32_t* dst = t.data() + (size_t)off[g] * CHUNK + r;
+        for (uint64_t j = 0; j < w; ++j) dst[j * CHUNK] = tmp[j];
+    });
+    uint32_t *d_off = nullptr, *d_lits = nullptr, *d_perm = nullptr, *d_wb = nullptr;
+    int rc;
+    if ((rc = dalloc(c, &d_off, n_chunks + 1)) || (rc = dalloc(c, &d_lits, t.size())) || (rc = dalloc(c, &d_perm, m)))
+        return rc;
+    std::vector<uint32_t> wb;
+    if (windows) {
+        const uint32_t lds_words = std::min<uint32_t>(b.n_words, b.win_words);
+        wb.assign(b.n_tiles, 0u);
+        for (uint32_t tt = 0; tt < b.n_tiles; ++tt) {
+            const uint64_t p = (uint64_t)tt * TILE;
+            if (p >= m) break;
+            const uint64_t cl = perm[p];
+            uint32_t lo = ~0u;
+            for (uint64_t j = offs[cl]; j < offs[cl + 1]; ++j) lo = std::min(lo, lits[j] >> 1);
+            if (lo == ~0u) lo = 0;
+            wb[tt] = std::min<uint64_t>((uint64_t)(lo / win_vars) * b.win_words, b.n_words - lds_words);
+        }
+        if ((rc = dalloc(c, &d_wb, b.n_tiles))) return rc;
+    }
+    if (hipStreamSynchronize(c->stream) != hipSuccess ||
+        hipMemcpy(d_off, off.data(), off.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        (!t.empty() && hipMemcpy(d_lits, t.data(), t.size() * 4, hipMemcpyHostToDevice) != hipSuccess) ||
+        hipMemcpy(d_perm, perm.data(), m * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        (d_wb && hipMemcpy(d_wb, wb.data(), wb.size() * 4, hipMemcpyHostToDevice) != hipSuccess))
+        return fail(ALLL_ERR_HIP, "ragged layout upload failed");
+    cv.rg_off = d_off;
+    cv.rg_lits = d_lits;
+    cv.perm = d_perm;
+    if (d_wb) b.win_base = d_wb;
+    return ALLL_OK;
+}
+
 int read_state(alll_ctx* c) {
     HIP_TRY(hipMemcpyAsync(c->h_state, c->b.state, sizeof(DevState), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -178,6 +275,7 @@ int write_limits(alll_ctx* c, uint64_t limit_eval, uint64_t limit_nores) {
 }
 
 hipError_t eval_launch(alll_ctx* c, uint32_t tb, uint32_t te, bool gated) {
+    if (c->cv.rg_off) return launch_eval_ragged(c->cv, c->b, tb, te, gated, c->n_cu, c->stream);
     if (c->hybrid) {
         int grid = c->n_cu * c->eval_wgs;
         if (const char* e = getenv("ALLL_EVAL_GRID")) grid = atoi(e);  // tuning experiments
@@ -779,6 +877,12 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
         if (hipMemcpy(d_o, o32.data(), (m + 1) * 4, hipMemcpyHostToDevice) != hipSuccess)
             return bail(fail(ALLL_ERR_HIP, "offset upload failed"));
         cv.offs = d_o;
+        // Ragged widths, T = 1, not streaming: chunk-transposed copy for k_eval_ragged (the
+        // CSR arrays above stay: the LFMIS kernels read clauses by id).  ALLL_FLAG_GENERIC_CSR
+        // keeps the clause-order CSR evaluation.
+        const bool ragged = m && !rr_T && !opt.stream_batch && !(opt.flags & ALLL_FLAG_GENERIC_CSR) &&
+                            c->n_vars < (1u << 30) && !getenv("ALLL_NO_RAGGED");
+        if (ragged && (rc = build_ragged(c, prob))) return bail(rc);
     }
 
     // ---- state + initial assignment
@@ -808,7 +912,8 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
         return bail(fail(ALLL_ERR_HIP, "create: stream sync failed: %s", hipGetErrorString(hipGetLastError())));
     c->hybrid = cv.k > 0 && !(opt.flags & ALLL_FLAG_NO_RANGED);
     char nm[64];
-    if (c->hybrid) snprintf(nm, sizeof nm, "k_eval_hybrid<%u>", cv.k);
+    if (cv.rg_off) snprintf(nm, sizeof nm, "k_eval_ragged");
+    else if (c->hybrid) snprintf(nm, sizeof nm, "k_eval_hybrid<%u>", cv.k);
     else if (cv.k) snprintf(nm, sizeof nm, "k_eval_fixed<%u>", cv.k);
     else snprintf(nm, sizeof nm, "k_eval_csr");
     c->eval_name = nm;

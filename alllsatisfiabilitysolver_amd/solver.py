@@ -39,6 +39,20 @@ def generate_ksat(gen_seed: int, n_vars: int, n_clauses: int, k: int, kind: int 
     return offs, lits
 
 
+def generate_mixed(gen_seed: int, n_vars: int, n_clauses: int, w_min: int, w_max: int):
+    """Random clauses of mixed widths (uniform in [w_min, w_max]), variables and signs uniform
+    (a variable may repeat inside a clause, as DIMACS allows).  Returns (offsets uint64[m+1],
+    literals uint32[L]); deterministic for a seed (numpy PCG64)."""
+    rng = np.random.default_rng(gen_seed)
+    w = rng.integers(w_min, w_max + 1, n_clauses, dtype=np.int64)
+    offs = np.zeros(n_clauses + 1, np.uint64)
+    np.cumsum(w, out=offs[1:])
+    L = int(offs[-1])
+    v = rng.integers(0, n_vars, L, dtype=np.uint32)
+    sgn = rng.integers(0, 2, L, dtype=np.uint32)
+    return offs, (v << np.uint32(1)) | sgn
+
+
 def parse_dimacs(text: bytes):
     """DIMACS text -> (n_vars, offsets, literals) with the reference loader semantics."""
     L = N.lib()

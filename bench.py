@@ -14,7 +14,7 @@ size is fixed (strong scaling).  Under torch.distributed.run the ranks come from
 environment; `python bench.py --gpus N` alone starts the N ranks itself.  An RCCL failure is
 fatal; the host-staged gloo exchange is only used with --exchange-impl host.
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config M|C2|C3|C4|C5]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config M|C2|C3|C4|C5|R]
 """
 import argparse
 import json
@@ -36,6 +36,8 @@ CONFIGS = {
     "C3": (4_000_000, 6_000_000, 8, 0, "random 8-SAT m/n 1.5, 4M vars / 6M clauses"),
     "C4": (32_000_000, 128_000_000, 3, 0, "random 3-SAT ratio 4, 32M vars / 128M clauses"),
     "C5": (2_500_000, 10_000_000, 3, 1, "power-law (beta 0.8) 3-SAT, 2.5M vars / 10M clauses"),
+    # ragged widths (DIMACS-like mixed clause lengths): the chunk-transposed ragged evaluation
+    "R": (1_000_000, 4_000_000, (2, 12), 0, "mixed widths 2-12 (uniform), 1M vars / 4M clauses"),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 
@@ -93,6 +95,9 @@ def cpu_baseline(cfg, budget_s):
     sources) on the host cores: full resample iterations on bounded samples of the same
     generator (BASELINE.md "CPU-baseline plan"), plus the eval-phase rate at the full size."""
     n, m, k, kind, _ = CONFIGS[cfg]
+    if isinstance(k, tuple):  # the reference probe only generates fixed-width k-SAT
+        return {"value": None, "unit": "clause-evals/s", "cores": 0, "kind": "reference",
+                "sample": "not measured: the reference generator has no mixed-width mode"}
     threads, why = cpu_threads()
     probe = os.path.join(ROOT, "oracle", "_ref", "ref_probe")
     if os.path.exists(probe):
@@ -210,7 +215,12 @@ def main():
 
     n, m, k, kind, desc = CONFIGS[args.config]
     t0 = time.perf_counter()
-    offs, lits = generate_ksat(1, n, m, k, kind)
+    if isinstance(k, tuple):
+        from alllsatisfiabilitysolver_amd import generate_mixed
+
+        offs, lits = generate_mixed(1, n, m, *k)
+    else:
+        offs, lits = generate_ksat(1, n, m, k, kind)
     t_gen = time.perf_counter() - t0
     flags = N.FLAG_KERNEL_TIMING  # kernels stamp device wall-clock times of every iteration
     if args.exchange == "allreduce":

@@ -73,12 +73,15 @@ SPECS = {
     "small": (7000, 28000, 3, 0, 5, 8),
     # more variables than one LDS window holds: windowed evaluation order inside every shard
     "windows": (1_600_000, 40000, 3, 0, 5, 4),
+    # 300 iterations: the 8-bit cover stamps wrap once (the reduce clears them at iteration 255)
+    "long": (3000, 12000, 3, 0, 6, 300),
 }
 
 
 @pytest.mark.parametrize("world,mode,spec_name", [(2, "allgather", "small"), (2, "allreduce", "small"),
                                                   (3, "allgather", "small"), (3, "allreduce", "small"),
-                                                  (2, "allgather", "windows")])
+                                                  (2, "allgather", "windows"), (2, "allgather", "long"),
+                                                  (2, "allreduce", "long")])
 def test_sharded_solver_matches_oracle(oracle_mod, native, world, mode, spec_name):
     o = oracle_mod
     n, m, k, kind, seed, K = spec = SPECS[spec_name]

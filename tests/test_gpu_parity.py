@@ -103,6 +103,15 @@ def _instances():
     offs[1:] = np.cumsum(w)
     lits = rng.integers(0, 2 * 9000, int(offs[-1])).astype(np.uint32)
     out["ragged"] = (9000, offs, lits)
+    # ragged with a few very wide clauses (their chunks get wide) and empty clauses (always
+    # violated: every slot is the padding literal)
+    w = rng.integers(1, 9, 30000)
+    w[rng.choice(w.size, 40, replace=False)] = rng.integers(40, 150, 40)
+    w[rng.choice(w.size, 3, replace=False)] = 0
+    offs = np.zeros(w.size + 1, np.uint64)
+    offs[1:] = np.cumsum(w)
+    lits = rng.integers(0, 2 * 12000, int(offs[-1])).astype(np.uint32)
+    out["ragged_wide"] = (12000, offs, lits)
     return out
 
 
@@ -118,7 +127,7 @@ def instances():
 
 @pytest.mark.parametrize("layout", list(LAYOUTS))
 @pytest.mark.parametrize("name", ["c1_ratio4", "u2500_ratio4", "ratio2_solves", "k8", "powerlaw",
-                                  "k5_multi_tile", "powerlaw_hot", "edge", "ragged"])
+                                  "k5_multi_tile", "powerlaw_hot", "edge", "ragged", "ragged_wide"])
 def test_trajectory_matches_oracle(gpu, oracle_mod, name, layout, monkeypatch):
     o = oracle_mod
     n, offs, lits = instances()[name]
@@ -297,6 +306,11 @@ BIG = {
     # C4 (the north star's 8-GPU instance) on one GPU: 27-bit clause ids do not fit in the
     # literals' spare bits (26-bit literals), so evaluation positions + perm; 26 LDS windows
     "C4_3sat_128M": (32_000_000, 128_000_000, 3, 0),
+    # ragged widths 2-12 (bench config R): the chunk-transposed ragged evaluation, CSR LFMIS
+    "R_mixed_4M": (1_000_000, 4_000_000, (2, 12), 0),
+    "R_mixed_4M_csr": (1_000_000, 4_000_000, (2, 12), 0, {"ALLL_NO_RAGGED": "1"}),
+    # more variables than one LDS window: windowed ragged evaluation
+    "R_mixed_windows": (4_000_000, 2_000_000, (1, 9), 0),
 }
 
 
@@ -308,7 +322,12 @@ def test_baseline_sizes_bit_exact_steps(gpu, oracle_mod, name, monkeypatch):
     n, m, k, kind = BIG[name][:4]
     for key, v in (BIG[name][4] if len(BIG[name]) > 4 else {}).items():
         monkeypatch.setenv(key, v)
-    offs, lits = generate_ksat(1, n, m, k, kind)
+    if isinstance(k, tuple):
+        from alllsatisfiabilitysolver_amd import generate_mixed
+
+        offs, lits = generate_mixed(1, n, m, *k)
+    else:
+        offs, lits = generate_ksat(1, n, m, k, kind)
     seed = 1
     with Solver(n, offs, lits, seed=seed) as s:
         A = s.assignment_words()

@@ -1321,7 +1321,9 @@ constexpr int BRS_THREADS = 512;
 // Items per thread and sweep: 20 (10240 pairs: ~8.9k per bucket at 10M clauses with one bucket
 // per CU; 150 VGPRs, one workgroup per CU), or 16 (8192 pairs; two workgroups per CU) when
 // there are more buckets than CUs.
-constexpr int BRS_UNROLL_WIDE = 20, BRS_UNROLL_NARROW = 16;
+constexpr int BRS_UNROLL_WIDE = 20, BRS_UNROLL_NARROW = 16, BRS_UNROLL_DEEP = 8;
+constexpr int BRS_THREADS_DEEP = 1024;
+constexpr uint32_t BRS_DEEP_LDS = 48u << 10;  // minima above this: the deep variant
 
 struct ResolveLds {
     uint32_t* min;          // bkt_width
@@ -1365,51 +1367,45 @@ __device__ __forceinline__ uint32_t resolve_batch(const LoopBuffers& b, const Re
     return total;
 }
 
-// Position of flat item f of the batch: largest q with pre[q] <= f (fixed depth, branch-free:
-// BKT_RUN_BATCH = 2^10 runs at most; a run with an empty segment shares its prefix with the
-// next one, and the largest wins).
-__device__ __forceinline__ uint32_t resolve_pos(const ResolveLds& L, uint32_t rb, uint32_t nr, uint32_t f,
-                                                uint32_t run_cap) {
-    uint32_t lo = 0;
-#pragma unroll
-    for (int step = 9; step >= 0; --step) {
-        const uint32_t mid = lo + (1u << step);
-        lo = (mid < nr && L.pre[min(mid, nr)] <= f) ? mid : lo;
-    }
-    return (rb + lo) * run_cap + L.start[lo] + (f - L.pre[lo]);
-}
-
-// One unrolled sweep over the batch items f0 + 64 u (u < U): positions and pairs
-// (items past np load the batch's last pair again; callers ignore them).
-template <int U>
-__device__ __forceinline__ void resolve_load(const LoopBuffers& b, const ResolveLds& L, uint32_t rb, uint32_t nr,
-                                             uint32_t np, uint32_t f0, uint32_t run_cap, uint32_t* pos,
-                                             unsigned long long* x) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) pos[u] = resolve_pos(L, rb, nr, min(f0 + 64 * u, np - 1), run_cap);
-#pragma unroll
-    for (int u = 0; u < U; ++u) x[u] = b.pairs[pos[u]];
-}
-
 __device__ __forceinline__ unsigned long long resolve_mark(const ResolveLds& L, unsigned long long x) {
     return L.min[(uint32_t)x & 0x7FFFu] != (uint32_t)(x >> 32) ? (x | PAIR_LOSE) : x;
 }
 
-template <int U>
-__global__ __launch_bounds__(BRS_THREADS, U <= BRS_UNROLL_NARROW ? 2 : 1) void k_bresolve(LoopBuffers b,
-                                                                                          uint32_t run_cap) {
+// Item -> segment table of one sweep: items [f0, f0 + cap) of the batch, filled segment by
+// segment (a thread per segment overlapping the sweep; first one found by binary search).
+__device__ __forceinline__ void resolve_seg_table(const ResolveLds& L, uint32_t nr, uint32_t np, uint32_t f0,
+                                                  uint32_t cap, uint16_t* s_seg) {
+    uint32_t lo = 0;  // largest q with pre[q] <= f0
+#pragma unroll
+    for (int step = 9; step >= 0; --step) {
+        const uint32_t mid = lo + (1u << step);
+        lo = (mid < nr && L.pre[min(mid, nr)] <= f0) ? mid : lo;
+    }
+    const uint32_t f1 = min(np, f0 + cap);
+    for (uint32_t q = lo + threadIdx.x; q < nr && L.pre[q] < f1; q += blockDim.x)
+        for (uint32_t f = max(L.pre[q], f0); f < min(L.pre[q + 1], f1); ++f) s_seg[f - f0] = (uint16_t)q;
+}
+
+// T threads, U items per thread and sweep.  <20, 512>: one bucket per CU (minima <= 128 KB, ~9k
+// pairs: one sweep); <16, 512>: more buckets than CUs with small minima (two workgroups per
+// CU); <8, 1024>: more buckets than CUs with 128 KB minima (one workgroup per CU: 16 waves
+// instead of 8 for the latency-bound sweeps).  Sweeps past the first use a per-sweep item ->
+// segment table too (no binary search per item).
+template <int U, int T>
+__global__ __launch_bounds__(T, (U <= BRS_UNROLL_NARROW && T <= 512) ? 2 : 1) void k_bresolve(LoopBuffers b,
+                                                                                              uint32_t run_cap) {
     if (!b.state->active) return;
     extern __shared__ uint32_t s_min[];
     __shared__ uint32_t s_start[BKT_RUN_BATCH], s_pre[BKT_RUN_BATCH + 1];
-    __shared__ uint32_t s_wsum[BRS_THREADS / 64];
-    __shared__ uint16_t s_seg[BRS_THREADS * U];  // single sweep: item -> segment
+    __shared__ uint32_t s_wsum[T / 64];
+    __shared__ uint16_t s_seg[T * U];  // item -> segment of the current sweep
     const uint32_t bv = b.bkt_width;
     ResolveLds L{s_min, s_start, s_pre, s_wsum};
     dbg_stamp(b, 1, 0);
     for (uint32_t i = threadIdx.x; i < bv; i += blockDim.x) L.min[i] = ~0u;
     // items of a wave: f0 + 64 u, f0 = wave * 64 U + lane (+ stride per sweep)
     const uint32_t first = (threadIdx.x >> 6) * 64 * U + (threadIdx.x & 63);
-    const uint32_t stride = blockDim.x * U;
+    const uint32_t stride = T * U;
     uint32_t pos[U];  // pair positions (the pair area holds < 2^32 pairs, checked at create)
     unsigned long long x[U];
     if (b.n_runs <= BKT_RUN_BATCH) {
@@ -1451,17 +1447,27 @@ __global__ __launch_bounds__(BRS_THREADS, U <= BRS_UNROLL_NARROW ? 2 : 1) void k
         for (uint32_t rb = 0; rb < b.n_runs; rb += BKT_RUN_BATCH) {
             const uint32_t nr = min(BKT_RUN_BATCH, b.n_runs - rb);
             const uint32_t np = resolve_batch(b, L, rb, nr);
-            for (uint32_t f0 = first; f0 < np; f0 += stride) {
-                resolve_load<U>(b, L, rb, nr, np, f0, run_cap, pos, x);
+            for (uint32_t s0 = 0; s0 < np; s0 += stride) {
+                resolve_seg_table(L, nr, np, s0, stride, s_seg);
+                __syncthreads();
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
-                    if (pass == 0) {
-                        if (f0 + 64 * u < np) atomicMin(&L.min[(uint32_t)x[u] & 0x7FFFu], (uint32_t)(x[u] >> 32));
-                    }
-                    else if (f0 + 64 * u < np) b.pairs[pos[u]] = resolve_mark(L, x[u]);
+                    const uint32_t f = min(s0 + first + 64 * u, np - 1);
+                    const uint32_t q = s_seg[f - s0];
+                    pos[u] = (rb + q) * run_cap + L.start[q] + (f - L.pre[q]);
                 }
+#pragma unroll
+                for (int u = 0; u < U; ++u) x[u] = b.pairs[pos[u]];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    if (s0 + first + 64 * u >= np) continue;
+                    if (pass == 0) atomicMin(&L.min[(uint32_t)x[u] & 0x7FFFu], (uint32_t)(x[u] >> 32));
+                    else b.pairs[pos[u]] = resolve_mark(L, x[u]);
+                }
+                __syncthreads();  // the table is rewritten by the next sweep
             }
-            __syncthreads();  // batch arrays are rewritten next; after pass 0: L.min is final
+            // (batch arrays are rewritten next; after pass 0: L.min is final -- the sweep's
+            // last barrier orders it)
         }
     }
     dbg_stamp(b, 1, 4);
@@ -2480,10 +2486,13 @@ hipError_t launch_round0_buckets(const ClauseView& cv, const LoopBuffers& b, boo
     const size_t lds = (size_t)4 * b.bkt_width;  // k_bresolve minima
     int dev;
     if (cv.k <= (uint32_t)MAX_FIXED_K && attr_pending(ATTR_BUCKETS + cv.k, dev)) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_bresolve<BRS_UNROLL_WIDE>,
+        hipError_t e = hipFuncSetAttribute((const void*)k_bresolve<BRS_UNROLL_WIDE, BRS_THREADS>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)(4u << BKT_SHIFT_MAX));
         if (e == hipSuccess)
-            e = hipFuncSetAttribute((const void*)k_bresolve<BRS_UNROLL_NARROW>,
+            e = hipFuncSetAttribute((const void*)k_bresolve<BRS_UNROLL_NARROW, BRS_THREADS>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)(4u << BKT_SHIFT_MAX));
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute((const void*)k_bresolve<BRS_UNROLL_DEEP, BRS_THREADS_DEEP>,
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)(4u << BKT_SHIFT_MAX));
         if (e != hipSuccess) return e;
         ALLL_DISPATCH_K(cv.k, (e = hipFuncSetAttribute((const void*)k_bscatter<(K > 0 ? K : 1)>,
@@ -2501,8 +2510,12 @@ hipError_t launch_round0_buckets(const ClauseView& cv, const LoopBuffers& b, boo
                               cv, b, b.stage[0], fr)));
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    if (b.n_bkt <= b.n_cu) k_bresolve<BRS_UNROLL_WIDE><<<b.n_bkt, BRS_THREADS, lds, s>>>(b, (uint32_t)run_cap);
-    else k_bresolve<BRS_UNROLL_NARROW><<<b.n_bkt, BRS_THREADS, lds, s>>>(b, (uint32_t)run_cap);
+    if (b.n_bkt <= b.n_cu)
+        k_bresolve<BRS_UNROLL_WIDE, BRS_THREADS><<<b.n_bkt, BRS_THREADS, lds, s>>>(b, (uint32_t)run_cap);
+    else if (lds > (size_t)BRS_DEEP_LDS)  // minima too large for two workgroups per CU
+        k_bresolve<BRS_UNROLL_DEEP, BRS_THREADS_DEEP><<<b.n_bkt, BRS_THREADS_DEEP, lds, s>>>(b, (uint32_t)run_cap);
+    else
+        k_bresolve<BRS_UNROLL_NARROW, BRS_THREADS><<<b.n_bkt, BRS_THREADS, lds, s>>>(b, (uint32_t)run_cap);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     const int l = last ? 1 : 0;

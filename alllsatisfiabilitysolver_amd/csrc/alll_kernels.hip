@@ -318,7 +318,11 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     };
     // window of a tile (words; b.win_base: instances sorted by smallest-variable block, else 0)
-    auto window = [&](uint32_t t) -> uint32_t { return b.win_base ? b.win_base[t] : 0u; };
+    // (bit 31 of win_base[t]: the smallest variable of every clause of tile t lies in its
+    // window, so slot K-1 is looked up in LDS only)
+    auto window = [&](uint32_t t) -> uint32_t { return b.win_base ? b.win_base[t] & 0x7FFFFFFFu : 0u; };
+    // the whole assignment fits the LDS window: every lookup is an LDS read
+    const bool all_lds = b.win_base == nullptr && b.n_words <= b.win_words;
     uint32_t wb = window(t0);
     // zero word for lanes that need no LDS word (past every word the fill writes)
     const uint32_t zslot = (lds_words + 3) / 4 * 4;
@@ -353,6 +357,7 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
         sa = se;
         for (uint64_t g = gbeg + wave; g < gend; g += HYB_THREADS / 64) {
             const uint64_t cb = g * CHUNK;
+            const bool small_lds = b.win_base && (b.win_base[g / (TILE / CHUNK)] >> 31);
             uint32_t sat[4] = {0u, 0u, 0u, 0u};
             uint4 x[K];
             {
@@ -378,6 +383,14 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
                     // from LDS reads the zero word s_A[zslot].  So w = global | LDS word.  A
                     // lane that needs no lookup is already satisfied, so its bit is ignored.
                     uint32_t gw[4], lw[4];
+                    if (all_lds || (j == K - 1 && small_lds)) {  // (uniform) window-only lookups
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            const uint32_t d = __builtin_amdgcn_ubfe(xs[q], 6u, wbits) - wb;
+                            gw[q] = 0u;
+                            lw[q] = s_A[(first || !(sat[q] & 1u)) ? d : zslot];
+                        }
+                    } else {
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
                         const uint32_t wi = __builtin_amdgcn_ubfe(xs[q], 6u, wbits);
@@ -386,6 +399,7 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
                         const bool inl = d < lds_words;
                         gw[q] = __builtin_amdgcn_raw_buffer_load_b32(rsA, (need && !inl) ? wi * 4u : 0x80000000u, 0, 0);
                         lw[q] = s_A[(need && inl) ? d : zslot];
+                    }
                     }
                     // bit 0 of sat: clause satisfied (the literal's value is its variable's bit
                     // xor the sign, bit 0 of the literal; the other bits of sat are don't-care)

@@ -864,6 +864,18 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
                 for (int j = 0; j < fixed_k; ++j) lo = std::min(lo, prob->literals[cl * fixed_k + j] >> 1);
                 wb[tt] = std::min<uint64_t>((uint64_t)(lo / win_vars) * b.win_words, b.n_words - lds_words);
             }
+            // bit 31: every clause of the tile has its smallest variable in the window (all but
+            // the tiles at block boundaries), so k_eval_hybrid reads slot K-1 from LDS only
+            parallel_for(n_tiles, host_threads(), [&](uint64_t tt) {
+                bool all_in = true;
+                for (uint64_t p = tt * TILE; p < std::min<uint64_t>(m, (tt + 1) * TILE) && all_in; ++p) {
+                    const uint64_t cl = perm[p];
+                    uint32_t lo = ~0u;
+                    for (int j = 0; j < fixed_k; ++j) lo = std::min(lo, prob->literals[cl * fixed_k + j] >> 1);
+                    all_in = (uint32_t)(lo / 32) - wb[tt] < lds_words;
+                }
+                if (all_in) wb[tt] |= 0x80000000u;
+            });
             uint32_t* d_wb = nullptr;
             if ((rc = dalloc(c, &d_wb, n_tiles))) return bail(rc);
             if (hipStreamSynchronize(c->stream) != hipSuccess ||

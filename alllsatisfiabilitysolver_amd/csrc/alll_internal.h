@@ -139,8 +139,10 @@ struct LoopBuffers {
     uint32_t bkt_magic;         // floor(2^32 / bkt_width): bucket by multiply-high
     uint32_t n_cu;              // compute units of the device
     uint32_t n_bkt;
-    uint32_t run_tiles;
+    uint32_t run_tiles;         // tiles per run at most (a run's pair area holds run_tiles * TILE * K)
     uint32_t n_runs;
+    const uint32_t* run_t0;     // n_runs + 1: first tile of every run (runs split the tile range of
+                                // every evaluation workgroup, so one GPU scatters inside k_eval_hybrid)
     unsigned long long* kdbg;   // diagnostics (env ALLL_DEBUG_PHASES): per-workgroup phase stamps
     // streaming solve (SATInstance::solve(getEnumeratedClause, ...), T = 1): LFMIS priority =
     // position in the clause generator's yield window (alll_options.stream_batch > 0)
@@ -165,8 +167,9 @@ hipError_t launch_init_state(const LoopBuffers& b, hipStream_t s);
 hipError_t launch_set_limits(const LoopBuffers& b, uint64_t n, hipStream_t s);
 hipError_t launch_eval(const ClauseView& cv, const LoopBuffers& b, uint32_t tile_begin,
                        uint32_t tile_end, bool gated, hipStream_t s);
+// scatter: also the bucket scatter of LFMIS round 0 (one GPU; runs split the workgroups' tiles)
 hipError_t launch_eval_hybrid(const ClauseView& cv, const LoopBuffers& b, uint32_t tile_begin,
-                              uint32_t tile_end, bool gated, int n_blocks, hipStream_t s);
+                              uint32_t tile_end, bool gated, int n_blocks, bool scatter, hipStream_t s);
 hipError_t launch_eval_ragged(const ClauseView& cv, const LoopBuffers& b, uint32_t tile_begin,
                               uint32_t tile_end, bool gated, int n_blocks, hipStream_t s);
 hipError_t launch_collect(const ClauseView& cv, const LoopBuffers& b, uint32_t own_begin,
@@ -175,7 +178,7 @@ hipError_t launch_reduce(const LoopBuffers& b, int mode, hipStream_t s);
 hipError_t launch_round(const ClauseView& cv, const LoopBuffers& b, uint32_t r, bool last,
                         uint32_t wave_from, hipStream_t s);
 hipError_t launch_round0_buckets(const ClauseView& cv, const LoopBuffers& b, bool last, bool fused_reduce,
-                                 hipStream_t s);
+                                 bool scattered, hipStream_t s);
 hipError_t launch_tail(const ClauseView& cv, const LoopBuffers& b, uint32_t first_round,
                        hipStream_t s);
 hipError_t launch_rr_mis(const ClauseView& cv, const LoopBuffers& b, hipStream_t s);

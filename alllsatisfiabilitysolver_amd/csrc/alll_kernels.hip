@@ -213,6 +213,39 @@ __device__ __forceinline__ void emit4(const ClauseView& cv, uint32_t* list, uint
     }
 }
 
+constexpr int BSC_THREADS = 1024;
+constexpr uint32_t BKT_STAGE = 12288;  // pairs staged in LDS by k_bscatter (96 KiB)
+// LDS of the bucket scatter of one run (the standalone kernel's arrays, or carved from the
+// evaluation kernel's window once its tiles are done).
+struct ScatterLds {
+    uint32_t* hist;               // BKT_MAX bucket counters / cursors
+    uint32_t* hk;                 // HOT_SLOTS hot-table keys
+    unsigned long long* hv;       // HOT_SLOTS hot-table minima
+    uint32_t* tc;                 // RUN_TILES_MAX tile counts
+    uint32_t* pre;                // RUN_TILES_MAX + 1 prefix
+    uint32_t* wsum;               // BSC_THREADS / 64
+    unsigned long long* pairs;    // BKT_STAGE staged pairs
+};
+constexpr size_t SCATTER_LDS_BYTES = 8 * BKT_STAGE + 8 * HOT_SLOTS + 4 * BKT_MAX + 4 * HOT_SLOTS + 4 * RUN_TILES_MAX +
+                                     4 * (RUN_TILES_MAX + 4) + 4 * (BSC_THREADS / 64);
+
+__device__ __forceinline__ ScatterLds carve_scatter_lds(void* base) {
+    char* p = static_cast<char*>(base);
+    ScatterLds L;
+    L.pairs = reinterpret_cast<unsigned long long*>(p); p += 8 * BKT_STAGE;
+    L.hv = reinterpret_cast<unsigned long long*>(p); p += 8 * HOT_SLOTS;
+    L.hist = reinterpret_cast<uint32_t*>(p); p += 4 * BKT_MAX;
+    L.hk = reinterpret_cast<uint32_t*>(p); p += 4 * HOT_SLOTS;
+    L.tc = reinterpret_cast<uint32_t*>(p); p += 4 * RUN_TILES_MAX;
+    L.pre = reinterpret_cast<uint32_t*>(p); p += 4 * (RUN_TILES_MAX + 4);
+    L.wsum = reinterpret_cast<uint32_t*>(p);
+    return L;
+}
+
+template <int K>
+__device__ void scatter_run(const ClauseView& cv, const LoopBuffers& b, uint32_t* list, uint32_t r, uint32_t epoch,
+                            const ScatterLds& L);
+
 // ------------------------------------------------------------------------------------
 // Clause evaluation, fixed width K, chunk-transposed literals, one tile per 256-thread
 // workgroup: lane i of a wave evaluates clauses 4i..4i+3 of a 256-clause chunk with one
@@ -288,7 +321,7 @@ __global__ __launch_bounds__(EVAL_THREADS) void k_eval_fixed(ClauseView cv, Loop
 template <int K>
 __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, LoopBuffers b,
                                                              uint32_t tile_begin, uint32_t tile_end,
-                                                             int gated) {
+                                                             int gated, int scatter) {
     if (gated && eval_gate_closed(b.state)) return;
     extern __shared__ __attribute__((aligned(16))) uint32_t s_A[];
     __shared__ uint32_t s_tcnt[HYB_MAX_TILES];
@@ -444,6 +477,19 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
         }
     }
     stamp_eval_end(b, gated);
+    if (scatter) {
+        // One GPU, bucketed LFMIS round 0: this workgroup's tiles form runs b.run_t0[r] ..
+        // (rpw runs per workgroup), so the workgroup scatters their claims itself, from the
+        // lists it has just written (L2-warm) and with the window's LDS, instead of a
+        // separate k_bscatter launch; the reduce then runs in k_bresolve (pre-reduce epoch).
+        __syncthreads();  // every wave is done with the window; the lists and counts are visible
+        const ScatterLds L = carve_scatter_lds(s_A);
+        const uint32_t rpw = b.n_runs / gridDim.x;
+        for (uint32_t r = blockIdx.x * rpw; r < (blockIdx.x + 1) * rpw; ++r) {
+            scatter_run<K>(cv, b, b.stage[0], r, b.state->round_next, L);
+            __syncthreads();  // (the LDS is reused by the next run)
+        }
+    }
 }
 
 // Clause evaluation, ragged widths (ClauseView::rg_off): the persistent LDS-window structure
@@ -1121,8 +1167,6 @@ __device__ __forceinline__ uint32_t run_tile_of(const uint32_t* pre, uint32_t nt
 // workgroup (the common case: ~2.5k entries per run at 10M clauses), they stay in registers
 // between the phases of a kernel instead of being re-read.
 constexpr int BKT_UNROLL = 4;
-constexpr int BSC_THREADS = 1024;
-constexpr uint32_t BKT_STAGE = 12288;  // pairs staged in LDS by k_bscatter (96 KiB)
 
 // Tile counts of run r -> LDS prefix (nt + 1 entries); returns the run's entry count.
 __device__ __forceinline__ uint32_t run_prefix(const LoopBuffers& b, uint32_t t0, uint32_t nt, uint32_t* s_tc,
@@ -1156,39 +1200,22 @@ __device__ __forceinline__ void load_run_entries(const uint32_t* list, uint32_t 
     }
 }
 
+// Bucket scatter of run r (tiles run_t0[r] .. run_t0[r+1]) by the whole workgroup
+// (BSC_THREADS threads): the pairs of its claims grouped by variable bucket into the run's
+// pair area, the segment table column runtab[.][r], hot claims into owner[] under `epoch`.
+// Every thread must call it (workgroup barriers inside).
 template <int K>
-//
-// fused_reduce (one GPU, no hot variables): the loop's reduce runs in an extra workgroup
-// (blockIdx.x == n_runs) beside the runs, saving the k_reduce launch.  The run workgroups then
-// read no loop state: when this iteration turns out inactive, their pairs are simply never
-// resolved (k_bresolve and k_bjoin test st->active, which the reduce has set by then), and a
-// skipped evaluation leaves empty or unconsumed lists.
-__global__ __launch_bounds__(BSC_THREADS) void k_bscatter(ClauseView cv, LoopBuffers b, uint32_t* list,
-                                                          int fused_reduce) {
-    const DevState* st = b.state;
-    if (fused_reduce) {
-        if (blockIdx.x == b.n_runs) {
-            if (eval_gate_closed(st)) {
-                if (threadIdx.x == 0) b.state->active = 0;
-            } else {
-                reduce_body(b, 0);
-            }
-            return;
-        }
-    } else if (!st->active) {
-        return;
-    }
+__device__ void scatter_run(const ClauseView& cv, const LoopBuffers& b, uint32_t* list, uint32_t r, uint32_t epoch,
+                            const ScatterLds& L) {
     constexpr int S = Ent<K>::S;
     constexpr int U = BKT_UNROLL;
-    const uint32_t r = blockIdx.x;
-    const uint32_t t0 = r * b.run_tiles, nt = min(b.run_tiles, b.n_tiles - t0);
-    __shared__ uint32_t s_hist[BKT_MAX];
-    __shared__ uint32_t s_hk[HOT_SLOTS];
-    __shared__ unsigned long long s_hv[HOT_SLOTS];
-    __shared__ uint32_t s_tc[RUN_TILES_MAX], s_pre[RUN_TILES_MAX + 1];
-    __shared__ uint32_t s_wsum[BSC_THREADS / 64];
-    extern __shared__ unsigned long long s_pairs[];  // BKT_STAGE pairs
-    HotTable ht{s_hk, s_hv};
+    const uint32_t t0 = b.run_t0[r], nt = b.run_t0[r + 1] - t0;
+    uint32_t* s_hist = L.hist;
+    uint32_t* s_tc = L.tc;
+    uint32_t* s_pre = L.pre;
+    uint32_t* s_wsum = L.wsum;
+    unsigned long long* s_pairs = L.pairs;
+    HotTable ht{L.hk, L.hv};
     const bool hot = cv.n_hot != 0;
     if (hot) ht.init();
     const uint32_t nb = b.n_bkt;
@@ -1197,7 +1224,7 @@ __global__ __launch_bounds__(BSC_THREADS) void k_bscatter(ClauseView cv, LoopBuf
     const uint32_t E = run_prefix(b, t0, nt, s_tc, s_pre);
     dbg_stamp(b, 0, 1);
     const bool single = E <= blockDim.x * U;
-    const unsigned long long keyhi = (unsigned long long)(~st->round_base) << 32;
+    const unsigned long long keyhi = (unsigned long long)(~epoch) << 32;
     Ent<K> e[U];
     bool ok[U];
     uint32_t tts[U], idx[U];
@@ -1255,7 +1282,7 @@ __global__ __launch_bounds__(BSC_THREADS) void k_bscatter(ClauseView cv, LoopBuf
     dbg_stamp(b, 0, 2);
     __syncthreads();
     dbg_stamp(b, 0, 3);
-    if (hot) ht.flush(owner_of(b, st->round_base), b);
+    if (hot) ht.flush(owner_of(b, epoch), b);
     // exclusive scan of the histogram: run-local start of every bucket
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t per = (nb + blockDim.x - 1) / blockDim.x;
@@ -1320,6 +1347,26 @@ __global__ __launch_bounds__(BSC_THREADS) void k_bscatter(ClauseView cv, LoopBuf
         for (uint32_t i = threadIdx.x; i < total; i += blockDim.x) gpr[i] = s_pairs[i];
     }
     dbg_stamp(b, 0, 6);
+}
+
+template <int K>
+// Standalone bucket scatter, workgroup per run.  pre_reduce: the loop's reduce has not run yet
+// (one GPU: it runs in an extra workgroup of k_bresolve), so this iteration's owner epoch is
+// state.round_next (the reduce makes it round_base), and the loop state is not read: an
+// inactive iteration leaves pairs that k_bjoin never consumes.  Otherwise (multi-GPU, after
+// k_reduce) the kernel is gated on state.active.
+__global__ __launch_bounds__(BSC_THREADS) void k_bscatter(ClauseView cv, LoopBuffers b, uint32_t* list,
+                                                          int pre_reduce) {
+    const DevState* st = b.state;
+    if (!pre_reduce && !st->active) return;
+    __shared__ uint32_t s_hist[BKT_MAX];
+    __shared__ uint32_t s_hk[HOT_SLOTS];
+    __shared__ unsigned long long s_hv[HOT_SLOTS];
+    __shared__ uint32_t s_tc[RUN_TILES_MAX], s_pre[RUN_TILES_MAX + 4];
+    __shared__ uint32_t s_wsum[BSC_THREADS / 64];
+    extern __shared__ unsigned long long s_pairs[];  // BKT_STAGE pairs
+    const ScatterLds L{s_hist, s_hk, s_hv, s_tc, s_pre, s_wsum, s_pairs};
+    scatter_run<K>(cv, b, list, blockIdx.x, pre_reduce ? st->round_next : st->round_base, L);
 }
 
 // Workgroup per bucket.  The run table column is processed in batches of BKT_RUN_BATCH runs:
@@ -1405,10 +1452,28 @@ __device__ __forceinline__ void resolve_seg_table(const ResolveLds& L, uint32_t 
 // CU); <8, 1024>: more buckets than CUs with 128 KB minima (one workgroup per CU: 16 waves
 // instead of 8 for the latency-bound sweeps).  Sweeps past the first use a per-sweep item ->
 // segment table too (no binary search per item).
+//
+// fused_reduce (one GPU): the loop's reduce runs in an extra workgroup (blockIdx.x == n_bkt)
+// beside the buckets, saving the k_reduce launch.  The bucket workgroups then read no loop
+// state: when the iteration turns out inactive, their marks are never consumed (k_bjoin tests
+// state.active, set by then), and a skipped evaluation leaves the previous pairs, which are
+// resolved again to the same marks.
 template <int U, int T>
 __global__ __launch_bounds__(T, (U <= BRS_UNROLL_NARROW && T <= 512) ? 2 : 1) void k_bresolve(LoopBuffers b,
-                                                                                              uint32_t run_cap) {
-    if (!b.state->active) return;
+                                                                                              uint32_t run_cap,
+                                                                                              int fused_reduce) {
+    if (fused_reduce) {
+        if (blockIdx.x == b.n_bkt) {
+            if (eval_gate_closed(b.state)) {
+                if (threadIdx.x == 0) b.state->active = 0;
+            } else {
+                reduce_body(b, 0);
+            }
+            return;
+        }
+    } else if (!b.state->active) {
+        return;
+    }
     extern __shared__ uint32_t s_min[];
     __shared__ uint32_t s_start[BKT_RUN_BATCH], s_pre[BKT_RUN_BATCH + 1];
     __shared__ uint32_t s_wsum[T / 64];
@@ -1500,7 +1565,7 @@ __global__ __launch_bounds__(BJN_THREADS) void k_bjoin(ClauseView cv, LoopBuffer
     constexpr int S = Ent<K>::S;
     constexpr int U = K <= 4 ? 2 * BKT_UNROLL : BKT_UNROLL;
     const uint32_t r = blockIdx.x;
-    const uint32_t t0 = r * b.run_tiles, nt = min(b.run_tiles, b.n_tiles - t0);
+    const uint32_t t0 = b.run_t0[r], nt = b.run_t0[r + 1] - t0;
     extern __shared__ uint32_t s_lost[];  // one byte per entry slot of the run's tiles
     __shared__ uint32_t s_tc[RUN_TILES_MAX], s_pre[RUN_TILES_MAX + 1], s_keep[RUN_TILES_MAX],
         s_join[RUN_TILES_MAX], s_mis0[RUN_TILES_MAX], s_base[RUN_TILES_MAX];
@@ -2409,13 +2474,15 @@ static void attr_mark(uint32_t bit, int dev) {
 }
 
 hipError_t launch_eval_hybrid(const ClauseView& cv, const LoopBuffers& b, uint32_t tile_begin,
-                              uint32_t tile_end, bool gated, int n_blocks, hipStream_t s) {
+                              uint32_t tile_end, bool gated, int n_blocks, bool scatter, hipStream_t s) {
     if (tile_end <= tile_begin) return hipSuccess;
     const uint32_t nt = tile_end - tile_begin;
     const dim3 grid(std::min<uint32_t>(nt, (uint32_t)std::max(1, n_blocks)));
-    // window words (a multiple of 4) + the zero word (a 16-byte slot)
-    const size_t lds = ((size_t)(std::min(b.n_words, b.win_words) + 3) / 4 * 4 + 4) * 4;
-    const int g = gated ? 1 : 0;
+    if (scatter && (!b.pairs || b.n_runs % grid.x != 0)) return hipErrorInvalidValue;  // runs per workgroup
+    // window words (a multiple of 4) + the zero word (a 16-byte slot); the scatter reuses it
+    size_t lds = ((size_t)(std::min(b.n_words, b.win_words) + 3) / 4 * 4 + 4) * 4;
+    if (scatter) lds = std::max(lds, SCATTER_LDS_BYTES);
+    const int g = gated ? 1 : 0, sc = scatter ? 1 : 0;
     int dev;
     if (cv.k >= 1 && cv.k <= (uint32_t)MAX_FIXED_K && attr_pending(ATTR_HYBRID + cv.k, dev)) {
         hipError_t e = hipSuccess;
@@ -2426,14 +2493,14 @@ hipError_t launch_eval_hybrid(const ClauseView& cv, const LoopBuffers& b, uint32
         attr_mark(ATTR_HYBRID + cv.k, dev);
     }
     switch (cv.k) {
-        case 1: k_eval_hybrid<1><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g); break;
-        case 2: k_eval_hybrid<2><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g); break;
-        case 3: k_eval_hybrid<3><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g); break;
-        case 4: k_eval_hybrid<4><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g); break;
-        case 5: k_eval_hybrid<5><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g); break;
-        case 6: k_eval_hybrid<6><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g); break;
-        case 7: k_eval_hybrid<7><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g); break;
-        case 8: k_eval_hybrid<8><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g); break;
+        case 1: k_eval_hybrid<1><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g, sc); break;
+        case 2: k_eval_hybrid<2><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g, sc); break;
+        case 3: k_eval_hybrid<3><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g, sc); break;
+        case 4: k_eval_hybrid<4><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g, sc); break;
+        case 5: k_eval_hybrid<5><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g, sc); break;
+        case 6: k_eval_hybrid<6><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g, sc); break;
+        case 7: k_eval_hybrid<7><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g, sc); break;
+        case 8: k_eval_hybrid<8><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g, sc); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -2492,8 +2559,7 @@ hipError_t launch_round(const ClauseView& cv, const LoopBuffers& b, uint32_t r, 
 }
 
 hipError_t launch_round0_buckets(const ClauseView& cv, const LoopBuffers& b, bool last, bool fused_reduce,
-                                 hipStream_t s) {
-    if (fused_reduce && cv.n_hot) return hipErrorInvalidValue;  // (hot claims need the epoch)
+                                 bool scattered, hipStream_t s) {
     // buffers as CLAIM(0) + JOIN(0): eval -> stage[0] (ids translated in place); JOIN stage[0] -> stage[1]
     if (b.n_tiles == 0 || cv.k == 0 || !b.pairs) return hipErrorInvalidValue;
     const uint64_t run_cap = (uint64_t)b.run_tiles * TILE * cv.k;
@@ -2519,17 +2585,22 @@ hipError_t launch_round0_buckets(const ClauseView& cv, const LoopBuffers& b, boo
         if (e != hipSuccess) return e;
         attr_mark(ATTR_BUCKETS + cv.k, dev);
     }
+    // fused_reduce: the loop's reduce has not run; it runs in an extra workgroup of k_bresolve
+    // (the scatter uses the pre-reduce epoch).  scattered: k_eval_hybrid has scattered the runs.
     const int fr = fused_reduce ? 1 : 0;
-    ALLL_DISPATCH_K(cv.k, (k_bscatter<(K > 0 ? K : 1)><<<b.n_runs + fr, BSC_THREADS, BKT_STAGE * 8, s>>>(
-                              cv, b, b.stage[0], fr)));
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
+    hipError_t e;
+    if (!scattered) {
+        ALLL_DISPATCH_K(cv.k, (k_bscatter<(K > 0 ? K : 1)><<<b.n_runs, BSC_THREADS, BKT_STAGE * 8, s>>>(
+                                  cv, b, b.stage[0], fr)));
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    const uint32_t nb = b.n_bkt + fr;
     if (b.n_bkt <= b.n_cu)
-        k_bresolve<BRS_UNROLL_WIDE, BRS_THREADS><<<b.n_bkt, BRS_THREADS, lds, s>>>(b, (uint32_t)run_cap);
+        k_bresolve<BRS_UNROLL_WIDE, BRS_THREADS><<<nb, BRS_THREADS, lds, s>>>(b, (uint32_t)run_cap, fr);
     else if (lds > (size_t)BRS_DEEP_LDS)  // minima too large for two workgroups per CU
-        k_bresolve<BRS_UNROLL_DEEP, BRS_THREADS_DEEP><<<b.n_bkt, BRS_THREADS_DEEP, lds, s>>>(b, (uint32_t)run_cap);
+        k_bresolve<BRS_UNROLL_DEEP, BRS_THREADS_DEEP><<<nb, BRS_THREADS_DEEP, lds, s>>>(b, (uint32_t)run_cap, fr);
     else
-        k_bresolve<BRS_UNROLL_NARROW, BRS_THREADS><<<b.n_bkt, BRS_THREADS, lds, s>>>(b, (uint32_t)run_cap);
+        k_bresolve<BRS_UNROLL_NARROW, BRS_THREADS><<<nb, BRS_THREADS, lds, s>>>(b, (uint32_t)run_cap, fr);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     const int l = last ? 1 : 0;

@@ -75,6 +75,8 @@ struct alll_ctx {
     uint32_t tiles_per_rank = 0, own_begin = 0, own_end = 0, n_tiles_padded = 0;
     uint32_t grid_rounds = DEFAULT_GRID_ROUNDS;
     bool fuse_reduce = true;     // env ALLL_FUSE_REDUCE=0: separate k_reduce (tests, A/B)
+    bool fuse_scatter = true;    // env ALLL_FUSE_SCATTER=0: separate k_bscatter (tests, A/B)
+    std::vector<uint32_t> run_t0;  // bucketed round 0: first tile of every run (+ end)
     uint32_t wave_round_min = WAVE_ROUND_MIN;  // first grid round with a wave per tile
     int rank = 0, world = 1;
     bool allreduce = false;
@@ -274,12 +276,12 @@ int write_limits(alll_ctx* c, uint64_t limit_eval, uint64_t limit_nores) {
     return ALLL_OK;
 }
 
-hipError_t eval_launch(alll_ctx* c, uint32_t tb, uint32_t te, bool gated) {
+hipError_t eval_launch(alll_ctx* c, uint32_t tb, uint32_t te, bool gated, bool scatter = false) {
     if (c->cv.rg_off) return launch_eval_ragged(c->cv, c->b, tb, te, gated, c->n_cu, c->stream);
     if (c->hybrid) {
         int grid = c->n_cu * c->eval_wgs;
         if (const char* e = getenv("ALLL_EVAL_GRID")) grid = atoi(e);  // tuning experiments
-        return launch_eval_hybrid(c->cv, c->b, tb, te, gated, grid, c->stream);
+        return launch_eval_hybrid(c->cv, c->b, tb, te, gated, grid, scatter, c->stream);
     }
     return launch_eval(c->cv, c->b, tb, te, gated, c->stream);
 }
@@ -314,7 +316,11 @@ int round0_variant(const alll_ctx* c) {
 int enqueue_iteration(alll_ctx* c, hipEvent_t* marks, int variant) {
     hipStream_t s = c->stream;
     if (marks) HIP_TRY(hipEventRecord(marks[0], s));
-    HIP_TRY(eval_launch(c, c->own_begin, c->own_end, true));
+    // one GPU, bucketed round 0: the evaluation workgroups scatter their runs' claims
+    // themselves (no k_bscatter), before the reduce (pre-reduce epoch)
+    const bool scatter = variant == 1 && c->world == 1 && c->hybrid && c->fuse_scatter && c->eval_wgs == 1 &&
+                         !c->b.rr_T && !getenv("ALLL_EVAL_GRID");
+    HIP_TRY(eval_launch(c, c->own_begin, c->own_end, true, scatter));
     if (marks) HIP_TRY(hipEventRecord(marks[1], s));
     if (c->world > 1) {
         const size_t words = (size_t)c->tiles_per_rank * TILE_WORDS;
@@ -330,13 +336,14 @@ int enqueue_iteration(alll_ctx* c, hipEvent_t* marks, int variant) {
     if (marks) HIP_TRY(hipEventRecord(marks[2], s));
     // the bucketed round 0 runs the reduce in an extra k_bscatter workgroup (one GPU, no hot
     // variables, not the round robin): one launch less
-    const bool fused = c->fuse_reduce && variant == 1 && c->world == 1 && c->cv.n_hot == 0 && !c->b.rr_T;
+    const bool fused = c->fuse_reduce && variant == 1 && c->world == 1 && !c->b.rr_T;
     if (!fused) HIP_TRY(launch_reduce(c->b, 0, s));
     if (c->b.rr_T) {
         HIP_TRY(launch_rr_mis(c->cv, c->b, s));
     } else {
         for (uint32_t r = 0; r < c->grid_rounds; ++r) {
-            if (r == 0 && variant == 1) HIP_TRY(launch_round0_buckets(c->cv, c->b, c->grid_rounds == 1, fused, s));
+            if (r == 0 && variant == 1)
+                HIP_TRY(launch_round0_buckets(c->cv, c->b, c->grid_rounds == 1, fused, scatter, s));
             else HIP_TRY(launch_round(c->cv, c->b, r, r + 1 == c->grid_rounds, c->wave_round_min, s));
         }
         HIP_TRY(launch_tail(c->cv, c->b, c->grid_rounds, s));
@@ -586,6 +593,7 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     c->use_graph = (opt.flags & ALLL_FLAG_NO_GRAPH) == 0;
     c->grid_rounds = opt.grid_rounds ? opt.grid_rounds : DEFAULT_GRID_ROUNDS;
     if (const char* e = getenv("ALLL_FUSE_REDUCE")) c->fuse_reduce = atoi(e) != 0;
+    if (const char* e = getenv("ALLL_FUSE_SCATTER")) c->fuse_scatter = atoi(e) != 0;
     if (const char* e = getenv("ALLL_WAVE_ROUND_MIN")) c->wave_round_min = (uint32_t)atoi(e);  // A/B
     auto bail = [&](int rc) { alll_destroy(c); return rc; };
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
@@ -708,17 +716,36 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
             const uint64_t mx = *std::max_element(load.begin(), load.end());
             skewed = mx > 4 * (L_pairs / nb + 1);
         }
-        // about one run per CU (k_bscatter holds one 1024-thread workgroup per CU)
-        uint32_t rt = std::max<uint32_t>(1, std::min<uint32_t>(RUN_TILES_MAX, (n_tiles + 255) / 256));
-        if (const char* e = getenv("ALLL_RUN_TILES"))  // tuning experiments
-            rt = std::max<uint32_t>(1, std::min<uint32_t>(RUN_TILES_MAX, (uint32_t)atoi(e)));
-        const uint64_t area = (uint64_t)((n_tiles + rt - 1) / rt) * rt * TILE * fixed_k;  // pairs
+        // Runs: the tile range of every evaluation workgroup (min(n_tiles, CUs) of them, the
+        // split of k_eval_hybrid) cut into rpw runs of at most RUN_TILES_MAX tiles, so that one
+        // GPU's evaluation workgroups scatter their own runs (k_eval_hybrid `scatter`).
+        const uint32_t nblk = std::min<uint32_t>(n_tiles, (uint32_t)c->n_cu);
+        const uint32_t wmax = (n_tiles + nblk - 1) / nblk;
+        const uint32_t rpw = (wmax + RUN_TILES_MAX - 1) / RUN_TILES_MAX;
+        c->run_t0.assign((size_t)nblk * rpw + 1, 0u);
+        uint32_t rt = 1;
+        for (uint32_t w = 0; w < nblk; ++w) {
+            const uint32_t t0 = (uint32_t)((uint64_t)n_tiles * w / nblk), t1 = (uint32_t)((uint64_t)n_tiles * (w + 1) / nblk);
+            for (uint32_t j = 0; j < rpw; ++j) {
+                const uint32_t a0 = t0 + (t1 - t0) * j / rpw, a1 = t0 + (t1 - t0) * (j + 1) / rpw;
+                c->run_t0[(size_t)w * rpw + j] = a0;
+                rt = std::max(rt, a1 - a0);
+            }
+        }
+        c->run_t0.back() = n_tiles;
+        const uint64_t area = (uint64_t)nblk * rpw * rt * TILE * fixed_k;  // pairs
         if (nb <= BKT_MAX && !skewed && area < (1ull << 32)) {  // pair positions are 32-bit in k_bresolve
             b.bkt_width = (uint32_t)width;
             b.bkt_magic = (uint32_t)((1ull << 32) / width);
             b.n_bkt = (uint32_t)nb;
             b.run_tiles = rt;
-            b.n_runs = (n_tiles + b.run_tiles - 1) / b.run_tiles;
+            b.n_runs = nblk * rpw;
+            uint32_t* d_rt0 = nullptr;
+            if ((rc = dalloc(c, &d_rt0, c->run_t0.size()))) return bail(rc);
+            if (hipStreamSynchronize(c->stream) != hipSuccess ||
+                hipMemcpy(d_rt0, c->run_t0.data(), c->run_t0.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+                return bail(fail(ALLL_ERR_HIP, "run table upload failed"));
+            b.run_t0 = d_rt0;
             const size_t run_cap = (size_t)b.run_tiles * TILE * fixed_k;
             if ((rc = dalloc(c, &b.pairs, (size_t)b.n_runs * run_cap))) return bail(rc);
             if ((rc = dalloc(c, &b.runtab, (size_t)b.n_bkt * b.n_runs))) return bail(rc);
@@ -834,7 +861,11 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
             const uint64_t cl = perm[p2];
             for (int j = 0; j < fixed_k; ++j)
                 tmp[j] = flagged.empty() ? prob->literals[cl * fixed_k + j] : flagged[cl * fixed_k + j];
-            std::sort(tmp, tmp + fixed_k, [](uint32_t x, uint32_t y) { return (x >> 1) > (y >> 1); });
+            // by descending variable (the hot flag, bit 31, is not part of it: slot K-1 must
+            // hold the smallest variable, which the tile's window and bit 31 of win_base cover)
+            std::sort(tmp, tmp + fixed_k, [](uint32_t x, uint32_t y) {
+                return ((x & 0x7FFFFFFFu) >> 1) > ((y & 0x7FFFFFFFu) >> 1);
+            });
             const uint64_t g = p2 / CHUNK, r = p2 % CHUNK;
             for (int j = 0; j < fixed_k; ++j) {
                 const uint32_t idp = cv.id_bits ? ((uint32_t)(cl >> (j * cv.id_bits)) & id_mask) << cv.id_shift : 0u;

@@ -1014,10 +1014,21 @@ __global__ __launch_bounds__(ROUND_THREADS) void k_wclaim(ClauseView cv, LoopBuf
     const DevState* st = b.state;
     if (!st->active) return;
     constexpr int S = Ent<K>::S;
+    // hot-variable instances: the workgroup's claims on hot variables are reduced in an LDS
+    // hash first and sent as one atomic per variable (a hub is claimed by hundreds of waves in
+    // the early wave rounds; memory-side atomics on one address serialise), so every wave
+    // reaches the workgroup barriers of the table
+    const bool hot = cv.n_hot != 0;
+    __shared__ uint32_t s_hk[HOT_SLOTS];
+    __shared__ unsigned long long s_hv[HOT_SLOTS];
+    HotTable ht{s_hk, s_hv};
+    if (hot) {
+        ht.init();
+        __syncthreads();
+    }
     const uint32_t tile = wave_tile();
-    if (tile >= b.n_tiles) return;
-    const uint32_t cnt = __builtin_amdgcn_readfirstlane(b.tile_cnt[tile]);
-    if (cnt == 0) return;
+    const uint32_t cnt = tile < b.n_tiles ? __builtin_amdgcn_readfirstlane(b.tile_cnt[tile]) : 0u;
+    if (cnt == 0 && !hot) return;
     const int lane = threadIdx.x & 63;
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     const uint32_t stamp = st->stamp;
@@ -1041,11 +1052,9 @@ __global__ __launch_bounds__(ROUND_THREADS) void k_wclaim(ClauseView cv, LoopBuf
                 if (!killed) {
                     for (uint32_t j = 0; j < len; ++j) {
                         const uint32_t raw = ent_lit<K>(cv, e, lb, j);
-                        unsigned long long* o = &owner[vmix(b, lit_var(raw))];
-                        // hubs: test first (see HotTable::flush)
-                        if (!(raw & LIT_HOT) ||
-                            (keyhi | key) < __hip_atomic_load(o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-                            __hip_atomic_fetch_min(o, keyhi | key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if (hot && (raw & LIT_HOT)) ht.claim(lit_var(raw), keyhi | key);
+                        else __hip_atomic_fetch_min(&owner[vmix(b, lit_var(raw))], keyhi | key, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
                     }
                     keep = true;
                 }
@@ -1055,7 +1064,11 @@ __global__ __launch_bounds__(ROUND_THREADS) void k_wclaim(ClauseView cv, LoopBuf
         if (keep) store_ent<K>(lout + (uint64_t)(kept + __popcll(km & lt)) * S, e);
         kept += (uint32_t)__popcll(km);
     }
-    if (lane == 0) b.tile_cnt[tile] = kept;
+    if (lane == 0 && cnt) b.tile_cnt[tile] = kept;
+    if (hot) {
+        __syncthreads();
+        ht.flush(owner, b);
+    }
 }
 
 template <int K>

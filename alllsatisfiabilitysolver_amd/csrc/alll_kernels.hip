@@ -1466,27 +1466,32 @@ __device__ __forceinline__ void resolve_seg_table(const ResolveLds& L, uint32_t 
 // instead of 8 for the latency-bound sweeps).  Sweeps past the first use a per-sweep item ->
 // segment table too (no binary search per item).
 //
-// fused_reduce (one GPU): the loop's reduce runs in an extra workgroup (blockIdx.x == n_bkt)
-// beside the buckets, saving the k_reduce launch.  The bucket workgroups then read no loop
+// fused_reduce (one GPU): the loop's reduce runs in workgroup 0 after its bucket, saving the
+// k_reduce launch.  The bucket workgroups then read no loop
 // state: when the iteration turns out inactive, their marks are never consumed (k_bjoin tests
 // state.active, set by then), and a skipped evaluation leaves the previous pairs, which are
 // resolved again to the same marks.
 template <int U, int T>
+__device__ void resolve_bucket(const LoopBuffers& b, uint32_t run_cap);
+
+template <int U, int T>
 __global__ __launch_bounds__(T, (U <= BRS_UNROLL_NARROW && T <= 512) ? 2 : 1) void k_bresolve(LoopBuffers b,
                                                                                               uint32_t run_cap,
                                                                                               int fused_reduce) {
-    if (fused_reduce) {
-        if (blockIdx.x == b.n_bkt) {
-            if (eval_gate_closed(b.state)) {
-                if (threadIdx.x == 0) b.state->active = 0;
-            } else {
-                reduce_body(b, 0);
-            }
-            return;
+    if (!fused_reduce && !b.state->active) return;
+    resolve_bucket<U, T>(b, run_cap);
+    if (fused_reduce && blockIdx.x == 0) {  // (no extra workgroup: every CU may hold a bucket)
+        __syncthreads();
+        if (eval_gate_closed(b.state)) {
+            if (threadIdx.x == 0) b.state->active = 0;
+        } else {
+            reduce_body(b, 0);
         }
-    } else if (!b.state->active) {
-        return;
     }
+}
+
+template <int U, int T>
+__device__ void resolve_bucket(const LoopBuffers& b, uint32_t run_cap) {
     extern __shared__ uint32_t s_min[];
     __shared__ uint32_t s_start[BKT_RUN_BATCH], s_pre[BKT_RUN_BATCH + 1];
     __shared__ uint32_t s_wsum[T / 64];
@@ -2607,7 +2612,7 @@ hipError_t launch_round0_buckets(const ClauseView& cv, const LoopBuffers& b, boo
                                   cv, b, b.stage[0], fr)));
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    const uint32_t nb = b.n_bkt + fr;
+    const uint32_t nb = b.n_bkt;
     if (b.n_bkt <= b.n_cu)
         k_bresolve<BRS_UNROLL_WIDE, BRS_THREADS><<<nb, BRS_THREADS, lds, s>>>(b, (uint32_t)run_cap, fr);
     else if (lds > (size_t)BRS_DEEP_LDS)  // minima too large for two workgroups per CU

@@ -75,7 +75,10 @@ struct alll_ctx {
     uint32_t tiles_per_rank = 0, own_begin = 0, own_end = 0, n_tiles_padded = 0;
     uint32_t grid_rounds = DEFAULT_GRID_ROUNDS;
     bool fuse_reduce = true;     // env ALLL_FUSE_REDUCE=0: separate k_reduce (tests, A/B)
-    bool fuse_scatter = true;    // env ALLL_FUSE_SCATTER=0: separate k_bscatter (tests, A/B)
+    // env ALLL_FUSE_SCATTER=1: the evaluation workgroups scatter their runs themselves (no
+    // k_bscatter launch; +2.6% iterations/s at M, but the evaluation kernel's duration then
+    // includes the scatter, so its roofline is no longer the evaluation's: off by default)
+    bool fuse_scatter = false;
     std::vector<uint32_t> run_t0;  // bucketed round 0: first tile of every run (+ end)
     uint32_t wave_round_min = WAVE_ROUND_MIN;  // first grid round with a wave per tile
     int rank = 0, world = 1;

@@ -28,8 +28,8 @@ LAYOUTS = {"hybrid": (0, {}), "fixed": (1 << 3, {}), "csr": (1 << 2, {}), "atomi
            "positions": (0, {"ALLL_PACKED_IDS": "0"}),
            # hot-variable instances without the owner/bucket spread (identity vmix)
            "no_vmix": (0, {"ALLL_NO_VMIX": "1", "ALLL_BUCKET_MIN_U": "0"}),
-           # bucketed round 0 with the standalone k_bscatter instead of the evaluation's scatter
-           "no_scatter": (0, {"ALLL_FUSE_SCATTER": "0", "ALLL_BUCKET_MIN_U": "0"}),
+           # bucketed round 0 scattered by the evaluation workgroups (no k_bscatter)
+           "scatter": (0, {"ALLL_FUSE_SCATTER": "1", "ALLL_BUCKET_MIN_U": "0"}),
            # ... and with the separate k_reduce
            "no_fusion": (0, {"ALLL_FUSE_SCATTER": "0", "ALLL_FUSE_REDUCE": "0", "ALLL_BUCKET_MIN_U": "0"})}
 
@@ -302,7 +302,8 @@ BIG = {
     "C5_powerlaw_10M": (2_500_000, 10_000_000, 3, 1),
     # power-law with the atomic round 0 (the default policy buckets it while |U| is large)
     "C5_atomic_round0": (2_500_000, 10_000_000, 3, 1, {"ALLL_BUCKET_MIN_U": str(1 << 62)}),
-    "C5_no_scatter": (2_500_000, 10_000_000, 3, 1, {"ALLL_FUSE_SCATTER": "0"}),
+    "C5_scatter": (2_500_000, 10_000_000, 3, 1, {"ALLL_FUSE_SCATTER": "1"}),
+    "M_scatter": (2_500_000, 10_000_000, 3, 0, {"ALLL_FUSE_SCATTER": "1"}),
     "C5_no_fusion": (2_500_000, 10_000_000, 3, 1, {"ALLL_FUSE_SCATTER": "0", "ALLL_FUSE_REDUCE": "0"}),
     "W_3sat_4Mvars": (4_000_000, 2_000_000, 3, 0),  # 4 LDS blocks of variables: windowed eval
     "M_no_windows": (2_500_000, 10_000_000, 3, 0, {"ALLL_EVAL_WINDOWS": "0"}),

@@ -16,6 +16,7 @@
 // Integer / bit work only: no MFMA.  HBM-bound on the literal stream of k_eval.
 #include <algorithm>
 #include <atomic>
+#include <type_traits>
 
 #include "alll_internal.h"
 
@@ -213,6 +214,44 @@ __device__ __forceinline__ void emit4(const ClauseView& cv, uint32_t* list, uint
     }
 }
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// Buffer resource over one tile's entry list (TILE entries; the range check drops the stores
+// that emit4_bf sends out of range).
+template <int K>
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t list_rsrc(uint32_t* list_tile) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)list_tile);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)list_tile >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uintptr_t)hi << 32) | lo), (short)0, (int)(TILE * 4u * Ent<K>::S), 0x00020000);
+}
+
+// emit4 without branches: every lane stores its four entries, those of satisfied clauses to an
+// out-of-range offset (no memory access), so the count of store instructions is fixed.
+template <int K>
+__device__ __forceinline__ void emit4_bf(__amdgpu_buffer_rsrc_t rs, uint32_t pos, uint64_t c0, const bool v[4],
+                                         const uint4 (&x)[K]) {
+    constexpr uint32_t S = Ent<K>::S;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t off = v[q] ? pos * (S * 4u) : 0x80000000u;
+        pos += v[q] ? 1u : 0u;
+        uint32_t w[S];
+        w[0] = (uint32_t)(c0 + q);
+#pragma unroll
+        for (int j = 0; j < K; ++j) {
+            const uint32_t xs[4] = {x[j].x, x[j].y, x[j].z, x[j].w};
+            w[1 + j] = xs[q];
+        }
+        if constexpr (S == 4) {
+            const u32x4 d = {w[0], w[1], w[2], w[3]};
+            __builtin_amdgcn_raw_buffer_store_b128(d, rs, off, 0, 0);
+        } else {
+#pragma unroll
+            for (uint32_t i = 0; i < S; ++i) __builtin_amdgcn_raw_buffer_store_b32(w[i], rs, off + 4u * i, 0, 0);
+        }
+    }
+}
+
 constexpr int BSC_THREADS = 1024;
 constexpr uint32_t BKT_STAGE = 12288;  // pairs staged in LDS by k_bscatter (96 KiB)
 // LDS of the bucket scatter of one run (the standalone kernel's arrays, or carved from the
@@ -369,6 +408,137 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
     const auto rsA = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(((uintptr_t)a_hi << 32) | a_lo), (short)0, (int)a_bytes, 0x00020000);
     const uint32_t wbits = __popc(cv.lit_mask) - 6u;  // word-index bits of a literal
+    const auto rsV = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)b.vmask, (short)0, (int)__builtin_amdgcn_readfirstlane(b.n_tiles * (TILE_WORDS * 8u)), 0x00020000);
+    // The four lookups of one literal slot (the lane's four clauses): the assignment word of
+    // literal xs[q]'s variable, from LDS when the window holds it, else from L2.  Branch-free
+    // per lane: a word a lane does not need from LDS (outside the window, or need[q] == false:
+    // the clause is already satisfied) reads the zero word s_A[zslot], a word it does not need
+    // from L2 gets an out-of-range buffer offset (the range check returns 0 without a memory
+    // access), so w = gw | lw.  The four buffer loads are issued only when some lane of the
+    // wave needs one (a wave-uniform branch: slot K-1 of a windowed tile and slot 0 of chunks
+    // whose largest variables lie in the window need none).  AL: the whole assignment is in LDS.
+    auto lookup4 = [&](auto al, const uint32_t (&xs)[4], const bool (&need)[4], uint32_t (&gw)[4], uint32_t (&lw)[4]) {
+        constexpr bool AL = decltype(al)::value;
+        bool ng[4];
+        uint32_t goff[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t wi = __builtin_amdgcn_ubfe(xs[q], 6u, wbits);
+            const uint32_t d = wi - wb;  // (unsigned: below the window too)
+            const bool inl = AL || d < lds_words;
+            ng[q] = need[q] && !inl;
+            goff[q] = ng[q] ? wi * 4u : 0x80000000u;
+            lw[q] = s_A[(need[q] && inl) ? d : zslot];
+        }
+        if constexpr (AL) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) gw[q] = 0u;
+        } else if (__builtin_amdgcn_ballot_w64(ng[0] || ng[1] || ng[2] || ng[3])) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) gw[q] = __builtin_amdgcn_raw_buffer_load_b32(rsA, goff[q], 0, 0);
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) gw[q] = 0u;
+        }
+    };
+    // bit 0: the literal is true (its variable's bit of word w, xor the sign, bit 0 of xs; the
+    // other bits are don't-care)
+    auto lit_true = [](uint32_t w, uint32_t xs) -> uint32_t { return __builtin_amdgcn_ubfe(w, xs >> 1, 1u) ^ xs; };
+    // The wave's chunks g = gbeg + wave, + 16, ... of one window segment, software-pipelined:
+    // per chunk, the lookups of slots 0 (largest variable: coalesced gathers) and K-1 (smallest:
+    // mostly in LDS) are issued together, then the literal loads of the wave's next chunk, and
+    // only then are the lookups consumed; the middle slots follow, each only for the clauses
+    // not yet satisfied.  So a wave waits for one literal load and one or two lookup round
+    // trips per chunk, not for a chain of them.
+    auto run_chunks_t = [&](auto al, uint64_t gbeg, uint64_t gend, uint32_t pt) {
+        uint64_t g = gbeg + wave;
+        if (g >= gend) return;
+        auto load_chunk = [&](uint64_t gg, uint4 (&xx)[K]) {
+            const uint4* src = reinterpret_cast<const uint4*>(cv.lits_t + gg * CHUNK * K) + lane;
+#pragma unroll
+            for (int j = 0; j < K; ++j) xx[j] = src[j * 64];
+        };
+        uint4 x[K], xn[K];
+        load_chunk(g, x);
+        for (;;) {
+            // (the last chunk reloads itself instead of a next one: no branch around the loads)
+            const uint64_t gn = g + HYB_THREADS / 64 < gend ? g + HYB_THREADS / 64 : g;
+            const uint64_t cb = g * CHUNK;
+            uint32_t sat[4];
+            {
+                const uint32_t xa[4] = {x[0].x, x[0].y, x[0].z, x[0].w};
+                const uint32_t xb[4] = {x[K - 1].x, x[K - 1].y, x[K - 1].z, x[K - 1].w};
+                uint32_t ga[4], la[4], gb[4], lb[4];
+                const bool all4[4] = {true, true, true, true};
+                lookup4(al, xa, all4, ga, la);
+                if constexpr (K > 1) lookup4(al, xb, all4, gb, lb);
+                // (scheduling barriers keep the next chunk's loads between the lookups' issue
+                // and their use)
+                __builtin_amdgcn_sched_barrier(0);
+                load_chunk(gn, xn);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    sat[q] = lit_true(ga[q] | la[q], xa[q]);
+                    if constexpr (K > 1) sat[q] |= lit_true(gb[q] | lb[q], xb[q]);
+                }
+            }
+#pragma unroll
+            for (int j = 1; j < K - 1; ++j) {  // middle slots (by descending variable)
+                const uint32_t xs[4] = {x[j].x, x[j].y, x[j].z, x[j].w};
+                uint32_t gw[4], lw[4];
+                const bool need[4] = {!(sat[0] & 1u), !(sat[1] & 1u), !(sat[2] & 1u), !(sat[3] & 1u)};
+                lookup4(al, xs, need, gw, lw);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) sat[q] |= lit_true(gw[q] | lw[q], xs[q]);
+            }
+            const uint64_t c0 = cb + 4u * lane;
+            // (wave-uniform: only the last chunk holds positions past m)
+            const uint32_t lim = (uint32_t)min((uint64_t)CHUNK, m - cb);
+            bool v[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) v[q] = !(sat[q] & 1u) && 4u * lane + q < lim;
+            const uint64_t b0 = __ballot(v[0]), b1 = __ballot(v[1]), b2 = __ballot(v[2]), b3 = __ballot(v[3]);
+            // Stores without branches, so that every chunk issues the same number of vector
+            // memory instructions and the wait for the next chunk's literals (loaded before the
+            // stores; the counter is in order) need not wait for the stores: lanes 0 and 1 write
+            // the chunk's four bitmask words (32 aligned bytes), the other lanes and the
+            // satisfied clauses store to an out-of-range offset (dropped by the range check).
+            {
+                const bool lo = lane == 0;
+                const u32x4 vw = {(uint32_t)(lo ? b0 : b2), (uint32_t)((lo ? b0 : b2) >> 32),
+                                  (uint32_t)(lo ? b1 : b3), (uint32_t)((lo ? b1 : b3) >> 32)};
+                __builtin_amdgcn_raw_buffer_store_b128(vw, rsV, lane < 2 ? (uint32_t)g * 32u + lane * 16u : 0x80000000u, 0, 0);
+            }
+            const uint32_t tot = __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
+            // (wide clauses are rarely violated: their entries are stored only by chunks that
+            // hold violated clauses, with the branching emit4)
+            if (K <= 4 || tot) {
+                const uint32_t tile = (uint32_t)(g / (TILE / CHUNK));
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(&s_tcnt[tile - pt], tot);
+                base = __builtin_amdgcn_readfirstlane(base);  // (every lane is active here)
+                // rank of the lane's first violated clause: set bits of the four ballots below
+                // the lane (mbcnt chain)
+                uint32_t pre = 0;
+                pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(b0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b0, pre));
+                pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(b1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b1, pre));
+                pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(b2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b2, pre));
+                pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(b3 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b3, pre));
+                if constexpr (K <= 4) emit4_bf<K>(list_rsrc<K>(b.stage[0] + (uint64_t)tile * TILE * Ent<K>::S), base + pre, c0, v, x);
+                else emit4<K>(cv, b.stage[0] + (uint64_t)tile * TILE * Ent<K>::S, base + pre, c0, v, x);
+            }
+            if (gn == g) break;
+            g = gn;
+#pragma unroll
+            for (int j = 0; j < K; ++j) x[j] = xn[j];
+        }
+    };
+    auto run_chunks = [&](uint64_t gbeg, uint64_t gend, uint32_t pt) {
+        if (all_lds) run_chunks_t(std::true_type{}, gbeg, gend, pt);
+        else run_chunks_t(std::false_type{}, gbeg, gend, pt);
+    };
     for (uint32_t pt = t0; pt < t1; pt += HYB_MAX_TILES) {
         const uint32_t pe = min(t1, pt + HYB_MAX_TILES);
         if (threadIdx.x < HYB_MAX_TILES) s_tcnt[threadIdx.x] = 0;
@@ -388,87 +558,7 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
         const uint64_t gbeg = (uint64_t)sa * (TILE / CHUNK);
         const uint64_t gend = min((uint64_t)se * (TILE / CHUNK), (m + CHUNK - 1) / CHUNK);
         sa = se;
-        for (uint64_t g = gbeg + wave; g < gend; g += HYB_THREADS / 64) {
-            const uint64_t cb = g * CHUNK;
-            const bool small_lds = b.win_base && (b.win_base[g / (TILE / CHUNK)] >> 31);
-            uint32_t sat[4] = {0u, 0u, 0u, 0u};
-            uint4 x[K];
-            {
-                const uint4* src = reinterpret_cast<const uint4*>(cv.lits_t + cb * K) + lane;
-#pragma unroll
-                for (int j = 0; j < K; ++j) x[j] = src[j * 64];
-                // slot by slot (largest variable first): a clause already satisfied skips the
-                // lookups of its remaining literals (half of them after slot 0, 3/4 after slot 1).
-                // Per slot, the global loads (words past the LDS range) of the lane's 4 clauses
-                // are issued first, then the LDS reads, into separate registers, and only then
-                // consumed: no load waits for another one.
-#pragma unroll
-                for (int jj = 0; jj < K; ++jj) {
-                    // phase 1: slots 0 and K-1 together (largest variable: coalesced; smallest:
-                    // mostly in LDS); then the middle slots, each only for unsatisfied clauses
-                    const int j = jj == 0 ? 0 : (jj == 1 ? K - 1 : jj - 1);
-                    const bool first = jj == 0 || jj == 1;
-                    const uint32_t xs[4] = {x[j].x, x[j].y, x[j].z, x[j].w};
-                    // Branch-free lookups: every lane issues one buffer load and one LDS read
-                    // per clause.  A word the lane does not need from L2 (in the window, or the
-                    // clause already satisfied) gets an out-of-range buffer offset, which the
-                    // range check turns into 0 without a memory access; a word it does not need
-                    // from LDS reads the zero word s_A[zslot].  So w = global | LDS word.  A
-                    // lane that needs no lookup is already satisfied, so its bit is ignored.
-                    uint32_t gw[4], lw[4];
-                    if (all_lds || (j == K - 1 && small_lds)) {  // (uniform) window-only lookups
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            const uint32_t d = __builtin_amdgcn_ubfe(xs[q], 6u, wbits) - wb;
-                            gw[q] = 0u;
-                            lw[q] = s_A[(first || !(sat[q] & 1u)) ? d : zslot];
-                        }
-                    } else {
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const uint32_t wi = __builtin_amdgcn_ubfe(xs[q], 6u, wbits);
-                        const uint32_t d = wi - wb;  // (unsigned: below the window too)
-                        const bool need = first || !(sat[q] & 1u);
-                        const bool inl = d < lds_words;
-                        gw[q] = __builtin_amdgcn_raw_buffer_load_b32(rsA, (need && !inl) ? wi * 4u : 0x80000000u, 0, 0);
-                        lw[q] = s_A[(need && inl) ? d : zslot];
-                    }
-                    }
-                    // bit 0 of sat: clause satisfied (the literal's value is its variable's bit
-                    // xor the sign, bit 0 of the literal; the other bits of sat are don't-care)
-#pragma unroll
-                    for (int q = 0; q < 4; ++q)
-                        sat[q] |= __builtin_amdgcn_ubfe(gw[q] | lw[q], xs[q] >> 1, 1u) ^ xs[q];
-                }
-            }
-            const uint64_t c0 = cb + 4u * lane;
-            // (wave-uniform: only the last chunk holds positions past m)
-            const uint32_t lim = (uint32_t)min((uint64_t)CHUNK, m - cb);
-            bool v[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) v[q] = !(sat[q] & 1u) && 4u * lane + q < lim;
-            const uint64_t b0 = __ballot(v[0]), b1 = __ballot(v[1]), b2 = __ballot(v[2]), b3 = __ballot(v[3]);
-            if (lane == 0) {  // the chunk's four bitmask words, 32 aligned bytes
-                uint4* vm = reinterpret_cast<uint4*>(b.vmask + g * 4);
-                vm[0] = make_uint4((uint32_t)b0, (uint32_t)(b0 >> 32), (uint32_t)b1, (uint32_t)(b1 >> 32));
-                vm[1] = make_uint4((uint32_t)b2, (uint32_t)(b2 >> 32), (uint32_t)b3, (uint32_t)(b3 >> 32));
-            }
-            const uint32_t tot = __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
-            if (tot) {
-                const uint32_t tile = (uint32_t)(g / (TILE / CHUNK));
-                uint32_t base = 0;
-                if (lane == 0) base = atomicAdd(&s_tcnt[tile - pt], tot);
-                base = __builtin_amdgcn_readfirstlane(base);  // (every lane is active here)
-                // rank of the lane's first violated clause: set bits of the four ballots below
-                // the lane (mbcnt chain)
-                uint32_t pre = 0;
-                pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(b0 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b0, pre));
-                pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(b1 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b1, pre));
-                pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(b2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b2, pre));
-                pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(b3 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b3, pre));
-                emit4<K>(cv, b.stage[0] + (uint64_t)tile * TILE * Ent<K>::S, base + pre, c0, v, x);
-            }
-        }
+        run_chunks(gbeg, gend, pt);
       }
         __syncthreads();
         if (threadIdx.x < pe - pt) {

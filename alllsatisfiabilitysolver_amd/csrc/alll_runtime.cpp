@@ -321,11 +321,12 @@ int enqueue_iteration(alll_ctx* c, hipEvent_t* marks, int variant) {
     if (marks) HIP_TRY(hipEventRecord(marks[0], s));
     // one GPU, bucketed round 0: the evaluation workgroups scatter their runs' claims
     // themselves (no k_bscatter), before the reduce (pre-reduce epoch)
-    const bool scatter = variant == 1 && c->world == 1 && c->hybrid && c->fuse_scatter && c->eval_wgs == 1 &&
+    const bool xchg = c->world > 1 || c->comm;  // the clause-sharded exchange path
+    const bool scatter = variant == 1 && !xchg && c->hybrid && c->fuse_scatter && c->eval_wgs == 1 &&
                          !c->b.rr_T && !getenv("ALLL_EVAL_GRID");
     HIP_TRY(eval_launch(c, c->own_begin, c->own_end, true, scatter));
     if (marks) HIP_TRY(hipEventRecord(marks[1], s));
-    if (c->world > 1) {
+    if (xchg) {
         const size_t words = (size_t)c->tiles_per_rank * TILE_WORDS;
         if (c->comm) {
             NCCL_TRY(ncclAllGather(c->b.vmask + (size_t)c->rank * words, c->b.vmask, words, ncclUint64,
@@ -339,7 +340,7 @@ int enqueue_iteration(alll_ctx* c, hipEvent_t* marks, int variant) {
     if (marks) HIP_TRY(hipEventRecord(marks[2], s));
     // the bucketed round 0 runs the reduce in an extra k_bscatter workgroup (one GPU, no hot
     // variables, not the round robin): one launch less
-    const bool fused = c->fuse_reduce && variant == 1 && c->world == 1 && !c->b.rr_T;
+    const bool fused = c->fuse_reduce && variant == 1 && !xchg && !c->b.rr_T;
     if (!fused) HIP_TRY(launch_reduce(c->b, 0, s));
     if (c->b.rr_T) {
         HIP_TRY(launch_rr_mis(c->cv, c->b, s));
@@ -352,7 +353,7 @@ int enqueue_iteration(alll_ctx* c, hipEvent_t* marks, int variant) {
         HIP_TRY(launch_tail(c->cv, c->b, c->grid_rounds, s));
     }
     if (marks) HIP_TRY(hipEventRecord(marks[3], s));
-    if (c->allreduce && c->world > 1) {
+    if (c->allreduce && xchg) {
         HIP_TRY(launch_resample(c->cv, c->b, c->own_begin, c->own_end, true, s));
         if (c->comm) {
             NCCL_TRY(ncclAllReduce(c->b.delta, c->b.delta, c->b.n_words, ncclUint32, ncclSum, c->comm, s));
@@ -941,10 +942,12 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     if (launch_init_assignment(b, c->stream) != hipSuccess)
         return bail(fail(ALLL_ERR_HIP, "init kernel launch failed"));
 
-    // ---- RCCL communicator (clause-sharded mode)
-    if (c->world > 1) {
-        bool zero = true;
-        for (int i = 0; i < 128; ++i) zero &= opt.comm_id[i] == 0;
+    // ---- RCCL communicator (clause-sharded mode; world 1 with a comm id: a one-rank
+    // communicator that runs the multi-GPU exchange path on one GPU)
+    bool zero_id = true;
+    for (int i = 0; i < 128; ++i) zero_id &= opt.comm_id[i] == 0;
+    if (c->world > 1 || !zero_id) {
+        const bool zero = zero_id;
         if (!zero) {
             ncclUniqueId id;
             memcpy(&id, opt.comm_id, 128);

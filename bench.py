@@ -172,6 +172,9 @@ def main():
     ap.add_argument("--exchange-impl", default="rccl", choices=["rccl", "host"],
                     help="N>1: RCCL collectives (default; a failure is fatal) or the host-staged gloo "
                          "exchange (rehearsal on one GPU, ALLL_BENCH_SAME_DEVICE=1)")
+    ap.add_argument("--rccl-self", action="store_true",
+                    help="N=1 only: run the multi-GPU exchange path over a one-rank RCCL communicator "
+                         "(all-gather / all-reduce inside the captured graphs; rehearsal on one GPU)")
     ap.add_argument("--no-ranged", action="store_true", help="use the L2-gather eval kernel")
     ap.add_argument("--atomic-claims", action="store_true", help="LFMIS round 0 by global atomics")
     ap.add_argument("--grid-rounds", type=int, default=0, help="full-grid LFMIS rounds (0 = default)")
@@ -212,6 +215,9 @@ def main():
             obj = [comm_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(obj, src=0)
             comm_id = obj[0]
+    elif args.rccl_self:
+        exchange_impl = "rccl-self"
+        comm_id = comm_unique_id()
 
     n, m, k, kind, desc = CONFIGS[args.config]
     t0 = time.perf_counter()
@@ -327,7 +333,7 @@ def main():
             "data": "synthetic (seeded counter-based random k-SAT generator, gen_seed=1)",
             "config": {"workload": f"{args.config}: {desc}", "n_vars": n, "n_clauses": m, "k": k,
                        "solve_seed": args.seed,
-                       "exchange": f"{args.exchange}/{exchange_impl}" if world > 1 else "none",
+                       "exchange": f"{args.exchange}/{exchange_impl}" if world > 1 or comm_id else "none",
                        "parallelism": f"clause-shard x{world}"},
             "value_kind": vkind,
             "resample_iters_per_s": iters_s,

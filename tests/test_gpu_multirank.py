@@ -99,3 +99,34 @@ def test_sharded_solver_matches_oracle(oracle_mod, native, world, mode, spec_nam
         assert sum(st["gpu_resamples"]) == st["n_resamples"]
     # all ranks agree on the last MIS
     assert all(r[3] == res[0][3] for r in res)
+
+
+@pytest.mark.parametrize("mode,spec_name", [("allgather", "small"), ("allreduce", "small"),
+                                            ("allgather", "windows")])
+def test_rccl_one_rank_matches_oracle(oracle_mod, native, mode, spec_name):
+    """The multi-GPU exchange path over a real RCCL communicator of one rank: the all-gather of
+    the violated bitmask (and the all-reduce of the XOR delta) run inside the captured hipGraphs
+    of 1 and 8 iterations, the other-shard collect runs, and the trajectory stays the oracle's."""
+    from alllsatisfiabilitysolver_amd import Solver, comm_unique_id
+
+    o = oracle_mod
+    n, m, k, kind, seed, K = SPECS[spec_name]
+    K = max(K, 12)
+    flags = native.FLAG_EXCHANGE_ALLREDUCE if mode == "allreduce" else 0
+    offs, lits = o.generate_ksat(1, n, m, k, kind)
+    st_o, A_o, rows = o.solve(n, offs, lits, seed, max_iters=K + 1, trace=True)
+    def at(i):  # assignment after iteration i (a converged run keeps its last one)
+        return rows[min(i, len(rows) - 1)][4]
+
+    with Solver(n, offs, lits, seed=seed, device=0, rank=0, world=1, comm_id=comm_unique_id(), flags=flags) as s:
+        assert s.comm_size() == 1
+        for i in range(3):  # single-iteration graphs
+            s.run(1)
+            np.testing.assert_array_equal(s.assignment_words(), at(i), err_msg=f"iter {i}")
+        s.run(8)  # the 8-iteration graph
+        np.testing.assert_array_equal(s.assignment_words(), at(10), err_msg="iter 10")
+        s.run(K - 11)
+        np.testing.assert_array_equal(s.assignment_words(), at(K - 1), err_msg=f"iter {K - 1}")
+        st = s.stats()
+    assert st["n_resamples"] == sum(r[3] for r in rows[:K])
+    assert st["n_gpus"] == 1

@@ -89,6 +89,8 @@ struct ClauseView {
     uint32_t lit_mask;      // lits_t literal bits (LIT_MASK when ids are not packed)
     uint32_t id_shift;      // = bit width of the literals when packed
     uint32_t id_bits;       // id bits per slot; 0 = not packed (entries carry positions)
+    uint32_t lits_nt;       // hybrid eval: non-temporal loads of lits_t (a stream larger than
+                            // the Infinity Cache)
     // Ragged widths (generic CSR entries, T = 1, not streaming): the evaluation reads a
     // chunk-transposed copy instead of the CSR arrays.  Clauses are evaluated sorted by width
     // (then by the block of their smallest variable and their largest variable; perm maps

@@ -418,7 +418,11 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
     // access), so w = gw | lw.  The four buffer loads are issued only when some lane of the
     // wave needs one (a wave-uniform branch: slot K-1 of a windowed tile and slot 0 of chunks
     // whose largest variables lie in the window need none).  AL: the whole assignment is in LDS.
-    auto lookup4 = [&](auto al, const uint32_t (&xs)[4], const bool (&need)[4], uint32_t (&gw)[4], uint32_t (&lw)[4]) {
+    // MG: lanes that need no L2 word are masked off instead of sent out of range (instances
+    // larger than the Infinity Cache, whose L2 lookups go to memory: C4 eval 456 -> 427 us; at
+    // M, where they hit in L2, the out-of-range form is as fast or faster)
+    auto lookup4 = [&](auto al, auto mg, const uint32_t (&xs)[4], const bool (&need)[4], uint32_t (&gw)[4],
+                       uint32_t (&lw)[4]) {
         constexpr bool AL = decltype(al)::value;
         bool ng[4];
         uint32_t goff[4];
@@ -435,8 +439,13 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
 #pragma unroll
             for (int q = 0; q < 4; ++q) gw[q] = 0u;
         } else if (__builtin_amdgcn_ballot_w64(ng[0] || ng[1] || ng[2] || ng[3])) {
+            if constexpr (decltype(mg)::value) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) gw[q] = __builtin_amdgcn_raw_buffer_load_b32(rsA, goff[q], 0, 0);
+                for (int q = 0; q < 4; ++q) gw[q] = ng[q] ? __builtin_amdgcn_raw_buffer_load_b32(rsA, goff[q], 0, 0) : 0u;
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) gw[q] = __builtin_amdgcn_raw_buffer_load_b32(rsA, goff[q], 0, 0);
+            }
         } else {
 #pragma unroll
             for (int q = 0; q < 4; ++q) gw[q] = 0u;
@@ -451,13 +460,22 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
     // only then are the lookups consumed; the middle slots follow, each only for the clauses
     // not yet satisfied.  So a wave waits for one literal load and one or two lookup round
     // trips per chunk, not for a chain of them.
-    auto run_chunks_t = [&](auto al, uint64_t gbeg, uint64_t gend, uint32_t pt) {
+    auto run_chunks_t = [&](auto al, auto nt, uint64_t gbeg, uint64_t gend, uint32_t pt) {
         uint64_t g = gbeg + wave;
         if (g >= gend) return;
+        // NT: non-temporal literal loads (a stream larger than the Infinity Cache: it would
+        // only evict the assignment words the L2 lookups need)
         auto load_chunk = [&](uint64_t gg, uint4 (&xx)[K]) {
             const uint4* src = reinterpret_cast<const uint4*>(cv.lits_t + gg * CHUNK * K) + lane;
 #pragma unroll
-            for (int j = 0; j < K; ++j) xx[j] = src[j * 64];
+            for (int j = 0; j < K; ++j) {
+                if constexpr (decltype(nt)::value) {
+                    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src + j * 64));
+                    xx[j] = make_uint4(v.x, v.y, v.z, v.w);
+                } else {
+                    xx[j] = src[j * 64];
+                }
+            }
         };
         uint4 x[K], xn[K];
         load_chunk(g, x);
@@ -471,8 +489,8 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
                 const uint32_t xb[4] = {x[K - 1].x, x[K - 1].y, x[K - 1].z, x[K - 1].w};
                 uint32_t ga[4], la[4], gb[4], lb[4];
                 const bool all4[4] = {true, true, true, true};
-                lookup4(al, xa, all4, ga, la);
-                if constexpr (K > 1) lookup4(al, xb, all4, gb, lb);
+                lookup4(al, nt, xa, all4, ga, la);
+                if constexpr (K > 1) lookup4(al, nt, xb, all4, gb, lb);
                 // (scheduling barriers keep the next chunk's loads between the lookups' issue
                 // and their use)
                 __builtin_amdgcn_sched_barrier(0);
@@ -489,7 +507,7 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
                 const uint32_t xs[4] = {x[j].x, x[j].y, x[j].z, x[j].w};
                 uint32_t gw[4], lw[4];
                 const bool need[4] = {!(sat[0] & 1u), !(sat[1] & 1u), !(sat[2] & 1u), !(sat[3] & 1u)};
-                lookup4(al, xs, need, gw, lw);
+                lookup4(al, nt, xs, need, gw, lw);
 #pragma unroll
                 for (int q = 0; q < 4; ++q) sat[q] |= lit_true(gw[q] | lw[q], xs[q]);
             }
@@ -536,8 +554,9 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
         }
     };
     auto run_chunks = [&](uint64_t gbeg, uint64_t gend, uint32_t pt) {
-        if (all_lds) run_chunks_t(std::true_type{}, gbeg, gend, pt);
-        else run_chunks_t(std::false_type{}, gbeg, gend, pt);
+        if (all_lds) run_chunks_t(std::true_type{}, std::false_type{}, gbeg, gend, pt);
+        else if (cv.lits_nt) run_chunks_t(std::false_type{}, std::true_type{}, gbeg, gend, pt);
+        else run_chunks_t(std::false_type{}, std::false_type{}, gbeg, gend, pt);
     };
     for (uint32_t pt = t0; pt < t1; pt += HYB_MAX_TILES) {
         const uint32_t pe = min(t1, pt + HYB_MAX_TILES);

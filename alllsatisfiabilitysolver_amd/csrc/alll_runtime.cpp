@@ -887,6 +887,11 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
             cv.perm = d_perm;
         }
         cv.lits_t = d_t;
+        // a literal stream larger than the 256 MB Infinity Cache is read non-temporally (it
+        // cannot stay cached between iterations and would evict the assignment words of the L2
+        // lookups); ALLL_EVAL_NT=0/1 overrides (tuning, tests)
+        cv.lits_nt = (uint64_t)real_chunks * CHUNK * fixed_k * 4 > (256ull << 20) ? 1u : 0u;
+        if (const char* e = getenv("ALLL_EVAL_NT")) cv.lits_nt = atoi(e) != 0;
         cv.offs = nullptr;
         if (windows && m) {  // LDS window of every tile: the block of its first clause's smallest variable
             const uint32_t lds_words = std::min<uint32_t>(b.n_words, b.win_words);

@@ -31,7 +31,10 @@ LAYOUTS = {"hybrid": (0, {}), "fixed": (1 << 3, {}), "csr": (1 << 2, {}), "atomi
            # bucketed round 0 scattered by the evaluation workgroups (no k_bscatter)
            "scatter": (0, {"ALLL_FUSE_SCATTER": "1", "ALLL_BUCKET_MIN_U": "0"}),
            # ... and with the separate k_reduce
-           "no_fusion": (0, {"ALLL_FUSE_SCATTER": "0", "ALLL_FUSE_REDUCE": "0", "ALLL_BUCKET_MIN_U": "0"})}
+           "no_fusion": (0, {"ALLL_FUSE_SCATTER": "0", "ALLL_FUSE_REDUCE": "0", "ALLL_BUCKET_MIN_U": "0"}),
+           # the large-instance evaluation (non-temporal literal loads, exec-masked L2 lookups)
+           # with windows
+           "nt_windows": (0, {"ALLL_EVAL_NT": "1", "ALLL_EVAL_WINDOWS": "1"})}
 
 
 def make_solver(layout, monkeypatch, *args, **kw):
@@ -313,6 +316,8 @@ BIG = {
     # C4 (the north star's 8-GPU instance) on one GPU: 27-bit clause ids do not fit in the
     # literals' spare bits (26-bit literals), so evaluation positions + perm; 26 LDS windows
     "C4_3sat_128M": (32_000_000, 128_000_000, 3, 0),
+    # M through the large-instance evaluation variant (C4 takes it by default)
+    "M_nt": (2_500_000, 10_000_000, 3, 0, {"ALLL_EVAL_NT": "1"}),
     # ragged widths 2-12 (bench config R): the chunk-transposed ragged evaluation, CSR LFMIS
     "R_mixed_4M": (1_000_000, 4_000_000, (2, 12), 0),
     "R_mixed_4M_csr": (1_000_000, 4_000_000, (2, 12), 0, {"ALLL_NO_RAGGED": "1"}),

@@ -196,6 +196,12 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but the launcher started WORLD_SIZE={world} ranks")
     if os.environ.get("ALLL_BENCH_SAME_DEVICE"):  # rehearsal of the N>1 path on a 1-GPU box
         local_rank = 0
+    # The result is ONE JSON line on stdout: keep a private handle on it and send everything
+    # else written to file descriptor 1 (RCCL's version banner at communicator init, library
+    # prints) to stderr.
+    result_out = os.fdopen(os.dup(1), "w")
+    sys.stdout.flush()
+    os.dup2(2, 1)
 
     import torch
 
@@ -364,7 +370,8 @@ def main():
         except Exception as e:  # reported, never fatal for the GPU number
             out["cpu_baseline"] = {"value": None, "error": str(e)}
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        result_out.write(json.dumps(out) + "\n")
+        result_out.flush()
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

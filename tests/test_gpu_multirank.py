@@ -130,3 +130,32 @@ def test_rccl_one_rank_matches_oracle(oracle_mod, native, mode, spec_name):
         st = s.stats()
     assert st["n_resamples"] == sum(r[3] for r in rows[:K])
     assert st["n_gpus"] == 1
+
+
+def _bench_stdout(args, env_extra=None):
+    import json
+    import subprocess
+    import sys
+
+    env = dict(os.environ, **(env_extra or {}))
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                       timeout=400, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, f"stdout must be one JSON line, got {len(lines)}: {r.stdout[:500]!r}"
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("mode", ["rccl_self", "host_n2"])
+def test_bench_prints_one_json_line(mode):
+    """The driver reads one JSON line from bench.py's stdout: RCCL's banner at communicator
+    init and the rank processes' output must not reach it (N=1 over a one-rank RCCL
+    communicator; N=2 self-launched ranks over the host exchange on this one GPU)."""
+    common = ["--config", "C2", "--steps", "4", "--warmup", "1", "--no-cpu-baseline", "--event-iters", "0"]
+    if mode == "rccl_self":
+        d = _bench_stdout(common + ["--rccl-self"])
+        assert d["n_gpus"] == 1 and d["config"]["exchange"] == "allgather/rccl-self"
+    else:
+        d = _bench_stdout(common + ["--gpus", "2", "--exchange-impl", "host"], {"ALLL_BENCH_SAME_DEVICE": "1"})
+        assert d["n_gpus"] == 2 and d["ranks_seen"] == 2
+    assert d["steps_done"] == 4 and d["value"] > 0

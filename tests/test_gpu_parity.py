@@ -99,6 +99,11 @@ def _instances():
         "powerlaw": (2000, 8000, 3, 1),
         "k5_multi_tile": (30000, 60000, 5, 0),
         "powerlaw_hot": (20000, 80000, 3, 1),   # hub variables -> LDS-aggregated claims
+        # the other fixed widths of the evaluation (no middle slot, one middle slot, several)
+        "k1": (3000, 2000, 1, 0),
+        "k2": (6000, 9000, 2, 0),
+        "k4": (20000, 60000, 4, 0),
+        "k7": (8000, 12000, 7, 0),
     }.items():
         out[name] = (n,) + generate_ksat(1, n, m, k, kind)
     f = dict(np.load(os.path.join(GOLDEN, "edge_T1.npz")))
@@ -134,7 +139,8 @@ def instances():
 
 @pytest.mark.parametrize("layout", list(LAYOUTS))
 @pytest.mark.parametrize("name", ["c1_ratio4", "u2500_ratio4", "ratio2_solves", "k8", "powerlaw",
-                                  "k5_multi_tile", "powerlaw_hot", "edge", "ragged", "ragged_wide"])
+                                  "k5_multi_tile", "powerlaw_hot", "edge", "ragged", "ragged_wide",
+                                  "k1", "k2", "k4", "k7"])
 def test_trajectory_matches_oracle(gpu, oracle_mod, name, layout, monkeypatch):
     o = oracle_mod
     n, offs, lits = instances()[name]

@@ -58,6 +58,7 @@ constexpr uint32_t DEFAULT_GRID_ROUNDS = 4;
 // captured graphs of 1, 2, 4 and 8 iterations: a batch of n iterations replays n / 8 eight-
 // iteration graphs and at most one of each smaller size (one launch gap per graph)
 constexpr int GRAPH_SIZES = 4;
+constexpr uint64_t SMALL_U_DEFAULT = 8192;
 constexpr uint32_t GRAPH_UNROLL = 1u << (GRAPH_SIZES - 1);
 constexpr uint32_t SKEWED_GRID_ROUNDS = 6;  // instances with hot variables
 
@@ -87,11 +88,14 @@ struct alll_ctx {
     // device allocations
     std::vector<void*> allocs;
     DevState* h_state = nullptr;  // pinned mirror
-    // captured iterations per LFMIS round-0 variant (0: atomic claims, 1: bucketed): [v][j]
+    // captured iterations per LFMIS variant (0: atomic round 0, 1: bucketed round 0, 2: one grid
+    // round + tail for few violated clauses): [v][j]
     // holds 2^j iterations
-    hipGraph_t graph[2][GRAPH_SIZES] = {};
-    hipGraphExec_t graph_exec[2][GRAPH_SIZES] = {};
+    hipGraph_t graph[3][GRAPH_SIZES] = {};
+    hipGraphExec_t graph_exec[3][GRAPH_SIZES] = {};
     bool use_graph = true;
+    uint64_t small_u = 0;       // one grid round (then the tail) when the last pass found at most
+                                // this many violated clauses (variant 2)
     uint64_t bucket_min_u = 0;  // bucketed round 0 when the last pass found at least this many
     hipEvent_t ev[8] = {};
     int n_cu = 256;
@@ -312,8 +316,13 @@ int host_exchange(alll_ctx* c, int op, void* dev, size_t bytes, size_t own_off) 
 // have a fixed cost that only pays off on large violated sets (and they are not built for
 // skewed instances, see create).
 int round0_variant(const alll_ctx* c) {
-    if (!c->b.pairs) return 0;
-    return (c->h_state->n_iter == 0 || c->h_state->u_total >= c->bucket_min_u) ? 1 : 0;
+    const uint64_t u = c->h_state->u_total;
+    if (c->b.pairs && (c->h_state->n_iter == 0 || u >= c->bucket_min_u)) return 1;
+    // few violated clauses (the end of a converging solve): round 0 on the grid, the rest in
+    // the one-workgroup tail -- 6 launches per iteration instead of 12, each ~4.5 us even
+    // when it has almost nothing to do
+    if (c->h_state->n_iter > 0 && u <= c->small_u && !c->b.rr_T) return 2;
+    return 0;
 }
 
 int enqueue_iteration(alll_ctx* c, hipEvent_t* marks, int variant) {
@@ -345,12 +354,13 @@ int enqueue_iteration(alll_ctx* c, hipEvent_t* marks, int variant) {
     if (c->b.rr_T) {
         HIP_TRY(launch_rr_mis(c->cv, c->b, s));
     } else {
-        for (uint32_t r = 0; r < c->grid_rounds; ++r) {
+        const uint32_t rounds = variant == 2 ? 1u : c->grid_rounds;
+        for (uint32_t r = 0; r < rounds; ++r) {
             if (r == 0 && variant == 1)
-                HIP_TRY(launch_round0_buckets(c->cv, c->b, c->grid_rounds == 1, fused, scatter, s));
-            else HIP_TRY(launch_round(c->cv, c->b, r, r + 1 == c->grid_rounds, c->wave_round_min, s));
+                HIP_TRY(launch_round0_buckets(c->cv, c->b, rounds == 1, fused, scatter, s));
+            else HIP_TRY(launch_round(c->cv, c->b, r, r + 1 == rounds, c->wave_round_min, s));
         }
-        HIP_TRY(launch_tail(c->cv, c->b, c->grid_rounds, s));
+        HIP_TRY(launch_tail(c->cv, c->b, rounds, s));
     }
     if (marks) HIP_TRY(hipEventRecord(marks[3], s));
     if (c->allreduce && xchg) {
@@ -596,6 +606,8 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     c->allreduce = (opt.flags & ALLL_FLAG_EXCHANGE_ALLREDUCE) != 0;
     c->use_graph = (opt.flags & ALLL_FLAG_NO_GRAPH) == 0;
     c->grid_rounds = opt.grid_rounds ? opt.grid_rounds : DEFAULT_GRID_ROUNDS;
+    c->small_u = SMALL_U_DEFAULT;
+    if (const char* e = getenv("ALLL_SMALL_U")) c->small_u = strtoull(e, nullptr, 10);  // tuning, tests
     if (const char* e = getenv("ALLL_FUSE_REDUCE")) c->fuse_reduce = atoi(e) != 0;
     if (const char* e = getenv("ALLL_FUSE_SCATTER")) c->fuse_scatter = atoi(e) != 0;
     if (const char* e = getenv("ALLL_WAVE_ROUND_MIN")) c->wave_round_min = (uint32_t)atoi(e);  // A/B
@@ -979,7 +991,7 @@ int alll_destroy(alll_ctx* c) {
     if (!c) return ALLL_OK;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (int v = 0; v < 2; ++v)
+    for (int v = 0; v < 3; ++v)
         for (int u = 0; u < GRAPH_SIZES; ++u) {
             if (c->graph_exec[v][u]) (void)hipGraphExecDestroy(c->graph_exec[v][u]);
             if (c->graph[v][u]) (void)hipGraphDestroy(c->graph[v][u]);

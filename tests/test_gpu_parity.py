@@ -34,7 +34,9 @@ LAYOUTS = {"hybrid": (0, {}), "fixed": (1 << 3, {}), "csr": (1 << 2, {}), "atomi
            "no_fusion": (0, {"ALLL_FUSE_SCATTER": "0", "ALLL_FUSE_REDUCE": "0", "ALLL_BUCKET_MIN_U": "0"}),
            # the large-instance evaluation (non-temporal literal loads, exec-masked L2 lookups)
            # with windows
-           "nt_windows": (0, {"ALLL_EVAL_NT": "1", "ALLL_EVAL_WINDOWS": "1"})}
+           "nt_windows": (0, {"ALLL_EVAL_NT": "1", "ALLL_EVAL_WINDOWS": "1"}),
+           # one grid round + the tail in every iteration after the first (variant 2), and never
+           "tail_all": (0, {"ALLL_SMALL_U": str(1 << 62)}), "no_small_u": (0, {"ALLL_SMALL_U": "0"})}
 
 
 def make_solver(layout, monkeypatch, *args, **kw):

@@ -11,5 +11,5 @@ cp $SRC/trace/run_kernel_stats.csv $SRC/trace/run_domain_stats.csv $DST/trace/
 for d in $SRC/pmc_*/; do n=$(basename $d); mkdir -p $DST/$n; cp $d/run_counter_collection.csv $DST/$n/; done
 [ -n "$3" ] && cp "$3" $DST/bench_default.json
 [ "$CFG" = M ] && cp $SRC/pmc_eval_traffic.json profiles/pmc_eval_traffic.json
-python3 tools/timeline.py $SRC/trace/run_kernel_trace.csv 30 > $DST/iteration_timeline.txt
+python3 tools/timeline.py $SRC/trace/run_kernel_trace.csv ${TL_INDEX:-8} > $DST/iteration_timeline.txt
 du -sh $DST

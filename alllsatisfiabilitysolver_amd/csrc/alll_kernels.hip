@@ -400,13 +400,8 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
     const uint32_t zslot = (lds_words + 3) / 4 * 4;
     if (threadIdx.x == 0) s_A[zslot] = 0u;
     fill(wb);
-    // L2 lookups through a buffer descriptor over the assignment: its range check returns 0
-    // for the out-of-range offsets of lanes that need no L2 word
     const uint32_t a_lo = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)b.A);
     const uint32_t a_hi = __builtin_amdgcn_readfirstlane((uint32_t)((uintptr_t)b.A >> 32));
-    const uint32_t a_bytes = __builtin_amdgcn_readfirstlane(b.n_words * 4u);
-    const auto rsA = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(((uintptr_t)a_hi << 32) | a_lo), (short)0, (int)a_bytes, 0x00020000);
     const uint32_t wbits = __popc(cv.lit_mask) - 6u;  // word-index bits of a literal
     const auto rsV = __builtin_amdgcn_make_buffer_rsrc(
         (void*)b.vmask, (short)0, (int)__builtin_amdgcn_readfirstlane(b.n_tiles * (TILE_WORDS * 8u)), 0x00020000);
@@ -421,19 +416,22 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
     // MG: lanes that need no L2 word are masked off instead of sent out of range (instances
     // larger than the Infinity Cache, whose L2 lookups go to memory: C4 eval 456 -> 427 us; at
     // M, where they hit in L2, the out-of-range form is as fast or faster)
-    auto lookup4 = [&](auto al, auto mg, const uint32_t (&xs)[4], const bool (&need)[4], uint32_t (&gw)[4],
-                       uint32_t (&lw)[4]) {
+    // Offsets are bytes from the window's first word, for LDS and L2 alike (rsW is based at the
+    // window): every variable of a clause is >= its smallest one, whose block starts at or
+    // after its tile's window (§2 of DESIGN.md), so no offset is negative.
+    const uint32_t lds_bytes = lds_words * 4u, zbyte = zslot * 4u;
+    auto lookup4 = [&](auto al, auto mg, __amdgpu_buffer_rsrc_t rsW, uint32_t wb4n, const uint32_t (&xs)[4],
+                       const bool (&need)[4], uint32_t (&gw)[4], uint32_t (&lw)[4]) {
         constexpr bool AL = decltype(al)::value;
         bool ng[4];
         uint32_t goff[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const uint32_t wi = __builtin_amdgcn_ubfe(xs[q], 6u, wbits);
-            const uint32_t d = wi - wb;  // (unsigned: below the window too)
-            const bool inl = AL || d < lds_words;
+            const uint32_t db = __builtin_amdgcn_ubfe(xs[q], 6u, wbits) * 4u + wb4n;
+            const bool inl = AL || db < lds_bytes;
             ng[q] = need[q] && !inl;
-            goff[q] = ng[q] ? wi * 4u : 0x80000000u;
-            lw[q] = s_A[(need[q] && inl) ? d : zslot];
+            goff[q] = ng[q] ? db : 0x80000000u;
+            lw[q] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(s_A) + ((need[q] && inl) ? db : zbyte));
         }
         if constexpr (AL) {
 #pragma unroll
@@ -441,10 +439,10 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
         } else if (__builtin_amdgcn_ballot_w64(ng[0] || ng[1] || ng[2] || ng[3])) {
             if constexpr (decltype(mg)::value) {
 #pragma unroll
-                for (int q = 0; q < 4; ++q) gw[q] = ng[q] ? __builtin_amdgcn_raw_buffer_load_b32(rsA, goff[q], 0, 0) : 0u;
+                for (int q = 0; q < 4; ++q) gw[q] = ng[q] ? __builtin_amdgcn_raw_buffer_load_b32(rsW, goff[q], 0, 0) : 0u;
             } else {
 #pragma unroll
-                for (int q = 0; q < 4; ++q) gw[q] = __builtin_amdgcn_raw_buffer_load_b32(rsA, goff[q], 0, 0);
+                for (int q = 0; q < 4; ++q) gw[q] = __builtin_amdgcn_raw_buffer_load_b32(rsW, goff[q], 0, 0);
             }
         } else {
 #pragma unroll
@@ -463,6 +461,12 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
     auto run_chunks_t = [&](auto al, auto nt, uint64_t gbeg, uint64_t gend, uint32_t pt) {
         uint64_t g = gbeg + wave;
         if (g >= gend) return;
+        // L2 lookups through a buffer descriptor over the assignment from the window on: its
+        // range check returns 0 for the out-of-range offsets of lanes that need no L2 word
+        const uint32_t wbu = __builtin_amdgcn_readfirstlane(wb);
+        const auto rsW = __builtin_amdgcn_make_buffer_rsrc((void*)(((uintptr_t)a_hi << 32 | a_lo) + 4ull * wbu), (short)0,
+                                                           (int)((b.n_words - wbu) * 4u), 0x00020000);
+        const uint32_t wb4n = 0u - 4u * wbu;
         // NT: non-temporal literal loads (a stream larger than the Infinity Cache: it would
         // only evict the assignment words the L2 lookups need)
         auto load_chunk = [&](uint64_t gg, uint4 (&xx)[K]) {
@@ -489,8 +493,8 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
                 const uint32_t xb[4] = {x[K - 1].x, x[K - 1].y, x[K - 1].z, x[K - 1].w};
                 uint32_t ga[4], la[4], gb[4], lb[4];
                 const bool all4[4] = {true, true, true, true};
-                lookup4(al, nt, xa, all4, ga, la);
-                if constexpr (K > 1) lookup4(al, nt, xb, all4, gb, lb);
+                lookup4(al, nt, rsW, wb4n, xa, all4, ga, la);
+                if constexpr (K > 1) lookup4(al, nt, rsW, wb4n, xb, all4, gb, lb);
                 // (scheduling barriers keep the next chunk's loads between the lookups' issue
                 // and their use)
                 __builtin_amdgcn_sched_barrier(0);
@@ -507,7 +511,7 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
                 const uint32_t xs[4] = {x[j].x, x[j].y, x[j].z, x[j].w};
                 uint32_t gw[4], lw[4];
                 const bool need[4] = {!(sat[0] & 1u), !(sat[1] & 1u), !(sat[2] & 1u), !(sat[3] & 1u)};
-                lookup4(al, nt, xs, need, gw, lw);
+                lookup4(al, nt, rsW, wb4n, xs, need, gw, lw);
 #pragma unroll
                 for (int q = 0; q < 4; ++q) sat[q] |= lit_true(gw[q] | lw[q], xs[q]);
             }

@@ -72,7 +72,10 @@ typedef struct alll_options {
     int32_t rank;           /* clause shard of this process (0 .. world-1) */
     int32_t world;          /* number of GPUs the clauses are sharded over (1 = single GPU) */
     uint8_t comm_id[128];   /* RCCL unique id from alll_comm_unique_id() on rank 0 (world > 1);
-                               all zero: no RCCL, alll_set_host_exchange() is required */
+                               all zero: no RCCL, alll_set_host_exchange() is required.  With
+                               world == 1 a non-zero id creates a one-rank communicator and runs
+                               the clause-sharded exchange path on one GPU (a rehearsal of the
+                               multi-GPU path; the results are the same) */
     uint32_t flags;         /* ALLL_FLAG_* */
     uint32_t grid_rounds;   /* full-grid LFMIS rounds before the tail kernel (0 = default) */
     uint64_t stream_batch;  /* 0: SATInstance::solve(vector<ClauseArray*>*) semantics.  > 0: the

@@ -348,6 +348,11 @@ def main():
             "lfmis_rounds_max": st["lfmis_rounds_max"],
             "phase_ms": {k2: pt[k2] for k2 in ("eval_ms", "exchange_ms", "mis_ms", "resample_ms", "total_ms")},
             "phase_iters": pt["iterations"],
+            "phase_note": ("device wall-clock stamps per timed iteration: eval = evaluation kernel; "
+                           "exchange = evaluation end to the reduce's start (N>1: bitmask all-gather "
+                           "+ k_collect; one GPU: the LFMIS round-0 bucket scatter k_bscatter); "
+                           "mis = reduce start to LFMIS tail end; resample = tail end to the next "
+                           "evaluation start (k_resample_vars + launch gaps)"),
             "roofline": {
                 "bound": "hbm",
                 "achieved": achieved,

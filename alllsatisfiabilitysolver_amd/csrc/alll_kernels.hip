@@ -63,6 +63,10 @@ __device__ __forceinline__ uint32_t abit(const uint32_t* __restrict__ A, uint32_
     return (A[v >> 5] >> (v & 31u)) & 1u;
 }
 
+// Compiler fence after loads issued ahead of the branches that decide whether they are needed:
+// the compiler may not sink a load past it, so the loads are in flight together (no wait).
+__device__ __forceinline__ void spec_fence() { asm volatile("" ::: "memory"); }
+
 __device__ __forceinline__ bool eval_gate_closed(const DevState* st) {
     return st->done != 0 || st->n_iter >= st->limit_eval;
 }
@@ -988,11 +992,17 @@ template <int K>
 __global__ __launch_bounds__(ROUND_THREADS) void k_claim(ClauseView cv, LoopBuffers b, uint32_t r,
                                                          uint32_t* in, uint32_t* out) {
     const DevState* st = b.state;
-    if (!st->active) return;
     const uint32_t tile = blockIdx.x;
-    const uint32_t cnt = b.tile_cnt[tile];
-    if (cnt == 0) return;
     constexpr int S = Ent<K>::S;
+    uint32_t* lin = in + (uint64_t)tile * TILE * S;
+    // loop state, count and the first entry of every thread (speculatively: TILE slots per
+    // tile) in one round trip (k_wclaim)
+    Ent<K> e0;
+    load_ent<K>(e0, lin + (uint64_t)threadIdx.x * S);
+    const uint32_t cnt = b.tile_cnt[tile];
+    const uint32_t active = st->active, stamp = st->stamp, rbase = st->round_base;
+    spec_fence();
+    if (!active || cnt == 0) return;
     __shared__ uint32_t s_hk[HOT_SLOTS];
     __shared__ unsigned long long s_hv[HOT_SLOTS];
     __shared__ uint32_t s_keep;
@@ -1001,14 +1011,13 @@ __global__ __launch_bounds__(ROUND_THREADS) void k_claim(ClauseView cv, LoopBuff
     if (hot) ht.init();
     if (threadIdx.x == 0) s_keep = 0;
     __syncthreads();
-    const uint32_t stamp = st->stamp;
-    const unsigned long long keyhi = (unsigned long long)(~(st->round_base + r)) << 32;
-    unsigned long long* owner = owner_of(b, st->round_base + r);
-    uint32_t* lin = in + (uint64_t)tile * TILE * S;
+    const unsigned long long keyhi = (unsigned long long)(~(rbase + r)) << 32;
+    unsigned long long* owner = owner_of(b, rbase + r);
     uint32_t* lout = out + (uint64_t)tile * TILE * S;
     for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
         Ent<K> e;
-        load_ent<K>(e, lin + (uint64_t)i * S);
+        if (i == threadIdx.x) e = e0;
+        else load_ent<K>(e, lin + (uint64_t)i * S);
         if (r == 0 && (cv.id_bits || cv.perm)) {  // raw entry from the evaluation
             ent_unpack<K>(cv, e);
             store_ent<K>(lin + (uint64_t)i * S, e);
@@ -1035,8 +1044,8 @@ __global__ __launch_bounds__(ROUND_THREADS) void k_claim(ClauseView cv, LoopBuff
 // compacted from `in` to `out` (in the last grid round: into the tail kernel's compact list).
 template <int K, typename OwnFn>
 __device__ __forceinline__ void join_tile(const ClauseView& cv, const LoopBuffers& b, uint32_t tile, uint32_t cnt,
-                                          const uint32_t* __restrict__ in, uint32_t* out, int last,
-                                          uint32_t stamp, OwnFn own) {
+                                          const uint32_t* in, uint32_t* out, int last,
+                                          uint32_t stamp, uint32_t mis0, const Ent<K>& e0, OwnFn own) {
     DevState* st = b.state;
     constexpr int S = Ent<K>::S;
     __shared__ uint32_t s_keep, s_join, s_base;
@@ -1045,11 +1054,12 @@ __device__ __forceinline__ void join_tile(const ClauseView& cv, const LoopBuffer
     __syncthreads();
     const uint32_t* lin = in + (uint64_t)tile * TILE * S;
     uint32_t* lout = out + (uint64_t)tile * TILE * S;
-    uint32_t* mis = b.mis + (uint64_t)tile * TILE + b.mis_cnt[tile];
+    uint32_t* mis = b.mis + (uint64_t)tile * TILE + mis0;
     unsigned long long my_lits = 0, my_w = 0;
     for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
         Ent<K> e;
-        load_ent<K>(e, lin + (uint64_t)i * S);
+        if (i == threadIdx.x) e = e0;  // (loaded by the caller with the counts)
+        else load_ent<K>(e, lin + (uint64_t)i * S);
         const uint32_t c = e.w[0];
         const uint32_t key = prio(b, st, c);
         if (key == ~0u) continue;  // streaming: not yielded this iteration, leaves the list
@@ -1082,7 +1092,7 @@ __device__ __forceinline__ void join_tile(const ClauseView& cv, const LoopBuffer
     }
     if (threadIdx.x == 0) {
         b.tile_cnt[tile] = last ? 0u : kept;
-        b.mis_cnt[tile] += s_join;
+        b.mis_cnt[tile] = mis0 + s_join;
         if (s_join) {
             atomicAdd(&b.tile_stats[2 * tile], s_w);  // = s_join unless streaming
             atomicAdd(&b.tile_stats[2 * tile + 1], s_lits);
@@ -1094,16 +1104,20 @@ __device__ __forceinline__ void join_tile(const ClauseView& cv, const LoopBuffer
 // JOIN(r): a clause joins iff owner[v] holds its round-r key for every variable.
 template <int K>
 __global__ __launch_bounds__(JOIN_THREADS) void k_join(ClauseView cv, LoopBuffers b, uint32_t r,
-                                                        const uint32_t* __restrict__ in, uint32_t* out,
+                                                        const uint32_t* in, uint32_t* out,
                                                         int last) {
     const DevState* st = b.state;
-    if (!st->active) return;
     const uint32_t tile = blockIdx.x;
-    const uint32_t cnt = b.tile_cnt[tile];
-    if (cnt == 0) return;
-    const unsigned long long keyhi = (unsigned long long)(~(st->round_base + r)) << 32;
-    const unsigned long long* owner = owner_of(b, st->round_base + r);
-    join_tile<K>(cv, b, tile, cnt, in, out, last, st->stamp,
+    // loop state, counts and the first entry of every thread in one round trip (k_wclaim)
+    Ent<K> e0;
+    load_ent<K>(e0, in + ((uint64_t)tile * TILE + threadIdx.x) * Ent<K>::S);
+    const uint32_t cnt = b.tile_cnt[tile], mis0 = b.mis_cnt[tile];
+    const uint32_t active = st->active, stamp = st->stamp, rbase = st->round_base;
+    spec_fence();
+    if (!active || cnt == 0) return;
+    const unsigned long long keyhi = (unsigned long long)(~(rbase + r)) << 32;
+    const unsigned long long* owner = owner_of(b, rbase + r);
+    join_tile<K>(cv, b, tile, cnt, in, out, last, stamp, mis0, e0,
                  [&](const Ent<K>& e, uint32_t, uint64_t lb, uint32_t len) {
                      bool own = true;
                      const unsigned long long key = keyhi | prio(b, st, e.w[0]);
@@ -1123,10 +1137,22 @@ __device__ __forceinline__ uint32_t wave_tile() {
 
 template <int K>
 __global__ __launch_bounds__(ROUND_THREADS) void k_wclaim(ClauseView cv, LoopBuffers b, uint32_t r,
-                                                          const uint32_t* __restrict__ in, uint32_t* out) {
+                                                          const uint32_t* in, uint32_t* out) {
     const DevState* st = b.state;
-    if (!st->active) return;
     constexpr int S = Ent<K>::S;
+    const uint32_t tile = wave_tile();
+    const int lane = threadIdx.x & 63;
+    const bool tv = tile < b.n_tiles;
+    const uint32_t* lin = in + (uint64_t)(tv ? tile : 0u) * TILE * S;
+    // The loop state, the tile's count and the wave's first 64 entries are loaded together
+    // (the entries speculatively: a tile's list always holds TILE slots), so the kernel pays one
+    // memory round trip before its kill tests instead of three dependent ones.
+    Ent<K> e0;
+    load_ent<K>(e0, lin + (uint64_t)lane * S);
+    const uint32_t cnt0 = b.tile_cnt[tv ? tile : 0u];
+    const uint32_t active = st->active, stamp = st->stamp, rbase = st->round_base;
+    spec_fence();
+    if (!active) return;
     // hot-variable instances: the workgroup's claims on hot variables are reduced in an LDS
     // hash first and sent as one atomic per variable (a hub is claimed by hundreds of waves in
     // the early wave rounds; memory-side atomics on one address serialise), so every wave
@@ -1139,15 +1165,11 @@ __global__ __launch_bounds__(ROUND_THREADS) void k_wclaim(ClauseView cv, LoopBuf
         ht.init();
         __syncthreads();
     }
-    const uint32_t tile = wave_tile();
-    const uint32_t cnt = tile < b.n_tiles ? __builtin_amdgcn_readfirstlane(b.tile_cnt[tile]) : 0u;
+    const uint32_t cnt = tv ? __builtin_amdgcn_readfirstlane(cnt0) : 0u;
     if (cnt == 0 && !hot) return;
-    const int lane = threadIdx.x & 63;
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-    const uint32_t stamp = st->stamp;
-    const unsigned long long keyhi = (unsigned long long)(~(st->round_base + r)) << 32;
-    unsigned long long* owner = owner_of(b, st->round_base + r);
-    const uint32_t* lin = in + (uint64_t)tile * TILE * S;
+    const unsigned long long keyhi = (unsigned long long)(~(rbase + r)) << 32;
+    unsigned long long* owner = owner_of(b, rbase + r);
     uint32_t* lout = out + (uint64_t)tile * TILE * S;
     uint32_t kept = 0;
     for (uint32_t i0 = 0; i0 < cnt; i0 += 64) {
@@ -1155,7 +1177,8 @@ __global__ __launch_bounds__(ROUND_THREADS) void k_wclaim(ClauseView cv, LoopBuf
         Ent<K> e;
         bool keep = false;
         if (i < cnt) {
-            load_ent<K>(e, lin + (uint64_t)i * S);
+            if (i0 == 0) e = e0;
+            else load_ent<K>(e, lin + (uint64_t)i * S);
             uint64_t lb;
             const uint32_t len = ent_len<K>(cv, e, lb);
             const uint32_t key = prio(b, st, e.w[0]);
@@ -1186,22 +1209,27 @@ __global__ __launch_bounds__(ROUND_THREADS) void k_wclaim(ClauseView cv, LoopBuf
 
 template <int K>
 __global__ __launch_bounds__(ROUND_THREADS) void k_wjoin(ClauseView cv, LoopBuffers b, uint32_t r,
-                                                         const uint32_t* __restrict__ in, uint32_t* out, int last) {
+                                                         const uint32_t* in, uint32_t* out, int last) {
     DevState* st = b.state;
-    if (!st->active) return;
     constexpr int S = Ent<K>::S;
     const uint32_t tile = wave_tile();
     if (tile >= b.n_tiles) return;
-    const uint32_t cnt = __builtin_amdgcn_readfirstlane(b.tile_cnt[tile]);
-    if (cnt == 0) return;
     const int lane = threadIdx.x & 63;
-    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-    const uint32_t stamp = st->stamp;
-    const unsigned long long keyhi = (unsigned long long)(~(st->round_base + r)) << 32;
-    const unsigned long long* owner = owner_of(b, st->round_base + r);
     const uint32_t* lin = in + (uint64_t)tile * TILE * S;
+    // loop state, counts and the first 64 entries (speculatively) in one round trip (k_wclaim)
+    Ent<K> e0;
+    load_ent<K>(e0, lin + (uint64_t)lane * S);
+    const uint32_t cnt0 = b.tile_cnt[tile], mc0 = b.mis_cnt[tile];
+    const uint32_t active = st->active, stamp = st->stamp, rbase = st->round_base;
+    spec_fence();
+    if (!active) return;
+    const uint32_t cnt = __builtin_amdgcn_readfirstlane(cnt0);
+    if (cnt == 0) return;
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    const unsigned long long keyhi = (unsigned long long)(~(rbase + r)) << 32;
+    const unsigned long long* owner = owner_of(b, rbase + r);
     uint32_t* lout = out + (uint64_t)tile * TILE * S;
-    const uint32_t m0 = __builtin_amdgcn_readfirstlane(b.mis_cnt[tile]);
+    const uint32_t m0 = __builtin_amdgcn_readfirstlane(mc0);
     uint32_t* mis = b.mis + (uint64_t)tile * TILE + m0;
     uint32_t kept = 0, joined = 0;
     unsigned long long lits = 0, w = 0;
@@ -1210,7 +1238,8 @@ __global__ __launch_bounds__(ROUND_THREADS) void k_wjoin(ClauseView cv, LoopBuff
         Ent<K> e;
         bool own = false, keep = false;
         if (i < cnt) {
-            load_ent<K>(e, lin + (uint64_t)i * S);
+            if (i0 == 0) e = e0;
+            else load_ent<K>(e, lin + (uint64_t)i * S);
             uint64_t lb;
             const uint32_t len = ent_len<K>(cv, e, lb);
             const uint32_t kc = prio(b, st, e.w[0]);
@@ -1692,11 +1721,15 @@ template <int K>
 __global__ __launch_bounds__(BJN_THREADS) void k_bjoin(ClauseView cv, LoopBuffers b, const uint32_t* in,
                                                        uint32_t* out, int last) {
     DevState* st = b.state;
-    if (!st->active) return;
     constexpr int S = Ent<K>::S;
     constexpr int U = K <= 4 ? 2 * BKT_UNROLL : BKT_UNROLL;
     const uint32_t r = blockIdx.x;
+    // the loop state with the run's bounds and pair count (one round trip)
     const uint32_t t0 = b.run_t0[r], nt = b.run_t0[r + 1] - t0;
+    const uint32_t np = b.run_pairs[r];
+    const uint32_t active = st->active, stamp = st->stamp, rbase = st->round_base;
+    spec_fence();
+    if (!active) return;
     extern __shared__ uint32_t s_lost[];  // one byte per entry slot of the run's tiles
     __shared__ uint32_t s_tc[RUN_TILES_MAX], s_pre[RUN_TILES_MAX + 1], s_keep[RUN_TILES_MAX],
         s_join[RUN_TILES_MAX], s_mis0[RUN_TILES_MAX], s_base[RUN_TILES_MAX];
@@ -1718,7 +1751,6 @@ __global__ __launch_bounds__(BJN_THREADS) void k_bjoin(ClauseView cv, LoopBuffer
     if (single) load_run_entries<K, U>(in, t0, nt, s_pre, E, threadIdx.x, e, ok, tts, idx);
     uint8_t* lost = reinterpret_cast<uint8_t*>(s_lost);
     const unsigned long long* pr = b.pairs + (uint64_t)r * b.run_tiles * TILE * K;
-    const uint32_t np = b.run_pairs[r];
     constexpr int PU = 16;  // pairs per thread per sweep (~3 per clause: one sweep at 10M clauses)
     for (uint32_t i0 = threadIdx.x; i0 < np; i0 += blockDim.x * PU) {
         unsigned long long x[PU];
@@ -1735,9 +1767,8 @@ __global__ __launch_bounds__(BJN_THREADS) void k_bjoin(ClauseView cv, LoopBuffer
     __syncthreads();
     dbg_stamp(b, 2, 3);
     const bool hot = cv.n_hot != 0;
-    const unsigned long long keyhi = (unsigned long long)(~st->round_base) << 32;
-    const unsigned long long* owner = owner_of(b, st->round_base);
-    const uint32_t stamp = st->stamp;
+    const unsigned long long keyhi = (unsigned long long)(~rbase) << 32;
+    const unsigned long long* owner = owner_of(b, rbase);
     auto decide = [&]() {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -1905,18 +1936,20 @@ __device__ __forceinline__ uint32_t resample_word(uint64_t seed, uint64_t it, ui
 
 __global__ __launch_bounds__(256) void k_resample_vars(LoopBuffers b) {
     const DevState* st = b.state;
-    if (!st->active) return;
-    const uint32_t stamp = st->stamp;
-    const uint64_t it = st->n_iter - 1;
     const int lane = threadIdx.x & 63;
     const bool lead = (lane & 1) == 0;
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // variables 16t .. 16t+15
     const uint32_t w = (uint32_t)(t >> 1);
     const bool live = w < b.n_words;  // (cover is padded to whole words with zeros)
+    // the stamps and the word are loaded with the loop state (one round trip)
     uint32_t a = 0;
     if (lead && live) a = b.A[w];
     uint4 c = make_uint4(0u, 0u, 0u, 0u);
     if (live) c = reinterpret_cast<const uint4*>(b.cover)[t];
+    const uint32_t active = st->active, stamp = st->stamp;
+    const uint64_t it = st->n_iter - 1;
+    spec_fence();
+    if (!active) return;
     const uint32_t cs[4] = {c.x, c.y, c.z, c.w};
     uint32_t cm = 0;
 #pragma unroll

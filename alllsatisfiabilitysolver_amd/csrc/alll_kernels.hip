@@ -1833,12 +1833,17 @@ __global__ __launch_bounds__(BJN_THREADS) void k_bjoin(ClauseView cv, LoopBuffer
 template <int K>
 __global__ __launch_bounds__(TAIL_THREADS) void k_tail(ClauseView cv, LoopBuffers b, uint32_t first_round) {
     DevState* st = b.state;
-    if (!st->active) return;
     constexpr int S = Ent<K>::S;
-    const uint32_t stamp = st->stamp;
+    // the loop state and the first entry of every thread (speculatively: the list holds
+    // n_tiles * TILE >= TAIL_THREADS entries) in one round trip
+    Ent<K> e0;
+    if (b.n_tiles) load_ent<K>(e0, b.left + (uint64_t)threadIdx.x * S);
+    const uint32_t active = st->active, stamp = st->stamp, n0 = st->left_cnt, rbase = st->round_base;
+    spec_fence();
+    if (!active) return;
     __shared__ uint32_t s_wp, s_tm;
-    uint32_t n = st->left_cnt;
-    uint32_t epoch = st->round_base + first_round;
+    uint32_t n = n0;
+    uint32_t epoch = rbase + first_round;
     uint32_t rounds = 0;
     if (threadIdx.x == 0) s_tm = 0;
     uint32_t* left = b.left;
@@ -1851,7 +1856,10 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail(ClauseView cv, LoopBuffer
         for (uint32_t base = 0; base < n; base += blockDim.x) {
             const uint32_t i = base + threadIdx.x;
             Ent<K> e;
-            if (i < n) load_ent<K>(e, left + (uint64_t)i * S);
+            if (i < n) {
+                if (rounds == 0 && base == 0) e = e0;  // (nothing has been written back yet)
+                else load_ent<K>(e, left + (uint64_t)i * S);
+            }
             __syncthreads();
             if (i < n) {
                 uint64_t lb;

@@ -1383,6 +1383,9 @@ __device__ void scatter_run(const ClauseView& cv, const LoopBuffers& b, uint32_t
     Ent<K> e[U];
     bool ok[U];
     uint32_t tts[U], idx[U];
+    // single sweep: the histogram's atomics return each claim's rank in its bucket, so pass 2
+    // places the pair at bucket start + rank without a second (cursor) atomic
+    uint32_t rk[U][K];
 #pragma unroll
     for (int u = 0; u < U; ++u) ok[u] = false;  // threads past the last entry emit nothing
     // pass 1: bucket histogram (variables only: it runs while the clause-id loads are in
@@ -1407,7 +1410,9 @@ __device__ void scatter_run(const ClauseView& cv, const LoopBuffers& b, uint32_t
             for (int j = 0; j < K; ++j) {
                 const uint32_t raw = e[u].w[1 + j];
                 uint32_t off;
-                if (!(hot && (raw & LIT_HOT))) atomicAdd(&s_hist[bucket_of(b, lit_var(raw), off)], 1u);
+                if (hot && (raw & LIT_HOT)) continue;
+                if (single) rk[u][j] = atomicAdd(&s_hist[bucket_of(b, lit_var(raw), off)], 1u);
+                else atomicAdd(&s_hist[bucket_of(b, lit_var(raw), off)], 1u);
             }
         }
         if (cv.id_bits) {  // the unpacked entries replace the raw ones (k_bjoin reads them)
@@ -1481,7 +1486,8 @@ __device__ void scatter_run(const ClauseView& cv, const LoopBuffers& b, uint32_t
                 if (hot && (raw & LIT_HOT)) continue;
                 const uint32_t v = lit_var(raw);
                 uint32_t off;
-                const uint32_t pos = atomicAdd(&s_hist[bucket_of(b, v, off)], 1u);
+                const uint32_t bk = bucket_of(b, v, off);
+                const uint32_t pos = single ? s_hist[bk] + rk[u][j] : atomicAdd(&s_hist[bk], 1u);
                 const unsigned long long x = make_pair(e[u].w[0], el, off);
                 if (staged) s_pairs[pos] = x;
                 else gpr[pos] = x;

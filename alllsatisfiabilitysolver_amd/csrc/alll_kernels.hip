@@ -1593,19 +1593,28 @@ __device__ __forceinline__ unsigned long long resolve_mark(const ResolveLds& L, 
     return L.min[(uint32_t)x & 0x7FFFu] != (uint32_t)(x >> 32) ? (x | PAIR_LOSE) : x;
 }
 
-// Item -> segment table of one sweep: items [f0, f0 + cap) of the batch, filled segment by
-// segment (a thread per segment overlapping the sweep; first one found by binary search).
+// Item -> segment table of one sweep: items [f0, f0 + cap) of the batch (nr <= BKT_RUN_BATCH
+// segments, pre[nr] = the batch's pair count).  Every thread takes a contiguous range of items,
+// finds the first one's segment by binary search and walks on, so the fill costs the same
+// whatever the segment count (a thread per segment serialised on instances with few runs).
 __device__ __forceinline__ void resolve_seg_table(const ResolveLds& L, uint32_t nr, uint32_t np, uint32_t f0,
                                                   uint32_t cap, uint16_t* s_seg) {
-    uint32_t lo = 0;  // largest q with pre[q] <= f0
+    const uint32_t f1 = min(np, f0 + cap);
+    if (f1 <= f0) return;
+    const uint32_t per = (f1 - f0 + blockDim.x - 1) / blockDim.x;
+    uint32_t f = f0 + threadIdx.x * per;
+    const uint32_t fe = min(f1, f + per);
+    if (f >= fe) return;
+    uint32_t q = 0;  // largest q < nr with pre[q] <= f
 #pragma unroll
     for (int step = 9; step >= 0; --step) {
-        const uint32_t mid = lo + (1u << step);
-        lo = (mid < nr && L.pre[min(mid, nr)] <= f0) ? mid : lo;
+        const uint32_t mid = q + (1u << step);
+        q = (mid < nr && L.pre[min(mid, nr)] <= f) ? mid : q;
     }
-    const uint32_t f1 = min(np, f0 + cap);
-    for (uint32_t q = lo + threadIdx.x; q < nr && L.pre[q] < f1; q += blockDim.x)
-        for (uint32_t f = max(L.pre[q], f0); f < min(L.pre[q + 1], f1); ++f) s_seg[f - f0] = (uint16_t)q;
+    for (; f < fe; ++f) {
+        while (L.pre[q + 1] <= f) ++q;  // (skips empty segments; f < pre[nr])
+        s_seg[f - f0] = (uint16_t)q;
+    }
 }
 
 // T threads, U items per thread and sweep.  <20, 512>: one bucket per CU (minima <= 128 KB, ~9k
@@ -1658,10 +1667,8 @@ __device__ void resolve_bucket(const LoopBuffers& b, uint32_t run_cap) {
         dbg_stamp(b, 1, 1);
         if (np <= stride) {
             if (np > 0) {
-                // item -> segment table (one LDS read per item instead of a binary search):
-                // a thread fills the items of its segments
-                for (uint32_t q = threadIdx.x; q < b.n_runs; q += blockDim.x)
-                    for (uint32_t f = L.pre[q]; f < L.pre[q + 1]; ++f) s_seg[f] = (uint16_t)q;
+                // item -> segment table (one LDS read per item instead of a binary search)
+                resolve_seg_table(L, b.n_runs, np, 0u, np, s_seg);
                 __syncthreads();
 #pragma unroll
                 for (int u = 0; u < U; ++u) {

@@ -94,6 +94,17 @@ struct alll_ctx {
     hipGraph_t graph[3][GRAPH_SIZES] = {};
     hipGraphExec_t graph_exec[3][GRAPH_SIZES] = {};
     bool use_graph = true;
+    std::string graph_note;      // why the loop launches eagerly (empty: graphs replay)
+    // Hint for the LFMIS variant of the next launch batch (round0_variant): the violated count
+    // and pass count of the last pass the host knows of.  read_state refreshes it; every
+    // launch batch ends with an asynchronous copy of the device state into h_async, adopted
+    // by the next batch once its event has completed (so a run(sync=False) loop follows the
+    // device a batch behind instead of freezing at the last read); an assignment set by the
+    // caller makes it unknown (treated as large).
+    uint64_t hint_u = ~0ull, hint_iter = 0;
+    DevState* h_async = nullptr;  // pinned
+    hipEvent_t ev_async = nullptr;
+    bool async_pending = false;
     uint64_t small_u = 0;       // one grid round (then the tail) when the last pass found at most
                                 // this many violated clauses (variant 2)
     uint64_t bucket_min_u = 0;  // bucketed round 0 when the last pass found at least this many
@@ -221,6 +232,8 @@ int build_ragged(alll_ctx* c, const alll_problem* prob) {
         if (acc >= (1ull << 32)) return fail(ALLL_ERR_UNSUPPORTED, "ragged layout exceeds 2^32 chunk slots");
     }
     off[n_chunks] = (uint32_t)acc;
+    static_assert(sizeof(b.n_words) == 4, "n_words");
+    if (b.n_words >= (1u << 25)) return fail(ALLL_ERR_UNSUPPORTED, "ragged layout needs n_words < 2^25");
     const uint32_t false_lit = 64u * b.n_words;  // variable 32 * n_words: its word is out of range
     std::vector<uint32_t> t((size_t)acc * CHUNK, false_lit);
     parallel_for(m, nt, [&](uint64_t p) {
@@ -266,6 +279,9 @@ int build_ragged(alll_ctx* c, const alll_problem* prob) {
 int read_state(alll_ctx* c) {
     HIP_TRY(hipMemcpyAsync(c->h_state, c->b.state, sizeof(DevState), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    c->hint_u = c->h_state->u_total;
+    c->hint_iter = c->h_state->n_iter;
+    c->async_pending = false;  // (the stream is drained: this read is newer)
     if (c->h_state->error)
         return fail(ALLL_ERR_UNSUPPORTED, c->b.rr_T ? "round-robin MIS exceeded its batch cap in one iteration"
                                                     : "LFMIS needed more than %u rounds in one iteration",
@@ -316,13 +332,28 @@ int host_exchange(alll_ctx* c, int op, void* dev, size_t bytes, size_t own_off) 
 // have a fixed cost that only pays off on large violated sets (and they are not built for
 // skewed instances, see create).
 int round0_variant(const alll_ctx* c) {
-    const uint64_t u = c->h_state->u_total;
-    if (c->b.pairs && (c->h_state->n_iter == 0 || u >= c->bucket_min_u)) return 1;
+    const uint64_t u = c->hint_u;
+    if (c->b.pairs && (c->hint_iter == 0 || u >= c->bucket_min_u)) return 1;
     // few violated clauses (the end of a converging solve): round 0 on the grid, the rest in
     // the one-workgroup tail -- 6 launches per iteration instead of 12, each ~4.5 us even
     // when it has almost nothing to do
-    if (c->h_state->n_iter > 0 && u <= c->small_u && !c->b.rr_T) return 2;
+    if (c->hint_iter > 0 && u <= c->small_u && !c->b.rr_T) return 2;
     return 0;
+}
+
+// Adopt the asynchronous state copy of the last launch batch once it has landed.
+void refresh_hint(alll_ctx* c) {
+    if (!c->async_pending || hipEventQuery(c->ev_async) != hipSuccess) return;
+    c->hint_u = c->h_async->u_total;
+    c->hint_iter = c->h_async->n_iter;
+    c->async_pending = false;
+}
+
+int post_state_copy(alll_ctx* c) {
+    HIP_TRY(hipMemcpyAsync(c->h_async, c->b.state, sizeof(DevState), hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipEventRecord(c->ev_async, c->stream));
+    c->async_pending = true;
+    return ALLL_OK;
 }
 
 int enqueue_iteration(alll_ctx* c, hipEvent_t* marks, int variant) {
@@ -382,15 +413,22 @@ int enqueue_iteration(alll_ctx* c, hipEvent_t* marks, int variant) {
 int ensure_graph(alll_ctx* c, int variant, int j) {
     if (!c->use_graph || c->graph_exec[variant][j]) return ALLL_OK;
     hipError_t e = hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal);
-    if (e != hipSuccess) { c->use_graph = false; return ALLL_OK; }
+    if (e != hipSuccess) {
+        c->use_graph = false;
+        c->graph_note = std::string("hipStreamBeginCapture: ") + hipGetErrorString(e);
+        (void)hipGetLastError();
+        return ALLL_OK;
+    }
     int rc = ALLL_OK;
     for (uint32_t i = 0; i < (1u << j) && rc == ALLL_OK; ++i) rc = enqueue_iteration(c, nullptr, variant);
     hipGraph_t g = nullptr;
     e = hipStreamEndCapture(c->stream, &g);
     if (rc != ALLL_OK || e != hipSuccess || !g) {
         if (g) (void)hipGraphDestroy(g);
+        c->graph_note = rc != ALLL_OK ? "capture of the iteration failed: " + g_err
+                                      : std::string("hipStreamEndCapture: ") + hipGetErrorString(e);
         (void)hipGetLastError();
-        c->use_graph = false;  // fall back to eager launches
+        c->use_graph = false;  // fall back to eager launches (alll_uses_graphs reports it)
         return ALLL_OK;
     }
     e = hipGraphInstantiate(&c->graph_exec[variant][j], g, nullptr, nullptr, 0);
@@ -398,6 +436,8 @@ int ensure_graph(alll_ctx* c, int variant, int j) {
         (void)hipGraphDestroy(g);
         c->graph_exec[variant][j] = nullptr;
         c->use_graph = false;
+        c->graph_note = std::string("hipGraphInstantiate: ") + hipGetErrorString(e);
+        (void)hipGetLastError();
         return ALLL_OK;
     }
     c->graph[variant][j] = g;
@@ -407,6 +447,7 @@ int ensure_graph(alll_ctx* c, int variant, int j) {
 
 // n iterations: n / 8 replays of the 8-iteration graph, then one replay per set bit of n % 8
 int launch_iterations(alll_ctx* c, uint64_t n) {
+    refresh_hint(c);
     const int variant = round0_variant(c);
     int rc;
     // every size is captured, instantiated and uploaded at the variant's first launch, so a
@@ -416,13 +457,13 @@ int launch_iterations(alll_ctx* c, uint64_t n) {
     if (!c->use_graph) {
         for (uint64_t i = 0; i < n; ++i)
             if ((rc = enqueue_iteration(c, nullptr, variant))) return rc;
-        return ALLL_OK;
+        return post_state_copy(c);
     }
     for (; n >= GRAPH_UNROLL; n -= GRAPH_UNROLL)
         HIP_TRY(hipGraphLaunch(c->graph_exec[variant][GRAPH_SIZES - 1], c->stream));
     for (int j = GRAPH_SIZES - 2; j >= 0; --j)
         if ((n >> j) & 1u) HIP_TRY(hipGraphLaunch(c->graph_exec[variant][j], c->stream));
-    return ALLL_OK;
+    return post_state_copy(c);
 }
 
 int fill_stats(alll_ctx* c, alll_stats* st) {
@@ -605,19 +646,24 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     c->world = opt.world;
     c->allreduce = (opt.flags & ALLL_FLAG_EXCHANGE_ALLREDUCE) != 0;
     c->use_graph = (opt.flags & ALLL_FLAG_NO_GRAPH) == 0;
+    if (!c->use_graph) c->graph_note = "ALLL_FLAG_NO_GRAPH";
     c->grid_rounds = opt.grid_rounds ? opt.grid_rounds : DEFAULT_GRID_ROUNDS;
     c->small_u = SMALL_U_DEFAULT;
     if (const char* e = getenv("ALLL_SMALL_U")) c->small_u = strtoull(e, nullptr, 10);  // tuning, tests
     if (const char* e = getenv("ALLL_FUSE_REDUCE")) c->fuse_reduce = atoi(e) != 0;
     if (const char* e = getenv("ALLL_FUSE_SCATTER")) c->fuse_scatter = atoi(e) != 0;
-    if (const char* e = getenv("ALLL_WAVE_ROUND_MIN")) c->wave_round_min = (uint32_t)atoi(e);  // A/B
+    // (A/B; at least 1: round 0's raw evaluation entries are unpacked only by k_claim / k_bscatter)
+    if (const char* e = getenv("ALLL_WAVE_ROUND_MIN")) c->wave_round_min = (uint32_t)std::max(1, atoi(e));
     auto bail = [&](int rc) { alll_destroy(c); return rc; };
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
         return bail(fail(ALLL_ERR_HIP, "hipStreamCreate failed"));
     for (auto& e : c->ev)
         if (hipEventCreate(&e) != hipSuccess) return bail(fail(ALLL_ERR_HIP, "hipEventCreate failed"));
-    if (hipHostMalloc((void**)&c->h_state, sizeof(DevState), 0) != hipSuccess)
+    if (hipHostMalloc((void**)&c->h_state, sizeof(DevState), 0) != hipSuccess ||
+        hipHostMalloc((void**)&c->h_async, sizeof(DevState), 0) != hipSuccess)
         return bail(fail(ALLL_ERR_OOM, "hipHostMalloc failed"));
+    if (hipEventCreateWithFlags(&c->ev_async, hipEventDisableTiming) != hipSuccess)
+        return bail(fail(ALLL_ERR_HIP, "hipEventCreate failed"));
 
     // ---- tiles and shards (contiguous clause ranges; concatenation = clause order)
     const uint32_t n_tiles = (uint32_t)((m + TILE - 1) / TILE);
@@ -944,8 +990,12 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
         // Ragged widths, T = 1, not streaming: chunk-transposed copy for k_eval_ragged (the
         // CSR arrays above stay: the LFMIS kernels read clauses by id).  ALLL_FLAG_GENERIC_CSR
         // keeps the clause-order CSR evaluation.
-        const bool ragged = m && !rr_T && !opt.stream_batch && !(opt.flags & ALLL_FLAG_GENERIC_CSR) &&
-                            c->n_vars < (1u << 30) && !getenv("ALLL_NO_RAGGED");
+        // (the padding literal 64 * n_words must decode to an out-of-range word through the 25
+        // word-index bits k_eval_ragged extracts, and leave bit 31 clear: n_words < 2^25;
+        // ALLL_FLAG_NO_RANGED keeps the clause-order CSR evaluation like GENERIC_CSR)
+        const bool ragged = m && !rr_T && !opt.stream_batch &&
+                            !(opt.flags & (ALLL_FLAG_GENERIC_CSR | ALLL_FLAG_NO_RANGED)) &&
+                            b.n_words < (1u << 25) && !getenv("ALLL_NO_RAGGED");
         if (ragged && (rc = build_ragged(c, prob))) return bail(rc);
     }
 
@@ -972,6 +1022,7 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
             if (r != ncclSuccess) return bail(fail(ALLL_ERR_RCCL, "ncclCommInitRank: %s", ncclGetErrorString(r)));
         } else {
             c->use_graph = false;  // host-staged exchange: eager launches
+            c->graph_note = "host-staged exchange (eager launches)";
         }
     }
     if (hipStreamSynchronize(c->stream) != hipSuccess)
@@ -1001,6 +1052,8 @@ int alll_destroy(alll_ctx* c) {
     for (auto& e : c->ev)
         if (e) (void)hipEventDestroy(e);
     if (c->h_state) (void)hipHostFree(c->h_state);
+    if (c->h_async) (void)hipHostFree(c->h_async);
+    if (c->ev_async) (void)hipEventDestroy(c->ev_async);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return ALLL_OK;
@@ -1011,6 +1064,7 @@ int alll_set_host_exchange(alll_ctx* c, alll_exchange_fn fn, void* user) {
     c->xfn = fn;
     c->xuser = user;
     c->use_graph = false;
+    c->graph_note = "host-staged exchange (eager launches)";
     return ALLL_OK;
 }
 
@@ -1096,6 +1150,8 @@ int alll_set_assignment_words(alll_ctx* c, const uint32_t* in, uint64_t n_words)
     if (!w.empty() && (c->n_vars & 31)) w.back() &= (1u << (c->n_vars & 31)) - 1u;
     HIP_TRY(hipStreamSynchronize(c->stream));
     if (c->b.n_words) HIP_TRY(hipMemcpy(c->b.A, w.data(), c->b.n_words * 4ull, hipMemcpyHostToDevice));
+    c->hint_u = ~0ull;  // the next pass's violated count is unknown: no small-set variant
+    c->async_pending = false;
     return ALLL_OK;
 }
 
@@ -1306,5 +1362,11 @@ int alll_comm_size(alll_ctx* c) {
 }
 
 const char* alll_eval_kernel(alll_ctx* c) { return c ? c->eval_name.c_str() : ""; }
+
+int alll_uses_graphs(alll_ctx* c, const char** why) {
+    if (!c) return -1;
+    if (why) *why = c->graph_note.c_str();
+    return c->use_graph ? 1 : 0;
+}
 
 }  // extern "C"

@@ -245,6 +245,13 @@ class Solver:
     def eval_kernel(self) -> str:
         return self._L.alll_eval_kernel(self._ctx).decode()
 
+    def uses_graphs(self):
+        """(True, "") when the loop replays captured hipGraphs; (False, reason) when it launches
+        eagerly (ALLL_FLAG_NO_GRAPH, a host-staged exchange, or a failed capture)."""
+        why = ctypes.c_char_p()
+        r = int(self._L.alll_uses_graphs(self._ctx, ctypes.byref(why)))
+        return r == 1, (why.value or b"").decode()
+
     def comm_size(self) -> int:
         """Ranks in the solve: the RCCL communicator's count (or world with a host exchange)."""
         n = int(self._L.alll_comm_size(self._ctx))

@@ -286,6 +286,15 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     st = s.stats()
+    # the timed loop must have replayed the captured graphs; an eager fallback (a capture or an
+    # RCCL call under capture that failed) would time a different launch pattern unannounced
+    graphs, graph_note = s.uses_graphs()
+    graphs_expected = exchange_impl != "host"
+    create_max = t_create
+    if dist is not None:
+        tc = torch.tensor([t_create], dtype=torch.float64)
+        dist.all_reduce(tc, op=dist.ReduceOp.MAX)
+        create_max = float(tc.item())
     # iterations actually run: an instance that converges stops early (every kernel is gated
     # off after the final zero-violation pass), so m * K / t would overstate the rate
     steps_done = st["n_iterations"] - it0
@@ -342,6 +351,9 @@ def main():
                        "exchange": f"{args.exchange}/{exchange_impl}" if world > 1 or comm_id else "none",
                        "parallelism": f"clause-shard x{world}"},
             "value_kind": vkind,
+            "graphs": graphs,
+            "graph_note": graph_note or None,
+            "create_s_max_over_ranks": create_max,
             "resample_iters_per_s": iters_s,
             "violated_last": st["n_violated"],
             "avg_mis_size": st["avg_mis_size"],
@@ -380,6 +392,10 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+    if graphs_expected and not graphs:
+        log(f"[rank {rank}] FAIL: the loop fell back to eager launches ({graph_note}); the line above "
+            f"does not time the graph-replayed loop")
+        sys.exit(3)
 
 
 if __name__ == "__main__":

@@ -202,6 +202,11 @@ uint64_t alll_eval_bytes(alll_ctx* ctx);
 int alll_layout(alll_ctx* ctx);
 /* Name of the evaluation kernel the loop launches (e.g. "k_eval_hybrid<3>"). */
 const char* alll_eval_kernel(alll_ctx* ctx);
+/* 1 when the loop replays captured hipGraphs, 0 when it launches eagerly (ALLL_FLAG_NO_GRAPH, a
+ * host-staged exchange, or a capture / instantiation that failed: the loop then falls back to
+ * eager launches with the same results); *why (may be NULL) names the reason.  -1: null ctx.
+ * (No reference counterpart: measurement honesty of the benchmark) */
+int alll_uses_graphs(alll_ctx* ctx, const char** why);
 /* Ranks taking part in the clause-sharded solve: ncclCommCount of the RCCL communicator, or
  * alll_options.world with a host-staged exchange (1 on one GPU); -1 on failure.  (The
  * reference counterpart is the thread count of the -p path, example/main.cpp:76-84.) */

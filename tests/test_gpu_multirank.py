@@ -75,13 +75,17 @@ SPECS = {
     "windows": (1_600_000, 40000, 3, 0, 5, 4),
     # 300 iterations: the 8-bit cover stamps wrap once (the reduce clears them at iteration 255)
     "long": (3000, 12000, 3, 0, 6, 300),
+    # BASELINE config C2 at full size (1M variables, 4M clauses = 977 tiles, 489 per rank):
+    # two iterations, bit-exact on both ranks
+    "c2": (1_000_000, 4_000_000, 3, 0, 1, 2),
 }
 
 
 @pytest.mark.parametrize("world,mode,spec_name", [(2, "allgather", "small"), (2, "allreduce", "small"),
                                                   (3, "allgather", "small"), (3, "allreduce", "small"),
                                                   (2, "allgather", "windows"), (2, "allgather", "long"),
-                                                  (2, "allreduce", "long")])
+                                                  (2, "allreduce", "long"), (2, "allgather", "c2"),
+                                                  (2, "allreduce", "c2")])
 def test_sharded_solver_matches_oracle(oracle_mod, native, world, mode, spec_name):
     o = oracle_mod
     n, m, k, kind, seed, K = spec = SPECS[spec_name]

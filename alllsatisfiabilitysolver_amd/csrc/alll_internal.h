@@ -40,7 +40,18 @@ constexpr uint32_t BKT_SHIFT_MIN = 10;
 constexpr uint32_t BKT_SHIFT_MAX = 15;        // LDS minima of k_bresolve: 4 << 15 = 128 KiB
 constexpr uint32_t RUN_TILES_MAX = 16;        // entry index within a run < 16 * TILE = 2^16
 constexpr int BKT_THREADS = 512;
+constexpr uint32_t BKT_RUN_BATCH = 1024;        // runs per segment-table batch of k_bresolve / k_bsort
 constexpr unsigned long long PAIR_LOSE = 1ull << 31;
+// Dependency-driven LFMIS (one GPU, fixed width, no hot variables, clause-order priorities):
+// k_bsort links every round-0 pair to the next claimant of its variable in clause order, then
+// k_decide (one persistent workgroup per run, all resident) decides every violated clause by
+// messages along those per-variable chains instead of grid rounds.
+constexpr int DDS_THREADS = 512;        // k_bsort workgroup        // k_bsort workgroup        // k_bsort workgroup        // k_bsort workgroup
+constexpr int DDS_UNROLL = 8;           // items per thread and sweep           // items per thread and sweep           // items per thread and sweep           // items per thread and sweep (16384 per sweep)
+constexpr uint32_t DDS_SUBW = 2048;      // variables per sort sub-range (LDS counters)
+constexpr uint32_t DDS_CAP = 4096;       // pairs sorted in LDS at once (a variable's claimants must fit)
+constexpr int DDD_THREADS = 1024;        // k_decide workgroup (one per CU)
+constexpr uint32_t DD_TIMEOUT = 10000000u;  // k_decide gives up after 100 ms (100 MHz wall clock)
 // Round-robin MIS of T > 1 clause chunks (the reference's n_threads > 1): at most RR_TMAX sets.
 constexpr uint32_t RR_TMAX = 2048;
 // In-loop kernel timing (ALLL_FLAG_KERNEL_TIMING): per iteration i, slot i % TIME_SLOTS holds
@@ -127,6 +138,9 @@ struct LoopBuffers {
     unsigned long long* pairs;  // bucketed round 0: n_runs x run_tiles*TILE*K pairs (nullptr = atomics)
     unsigned long long* runtab; // [bucket][run]: start | count << 32 of the bucket's pairs in the run
     uint32_t* run_pairs;        // pairs per run
+    uint32_t* dd_msg;           // dependency-driven LFMIS: one message word per pair position (chain
+                                // state of the pair's variable below its clause, tagged with n_iter);
+                                // nullptr = the round-synchronous LFMIS
     const uint32_t* win_base;   // hybrid eval: per tile, first assignment word of its LDS window
                                 // (nullptr: words [0, win_words) for every tile)
     uint32_t win_words;         // hybrid eval: LDS window size in words (<= LDS_WORDS)
@@ -181,6 +195,13 @@ hipError_t launch_round(const ClauseView& cv, const LoopBuffers& b, uint32_t r, 
                         uint32_t wave_from, hipStream_t s);
 hipError_t launch_round0_buckets(const ClauseView& cv, const LoopBuffers& b, bool last, bool fused_reduce,
                                  bool scattered, hipStream_t s);
+// Dependency-driven LFMIS: k_bscatter (unless `scattered`), k_bsort (+ the loop's reduce in
+// workgroup 0 when `fused_reduce`), k_decide.  Replaces round 0 .. tail.
+hipError_t launch_lfmis_dd(const ClauseView& cv, const LoopBuffers& b, bool scattered, bool fused_reduce,
+                           hipStream_t s);
+// LDS bytes of k_bsort / k_decide for these buffers (the host checks them against the CU's LDS)
+size_t dd_sort_lds(const LoopBuffers& b);
+size_t dd_decide_lds(const LoopBuffers& b, uint32_t k);
 hipError_t launch_tail(const ClauseView& cv, const LoopBuffers& b, uint32_t first_round,
                        hipStream_t s);
 hipError_t launch_rr_mis(const ClauseView& cv, const LoopBuffers& b, hipStream_t s);

@@ -1538,7 +1538,6 @@ __global__ __launch_bounds__(BSC_THREADS) void k_bscatter(ClauseView cv, LoopBuf
 // common case), they stay in registers between the minimum and the marking pass; otherwise
 // the marking pass re-reads them.  Every pair is written back, with PAIR_LOSE set when it is
 // not its variable's minimum: a segment's pairs are contiguous, so these are whole-line stores.
-constexpr uint32_t BKT_RUN_BATCH = 1024;
 constexpr int BRS_THREADS = 512;
 // Items per thread and sweep: 20 (10240 pairs: ~8.9k per bucket at 10M clauses with one bucket
 // per CU; 150 VGPRs, one workgroup per CU), or 16 (8192 pairs; two workgroups per CU) when
@@ -1836,6 +1835,404 @@ __global__ __launch_bounds__(BJN_THREADS) void k_bjoin(ClauseView cv, LoopBuffer
         }
     }
     dbg_stamp(b, 2, 5);
+}
+
+// ------------------------------------------------------------------------------------
+// Dependency-driven LFMIS (one GPU, fixed width, no hot variables).  After the
+// bucket scatter every violated clause c has one pair per literal {c, its entry in the run, its
+// variable's offset in the bucket}.  For a variable v let c_1 < c_2 < ... be the violated
+// clauses that contain it.  c is in the LFMIS iff no lower clause sharing a variable with it is,
+// and "some c_j < c_i on v is in" = (c_{i-1} is in) or (some c_j < c_{i-1} on v is in).  So every
+// pair passes one bit, "covered below", to the next pair of its variable: an IN clause sends 1 on
+// every pair, an OUT clause forwards what its pair received (0 when it has no predecessor).  A
+// clause that receives a 1 is OUT; one that received 0 on every pair with a predecessor is IN.
+// Every message travels from a lower clause to a higher one, so the lowest undecided clause can
+// always decide: the exchange ends with exactly the LFMIS of SATInstance.h:391-451, without
+// grid rounds (the same decisions as CLAIM/JOIN, in ~12 message hops instead of ~12 launches).
+//
+// k_bsort (workgroup per bucket): the bucket's pairs of every run are counted per variable,
+// placed by variable in LDS, and each pair scans its variable's short segment for its
+// predecessor and successor in clause order; it is written back in place as
+//   {successor pair position:32 (~0: none) | has predecessor:1 | entry in run:16 | inert:1}.
+// A clause holding a variable twice keeps its first pair (lowest position) and marks the other
+// inert.  Variables are handled DDS_SUBW at a time (LDS counters) in pieces whose pairs fit
+// DDS_CAP (the host admits only instances whose variables fit one piece).
+constexpr uint32_t DD_NONE = 0xFFFFFFFFu;
+constexpr uint32_t DD_PRED = 1u << 31;
+constexpr uint32_t DD_INERT = 1u;
+constexpr uint32_t DD_EL_MASK = 0xFFFFu << 15;
+
+struct DdSortLds {
+    unsigned long long* sorted;  // DDS_CAP: {clause:32 | pair position:32}
+    uint32_t* cnt;               // DDS_SUBW: per-variable counts, then cursors
+    uint32_t* vst;               // DDS_SUBW + 1: exclusive prefix of the counts
+    uint32_t* start;             // n_runs: segment starts of this bucket
+    uint32_t* pre;               // n_runs + 1: prefix of the segment lengths
+    uint32_t* wsum;              // threads / 64
+    uint16_t* seg;               // threads * unroll: item -> run segment of the current sweep
+};
+
+size_t dd_sort_lds(const LoopBuffers& b) {
+    return 8ull * DDS_CAP + 4ull * DDS_SUBW + 4ull * (DDS_SUBW + 4) + 4ull * (b.n_runs + 4) +
+           4ull * (b.n_runs + 4) + 4ull * (DDS_THREADS / 64) + 2ull * DDS_THREADS * DDS_UNROLL;
+}
+
+// Exclusive prefix of a[0, n) into o[0, n] (o[n] = total; a == o allowed), whole workgroup.
+__device__ uint32_t block_excl_scan(const uint32_t* a, uint32_t* o, uint32_t n, uint32_t* wsum) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t per = (n + blockDim.x - 1) / blockDim.x;
+    const uint32_t q0 = min(n, threadIdx.x * per), q1 = min(n, q0 + per);
+    uint32_t sum = 0;
+    for (uint32_t q = q0; q < q1; ++q) sum += a[q];
+    uint32_t incl = sum;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(incl, d, 64);
+        if (lane >= d) incl += y;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    uint32_t run = incl - sum, total = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+        if (w < wave) run += wsum[w];
+        total += wsum[w];
+    }
+    for (uint32_t q = q0; q < q1; ++q) {
+        const uint32_t c = a[q];
+        o[q] = run;
+        run += c;
+    }
+    if (threadIdx.x == 0) o[n] = total;
+    __syncthreads();
+    return total;
+}
+
+template <int U, int T>
+__global__ __launch_bounds__(T) void k_bsort(LoopBuffers b, uint32_t run_cap, int fused_reduce) {
+    extern __shared__ __attribute__((aligned(16))) unsigned long long s_dds[];
+    DdSortLds L;
+    {
+        char* p = reinterpret_cast<char*>(s_dds);
+        L.sorted = reinterpret_cast<unsigned long long*>(p); p += 8ull * DDS_CAP;
+        L.cnt = reinterpret_cast<uint32_t*>(p); p += 4ull * DDS_SUBW;
+        L.vst = reinterpret_cast<uint32_t*>(p); p += 4ull * (DDS_SUBW + 4);
+        L.start = reinterpret_cast<uint32_t*>(p); p += 4ull * (b.n_runs + 4);
+        L.pre = reinterpret_cast<uint32_t*>(p); p += 4ull * (b.n_runs + 4);
+        L.wsum = reinterpret_cast<uint32_t*>(p); p += 4ull * (T / 64);
+        L.seg = reinterpret_cast<uint16_t*>(p);
+    }
+    const ResolveLds R{nullptr, L.start, L.pre, L.wsum};
+    const uint32_t nr = b.n_runs;  // <= BKT_RUN_BATCH (checked at create)
+    const uint32_t np = resolve_batch(b, R, 0, nr);
+    const uint32_t width = b.bkt_width;
+    const uint32_t stride = T * U;
+    const bool single = np <= stride;
+    const uint32_t first = (threadIdx.x >> 6) * 64 * U + (threadIdx.x & 63);
+    unsigned long long x[U];
+    uint32_t pos[U], rk[U];
+    bool ok[U];
+    // items [s0, s0 + stride) of the bucket's flat index space: positions and pairs
+    auto load_sweep = [&](uint32_t s0) {
+        resolve_seg_table(R, nr, np, s0, stride, L.seg);
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t f = s0 + first + 64 * u;
+            ok[u] = f < np;
+            const uint32_t ff = min(f, np - 1);
+            const uint32_t q = L.seg[ff - s0];
+            pos[u] = q * run_cap + L.start[q] + (ff - L.pre[q]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u] = b.pairs[pos[u]];
+    };
+    if (single && np) load_sweep(0);
+    for (uint32_t v0 = 0; np && v0 < width; v0 += DDS_SUBW) {
+        const uint32_t sw = min(DDS_SUBW, width - v0);
+        for (uint32_t i = threadIdx.x; i < sw; i += T) L.cnt[i] = 0;
+        __syncthreads();
+        // per-variable counts; with one sweep the atomics' results are each pair's rank in its
+        // variable, so the placement needs no cursors
+        if (single) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint32_t v = ((uint32_t)x[u] & 0x7FFFu) - v0;
+                if (ok[u] && v < sw) rk[u] = atomicAdd(&L.cnt[v], 1u);
+            }
+        } else {
+            for (uint32_t s0 = 0; s0 < np; s0 += stride) {
+                load_sweep(s0);
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const uint32_t v = ((uint32_t)x[u] & 0x7FFFu) - v0;
+                    if (ok[u] && v < sw) atomicAdd(&L.cnt[v], 1u);
+                }
+                __syncthreads();  // (the segment table is rewritten by the next sweep)
+            }
+        }
+        __syncthreads();
+        const uint32_t tot = block_excl_scan(L.cnt, L.vst, sw, L.wsum);
+        if (tot == 0) continue;  // (uniform)
+        if (!single) {
+            for (uint32_t i = threadIdx.x; i < sw; i += T) L.cnt[i] = 0;
+            __syncthreads();
+        }
+        for (uint32_t a = 0; a < sw;) {
+            // piece [a, e): the largest e whose pairs fit DDS_CAP (at least one variable)
+            uint32_t lo = a + 1, hi = sw;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi + 1) / 2;
+                if (L.vst[mid] - L.vst[a] <= DDS_CAP) lo = mid; else hi = mid - 1;
+            }
+            const uint32_t e = lo, base = L.vst[a];
+            if (L.vst[e] - base > DDS_CAP && threadIdx.x == 0) b.state->error = 2;  // (host-prevented)
+            auto in_piece = [&](int u) {
+                const uint32_t v = ((uint32_t)x[u] & 0x7FFFu) - v0;
+                return ok[u] && v >= a && v < e;
+            };
+            auto place = [&](int u, uint32_t r) {
+                const uint32_t v = ((uint32_t)x[u] & 0x7FFFu) - v0;
+                const uint32_t slot = L.vst[v] - base + r;
+                if (slot < DDS_CAP) L.sorted[slot] = (x[u] & 0xFFFFFFFF00000000ull) | pos[u];
+            };
+            auto link = [&](int u) {
+                const uint32_t c = (uint32_t)(x[u] >> 32);
+                const uint32_t v = ((uint32_t)x[u] & 0x7FFFu) - v0;
+                const uint32_t sa = L.vst[v] - base, se = min(L.vst[v + 1] - base, DDS_CAP);
+                bool rep = true, pred = false;
+                uint32_t sc = ~0u, sp = DD_NONE;
+                for (uint32_t j = sa; j < se; ++j) {
+                    const unsigned long long y = L.sorted[j];
+                    const uint32_t yc = (uint32_t)(y >> 32), yp = (uint32_t)y;
+                    if (yc < c) pred = true;
+                    else if (yc == c) rep = rep && !(yp < pos[u]);
+                    else if (yc < sc || (yc == sc && yp < sp)) { sc = yc; sp = yp; }
+                }
+                uint32_t lw = (uint32_t)x[u] & DD_EL_MASK;
+                if (!rep) { lw |= DD_INERT; sp = DD_NONE; }
+                else if (pred) lw |= DD_PRED;
+                b.pairs[pos[u]] = ((unsigned long long)sp << 32) | lw;
+            };
+            if (single) {
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    if (in_piece(u)) place(u, rk[u]);
+                __syncthreads();
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    if (in_piece(u)) link(u);
+            } else {
+                for (uint32_t s0 = 0; s0 < np; s0 += stride) {
+                    load_sweep(s0);
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+                        if (in_piece(u)) place(u, atomicAdd(&L.cnt[((uint32_t)x[u] & 0x7FFFu) - v0], 1u));
+                    __syncthreads();
+                }
+                for (uint32_t s0 = 0; s0 < np; s0 += stride) {
+                    load_sweep(s0);
+#pragma unroll
+                    for (int u = 0; u < U; ++u)
+                        if (in_piece(u)) link(u);
+                    __syncthreads();
+                }
+            }
+            __syncthreads();  // (the sorted array is rewritten by the next piece)
+            a = e;
+        }
+    }
+    if (fused_reduce && blockIdx.x == 0) {  // the loop's reduce (one GPU), as in k_bresolve
+        __syncthreads();
+        if (eval_gate_closed(b.state)) {
+            if (threadIdx.x == 0) b.state->active = 0;
+        } else {
+            reduce_body(b, 0);
+        }
+    }
+}
+
+// k_decide (one persistent workgroup per run, all runs resident: n_runs <= CUs): the run's pairs
+// are read in blocks of DDD_BLK (lane l of a wave holds pairs 64 k + l, k < DDD_PB, of its
+// block) and their state is one LDS word per (block, lane): bits 0-7 finished, 8-15 received,
+// 16-23 the received bit, 24-31 has a predecessor.  Entries: one LDS byte per entry slot of the
+// run's tiles: bits 0-3 pairs still waiting for a 0 from their predecessor, bit 4 IN, bit 5
+// OUT.  A pass: (A) poll the message words of the pairs still waiting (relaxed agent-scope
+// loads of words written by relaxed agent-scope stores, i.e. write-through: the tagged
+// single-store granules of MI355X_MICROARCH.md §visibility; tag = n_iter, so nothing is ever
+// reset); a 1 makes the entry OUT, the last 0 makes it IN, and the thread whose decrement
+// reached 0 covers its variables and lists it in its tile's MIS; (B) every pair of a decided
+// entry forwards its chain state to its successor and finishes.  The run is done when all its
+// pairs have finished; the wait is bounded by DD_TIMEOUT (state.error = 3, the loop stops).
+constexpr int DDD_PB = 8;
+constexpr uint32_t DDD_BLK = 64 * DDD_PB;
+
+size_t dd_decide_lds(const LoopBuffers& b, uint32_t k) {
+    const size_t slots = (size_t)b.run_tiles * TILE;
+    const size_t cap = slots * k;
+    return slots + 4 * 64 * ((cap + DDD_BLK - 1) / DDD_BLK);
+}
+
+template <int K>
+__global__ __launch_bounds__(DDD_THREADS) void k_decide(ClauseView cv, LoopBuffers b, const uint32_t* in,
+                                                        uint32_t run_cap) {
+    DevState* st = b.state;
+    constexpr int S = Ent<K>::S;
+    constexpr uint32_t IN_BIT = 0x10u, OUT_BIT = 0x20u;
+    const uint32_t r = blockIdx.x;
+    // the loop state with the run's bounds and pair count (one round trip)
+    const uint32_t t0 = b.run_t0[r], nt = b.run_t0[r + 1] - t0;
+    const uint32_t np = b.run_pairs[r];
+    const uint32_t active = st->active, stamp = st->stamp;
+    const uint32_t tag = (uint32_t)st->n_iter & 0x7FFFFFFFu;  // >= 1 here: never the zero fill
+    spec_fence();
+    if (!active) return;
+    extern __shared__ __attribute__((aligned(16))) uint32_t s_dd[];
+    const uint32_t slots = nt * TILE;
+    uint32_t* entw = s_dd;
+    uint8_t* ent = reinterpret_cast<uint8_t*>(s_dd);
+    uint32_t* pst = s_dd + (size_t)b.run_tiles * TILE / 4;
+    const uint32_t nblk = (np + DDD_BLK - 1) / DDD_BLK;
+    __shared__ uint32_t s_tc[RUN_TILES_MAX], s_pre[RUN_TILES_MAX + 1], s_join[RUN_TILES_MAX], s_mis0[RUN_TILES_MAX];
+    __shared__ unsigned long long s_lits[RUN_TILES_MAX];
+    __shared__ uint32_t s_undone[2], s_stop;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    constexpr int NW = DDD_THREADS / 64;
+    for (uint32_t i = threadIdx.x; i < slots / 4; i += DDD_THREADS) entw[i] = 0;
+    if (threadIdx.x < nt) {
+        s_join[threadIdx.x] = 0;
+        s_lits[threadIdx.x] = 0;
+        s_mis0[threadIdx.x] = b.mis_cnt[t0 + threadIdx.x];
+    }
+    if (threadIdx.x == 0) { s_undone[0] = 0; s_undone[1] = 0; s_stop = 0; }
+    run_prefix(b, t0, nt, s_tc, s_pre);  // (its barriers publish the zeroing above)
+    const unsigned long long* pr = b.pairs + (uint64_t)r * run_cap;
+    const uint32_t* rmsg = b.dd_msg + (uint64_t)r * run_cap;
+    // IN: cover the entry's variables (the resample reads cover), list it in its tile's MIS
+    auto join = [&](uint32_t el) {
+        const uint32_t tt = el / TILE, idx = el % TILE;
+        Ent<K> e;
+        load_ent<K>(e, in + ((uint64_t)(t0 + tt) * TILE + idx) * S);
+#pragma unroll
+        for (int j = 0; j < K; ++j) b.cover[lit_var(e.w[1 + j])] = (uint8_t)stamp;
+        b.mis[(uint64_t)(t0 + tt) * TILE + s_mis0[tt] + atomicAdd(&s_join[tt], 1u)] = e.w[0];
+        atomicAdd(&s_lits[tt], (unsigned long long)K);
+    };
+    auto send = [&](uint32_t sp, uint32_t v) {
+        __hip_atomic_store(b.dd_msg + sp, (tag << 1) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    // pass 0: waiting counts; pairs with nothing to receive and nothing to send finish
+    for (uint32_t blk = wave; blk < nblk; blk += NW) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int k = 0; k < DDD_PB; ++k) {
+            const uint32_t i = blk * DDD_BLK + k * 64 + lane;
+            if (i >= np) { w |= 1u << k; continue; }
+            const unsigned long long x = pr[i];
+            const uint32_t lw = (uint32_t)x, el = (lw >> 15) & 0xFFFFu;
+            if (lw & DD_INERT) w |= 1u << k;
+            else if (lw & DD_PRED) { w |= 1u << (24 + k); atomicAdd(&entw[el >> 2], 1u << (8 * (el & 3))); }
+            else if ((uint32_t)(x >> 32) == DD_NONE) w |= 1u << k;
+        }
+        pst[blk * 64 + lane] = w;
+    }
+    __syncthreads();
+    // entries without a predecessor on any variable: IN
+    for (uint32_t el = threadIdx.x; el < slots; el += DDD_THREADS) {
+        const uint32_t tt = el / TILE;
+        if (el % TILE < s_tc[tt] && ent[el] == 0) {
+            ent[el] = (uint8_t)IN_BIT;
+            join(el);
+        }
+    }
+    __syncthreads();
+    const unsigned long long t_begin = wall_now();
+    for (uint32_t pass = 0;; ++pass) {
+        // (A) receive
+        for (uint32_t blk = wave; blk < nblk; blk += NW) {
+            uint32_t w = pst[blk * 64 + lane];
+            const uint32_t want = (w >> 24) & ~w & ~(w >> 8) & 0xFFu;
+            if (!want) continue;
+            uint32_t m[DDD_PB];
+#pragma unroll
+            for (int k = 0; k < DDD_PB; ++k)
+                m[k] = ((want >> k) & 1u) ? __hip_atomic_load(rmsg + blk * DDD_BLK + k * 64 + lane, __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_AGENT)
+                                          : 0u;
+#pragma unroll
+            for (int k = 0; k < DDD_PB; ++k) {
+                if (!((want >> k) & 1u) || (m[k] >> 1) != tag) continue;
+                const uint32_t v = m[k] & 1u;
+                w |= (1u << (8 + k)) | (v << (16 + k));
+                const uint32_t el = ((uint32_t)pr[blk * DDD_BLK + k * 64 + lane] >> 15) & 0xFFFFu;
+                const uint32_t sh = 8 * (el & 3);
+                if (v) {
+                    atomicOr(&entw[el >> 2], OUT_BIT << sh);
+                } else {
+                    const uint32_t old = atomicSub(&entw[el >> 2], 1u << sh);
+                    if (((old >> sh) & 0xFFu) == 1u) {  // the last wait, no 1 received: IN
+                        atomicOr(&entw[el >> 2], IN_BIT << sh);
+                        join(el);
+                    }
+                }
+            }
+            pst[blk * 64 + lane] = w;
+        }
+        __syncthreads();
+        // (B) forward the chain state of decided entries
+        uint32_t undone = 0;
+        for (uint32_t blk = wave; blk < nblk; blk += NW) {
+            uint32_t w = pst[blk * 64 + lane];
+            const uint32_t open = ~w & 0xFFu;
+            if (open) {
+#pragma unroll
+                for (int k = 0; k < DDD_PB; ++k) {
+                    if (!((open >> k) & 1u)) continue;
+                    const unsigned long long x = pr[blk * DDD_BLK + k * 64 + lane];
+                    const uint32_t lw = (uint32_t)x, sp = (uint32_t)(x >> 32), el = (lw >> 15) & 0xFFFFu;
+                    const uint32_t es = ent[el];
+                    const bool recv = (w >> (8 + k)) & 1u;
+                    if (es & IN_BIT) {
+                        if (sp != DD_NONE) send(sp, 1u);
+                        w |= 1u << k;
+                    } else if (es & OUT_BIT) {
+                        if (!(lw & DD_PRED)) {
+                            send(sp, 0u);  // (a pair with neither neighbour finished at pass 0)
+                            w |= 1u << k;
+                        } else if (recv) {
+                            if (sp != DD_NONE) send(sp, (w >> (16 + k)) & 1u);
+                            w |= 1u << k;
+                        }
+                    } else if (recv && sp == DD_NONE) {
+                        w |= 1u << k;  // counted; nothing to pass on
+                    }
+                }
+                pst[blk * 64 + lane] = w;
+            }
+            undone += (uint32_t)__popc(~w & 0xFFu);
+        }
+        for (int d = 32; d > 0; d >>= 1) undone += __shfl_down(undone, d, 64);
+        if (lane == 0 && undone) atomicAdd(&s_undone[pass & 1], undone);
+        if (threadIdx.x == 0) {
+            s_undone[(pass + 1) & 1] = 0;
+            if (wall_now() - t_begin > DD_TIMEOUT) s_stop = 1;
+        }
+        __syncthreads();
+        if (s_undone[pass & 1] == 0) break;
+        if (s_stop) {
+            if (threadIdx.x == 0) { st->error = 3; st->done = 3; }
+            break;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < nt) {
+        const uint32_t tt = threadIdx.x, tile = t0 + tt;
+        b.tile_cnt[tile] = 0;
+        b.mis_cnt[tile] = s_mis0[tt] + s_join[tt];
+        if (s_join[tt]) {
+            atomicAdd(&b.tile_stats[2 * tile], (unsigned long long)s_join[tt]);
+            atomicAdd(&b.tile_stats[2 * tile + 1], s_lits[tt]);
+        }
+    }
+    if (threadIdx.x == 0 && b.ktime) atomicMax(time_slot(b, st->n_iter - 1) + 3, wall_now());
 }
 
 // Tail: one workgroup finishes the LFMIS over the compact list handed over by the last grid
@@ -2646,7 +3043,7 @@ hipError_t launch_eval(const ClauseView& cv, const LoopBuffers& b, uint32_t tile
 // and device records what is set (contexts on several devices may share a process).
 constexpr int ATTR_MAX_DEV = 64;
 static std::atomic<uint32_t> g_attr_done[ATTR_MAX_DEV];
-enum : uint32_t { ATTR_HYBRID = 0, ATTR_BUCKETS = 9, ATTR_RR = 18, ATTR_RAGGED = 30 };  // + k for per-width groups
+enum : uint32_t { ATTR_HYBRID = 0, ATTR_BUCKETS = 9, ATTR_RR = 18, ATTR_DD = 19, ATTR_RAGGED = 30 };  // + k for per-width groups
 static bool attr_pending(uint32_t bit, int& dev) {
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= ATTR_MAX_DEV) {
         dev = -1;
@@ -2791,6 +3188,38 @@ hipError_t launch_round0_buckets(const ClauseView& cv, const LoopBuffers& b, boo
     const int l = last ? 1 : 0;
     ALLL_DISPATCH_K(cv.k, (k_bjoin<(K > 0 ? K : 1)><<<b.n_runs, BJN_THREADS, (size_t)b.run_tiles * TILE, s>>>(
                               cv, b, b.stage[0], b.stage[1], l)));
+    return hipGetLastError();
+}
+
+hipError_t launch_lfmis_dd(const ClauseView& cv, const LoopBuffers& b, bool scattered, bool fused_reduce,
+                           hipStream_t s) {
+    if (b.n_tiles == 0 || cv.k == 0 || cv.k > (uint32_t)MAX_FIXED_K || !b.pairs || !b.dd_msg) return hipErrorInvalidValue;
+    const uint32_t run_cap = b.run_tiles * TILE * cv.k;
+    const size_t lds_sort = dd_sort_lds(b), lds_dec = dd_decide_lds(b, cv.k);
+    int dev;
+    if (attr_pending(ATTR_DD + cv.k, dev)) {
+        hipError_t e = hipFuncSetAttribute((const void*)k_bsort<DDS_UNROLL, DDS_THREADS>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 512);
+        if (e != hipSuccess) return e;
+        ALLL_DISPATCH_K(cv.k, (e = hipFuncSetAttribute((const void*)k_decide<(K > 0 ? K : 1)>,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 1024)));
+        if (e != hipSuccess) return e;
+        ALLL_DISPATCH_K(cv.k, (e = hipFuncSetAttribute((const void*)k_bscatter<(K > 0 ? K : 1)>,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       (int)(BKT_STAGE * 8))));
+        if (e != hipSuccess) return e;
+        attr_mark(ATTR_DD + cv.k, dev);
+    }
+    const int fr = fused_reduce ? 1 : 0;
+    hipError_t e;
+    if (!scattered) {
+        ALLL_DISPATCH_K(cv.k, (k_bscatter<(K > 0 ? K : 1)><<<b.n_runs, BSC_THREADS, BKT_STAGE * 8, s>>>(
+                                  cv, b, b.stage[0], fr)));
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    k_bsort<DDS_UNROLL, DDS_THREADS><<<b.n_bkt, DDS_THREADS, lds_sort, s>>>(b, run_cap, fr);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    ALLL_DISPATCH_K(cv.k, (k_decide<(K > 0 ? K : 1)><<<b.n_runs, DDD_THREADS, lds_dec, s>>>(cv, b, b.stage[0], run_cap)));
     return hipGetLastError();
 }
 

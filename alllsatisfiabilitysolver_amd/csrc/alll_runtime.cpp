@@ -82,6 +82,7 @@ struct alll_ctx {
     bool fuse_scatter = false;
     std::vector<uint32_t> run_t0;  // bucketed round 0: first tile of every run (+ end)
     uint32_t wave_round_min = WAVE_ROUND_MIN;  // first grid round with a wave per tile
+    bool dd = false;             // dependency-driven LFMIS for the bucketed variant
     int rank = 0, world = 1;
     bool allreduce = false;
     ncclComm_t comm = nullptr;
@@ -282,6 +283,12 @@ int read_state(alll_ctx* c) {
     c->hint_u = c->h_state->u_total;
     c->hint_iter = c->h_state->n_iter;
     c->async_pending = false;  // (the stream is drained: this read is newer)
+    if (c->h_state->error == 2)
+        return fail(ALLL_ERR_UNSUPPORTED, "a variable has more violated claimants than the dependency-driven "
+                                          "LFMIS sorts at once (%u)", DDS_CAP);
+    if (c->h_state->error == 3)
+        return fail(ALLL_ERR_UNSUPPORTED, "dependency-driven LFMIS: a run did not finish within %u ms",
+                    DD_TIMEOUT / 100000u);
     if (c->h_state->error)
         return fail(ALLL_ERR_UNSUPPORTED, c->b.rr_T ? "round-robin MIS exceeded its batch cap in one iteration"
                                                     : "LFMIS needed more than %u rounds in one iteration",
@@ -384,6 +391,8 @@ int enqueue_iteration(alll_ctx* c, hipEvent_t* marks, int variant) {
     if (!fused) HIP_TRY(launch_reduce(c->b, 0, s));
     if (c->b.rr_T) {
         HIP_TRY(launch_rr_mis(c->cv, c->b, s));
+    } else if (variant == 1 && c->dd) {
+        HIP_TRY(launch_lfmis_dd(c->cv, c->b, scatter, fused, s));
     } else {
         const uint32_t rounds = variant == 2 ? 1u : c->grid_rounds;
         for (uint32_t r = 0; r < rounds; ++r) {
@@ -605,9 +614,11 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     // at most HOT_MAX of the highest; flagged in bit 31 of every literal copy the device uses
     std::vector<uint8_t> is_hot;
     uint32_t n_hot = 0;
+    uint32_t max_deg = ~0u;  // most literals of one variable (unknown: ~0)
     if (L && prob->n_vars && prob->n_vars < (1u << 30)) {
         std::vector<uint32_t> deg(prob->n_vars, 0u);
         for (uint64_t j = 0; j < L; ++j) ++deg[prob->literals[j] >> 1];
+        max_deg = *std::max_element(deg.begin(), deg.end());
         const uint64_t thr = std::max<uint64_t>(1024, 32 * (L / prob->n_vars + 1));
         std::vector<std::pair<uint32_t, uint32_t>> hot;
         for (uint32_t v = 0; v < prob->n_vars; ++v)
@@ -755,7 +766,19 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     if (fixed_k > 0 && !(opt.flags & ALLL_FLAG_ATOMIC_CLAIMS) && n_tiles > 0 && c->n_vars > 0) {
         uint32_t shift = BKT_SHIFT_MIN;
         while (shift < BKT_SHIFT_MAX && (vrange >> shift) > 384) ++shift;
-        uint64_t width = (vrange + c->n_cu - 1) / c->n_cu;
+        // (the dependency-driven LFMIS sorts a bucket's pairs in one 8192-item sweep when it
+        // can: two buckets per CU by default, ALLL_DD_BKT_PER_CU to tune)
+        uint32_t per_cu = 1;
+        {
+            bool zid = true;
+            for (int i = 0; i < 128; ++i) zid &= opt.comm_id[i] == 0;
+            const char* e = getenv("ALLL_DD");
+            if (c->world == 1 && zid && !n_hot && !opt.stream_batch && !rr_T && !(e && atoi(e) == 0)) {
+                per_cu = 2;
+                if (const char* e2 = getenv("ALLL_DD_BKT_PER_CU")) per_cu = (uint32_t)std::max(1, atoi(e2));
+            }
+        }
+        uint64_t width = (vrange + (uint64_t)c->n_cu * per_cu - 1) / ((uint64_t)c->n_cu * per_cu);
         width = std::max<uint64_t>(width, 1u << BKT_SHIFT_MIN);
         if (width > (1u << BKT_SHIFT_MAX) || getenv("ALLL_BKT_POW2")) width = 1u << shift;
         if (const char* e = getenv("ALLL_BKT_SHIFT"))  // tuning experiments
@@ -815,6 +838,23 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
             // below this many violated clauses the atomic round 0 is cheaper (fixed costs)
             c->bucket_min_u = std::max<uint64_t>(65536, m / 64);
             if (const char* e = getenv("ALLL_BUCKET_MIN_U")) c->bucket_min_u = strtoull(e, nullptr, 10);
+            // Dependency-driven LFMIS in place of the bucketed rounds: one GPU
+            // without an exchange, clause-order priorities, no hot variables; every run's decide
+            // workgroup resident at once (one per CU), the runs' segment table in one batch, the
+            // LDS of both kernels within a CU's, and every variable's claimants within one sort
+            // piece.  ALLL_DD=0 keeps the round-synchronous LFMIS (tests, A/B).
+            bool zero_id = true;
+            for (int i = 0; i < 128; ++i) zero_id &= opt.comm_id[i] == 0;
+            const uint32_t run_cap32 = b.run_tiles * TILE * (uint32_t)fixed_k;
+            c->dd = c->world == 1 && zero_id && !n_hot && !opt.stream_batch && !rr_T &&
+                    b.n_runs <= (uint32_t)c->n_cu && b.n_runs <= BKT_RUN_BATCH && b.run_tiles <= RUN_TILES_MAX &&
+                    dd_sort_lds(b) <= 160u * 1024 - 512 && dd_decide_lds(b, (uint32_t)fixed_k) <= 160u * 1024 - 1024 &&
+                    max_deg <= DDS_CAP && (uint64_t)b.n_runs * run_cap32 < 0xFFFFFFFFull;
+            if (const char* e = getenv("ALLL_DD")) c->dd = c->dd && atoi(e) != 0;
+            if (c->dd) {
+                if ((rc = dalloc(c, &b.dd_msg, (size_t)b.n_runs * run_cap32))) return bail(rc);
+                c->bucket_min_u = 0;  // three launches at any violated count (no small-set variants)
+            }
         }
     }
     // ---- clause storage allocations, then drain the zero-fills before synchronous uploads

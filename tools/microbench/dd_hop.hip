@@ -33,7 +33,7 @@ __global__ void k_scatter(uint32_t* a, uint32_t mask, uint32_t per, uint32_t sal
 
 // hop h lives at word pos[h] of workgroup wg[h]'s mailbox; its token value is tag + h.  A
 // workgroup's threads each own P / blockDim words and poll the ones they still wait on.
-constexpr int WPT = 16;  // words per thread
+template <int WPT>  // words per thread
 __global__ void k_chain(uint32_t* mbox, const uint32_t* wg, const uint32_t* pos, uint32_t L, uint32_t tag,
                         unsigned long long* arrive, uint32_t* done, uint32_t* timeout, int sleep) {
     const uint32_t P = blockDim.x * WPT;
@@ -105,9 +105,12 @@ int main() {
         }
     }
     // chains
-    for (int cfg = 0; cfg < 4; ++cfg) {
-        const uint32_t th = (cfg & 1) ? 1024 : 256;
-        const int sleep = cfg >> 1;
+    for (int cfg = 0; cfg < 6; ++cfg) {
+        // (threads, words per thread): the 4096-word region by 256 x 16 and 1024 x 4 (residency
+        // vs polling volume), then 1024 x 16 (four times the polling)
+        const uint32_t th = cfg % 3 == 0 ? 256 : 1024;
+        const uint32_t WPT = cfg % 3 == 1 ? 4 : 16;
+        const int sleep = cfg / 3;
         const uint32_t L = 200, P = th * WPT;
         std::vector<uint32_t> wg(L), pos(L);
         uint64_t s = 0x9E3779B97F4A7C15ull + cfg;
@@ -131,7 +134,8 @@ int main() {
         for (int rep = 0; rep < 3; ++rep) {
             const uint32_t tag = 1000u * (rep + 1);
             CK(hipEventRecord(e0));
-            k_chain<<<blocks, th>>>(mb, dwg, dpos, L, tag, arr, done, tmo, sleep);
+            if (WPT == 4) k_chain<4><<<blocks, th>>>(mb, dwg, dpos, L, tag, arr, done, tmo, sleep);
+            else k_chain<16><<<blocks, th>>>(mb, dwg, dpos, L, tag, arr, done, tmo, sleep);
             CK(hipEventRecord(e1));
             CK(hipEventSynchronize(e1));
             float ms;
@@ -143,8 +147,9 @@ int main() {
             std::vector<double> d;
             for (uint32_t i = 1; i < L; ++i) d.push_back((double)(h[i] - h[i - 1]) * 0.01);  // 100 MHz -> us
             std::sort(d.begin(), d.end());
-            printf("chain threads %u sleep %d rep %d: kernel %.1f us, %u hops: total %.1f us, per hop median %.2f p90 %.2f max %.2f us, timeouts %u\n",
-                   th, sleep, rep, ms * 1e3, L - 1, (double)(h[L - 1] - h[0]) * 0.01, d[d.size() / 2], d[d.size() * 9 / 10], d.back(), to);
+            if (h[L - 1] < h[0] || to) { printf("chain threads %u words/thread %u sleep %d rep %d: kernel %.1f us, INCOMPLETE (%u timeouts)\n", th, WPT, sleep, rep, ms * 1e3, to); CK(hipMemset(tmo, 0, 64)); continue; }
+            printf("chain threads %u words/thread %u sleep %d rep %d: kernel %.1f us, %u hops: total %.1f us, per hop median %.2f p90 %.2f max %.2f us, timeouts %u\n",
+                   th, WPT, sleep, rep, ms * 1e3, L - 1, (double)(h[L - 1] - h[0]) * 0.01, d[d.size() / 2], d[d.size() * 9 / 10], d.back(), to);
         }
         hipFree(mb); hipFree(dwg); hipFree(dpos); hipFree(arr); hipFree(done); hipFree(tmo);
     }

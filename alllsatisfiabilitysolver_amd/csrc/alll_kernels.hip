@@ -1922,7 +1922,9 @@ __global__ __launch_bounds__(T) void k_bsort(LoopBuffers b, uint32_t run_cap, in
     }
     const ResolveLds R{nullptr, L.start, L.pre, L.wsum};
     const uint32_t nr = b.n_runs;  // <= BKT_RUN_BATCH (checked at create)
+    dbg_stamp(b, 1, 0);
     const uint32_t np = resolve_batch(b, R, 0, nr);
+    dbg_stamp(b, 1, 1);
     const uint32_t width = b.bkt_width;
     const uint32_t stride = T * U;
     const bool single = np <= stride;
@@ -1946,6 +1948,7 @@ __global__ __launch_bounds__(T) void k_bsort(LoopBuffers b, uint32_t run_cap, in
         for (int u = 0; u < U; ++u) x[u] = b.pairs[pos[u]];
     };
     if (single && np) load_sweep(0);
+    dbg_stamp(b, 1, 2);
     for (uint32_t v0 = 0; np && v0 < width; v0 += DDS_SUBW) {
         const uint32_t sw = min(DDS_SUBW, width - v0);
         for (uint32_t i = threadIdx.x; i < sw; i += T) L.cnt[i] = 0;
@@ -2040,6 +2043,7 @@ __global__ __launch_bounds__(T) void k_bsort(LoopBuffers b, uint32_t run_cap, in
             a = e;
         }
     }
+    dbg_stamp(b, 1, 3);
     if (fused_reduce && blockIdx.x == 0) {  // the loop's reduce (one GPU), as in k_bresolve
         __syncthreads();
         if (eval_gate_closed(b.state)) {
@@ -2052,16 +2056,19 @@ __global__ __launch_bounds__(T) void k_bsort(LoopBuffers b, uint32_t run_cap, in
 
 // k_decide (one persistent workgroup per run, all runs resident: n_runs <= CUs): the run's pairs
 // are read in blocks of DDD_BLK (lane l of a wave holds pairs 64 k + l, k < DDD_PB, of its
-// block) and their state is one LDS word per (block, lane): bits 0-7 finished, 8-15 received,
-// 16-23 the received bit, 24-31 has a predecessor.  Entries: one LDS byte per entry slot of the
-// run's tiles: bits 0-3 pairs still waiting for a 0 from their predecessor, bit 4 IN, bit 5
-// OUT.  A pass: (A) poll the message words of the pairs still waiting (relaxed agent-scope
-// loads of words written by relaxed agent-scope stores, i.e. write-through: the tagged
-// single-store granules of MI355X_MICROARCH.md §visibility; tag = n_iter, so nothing is ever
-// reset); a 1 makes the entry OUT, the last 0 makes it IN, and the thread whose decrement
-// reached 0 covers its variables and lists it in its tile's MIS; (B) every pair of a decided
-// entry forwards its chain state to its successor and finishes.  The run is done when all its
-// pairs have finished; the wait is bounded by DD_TIMEOUT (state.error = 3, the loop stops).
+// blocks: blk = wave, wave + 16, ...) and their state is one LDS word per (block, lane): bits 0-7
+// finished, 8-15 received, 16-23 the received bit, 24-31 has a predecessor.  Entries: one LDS
+// byte per entry slot of the run's tiles: bits 0-3 pairs still waiting for a 0 from their
+// predecessor, bit 4 IN, bit 5 OUT (LDS atomics; every wave sees them at once).
+// After pass 0 every wave runs on its own, without workgroup barriers, until its pairs have
+// finished: per block it loads the open pairs and the message words of those still waiting
+// (one round trip; relaxed agent-scope loads of words written by relaxed agent-scope stores,
+// i.e. write-through: the tagged single-store granules of MI355X_MICROARCH.md §visibility, tag =
+// n_iter, so nothing is ever reset); a 1 makes the entry OUT, the last 0 makes it IN (the lane
+// whose decrement reached 0 covers the clause's variables and lists it in its tile's MIS), and
+// every open pair whose entry is decided forwards its chain state to its successor and
+// finishes.  A wave that found nothing new sleeps briefly.  The wait is bounded by DD_TIMEOUT
+// (state.error = 3; the loop stops).
 constexpr int DDD_PB = 8;
 constexpr uint32_t DDD_BLK = 64 * DDD_PB;
 
@@ -2088,12 +2095,12 @@ __global__ __launch_bounds__(DDD_THREADS) void k_decide(ClauseView cv, LoopBuffe
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dd[];
     const uint32_t slots = nt * TILE;
     uint32_t* entw = s_dd;
-    uint8_t* ent = reinterpret_cast<uint8_t*>(s_dd);
+    volatile uint8_t* ent = reinterpret_cast<volatile uint8_t*>(s_dd);
     uint32_t* pst = s_dd + (size_t)b.run_tiles * TILE / 4;
     const uint32_t nblk = (np + DDD_BLK - 1) / DDD_BLK;
     __shared__ uint32_t s_tc[RUN_TILES_MAX], s_pre[RUN_TILES_MAX + 1], s_join[RUN_TILES_MAX], s_mis0[RUN_TILES_MAX];
     __shared__ unsigned long long s_lits[RUN_TILES_MAX];
-    __shared__ uint32_t s_undone[2], s_stop;
+    __shared__ uint32_t s_passes;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     constexpr int NW = DDD_THREADS / 64;
     for (uint32_t i = threadIdx.x; i < slots / 4; i += DDD_THREADS) entw[i] = 0;
@@ -2102,67 +2109,90 @@ __global__ __launch_bounds__(DDD_THREADS) void k_decide(ClauseView cv, LoopBuffe
         s_lits[threadIdx.x] = 0;
         s_mis0[threadIdx.x] = b.mis_cnt[t0 + threadIdx.x];
     }
-    if (threadIdx.x == 0) { s_undone[0] = 0; s_undone[1] = 0; s_stop = 0; }
+    if (threadIdx.x == 0) s_passes = 0;
+    dbg_stamp(b, 2, 0);
     run_prefix(b, t0, nt, s_tc, s_pre);  // (its barriers publish the zeroing above)
+    dbg_stamp(b, 2, 1);
     const unsigned long long* pr = b.pairs + (uint64_t)r * run_cap;
     const uint32_t* rmsg = b.dd_msg + (uint64_t)r * run_cap;
-    // IN: cover the entry's variables (the resample reads cover), list it in its tile's MIS
-    auto join = [&](uint32_t el) {
-        const uint32_t tt = el / TILE, idx = el % TILE;
-        Ent<K> e;
-        load_ent<K>(e, in + ((uint64_t)(t0 + tt) * TILE + idx) * S);
+    auto cover_and_list = [&](uint32_t tt, const Ent<K>& e) {
 #pragma unroll
         for (int j = 0; j < K; ++j) b.cover[lit_var(e.w[1 + j])] = (uint8_t)stamp;
         b.mis[(uint64_t)(t0 + tt) * TILE + s_mis0[tt] + atomicAdd(&s_join[tt], 1u)] = e.w[0];
         atomicAdd(&s_lits[tt], (unsigned long long)K);
     };
-    auto send = [&](uint32_t sp, uint32_t v) {
-        __hip_atomic_store(b.dd_msg + sp, (tag << 1) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    };
     // pass 0: waiting counts; pairs with nothing to receive and nothing to send finish
     for (uint32_t blk = wave; blk < nblk; blk += NW) {
+        unsigned long long x[DDD_PB];
+#pragma unroll
+        for (int k = 0; k < DDD_PB; ++k) x[k] = pr[min(blk * DDD_BLK + k * 64 + lane, np - 1)];
         uint32_t w = 0;
 #pragma unroll
         for (int k = 0; k < DDD_PB; ++k) {
             const uint32_t i = blk * DDD_BLK + k * 64 + lane;
-            if (i >= np) { w |= 1u << k; continue; }
-            const unsigned long long x = pr[i];
-            const uint32_t lw = (uint32_t)x, el = (lw >> 15) & 0xFFFFu;
-            if (lw & DD_INERT) w |= 1u << k;
+            const uint32_t lw = (uint32_t)x[k], el = (lw >> 15) & 0xFFFFu;
+            if (i >= np || (lw & DD_INERT)) w |= 1u << k;
             else if (lw & DD_PRED) { w |= 1u << (24 + k); atomicAdd(&entw[el >> 2], 1u << (8 * (el & 3))); }
-            else if ((uint32_t)(x >> 32) == DD_NONE) w |= 1u << k;
+            else if ((uint32_t)(x[k] >> 32) == DD_NONE) w |= 1u << k;
         }
         pst[blk * 64 + lane] = w;
     }
     __syncthreads();
-    // entries without a predecessor on any variable: IN
-    for (uint32_t el = threadIdx.x; el < slots; el += DDD_THREADS) {
-        const uint32_t tt = el / TILE;
-        if (el % TILE < s_tc[tt] && ent[el] == 0) {
-            ent[el] = (uint8_t)IN_BIT;
-            join(el);
+    // entries without a predecessor on any variable are IN: four slots (one LDS word) per thread,
+    // their entries loaded together
+    for (uint32_t tt = 0; tt < nt; ++tt) {
+        const uint32_t cnt = s_tc[tt];
+        for (uint32_t i0 = threadIdx.x * 4; i0 < cnt; i0 += DDD_THREADS * 4) {
+            const uint32_t el0 = tt * TILE + i0;
+            const uint32_t word = entw[el0 >> 2];
+            uint32_t cand = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (i0 + q < cnt && ((word >> (8 * q)) & 0xFFu) == 0) cand |= 1u << q;
+            if (!cand) continue;
+            Ent<K> e[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) load_ent<K>(e[q], in + ((uint64_t)(t0 + tt) * TILE + i0 + q) * S);
+            uint32_t nw = word;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if ((cand >> q) & 1u) {
+                    cover_and_list(tt, e[q]);
+                    nw |= IN_BIT << (8 * q);
+                }
+            entw[el0 >> 2] = nw;  // (no other thread touches this word in this phase)
         }
     }
     __syncthreads();
+    dbg_stamp(b, 2, 2);
+    // every wave on its own until its pairs have finished
     const unsigned long long t_begin = wall_now();
-    for (uint32_t pass = 0;; ++pass) {
-        // (A) receive
+    uint32_t iters = 0;
+    bool stop = false;
+    for (;;) {
+        ++iters;
+        bool open_any = false, moved = false;
         for (uint32_t blk = wave; blk < nblk; blk += NW) {
             uint32_t w = pst[blk * 64 + lane];
-            const uint32_t want = (w >> 24) & ~w & ~(w >> 8) & 0xFFu;
-            if (!want) continue;
+            const uint32_t open = ~w & 0xFFu;
+            if (!__builtin_amdgcn_ballot_w64(open != 0)) continue;  // (wave-uniform skip)
+            const uint32_t want = (w >> 24) & open & ~(w >> 8);
+            unsigned long long x[DDD_PB];
             uint32_t m[DDD_PB];
 #pragma unroll
-            for (int k = 0; k < DDD_PB; ++k)
-                m[k] = ((want >> k) & 1u) ? __hip_atomic_load(rmsg + blk * DDD_BLK + k * 64 + lane, __ATOMIC_RELAXED,
-                                                              __HIP_MEMORY_SCOPE_AGENT)
-                                          : 0u;
+            for (int k = 0; k < DDD_PB; ++k) {
+                const uint32_t i = min(blk * DDD_BLK + k * 64 + lane, np - 1);
+                x[k] = pr[i];
+                m[k] = ((want >> k) & 1u) ? __hip_atomic_load(rmsg + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+            }
+            // receive: a 1 makes the entry OUT, the last 0 makes it IN
 #pragma unroll
             for (int k = 0; k < DDD_PB; ++k) {
                 if (!((want >> k) & 1u) || (m[k] >> 1) != tag) continue;
                 const uint32_t v = m[k] & 1u;
                 w |= (1u << (8 + k)) | (v << (16 + k));
-                const uint32_t el = ((uint32_t)pr[blk * DDD_BLK + k * 64 + lane] >> 15) & 0xFFFFu;
+                moved = true;
+                const uint32_t el = ((uint32_t)x[k] >> 15) & 0xFFFFu;
                 const uint32_t sh = 8 * (el & 3);
                 if (v) {
                     atomicOr(&entw[el >> 2], OUT_BIT << sh);
@@ -2170,59 +2200,56 @@ __global__ __launch_bounds__(DDD_THREADS) void k_decide(ClauseView cv, LoopBuffe
                     const uint32_t old = atomicSub(&entw[el >> 2], 1u << sh);
                     if (((old >> sh) & 0xFFu) == 1u) {  // the last wait, no 1 received: IN
                         atomicOr(&entw[el >> 2], IN_BIT << sh);
-                        join(el);
+                        const uint32_t tt = el / TILE;
+                        Ent<K> e;
+                        load_ent<K>(e, in + ((uint64_t)(t0 + tt) * TILE + el % TILE) * S);
+                        cover_and_list(tt, e);
                     }
                 }
+            }
+            // forward the chain state of decided entries
+#pragma unroll
+            for (int k = 0; k < DDD_PB; ++k) {
+                if (!((open >> k) & 1u)) continue;
+                const uint32_t lw = (uint32_t)x[k], sp = (uint32_t)(x[k] >> 32), el = (lw >> 15) & 0xFFFFu;
+                const uint32_t es = ent[el];
+                const bool recv = (w >> (8 + k)) & 1u;
+                uint32_t fin = 0;
+                if (es & IN_BIT) {
+                    if (sp != DD_NONE) __hip_atomic_store(b.dd_msg + sp, (tag << 1) | 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    fin = 1;
+                } else if (es & OUT_BIT) {
+                    if (!(lw & DD_PRED)) {  // (a pair with neither neighbour finished at pass 0)
+                        __hip_atomic_store(b.dd_msg + sp, tag << 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        fin = 1;
+                    } else if (recv) {
+                        if (sp != DD_NONE)
+                            __hip_atomic_store(b.dd_msg + sp, (tag << 1) | ((w >> (16 + k)) & 1u), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                        fin = 1;
+                    }
+                } else if (recv && sp == DD_NONE) {
+                    fin = 1;  // counted; nothing to pass on
+                }
+                w |= fin << k;
+                moved |= fin != 0;
             }
             pst[blk * 64 + lane] = w;
+            open_any |= (~w & 0xFFu) != 0;
         }
-        __syncthreads();
-        // (B) forward the chain state of decided entries
-        uint32_t undone = 0;
-        for (uint32_t blk = wave; blk < nblk; blk += NW) {
-            uint32_t w = pst[blk * 64 + lane];
-            const uint32_t open = ~w & 0xFFu;
-            if (open) {
-#pragma unroll
-                for (int k = 0; k < DDD_PB; ++k) {
-                    if (!((open >> k) & 1u)) continue;
-                    const unsigned long long x = pr[blk * DDD_BLK + k * 64 + lane];
-                    const uint32_t lw = (uint32_t)x, sp = (uint32_t)(x >> 32), el = (lw >> 15) & 0xFFFFu;
-                    const uint32_t es = ent[el];
-                    const bool recv = (w >> (8 + k)) & 1u;
-                    if (es & IN_BIT) {
-                        if (sp != DD_NONE) send(sp, 1u);
-                        w |= 1u << k;
-                    } else if (es & OUT_BIT) {
-                        if (!(lw & DD_PRED)) {
-                            send(sp, 0u);  // (a pair with neither neighbour finished at pass 0)
-                            w |= 1u << k;
-                        } else if (recv) {
-                            if (sp != DD_NONE) send(sp, (w >> (16 + k)) & 1u);
-                            w |= 1u << k;
-                        }
-                    } else if (recv && sp == DD_NONE) {
-                        w |= 1u << k;  // counted; nothing to pass on
-                    }
-                }
-                pst[blk * 64 + lane] = w;
-            }
-            undone += (uint32_t)__popc(~w & 0xFFu);
-        }
-        for (int d = 32; d > 0; d >>= 1) undone += __shfl_down(undone, d, 64);
-        if (lane == 0 && undone) atomicAdd(&s_undone[pass & 1], undone);
-        if (threadIdx.x == 0) {
-            s_undone[(pass + 1) & 1] = 0;
-            if (wall_now() - t_begin > DD_TIMEOUT) s_stop = 1;
-        }
-        __syncthreads();
-        if (s_undone[pass & 1] == 0) break;
-        if (s_stop) {
-            if (threadIdx.x == 0) { st->error = 3; st->done = 3; }
+        if (!__builtin_amdgcn_ballot_w64(open_any)) break;
+        if (lane == 0 && (iters & 15) == 0 && wall_now() - t_begin > DD_TIMEOUT) stop = true;
+        if (__builtin_amdgcn_readfirstlane(stop ? 1u : 0u)) {
+            if (lane == 0) { st->error = 3; st->done = 3; }
             break;
         }
+        if (!__builtin_amdgcn_ballot_w64(moved)) __builtin_amdgcn_s_sleep(2);
     }
+    if (lane == 0) atomicMax(&s_passes, iters);
     __syncthreads();
+    dbg_stamp(b, 2, 4);
+    if (b.kdbg && threadIdx.x == 0 && blockIdx.x < DBG_BLOCKS)  // (wave iterations, not a stamp)
+        b.kdbg[((uint64_t)2 * DBG_BLOCKS + blockIdx.x) * DBG_FIELDS + 7] = s_passes;
     if (threadIdx.x < nt) {
         const uint32_t tt = threadIdx.x, tile = t0 + tt;
         b.tile_cnt[tile] = 0;

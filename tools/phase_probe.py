@@ -20,7 +20,7 @@ args = ap.parse_args()
 n, m, k, kind, _ = bench.CONFIGS[args.config]
 offs, lits = generate_ksat(1, n, m, k, kind)
 KER, BLK, FLD = 4, 8192, 8
-names = {0: "k_bscatter", 1: "k_bresolve", 2: "k_bjoin"}
+names = {0: "k_bscatter", 1: "k_bresolve | k_bsort", 2: "k_bjoin | k_decide"}
 with Solver(n, offs, lits, seed=1) as s:
     s.run(args.iters)
     buf = np.zeros(KER * BLK * FLD, np.uint64)
@@ -37,7 +37,9 @@ with Solver(n, offs, lits, seed=1) as s:
         t = t[used]
         t0 = t[:, 0].min()
         print(f"{name}: {used.sum()} workgroups, start spread {(t[:, 0].max() - t0) * tick_us:.2f} us")
-        for p in range(FLD):
+        if kr == 2 and (t[:, 7] < 1 << 20).all() and t[:, 7].max() > 0:  # k_decide: field 7 = passes
+            print(f"   passes per workgroup: med {np.median(t[:, 7]):.0f} max {t[:, 7].max()}")
+        for p in range(FLD - (1 if kr == 2 else 0)):
             v = t[:, p]
             ok = v > 0
             if not ok.any():

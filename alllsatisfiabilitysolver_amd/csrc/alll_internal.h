@@ -47,7 +47,7 @@ constexpr unsigned long long PAIR_LOSE = 1ull << 31;
 // k_decide (one persistent workgroup per run, all resident) decides every violated clause by
 // messages along those per-variable chains instead of grid rounds.
 constexpr int DDS_THREADS = 1024;        // k_bsort workgroup
-constexpr int DDS_UNROLL = 8;            // items per thread and sweep (8192 per sweep)
+constexpr int DDS_UNROLL = 12;           // items per thread and sweep (12288 per sweep)
 constexpr uint32_t DDS_SUBW = 2048;      // variables per sort sub-range (LDS counters)
 constexpr uint32_t DDS_CAP = 4096;       // pairs sorted in LDS at once (a variable's claimants must fit)
 constexpr int DDD_THREADS = 1024;        // k_decide workgroup (one per CU)

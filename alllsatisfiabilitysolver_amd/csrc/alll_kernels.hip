@@ -1862,23 +1862,42 @@ constexpr uint32_t DD_PRED = 1u << 31;
 constexpr uint32_t DD_INERT = 1u;
 constexpr uint32_t DD_EL_MASK = 0xFFFFu << 15;
 
+// LDS of k_bsort.  Fast path (one sweep of at most DDS_THREADS * DDS_UNROLL pairs, every variable
+// of a bucket of at most DDS_FAST_W variables at once): 16-bit per-variable counts and prefix, the
+// placed pairs as {clause} + {item index}.  General path (sub-ranges of DDS_SUBW variables, pieces
+// of DDS_CAP pairs, several sweeps): 32-bit counters and {clause | position} entries.  Both carve
+// the same dynamic LDS after the common arrays.
+constexpr uint32_t DDS_FAST_W = 10240;
+
 struct DdSortLds {
-    unsigned long long* sorted;  // DDS_CAP: {clause:32 | pair position:32}
-    uint32_t* cnt;               // DDS_SUBW: per-variable counts, then cursors
-    uint32_t* vst;               // DDS_SUBW + 1: exclusive prefix of the counts
     uint32_t* start;             // n_runs: segment starts of this bucket
     uint32_t* pre;               // n_runs + 1: prefix of the segment lengths
     uint32_t* wsum;              // threads / 64
     uint16_t* seg;               // threads * unroll: item -> run segment of the current sweep
+    uint16_t* cnt16;             // fast: DDS_FAST_W per-variable counts
+    uint16_t* vst16;             // fast: DDS_FAST_W + 1 exclusive prefix
+    uint32_t* cl;                // fast: placed pairs' clauses
+    uint16_t* fi;                // fast: placed pairs' item indices
+    unsigned long long* sorted;  // general: DDS_CAP {clause:32 | pair position:32}
+    uint32_t* cnt;               // general: DDS_SUBW counts, then cursors
+    uint32_t* vst;               // general: DDS_SUBW + 1 exclusive prefix
 };
 
+constexpr size_t dd_align16(size_t x) { return (x + 15) & ~(size_t)15; }
+__host__ __device__ inline size_t dd_sort_common(uint32_t n_runs) {
+    return dd_align16(8ull * (n_runs + 4) + 4ull * (DDS_THREADS / 64) + 2ull * DDS_THREADS * DDS_UNROLL);
+}
+constexpr size_t DD_SORT_FAST = 2 * dd_align16(2ull * (DDS_FAST_W + 8)) + 4ull * DDS_THREADS * DDS_UNROLL +
+                                2ull * DDS_THREADS * DDS_UNROLL;
+constexpr size_t DD_SORT_GENERAL = 8ull * DDS_CAP + 4ull * DDS_SUBW + 4ull * (DDS_SUBW + 4);
+
 size_t dd_sort_lds(const LoopBuffers& b) {
-    return 8ull * DDS_CAP + 4ull * DDS_SUBW + 4ull * (DDS_SUBW + 4) + 4ull * (b.n_runs + 4) +
-           4ull * (b.n_runs + 4) + 4ull * (DDS_THREADS / 64) + 2ull * DDS_THREADS * DDS_UNROLL;
+    return dd_sort_common(b.n_runs) + std::max(DD_SORT_FAST, DD_SORT_GENERAL);
 }
 
 // Exclusive prefix of a[0, n) into o[0, n] (o[n] = total; a == o allowed), whole workgroup.
-__device__ uint32_t block_excl_scan(const uint32_t* a, uint32_t* o, uint32_t n, uint32_t* wsum) {
+template <typename TA>
+__device__ uint32_t block_excl_scan(const TA* a, TA* o, uint32_t n, uint32_t* wsum) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t per = (n + blockDim.x - 1) / blockDim.x;
     const uint32_t q0 = min(n, threadIdx.x * per), q1 = min(n, q0 + per);
@@ -1898,41 +1917,34 @@ __device__ uint32_t block_excl_scan(const uint32_t* a, uint32_t* o, uint32_t n, 
     }
     for (uint32_t q = q0; q < q1; ++q) {
         const uint32_t c = a[q];
-        o[q] = run;
+        o[q] = (TA)run;
         run += c;
     }
-    if (threadIdx.x == 0) o[n] = total;
+    if (threadIdx.x == 0) o[n] = (TA)total;
     __syncthreads();
     return total;
 }
 
+// 16-bit LDS counter i (two per word; counts stay below 2^16): returns its old value
+__device__ __forceinline__ uint32_t lds_inc16(uint16_t* a, uint32_t i) {
+    uint32_t* w = reinterpret_cast<uint32_t*>(a) + (i >> 1);
+    const uint32_t sh = 16 * (i & 1);
+    return (atomicAdd(w, 1u << sh) >> sh) & 0xFFFFu;
+}
+
+// General path of k_bsort (a bucket wider than DDS_FAST_W variables, or more pairs than one
+// sweep): variables DDS_SUBW at a time, pieces of DDS_CAP pairs, items reloaded per sweep.  Not
+// inlined, so that the fast path keeps its registers.
 template <int U, int T>
-__global__ __launch_bounds__(T) void k_bsort(LoopBuffers b, uint32_t run_cap, int fused_reduce) {
-    extern __shared__ __attribute__((aligned(16))) unsigned long long s_dds[];
-    DdSortLds L;
-    {
-        char* p = reinterpret_cast<char*>(s_dds);
-        L.sorted = reinterpret_cast<unsigned long long*>(p); p += 8ull * DDS_CAP;
-        L.cnt = reinterpret_cast<uint32_t*>(p); p += 4ull * DDS_SUBW;
-        L.vst = reinterpret_cast<uint32_t*>(p); p += 4ull * (DDS_SUBW + 4);
-        L.start = reinterpret_cast<uint32_t*>(p); p += 4ull * (b.n_runs + 4);
-        L.pre = reinterpret_cast<uint32_t*>(p); p += 4ull * (b.n_runs + 4);
-        L.wsum = reinterpret_cast<uint32_t*>(p); p += 4ull * (T / 64);
-        L.seg = reinterpret_cast<uint16_t*>(p);
-    }
+__device__ __noinline__ void bsort_general(const LoopBuffers& b, const DdSortLds& L, uint32_t run_cap, uint32_t np) {
     const ResolveLds R{nullptr, L.start, L.pre, L.wsum};
-    const uint32_t nr = b.n_runs;  // <= BKT_RUN_BATCH (checked at create)
-    dbg_stamp(b, 1, 0);
-    const uint32_t np = resolve_batch(b, R, 0, nr);
-    dbg_stamp(b, 1, 1);
+    const uint32_t nr = b.n_runs;
     const uint32_t width = b.bkt_width;
     const uint32_t stride = T * U;
-    const bool single = np <= stride;
     const uint32_t first = (threadIdx.x >> 6) * 64 * U + (threadIdx.x & 63);
     unsigned long long x[U];
-    uint32_t pos[U], rk[U];
+    uint32_t pos[U];
     bool ok[U];
-    // items [s0, s0 + stride) of the bucket's flat index space: positions and pairs
     auto load_sweep = [&](uint32_t s0) {
         resolve_seg_table(R, nr, np, s0, stride, L.seg);
         __syncthreads();
@@ -1947,38 +1959,24 @@ __global__ __launch_bounds__(T) void k_bsort(LoopBuffers b, uint32_t run_cap, in
 #pragma unroll
         for (int u = 0; u < U; ++u) x[u] = b.pairs[pos[u]];
     };
-    if (single && np) load_sweep(0);
-    dbg_stamp(b, 1, 2);
-    for (uint32_t v0 = 0; np && v0 < width; v0 += DDS_SUBW) {
+    auto voff = [&](int u) { return (uint32_t)x[u] & 0x7FFFu; };
+    for (uint32_t v0 = 0; v0 < width; v0 += DDS_SUBW) {
         const uint32_t sw = min(DDS_SUBW, width - v0);
         for (uint32_t i = threadIdx.x; i < sw; i += T) L.cnt[i] = 0;
         __syncthreads();
-        // per-variable counts; with one sweep the atomics' results are each pair's rank in its
-        // variable, so the placement needs no cursors
-        if (single) {
+        for (uint32_t s0 = 0; s0 < np; s0 += stride) {
+            load_sweep(s0);
 #pragma unroll
             for (int u = 0; u < U; ++u) {
-                const uint32_t v = ((uint32_t)x[u] & 0x7FFFu) - v0;
-                if (ok[u] && v < sw) rk[u] = atomicAdd(&L.cnt[v], 1u);
+                const uint32_t v = voff(u) - v0;
+                if (ok[u] && v < sw) atomicAdd(&L.cnt[v], 1u);
             }
-        } else {
-            for (uint32_t s0 = 0; s0 < np; s0 += stride) {
-                load_sweep(s0);
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const uint32_t v = ((uint32_t)x[u] & 0x7FFFu) - v0;
-                    if (ok[u] && v < sw) atomicAdd(&L.cnt[v], 1u);
-                }
-                __syncthreads();  // (the segment table is rewritten by the next sweep)
-            }
+            __syncthreads();  // (the segment table is rewritten by the next sweep)
         }
-        __syncthreads();
-        const uint32_t tot = block_excl_scan(L.cnt, L.vst, sw, L.wsum);
+        const uint32_t tot = block_excl_scan<uint32_t>(L.cnt, L.vst, sw, L.wsum);
         if (tot == 0) continue;  // (uniform)
-        if (!single) {
-            for (uint32_t i = threadIdx.x; i < sw; i += T) L.cnt[i] = 0;
-            __syncthreads();
-        }
+        for (uint32_t i = threadIdx.x; i < sw; i += T) L.cnt[i] = 0;
+        __syncthreads();
         for (uint32_t a = 0; a < sw;) {
             // piece [a, e): the largest e whose pairs fit DDS_CAP (at least one variable)
             uint32_t lo = a + 1, hi = sw;
@@ -1988,60 +1986,155 @@ __global__ __launch_bounds__(T) void k_bsort(LoopBuffers b, uint32_t run_cap, in
             }
             const uint32_t e = lo, base = L.vst[a];
             if (L.vst[e] - base > DDS_CAP && threadIdx.x == 0) b.state->error = 2;  // (host-prevented)
-            auto in_piece = [&](int u) {
-                const uint32_t v = ((uint32_t)x[u] & 0x7FFFu) - v0;
-                return ok[u] && v >= a && v < e;
-            };
-            auto place = [&](int u, uint32_t r) {
-                const uint32_t v = ((uint32_t)x[u] & 0x7FFFu) - v0;
-                const uint32_t slot = L.vst[v] - base + r;
-                if (slot < DDS_CAP) L.sorted[slot] = (x[u] & 0xFFFFFFFF00000000ull) | pos[u];
-            };
-            auto link = [&](int u) {
-                const uint32_t c = (uint32_t)(x[u] >> 32);
-                const uint32_t v = ((uint32_t)x[u] & 0x7FFFu) - v0;
-                const uint32_t sa = L.vst[v] - base, se = min(L.vst[v + 1] - base, DDS_CAP);
-                bool rep = true, pred = false;
-                uint32_t sc = ~0u, sp = DD_NONE;
-                for (uint32_t j = sa; j < se; ++j) {
-                    const unsigned long long y = L.sorted[j];
-                    const uint32_t yc = (uint32_t)(y >> 32), yp = (uint32_t)y;
-                    if (yc < c) pred = true;
-                    else if (yc == c) rep = rep && !(yp < pos[u]);
-                    else if (yc < sc || (yc == sc && yp < sp)) { sc = yc; sp = yp; }
-                }
-                uint32_t lw = (uint32_t)x[u] & DD_EL_MASK;
-                if (!rep) { lw |= DD_INERT; sp = DD_NONE; }
-                else if (pred) lw |= DD_PRED;
-                b.pairs[pos[u]] = ((unsigned long long)sp << 32) | lw;
-            };
-            if (single) {
+            for (uint32_t s0 = 0; s0 < np; s0 += stride) {
+                load_sweep(s0);
 #pragma unroll
-                for (int u = 0; u < U; ++u)
-                    if (in_piece(u)) place(u, rk[u]);
+                for (int u = 0; u < U; ++u) {
+                    const uint32_t v = voff(u) - v0;
+                    if (!ok[u] || v < a || v >= e) continue;
+                    const uint32_t slot = L.vst[v] - base + atomicAdd(&L.cnt[v], 1u);
+                    if (slot < DDS_CAP) L.sorted[slot] = (x[u] & 0xFFFFFFFF00000000ull) | pos[u];
+                }
                 __syncthreads();
+            }
+            for (uint32_t s0 = 0; s0 < np; s0 += stride) {
+                load_sweep(s0);
 #pragma unroll
-                for (int u = 0; u < U; ++u)
-                    if (in_piece(u)) link(u);
-            } else {
-                for (uint32_t s0 = 0; s0 < np; s0 += stride) {
-                    load_sweep(s0);
-#pragma unroll
-                    for (int u = 0; u < U; ++u)
-                        if (in_piece(u)) place(u, atomicAdd(&L.cnt[((uint32_t)x[u] & 0x7FFFu) - v0], 1u));
-                    __syncthreads();
+                for (int u = 0; u < U; ++u) {
+                    const uint32_t v = voff(u) - v0;
+                    if (!ok[u] || v < a || v >= e) continue;
+                    const uint32_t c = (uint32_t)(x[u] >> 32);
+                    const uint32_t sa = L.vst[v] - base, se = min(L.vst[v + 1] - base, DDS_CAP);
+                    bool rep = true, pred = false;
+                    uint32_t sc = ~0u, sp = DD_NONE;
+                    for (uint32_t j = sa; j < se; ++j) {
+                        const unsigned long long y = L.sorted[j];
+                        const uint32_t yc = (uint32_t)(y >> 32), yp = (uint32_t)y;
+                        if (yc < c) pred = true;
+                        else if (yc == c) rep = rep && !(yp < pos[u]);
+                        else if (yc < sc || (yc == sc && yp < sp)) { sc = yc; sp = yp; }
+                    }
+                    uint32_t lw = (uint32_t)x[u] & DD_EL_MASK;
+                    if (!rep) { lw |= DD_INERT; sp = DD_NONE; }
+                    else if (pred) lw |= DD_PRED;
+                    b.pairs[pos[u]] = ((unsigned long long)sp << 32) | lw;
                 }
-                for (uint32_t s0 = 0; s0 < np; s0 += stride) {
-                    load_sweep(s0);
-#pragma unroll
-                    for (int u = 0; u < U; ++u)
-                        if (in_piece(u)) link(u);
-                    __syncthreads();
-                }
+                __syncthreads();
             }
             __syncthreads();  // (the sorted array is rewritten by the next piece)
             a = e;
         }
+    }
+}
+
+template <int U, int T>
+__global__ __launch_bounds__(T) void k_bsort(LoopBuffers b, uint32_t run_cap, int fused_reduce) {
+    extern __shared__ __attribute__((aligned(16))) unsigned long long s_dds[];
+    DdSortLds L;
+    {
+        char* p = reinterpret_cast<char*>(s_dds);
+        L.start = reinterpret_cast<uint32_t*>(p); p += 4ull * (b.n_runs + 4);
+        L.pre = reinterpret_cast<uint32_t*>(p); p += 4ull * (b.n_runs + 4);
+        L.wsum = reinterpret_cast<uint32_t*>(p); p += 4ull * (T / 64);
+        L.seg = reinterpret_cast<uint16_t*>(p);
+        p = reinterpret_cast<char*>(s_dds) + dd_sort_common(b.n_runs);
+        char* u = p;  // union of the two paths
+        L.cnt16 = reinterpret_cast<uint16_t*>(u); u += dd_align16(2ull * (DDS_FAST_W + 8));
+        L.vst16 = reinterpret_cast<uint16_t*>(u); u += dd_align16(2ull * (DDS_FAST_W + 8));
+        L.cl = reinterpret_cast<uint32_t*>(u); u += 4ull * T * U;
+        L.fi = reinterpret_cast<uint16_t*>(u);
+        L.sorted = reinterpret_cast<unsigned long long*>(p); p += 8ull * DDS_CAP;
+        L.cnt = reinterpret_cast<uint32_t*>(p); p += 4ull * DDS_SUBW;
+        L.vst = reinterpret_cast<uint32_t*>(p);
+    }
+    const ResolveLds R{nullptr, L.start, L.pre, L.wsum};
+    const uint32_t nr = b.n_runs;  // <= BKT_RUN_BATCH (checked at create)
+    dbg_stamp(b, 1, 0);
+    const uint32_t np = resolve_batch(b, R, 0, nr);
+    dbg_stamp(b, 1, 1);
+    const uint32_t width = b.bkt_width;
+    const uint32_t stride = T * U;
+    const bool single = np <= stride;
+    const uint32_t first = (threadIdx.x >> 6) * 64 * U + (threadIdx.x & 63);
+    unsigned long long x[U];
+    uint32_t pos[U], rk[U];
+    bool ok[U];
+    auto pos_of = [&](uint32_t f, uint32_t s0) {
+        const uint32_t q = L.seg[f - s0];
+        return q * run_cap + L.start[q] + (f - L.pre[q]);
+    };
+    // items [s0, s0 + stride) of the bucket's flat index space: positions and pairs
+    auto load_sweep = [&](uint32_t s0) {
+        resolve_seg_table(R, nr, np, s0, stride, L.seg);
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t f = s0 + first + 64 * u;
+            ok[u] = f < np;
+            pos[u] = pos_of(min(f, np - 1), s0);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u] = b.pairs[pos[u]];
+    };
+    auto voff = [&](int u) { return (uint32_t)x[u] & 0x7FFFu; };
+    const bool fast = np && single && width <= DDS_FAST_W;
+    if (fast) load_sweep(0);
+    dbg_stamp(b, 1, 2);
+    if (fast) {
+        // ---- fast path: count, prefix, place, link; every variable of the bucket at once
+        uint32_t* c32 = reinterpret_cast<uint32_t*>(L.cnt16);
+        for (uint32_t i = threadIdx.x; i < (width + 1) / 2; i += T) c32[i] = 0;
+        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (ok[u]) rk[u] = lds_inc16(L.cnt16, voff(u));
+        __syncthreads();
+        dbg_stamp(b, 1, 4);
+        block_excl_scan<uint16_t>(L.cnt16, L.vst16, width, L.wsum);
+        dbg_stamp(b, 1, 5);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!ok[u]) continue;
+            const uint32_t slot = L.vst16[voff(u)] + rk[u];
+            L.cl[slot] = (uint32_t)(x[u] >> 32);
+            L.fi[slot] = (uint16_t)(first + 64 * u);
+        }
+        __syncthreads();
+        dbg_stamp(b, 1, 6);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!ok[u]) continue;
+            const uint32_t c = (uint32_t)(x[u] >> 32), f = first + 64 * u;
+            const uint32_t sa = L.vst16[voff(u)], se = L.vst16[voff(u) + 1];
+            bool rep = true, pred = false;
+            uint32_t sc = ~0u, sf = ~0u;
+            for (uint32_t j0 = sa; j0 < se; j0 += 4) {  // (segments are short: 4 reads in flight)
+                uint32_t yc[4], yf[4];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t j = min(j0 + q, se - 1);
+                    yc[q] = L.cl[j];
+                    yf[q] = L.fi[j];
+                }
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    if (j0 + q >= se) continue;
+                    if (yc[q] < c) pred = true;
+                    else if (yc[q] == c) rep = rep && !(yf[q] < f);
+                    else if (yc[q] < sc || (yc[q] == sc && yf[q] < sf)) { sc = yc[q]; sf = yf[q]; }
+                }
+            }
+            uint32_t lw = (uint32_t)x[u] & DD_EL_MASK, sp = DD_NONE;
+            if (!rep) lw |= DD_INERT;
+            else {
+                if (pred) lw |= DD_PRED;
+                if (sf != ~0u) sp = pos_of(sf, 0);
+            }
+            b.pairs[pos[u]] = ((unsigned long long)sp << 32) | lw;
+        }
+        dbg_stamp(b, 1, 7);
+    } else if (np) {
+        bsort_general<U, T>(b, L, run_cap, np);
     }
     dbg_stamp(b, 1, 3);
     if (fused_reduce && blockIdx.x == 0) {  // the loop's reduce (one GPU), as in k_bresolve
@@ -2056,21 +2149,22 @@ __global__ __launch_bounds__(T) void k_bsort(LoopBuffers b, uint32_t run_cap, in
 
 // k_decide (one persistent workgroup per run, all runs resident: n_runs <= CUs): the run's pairs
 // are read in blocks of DDD_BLK (lane l of a wave holds pairs 64 k + l, k < DDD_PB, of its
-// blocks: blk = wave, wave + 16, ...) and their state is one LDS word per (block, lane): bits 0-7
-// finished, 8-15 received, 16-23 the received bit, 24-31 has a predecessor.  Entries: one LDS
-// byte per entry slot of the run's tiles: bits 0-3 pairs still waiting for a 0 from their
-// predecessor, bit 4 IN, bit 5 OUT (LDS atomics; every wave sees them at once).
+// blocks: blk = wave, wave + 16, ...; the first DDD_CACHED blocks stay in registers) and their
+// state is one LDS word per (block, lane): bits 0-7 finished, 8-15 received, 16-23 the received
+// bit, 24-31 has a predecessor.  Entries: one LDS byte per entry slot of the run's tiles: bits
+// 0-3 pairs still waiting for a 0 from their predecessor, bit 4 IN, bit 5 OUT (LDS atomics;
+// every wave sees them at once).
 // After pass 0 every wave runs on its own, without workgroup barriers, until its pairs have
-// finished: per block it loads the open pairs and the message words of those still waiting
-// (one round trip; relaxed agent-scope loads of words written by relaxed agent-scope stores,
-// i.e. write-through: the tagged single-store granules of MI355X_MICROARCH.md §visibility, tag =
-// n_iter, so nothing is ever reset); a 1 makes the entry OUT, the last 0 makes it IN (the lane
-// whose decrement reached 0 covers the clause's variables and lists it in its tile's MIS), and
-// every open pair whose entry is decided forwards its chain state to its successor and
-// finishes.  A wave that found nothing new sleeps briefly.  The wait is bounded by DD_TIMEOUT
-// (state.error = 3; the loop stops).
+// finished: per block it loads the message words of the pairs still waiting (relaxed agent-scope
+// loads of words written by relaxed agent-scope stores, i.e. write-through: the tagged
+// single-store granules of MI355X_MICROARCH.md §visibility; tag = n_iter, so nothing is ever
+// reset); a 1 makes the entry OUT, the last 0 makes it IN, and every open pair whose entry is
+// decided forwards its chain state to its successor and finishes.  A wave that found nothing new
+// sleeps briefly.  IN entries are covered and listed once every wave is done (their entries
+// loaded four at a time).  The wait is bounded by DD_TIMEOUT (state.error = 3; the loop stops).
 constexpr int DDD_PB = 8;
 constexpr uint32_t DDD_BLK = 64 * DDD_PB;
+constexpr int DDD_CACHED = 1;
 
 size_t dd_decide_lds(const LoopBuffers& b, uint32_t k) {
     const size_t slots = (size_t)b.run_tiles * TILE;
@@ -2111,21 +2205,32 @@ __global__ __launch_bounds__(DDD_THREADS) void k_decide(ClauseView cv, LoopBuffe
     }
     if (threadIdx.x == 0) s_passes = 0;
     dbg_stamp(b, 2, 0);
-    run_prefix(b, t0, nt, s_tc, s_pre);  // (its barriers publish the zeroing above)
+    const uint32_t E = run_prefix(b, t0, nt, s_tc, s_pre);  // (its barriers publish the zeroing above)
     dbg_stamp(b, 2, 1);
     const unsigned long long* pr = b.pairs + (uint64_t)r * run_cap;
     const uint32_t* rmsg = b.dd_msg + (uint64_t)r * run_cap;
-    auto cover_and_list = [&](uint32_t tt, const Ent<K>& e) {
-#pragma unroll
-        for (int j = 0; j < K; ++j) b.cover[lit_var(e.w[1 + j])] = (uint8_t)stamp;
-        b.mis[(uint64_t)(t0 + tt) * TILE + s_mis0[tt] + atomicAdd(&s_join[tt], 1u)] = e.w[0];
-        atomicAdd(&s_lits[tt], (unsigned long long)K);
-    };
-    // pass 0: waiting counts; pairs with nothing to receive and nothing to send finish
-    for (uint32_t blk = wave; blk < nblk; blk += NW) {
-        unsigned long long x[DDD_PB];
+    // the pairs of a block, DDD_PB loads in flight together (clamped to the run's last pair)
+    auto load_blk = [&](uint32_t blk, unsigned long long (&x)[DDD_PB]) {
 #pragma unroll
         for (int k = 0; k < DDD_PB; ++k) x[k] = pr[min(blk * DDD_BLK + k * 64 + lane, np - 1)];
+    };
+    unsigned long long xc[DDD_CACHED][DDD_PB];
+#pragma unroll
+    for (int c = 0; c < DDD_CACHED; ++c)
+        if (wave + c * NW < nblk) load_blk(wave + c * NW, xc[c]);
+    // fn(blk, pairs) over this wave's blocks: the first DDD_CACHED from registers, the rest reloaded
+    auto for_blocks = [&](auto&& fn) {
+#pragma unroll
+        for (int c = 0; c < DDD_CACHED; ++c)
+            if (wave + c * NW < nblk) fn(wave + c * NW, xc[c]);
+        for (uint32_t blk = wave + DDD_CACHED * NW; blk < nblk; blk += NW) {
+            unsigned long long x[DDD_PB];
+            load_blk(blk, x);
+            fn(blk, x);
+        }
+    };
+    // pass 0: waiting counts; pairs with nothing to receive and nothing to send finish
+    for_blocks([&](uint32_t blk, unsigned long long (&x)[DDD_PB]) {
         uint32_t w = 0;
 #pragma unroll
         for (int k = 0; k < DDD_PB; ++k) {
@@ -2136,32 +2241,13 @@ __global__ __launch_bounds__(DDD_THREADS) void k_decide(ClauseView cv, LoopBuffe
             else if ((uint32_t)(x[k] >> 32) == DD_NONE) w |= 1u << k;
         }
         pst[blk * 64 + lane] = w;
-    }
+    });
     __syncthreads();
-    // entries without a predecessor on any variable are IN: four slots (one LDS word) per thread,
-    // their entries loaded together
-    for (uint32_t tt = 0; tt < nt; ++tt) {
-        const uint32_t cnt = s_tc[tt];
-        for (uint32_t i0 = threadIdx.x * 4; i0 < cnt; i0 += DDD_THREADS * 4) {
-            const uint32_t el0 = tt * TILE + i0;
-            const uint32_t word = entw[el0 >> 2];
-            uint32_t cand = 0;
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                if (i0 + q < cnt && ((word >> (8 * q)) & 0xFFu) == 0) cand |= 1u << q;
-            if (!cand) continue;
-            Ent<K> e[4];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) load_ent<K>(e[q], in + ((uint64_t)(t0 + tt) * TILE + i0 + q) * S);
-            uint32_t nw = word;
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                if ((cand >> q) & 1u) {
-                    cover_and_list(tt, e[q]);
-                    nw |= IN_BIT << (8 * q);
-                }
-            entw[el0 >> 2] = nw;  // (no other thread touches this word in this phase)
-        }
+    // entries without a predecessor on any variable are IN (flat over the run's entries)
+    for (uint32_t f = threadIdx.x; f < E; f += DDD_THREADS) {
+        const uint32_t tt = run_tile_of(s_pre, nt, f);
+        const uint32_t el = tt * TILE + (f - s_pre[tt]);
+        if (ent[el] == 0) ent[el] = (uint8_t)IN_BIT;  // (no atomics on entries in this phase)
     }
     __syncthreads();
     dbg_stamp(b, 2, 2);
@@ -2172,19 +2258,17 @@ __global__ __launch_bounds__(DDD_THREADS) void k_decide(ClauseView cv, LoopBuffe
     for (;;) {
         ++iters;
         bool open_any = false, moved = false;
-        for (uint32_t blk = wave; blk < nblk; blk += NW) {
+        for_blocks([&](uint32_t blk, unsigned long long (&x)[DDD_PB]) {
             uint32_t w = pst[blk * 64 + lane];
             const uint32_t open = ~w & 0xFFu;
-            if (!__builtin_amdgcn_ballot_w64(open != 0)) continue;  // (wave-uniform skip)
+            if (!__builtin_amdgcn_ballot_w64(open != 0)) return;  // (wave-uniform skip)
             const uint32_t want = (w >> 24) & open & ~(w >> 8);
-            unsigned long long x[DDD_PB];
             uint32_t m[DDD_PB];
 #pragma unroll
-            for (int k = 0; k < DDD_PB; ++k) {
-                const uint32_t i = min(blk * DDD_BLK + k * 64 + lane, np - 1);
-                x[k] = pr[i];
-                m[k] = ((want >> k) & 1u) ? __hip_atomic_load(rmsg + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-            }
+            for (int k = 0; k < DDD_PB; ++k)
+                m[k] = ((want >> k) & 1u) ? __hip_atomic_load(rmsg + blk * DDD_BLK + k * 64 + lane, __ATOMIC_RELAXED,
+                                                              __HIP_MEMORY_SCOPE_AGENT)
+                                          : 0u;
             // receive: a 1 makes the entry OUT, the last 0 makes it IN
 #pragma unroll
             for (int k = 0; k < DDD_PB; ++k) {
@@ -2198,13 +2282,7 @@ __global__ __launch_bounds__(DDD_THREADS) void k_decide(ClauseView cv, LoopBuffe
                     atomicOr(&entw[el >> 2], OUT_BIT << sh);
                 } else {
                     const uint32_t old = atomicSub(&entw[el >> 2], 1u << sh);
-                    if (((old >> sh) & 0xFFu) == 1u) {  // the last wait, no 1 received: IN
-                        atomicOr(&entw[el >> 2], IN_BIT << sh);
-                        const uint32_t tt = el / TILE;
-                        Ent<K> e;
-                        load_ent<K>(e, in + ((uint64_t)(t0 + tt) * TILE + el % TILE) * S);
-                        cover_and_list(tt, e);
-                    }
+                    if (((old >> sh) & 0xFFu) == 1u) atomicOr(&entw[el >> 2], IN_BIT << sh);  // the last wait: IN
                 }
             }
             // forward the chain state of decided entries
@@ -2214,29 +2292,29 @@ __global__ __launch_bounds__(DDD_THREADS) void k_decide(ClauseView cv, LoopBuffe
                 const uint32_t lw = (uint32_t)x[k], sp = (uint32_t)(x[k] >> 32), el = (lw >> 15) & 0xFFFFu;
                 const uint32_t es = ent[el];
                 const bool recv = (w >> (8 + k)) & 1u;
-                uint32_t fin = 0;
+                uint32_t fin = 0, val = 2;  // val: the bit to send (2: nothing)
                 if (es & IN_BIT) {
-                    if (sp != DD_NONE) __hip_atomic_store(b.dd_msg + sp, (tag << 1) | 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     fin = 1;
+                    val = 1;
                 } else if (es & OUT_BIT) {
                     if (!(lw & DD_PRED)) {  // (a pair with neither neighbour finished at pass 0)
-                        __hip_atomic_store(b.dd_msg + sp, tag << 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         fin = 1;
+                        val = 0;
                     } else if (recv) {
-                        if (sp != DD_NONE)
-                            __hip_atomic_store(b.dd_msg + sp, (tag << 1) | ((w >> (16 + k)) & 1u), __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
                         fin = 1;
+                        val = (w >> (16 + k)) & 1u;
                     }
                 } else if (recv && sp == DD_NONE) {
                     fin = 1;  // counted; nothing to pass on
                 }
+                if (val != 2 && sp != DD_NONE)
+                    __hip_atomic_store(b.dd_msg + sp, (tag << 1) | val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 w |= fin << k;
                 moved |= fin != 0;
             }
             pst[blk * 64 + lane] = w;
             open_any |= (~w & 0xFFu) != 0;
-        }
+        });
         if (!__builtin_amdgcn_ballot_w64(open_any)) break;
         if (lane == 0 && (iters & 15) == 0 && wall_now() - t_begin > DD_TIMEOUT) stop = true;
         if (__builtin_amdgcn_readfirstlane(stop ? 1u : 0u)) {
@@ -2246,6 +2324,34 @@ __global__ __launch_bounds__(DDD_THREADS) void k_decide(ClauseView cv, LoopBuffe
         if (!__builtin_amdgcn_ballot_w64(moved)) __builtin_amdgcn_s_sleep(2);
     }
     if (lane == 0) atomicMax(&s_passes, iters);
+    __syncthreads();
+    dbg_stamp(b, 2, 3);
+    // IN entries: cover their variables (the resample reads cover) and list them in their tile's
+    // MIS; four entries per thread, loaded together
+    for (uint32_t f0 = threadIdx.x * 4; f0 < E; f0 += DDD_THREADS * 4) {
+        uint32_t el[4];
+        bool is_in[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint32_t f = min(f0 + q, E - 1);
+            const uint32_t tt = run_tile_of(s_pre, nt, f);
+            el[q] = tt * TILE + (f - s_pre[tt]);
+            is_in[q] = f0 + q < E && (ent[el[q]] & IN_BIT);
+        }
+        if (!(is_in[0] || is_in[1] || is_in[2] || is_in[3])) continue;
+        Ent<K> e[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) load_ent<K>(e[q], in + ((uint64_t)t0 * TILE + el[q]) * S);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (!is_in[q]) continue;
+            const uint32_t tt = el[q] / TILE;
+#pragma unroll
+            for (int j = 0; j < K; ++j) b.cover[lit_var(e[q].w[1 + j])] = (uint8_t)stamp;
+            b.mis[(uint64_t)(t0 + tt) * TILE + s_mis0[tt] + atomicAdd(&s_join[tt], 1u)] = e[q].w[0];
+            atomicAdd(&s_lits[tt], (unsigned long long)K);
+        }
+    }
     __syncthreads();
     dbg_stamp(b, 2, 4);
     if (b.kdbg && threadIdx.x == 0 && blockIdx.x < DBG_BLOCKS)  // (wave iterations, not a stamp)

@@ -766,15 +766,14 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     if (fixed_k > 0 && !(opt.flags & ALLL_FLAG_ATOMIC_CLAIMS) && n_tiles > 0 && c->n_vars > 0) {
         uint32_t shift = BKT_SHIFT_MIN;
         while (shift < BKT_SHIFT_MAX && (vrange >> shift) > 384) ++shift;
-        // (the dependency-driven LFMIS sorts a bucket's pairs in one 8192-item sweep when it
-        // can: two buckets per CU by default, ALLL_DD_BKT_PER_CU to tune)
+        // (one bucket per CU: the dependency-driven LFMIS sorts a bucket's pairs in one sweep of
+        // 12288 when its width is at most 10240 variables; ALLL_DD_BKT_PER_CU to tune)
         uint32_t per_cu = 1;
         {
             bool zid = true;
             for (int i = 0; i < 128; ++i) zid &= opt.comm_id[i] == 0;
             const char* e = getenv("ALLL_DD");
             if (c->world == 1 && zid && !n_hot && !opt.stream_batch && !rr_T && !(e && atoi(e) == 0)) {
-                per_cu = 2;
                 if (const char* e2 = getenv("ALLL_DD_BKT_PER_CU")) per_cu = (uint32_t)std::max(1, atoi(e2));
             }
         }

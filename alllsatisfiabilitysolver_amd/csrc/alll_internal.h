@@ -47,7 +47,8 @@ constexpr unsigned long long PAIR_LOSE = 1ull << 31;
 // k_decide (one persistent workgroup per run, all resident) decides every violated clause by
 // messages along those per-variable chains instead of grid rounds.
 constexpr int DDS_THREADS = 1024;        // k_bsort workgroup
-constexpr int DDS_UNROLL = 12;           // items per thread and sweep (12288 per sweep)
+constexpr int DDS_UNROLL = 12;           // items per thread and sweep of k_bsort (12288 per sweep)
+constexpr int DDS_UNROLL_GEN = 8;        // items per thread and sweep of k_bsort_general
 constexpr uint32_t DDS_SUBW = 2048;      // variables per sort sub-range (LDS counters)
 constexpr uint32_t DDS_CAP = 4096;       // pairs sorted in LDS at once (a variable's claimants must fit)
 constexpr int DDD_THREADS = 1024;        // k_decide workgroup (one per CU)
@@ -201,6 +202,7 @@ hipError_t launch_lfmis_dd(const ClauseView& cv, const LoopBuffers& b, bool scat
                            hipStream_t s);
 // LDS bytes of k_bsort / k_decide for these buffers (the host checks them against the CU's LDS)
 size_t dd_sort_lds(const LoopBuffers& b);
+size_t dd_sort_general_lds(const LoopBuffers& b);
 size_t dd_decide_lds(const LoopBuffers& b, uint32_t k);
 hipError_t launch_tail(const ClauseView& cv, const LoopBuffers& b, uint32_t first_round,
                        hipStream_t s);

@@ -1862,37 +1862,57 @@ constexpr uint32_t DD_PRED = 1u << 31;
 constexpr uint32_t DD_INERT = 1u;
 constexpr uint32_t DD_EL_MASK = 0xFFFFu << 15;
 
-// LDS of k_bsort.  Fast path (one sweep of at most DDS_THREADS * DDS_UNROLL pairs, every variable
-// of a bucket of at most DDS_FAST_W variables at once): 16-bit per-variable counts and prefix, the
-// placed pairs as {clause} + {item index}.  General path (sub-ranges of DDS_SUBW variables, pieces
-// of DDS_CAP pairs, several sweeps): 32-bit counters and {clause | position} entries.  Both carve
-// the same dynamic LDS after the common arrays.
+// k_bsort (fast kernel): one sweep of at most DDS_THREADS * DDS_UNROLL pairs and a bucket of at
+// most DDS_FAST_W variables: 16-bit per-variable counts turned into their prefix in place, the
+// placed pairs as {clause} + {item index}, and one 16-bit result per item.  Other buckets (more
+// pairs than one sweep: the first iterations of large instances) are left to k_bsort_general
+// (sub-ranges of DDS_SUBW variables, pieces of DDS_CAP pairs, several sweeps).
 constexpr uint32_t DDS_FAST_W = 10240;
+constexpr uint32_t DDS_RES_NONE = 0x3FFFu, DDS_RES_PRED = 1u << 14, DDS_RES_INERT = 1u << 15;
+static_assert(DDS_THREADS * DDS_UNROLL < DDS_RES_NONE, "item indices fit the 14-bit successor field");
 
 struct DdSortLds {
     uint32_t* start;             // n_runs: segment starts of this bucket
     uint32_t* pre;               // n_runs + 1: prefix of the segment lengths
     uint32_t* wsum;              // threads / 64
     uint16_t* seg;               // threads * unroll: item -> run segment of the current sweep
-    uint16_t* cnt16;             // fast: DDS_FAST_W per-variable counts
-    uint16_t* vst16;             // fast: DDS_FAST_W + 1 exclusive prefix
+    uint16_t* vst16;             // fast: DDS_FAST_W + 1 per-variable counts -> exclusive prefix
     uint32_t* cl;                // fast: placed pairs' clauses
     uint16_t* fi;                // fast: placed pairs' item indices
+    uint16_t* res;               // fast: per item {successor item:14 | has predecessor:1 | inert:1}
     unsigned long long* sorted;  // general: DDS_CAP {clause:32 | pair position:32}
     uint32_t* cnt;               // general: DDS_SUBW counts, then cursors
     uint32_t* vst;               // general: DDS_SUBW + 1 exclusive prefix
 };
 
 constexpr size_t dd_align16(size_t x) { return (x + 15) & ~(size_t)15; }
-__host__ __device__ inline size_t dd_sort_common(uint32_t n_runs) {
+inline __host__ __device__ size_t dd_sort_common(uint32_t n_runs) {
     return dd_align16(8ull * (n_runs + 4) + 4ull * (DDS_THREADS / 64) + 2ull * DDS_THREADS * DDS_UNROLL);
 }
-constexpr size_t DD_SORT_FAST = 2 * dd_align16(2ull * (DDS_FAST_W + 8)) + 4ull * DDS_THREADS * DDS_UNROLL +
-                                2ull * DDS_THREADS * DDS_UNROLL;
+constexpr size_t DD_SORT_FAST = dd_align16(2ull * (DDS_FAST_W + 8)) + 4ull * DDS_THREADS * DDS_UNROLL +
+                                2ull * DDS_THREADS * DDS_UNROLL + 2ull * DDS_THREADS * DDS_UNROLL;
 constexpr size_t DD_SORT_GENERAL = 8ull * DDS_CAP + 4ull * DDS_SUBW + 4ull * (DDS_SUBW + 4);
 
-size_t dd_sort_lds(const LoopBuffers& b) {
-    return dd_sort_common(b.n_runs) + std::max(DD_SORT_FAST, DD_SORT_GENERAL);
+size_t dd_sort_lds(const LoopBuffers& b) { return dd_sort_common(b.n_runs) + DD_SORT_FAST; }
+size_t dd_sort_general_lds(const LoopBuffers& b) { return dd_sort_common(b.n_runs) + DD_SORT_GENERAL; }
+
+__device__ __forceinline__ DdSortLds dd_carve(void* base, uint32_t n_runs, int T) {
+    DdSortLds L;
+    char* p = static_cast<char*>(base);
+    L.start = reinterpret_cast<uint32_t*>(p); p += 4ull * (n_runs + 4);
+    L.pre = reinterpret_cast<uint32_t*>(p); p += 4ull * (n_runs + 4);
+    L.wsum = reinterpret_cast<uint32_t*>(p); p += 4ull * (T / 64);
+    L.seg = reinterpret_cast<uint16_t*>(p);
+    p = static_cast<char*>(base) + dd_sort_common(n_runs);
+    char* u = p;  // the fast and the general layouts share the rest
+    L.vst16 = reinterpret_cast<uint16_t*>(u); u += dd_align16(2ull * (DDS_FAST_W + 8));
+    L.cl = reinterpret_cast<uint32_t*>(u); u += 4ull * DDS_THREADS * DDS_UNROLL;
+    L.fi = reinterpret_cast<uint16_t*>(u); u += 2ull * DDS_THREADS * DDS_UNROLL;
+    L.res = reinterpret_cast<uint16_t*>(u);
+    L.sorted = reinterpret_cast<unsigned long long*>(p); p += 8ull * DDS_CAP;
+    L.cnt = reinterpret_cast<uint32_t*>(p); p += 4ull * DDS_SUBW;
+    L.vst = reinterpret_cast<uint32_t*>(p);
+    return L;
 }
 
 // Exclusive prefix of a[0, n) into o[0, n] (o[n] = total; a == o allowed), whole workgroup.
@@ -1932,14 +1952,109 @@ __device__ __forceinline__ uint32_t lds_inc16(uint16_t* a, uint32_t i) {
     return (atomicAdd(w, 1u << sh) >> sh) & 0xFFFFu;
 }
 
-// General path of k_bsort (a bucket wider than DDS_FAST_W variables, or more pairs than one
-// sweep): variables DDS_SUBW at a time, pieces of DDS_CAP pairs, items reloaded per sweep.  Not
-// inlined, so that the fast path keeps its registers.
+__device__ __forceinline__ bool dd_fast_bucket(uint32_t np, uint32_t width) {
+    return np <= (uint32_t)(DDS_THREADS * DDS_UNROLL) && width <= DDS_FAST_W;
+}
+
 template <int U, int T>
-__device__ __noinline__ void bsort_general(const LoopBuffers& b, const DdSortLds& L, uint32_t run_cap, uint32_t np) {
+__global__ __launch_bounds__(T) void k_bsort(LoopBuffers b, uint32_t run_cap, int fused_reduce) {
+    extern __shared__ __attribute__((aligned(16))) unsigned long long s_dds[];
+    const DdSortLds L = dd_carve(s_dds, b.n_runs, T);
+    const ResolveLds R{nullptr, L.start, L.pre, L.wsum};
+    const uint32_t nr = b.n_runs;  // <= BKT_RUN_BATCH (checked at create)
+    dbg_stamp(b, 1, 0);
+    const uint32_t np = resolve_batch(b, R, 0, nr);
+    dbg_stamp(b, 1, 1);
+    const uint32_t width = b.bkt_width;
+    if (np && dd_fast_bucket(np, width)) {  // (uniform; the others: k_bsort_general)
+        const uint32_t first = (threadIdx.x >> 6) * 64 * U + (threadIdx.x & 63);
+        resolve_seg_table(R, nr, np, 0, T * U, L.seg);
+        uint32_t* v32 = reinterpret_cast<uint32_t*>(L.vst16);
+        for (uint32_t i = threadIdx.x; i < (width + 2) / 2; i += T) v32[i] = 0;
+        __syncthreads();
+        auto pos_of = [&](uint32_t f) {
+            const uint32_t q = L.seg[f];
+            return q * run_cap + L.start[q] + (f - L.pre[q]);
+        };
+        unsigned long long x[U];
+        uint32_t pos[U], rk[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) pos[u] = pos_of(min(first + 64 * u, np - 1));
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u] = b.pairs[pos[u]];
+        dbg_stamp(b, 1, 2);
+        // per-variable counts (the atomics' results rank the pairs of a variable)
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (first + 64 * u < np) rk[u] = lds_inc16(L.vst16, (uint32_t)x[u] & 0x7FFFu);
+        __syncthreads();
+        dbg_stamp(b, 1, 4);
+        block_excl_scan<uint16_t>(L.vst16, L.vst16, width, L.wsum);
+        dbg_stamp(b, 1, 5);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (first + 64 * u >= np) continue;
+            const uint32_t slot = L.vst16[(uint32_t)x[u] & 0x7FFFu] + rk[u];
+            L.cl[slot] = (uint32_t)(x[u] >> 32);
+            L.fi[slot] = (uint16_t)(first + 64 * u);
+        }
+        __syncthreads();
+        dbg_stamp(b, 1, 6);
+        // a thread per variable links its (short) segment: for each pair, whether a lower
+        // clause holds the variable, whether it is its clause's first pair on the variable, and
+        // the first pair of the next clause
+        for (uint32_t v = threadIdx.x; v < width; v += T) {
+            const uint32_t sa = L.vst16[v], se = L.vst16[v + 1];
+            if (se == sa) continue;
+            if (se == sa + 1) { L.res[L.fi[sa]] = (uint16_t)DDS_RES_NONE; continue; }
+            for (uint32_t i = sa; i < se; ++i) {
+                const uint32_t ci = L.cl[i], fi = L.fi[i];
+                bool rep = true, pred = false;
+                uint32_t sc = ~0u, sf = DDS_RES_NONE;
+                for (uint32_t j = sa; j < se; ++j) {
+                    const uint32_t cj = L.cl[j], fj = L.fi[j];
+                    if (cj < ci) pred = true;
+                    else if (cj == ci) rep = rep && !(fj < fi);
+                    else if (cj < sc || (cj == sc && fj < sf)) { sc = cj; sf = fj; }
+                }
+                L.res[fi] = (uint16_t)(!rep ? (DDS_RES_INERT | DDS_RES_NONE) : ((pred ? DDS_RES_PRED : 0u) | sf));
+            }
+        }
+        __syncthreads();
+        dbg_stamp(b, 1, 7);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (first + 64 * u >= np) continue;
+            const uint32_t rs = L.res[first + 64 * u], sf = rs & DDS_RES_NONE;
+            uint32_t lw = (uint32_t)x[u] & DD_EL_MASK;
+            if (rs & DDS_RES_INERT) lw |= DD_INERT;
+            else if (rs & DDS_RES_PRED) lw |= DD_PRED;
+            const uint32_t sp = (rs & DDS_RES_INERT) || sf == DDS_RES_NONE ? DD_NONE : pos_of(sf);
+            b.pairs[pos[u]] = ((unsigned long long)sp << 32) | lw;
+        }
+    }
+    dbg_stamp(b, 1, 3);
+    if (fused_reduce && blockIdx.x == 0) {  // the loop's reduce (one GPU), as in k_bresolve
+        __syncthreads();
+        if (eval_gate_closed(b.state)) {
+            if (threadIdx.x == 0) b.state->active = 0;
+        } else {
+            reduce_body(b, 0);
+        }
+    }
+}
+
+// k_bsort_general: the buckets k_bsort leaves (more pairs than one sweep, or wider than
+// DDS_FAST_W): variables DDS_SUBW at a time, pieces of DDS_CAP pairs, items reloaded per sweep.
+template <int U, int T>
+__global__ __launch_bounds__(T) void k_bsort_general(LoopBuffers b, uint32_t run_cap) {
+    extern __shared__ __attribute__((aligned(16))) unsigned long long s_ddg[];
+    const DdSortLds L = dd_carve(s_ddg, b.n_runs, T);
     const ResolveLds R{nullptr, L.start, L.pre, L.wsum};
     const uint32_t nr = b.n_runs;
+    const uint32_t np = resolve_batch(b, R, 0, nr);
     const uint32_t width = b.bkt_width;
+    if (np == 0 || dd_fast_bucket(np, width)) return;
     const uint32_t stride = T * U;
     const uint32_t first = (threadIdx.x >> 6) * 64 * U + (threadIdx.x & 63);
     unsigned long long x[U];
@@ -2027,133 +2142,13 @@ __device__ __noinline__ void bsort_general(const LoopBuffers& b, const DdSortLds
     }
 }
 
-template <int U, int T>
-__global__ __launch_bounds__(T) void k_bsort(LoopBuffers b, uint32_t run_cap, int fused_reduce) {
-    extern __shared__ __attribute__((aligned(16))) unsigned long long s_dds[];
-    DdSortLds L;
-    {
-        char* p = reinterpret_cast<char*>(s_dds);
-        L.start = reinterpret_cast<uint32_t*>(p); p += 4ull * (b.n_runs + 4);
-        L.pre = reinterpret_cast<uint32_t*>(p); p += 4ull * (b.n_runs + 4);
-        L.wsum = reinterpret_cast<uint32_t*>(p); p += 4ull * (T / 64);
-        L.seg = reinterpret_cast<uint16_t*>(p);
-        p = reinterpret_cast<char*>(s_dds) + dd_sort_common(b.n_runs);
-        char* u = p;  // union of the two paths
-        L.cnt16 = reinterpret_cast<uint16_t*>(u); u += dd_align16(2ull * (DDS_FAST_W + 8));
-        L.vst16 = reinterpret_cast<uint16_t*>(u); u += dd_align16(2ull * (DDS_FAST_W + 8));
-        L.cl = reinterpret_cast<uint32_t*>(u); u += 4ull * T * U;
-        L.fi = reinterpret_cast<uint16_t*>(u);
-        L.sorted = reinterpret_cast<unsigned long long*>(p); p += 8ull * DDS_CAP;
-        L.cnt = reinterpret_cast<uint32_t*>(p); p += 4ull * DDS_SUBW;
-        L.vst = reinterpret_cast<uint32_t*>(p);
-    }
-    const ResolveLds R{nullptr, L.start, L.pre, L.wsum};
-    const uint32_t nr = b.n_runs;  // <= BKT_RUN_BATCH (checked at create)
-    dbg_stamp(b, 1, 0);
-    const uint32_t np = resolve_batch(b, R, 0, nr);
-    dbg_stamp(b, 1, 1);
-    const uint32_t width = b.bkt_width;
-    const uint32_t stride = T * U;
-    const bool single = np <= stride;
-    const uint32_t first = (threadIdx.x >> 6) * 64 * U + (threadIdx.x & 63);
-    unsigned long long x[U];
-    uint32_t pos[U], rk[U];
-    bool ok[U];
-    auto pos_of = [&](uint32_t f, uint32_t s0) {
-        const uint32_t q = L.seg[f - s0];
-        return q * run_cap + L.start[q] + (f - L.pre[q]);
-    };
-    // items [s0, s0 + stride) of the bucket's flat index space: positions and pairs
-    auto load_sweep = [&](uint32_t s0) {
-        resolve_seg_table(R, nr, np, s0, stride, L.seg);
-        __syncthreads();
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t f = s0 + first + 64 * u;
-            ok[u] = f < np;
-            pos[u] = pos_of(min(f, np - 1), s0);
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) x[u] = b.pairs[pos[u]];
-    };
-    auto voff = [&](int u) { return (uint32_t)x[u] & 0x7FFFu; };
-    const bool fast = np && single && width <= DDS_FAST_W;
-    if (fast) load_sweep(0);
-    dbg_stamp(b, 1, 2);
-    if (fast) {
-        // ---- fast path: count, prefix, place, link; every variable of the bucket at once
-        uint32_t* c32 = reinterpret_cast<uint32_t*>(L.cnt16);
-        for (uint32_t i = threadIdx.x; i < (width + 1) / 2; i += T) c32[i] = 0;
-        __syncthreads();
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (ok[u]) rk[u] = lds_inc16(L.cnt16, voff(u));
-        __syncthreads();
-        dbg_stamp(b, 1, 4);
-        block_excl_scan<uint16_t>(L.cnt16, L.vst16, width, L.wsum);
-        dbg_stamp(b, 1, 5);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (!ok[u]) continue;
-            const uint32_t slot = L.vst16[voff(u)] + rk[u];
-            L.cl[slot] = (uint32_t)(x[u] >> 32);
-            L.fi[slot] = (uint16_t)(first + 64 * u);
-        }
-        __syncthreads();
-        dbg_stamp(b, 1, 6);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (!ok[u]) continue;
-            const uint32_t c = (uint32_t)(x[u] >> 32), f = first + 64 * u;
-            const uint32_t sa = L.vst16[voff(u)], se = L.vst16[voff(u) + 1];
-            bool rep = true, pred = false;
-            uint32_t sc = ~0u, sf = ~0u;
-            for (uint32_t j0 = sa; j0 < se; j0 += 4) {  // (segments are short: 4 reads in flight)
-                uint32_t yc[4], yf[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const uint32_t j = min(j0 + q, se - 1);
-                    yc[q] = L.cl[j];
-                    yf[q] = L.fi[j];
-                }
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    if (j0 + q >= se) continue;
-                    if (yc[q] < c) pred = true;
-                    else if (yc[q] == c) rep = rep && !(yf[q] < f);
-                    else if (yc[q] < sc || (yc[q] == sc && yf[q] < sf)) { sc = yc[q]; sf = yf[q]; }
-                }
-            }
-            uint32_t lw = (uint32_t)x[u] & DD_EL_MASK, sp = DD_NONE;
-            if (!rep) lw |= DD_INERT;
-            else {
-                if (pred) lw |= DD_PRED;
-                if (sf != ~0u) sp = pos_of(sf, 0);
-            }
-            b.pairs[pos[u]] = ((unsigned long long)sp << 32) | lw;
-        }
-        dbg_stamp(b, 1, 7);
-    } else if (np) {
-        bsort_general<U, T>(b, L, run_cap, np);
-    }
-    dbg_stamp(b, 1, 3);
-    if (fused_reduce && blockIdx.x == 0) {  // the loop's reduce (one GPU), as in k_bresolve
-        __syncthreads();
-        if (eval_gate_closed(b.state)) {
-            if (threadIdx.x == 0) b.state->active = 0;
-        } else {
-            reduce_body(b, 0);
-        }
-    }
-}
-
 // k_decide (one persistent workgroup per run, all runs resident: n_runs <= CUs): the run's pairs
 // are read in blocks of DDD_BLK (lane l of a wave holds pairs 64 k + l, k < DDD_PB, of its
-// blocks: blk = wave, wave + 16, ...; the first DDD_CACHED blocks stay in registers) and their
-// state is one LDS word per (block, lane): bits 0-7 finished, 8-15 received, 16-23 the received
-// bit, 24-31 has a predecessor.  Entries: one LDS byte per entry slot of the run's tiles: bits
-// 0-3 pairs still waiting for a 0 from their predecessor, bit 4 IN, bit 5 OUT (LDS atomics;
-// every wave sees them at once).
+// blocks: blk = wave, wave + 16, ...; the first one stays in registers) and their state is two
+// LDS words per (block, lane): {finished:16 | received:16}, {received bit:16 | has a
+// predecessor:16}.  Entries: one LDS byte per entry slot of the run's tiles: bits 0-3 pairs still
+// waiting for a 0 from their predecessor, bit 4 IN, bit 5 OUT (LDS atomics; every wave sees them
+// at once).
 // After pass 0 every wave runs on its own, without workgroup barriers, until its pairs have
 // finished: per block it loads the message words of the pairs still waiting (relaxed agent-scope
 // loads of words written by relaxed agent-scope stores, i.e. write-through: the tagged
@@ -2162,14 +2157,14 @@ __global__ __launch_bounds__(T) void k_bsort(LoopBuffers b, uint32_t run_cap, in
 // decided forwards its chain state to its successor and finishes.  A wave that found nothing new
 // sleeps briefly.  IN entries are covered and listed once every wave is done (their entries
 // loaded four at a time).  The wait is bounded by DD_TIMEOUT (state.error = 3; the loop stops).
-constexpr int DDD_PB = 8;
+constexpr int DDD_PB = 12;
 constexpr uint32_t DDD_BLK = 64 * DDD_PB;
-constexpr int DDD_CACHED = 1;
+constexpr uint32_t DDD_ALL = (1u << DDD_PB) - 1u;
 
 size_t dd_decide_lds(const LoopBuffers& b, uint32_t k) {
     const size_t slots = (size_t)b.run_tiles * TILE;
     const size_t cap = slots * k;
-    return slots + 4 * 64 * ((cap + DDD_BLK - 1) / DDD_BLK);
+    return slots + 8 * 64 * ((cap + DDD_BLK - 1) / DDD_BLK);
 }
 
 template <int K>
@@ -2189,8 +2184,12 @@ __global__ __launch_bounds__(DDD_THREADS) void k_decide(ClauseView cv, LoopBuffe
     extern __shared__ __attribute__((aligned(16))) uint32_t s_dd[];
     const uint32_t slots = nt * TILE;
     uint32_t* entw = s_dd;
-    volatile uint8_t* ent = reinterpret_cast<volatile uint8_t*>(s_dd);
-    uint32_t* pst = s_dd + (size_t)b.run_tiles * TILE / 4;
+    // (entry states are read as whole LDS words: atomic loads, so a spin never reuses a stale
+    // register copy, and the compiler keeps them ds_ operations)
+    auto ent_get = [&](uint32_t el) -> uint32_t {
+        return (__hip_atomic_load(&entw[el >> 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >> (8 * (el & 3))) & 0xFFu;
+    };
+    uint2* pst = reinterpret_cast<uint2*>(s_dd + (size_t)b.run_tiles * TILE / 4);
     const uint32_t nblk = (np + DDD_BLK - 1) / DDD_BLK;
     __shared__ uint32_t s_tc[RUN_TILES_MAX], s_pre[RUN_TILES_MAX + 1], s_join[RUN_TILES_MAX], s_mis0[RUN_TILES_MAX];
     __shared__ unsigned long long s_lits[RUN_TILES_MAX];
@@ -2208,46 +2207,51 @@ __global__ __launch_bounds__(DDD_THREADS) void k_decide(ClauseView cv, LoopBuffe
     const uint32_t E = run_prefix(b, t0, nt, s_tc, s_pre);  // (its barriers publish the zeroing above)
     dbg_stamp(b, 2, 1);
     const unsigned long long* pr = b.pairs + (uint64_t)r * run_cap;
-    const uint32_t* rmsg = b.dd_msg + (uint64_t)r * run_cap;
+    // message words through buffer descriptors (32-bit offsets; aux 16 = sc1: write-through
+    // stores, loads that bypass L1): the whole array for the sends, this run's part for the polls
+    const auto rs_all = __builtin_amdgcn_make_buffer_rsrc(b.dd_msg, (short)0, (int)(b.n_runs * run_cap * 4u), 0x00020000);
+    const auto rs_run = __builtin_amdgcn_make_buffer_rsrc(b.dd_msg + (uint64_t)r * run_cap, (short)0, (int)(run_cap * 4u),
+                                                          0x00020000);
     // the pairs of a block, DDD_PB loads in flight together (clamped to the run's last pair)
     auto load_blk = [&](uint32_t blk, unsigned long long (&x)[DDD_PB]) {
 #pragma unroll
         for (int k = 0; k < DDD_PB; ++k) x[k] = pr[min(blk * DDD_BLK + k * 64 + lane, np - 1)];
     };
-    unsigned long long xc[DDD_CACHED][DDD_PB];
-#pragma unroll
-    for (int c = 0; c < DDD_CACHED; ++c)
-        if (wave + c * NW < nblk) load_blk(wave + c * NW, xc[c]);
-    // fn(blk, pairs) over this wave's blocks: the first DDD_CACHED from registers, the rest reloaded
+    unsigned long long xc[DDD_PB];
+    if ((uint32_t)wave < nblk) load_blk(wave, xc);
+    // fn(blk, pairs) over this wave's blocks: the first from registers, the rest reloaded (one
+    // copy of fn: the block's pairs are copied or loaded into x)
     auto for_blocks = [&](auto&& fn) {
-#pragma unroll
-        for (int c = 0; c < DDD_CACHED; ++c)
-            if (wave + c * NW < nblk) fn(wave + c * NW, xc[c]);
-        for (uint32_t blk = wave + DDD_CACHED * NW; blk < nblk; blk += NW) {
+        for (uint32_t blk = wave; blk < nblk; blk += NW) {
             unsigned long long x[DDD_PB];
-            load_blk(blk, x);
+            if (blk == (uint32_t)wave) {
+#pragma unroll
+                for (int k = 0; k < DDD_PB; ++k) x[k] = xc[k];
+            } else {
+                load_blk(blk, x);
+            }
             fn(blk, x);
         }
     };
     // pass 0: waiting counts; pairs with nothing to receive and nothing to send finish
     for_blocks([&](uint32_t blk, unsigned long long (&x)[DDD_PB]) {
-        uint32_t w = 0;
+        uint32_t fin = 0, pred = 0;
 #pragma unroll
         for (int k = 0; k < DDD_PB; ++k) {
             const uint32_t i = blk * DDD_BLK + k * 64 + lane;
             const uint32_t lw = (uint32_t)x[k], el = (lw >> 15) & 0xFFFFu;
-            if (i >= np || (lw & DD_INERT)) w |= 1u << k;
-            else if (lw & DD_PRED) { w |= 1u << (24 + k); atomicAdd(&entw[el >> 2], 1u << (8 * (el & 3))); }
-            else if ((uint32_t)(x[k] >> 32) == DD_NONE) w |= 1u << k;
+            if (i >= np || (lw & DD_INERT)) fin |= 1u << k;
+            else if (lw & DD_PRED) { pred |= 1u << k; atomicAdd(&entw[el >> 2], 1u << (8 * (el & 3))); }
+            else if ((uint32_t)(x[k] >> 32) == DD_NONE) fin |= 1u << k;
         }
-        pst[blk * 64 + lane] = w;
+        pst[blk * 64 + lane] = make_uint2(fin, pred << 16);
     });
     __syncthreads();
     // entries without a predecessor on any variable are IN (flat over the run's entries)
     for (uint32_t f = threadIdx.x; f < E; f += DDD_THREADS) {
         const uint32_t tt = run_tile_of(s_pre, nt, f);
         const uint32_t el = tt * TILE + (f - s_pre[tt]);
-        if (ent[el] == 0) ent[el] = (uint8_t)IN_BIT;  // (no atomics on entries in this phase)
+        if (ent_get(el) == 0) atomicOr(&entw[el >> 2], IN_BIT << (8 * (el & 3)));
     }
     __syncthreads();
     dbg_stamp(b, 2, 2);
@@ -2259,22 +2263,23 @@ __global__ __launch_bounds__(DDD_THREADS) void k_decide(ClauseView cv, LoopBuffe
         ++iters;
         bool open_any = false, moved = false;
         for_blocks([&](uint32_t blk, unsigned long long (&x)[DDD_PB]) {
-            uint32_t w = pst[blk * 64 + lane];
-            const uint32_t open = ~w & 0xFFu;
+            uint2 w = pst[blk * 64 + lane];
+            const uint32_t open = ~w.x & DDD_ALL;
             if (!__builtin_amdgcn_ballot_w64(open != 0)) return;  // (wave-uniform skip)
-            const uint32_t want = (w >> 24) & open & ~(w >> 8);
+            const uint32_t want = (w.y >> 16) & open & ~(w.x >> 16);
             uint32_t m[DDD_PB];
 #pragma unroll
             for (int k = 0; k < DDD_PB; ++k)
-                m[k] = ((want >> k) & 1u) ? __hip_atomic_load(rmsg + blk * DDD_BLK + k * 64 + lane, __ATOMIC_RELAXED,
-                                                              __HIP_MEMORY_SCOPE_AGENT)
+                m[k] = ((want >> k) & 1u) ? __builtin_amdgcn_raw_buffer_load_b32(rs_run, (blk * DDD_BLK + k * 64 + lane) * 4u,
+                                                                                  0, 16)
                                           : 0u;
             // receive: a 1 makes the entry OUT, the last 0 makes it IN
 #pragma unroll
             for (int k = 0; k < DDD_PB; ++k) {
                 if (!((want >> k) & 1u) || (m[k] >> 1) != tag) continue;
                 const uint32_t v = m[k] & 1u;
-                w |= (1u << (8 + k)) | (v << (16 + k));
+                w.x |= 1u << (16 + k);
+                w.y |= v << k;
                 moved = true;
                 const uint32_t el = ((uint32_t)x[k] >> 15) & 0xFFFFu;
                 const uint32_t sh = 8 * (el & 3);
@@ -2290,8 +2295,8 @@ __global__ __launch_bounds__(DDD_THREADS) void k_decide(ClauseView cv, LoopBuffe
             for (int k = 0; k < DDD_PB; ++k) {
                 if (!((open >> k) & 1u)) continue;
                 const uint32_t lw = (uint32_t)x[k], sp = (uint32_t)(x[k] >> 32), el = (lw >> 15) & 0xFFFFu;
-                const uint32_t es = ent[el];
-                const bool recv = (w >> (8 + k)) & 1u;
+                const uint32_t es = ent_get(el);
+                const bool recv = (w.x >> (16 + k)) & 1u;
                 uint32_t fin = 0, val = 2;  // val: the bit to send (2: nothing)
                 if (es & IN_BIT) {
                     fin = 1;
@@ -2302,18 +2307,17 @@ __global__ __launch_bounds__(DDD_THREADS) void k_decide(ClauseView cv, LoopBuffe
                         val = 0;
                     } else if (recv) {
                         fin = 1;
-                        val = (w >> (16 + k)) & 1u;
+                        val = (w.y >> k) & 1u;
                     }
                 } else if (recv && sp == DD_NONE) {
                     fin = 1;  // counted; nothing to pass on
                 }
-                if (val != 2 && sp != DD_NONE)
-                    __hip_atomic_store(b.dd_msg + sp, (tag << 1) | val, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                w |= fin << k;
+                if (val != 2 && sp != DD_NONE) __builtin_amdgcn_raw_buffer_store_b32((tag << 1) | val, rs_all, sp * 4u, 0, 16);
+                w.x |= fin << k;
                 moved |= fin != 0;
             }
             pst[blk * 64 + lane] = w;
-            open_any |= (~w & 0xFFu) != 0;
+            open_any |= (~w.x & DDD_ALL) != 0;
         });
         if (!__builtin_amdgcn_ballot_w64(open_any)) break;
         if (lane == 0 && (iters & 15) == 0 && wall_now() - t_begin > DD_TIMEOUT) stop = true;
@@ -2336,7 +2340,7 @@ __global__ __launch_bounds__(DDD_THREADS) void k_decide(ClauseView cv, LoopBuffe
             const uint32_t f = min(f0 + q, E - 1);
             const uint32_t tt = run_tile_of(s_pre, nt, f);
             el[q] = tt * TILE + (f - s_pre[tt]);
-            is_in[q] = f0 + q < E && (ent[el[q]] & IN_BIT);
+            is_in[q] = f0 + q < E && (ent_get(el[q]) & IN_BIT);
         }
         if (!(is_in[0] || is_in[1] || is_in[2] || is_in[3])) continue;
         Ent<K> e[4];
@@ -3328,11 +3332,14 @@ hipError_t launch_lfmis_dd(const ClauseView& cv, const LoopBuffers& b, bool scat
                            hipStream_t s) {
     if (b.n_tiles == 0 || cv.k == 0 || cv.k > (uint32_t)MAX_FIXED_K || !b.pairs || !b.dd_msg) return hipErrorInvalidValue;
     const uint32_t run_cap = b.run_tiles * TILE * cv.k;
-    const size_t lds_sort = dd_sort_lds(b), lds_dec = dd_decide_lds(b, cv.k);
+    const size_t lds_sort = dd_sort_lds(b), lds_gen = dd_sort_general_lds(b), lds_dec = dd_decide_lds(b, cv.k);
     int dev;
     if (attr_pending(ATTR_DD + cv.k, dev)) {
         hipError_t e = hipFuncSetAttribute((const void*)k_bsort<DDS_UNROLL, DDS_THREADS>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 512);
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute((const void*)k_bsort_general<DDS_UNROLL_GEN, DDS_THREADS>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 512);
         if (e != hipSuccess) return e;
         ALLL_DISPATCH_K(cv.k, (e = hipFuncSetAttribute((const void*)k_decide<(K > 0 ? K : 1)>,
                                                        hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 1024)));
@@ -3351,6 +3358,8 @@ hipError_t launch_lfmis_dd(const ClauseView& cv, const LoopBuffers& b, bool scat
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     k_bsort<DDS_UNROLL, DDS_THREADS><<<b.n_bkt, DDS_THREADS, lds_sort, s>>>(b, run_cap, fr);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    k_bsort_general<DDS_UNROLL_GEN, DDS_THREADS><<<b.n_bkt, DDS_THREADS, lds_gen, s>>>(b, run_cap);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     ALLL_DISPATCH_K(cv.k, (k_decide<(K > 0 ? K : 1)><<<b.n_runs, DDD_THREADS, lds_dec, s>>>(cv, b, b.stage[0], run_cap)));
     return hipGetLastError();

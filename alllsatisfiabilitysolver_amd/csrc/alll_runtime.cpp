@@ -847,8 +847,8 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
             const uint32_t run_cap32 = b.run_tiles * TILE * (uint32_t)fixed_k;
             c->dd = c->world == 1 && zero_id && !n_hot && !opt.stream_batch && !rr_T &&
                     b.n_runs <= (uint32_t)c->n_cu && b.n_runs <= BKT_RUN_BATCH && b.run_tiles <= RUN_TILES_MAX &&
-                    dd_sort_lds(b) <= 160u * 1024 - 512 && dd_decide_lds(b, (uint32_t)fixed_k) <= 160u * 1024 - 1024 &&
-                    max_deg <= DDS_CAP && (uint64_t)b.n_runs * run_cap32 < 0xFFFFFFFFull;
+                    dd_sort_lds(b) <= 160u * 1024 - 512 && dd_sort_general_lds(b) <= 160u * 1024 - 512 && dd_decide_lds(b, (uint32_t)fixed_k) <= 160u * 1024 - 1024 &&
+                    max_deg <= DDS_CAP && (uint64_t)b.n_runs * run_cap32 * 4 < (1ull << 31);  // (buffer offsets)
             if (const char* e = getenv("ALLL_DD")) c->dd = c->dd && atoi(e) != 0;
             if (c->dd) {
                 if ((rc = dalloc(c, &b.dd_msg, (size_t)b.n_runs * run_cap32))) return bail(rc);

@@ -142,6 +142,7 @@ struct LoopBuffers {
     uint32_t* dd_msg;           // dependency-driven LFMIS: one message word per pair position (chain
                                 // state of the pair's variable below its clause, tagged with n_iter);
                                 // nullptr = the round-synchronous LFMIS
+    uint32_t dd_senders;        // k_decide: one wave only sends (the others queue in LDS)
     const uint32_t* win_base;   // hybrid eval: per tile, first assignment word of its LDS window
                                 // (nullptr: words [0, win_words) for every tile)
     uint32_t win_words;         // hybrid eval: LDS window size in words (<= LDS_WORDS)

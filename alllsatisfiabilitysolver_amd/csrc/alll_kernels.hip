@@ -2007,17 +2007,45 @@ __global__ __launch_bounds__(T) void k_bsort(LoopBuffers b, uint32_t run_cap, in
             const uint32_t sa = L.vst16[v], se = L.vst16[v + 1];
             if (se == sa) continue;
             if (se == sa + 1) { L.res[L.fi[sa]] = (uint16_t)DDS_RES_NONE; continue; }
-            for (uint32_t i = sa; i < se; ++i) {
-                const uint32_t ci = L.cl[i], fi = L.fi[i];
-                bool rep = true, pred = false;
-                uint32_t sc = ~0u, sf = DDS_RES_NONE;
-                for (uint32_t j = sa; j < se; ++j) {
-                    const uint32_t cj = L.cl[j], fj = L.fi[j];
-                    if (cj < ci) pred = true;
-                    else if (cj == ci) rep = rep && !(fj < fi);
-                    else if (cj < sc || (cj == sc && fj < sf)) { sc = cj; sf = fj; }
+            // up to DDS_SEG claimants (all but a few variables): read at once, compared unrolled;
+            // longer segments: each member scans the segment, DDS_SEG reads in flight
+            constexpr int G = 8;
+            const uint32_t n8 = se - sa;
+            for (uint32_t i0 = 0; i0 < n8; i0 += G) {
+                uint32_t ci[G], fi[G];
+#pragma unroll
+                for (int q = 0; q < G; ++q) {
+                    const uint32_t j = sa + min(i0 + q, n8 - 1);
+                    ci[q] = L.cl[j];
+                    fi[q] = L.fi[j];
                 }
-                L.res[fi] = (uint16_t)(!rep ? (DDS_RES_INERT | DDS_RES_NONE) : ((pred ? DDS_RES_PRED : 0u) | sf));
+                bool rep[G], pred[G];
+                uint32_t sc[G], sf[G];
+#pragma unroll
+                for (int q = 0; q < G; ++q) { rep[q] = true; pred[q] = false; sc[q] = ~0u; sf[q] = DDS_RES_NONE; }
+                for (uint32_t j0 = 0; j0 < n8; j0 += G) {
+                    uint32_t cj[G], fj[G];
+#pragma unroll
+                    for (int q = 0; q < G; ++q) {
+                        const uint32_t j = sa + min(j0 + q, n8 - 1);
+                        cj[q] = L.cl[j];
+                        fj[q] = L.fi[j];
+                    }
+#pragma unroll
+                    for (int i = 0; i < G; ++i)
+#pragma unroll
+                        for (int q = 0; q < G; ++q) {
+                            if (j0 + q >= n8) continue;
+                            if (cj[q] < ci[i]) pred[i] = true;
+                            else if (cj[q] == ci[i]) rep[i] = rep[i] && !(fj[q] < fi[i]);
+                            else if (cj[q] < sc[i] || (cj[q] == sc[i] && fj[q] < sf[i])) { sc[i] = cj[q]; sf[i] = fj[q]; }
+                        }
+                }
+#pragma unroll
+                for (int i = 0; i < G; ++i)
+                    if (i0 + i < n8)
+                        L.res[fi[i]] = (uint16_t)(!rep[i] ? (DDS_RES_INERT | DDS_RES_NONE)
+                                                          : ((pred[i] ? DDS_RES_PRED : 0u) | sf[i]));
             }
         }
         __syncthreads();
@@ -2030,7 +2058,7 @@ __global__ __launch_bounds__(T) void k_bsort(LoopBuffers b, uint32_t run_cap, in
             if (rs & DDS_RES_INERT) lw |= DD_INERT;
             else if (rs & DDS_RES_PRED) lw |= DD_PRED;
             const uint32_t sp = (rs & DDS_RES_INERT) || sf == DDS_RES_NONE ? DD_NONE : pos_of(sf);
-            b.pairs[pos[u]] = ((unsigned long long)sp << 32) | lw;
+            b.pairs[pos_of(first + 64 * u)] = ((unsigned long long)sp << 32) | lw;  // (pos[] recomputed: registers)
         }
     }
     dbg_stamp(b, 1, 3);
@@ -2161,10 +2189,12 @@ constexpr int DDD_PB = 12;
 constexpr uint32_t DDD_BLK = 64 * DDD_PB;
 constexpr uint32_t DDD_ALL = (1u << DDD_PB) - 1u;
 
+constexpr uint32_t DDD_RING = 2048;  // send queue of the sender wave (entries {slot:32 | payload:32})
+
 size_t dd_decide_lds(const LoopBuffers& b, uint32_t k) {
     const size_t slots = (size_t)b.run_tiles * TILE;
     const size_t cap = slots * k;
-    return slots + 8 * 64 * ((cap + DDD_BLK - 1) / DDD_BLK);
+    return slots + 8 * 64 * ((cap + DDD_BLK - 1) / DDD_BLK) + 8 * DDD_RING;
 }
 
 template <int K>
@@ -2191,18 +2221,27 @@ __global__ __launch_bounds__(DDD_THREADS) void k_decide(ClauseView cv, LoopBuffe
     };
     uint2* pst = reinterpret_cast<uint2*>(s_dd + (size_t)b.run_tiles * TILE / 4);
     const uint32_t nblk = (np + DDD_BLK - 1) / DDD_BLK;
+    const size_t cap_blocks = ((size_t)b.run_tiles * TILE * K + DDD_BLK - 1) / DDD_BLK;
+    unsigned long long* ring = reinterpret_cast<unsigned long long*>(pst + cap_blocks * 64);
     __shared__ uint32_t s_tc[RUN_TILES_MAX], s_pre[RUN_TILES_MAX + 1], s_join[RUN_TILES_MAX], s_mis0[RUN_TILES_MAX];
     __shared__ unsigned long long s_lits[RUN_TILES_MAX];
-    __shared__ uint32_t s_passes;
+    __shared__ uint32_t s_passes, s_qtail, s_qhead, s_pdone, s_stop;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     constexpr int NW = DDD_THREADS / 64;
+    // With b.dd_senders the last wave only sends: the others queue their messages in LDS, so
+    // that a poll's wait never includes the completion of the write-through stores.
+    const uint32_t senders = b.dd_senders ? 1u : 0u;
+    const uint32_t NWP = NW - senders;  // polling waves
+    const bool is_sender = senders && (uint32_t)wave == NW - 1;
     for (uint32_t i = threadIdx.x; i < slots / 4; i += DDD_THREADS) entw[i] = 0;
     if (threadIdx.x < nt) {
         s_join[threadIdx.x] = 0;
         s_lits[threadIdx.x] = 0;
         s_mis0[threadIdx.x] = b.mis_cnt[t0 + threadIdx.x];
     }
-    if (threadIdx.x == 0) s_passes = 0;
+    if (threadIdx.x == 0) { s_passes = 0; s_qtail = 0; s_qhead = 0; s_pdone = 0; s_stop = 0; }
+    if (senders)
+        for (uint32_t i = threadIdx.x; i < DDD_RING; i += DDD_THREADS) ring[i] = ~0ull;  // (no slot matches)
     dbg_stamp(b, 2, 0);
     const uint32_t E = run_prefix(b, t0, nt, s_tc, s_pre);  // (its barriers publish the zeroing above)
     dbg_stamp(b, 2, 1);
@@ -2218,11 +2257,12 @@ __global__ __launch_bounds__(DDD_THREADS) void k_decide(ClauseView cv, LoopBuffe
         for (int k = 0; k < DDD_PB; ++k) x[k] = pr[min(blk * DDD_BLK + k * 64 + lane, np - 1)];
     };
     unsigned long long xc[DDD_PB];
-    if ((uint32_t)wave < nblk) load_blk(wave, xc);
-    // fn(blk, pairs) over this wave's blocks: the first from registers, the rest reloaded (one
-    // copy of fn: the block's pairs are copied or loaded into x)
+    if (!is_sender && (uint32_t)wave < nblk) load_blk(wave, xc);
+    // fn(blk, pairs) over this (polling) wave's blocks: the first from registers, the rest
+    // reloaded (one copy of fn: the block's pairs are copied or loaded into x)
     auto for_blocks = [&](auto&& fn) {
-        for (uint32_t blk = wave; blk < nblk; blk += NW) {
+        if (is_sender) return;
+        for (uint32_t blk = wave; blk < nblk; blk += NWP) {
             unsigned long long x[DDD_PB];
             if (blk == (uint32_t)wave) {
 #pragma unroll
@@ -2259,7 +2299,55 @@ __global__ __launch_bounds__(DDD_THREADS) void k_decide(ClauseView cv, LoopBuffe
     const unsigned long long t_begin = wall_now();
     uint32_t iters = 0;
     bool stop = false;
+    if (is_sender) {
+        // drain the queue: slot s holds {s, val << 31 | successor position} once written
+        uint32_t head = 0;
+        for (;;) {
+            const uint32_t tail = __hip_atomic_load(&s_qtail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (tail != head) {
+                const uint32_t n = min(64u, tail - head), slot = head + lane;
+                if ((uint32_t)lane < n) {
+                    unsigned long long e;
+                    do {
+                        e = __hip_atomic_load(&ring[slot % DDD_RING], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    } while ((uint32_t)(e >> 32) != slot);
+                    const uint32_t pl = (uint32_t)e;
+                    __builtin_amdgcn_raw_buffer_store_b32((tag << 1) | (pl >> 31), rs_all, (pl & 0x7FFFFFFFu) * 4u, 0, 16);
+                }
+                head += n;
+                if (lane == 0) __hip_atomic_store(&s_qhead, head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                continue;
+            }
+            if (__hip_atomic_load(&s_pdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == NWP) {
+                if (__hip_atomic_load(&s_qtail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == head) break;
+                continue;
+            }
+            if (__hip_atomic_load(&s_stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    // a polling wave's message: queued for the sender wave (one LDS atomic per wave and slot k),
+    // or stored directly
+    auto send = [&](bool go, uint32_t sp, uint32_t val) {
+        if (!senders) {
+            if (go) __builtin_amdgcn_raw_buffer_store_b32((tag << 1) | val, rs_all, sp * 4u, 0, 16);
+            return;
+        }
+        const uint64_t bm = __builtin_amdgcn_ballot_w64(go);
+        if (!bm) return;
+        uint32_t base = 0;
+        const uint32_t lead = (uint32_t)__builtin_ctzll(bm);
+        if ((uint32_t)lane == lead) base = atomicAdd(&s_qtail, (uint32_t)__popcll(bm));
+        base = __shfl(base, lead, 64);
+        if (!go) return;
+        const uint32_t slot = base + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull));
+        while (slot - __hip_atomic_load(&s_qhead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= DDD_RING)
+            __builtin_amdgcn_s_sleep(1);  // (ring full: the sender drains it independently)
+        __hip_atomic_store(&ring[slot % DDD_RING], ((unsigned long long)slot << 32) | (val << 31) | sp,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
     for (;;) {
+        if (is_sender) break;
         ++iters;
         bool open_any = false, moved = false;
         for_blocks([&](uint32_t blk, unsigned long long (&x)[DDD_PB]) {
@@ -2312,7 +2400,7 @@ __global__ __launch_bounds__(DDD_THREADS) void k_decide(ClauseView cv, LoopBuffe
                 } else if (recv && sp == DD_NONE) {
                     fin = 1;  // counted; nothing to pass on
                 }
-                if (val != 2 && sp != DD_NONE) __builtin_amdgcn_raw_buffer_store_b32((tag << 1) | val, rs_all, sp * 4u, 0, 16);
+                send(val != 2 && sp != DD_NONE, sp, val);
                 w.x |= fin << k;
                 moved |= fin != 0;
             }
@@ -2322,10 +2410,18 @@ __global__ __launch_bounds__(DDD_THREADS) void k_decide(ClauseView cv, LoopBuffe
         if (!__builtin_amdgcn_ballot_w64(open_any)) break;
         if (lane == 0 && (iters & 15) == 0 && wall_now() - t_begin > DD_TIMEOUT) stop = true;
         if (__builtin_amdgcn_readfirstlane(stop ? 1u : 0u)) {
-            if (lane == 0) { st->error = 3; st->done = 3; }
+            if (lane == 0) {
+                st->error = 3;
+                st->done = 3;
+                __hip_atomic_store(&s_stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
             break;
         }
         if (!__builtin_amdgcn_ballot_w64(moved)) __builtin_amdgcn_s_sleep(2);
+    }
+    if (!is_sender && lane == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // (this wave's queue entries first)
+        atomicAdd(&s_pdone, 1u);
     }
     if (lane == 0) atomicMax(&s_passes, iters);
     __syncthreads();

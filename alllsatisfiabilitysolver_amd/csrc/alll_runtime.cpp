@@ -852,6 +852,8 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
             if (const char* e = getenv("ALLL_DD")) c->dd = c->dd && atoi(e) != 0;
             if (c->dd) {
                 if ((rc = dalloc(c, &b.dd_msg, (size_t)b.n_runs * run_cap32))) return bail(rc);
+                b.dd_senders = 1;
+                if (const char* e = getenv("ALLL_DD_SENDERS")) b.dd_senders = atoi(e) != 0;  // A/B
                 c->bucket_min_u = 0;  // three launches at any violated count (no small-set variants)
             }
         }

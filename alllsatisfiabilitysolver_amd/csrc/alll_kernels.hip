@@ -1880,6 +1880,7 @@ struct DdSortLds {
     uint32_t* cl;                // fast: placed pairs' clauses
     uint16_t* fi;                // fast: placed pairs' item indices
     uint16_t* res;               // fast: per item {successor item:14 | has predecessor:1 | inert:1}
+    uint16_t* mlist;             // fast: variables with several claimants (at most items / 2)
     unsigned long long* sorted;  // general: DDS_CAP {clause:32 | pair position:32}
     uint32_t* cnt;               // general: DDS_SUBW counts, then cursors
     uint32_t* vst;               // general: DDS_SUBW + 1 exclusive prefix
@@ -1890,7 +1891,8 @@ inline __host__ __device__ size_t dd_sort_common(uint32_t n_runs) {
     return dd_align16(8ull * (n_runs + 4) + 4ull * (DDS_THREADS / 64) + 2ull * DDS_THREADS * DDS_UNROLL);
 }
 constexpr size_t DD_SORT_FAST = dd_align16(2ull * (DDS_FAST_W + 8)) + 4ull * DDS_THREADS * DDS_UNROLL +
-                                2ull * DDS_THREADS * DDS_UNROLL + 2ull * DDS_THREADS * DDS_UNROLL;
+                                2ull * DDS_THREADS * DDS_UNROLL + 2ull * DDS_THREADS * DDS_UNROLL +
+                                1ull * DDS_THREADS * DDS_UNROLL;
 constexpr size_t DD_SORT_GENERAL = 8ull * DDS_CAP + 4ull * DDS_SUBW + 4ull * (DDS_SUBW + 4);
 
 size_t dd_sort_lds(const LoopBuffers& b) { return dd_sort_common(b.n_runs) + DD_SORT_FAST; }
@@ -1908,7 +1910,8 @@ __device__ __forceinline__ DdSortLds dd_carve(void* base, uint32_t n_runs, int T
     L.vst16 = reinterpret_cast<uint16_t*>(u); u += dd_align16(2ull * (DDS_FAST_W + 8));
     L.cl = reinterpret_cast<uint32_t*>(u); u += 4ull * DDS_THREADS * DDS_UNROLL;
     L.fi = reinterpret_cast<uint16_t*>(u); u += 2ull * DDS_THREADS * DDS_UNROLL;
-    L.res = reinterpret_cast<uint16_t*>(u);
+    L.res = reinterpret_cast<uint16_t*>(u); u += 2ull * DDS_THREADS * DDS_UNROLL;
+    L.mlist = reinterpret_cast<uint16_t*>(u);
     L.sorted = reinterpret_cast<unsigned long long*>(p); p += 8ull * DDS_CAP;
     L.cnt = reinterpret_cast<uint32_t*>(p); p += 4ull * DDS_SUBW;
     L.vst = reinterpret_cast<uint32_t*>(p);
@@ -2000,52 +2003,69 @@ __global__ __launch_bounds__(T) void k_bsort(LoopBuffers b, uint32_t run_cap, in
         }
         __syncthreads();
         dbg_stamp(b, 1, 6);
-        // a thread per variable links its (short) segment: for each pair, whether a lower
-        // clause holds the variable, whether it is its clause's first pair on the variable, and
-        // the first pair of the next clause
+        // Links of each variable's (short) segment: for each pair, whether a lower clause holds
+        // the variable, whether it is its clause's first pair on the variable, and the first pair
+        // of the next clause.  One claimant: nothing to link.  Several (a quarter of the variables
+        // at 3-SAT ratio 4): listed first, so that each sorting pass runs on full waves.
+        __shared__ uint32_t s_nmulti;
+        if (threadIdx.x == 0) s_nmulti = 0;
+        __syncthreads();
         for (uint32_t v = threadIdx.x; v < width; v += T) {
             const uint32_t sa = L.vst16[v], se = L.vst16[v + 1];
-            if (se == sa) continue;
-            if (se == sa + 1) { L.res[L.fi[sa]] = (uint16_t)DDS_RES_NONE; continue; }
-            // up to DDS_SEG claimants (all but a few variables): read at once, compared unrolled;
-            // longer segments: each member scans the segment, DDS_SEG reads in flight
-            constexpr int G = 8;
-            const uint32_t n8 = se - sa;
-            for (uint32_t i0 = 0; i0 < n8; i0 += G) {
-                uint32_t ci[G], fi[G];
+            if (se == sa + 1) L.res[L.fi[sa]] = (uint16_t)DDS_RES_NONE;
+            const bool multi = se > sa + 1;
+            const uint64_t bm = __builtin_amdgcn_ballot_w64(multi);
+            if (!bm) continue;
+            const uint32_t lead = (uint32_t)__builtin_ctzll(bm);
+            uint32_t base = 0;
+            if ((threadIdx.x & 63) == lead) base = atomicAdd(&s_nmulti, (uint32_t)__popcll(bm));
+            base = __shfl(base, lead, 64);
+            if (multi) L.mlist[base + (uint32_t)__popcll(bm & ((1ull << (threadIdx.x & 63)) - 1ull))] = (uint16_t)v;
+        }
+        __syncthreads();
+        const uint32_t nm = s_nmulti;
+        for (uint32_t idx = threadIdx.x; idx < nm; idx += T) {
+            const uint32_t v = L.mlist[idx];
+            const uint32_t sa = L.vst16[v], se = L.vst16[v + 1], n = se - sa;
+            if (n <= 4) {
+                // sort up to four {clause:32 | item:16} keys (a 5-exchange network; missing ones
+                // are ~0 and sort last), then read the links off the neighbours
+                unsigned long long k4[4];
 #pragma unroll
-                for (int q = 0; q < G; ++q) {
-                    const uint32_t j = sa + min(i0 + q, n8 - 1);
-                    ci[q] = L.cl[j];
-                    fi[q] = L.fi[j];
+                for (int q = 0; q < 4; ++q)
+                    k4[q] = (uint32_t)q < n ? ((unsigned long long)L.cl[sa + q] << 16) | L.fi[sa + q] : ~0ull;
+                auto cx = [](unsigned long long& a, unsigned long long& c) {
+                    const unsigned long long lo = a < c ? a : c, hi = a < c ? c : a;
+                    a = lo;
+                    c = hi;
+                };
+                cx(k4[0], k4[1]); cx(k4[2], k4[3]); cx(k4[0], k4[2]); cx(k4[1], k4[3]); cx(k4[1], k4[2]);
+                const uint64_t c0 = k4[0] >> 16;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    if ((uint32_t)i >= n) continue;
+                    const uint64_t ci = k4[i] >> 16;
+                    const bool rep = i == 0 || (k4[i - 1] >> 16) != ci;
+                    uint32_t sf = DDS_RES_NONE;
+#pragma unroll
+                    for (int j = 3; j > i; --j)
+                        if ((uint32_t)j < n && (k4[j] >> 16) != ci && (j == i + 1 || (k4[j - 1] >> 16) == ci)) sf = (uint32_t)k4[j] & 0xFFFFu;
+                    L.res[(uint32_t)k4[i] & 0xFFFFu] = (uint16_t)(!rep ? (DDS_RES_INERT | DDS_RES_NONE)
+                                                                       : ((c0 < ci ? DDS_RES_PRED : 0u) | sf));
                 }
-                bool rep[G], pred[G];
-                uint32_t sc[G], sf[G];
-#pragma unroll
-                for (int q = 0; q < G; ++q) { rep[q] = true; pred[q] = false; sc[q] = ~0u; sf[q] = DDS_RES_NONE; }
-                for (uint32_t j0 = 0; j0 < n8; j0 += G) {
-                    uint32_t cj[G], fj[G];
-#pragma unroll
-                    for (int q = 0; q < G; ++q) {
-                        const uint32_t j = sa + min(j0 + q, n8 - 1);
-                        cj[q] = L.cl[j];
-                        fj[q] = L.fi[j];
+            } else {
+                for (uint32_t i = sa; i < se; ++i) {  // (rare: five or more claimants)
+                    const uint32_t ci = L.cl[i], fi = L.fi[i];
+                    bool rep = true, pred = false;
+                    uint32_t sc = ~0u, sf = DDS_RES_NONE;
+                    for (uint32_t j = sa; j < se; ++j) {
+                        const uint32_t cj = L.cl[j], fj = L.fi[j];
+                        if (cj < ci) pred = true;
+                        else if (cj == ci) rep = rep && !(fj < fi);
+                        else if (cj < sc || (cj == sc && fj < sf)) { sc = cj; sf = fj; }
                     }
-#pragma unroll
-                    for (int i = 0; i < G; ++i)
-#pragma unroll
-                        for (int q = 0; q < G; ++q) {
-                            if (j0 + q >= n8) continue;
-                            if (cj[q] < ci[i]) pred[i] = true;
-                            else if (cj[q] == ci[i]) rep[i] = rep[i] && !(fj[q] < fi[i]);
-                            else if (cj[q] < sc[i] || (cj[q] == sc[i] && fj[q] < sf[i])) { sc[i] = cj[q]; sf[i] = fj[q]; }
-                        }
+                    L.res[fi] = (uint16_t)(!rep ? (DDS_RES_INERT | DDS_RES_NONE) : ((pred ? DDS_RES_PRED : 0u) | sf));
                 }
-#pragma unroll
-                for (int i = 0; i < G; ++i)
-                    if (i0 + i < n8)
-                        L.res[fi[i]] = (uint16_t)(!rep[i] ? (DDS_RES_INERT | DDS_RES_NONE)
-                                                          : ((pred[i] ? DDS_RES_PRED : 0u) | sf[i]));
             }
         }
         __syncthreads();

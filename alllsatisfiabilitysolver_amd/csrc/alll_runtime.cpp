@@ -773,7 +773,7 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
             bool zid = true;
             for (int i = 0; i < 128; ++i) zid &= opt.comm_id[i] == 0;
             const char* e = getenv("ALLL_DD");
-            if (c->world == 1 && zid && !n_hot && !opt.stream_batch && !rr_T && !(e && atoi(e) == 0)) {
+            if (c->world == 1 && zid && !n_hot && !opt.stream_batch && !rr_T && e && atoi(e) != 0) {
                 if (const char* e2 = getenv("ALLL_DD_BKT_PER_CU")) per_cu = (uint32_t)std::max(1, atoi(e2));
             }
         }
@@ -849,7 +849,11 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
                     b.n_runs <= (uint32_t)c->n_cu && b.n_runs <= BKT_RUN_BATCH && b.run_tiles <= RUN_TILES_MAX &&
                     dd_sort_lds(b) <= 160u * 1024 - 512 && dd_sort_general_lds(b) <= 160u * 1024 - 512 && dd_decide_lds(b, (uint32_t)fixed_k) <= 160u * 1024 - 1024 &&
                     max_deg <= DDS_CAP && (uint64_t)b.n_runs * run_cap32 * 4 < (1ull << 31);  // (buffer offsets)
-            if (const char* e = getenv("ALLL_DD")) c->dd = c->dd && atoi(e) != 0;
+            // (opt-in: measured slower than the round-synchronous LFMIS at M)
+            {
+                const char* e = getenv("ALLL_DD");
+                c->dd = c->dd && e && atoi(e) != 0;
+            }
             if (c->dd) {
                 if ((rc = dalloc(c, &b.dd_msg, (size_t)b.n_runs * run_cap32))) return bail(rc);
                 b.dd_senders = 1;

@@ -36,12 +36,11 @@ LAYOUTS = {"hybrid": (0, {}), "fixed": (1 << 3, {}), "csr": (1 << 2, {}), "atomi
            # with windows
            "nt_windows": (0, {"ALLL_EVAL_NT": "1", "ALLL_EVAL_WINDOWS": "1"}),
            # one grid round + the tail in every iteration after the first (variant 2), and never
-           "tail_all": (0, {"ALLL_SMALL_U": str(1 << 62), "ALLL_DD": "0"}),
-           "no_small_u": (0, {"ALLL_SMALL_U": "0", "ALLL_DD": "0"}),
-           # the round-synchronous LFMIS (bucketed round 0, claim/join rounds, tail) instead of the
-           # dependency-driven one (the default where eligible)
-           "rounds": (0, {"ALLL_DD": "0", "ALLL_BUCKET_MIN_U": "0"}),
-           "rounds_scatter": (0, {"ALLL_DD": "0", "ALLL_FUSE_SCATTER": "1", "ALLL_BUCKET_MIN_U": "0"})}
+           "tail_all": (0, {"ALLL_SMALL_U": str(1 << 62)}), "no_small_u": (0, {"ALLL_SMALL_U": "0"}),
+           # the dependency-driven LFMIS (opt-in) instead of the round-synchronous one
+           "dd": (0, {"ALLL_DD": "1"}),
+           "dd_scatter": (0, {"ALLL_DD": "1", "ALLL_FUSE_SCATTER": "1"}),
+           "dd_no_senders": (0, {"ALLL_DD": "1", "ALLL_DD_SENDERS": "0"})}
 
 
 def make_solver(layout, monkeypatch, *args, **kw):
@@ -332,9 +331,10 @@ BIG = {
     "C4_3sat_128M": (32_000_000, 128_000_000, 3, 0),
     # M through the large-instance evaluation variant (C4 takes it by default)
     "M_nt": (2_500_000, 10_000_000, 3, 0, {"ALLL_EVAL_NT": "1"}),
-    # the round-synchronous LFMIS at full size (the default there is the dependency-driven one)
-    "M_rounds": (2_500_000, 10_000_000, 3, 0, {"ALLL_DD": "0"}),
-    "C3_rounds": (4_000_000, 6_000_000, 8, 0, {"ALLL_DD": "0"}),
+    # the dependency-driven LFMIS at full size (opt-in; first iteration through k_bsort_general)
+    "M_dd": (2_500_000, 10_000_000, 3, 0, {"ALLL_DD": "1"}),
+    "C2_dd": (1_000_000, 4_000_000, 3, 0, {"ALLL_DD": "1"}),
+    "C3_dd": (4_000_000, 6_000_000, 8, 0, {"ALLL_DD": "1"}),
     # ragged widths 2-12 (bench config R): the chunk-transposed ragged evaluation, CSR LFMIS
     "R_mixed_4M": (1_000_000, 4_000_000, (2, 12), 0),
     "R_mixed_4M_csr": (1_000_000, 4_000_000, (2, 12), 0, {"ALLL_NO_RAGGED": "1"}),

@@ -2703,8 +2703,8 @@ __global__ void k_apply_delta(LoopBuffers b) {
 // erasure.  Skipped clauses before a group's first uncommitted pick are erased for certain
 // (covered by committed picks), so no scan is repeated.
 constexpr int RR_THREADS = 1024;
-constexpr uint32_t RR_HBITS = 11;
-constexpr uint32_t RR_HASH = 1u << RR_HBITS;  // batch hash slots (variable -> earliest turn, groups)
+constexpr uint32_t RR_HBITS = 12;
+constexpr uint32_t RR_HASH = 1u << RR_HBITS;  // batch hash slots (variable -> earliest turn)
 constexpr uint32_t RR_VCAP = RR_HASH / 2;     // variables of the picks of one batch
 constexpr uint32_t RR_CMAX = 2048;            // picks of one batch
 constexpr uint32_t RR_SHASH = 8192;           // step hash slots {variable:32 | lane:32}, split between groups
@@ -2716,7 +2716,6 @@ constexpr unsigned long long RR_EMPTY64 = ~0ull;
 struct RRLds {
     uint32_t hkey[RR_HASH];
     uint32_t hmin[RR_HASH];
-    unsigned long long hgrp[RR_HASH];
     unsigned long long skey[RR_SHASH];
     uint32_t cc[RR_CMAX];      // group g: [g*cpg, g*cpg + ncand[g]) picked clause ids
     uint32_t cpos[RR_CMAX];    // their positions in U
@@ -2724,33 +2723,45 @@ struct RRLds {
     uint32_t end[RR_TMAX];     // per set: end of its clauses in U
     uint16_t live[RR_TMAX];    // live sets in the reference's vector order
     uint32_t ncand[64], scan_end[64], exh[64];
-    uint32_t n_live, t, trunc, tm, wide;
+    uint32_t n_live, t, conf, tm, wide;
     uint32_t n_steps, n_rounds;  // diagnostics (ALLL_DEBUG_PHASES)
+    unsigned long long gdur_sum, gdur_max, gdur_spread;
 };
 
 __device__ __forceinline__ uint32_t rr_hash(uint32_t v, uint32_t bits) { return (v * 0x9E3779B1u) >> (32 - bits); }
 
-// batch hash: v picked at turn tau by group g
-__device__ __forceinline__ void rr_insert(RRLds& L, uint32_t v, uint32_t tau, uint32_t g) {
+// batch hash: v picked at turn tau.  A slot keeps the earliest turn; every insert that meets
+// another turn in its slot offers the later of the two to L.conf, so that after the scan
+// L.conf = min over slots of the second-earliest turn = the first pick that shares a variable
+// with a pick of an earlier turn (the batch is exact below it).  A clause that repeats a
+// variable meets its own turn, which is no conflict.
+__device__ __forceinline__ void rr_insert(RRLds& L, uint32_t v, uint32_t tau) {
     uint32_t h = rr_hash(v, RR_HBITS);
     while (true) {
         const uint32_t k = atomicCAS(&L.hkey[h], RR_EMPTY, v);
         if (k == RR_EMPTY || k == v) {
-            atomicMin(&L.hmin[h], tau);
-            atomicOr(&L.hgrp[h], 1ull << g);
+            const uint32_t old = atomicMin(&L.hmin[h], tau);
+            if (old != RR_EMPTY && old != tau) atomicMin(&L.conf, old > tau ? old : tau);
             return;
         }
         h = (h + 1) & (RR_HASH - 1);
     }
 }
 
-// did group g pick a clause with variable v in this batch?  (The group's own inserts precede
-// this lookup in its wave's LDS order; slots never empty within a batch.)
-__device__ __forceinline__ bool rr_own(const RRLds& L, uint32_t v, uint32_t g) {
+// did group g pick a clause with variable v in this batch?  The slot's earliest turn is g's
+// (turn = level * B + g).  When another group's earlier turn holds the slot instead, g's own
+// pick of v conflicts with it and every later turn of g lies beyond the batch's exact prefix,
+// so the answer no longer matters.  (g's own inserts precede this lookup in its wave's LDS
+// order, so a slot g filled is never seen without its turn; slots never empty within a batch.)
+__device__ __forceinline__ bool rr_turn_is(uint32_t m, uint32_t B, uint32_t g) {
+    return m != RR_EMPTY && m % B == g;
+}
+
+__device__ __forceinline__ bool rr_own(const RRLds& L, uint32_t v, uint32_t B, uint32_t g) {
     uint32_t h = rr_hash(v, RR_HBITS);
     while (true) {
         const uint32_t k = L.hkey[h];
-        if (k == v) return (L.hgrp[h] >> g) & 1ull;
+        if (k == v) return rr_turn_is(L.hmin[h], B, g);
         if (k == RR_EMPTY) return false;
         h = (h + 1) & (RR_HASH - 1);
     }
@@ -2759,7 +2770,8 @@ __device__ __forceinline__ bool rr_own(const RRLds& L, uint32_t v, uint32_t g) {
 // does group g own any of the variables rv[0..n) (n <= KR) in the batch hash?  The probes
 // of the variables run interleaved so that their LDS latencies overlap.
 template <uint32_t KR>
-__device__ __forceinline__ bool rr_own_any(const RRLds& L, const uint32_t (&rv)[KR], uint32_t n, uint32_t g) {
+__device__ __forceinline__ bool rr_own_any(const RRLds& L, const uint32_t (&rv)[KR], uint32_t n, uint32_t B,
+                                           uint32_t g) {
     uint32_t h[KR];
     uint32_t act = 0;
 #pragma unroll
@@ -2774,7 +2786,7 @@ __device__ __forceinline__ bool rr_own_any(const RRLds& L, const uint32_t (&rv)[
             if (!((act >> j) & 1u)) continue;
             const uint32_t k = L.hkey[h[j]];
             if (k == rv[j]) {
-                own |= (L.hgrp[h[j]] >> g) & 1ull;
+                own |= rr_turn_is(L.hmin[h[j]], B, g);
                 act &= ~(1u << j);
             } else if (k == RR_EMPTY) {
                 act &= ~(1u << j);
@@ -2910,8 +2922,10 @@ __global__ __launch_bounds__(RR_THREADS) void k_rr_mis(ClauseView cv, LoopBuffer
     const uint32_t lane = tid & 63;
     const uint32_t T = b.rr_T;
     const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
+    const auto rsC = __builtin_amdgcn_make_buffer_rsrc(b.cover, (short)0, (int)b.n_vars, 0x00020000);
     const bool prof = b.kdbg != nullptr;  // diagnostics: phase times of thread 0
     unsigned long long tp0 = prof ? wall_now() : 0, tacc[4] = {0, 0, 0, 0};
+    unsigned long long gacc[4] = {0, 0, 0, 0};  // diagnostics, group 0 lane 0: loads, steps, rounds, scans
 
     const uint32_t nu = (uint32_t)st->u_total;  // entries written by k_rr_entries
     // ---- sets: [lower_bound(start q), lower_bound(start q+1)) of U
@@ -2930,8 +2944,11 @@ __global__ __launch_bounds__(RR_THREADS) void k_rr_mis(ClauseView cv, LoopBuffer
         L.end[q] = bnd[1];
         L.live[q] = (uint16_t)q;
     }
-    if (tid == 0) { L.n_live = T; L.t = 0; L.tm = 0; L.wide = 0; L.n_steps = 0; L.n_rounds = 0; }
-    for (uint32_t i = tid; i < RR_HASH; i += RR_THREADS) { L.hkey[i] = RR_EMPTY; L.hmin[i] = RR_EMPTY; L.hgrp[i] = 0; }
+    if (tid == 0) {
+        L.n_live = T; L.t = 0; L.tm = 0; L.wide = 0; L.n_steps = 0; L.n_rounds = 0; L.conf = RR_EMPTY;
+        L.gdur_sum = 0; L.gdur_max = 0; L.gdur_spread = 0;
+    }
+    for (uint32_t i = tid; i < RR_HASH; i += RR_THREADS) { L.hkey[i] = RR_EMPTY; L.hmin[i] = RR_EMPTY; }
     __syncthreads();
 
     uint32_t batches = 0;
@@ -2966,7 +2983,10 @@ __global__ __launch_bounds__(RR_THREADS) void k_rr_mis(ClauseView cv, LoopBuffer
                 uint32_t nc = 0, nv = 0, scan_end = pos, exhausted = 0, n_steps = 0, n_rounds = 0;
                 const uint32_t cb = g * cpg;
                 bool stop = false;
+                const bool gprof = prof && tid == 0;
+                const unsigned long long gstart = prof ? wall_now() : 0;
                 for (uint32_t round = 0; round < RR_ROUNDS && !stop; ++round) {
+                    unsigned long long gt0 = gprof ? wall_now() : 0;
                     // loads of ST steps: clause, width, variables, covered test
                     uint32_t c[ST], lb[ST], w[ST], rv[ST][KR];
                     bool alive[ST];
@@ -2982,16 +3002,30 @@ __global__ __launch_bounds__(RR_THREADS) void k_rr_mis(ClauseView cv, LoopBuffer
 #pragma unroll
                         for (uint32_t j = 0; j < KR; ++j) rv[u][j] = ev[j];
                     }
+                    // cover stamps of all ST steps by write-through (sc1) buffer loads, issued
+                    // together: they see the previous batches' commits (unlike atomic loads they
+                    // are not ordered among themselves); RR_EMPTY past a clause's width is out of
+                    // range and reads 0
+                    uint32_t cs[ST][KR];
+#pragma unroll
+                    for (uint32_t u = 0; u < ST; ++u)
+#pragma unroll
+                        for (uint32_t j = 0; j < KR; ++j) cs[u][j] = __builtin_amdgcn_raw_buffer_load_b8(rsC, rv[u][j], 0, 16);
 #pragma unroll
                     for (uint32_t u = 0; u < ST; ++u) {
 #pragma unroll
-                        for (uint32_t j = 0; j < KR; ++j)
-                            if (j < w[u])
-                                alive[u] &= __hip_atomic_load(&b.cover[rv[u][j]], __ATOMIC_RELAXED,
-                                                              __HIP_MEMORY_SCOPE_AGENT) != stamp;
+                        for (uint32_t j = 0; j < KR; ++j) alive[u] &= cs[u][j] != stamp;
+                    }
+#pragma unroll
+                    for (uint32_t u = 0; u < ST; ++u)
                         for (uint32_t j = KR; j < w[u]; ++j)
-                            alive[u] &= __hip_atomic_load(&b.cover[lit_var(cv.lits[lb[u] + j])], __ATOMIC_RELAXED,
-                                                          __HIP_MEMORY_SCOPE_AGENT) != stamp;
+                            alive[u] &= __builtin_amdgcn_raw_buffer_load_b8(rsC, lit_var(cv.lits[lb[u] + j]), 0, 16) != stamp;
+                    if (gprof) {
+                        __builtin_amdgcn_s_waitcnt(0);
+                        const unsigned long long gt1 = wall_now();
+                        gacc[0] += gt1 - gt0;
+                        gt0 = gt1;
+                        ++gacc[2];
                     }
 #pragma unroll
                     for (uint32_t u = 0; u < ST; ++u) {
@@ -3005,9 +3039,9 @@ __global__ __launch_bounds__(RR_THREADS) void k_rr_mis(ClauseView cv, LoopBuffer
                         };
                         // erased by an earlier pick of this group in the batch
                         if (al && nc) {
-                            al = !rr_own_any(L, rv[u], w[u] < KR ? w[u] : KR, g);
+                            al = !rr_own_any(L, rv[u], w[u] < KR ? w[u] : KR, B, g);
                             for (uint32_t j = KR; al && j < w[u]; ++j)
-                                if (rr_own(L, var_of(j), g)) al = false;
+                                if (rr_own(L, var_of(j), B, g)) al = false;
                         }
                         uint64_t und = (__ballot(al) >> gshift) & gmask;
                         if (!und) continue;
@@ -3100,7 +3134,7 @@ __global__ __launch_bounds__(RR_THREADS) void k_rr_mis(ClauseView cv, LoopBuffer
                             const uint32_t idx = nc + rank, tau = idx * B + g;
                             L.cc[cb + idx] = c[u];
                             L.cpos[cb + idx] = i;
-                            for (uint32_t j = 0; j < w[u]; ++j) rr_insert(L, var_of(j), tau, g);
+                            for (uint32_t j = 0; j < w[u]; ++j) rr_insert(L, var_of(j), tau);
                         }
                         const uint32_t np = (uint32_t)__popcll(pm);
                         if (np) {
@@ -3130,47 +3164,44 @@ __global__ __launch_bounds__(RR_THREADS) void k_rr_mis(ClauseView cv, LoopBuffer
                         }
                     }
                     if (!stop) { pos += ST * GS; scan_end = pos; }
+                    if (gprof) gacc[1] += wall_now() - gt0;
                 }
+                if (gprof) ++gacc[3];
                 if (!stop && pos >= end) { exhausted = 1; scan_end = end; }
                 if (gl == 0) {
                     L.ncand[g] = nc;
                     L.scan_end[g] = scan_end;
                     L.exh[g] = exhausted;
-                    if (prof) { atomicAdd(&L.n_steps, n_steps); atomicAdd(&L.n_rounds, n_rounds); }
+                    if (prof) {
+                        atomicAdd(&L.n_steps, n_steps); atomicAdd(&L.n_rounds, n_rounds);
+                        const unsigned long long gd = wall_now() - gstart;
+                        atomicAdd(&L.gdur_sum, gd); atomicMax(&L.gdur_spread, gd);
+                    }
                 }
             }
         }
-        if (tid == 0) L.trunc = L.wide ? 1u : D * B;
         __syncthreads();
-        if (prof) { const unsigned long long t1 = wall_now(); tacc[1] += t1 - tp0; tp0 = t1; }
-        // ---- the first turn a group did not decide, and the first pick that shares a variable
-        // with a pick of an earlier turn
+        if (prof) {
+            const unsigned long long t1 = wall_now();
+            tacc[1] += t1 - tp0;
+            tp0 = t1;
+            if (tid == 0) { L.gdur_max += L.gdur_spread; L.gdur_spread = 0; }
+        }
+        // ---- the batch is exact below the first turn a group did not decide and the first
+        // pick that shares a variable with a pick of an earlier turn (L.conf, from the inserts)
         if (tid < B) {
             const uint32_t nc = L.ncand[tid];
-            if (nc < D) atomicMin(&L.trunc, nc * B + tid);
-        }
-        for (uint32_t e = tid; e < B * cpg; e += RR_THREADS) {
-            const uint32_t g = e / cpg, l = e - g * cpg;
-            if (l >= L.ncand[g] || (L.wide && e == 0)) continue;
-            const uint32_t tau = l * B + g, c = L.cc[e], lb = cv.offs[c], w = cv.offs[c + 1] - lb;
-            for (uint32_t j = 0; j < w; ++j) {
-                const uint32_t v = lit_var(cv.lits[lb + j]);
-                uint32_t h = rr_hash(v, RR_HBITS);
-                while (L.hkey[h] != v) h = (h + 1) & (RR_HASH - 1);
-                if (L.hmin[h] < tau) { atomicMin(&L.trunc, tau); break; }
-            }
+            if (nc < D) atomicMin(&L.conf, nc * B + tid);
         }
         __syncthreads();
         if (prof) { const unsigned long long t1 = wall_now(); tacc[2] += t1 - tp0; tp0 = t1; }
-        const uint32_t trunc = L.trunc;
+        const uint32_t trunc = L.wide ? 1u : min(D * B, L.conf);  // (L.conf is reset after the next barrier)
         // ---- commit turns < trunc: covers, MIS, statistics; reset the batch hash
         for (uint32_t i = tid; i < RR_HASH; i += RR_THREADS) {
             const uint32_t k = L.hkey[i];
-            if (k != RR_EMPTY && L.hmin[i] < trunc)
-                __hip_atomic_store(&b.cover[k], (uint8_t)stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (k != RR_EMPTY && L.hmin[i] < trunc) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)stamp, rsC, k, 0, 16);
             L.hkey[i] = RR_EMPTY;
             L.hmin[i] = RR_EMPTY;
-            L.hgrp[i] = 0;
         }
         if (L.wide) {
             const uint32_t c = L.cc[0], lb = cv.offs[c], w = cv.offs[c + 1] - lb;
@@ -3218,6 +3249,7 @@ __global__ __launch_bounds__(RR_THREADS) void k_rr_mis(ClauseView cv, LoopBuffer
         }
         if (tid == 0) {
             L.wide = 0;
+            L.conf = RR_EMPTY;
             if (erase) {
                 L.n_live = n_live - 1;
                 L.t = idx_e;  // t is not decremented: the next turn skips the moved-up set
@@ -3253,6 +3285,8 @@ __global__ __launch_bounds__(RR_THREADS) void k_rr_mis(ClauseView cv, LoopBuffer
             unsigned long long* d = b.kdbg + (uint64_t)3 * DBG_BLOCKS * DBG_FIELDS;
             d[0] = tacc[0]; d[1] = tacc[1]; d[2] = tacc[2]; d[3] = tacc[3];
             d[4] = batches; d[5] = L.n_steps; d[6] = L.n_rounds; d[7] = L.tm;
+            d[8] = gacc[0]; d[9] = gacc[1]; d[10] = gacc[2]; d[11] = gacc[3];
+            d[12] = L.gdur_sum; d[13] = L.gdur_max;
         }
         if (batches > st->max_rounds) st->max_rounds = batches;
         if (b.ktime) time_slot(b, st->n_iter - 1)[3] = wall_now();

@@ -40,7 +40,10 @@ def main():
                 print(json.dumps({"T": T, "iter": it + 1, "prologue_us": us[0], "scan_us": us[1], "validate_us": us[2],
                                   "commit_us": us[3], "batches": int(d[4]), "scan_steps": int(d[5]),
                                   "greedy_rounds": int(d[6]), "picks": int(d[7]),
-                                  "us_per_batch": float(us[1:].sum() / max(1, d[4]))}), flush=True)
+                                  "us_per_batch": float(us[1:].sum() / max(1, d[4])),
+                                  "group0": {"load_us": d[8] / (khz.value / 1e3), "steps_us": d[9] / (khz.value / 1e3),
+                                             "rounds": int(d[10]), "scans": int(d[11])},
+                                  "group_scan_us_sum": d[12] / (khz.value / 1e3), "group_scan_us_max_sum": d[13] / (khz.value / 1e3)}), flush=True)
 
 
 if __name__ == "__main__":

@@ -130,6 +130,9 @@ struct LoopBuffers {
     uint32_t* left;         // compact list of undecided entries handed to the tail kernel
     uint32_t* tmis;         // MIS clauses decided by the tail kernel
     unsigned long long* owner; // n_vars 64-bit owner keys (epoch-tagged, never reset)
+    uint64_t owner_alt;        // 0: one owner array for every epoch; else the offset (in keys) of
+                               // a second array that odd epochs use (the fused JOIN(r)+CLAIM(r+1)
+                               // rounds read round r's keys while claiming round r+1's)
     uint8_t* cover;         // per variable: stamp of the iteration whose MIS covers it (the
                             // reduce clears it when the stamp cycles back to 1)
     unsigned long long* tile_stats; // per tile: [2t] sum |MIS|, [2t+1] sum resampled literals
@@ -205,6 +208,12 @@ hipError_t launch_lfmis_dd(const ClauseView& cv, const LoopBuffers& b, bool scat
 size_t dd_sort_lds(const LoopBuffers& b);
 size_t dd_sort_general_lds(const LoopBuffers& b);
 size_t dd_decide_lds(const LoopBuffers& b, uint32_t k);
+hipError_t launch_join_claim(const ClauseView& cv, const LoopBuffers& b, uint32_t r, const uint32_t* in, uint32_t* out,
+                             hipStream_t s);
+hipError_t launch_join_only(const ClauseView& cv, const LoopBuffers& b, uint32_t r, bool last, uint32_t wave_from,
+                            const uint32_t* in, uint32_t* out, hipStream_t s);
+hipError_t launch_claim_only(const ClauseView& cv, const LoopBuffers& b, uint32_t r, uint32_t wave_from,
+                             const uint32_t* in, uint32_t* out, hipStream_t s);
 hipError_t launch_tail(const ClauseView& cv, const LoopBuffers& b, uint32_t first_round,
                        hipStream_t s);
 hipError_t launch_rr_mis(const ClauseView& cv, const LoopBuffers& b, hipStream_t s);

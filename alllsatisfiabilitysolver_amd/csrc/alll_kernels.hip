@@ -969,10 +969,12 @@ struct HotTable {
     }
 };
 
-// One owner array for every epoch: JOIN(r) and CLAIM(r+1) are separated by a kernel boundary
-// (or, in the tail, a workgroup barrier), and keys of later epochs are always smaller.
-__device__ __forceinline__ unsigned long long* owner_of(const LoopBuffers& b, uint32_t /*epoch*/) {
-    return b.owner;
+// One owner array for every epoch when JOIN(r) and CLAIM(r+1) are separated by a kernel
+// boundary (or, in the tail, a workgroup barrier): keys of later epochs are always smaller.
+// With the fused JOIN(r)+CLAIM(r+1) rounds (k_wjc) odd epochs use a second array, so that
+// round r's keys stay readable while round r+1 claims.
+__device__ __forceinline__ unsigned long long* owner_of(const LoopBuffers& b, uint32_t epoch) {
+    return b.owner + ((epoch & 1u) ? b.owner_alt : 0ull);
 }
 
 template <int K>
@@ -1278,6 +1280,126 @@ __global__ __launch_bounds__(ROUND_THREADS) void k_wjoin(ClauseView cv, LoopBuff
             b.tile_stats[2 * tile] += w;
             b.tile_stats[2 * tile + 1] += lits;
         }
+    }
+}
+
+// JOIN(r) and CLAIM(r+1) in one launch (fixed k, clause-order keys, two owner arrays), a wave
+// per tile.  A clause that holds all its variables joins, as in k_wjoin.  A clause that lost a
+// variable v cannot wait for a boundary to learn whether it was killed in round r, so it
+// decides that itself: the only round-r joiner that can cover one of its variables is that
+// variable's round-r owner d (a joiner held every variable it covers, and the clause claimed v
+// too), and d joined iff it holds all of its own variables -- d's literals (AoS, clause order)
+// and their owner keys, read from round r's array while the survivors' round r+1 claims go to
+// the other one.  Joins of earlier rounds were excluded by the kill tests before round r.
+// Decisions equal JOIN(r) + CLAIM(r+1); one launch and one boundary fewer per round.
+template <int K>
+__global__ __launch_bounds__(ROUND_THREADS) void k_wjc(ClauseView cv, LoopBuffers b, uint32_t r,
+                                                       const uint32_t* in, uint32_t* out) {
+    DevState* st = b.state;
+    constexpr int S = Ent<K>::S;
+    const uint32_t tile = wave_tile();
+    const int lane = threadIdx.x & 63;
+    const bool tv = tile < b.n_tiles;
+    const uint32_t* lin = in + (uint64_t)(tv ? tile : 0u) * TILE * S;
+    // loop state, counts and the first 64 entries (speculatively) in one round trip (k_wclaim)
+    Ent<K> e0;
+    load_ent<K>(e0, lin + (uint64_t)lane * S);
+    const uint32_t cnt0 = b.tile_cnt[tv ? tile : 0u], mc0 = b.mis_cnt[tv ? tile : 0u];
+    const uint32_t active = st->active, stamp = st->stamp, rbase = st->round_base;
+    spec_fence();
+    if (!active) return;
+    const bool hot = cv.n_hot != 0;
+    __shared__ uint32_t s_hk[HOT_SLOTS];
+    __shared__ unsigned long long s_hv[HOT_SLOTS];
+    HotTable ht{s_hk, s_hv};
+    if (hot) {
+        ht.init();
+        __syncthreads();
+    }
+    const uint32_t cnt = tv ? __builtin_amdgcn_readfirstlane(cnt0) : 0u;
+    if (cnt == 0 && !hot) return;
+    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+    const unsigned long long keyr = (unsigned long long)(~(rbase + r)) << 32;
+    const unsigned long long keyn = (unsigned long long)(~(rbase + r + 1)) << 32;
+    const unsigned long long* own_r = owner_of(b, rbase + r);
+    unsigned long long* own_n = owner_of(b, rbase + r + 1);
+    uint32_t* lout = out + (uint64_t)(tv ? tile : 0u) * TILE * S;
+    const uint32_t m0 = __builtin_amdgcn_readfirstlane(mc0);
+    uint32_t* mis = b.mis + (uint64_t)(tv ? tile : 0u) * TILE + m0;
+    uint32_t kept = 0, joined = 0;
+    unsigned long long lits = 0, w = 0;
+    for (uint32_t i0 = 0; i0 < cnt; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        Ent<K> e;
+        bool join = false, keep = false;
+        if (i < cnt) {
+            if (i0 == 0) e = e0;
+            else load_ent<K>(e, lin + (uint64_t)i * S);
+            const unsigned long long mine = keyr | e.w[0];
+            unsigned long long o[K];
+#pragma unroll
+            for (int j = 0; j < K; ++j) o[j] = own_r[vmix(b, lit_var(e.w[1 + j]))];
+            join = true;
+#pragma unroll
+            for (int j = 0; j < K; ++j) join &= o[j] == mine;
+            if (join) {
+#pragma unroll
+                for (int j = 0; j < K; ++j) b.cover[lit_var(e.w[1 + j])] = (uint8_t)stamp;
+                lits += K;
+                w += 1;
+            } else {
+                // the owners of the lost variables: did one of them join in round r?
+                uint32_t dl[K][K];
+#pragma unroll
+                for (int j = 0; j < K; ++j) {
+                    const bool lost = o[j] != mine;
+#pragma unroll
+                    for (int q = 0; q < K; ++q)
+                        dl[j][q] = lost ? cv.lits[(uint64_t)(uint32_t)o[j] * K + q] : 0u;
+                }
+                bool killed = false;
+#pragma unroll
+                for (int j = 0; j < K; ++j) {
+                    if (o[j] == mine) continue;
+                    bool dj = true;
+#pragma unroll
+                    for (int q = 0; q < K; ++q) dj &= own_r[vmix(b, lit_var(dl[j][q]))] == o[j];
+                    killed |= dj;
+                }
+                if (!killed) {
+                    const unsigned long long kn = keyn | e.w[0];
+#pragma unroll
+                    for (int j = 0; j < K; ++j) {
+                        const uint32_t raw = e.w[1 + j];
+                        if (hot && (raw & LIT_HOT)) ht.claim(lit_var(raw), kn);
+                        else __hip_atomic_fetch_min(&own_n[vmix(b, lit_var(raw))], kn, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                    keep = true;
+                }
+            }
+        }
+        const uint64_t jm = __ballot(join), km = __ballot(keep);
+        if (join) mis[joined + __popcll(jm & lt)] = e.w[0];
+        if (keep) store_ent<K>(lout + (uint64_t)(kept + __popcll(km & lt)) * S, e);
+        joined += (uint32_t)__popcll(jm);
+        kept += (uint32_t)__popcll(km);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        lits += __shfl_down(lits, o, 64);
+        w += __shfl_down(w, o, 64);
+    }
+    if (lane == 0 && cnt) {
+        b.tile_cnt[tile] = kept;
+        b.mis_cnt[tile] = m0 + joined;
+        if (joined) {  // (the wave owns the tile: no other writer in this kernel)
+            b.tile_stats[2 * tile] += w;
+            b.tile_stats[2 * tile + 1] += lits;
+        }
+    }
+    if (hot) {
+        __syncthreads();
+        ht.flush(own_n, b);
     }
 }
 
@@ -3424,6 +3546,40 @@ hipError_t launch_round(const ClauseView& cv, const LoopBuffers& b, uint32_t r, 
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     ALLL_DISPATCH_K(cv.k, (k_join<K><<<b.n_tiles, JOIN_THREADS, 0, s>>>(cv, b, r, s0, s1, l)));
+    return hipGetLastError();
+}
+
+hipError_t launch_claim_only(const ClauseView& cv, const LoopBuffers& b, uint32_t r, uint32_t wave_from,
+                             const uint32_t* in, uint32_t* out, hipStream_t s) {
+    if (b.n_tiles == 0) return hipSuccess;
+    if (r >= wave_from) {
+        const uint32_t grid = (b.n_tiles + ROUND_THREADS / 64 - 1) / (ROUND_THREADS / 64);
+        ALLL_DISPATCH_K(cv.k, (k_wclaim<K><<<grid, ROUND_THREADS, 0, s>>>(cv, b, r, in, out)));
+    } else {
+        ALLL_DISPATCH_K(cv.k, (k_claim<K><<<b.n_tiles, ROUND_THREADS, 0, s>>>(cv, b, r, const_cast<uint32_t*>(in), out)));
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_join_only(const ClauseView& cv, const LoopBuffers& b, uint32_t r, bool last, uint32_t wave_from,
+                            const uint32_t* in, uint32_t* out, hipStream_t s) {
+    if (b.n_tiles == 0) return hipSuccess;
+    const int l = last ? 1 : 0;
+    if (r >= wave_from) {
+        const uint32_t grid = (b.n_tiles + ROUND_THREADS / 64 - 1) / (ROUND_THREADS / 64);
+        ALLL_DISPATCH_K(cv.k, (k_wjoin<K><<<grid, ROUND_THREADS, 0, s>>>(cv, b, r, in, out, l)));
+    } else {
+        ALLL_DISPATCH_K(cv.k, (k_join<K><<<b.n_tiles, JOIN_THREADS, 0, s>>>(cv, b, r, in, out, l)));
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_join_claim(const ClauseView& cv, const LoopBuffers& b, uint32_t r, const uint32_t* in, uint32_t* out,
+                             hipStream_t s) {
+    if (b.n_tiles == 0) return hipSuccess;
+    if (cv.k == 0 || cv.k > (uint32_t)MAX_FIXED_K || !b.owner_alt) return hipErrorInvalidValue;
+    const uint32_t grid = (b.n_tiles + ROUND_THREADS / 64 - 1) / (ROUND_THREADS / 64);
+    ALLL_DISPATCH_K(cv.k, (k_wjc<(K > 0 ? K : 1)><<<grid, ROUND_THREADS, 0, s>>>(cv, b, r, in, out)));
     return hipGetLastError();
 }
 

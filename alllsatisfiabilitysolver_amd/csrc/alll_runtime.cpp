@@ -76,6 +76,9 @@ struct alll_ctx {
     uint32_t tiles_per_rank = 0, own_begin = 0, own_end = 0, n_tiles_padded = 0;
     uint32_t grid_rounds = DEFAULT_GRID_ROUNDS;
     bool fuse_reduce = true;     // env ALLL_FUSE_REDUCE=0: separate k_reduce (tests, A/B)
+    uint32_t fuse_jc = 0;        // env ALLL_FUSE_JC=f >= 1 (fixed k): JOIN(r) + CLAIM(r+1) in one launch
+                                 // for f <= r < G - 1 (k_wjc, two owner arrays); measured no faster
+                                 // (DESIGN.md §7.1), so off by default
     // env ALLL_FUSE_SCATTER=1: the evaluation workgroups scatter their runs themselves (no
     // k_bscatter launch; +2.6% iterations/s at M, but the evaluation kernel's duration then
     // includes the scatter, so its roofline is no longer the evaluation's: off by default)
@@ -395,10 +398,23 @@ int enqueue_iteration(alll_ctx* c, hipEvent_t* marks, int variant) {
         HIP_TRY(launch_lfmis_dd(c->cv, c->b, scatter, fused, s));
     } else {
         const uint32_t rounds = variant == 2 ? 1u : c->grid_rounds;
-        for (uint32_t r = 0; r < rounds; ++r) {
+        // rounds [0, f) as separate CLAIM / JOIN launches, then (f + 2 <= G) CLAIM(f), JOIN(r) +
+        // CLAIM(r + 1) fused for f <= r < G - 1, and the last JOIN
+        const uint32_t f = c->fuse_jc && c->fuse_jc + 2 <= rounds ? c->fuse_jc : rounds;
+        for (uint32_t r = 0; r < f; ++r) {
             if (r == 0 && variant == 1)
                 HIP_TRY(launch_round0_buckets(c->cv, c->b, rounds == 1, fused, scatter, s));
             else HIP_TRY(launch_round(c->cv, c->b, r, r + 1 == rounds, c->wave_round_min, s));
+        }
+        if (f < rounds) {
+            // after JOIN(f-1) the list is in stage[1]: CLAIM(f) -> stage[0], then the fused rounds
+            // alternate between the two, and the last JOIN hands the survivors to the tail
+            uint32_t* st2[2] = {c->b.stage[0], c->b.stage[1]};
+            HIP_TRY(launch_claim_only(c->cv, c->b, f, c->wave_round_min, st2[1], st2[0], s));
+            uint32_t cur = 0;
+            for (uint32_t r = f; r + 1 < rounds; ++r, cur ^= 1u)
+                HIP_TRY(launch_join_claim(c->cv, c->b, r, st2[cur], st2[cur ^ 1u], s));
+            HIP_TRY(launch_join_only(c->cv, c->b, rounds - 1, true, c->wave_round_min, st2[cur], st2[cur ^ 1u], s));
         }
         HIP_TRY(launch_tail(c->cv, c->b, rounds, s));
     }
@@ -740,7 +756,10 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
         b.vmix_mul = 0x9E3779B1u;
         b.vmix_mask = (uint32_t)(vrange - 1);
     }
-    if ((rc = dalloc(c, &b.owner, (size_t)vrange, 0xFF))) return bail(rc);
+    if (const char* e = getenv("ALLL_FUSE_JC")) c->fuse_jc = (uint32_t)std::max(0, atoi(e));
+    if (fixed_k <= 0) c->fuse_jc = 0;
+    if ((rc = dalloc(c, &b.owner, (size_t)vrange * (c->fuse_jc ? 2 : 1), 0xFF))) return bail(rc);
+    b.owner_alt = c->fuse_jc ? vrange : 0;
     if ((rc = dalloc(c, &b.cover, (size_t)b.n_words * 32))) return bail(rc);  // whole words, zero-padded
     if ((rc = dalloc(c, &b.tile_stats, 2 * (size_t)n_tiles))) return bail(rc);
     if ((rc = dalloc(c, &b.delta, b.n_words))) return bail(rc);

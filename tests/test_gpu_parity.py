@@ -40,7 +40,10 @@ LAYOUTS = {"hybrid": (0, {}), "fixed": (1 << 3, {}), "csr": (1 << 2, {}), "atomi
            # the dependency-driven LFMIS (opt-in) instead of the round-synchronous one
            "dd": (0, {"ALLL_DD": "1"}),
            "dd_scatter": (0, {"ALLL_DD": "1", "ALLL_FUSE_SCATTER": "1"}),
-           "dd_no_senders": (0, {"ALLL_DD": "1", "ALLL_DD_SENDERS": "0"})}
+           "dd_no_senders": (0, {"ALLL_DD": "1", "ALLL_DD_SENDERS": "0"}),
+           # JOIN(r) and CLAIM(r+1) fused in one launch (k_wjc, opt-in) from round 1 / round 2 on
+           "fuse_jc": (0, {"ALLL_FUSE_JC": "1"}),
+           "fuse_jc2_atomic": (1 << 5, {"ALLL_FUSE_JC": "2"})}
 
 
 def make_solver(layout, monkeypatch, *args, **kw):
@@ -255,16 +258,19 @@ def test_empty_instance(gpu):
         assert st["solved"] == 1 and st["n_iterations"] == 1 and st["n_resamples"] == 0
 
 
+@pytest.mark.parametrize("fuse_jc", ["0", "1", "2"])
 @pytest.mark.parametrize("grid_rounds", [1, 2, 3, 8])
-def test_grid_round_split_is_invisible(gpu, oracle_mod, grid_rounds, monkeypatch):
+def test_grid_round_split_is_invisible(gpu, oracle_mod, grid_rounds, fuse_jc, monkeypatch):
     """The split between full-grid LFMIS rounds and the single-workgroup tail changes
-    nothing: same trajectory as the oracle."""
+    nothing, and neither do the fused JOIN(r)+CLAIM(r+1) launches (ALLL_FUSE_JC=f: from round
+    f on): same trajectory as the oracle."""
     from alllsatisfiabilitysolver_amd import Solver
 
     n, offs, lits = instances()["k5_multi_tile"]
     st_o, A_o, rows = oracle_mod.solve(n, offs, lits, 77, max_iters=12, trace=True)
     monkeypatch.setenv("ALLL_BUCKET_MIN_U", "0")  # round 0 bucketed (incl. last-round hand-off at G=1)
     monkeypatch.setenv("ALLL_DD", "0")  # (the grid rounds exist only in the round-synchronous LFMIS)
+    monkeypatch.setenv("ALLL_FUSE_JC", fuse_jc)
     with Solver(n, offs, lits, seed=77, max_iters=12, grid_rounds=grid_rounds) as s:
         st = s.solve()
         assert st["n_resamples"] == st_o["n_resamples"]

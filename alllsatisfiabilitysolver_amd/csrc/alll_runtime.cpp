@@ -706,6 +706,8 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     b.n_words = (c->n_vars + 31) / 32;
     if (const char* e = getenv("ALLL_EVAL_WGS")) c->eval_wgs = std::max(1, std::min(2, atoi(e)));  // tuning
     b.win_words = LDS_WORDS / c->eval_wgs / 4 * 4;
+    if (const char* e = getenv("ALLL_WIN_WORDS"))  // tests: small windows on small instances
+        b.win_words = std::max<uint32_t>(16, std::min<uint32_t>(b.win_words, (uint32_t)std::max(0, atoi(e)))) / 8 * 8;
     b.n_cu = (uint32_t)c->n_cu;
     b.n_tiles = n_tiles;
     b.m = m;

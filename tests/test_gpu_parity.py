@@ -43,7 +43,11 @@ LAYOUTS = {"hybrid": (0, {}), "fixed": (1 << 3, {}), "csr": (1 << 2, {}), "atomi
            "dd_no_senders": (0, {"ALLL_DD": "1", "ALLL_DD_SENDERS": "0"}),
            # JOIN(r) and CLAIM(r+1) fused in one launch (k_wjc, opt-in) from round 1 / round 2 on
            "fuse_jc": (0, {"ALLL_FUSE_JC": "1"}),
-           "fuse_jc2_atomic": (1 << 5, {"ALLL_FUSE_JC": "2"})}
+           "fuse_jc2_atomic": (1 << 5, {"ALLL_FUSE_JC": "2"}),
+           # many small LDS windows (64 words: 2048 variables; the C4 layout on small instances),
+           # with the cached and with the non-temporal (C4) evaluation
+           "small_windows": (0, {"ALLL_EVAL_WINDOWS": "1", "ALLL_WIN_WORDS": "64"}),
+           "small_windows_nt": (0, {"ALLL_EVAL_WINDOWS": "1", "ALLL_WIN_WORDS": "64", "ALLL_EVAL_NT": "1"})}
 
 
 def make_solver(layout, monkeypatch, *args, **kw):

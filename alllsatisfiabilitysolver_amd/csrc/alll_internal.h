@@ -55,6 +55,8 @@ constexpr int DDD_THREADS = 1024;        // k_decide workgroup (one per CU)
 constexpr uint32_t DD_TIMEOUT = 10000000u;  // k_decide gives up after 100 ms (100 MHz wall clock)
 // Round-robin MIS of T > 1 clause chunks (the reference's n_threads > 1): at most RR_TMAX sets.
 constexpr uint32_t RR_TMAX = 2048;
+constexpr uint32_t RR_MW_GH = 1u << 15;  // k_rr_mw global hash slots
+constexpr uint32_t RR_MW_CTL_WORDS = 1024; // k_rr_mw control block (words)
 // In-loop kernel timing (ALLL_FLAG_KERNEL_TIMING): per iteration i, slot i % TIME_SLOTS holds
 // device wall-clock stamps (s_memrealtime) {eval start (min over workgroups), eval end (max),
 // reduce start, LFMIS tail end}.
@@ -175,6 +177,14 @@ struct LoopBuffers {
     const uint32_t* rr_sets;    // rr_T + 1 chunk starts (clause ids)
     uint32_t rr_T;
     uint32_t rr_k;              // common clause width (<= 8), 0 = ragged
+    // multi-workgroup round robin (k_rr_mw): control words, global batch hash (keys = variable
+    // + 1, 0 empty; minima = earliest turn, ~0 empty), per-set scan pointers and ends
+    uint32_t* rr_ctl;
+    uint32_t* rr_gkey;
+    uint32_t* rr_gmin;
+    uint32_t* rr_ptr;
+    uint32_t* rr_end;
+    uint32_t rr_mw;             // workgroups of k_rr_mw (0: the one-workgroup k_rr_mis)
     uint32_t n_vars;
     uint32_t n_words;
     uint32_t n_tiles;       // tiles covering [0, m)

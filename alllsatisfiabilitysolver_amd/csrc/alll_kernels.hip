@@ -2988,6 +2988,7 @@ static_assert(sizeof(RREnt) == 16 + 4 * RR_KE, "scan entry = header + RR_KE vari
 __global__ __launch_bounds__(256) void k_rr_entries(ClauseView cv, LoopBuffers b) {
     if (!b.state->active) return;
     const uint32_t tile = blockIdx.x, tid = threadIdx.x;
+    if (tile == 0 && tid < 2 && b.rr_ctl) b.rr_ctl[tid] = 0u;  // k_rr_mw: barrier counter, MIS count
     __shared__ uint32_t s_part[4], s_wpre[TILE_WORDS + 1];
     __shared__ uint32_t s_ids[TILE];
     uint32_t acc = 0;
@@ -3416,6 +3417,514 @@ __global__ __launch_bounds__(RR_THREADS) void k_rr_mis(ClauseView cv, LoopBuffer
 }
 
 // ------------------------------------------------------------------------------------
+// Round-robin MIS across workgroups (k_rr_mw): the batches of k_rr_mis with every lane group in
+// a workgroup of its own (one wave, one CU), so that the groups' scan steps -- chains of
+// dependent LDS hash operations -- no longer share one CU.  What the groups shared in LDS moves
+// to global memory:
+//   * the test "did my group pick this variable?" needs only the group's own picks: an LDS hash
+//     per workgroup (exact, no turn arithmetic);
+//   * the first conflicting turn comes from a global hash (variable -> earliest turn) that every
+//     group fills with its picks after its scan (interleaved CAS / min, one pass), each insert
+//     that meets another turn offering the later one to an epoch-tagged maximum of ~turn;
+//   * ncand / scan_end / exh per group, set pointers, the MIS count: global words.
+// Two grid barriers per batch (a monotonic counter per iteration, zeroed by k_rr_entries; every
+// spin bounded by a device-clock timeout).  Every workgroup keeps the same replicated live-set
+// list and turn index and takes the same decisions from the same global words, so the batch
+// sequence, its exact prefix and the set erasures are those of k_rr_mis.
+constexpr uint32_t RR_MW_MAX = 64;        // workgroups (groups per batch)
+constexpr uint32_t RR_MW_VPG = 256;       // variables of a group's picks per batch
+constexpr uint32_t RR_MW_CPG = 128;       // picks of a group per batch
+constexpr uint32_t RR_MW_OWN = 1024;      // own-pick hash slots (keys)
+constexpr unsigned long long RR_MW_TIMEOUT = 20000000ull;  // 200 ms at 100 MHz
+
+struct RRMwCtl {  // (b.rr_ctl: RR_MW_CTL_WORDS words, zeroed at allocation)
+    uint32_t bar, tm, epoch, wide_ep;
+    uint32_t pad0[12];
+    unsigned long long conf;  // (ep << 32) | ~first conflicting turn, by atomicMax
+    unsigned long long pad1[7];
+    uint32_t ncand[RR_MW_MAX], scan_end[RR_MW_MAX], exh[RR_MW_MAX];
+};
+
+static_assert(sizeof(RRMwCtl) <= 4 * RR_MW_CTL_WORDS, "control block");
+struct RRMwLds {
+    uint32_t okey[RR_MW_OWN];
+    unsigned long long skey[512];
+    uint32_t cc[RR_MW_CPG], cpos[RR_MW_CPG];
+    // the variables of this group's picks in the batch (pick index, global hash slot)
+    uint32_t ivar[RR_MW_VPG], ipick[RR_MW_VPG], islot[RR_MW_VPG];
+    uint32_t nvar;
+    uint32_t end[RR_TMAX];
+    uint16_t live[RR_TMAX];
+    uint16_t moved[RR_TMAX];
+};
+
+__device__ __forceinline__ bool rr_mw_own(const RRMwLds& L, uint32_t v) {
+    uint32_t h = rr_hash(v, 10);
+    while (true) {
+        const uint32_t k = L.okey[h];
+        if (k == v) return true;
+        if (k == RR_EMPTY) return false;
+        h = (h + 1) & (RR_MW_OWN - 1);
+    }
+}
+
+template <uint32_t KR>
+__device__ __forceinline__ bool rr_mw_own_any(const RRMwLds& L, const uint32_t (&rv)[KR], uint32_t n) {
+    uint32_t h[KR];
+    uint32_t act = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < KR; ++j) {
+        h[j] = rr_hash(rv[j], 10);
+        if (j < n) act |= 1u << j;
+    }
+    bool own = false;
+    while (act && !own) {
+#pragma unroll
+        for (uint32_t j = 0; j < KR; ++j) {
+            if (!((act >> j) & 1u)) continue;
+            const uint32_t k = L.okey[h[j]];
+            if (k == rv[j]) { own = true; act &= ~(1u << j); }
+            else if (k == RR_EMPTY) act &= ~(1u << j);
+            else h[j] = (h[j] + 1) & (RR_MW_OWN - 1);
+        }
+    }
+    return own;
+}
+
+__device__ __forceinline__ void rr_mw_own_insert(RRMwLds& L, uint32_t v) {
+    uint32_t h = rr_hash(v, 10);
+    while (true) {
+        const uint32_t k = atomicCAS(&L.okey[h], RR_EMPTY, v);
+        if (k == RR_EMPTY || k == v) return;
+        h = (h + 1) & (RR_MW_OWN - 1);
+    }
+}
+
+// grid barrier number k over nw workgroups (one wave each); false after a timeout
+__device__ __forceinline__ bool rr_mw_barrier(RRMwCtl* ctl, uint32_t target) {
+    uint32_t ok = 1;
+    if ((threadIdx.x & 63) == 0) {
+        __threadfence();
+        atomicAdd(&ctl->bar, 1u);
+        const unsigned long long t0 = wall_now();
+        while (__hip_atomic_load(&ctl->bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            if (wall_now() - t0 > RR_MW_TIMEOUT) { ok = 0; break; }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        __threadfence();
+    }
+    return __shfl(ok, 0, 64) != 0;
+}
+
+template <uint32_t KR, uint32_t ST>
+__global__ __launch_bounds__(64) void k_rr_mw(ClauseView cv, LoopBuffers b) {
+    DevState* st = b.state;
+    if (!st->active) return;
+    extern __shared__ __align__(16) unsigned char rr_mw_lds_raw[];
+    RRMwLds& L = *reinterpret_cast<RRMwLds*>(rr_mw_lds_raw);
+    RRMwCtl* ctl = reinterpret_cast<RRMwCtl*>(b.rr_ctl);
+    uint32_t* gkey = b.rr_gkey;
+    uint32_t* gmin = b.rr_gmin;
+    uint32_t* gptr = b.rr_ptr;
+    const uint32_t stamp = st->stamp;
+    const uint32_t lane = threadIdx.x;
+    const uint32_t NW = gridDim.x, g = blockIdx.x;
+    const uint32_t T = b.rr_T;
+    const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
+    const auto rsC = __builtin_amdgcn_make_buffer_rsrc(b.cover, (short)0, (int)b.n_vars, 0x00020000);
+    const uint32_t nu = (uint32_t)st->u_total;
+    const uint32_t base = __hip_atomic_load(&ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t nbar = 0;
+    bool ok = true;
+    // diagnostics (ALLL_DEBUG_PHASES): workgroup 0's time in scan, hash inserts, first barrier,
+    // commit, second barrier
+    const bool prof = b.kdbg != nullptr && g == 0;
+    unsigned long long pacc[5] = {0, 0, 0, 0, 0}, pt = prof ? wall_now() : 0;
+    unsigned long long sacc[6] = {0, 0, 0, 0, 0, 0}, st0 = 0;  // scan detail: loads, own, greedy, picks, steps, overhead
+    auto sstamp = [&](int k) {
+        if (prof) { const unsigned long long t1 = wall_now(); sacc[k] += t1 - st0; st0 = t1; }
+    };
+    if (prof) {  // cost of one stamp pair
+        const unsigned long long a0 = wall_now(), a1 = wall_now();
+        sacc[5] = a1 - a0;
+    }
+    auto pstamp = [&](int k) {
+        if (prof) { const unsigned long long t1 = wall_now(); pacc[k] += t1 - pt; pt = t1; }
+    };
+    // ---- sets: [lower_bound(start q), lower_bound(start q+1)) of U, spread over the workgroups
+    for (uint32_t q = g * 64 + lane; q < T; q += NW * 64) {
+        uint32_t bnd[2];
+        for (int e = 0; e < 2; ++e) {
+            const uint32_t key = b.rr_sets[q + e];
+            uint32_t lo = 0, hi = nu;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (U[mid].a.x < key) lo = mid + 1; else hi = mid;
+            }
+            bnd[e] = lo;
+        }
+        __hip_atomic_store(&gptr[q], bnd[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&b.rr_end[q], bnd[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    for (uint32_t i = lane; i < RR_MW_OWN; i += 64) L.okey[i] = RR_EMPTY;
+    if (lane == 0) L.nvar = 0;
+    ok = rr_mw_barrier(ctl, ++nbar * NW);
+    for (uint32_t q = lane; q < T; q += 64) {
+        L.end[q] = __builtin_amdgcn_raw_buffer_load_b32(
+            __builtin_amdgcn_make_buffer_rsrc(b.rr_end, (short)0, (int)(T * 4u), 0x00020000), q * 4u, 0, 16);
+        L.live[q] = (uint16_t)q;
+    }
+    __syncthreads();
+    uint32_t n_live = T, t = 0, batches = 0;
+    const uint64_t below = (1ull << lane) - 1ull;
+    const uint32_t sbits = 9u, shs = 1u << sbits, wcap = shs / 2;
+    unsigned long long* sk = L.skey;
+    while (ok && n_live > 0) {
+        if (++batches > 2 * nu + 2 * T + 64) {
+            if (g == 0 && lane == 0) { st->error = 1; st->done = 3; }
+            break;
+        }
+        const uint32_t ep = base + batches;
+        const uint32_t B = n_live < NW ? n_live : NW;
+        const uint32_t D = (B == n_live) ? RR_MW_CPG : 1u;
+        const uint32_t vpg = RR_MW_VPG;
+        const uint32_t t0 = t;
+        uint32_t nc = 0;
+        bool wide = false;
+        if (g < B) {
+            // ---- scan: this group decides the next D turns of set live[(t + 1 + g) % n_live]
+            const uint32_t s = L.live[(t0 + 1 + g) % n_live];
+            uint32_t pos = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&gptr[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            const uint32_t end = L.end[s];
+            uint32_t nv = 0, scan_end = pos, exhausted = 0;
+            bool stop = false;
+            for (uint32_t round = 0; round < RR_ROUNDS && !stop; ++round) {
+                if (prof) st0 = wall_now();
+                uint32_t c[ST], lb[ST], w[ST], rv[ST][KR];
+                bool alive[ST];
+#pragma unroll
+                for (uint32_t u = 0; u < ST; ++u) {
+                    const uint32_t i = pos + u * 64 + lane;
+                    alive[u] = i < end;
+                    RREnt e;
+                    if (alive[u]) e = U[i];
+                    else { e.a = make_uint4(0u, 0u, 0u, 0u); e.v0 = e.v1 = make_uint4(RR_EMPTY, RR_EMPTY, RR_EMPTY, RR_EMPTY); }
+                    c[u] = e.a.x; lb[u] = e.a.y; w[u] = e.a.z;
+                    const uint32_t ev[8] = {e.v0.x, e.v0.y, e.v0.z, e.v0.w, e.v1.x, e.v1.y, e.v1.z, e.v1.w};
+#pragma unroll
+                    for (uint32_t j = 0; j < KR; ++j) rv[u][j] = ev[j];
+                }
+                uint32_t cs[ST][KR];
+#pragma unroll
+                for (uint32_t u = 0; u < ST; ++u)
+#pragma unroll
+                    for (uint32_t j = 0; j < KR; ++j) cs[u][j] = __builtin_amdgcn_raw_buffer_load_b8(rsC, rv[u][j], 0, 16);
+#pragma unroll
+                for (uint32_t u = 0; u < ST; ++u) {
+#pragma unroll
+                    for (uint32_t j = 0; j < KR; ++j) alive[u] &= cs[u][j] != stamp;
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < ST; ++u)
+                    for (uint32_t j = KR; j < w[u]; ++j)
+                        alive[u] &= __builtin_amdgcn_raw_buffer_load_b8(rsC, lit_var(cv.lits[lb[u] + j]), 0, 16) != stamp;
+                if (prof) {
+                    bool any = false;
+#pragma unroll
+                    for (uint32_t u = 0; u < ST; ++u) any |= alive[u];
+                    if (__ballot(any) == 0x123ull) sacc[5] += 1;  // (consumes the loads before the stamp)
+                    sstamp(0);
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < ST; ++u) {
+                    if (stop) break;
+                    const uint32_t pu = pos + u * 64;
+                    if (pu >= end) { exhausted = 1; scan_end = end; stop = true; break; }
+                    const uint32_t i = pu + lane;
+                    bool al = alive[u];
+                    auto var_of = [&](uint32_t j) -> uint32_t {
+                        return j < KR ? rv[u][j] : lit_var(cv.lits[lb[u] + j]);
+                    };
+                    if (al && nc) {  // erased by an earlier pick of this group in the batch
+                        al = !rr_mw_own_any(L, rv[u], w[u] < KR ? w[u] : KR);
+                        for (uint32_t j = KR; al && j < w[u]; ++j)
+                            if (rr_mw_own(L, var_of(j))) al = false;
+                    }
+                    uint64_t und = __ballot(al);
+                    sstamp(1);
+                    if (!und) continue;
+                    if (prof) sacc[4] += 1;
+                    // greedy (lane order) subset S of the live candidates (as k_rr_mis)
+                    uint64_t S = 0;
+                    while (und) {
+                        const bool me = (und >> lane) & 1ull;
+                        uint32_t wsum = me ? w[u] : 0u;
+                        if (b.rr_k) {
+                            wsum = me ? b.rr_k * ((uint32_t)__popcll(und & below) + 1u) : 0u;
+                        } else {
+                            for (uint32_t o = 1; o < 64; o <<= 1) {
+                                const uint32_t y = __shfl_up(wsum, o, 64);
+                                if (lane >= o) wsum += y;
+                            }
+                        }
+                        const bool inwin = me && wsum <= wcap;
+                        const uint32_t first = (uint32_t)__builtin_ctzll(und);
+                        bool win = false, dead = false;
+                        const bool wide_first = !((__ballot(inwin) >> first) & 1ull);
+                        uint64_t W;
+                        if (wide_first) {
+                            win = lane == first;
+                            const uint32_t lb0 = __shfl(lb[u], (int)first, 64);
+                            const uint32_t w0 = __shfl(w[u], (int)first, 64);
+                            for (uint32_t j0 = 0; j0 < w0; ++j0) {
+                                const uint32_t v0 = lit_var(cv.lits[lb0 + j0]);
+                                if (me && !win && !dead)
+                                    for (uint32_t j = 0; j < w[u]; ++j) dead |= var_of(j) == v0;
+                            }
+                            W = __ballot(win);
+                        } else {
+                            for (uint32_t q = lane; q < shs; q += 64) sk[q] = RR_EMPTY64;
+                            __builtin_amdgcn_wave_barrier();
+                            bool dup = false;
+                            if (inwin)
+                                for (uint32_t j = 0; j < w[u]; ++j) dup |= rr_step_insert(sk, sbits, var_of(j), lane);
+                            __builtin_amdgcn_wave_barrier();
+                            const uint64_t wm = __ballot(inwin);
+                            if (!__ballot(dup) && wm == und) {
+                                win = me;
+                                W = und;
+                            } else {
+                                uint32_t ml[KR];
+                                rr_step_lanes(sk, sbits, rv[u], me ? (w[u] < KR ? w[u] : KR) : 0u, ml);
+                                win = inwin;
+#pragma unroll
+                                for (uint32_t j = 0; j < KR; ++j) win &= j >= w[u] || ml[j] == lane;
+                                for (uint32_t j = KR; win && j < w[u]; ++j) win = rr_step_lane(sk, sbits, var_of(j)) == lane;
+                                W = __ballot(win);
+                                if (me && !win) {
+#pragma unroll
+                                    for (uint32_t j = 0; j < KR; ++j)
+                                        dead |= j < w[u] && ml[j] != RR_EMPTY && ((W >> ml[j]) & 1ull);
+                                    for (uint32_t j = KR; !dead && j < w[u]; ++j) {
+                                        const uint32_t q = rr_step_lane(sk, sbits, var_of(j));
+                                        dead = q != RR_EMPTY && ((W >> q) & 1ull);
+                                    }
+                                }
+                            }
+                        }
+                        const uint64_t Dm = __ballot(dead);
+                        S |= W;
+                        und &= ~(W | Dm);
+                    }
+                    sstamp(2);
+                    // S in lane order, up to the level and variable capacities
+                    const bool inS = (S >> lane) & 1ull;
+                    const uint32_t rank = (uint32_t)__popcll(S & below);
+                    uint32_t wincl = inS ? w[u] : 0u;
+                    if (b.rr_k) {
+                        wincl = inS ? b.rr_k * (rank + 1u) : 0u;
+                    } else {
+                        for (uint32_t o = 1; o < 64; o <<= 1) {
+                            const uint32_t y = __shfl_up(wincl, o, 64);
+                            if (lane >= o) wincl += y;
+                        }
+                    }
+                    const bool picked = inS && nc + rank < D && nv + wincl <= vpg;
+                    const uint64_t pm = __ballot(picked);
+                    if (picked) {
+                        const uint32_t idx = nc + rank;
+                        L.cc[idx] = c[u];
+                        L.cpos[idx] = i;
+                        const uint32_t f = atomicAdd(&L.nvar, w[u]);  // (nv + wincl <= vpg: fits)
+                        for (uint32_t j = 0; j < w[u]; ++j) {
+                            const uint32_t v = var_of(j);
+                            L.ivar[f + j] = v;
+                            L.ipick[f + j] = idx;
+                            rr_mw_own_insert(L, v);
+                        }
+                    }
+                    if (prof) { __builtin_amdgcn_s_waitcnt(0); sstamp(3); }
+                    const uint32_t np = (uint32_t)__popcll(pm);
+                    if (np) {
+                        const uint32_t lastp = 63u - (uint32_t)__builtin_clzll(pm);
+                        nv += __shfl(wincl, (int)lastp, 64);
+                    }
+                    nc += np;
+                    const uint64_t rest = S & ~pm;
+                    if (rest) {
+                        const uint32_t i0 = (uint32_t)__builtin_ctzll(rest);
+                        stop = true;
+                        scan_end = pu + i0;
+                        if (np == 0 && nc == 0 && g == 0) {
+                            // turn 0 is always exact: a pick too wide to record is committed alone
+                            if (lane == i0) { L.cc[0] = c[u]; L.cpos[0] = i; }
+                            wide = true;
+                            nc = 1;
+                            scan_end = pu + i0 + 1;
+                        }
+                    } else if (nc == D) {
+                        stop = true;
+                        scan_end = pu + 64 < end ? pu + 64 : end;
+                    }
+                }
+                if (!stop) { pos += ST * 64; scan_end = pos; }
+            }
+            if (!stop && pos >= end) { exhausted = 1; scan_end = end; }
+            __syncthreads();
+            pstamp(0);
+            // ---- the picks' variables into the global hash (turn pick * B + g), RR_MW_VPG / 64
+            // per lane, their slot claims issued together, then their minima; an insert that
+            // meets another turn offers the later one to ctl->conf
+            if (!wide) {
+                constexpr uint32_t PL = RR_MW_VPG / 64;
+                const uint32_t nvv = L.nvar;
+                uint32_t v[PL], h[PL], tau[PL];
+                uint32_t act = 0;
+#pragma unroll
+                for (uint32_t q = 0; q < PL; ++q) {
+                    const uint32_t f = q * 64 + lane;
+                    v[q] = f < nvv ? L.ivar[f] : RR_EMPTY;
+                    tau[q] = f < nvv ? L.ipick[f] * B + g : RR_EMPTY;
+                    h[q] = (v[q] * 0x9E3779B1u) >> (32 - 15);
+                    if (f < nvv) act |= 1u << q;
+                }
+                const uint32_t have = act;
+                while (act) {
+                    uint32_t k[PL];
+#pragma unroll
+                    for (uint32_t q = 0; q < PL; ++q) k[q] = ((act >> q) & 1u) ? atomicCAS(&gkey[h[q]], 0u, v[q] + 1u) : 0u;
+#pragma unroll
+                    for (uint32_t q = 0; q < PL; ++q) {
+                        if (!((act >> q) & 1u)) continue;
+                        if (k[q] == 0u || k[q] == v[q] + 1u) act &= ~(1u << q);
+                        else h[q] = (h[q] + 1) & (RR_MW_GH - 1);
+                    }
+                }
+                uint32_t old[PL];
+#pragma unroll
+                for (uint32_t q = 0; q < PL; ++q) old[q] = ((have >> q) & 1u) ? atomicMin(&gmin[h[q]], tau[q]) : RR_EMPTY;
+                unsigned long long worst = 0;
+#pragma unroll
+                for (uint32_t q = 0; q < PL; ++q) {
+                    if ((have >> q) & 1u) L.islot[q * 64 + lane] = h[q];
+                    if (old[q] != RR_EMPTY && old[q] != tau[q]) {
+                        const uint32_t loser = old[q] > tau[q] ? old[q] : tau[q];
+                        const unsigned long long cand = ((unsigned long long)ep << 32) | (uint32_t)~loser;
+                        worst = cand > worst ? cand : worst;
+                    }
+                }
+                for (int o = 32; o > 0; o >>= 1) {
+                    const unsigned long long y = __shfl_xor(worst, o, 64);
+                    worst = y > worst ? y : worst;
+                }
+                if (lane == 0 && worst) atomicMax(&ctl->conf, worst);
+            } else if (lane == 0) {
+                __hip_atomic_store(&ctl->wide_ep, ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (lane == 0) {
+                __hip_atomic_store(&ctl->ncand[g], nc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&ctl->scan_end[g], scan_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&ctl->exh[g], exhausted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            // (the own-pick hash is cleared after the commit)
+            pstamp(1);
+            if (!(ok = rr_mw_barrier(ctl, ++nbar * NW))) break;
+            pstamp(2);
+            // ---- the exact prefix (identical in every workgroup)
+        } else {
+            if (!(ok = rr_mw_barrier(ctl, ++nbar * NW))) break;
+        }
+        const unsigned long long cf = __hip_atomic_load(&ctl->conf, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool wide_all = __hip_atomic_load(&ctl->wide_ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ep;
+        uint32_t trunc = (uint32_t)(cf >> 32) == ep ? ~(uint32_t)cf : RR_EMPTY;
+        const uint32_t ncl = lane < B ? __hip_atomic_load(&ctl->ncand[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : D;
+        uint32_t und = ncl < D ? ncl * B + lane : RR_EMPTY;
+        for (int o = 32; o > 0; o >>= 1) und = min(und, (uint32_t)__shfl_xor(und, o, 64));
+        trunc = min(trunc, und);
+        trunc = wide_all ? 1u : min(trunc, D * B);
+        // ---- commit this group's turns < trunc: covers, MIS, its set pointer; clear its hash slots
+        if (g < B) {
+            const uint32_t a_raw = trunc > g ? (trunc - g + B - 1) / B : 0u;
+            const uint32_t a = a_raw < nc ? a_raw : nc;
+            const uint32_t s = L.live[(t0 + 1 + g) % n_live];
+            if (wide) {
+                if (a) {
+                    const uint32_t cl = L.cc[0], lbp = cv.offs[cl], wp = cv.offs[cl + 1] - lbp;
+                    for (uint32_t j = lane; j < wp; j += 64)
+                        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)stamp, rsC, lit_var(cv.lits[lbp + j]), 0, 16);
+                }
+            } else {
+                const uint32_t nvv = L.nvar;
+                for (uint32_t f = lane; f < nvv; f += 64) {
+                    const uint32_t hs = L.islot[f];
+                    gkey[hs] = 0u;
+                    gmin[hs] = RR_EMPTY;
+                    if (L.ipick[f] < a) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)stamp, rsC, L.ivar[f], 0, 16);
+                }
+            }
+            uint32_t mb = 0;
+            if (lane == 0 && a) mb = atomicAdd(&ctl->tm, a);
+            mb = __shfl(mb, 0, 64);
+            for (uint32_t p = lane; p < a; p += 64) b.tmis[mb + p] = L.cc[p];
+            if (lane == 0) {
+                const uint32_t se = __hip_atomic_load(&ctl->scan_end[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(&gptr[s], a < nc ? L.cpos[a] : se, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            for (uint32_t i = lane; i < RR_MW_OWN; i += 64) L.okey[i] = RR_EMPTY;
+            if (lane == 0) L.nvar = 0;
+        }
+        // ---- erasure at turn trunc, or the next turn index (replicated in every workgroup)
+        bool erase = false;
+        uint32_t idx_e = 0;
+        if (trunc < D * B) {
+            const uint32_t ge = trunc % B, le = trunc / B;
+            const uint32_t nge = __hip_atomic_load(&ctl->ncand[ge], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t xge = __hip_atomic_load(&ctl->exh[ge], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            erase = le == nge && xge;
+            idx_e = (t0 + 1 + trunc) % n_live;
+        }
+        if (erase) {
+            for (uint32_t i = idx_e + lane; i + 1 < n_live; i += 64) L.moved[i] = L.live[i + 1];
+            __syncthreads();
+            for (uint32_t i = idx_e + lane; i + 1 < n_live; i += 64) L.live[i] = L.moved[i];
+            __syncthreads();
+            n_live -= 1;
+            t = idx_e;  // t is not decremented: the next turn skips the moved-up set
+        } else {
+            t = (t0 + trunc) % n_live;
+        }
+        pstamp(3);
+        if (!(ok = rr_mw_barrier(ctl, ++nbar * NW))) break;
+        pstamp(4);
+    }
+    if (!ok) {
+        if (lane == 0) { st->error = 1; st->done = 3; }
+        return;
+    }
+    // statistics of the MIS (per tile, like the LFMIS kernels), spread over the workgroups
+    const uint32_t tm = __hip_atomic_load(&ctl->tm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t i = g * 64 + lane; i < tm; i += NW * 64) {
+        const uint32_t c = b.tmis[i];
+        atomicAdd(&b.tile_stats[2 * (c / TILE)], 1ull);
+        atomicAdd(&b.tile_stats[2 * (c / TILE) + 1], (unsigned long long)(cv.offs[c + 1] - cv.offs[c]));
+    }
+    if (g == 0 && lane == 0) {
+        st->tmis_cnt = tm;
+        st->tail_rounds = batches;
+        if (batches > st->max_rounds) st->max_rounds = batches;
+        __hip_atomic_store(&ctl->epoch, base + batches + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (b.ktime) time_slot(b, st->n_iter - 1)[3] = wall_now();
+        if (prof) {
+            unsigned long long* d = b.kdbg + (uint64_t)3 * DBG_BLOCKS * DBG_FIELDS;
+            d[0] = 0; d[1] = pacc[0] + pacc[1]; d[2] = pacc[2]; d[3] = pacc[3] + pacc[4];
+            d[4] = batches; d[5] = 0; d[6] = 0; d[7] = tm;
+            d[8] = pacc[0]; d[9] = pacc[1]; d[10] = pacc[2]; d[11] = pacc[3]; d[12] = pacc[4];
+            d[13] = sacc[0]; d[14] = sacc[1]; d[15] = sacc[2]; d[16] = sacc[3]; d[17] = sacc[4]; d[18] = sacc[5];
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------
 // Launchers.
 hipError_t launch_init_assignment(const LoopBuffers& b, hipStream_t s) {
     if (b.n_words == 0) return hipSuccess;
@@ -3690,8 +4199,15 @@ hipError_t launch_rr_mis(const ClauseView& cv, const LoopBuffers& b, hipStream_t
     }
     if (b.n_tiles) k_rr_entries<<<b.n_tiles, 256, 0, s>>>(cv, b);
     // clause variables held in registers while scanning: 4 for instances of width <= 4
-    if (b.rr_k >= 1 && b.rr_k <= 4) k_rr_mis<4, 4><<<1, RR_THREADS, sizeof(RRLds), s>>>(cv, b);
-    else k_rr_mis<8, 2><<<1, RR_THREADS, sizeof(RRLds), s>>>(cv, b);
+    if (b.rr_mw) {
+        if (!b.rr_ctl || b.rr_mw > RR_MW_MAX) return hipErrorInvalidValue;
+        if (b.rr_k >= 1 && b.rr_k <= 4) k_rr_mw<4, 4><<<b.rr_mw, 64, sizeof(RRMwLds), s>>>(cv, b);
+        else k_rr_mw<8, 2><<<b.rr_mw, 64, sizeof(RRMwLds), s>>>(cv, b);
+    } else if (b.rr_k >= 1 && b.rr_k <= 4) {
+        k_rr_mis<4, 4><<<1, RR_THREADS, sizeof(RRLds), s>>>(cv, b);
+    } else {
+        k_rr_mis<8, 2><<<1, RR_THREADS, sizeof(RRLds), s>>>(cv, b);
+    }
     return hipGetLastError();
 }
 

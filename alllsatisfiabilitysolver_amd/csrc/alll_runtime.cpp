@@ -641,7 +641,10 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
             if (deg[v] >= thr) hot.push_back({deg[v], v});
         if (!hot.empty()) {
             std::sort(hot.rbegin(), hot.rend());
-            if (hot.size() > HOT_MAX) hot.resize(HOT_MAX);
+            size_t hot_max = HOT_MAX;
+            if (const char* e = getenv("ALLL_HOT_MAX"))  // tuning: fewer hot variables (<= HOT_MAX)
+                hot_max = std::min<size_t>(HOT_MAX, (size_t)std::max(0, atoi(e)));
+            if (hot.size() > hot_max) hot.resize(hot_max);
             is_hot.assign(prob->n_vars, 0);
             for (auto& h : hot) is_hot[h.second] = 1;
             n_hot = (uint32_t)hot.size();
@@ -737,6 +740,18 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
         b.rr_sets = d_sets;
         b.rr_T = rr_T;
         b.rr_k = (rr_width >= 1 && rr_width <= 8) ? (uint32_t)rr_width : 0u;
+        // the batches across workgroups (one per lane group, at most 64): ALLL_RR_MW=0 keeps the
+        // one-workgroup kernel
+        uint32_t mw = std::min<uint32_t>(rr_T, 64);
+        if (const char* e = getenv("ALLL_RR_MW")) mw = atoi(e) > 0 ? std::min<uint32_t>(rr_T, std::min(64, atoi(e))) : 0u;
+        if (mw) {
+            if ((rc = dalloc(c, &b.rr_ctl, RR_MW_CTL_WORDS))) return bail(rc);
+            if ((rc = dalloc(c, &b.rr_gkey, RR_MW_GH))) return bail(rc);
+            if ((rc = dalloc(c, &b.rr_gmin, RR_MW_GH, 0xFF))) return bail(rc);
+            if ((rc = dalloc(c, &b.rr_ptr, rr_T))) return bail(rc);
+            if ((rc = dalloc(c, &b.rr_end, rr_T))) return bail(rc);
+        }
+        b.rr_mw = mw;
     }
     if ((rc = dalloc(c, &b.A, b.n_words + 4))) return bail(rc);  // +4: 16-byte tail loads
     if ((rc = dalloc(c, &b.vmask, (size_t)c->n_tiles_padded * TILE_WORDS))) return bail(rc);

@@ -10,6 +10,9 @@ caller's vector<ClauseArray*>), bit-exact:
     sets than groups (16-lane groups, one level), erasures of empty chunks, clauses too wide
     for a group's variable buffer, caller-given chunk boundaries;
   * ALLL_FLAG_LFMIS keeps the one-set MIS for T > 1.
+
+Every test runs with both kernels: the batches across workgroups (k_rr_mw, default) and in
+one workgroup (k_rr_mis, ALLL_RR_MW=0).
 """
 import glob
 import os
@@ -31,6 +34,15 @@ def gpu(native):
     if device_count() == 0:
         pytest.fail("no GPU visible: the gpu tests must run on an MI355X")
     return True
+
+
+@pytest.fixture(params=["mw", "one"], autouse=True)
+def rr_kernel(request, monkeypatch):
+    if request.param == "one":
+        monkeypatch.setenv("ALLL_RR_MW", "0")
+    else:
+        monkeypatch.delenv("ALLL_RR_MW", raising=False)
+    return request.param
 
 
 def mask_to_list(vm, m):

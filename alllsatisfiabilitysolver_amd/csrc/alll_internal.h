@@ -57,6 +57,31 @@ constexpr uint32_t DD_TIMEOUT = 10000000u;  // k_decide gives up after 100 ms (1
 constexpr uint32_t RR_TMAX = 2048;
 constexpr uint32_t RR_MW_GH = 1u << 15;  // k_rr_mw global hash slots
 constexpr uint32_t RR_MW_CTL_WORDS = 1024; // k_rr_mw control block (words)
+// Round robin as a fixpoint: the round-robin MIS is the LFMIS of the
+// violated clauses under the priority (turn, clause order), where a clause's turn is the step
+// at which its set's scan reaches it -- a function of how many clauses its set picked before
+// it.  The pick sets are iterated, LFMIS(turns(P)) -> P, until they repeat.
+constexpr uint32_t FP_TMAX = 256;          // sets (the schedule keeps T x T phase records)
+constexpr uint32_t FP_B = 2048;            // entries per block of the count / turn passes
+constexpr uint32_t FP_G = 4;               // grid LFMIS rounds before the one-workgroup tail
+constexpr uint32_t FP_MAX_DEFAULT = 16;    // LFMIS passes per iteration (graph unroll)
+enum : uint32_t { FP_RUN = 0, FP_FINAL = 1, FP_DONE = 2, FP_OFF = 3, FP_FAIL = 4 };
+struct RRFpCtl {
+    uint32_t state;      // FP_*: RUN iterating; FINAL the last pass converged (finalize now);
+                         // DONE finalized; OFF inactive iteration; FAIL fall back to k_rr_mw
+    uint32_t nu;         // violated clauses (scan entries) of the iteration
+    uint32_t fp_iter;    // LFMIS passes so far in this iteration
+    uint32_t changes;    // picks that differ between the last two passes
+    uint32_t serial;     // cover serial of the current LFMIS pass (fp_cov), never 0
+    uint32_t ep_base;    // owner epoch of round 0 of the current pass (owner reset per iteration)
+    uint32_t ep_next;    // first epoch after the current pass
+    uint32_t total;      // picks of the last pass
+    uint32_t guess_num, guess_den;  // previous iteration's |M| / |U| (initial pick density)
+    uint32_t n_steps;    // schedule length (turns + erasures)
+    uint32_t pad[5];
+    uint32_t cntJ[16];   // survivors of JOIN(r)
+    uint32_t cntC[16];   // claimers of CLAIM(r)
+};
 // In-loop kernel timing (ALLL_FLAG_KERNEL_TIMING): per iteration i, slot i % TIME_SLOTS holds
 // device wall-clock stamps (s_memrealtime) {eval start (min over workgroups), eval end (max),
 // reduce start, LFMIS tail end}.
@@ -185,6 +210,23 @@ struct LoopBuffers {
     uint32_t* rr_ptr;
     uint32_t* rr_end;
     uint32_t rr_mw;             // workgroups of k_rr_mw (0: the one-workgroup k_rr_mis)
+    // round robin by fixpoint (nullptr = off; k_rr_mw / k_rr_mis then decide every iteration,
+    // otherwise only those whose fixpoint failed)
+    RRFpCtl* fp_ctl;
+    uint8_t* fp_in;             // per scan entry: bit 0 picked by the last pass, bit 1 by the one before
+    uint32_t* fp_turn;          // per scan entry: turn = LFMIS priority of the next pass
+    uint32_t* fp_list;          // 2 x m: round lists (JOIN output, CLAIM output)
+    unsigned long long* fp_owner; // n_vars claim keys {epoch | turn | entry}, reset every iteration
+    uint32_t* fp_cov;           // n_vars: serial of the pass whose pick covers the variable
+    uint32_t* fp_blk;           // 2 x blocks: pick counts, then their exclusive prefix
+    uint32_t* fp_sf;            // T + 1: first scan entry of every set (entries past the last: nu)
+    uint32_t* fp_bnd;           // T + 1: picks before the set's first entry inside its block
+    uint32_t* fp_pf;            // T + 1: picks before the set's first entry (global)
+    uint32_t* fp_nseg;          // T: schedule phases the set lives through
+    uint4* fp_seg;              // T x T: {first level, first step, stride, offset} per (set, phase)
+    uint32_t* fp_erase;         // T: erasure steps, ascending
+    uint32_t fp_ib, fp_tb;      // key bits of the entry index and of the turn
+    uint32_t fp_max;            // LFMIS passes per iteration
     uint32_t n_vars;
     uint32_t n_words;
     uint32_t n_tiles;       // tiles covering [0, m)
@@ -226,6 +268,8 @@ hipError_t launch_claim_only(const ClauseView& cv, const LoopBuffers& b, uint32_
                              const uint32_t* in, uint32_t* out, hipStream_t s);
 hipError_t launch_tail(const ClauseView& cv, const LoopBuffers& b, uint32_t first_round,
                        hipStream_t s);
+// round robin: k_rr_entries, the fixpoint passes (when b.fp_ctl), then k_rr_mw / k_rr_mis for
+// iterations the fixpoint did not settle
 hipError_t launch_rr_mis(const ClauseView& cv, const LoopBuffers& b, hipStream_t s);
 hipError_t launch_resample(const ClauseView& cv, const LoopBuffers& b, uint32_t tile_begin,
                            uint32_t tile_end, bool to_delta, hipStream_t s);

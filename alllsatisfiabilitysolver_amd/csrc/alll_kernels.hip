@@ -2979,6 +2979,11 @@ __device__ __forceinline__ uint32_t rr_step_lane(const unsigned long long* sk, u
 // Violated clauses of the iteration in clause order as scan entries {id, literal start, width,
 // variables 0..7} (one 256-thread workgroup per tile; tile offsets from the evaluation's
 // per-tile counts), so that a scan round of k_rr_mis is two dependent loads (entry, cover).
+// the fixpoint passes decided this iteration's MIS (k_rr_mw / k_rr_mis then skip it)
+__device__ __forceinline__ bool fp_settled(const LoopBuffers& b) {
+    return b.fp_ctl && (b.fp_ctl->state == FP_FINAL || b.fp_ctl->state == FP_DONE);
+}
+
 struct RREnt {
     uint4 a;      // {clause id, literal start, width, 0}
     uint4 v0, v1; // variables 0..RR_KE-1 (RR_EMPTY past the width)
@@ -3037,7 +3042,7 @@ __global__ __launch_bounds__(256) void k_rr_entries(ClauseView cv, LoopBuffers b
 template <uint32_t KR, uint32_t ST>
 __global__ __launch_bounds__(RR_THREADS) void k_rr_mis(ClauseView cv, LoopBuffers b) {
     DevState* st = b.state;
-    if (!st->active) return;
+    if (!st->active || fp_settled(b)) return;
     extern __shared__ __align__(16) unsigned char rr_lds_raw[];
     RRLds& L = *reinterpret_cast<RRLds*>(rr_lds_raw);
     const uint32_t stamp = st->stamp;
@@ -3519,7 +3524,7 @@ __device__ __forceinline__ bool rr_mw_barrier(RRMwCtl* ctl, uint32_t target) {
 template <uint32_t KR, uint32_t ST>
 __global__ __launch_bounds__(64) void k_rr_mw(ClauseView cv, LoopBuffers b) {
     DevState* st = b.state;
-    if (!st->active) return;
+    if (!st->active || fp_settled(b)) return;
     extern __shared__ __align__(16) unsigned char rr_mw_lds_raw[];
     RRMwLds& L = *reinterpret_cast<RRMwLds*>(rr_mw_lds_raw);
     RRMwCtl* ctl = reinterpret_cast<RRMwCtl*>(b.rr_ctl);
@@ -3925,6 +3930,516 @@ __global__ __launch_bounds__(64) void k_rr_mw(ClauseView cv, LoopBuffers b) {
 }
 
 // ------------------------------------------------------------------------------------
+// Round robin as a fixpoint of LFMIS passes (SATInstance.h:414-447).
+//
+// The scan entries (k_rr_entries) list the violated clauses in clause order; set s is the
+// entry range [sf[s], sf[s+1]).  In the reference's loop set s picks its front clause at each
+// of its turns, so it reaches the entries after its l-th pick at one step, turn(s, l), and
+// those steps depend on the sets' pick counts alone: the live sets take steps in cyclic order,
+// a set is erased at its first turn after its last pick, and the set that moves into its place
+// loses that cycle's turn (the schedule, k_fp_sched).  A clause is picked iff no clause sharing
+// a variable was picked at an earlier (turn, entry).  So the picks P are the LFMIS under the
+// priority (turn(s, level_P(x)), x), level_P(x) = P's picks before x in its set, and any P
+// with P = LFMIS(priority_P) is the reference's MIS (by induction over the steps: at every step
+// both take the same front, or erase the same set).  The passes iterate P <- LFMIS(priority_P)
+// from a guess (picks spread at the previous iteration's density) until a pass reproduces its
+// input -- about ten passes at 10M clauses.  An iteration that has not settled after fp_max
+// passes (or whose owner epochs ran out) is decided by k_rr_mw, so every result is exact.
+//
+// LFMIS pass: CLAIM(r) / JOIN(r) grid rounds as in §4 with 64-bit keys
+// {~epoch | turn | entry} on fp_owner (reset every iteration), FP_G grid rounds, then the
+// one-workgroup k_fp_tail.  Picks are bit 0 of fp_in (bit 1: the previous pass's).
+constexpr int FP_THREADS = 256;
+constexpr uint32_t FP_PER = FP_B / FP_THREADS;  // entries per thread in the count / turn passes
+static_assert(FP_PER == 8, "a thread's pick bytes are one 8-byte load");
+
+__device__ __forceinline__ unsigned long long fp_key(const LoopBuffers& b, uint32_t ep, uint32_t turn, uint32_t i) {
+    const uint32_t sh = b.fp_tb + b.fp_ib;
+    const unsigned long long epmax = (1ull << (64 - sh)) - 1ull;
+    return ((epmax - ep) << sh) | ((unsigned long long)turn << b.fp_ib) | i;
+}
+// epochs one iteration may use (keys of later epochs are smaller)
+__device__ __forceinline__ uint32_t fp_ep_budget(const LoopBuffers& b) {
+    const uint32_t eb = 64 - b.fp_tb - b.fp_ib;
+    return eb >= 31 ? 0x7FFFFFFFu : (1u << eb) - 1u;
+}
+
+// the variables of scan entry i: the entry's first 4 (KW = 4: every clause is that narrow),
+// the next 4, then the CSR literals
+template <uint32_t KW, typename F>
+__device__ __forceinline__ void fp_for_vars(const ClauseView& cv, const RREnt* U, uint32_t i, const uint4& a,
+                                            const uint4& v0, F&& f) {
+    const uint32_t w = a.z;
+    if (w > 0) f(v0.x);
+    if (w > 1) f(v0.y);
+    if (w > 2) f(v0.z);
+    if (w > 3) f(v0.w);
+    if constexpr (KW == 0) {
+        if (w > 4) {
+            const uint4 v1 = U[i].v1;
+            f(v1.x);
+            if (w > 5) f(v1.y);
+            if (w > 6) f(v1.z);
+            if (w > 7) f(v1.w);
+            for (uint32_t j = 8; j < w; ++j) f(lit_var(cv.lits[a.y + j]));
+        }
+    }
+}
+
+// largest s < T with sf[s] <= i (sf non-decreasing, sf[0] = 0): the set of entry i < nu
+__device__ __forceinline__ uint32_t fp_set_of(const uint32_t* sf, uint32_t T, uint32_t i) {
+    uint32_t lo = 0, hi = T;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (sf[mid] <= i) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// wave-aggregated append of `i` to list `out` (counter `cnt`); every lane of the wave calls it
+__device__ __forceinline__ void fp_append(bool keep, uint32_t i, uint32_t* cnt, uint32_t* out) {
+    const unsigned long long bal = __ballot(keep);
+    const uint32_t lane = threadIdx.x & 63;
+    uint32_t base = 0;
+    if (lane == 0 && bal) base = atomicAdd(cnt, (uint32_t)__popcll(bal));
+    base = __shfl(base, 0, 64);
+    if (keep) out[base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = i;
+}
+
+// Iteration start: entry count, set bounds, pass state.  Runs after the reduce.
+__global__ __launch_bounds__(256) void k_fp_begin(LoopBuffers b) {
+    RRFpCtl* ctl = b.fp_ctl;
+    const DevState* st = b.state;
+    if (!st->active) {
+        if (threadIdx.x == 0) ctl->state = FP_OFF;
+        return;
+    }
+    const uint32_t nu = (uint32_t)st->u_total, T = b.rr_T;
+    const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
+    for (uint32_t s = threadIdx.x; s <= T; s += blockDim.x) {  // first entry with id >= set start
+        const uint32_t key = b.rr_sets[s];
+        uint32_t lo = 0, hi = nu;
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (U[mid].a.x < key) lo = mid + 1;
+            else hi = mid;
+        }
+        b.fp_sf[s] = s == T ? nu : lo;
+    }
+    if (threadIdx.x < 16) { ctl->cntJ[threadIdx.x] = 0; ctl->cntC[threadIdx.x] = 0; }
+    if (threadIdx.x == 0) {
+        ctl->state = FP_RUN;
+        ctl->nu = nu;
+        ctl->fp_iter = 0;
+        ctl->changes = 0;
+        ctl->ep_base = 0;
+        ctl->ep_next = 0;
+        if (ctl->guess_den == 0) { ctl->guess_num = 1; ctl->guess_den = 2; }
+    }
+}
+
+// The first pass's input: picks spread evenly over every set at density num / den.
+__global__ __launch_bounds__(FP_THREADS) void k_fp_guess(LoopBuffers b) {
+    const RRFpCtl* ctl = b.fp_ctl;
+    if (ctl->state != FP_RUN) return;
+    __shared__ uint32_t s_sf[FP_TMAX + 1];
+    const uint32_t T = b.rr_T, nu = ctl->nu;
+    const unsigned long long num = ctl->guess_num, den = ctl->guess_den;
+    for (uint32_t s = threadIdx.x; s <= T; s += blockDim.x) s_sf[s] = b.fp_sf[s];
+    __syncthreads();
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nu; i += gridDim.x * blockDim.x) {
+        const unsigned long long pos = i - s_sf[fp_set_of(s_sf, T, i)];
+        b.fp_in[i] = (uint8_t)((pos + 1) * num / den > pos * num / den);
+    }
+}
+
+// CLAIM(r): round 0 takes every entry (and moves the picks of the last pass to bit 1); later
+// rounds take JOIN(r-1)'s survivors, drop those a pick of this pass covers, and list the rest.
+template <uint32_t KW>
+__global__ __launch_bounds__(FP_THREADS) void k_fp_claim(ClauseView cv, LoopBuffers b, uint32_t r) {
+    RRFpCtl* ctl = b.fp_ctl;
+    if (ctl->state != FP_RUN) return;
+    const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
+    const uint32_t ep = ctl->ep_base + r, serial = ctl->serial;
+    const uint32_t n = r == 0 ? ctl->nu : ctl->cntJ[r - 1];
+    const uint32_t* lin = b.fp_list;
+    uint32_t* lout = b.fp_list + b.m;
+    for (uint32_t j0 = blockIdx.x * blockDim.x; j0 < n; j0 += gridDim.x * blockDim.x) {
+        const uint32_t j = j0 + threadIdx.x;
+        bool keep = false;
+        uint32_t i = 0;
+        if (j < n) {
+            i = r == 0 ? j : lin[j];
+            const uint4 a = U[i].a, v0 = U[i].v0;
+            bool dead = false;
+            if (r > 0) fp_for_vars<KW>(cv, U, i, a, v0, [&](uint32_t v) { dead |= b.fp_cov[v] == serial; });
+            else b.fp_in[i] = (uint8_t)((b.fp_in[i] & 1u) << 1);
+            if (!dead) {
+                const unsigned long long key = fp_key(b, ep, b.fp_turn[i], i);
+                fp_for_vars<KW>(cv, U, i, a, v0, [&](uint32_t v) { atomicMin(&b.fp_owner[v], key); });
+                keep = true;
+            }
+        }
+        if (r > 0) fp_append(keep, i, &ctl->cntC[r], lout);
+    }
+}
+
+// JOIN(r): an entry that holds every variable it claimed is picked (its variables covered by
+// this pass's serial); the others survive to round r + 1.
+template <uint32_t KW>
+__global__ __launch_bounds__(FP_THREADS) void k_fp_join(ClauseView cv, LoopBuffers b, uint32_t r) {
+    RRFpCtl* ctl = b.fp_ctl;
+    if (ctl->state != FP_RUN) return;
+    const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
+    const uint32_t ep = ctl->ep_base + r, serial = ctl->serial;
+    const uint32_t n = r == 0 ? ctl->nu : ctl->cntC[r];
+    const uint32_t* lin = b.fp_list + b.m;
+    uint32_t* lout = b.fp_list;
+    for (uint32_t j0 = blockIdx.x * blockDim.x; j0 < n; j0 += gridDim.x * blockDim.x) {
+        const uint32_t j = j0 + threadIdx.x;
+        bool keep = false;
+        uint32_t i = 0;
+        if (j < n) {
+            i = r == 0 ? j : lin[j];
+            const uint4 a = U[i].a, v0 = U[i].v0;
+            const unsigned long long key = fp_key(b, ep, b.fp_turn[i], i);
+            bool own = true;
+            fp_for_vars<KW>(cv, U, i, a, v0, [&](uint32_t v) { own &= b.fp_owner[v] == key; });
+            if (own) {
+                fp_for_vars<KW>(cv, U, i, a, v0, [&](uint32_t v) { b.fp_cov[v] = serial; });
+                b.fp_in[i] = (uint8_t)(b.fp_in[i] | 1u);
+            }
+            keep = !own;
+        }
+        fp_append(keep, i, &ctl->cntJ[r], lout);
+    }
+}
+
+// The pass's remaining rounds in one workgroup (the lists are short by now).  Reads that other
+// threads' atomics or stores of this launch decide go around L1 (agent-scope loads).
+template <uint32_t KW>
+__global__ __launch_bounds__(1024) void k_fp_tail(ClauseView cv, LoopBuffers b) {
+    RRFpCtl* ctl = b.fp_ctl;
+    if (ctl->state != FP_RUN) return;
+    const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
+    __shared__ uint32_t s_cnt;
+    uint32_t* la = b.fp_list;
+    uint32_t* lb = b.fp_list + b.m;
+    const uint32_t serial = ctl->serial, budget = fp_ep_budget(b);
+    uint32_t n = ctl->cntJ[FP_G - 1], ep = ctl->ep_base + FP_G;
+    bool failed = false;
+    while (n > 0) {
+        if (ep >= budget) { failed = true; break; }
+        if (threadIdx.x == 0) s_cnt = 0;
+        __syncthreads();
+        for (uint32_t j0 = 0; j0 < n; j0 += blockDim.x) {  // CLAIM: la -> lb
+            const uint32_t j = j0 + threadIdx.x;
+            bool keep = false;
+            uint32_t i = 0;
+            if (j < n) {
+                i = la[j];
+                const uint4 a = U[i].a, v0 = U[i].v0;
+                bool dead = false;
+                fp_for_vars<KW>(cv, U, i, a, v0, [&](uint32_t v) {
+                    dead |= __hip_atomic_load(&b.fp_cov[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == serial;
+                });
+                if (!dead) {
+                    const unsigned long long key = fp_key(b, ep, b.fp_turn[i], i);
+                    fp_for_vars<KW>(cv, U, i, a, v0, [&](uint32_t v) { atomicMin(&b.fp_owner[v], key); });
+                    keep = true;
+                }
+            }
+            fp_append(keep, i, &s_cnt, lb);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        const uint32_t nc = s_cnt;
+        __syncthreads();
+        if (threadIdx.x == 0) s_cnt = 0;
+        __syncthreads();
+        for (uint32_t j0 = 0; j0 < nc; j0 += blockDim.x) {  // JOIN: lb -> la
+            const uint32_t j = j0 + threadIdx.x;
+            bool keep = false;
+            uint32_t i = 0;
+            if (j < nc) {
+                i = lb[j];
+                const uint4 a = U[i].a, v0 = U[i].v0;
+                const unsigned long long key = fp_key(b, ep, b.fp_turn[i], i);
+                bool own = true;
+                fp_for_vars<KW>(cv, U, i, a, v0, [&](uint32_t v) {
+                    own &= __hip_atomic_load(&b.fp_owner[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == key;
+                });
+                if (own) {
+                    fp_for_vars<KW>(cv, U, i, a, v0, [&](uint32_t v) {
+                        __hip_atomic_store(&b.fp_cov[v], serial, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    });
+                    b.fp_in[i] = (uint8_t)(b.fp_in[i] | 1u);
+                }
+                keep = !own;
+            }
+            fp_append(keep, i, &s_cnt, la);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        n = s_cnt;
+        ++ep;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        ctl->ep_next = ep;
+        if (failed) ctl->state = FP_FAIL;
+    }
+}
+
+// Workgroup exclusive scan of one value per thread (blockDim.x <= 1024); returns the total too.
+__device__ __forceinline__ uint32_t fp_block_scan(uint32_t x, uint32_t* s_w, uint32_t& total) {
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    uint32_t incl = x;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o, 64);
+        if ((int)lane >= o) incl += y;
+    }
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    uint32_t before = 0;
+    total = 0;
+    for (uint32_t w = 0; w < nw; ++w) {
+        const uint32_t c = s_w[w];
+        if (w < wave) before += c;
+        total += c;
+    }
+    __syncthreads();
+    return before + incl - x;
+}
+
+// Picks per block of FP_B entries, picks before every set start that falls in the block, and
+// (test) the picks that changed since the previous pass.
+__global__ __launch_bounds__(FP_THREADS) void k_fp_count(LoopBuffers b, int test) {
+    RRFpCtl* ctl = b.fp_ctl;
+    if (ctl->state != FP_RUN) return;
+    __shared__ uint32_t s_w[FP_THREADS / 64], s_ex[FP_THREADS], s_bits[FP_THREADS];
+    const uint32_t nu = ctl->nu, T = b.rr_T, nblk = (nu + FP_B - 1) / FP_B;
+    uint32_t changed = 0;
+    for (uint32_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+        const uint32_t i0 = blk * FP_B + threadIdx.x * FP_PER;
+        unsigned long long x = 0;
+        if (i0 < nu) {
+            x = *reinterpret_cast<const unsigned long long*>(b.fp_in + i0);
+            if (nu - i0 < FP_PER) x &= (1ull << (8 * (nu - i0))) - 1ull;
+        }
+        const unsigned long long b0 = x & 0x0101010101010101ull, b1 = (x >> 1) & 0x0101010101010101ull;
+        const uint32_t cnt = (uint32_t)__popcll(b0);
+        changed += (uint32_t)__popcll(b0 ^ b1);
+        uint32_t total;
+        const uint32_t ex = fp_block_scan(cnt, s_w, total);
+        s_ex[threadIdx.x] = ex;
+        s_bits[threadIdx.x] = (uint32_t)((b0 * 0x0102040810204080ull) >> 56);  // bit e = entry i0 + e
+        __syncthreads();
+        if (threadIdx.x == 0) b.fp_blk[blk] = total;
+        for (uint32_t s = threadIdx.x; s <= T; s += blockDim.x) {
+            const uint32_t f = b.fp_sf[s];
+            if (f >= nu || f / FP_B != blk) continue;
+            const uint32_t t = (f % FP_B) / FP_PER, e = f % FP_PER;
+            b.fp_bnd[s] = s_ex[t] + (uint32_t)__popc(s_bits[t] & ((1u << e) - 1u));
+        }
+        __syncthreads();
+    }
+    if (test) {
+        for (int o = 32; o > 0; o >>= 1) changed += __shfl_down(changed, o, 64);
+        if ((threadIdx.x & 63) == 0 && changed) atomicAdd(&ctl->changes, changed);
+    }
+}
+
+// One workgroup: convergence, block offsets, picks per set, the schedule, the next pass.
+__global__ __launch_bounds__(1024) void k_fp_sched(LoopBuffers b, int test) {
+    RRFpCtl* ctl = b.fp_ctl;
+    const uint32_t state = ctl->state;
+    if (state == FP_FINAL) {  // the finalizing k_fp_turn has run
+        if (threadIdx.x == 0) ctl->state = FP_DONE;
+        return;
+    }
+    if (state != FP_RUN) return;
+    __shared__ uint32_t s_w[16];
+    __shared__ uint32_t s_n[FP_TMAX], s_done[FP_TMAX], s_live[FP_TMAX], s_nseg[FP_TMAX];
+    const uint32_t nu = ctl->nu, T = b.rr_T, nblk = (nu + FP_B - 1) / FP_B;
+    const bool conv = test && ctl->changes == 0;
+    uint32_t* blkoff = b.fp_blk + (b.m / FP_B + 2);
+    // exclusive scan of the block counts
+    uint32_t carry = 0;
+    for (uint32_t k0 = 0; k0 < nblk; k0 += blockDim.x) {
+        const uint32_t k = k0 + threadIdx.x;
+        const uint32_t x = k < nblk ? b.fp_blk[k] : 0u;
+        uint32_t tot;
+        const uint32_t ex = fp_block_scan(x, s_w, tot);
+        if (k < nblk) blkoff[k] = carry + ex;
+        carry += tot;
+    }
+    __syncthreads();
+    const uint32_t total = carry;
+    // picks before every set's first entry, picks per set
+    for (uint32_t s = threadIdx.x; s <= T; s += blockDim.x) {
+        const uint32_t f = b.fp_sf[s];
+        b.fp_pf[s] = f >= nu ? total : blkoff[f / FP_B] + b.fp_bnd[s];
+    }
+    __syncthreads();
+    for (uint32_t s = threadIdx.x; s < T; s += blockDim.x) {
+        s_n[s] = b.fp_pf[s + 1] - b.fp_pf[s];
+        s_done[s] = 0;
+        s_live[s] = s;
+        s_nseg[s] = 0;
+    }
+    __syncthreads();
+    // schedule (wave 0): phases between erasures.  With L live sets and the turn index t, live
+    // index x takes its j-th turn of the phase at step + j L + o(x), o(x) = (x - t - 1) mod L;
+    // the first set to run out of picks is erased at its next turn E = step + min(r L + o), r =
+    // picks left; then t = its index (the reference's t is not decremented).
+    if (threadIdx.x < 64) {
+        const uint32_t lane = threadIdx.x;
+        uint32_t L = T, t = 0, step = 0;
+        for (uint32_t p = 0; p < T; ++p) {
+            unsigned long long best = ~0ull;
+            for (uint32_t x = lane; x < L; x += 64) {
+                const uint32_t s = s_live[x], o = (x + L - (t % L) - 1) % L;
+                const unsigned long long key = ((unsigned long long)(s_n[s] - s_done[s]) * L + o) << 12 | x;
+                best = key < best ? key : best;
+            }
+            for (int o = 32; o > 0; o >>= 1) {
+                const unsigned long long y = __shfl_xor(best, o, 64);
+                best = y < best ? y : best;
+            }
+            const uint32_t xs = (uint32_t)(best & 0xFFFu);
+            const unsigned long long d = best >> 12;  // E - step
+            for (uint32_t x = lane; x < L; x += 64) {
+                const uint32_t s = s_live[x], o = (x + L - (t % L) - 1) % L;
+                const uint32_t cnt = x == xs ? s_n[s] - s_done[s] : (d > o ? (uint32_t)((d - o + L - 1) / L) : 0u);
+                b.fp_seg[(uint64_t)s * T + s_nseg[s]] = make_uint4(s_done[s], step, L, o);
+                s_nseg[s] += 1;
+                s_done[s] += cnt;
+            }
+            const uint32_t E = step + (uint32_t)d;
+            if (lane == 0) b.fp_erase[p] = E;
+            // erase live index xs (every lane reads before any writes: one wave)
+            uint32_t mv[FP_TMAX / 64];
+#pragma unroll
+            for (uint32_t q = 0; q < FP_TMAX / 64; ++q) {
+                const uint32_t x = xs + lane + 64 * q;
+                mv[q] = x + 1 < L ? s_live[x + 1] : 0u;
+            }
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (uint32_t q = 0; q < FP_TMAX / 64; ++q) {
+                const uint32_t x = xs + lane + 64 * q;
+                if (x + 1 < L) s_live[x] = mv[q];
+            }
+            __builtin_amdgcn_wave_barrier();
+            L -= 1;
+            t = xs;
+            step = E + 1;
+        }
+        if (lane == 0) ctl->n_steps = step;
+    }
+    __syncthreads();
+    for (uint32_t s = threadIdx.x; s < T; s += blockDim.x) b.fp_nseg[s] = s_nseg[s];
+    if (threadIdx.x < 16) { ctl->cntJ[threadIdx.x] = 0; ctl->cntC[threadIdx.x] = 0; }
+    if (threadIdx.x == 0) {
+        ctl->total = total;
+        ctl->changes = 0;
+        if (conv) {
+            ctl->state = FP_FINAL;
+            ctl->guess_num = total;
+            ctl->guess_den = nu ? nu : 1u;
+        } else {
+            if (test) ctl->fp_iter += 1;
+            ctl->ep_base = ctl->ep_next;
+            ctl->serial = ctl->serial + 1u ? ctl->serial + 1u : 1u;
+            if (ctl->ep_base + FP_G + 1u >= fp_ep_budget(b)) ctl->state = FP_FAIL;
+        }
+    }
+}
+
+// Turns of every entry for the next pass (RUN), or, after the converged pass (FINAL), the
+// MIS: picks in step order into tmis (step minus the erasures before it), their variables
+// covered with the iteration's stamp, and the statistics of k_rr_mw.
+template <uint32_t KW>
+__global__ __launch_bounds__(FP_THREADS) void k_fp_turn(ClauseView cv, LoopBuffers b) {
+    const RRFpCtl* ctl = b.fp_ctl;
+    const uint32_t state = ctl->state;
+    if (state != FP_RUN && state != FP_FINAL) return;
+    const bool fin = state == FP_FINAL;
+    DevState* st = b.state;
+    __shared__ uint32_t s_w[FP_THREADS / 64];
+    __shared__ uint32_t s_sf[FP_TMAX + 1], s_pf[FP_TMAX + 1], s_nseg[FP_TMAX], s_er[FP_TMAX];
+    const uint32_t nu = ctl->nu, T = b.rr_T, nblk = (nu + FP_B - 1) / FP_B;
+    const uint32_t stamp = st->stamp;
+    const uint32_t* blkoff = b.fp_blk + (b.m / FP_B + 2);
+    const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
+    for (uint32_t s = threadIdx.x; s <= T; s += blockDim.x) {
+        s_sf[s] = b.fp_sf[s];
+        s_pf[s] = b.fp_pf[s];
+        if (s < T) { s_nseg[s] = b.fp_nseg[s]; s_er[s] = b.fp_erase[s]; }
+    }
+    __syncthreads();
+    for (uint32_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+        const uint32_t i0 = blk * FP_B + threadIdx.x * FP_PER;
+        unsigned long long x = 0;
+        if (i0 < nu) {
+            x = *reinterpret_cast<const unsigned long long*>(b.fp_in + i0);
+            if (nu - i0 < FP_PER) x &= (1ull << (8 * (nu - i0))) - 1ull;
+        }
+        const unsigned long long b0 = x & 0x0101010101010101ull;
+        uint32_t tot;
+        uint32_t P = blkoff[blk] + fp_block_scan((uint32_t)__popcll(b0), s_w, tot);
+        if (i0 < nu) {
+            uint32_t s = fp_set_of(s_sf, T, i0);
+            const uint32_t e1 = min(nu - i0, FP_PER);
+            for (uint32_t e = 0; e < e1; ++e) {
+                const uint32_t i = i0 + e;
+                while (i >= s_sf[s + 1]) ++s;
+                const bool pick = (b0 >> (8 * e)) & 1ull;
+                if (!fin || pick) {
+                    const uint32_t lev = P - s_pf[s];
+                    // last phase record of s whose first level <= lev
+                    const uint4* rec = b.fp_seg + (uint64_t)s * T;
+                    uint32_t lo = 0, hi = s_nseg[s];
+                    while (hi - lo > 1) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if (rec[mid].x <= lev) lo = mid;
+                        else hi = mid;
+                    }
+                    const uint4 g = rec[lo];
+                    const uint32_t turn = g.y + (lev - g.x) * g.z + g.w;
+                    if (!fin) {
+                        b.fp_turn[i] = turn;
+                    } else {
+                        uint32_t a = 0, z = T;  // erasures before the turn
+                        while (a < z) {
+                            const uint32_t mid = (a + z) >> 1;
+                            if (s_er[mid] < turn) a = mid + 1;
+                            else z = mid;
+                        }
+                        const uint4 ea = U[i].a;
+                        b.tmis[turn - a] = ea.x;
+                        const uint4 v0 = U[i].v0;
+                        fp_for_vars<KW>(cv, U, i, ea, v0, [&](uint32_t v) { b.cover[v] = (uint8_t)stamp; });
+                        atomicAdd(&b.tile_stats[2 * (ea.x / TILE)], 1ull);
+                        atomicAdd(&b.tile_stats[2 * (ea.x / TILE) + 1], (unsigned long long)ea.z);
+                    }
+                }
+                P += pick ? 1u : 0u;
+            }
+        }
+        __syncthreads();
+    }
+    if (fin && blockIdx.x == 0 && threadIdx.x == 0) {
+        st->tmis_cnt = ctl->total;
+        st->tail_rounds = ctl->fp_iter;
+        if (ctl->fp_iter > st->max_rounds) st->max_rounds = ctl->fp_iter;
+        if (b.ktime) time_slot(b, st->n_iter - 1)[3] = wall_now();
+    }
+}
+
+// ------------------------------------------------------------------------------------
 // Launchers.
 hipError_t launch_init_assignment(const LoopBuffers& b, hipStream_t s) {
     if (b.n_words == 0) return hipSuccess;
@@ -4198,6 +4713,37 @@ hipError_t launch_rr_mis(const ClauseView& cv, const LoopBuffers& b, hipStream_t
         attr_mark(ATTR_RR, dev);
     }
     if (b.n_tiles) k_rr_entries<<<b.n_tiles, 256, 0, s>>>(cv, b);
+    if (b.fp_ctl) {  // the fixpoint passes; k_rr_mw below only if they do not settle
+        if (b.rr_T > FP_TMAX || b.fp_max == 0) return hipErrorInvalidValue;
+        const bool narrow = b.rr_k >= 1 && b.rr_k <= 4;
+        const uint32_t gb = (uint32_t)std::min<uint64_t>((b.m + FP_B - 1) / FP_B + 1, 1024);
+        const uint32_t gl = (uint32_t)std::min<uint64_t>((b.m + FP_THREADS - 1) / FP_THREADS + 1, 2048);
+        hipError_t e = hipMemsetAsync(b.fp_owner, 0xFF, (size_t)b.n_vars * 8, s);
+        if (e != hipSuccess) return e;
+        k_fp_begin<<<1, 256, 0, s>>>(b);
+        k_fp_guess<<<gl, FP_THREADS, 0, s>>>(b);
+        auto turns = [&](int test) {
+            k_fp_count<<<gb, FP_THREADS, 0, s>>>(b, test);
+            k_fp_sched<<<1, 1024, 0, s>>>(b, test);
+            if (narrow) k_fp_turn<4><<<gb, FP_THREADS, 0, s>>>(cv, b);
+            else k_fp_turn<0><<<gb, FP_THREADS, 0, s>>>(cv, b);
+        };
+        turns(0);
+        for (uint32_t p = 0; p < b.fp_max; ++p) {
+            for (uint32_t r = 0; r < FP_G; ++r) {
+                if (narrow) {
+                    k_fp_claim<4><<<gl, FP_THREADS, 0, s>>>(cv, b, r);
+                    k_fp_join<4><<<gl, FP_THREADS, 0, s>>>(cv, b, r);
+                } else {
+                    k_fp_claim<0><<<gl, FP_THREADS, 0, s>>>(cv, b, r);
+                    k_fp_join<0><<<gl, FP_THREADS, 0, s>>>(cv, b, r);
+                }
+            }
+            if (narrow) k_fp_tail<4><<<1, 1024, 0, s>>>(cv, b);
+            else k_fp_tail<0><<<1, 1024, 0, s>>>(cv, b);
+            turns(1);
+        }
+    }
     // clause variables held in registers while scanning: 4 for instances of width <= 4
     if (b.rr_mw) {
         if (!b.rr_ctl || b.rr_mw > RR_MW_MAX) return hipErrorInvalidValue;

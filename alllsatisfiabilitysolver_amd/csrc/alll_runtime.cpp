@@ -752,6 +752,33 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
             if ((rc = dalloc(c, &b.rr_end, rr_T))) return bail(rc);
         }
         b.rr_mw = mw;
+        // the fixpoint passes: keys {epoch | turn | entry} need >= 10 epoch
+        // bits; ALLL_RR_FP=0 leaves every iteration to the batch kernels, ALLL_RR_FP_MAX sets the
+        // passes per iteration (graph unroll)
+        auto bits_of = [](uint64_t x) { uint32_t k = 1; while (k < 64 && (x >> k)) ++k; return k; };
+        const uint32_t ib = bits_of(m), tb = bits_of(m + rr_T + 1);
+        bool fp = rr_T <= FP_TMAX && ib + tb + 10 <= 64;
+        if (const char* e = getenv("ALLL_RR_FP")) fp = fp && atoi(e) != 0;
+        if (fp) {
+            const size_t nblk = m / FP_B + 2;
+            if ((rc = dalloc(c, &b.fp_ctl, 1))) return bail(rc);
+            if ((rc = dalloc(c, &b.fp_in, m + FP_B))) return bail(rc);
+            if ((rc = dalloc(c, &b.fp_turn, m + 1))) return bail(rc);
+            if ((rc = dalloc(c, &b.fp_list, 2 * (size_t)m + 2))) return bail(rc);
+            if ((rc = dalloc(c, &b.fp_owner, (size_t)prob->n_vars + 1, 0xFF))) return bail(rc);
+            if ((rc = dalloc(c, &b.fp_cov, (size_t)prob->n_vars + 1))) return bail(rc);
+            if ((rc = dalloc(c, &b.fp_blk, 2 * nblk))) return bail(rc);
+            if ((rc = dalloc(c, &b.fp_sf, rr_T + 1))) return bail(rc);
+            if ((rc = dalloc(c, &b.fp_bnd, rr_T + 1))) return bail(rc);
+            if ((rc = dalloc(c, &b.fp_pf, rr_T + 1))) return bail(rc);
+            if ((rc = dalloc(c, &b.fp_nseg, rr_T))) return bail(rc);
+            if ((rc = dalloc(c, &b.fp_seg, (size_t)rr_T * rr_T))) return bail(rc);
+            if ((rc = dalloc(c, &b.fp_erase, rr_T))) return bail(rc);
+            b.fp_ib = ib;
+            b.fp_tb = tb;
+            b.fp_max = FP_MAX_DEFAULT;
+            if (const char* e = getenv("ALLL_RR_FP_MAX")) b.fp_max = (uint32_t)std::max(1, std::min(256, atoi(e)));
+        }
     }
     if ((rc = dalloc(c, &b.A, b.n_words + 4))) return bail(rc);  // +4: 16-byte tail loads
     if ((rc = dalloc(c, &b.vmask, (size_t)c->n_tiles_padded * TILE_WORDS))) return bail(rc);

@@ -11,8 +11,10 @@ caller's vector<ClauseArray*>), bit-exact:
     for a group's variable buffer, caller-given chunk boundaries;
   * ALLL_FLAG_LFMIS keeps the one-set MIS for T > 1.
 
-Every test runs with both kernels: the batches across workgroups (k_rr_mw, default) and in
-one workgroup (k_rr_mis, ALLL_RR_MW=0).
+Every test runs with each way of deciding the MIS: the fixpoint passes (default, DESIGN.md
+§4.3.2), the same passes capped at one or two per iteration (ALLL_RR_FP_MAX, so that most
+iterations fall back to the batch kernel mid-run), and the batch kernels alone (ALLL_RR_FP=0):
+across workgroups (k_rr_mw) and in one workgroup (k_rr_mis, ALLL_RR_MW=0).
 """
 import glob
 import os
@@ -36,12 +38,16 @@ def gpu(native):
     return True
 
 
-@pytest.fixture(params=["mw", "one"], autouse=True)
+@pytest.fixture(params=["fp", "fp_cap1", "fp_cap2", "mw", "one"], autouse=True)
 def rr_kernel(request, monkeypatch):
-    if request.param == "one":
-        monkeypatch.setenv("ALLL_RR_MW", "0")
-    else:
-        monkeypatch.delenv("ALLL_RR_MW", raising=False)
+    for k in ("ALLL_RR_MW", "ALLL_RR_FP", "ALLL_RR_FP_MAX"):
+        monkeypatch.delenv(k, raising=False)
+    if request.param.startswith("fp_cap"):
+        monkeypatch.setenv("ALLL_RR_FP_MAX", request.param[-1])
+    elif request.param in ("mw", "one"):
+        monkeypatch.setenv("ALLL_RR_FP", "0")
+        if request.param == "one":
+            monkeypatch.setenv("ALLL_RR_MW", "0")
     return request.param
 
 

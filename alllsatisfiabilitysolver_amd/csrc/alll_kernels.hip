@@ -3952,6 +3952,7 @@ __global__ __launch_bounds__(64) void k_rr_mw(ClauseView cv, LoopBuffers b) {
 constexpr int FP_THREADS = 256;
 constexpr uint32_t FP_PER = FP_B / FP_THREADS;  // entries per thread in the count / turn passes
 static_assert(FP_PER == 8, "a thread's pick bytes are one 8-byte load");
+constexpr uint32_t FP_LDS_SEG_T = 32;  // k_fp_turn keeps the schedule in LDS up to this many sets
 
 __device__ __forceinline__ unsigned long long fp_key(const LoopBuffers& b, uint32_t ep, uint32_t turn, uint32_t i) {
     const uint32_t sh = b.fp_tb + b.fp_ib;
@@ -3997,7 +3998,8 @@ __device__ __forceinline__ uint32_t fp_set_of(const uint32_t* sf, uint32_t T, ui
     return lo;
 }
 
-// wave-aggregated append of `i` to list `out` (counter `cnt`); every lane of the wave calls it
+// wave-aggregated append of `i` to list `out` (counter `cnt`, LDS or global); every lane of the
+// wave calls it
 __device__ __forceinline__ void fp_append(bool keep, uint32_t i, uint32_t* cnt, uint32_t* out) {
     const unsigned long long bal = __ballot(keep);
     const uint32_t lane = threadIdx.x & 63;
@@ -4054,65 +4056,92 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_guess(LoopBuffers b) {
     }
 }
 
-// CLAIM(r): round 0 takes every entry (and moves the picks of the last pass to bit 1); later
-// rounds take JOIN(r-1)'s survivors, drop those a pick of this pass covers, and list the rest.
+// CLAIM(r), a workgroup per tile of FP_B entries: round 0 takes the tile's entries (and moves
+// the picks of the last pass to bit 1); later rounds take the tile's JOIN(r-1) survivors, drop
+// those a pick of this pass covers, and list the rest.  Lists are per tile (slots
+// [tile * FP_B, +count)), counted in LDS: no global counter.
 template <uint32_t KW>
 __global__ __launch_bounds__(FP_THREADS) void k_fp_claim(ClauseView cv, LoopBuffers b, uint32_t r) {
-    RRFpCtl* ctl = b.fp_ctl;
+    const RRFpCtl* ctl = b.fp_ctl;
     if (ctl->state != FP_RUN) return;
+    const uint32_t nu = ctl->nu;
+    __shared__ uint32_t s_cnt;
     const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
+    const uint32_t ntile = (nu + FP_B - 1) / FP_B;
     const uint32_t ep = ctl->ep_base + r, serial = ctl->serial;
-    const uint32_t n = r == 0 ? ctl->nu : ctl->cntJ[r - 1];
-    const uint32_t* lin = b.fp_list;
-    uint32_t* lout = b.fp_list + b.m;
-    for (uint32_t j0 = blockIdx.x * blockDim.x; j0 < n; j0 += gridDim.x * blockDim.x) {
-        const uint32_t j = j0 + threadIdx.x;
-        bool keep = false;
-        uint32_t i = 0;
-        if (j < n) {
-            i = r == 0 ? j : lin[j];
-            const uint4 a = U[i].a, v0 = U[i].v0;
-            bool dead = false;
-            if (r > 0) fp_for_vars<KW>(cv, U, i, a, v0, [&](uint32_t v) { dead |= b.fp_cov[v] == serial; });
-            else b.fp_in[i] = (uint8_t)((b.fp_in[i] & 1u) << 1);
-            if (!dead) {
-                const unsigned long long key = fp_key(b, ep, b.fp_turn[i], i);
-                fp_for_vars<KW>(cv, U, i, a, v0, [&](uint32_t v) { atomicMin(&b.fp_owner[v], key); });
-                keep = true;
+    for (uint32_t tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
+        const uint32_t i0 = tile * FP_B;
+        if (threadIdx.x == 0) s_cnt = 0;
+        __syncthreads();
+        const uint32_t n = r == 0 ? min(FP_B, nu - i0) : b.fp_tcnt[(2 * (r - 1)) * ntile + tile];
+        const uint32_t* lin = b.fp_list + i0;
+        uint32_t* lout = b.fp_list + b.m + i0;
+        for (uint32_t j0 = 0; j0 < n; j0 += blockDim.x) {
+            const uint32_t j = j0 + threadIdx.x;
+            bool keep = false;
+            uint32_t i = 0;
+            if (j < n) {
+                i = r == 0 ? i0 + j : lin[j];
+                const uint4 a = U[i].a, v0 = U[i].v0;
+                const uint32_t turn = b.fp_turn[i];
+                bool dead = false;
+                if (r > 0) fp_for_vars<KW>(cv, U, i, a, v0, [&](uint32_t v) { dead |= b.fp_cov[v] == serial; });
+                else b.fp_in[i] = (uint8_t)((b.fp_in[i] & 1u) << 1);
+                if (!dead) {
+                    const unsigned long long key = fp_key(b, ep, turn, i);
+                    fp_for_vars<KW>(cv, U, i, a, v0, [&](uint32_t v) { atomicMin(&b.fp_owner[v], key); });
+                    keep = true;
+                }
             }
+            if (r > 0) fp_append(keep, i, &s_cnt, lout);
         }
-        if (r > 0) fp_append(keep, i, &ctl->cntC[r], lout);
+        if (r > 0) {
+            __syncthreads();
+            if (threadIdx.x == 0) b.fp_tcnt[(2 * r - 1) * ntile + tile] = s_cnt;
+        }
+        __syncthreads();
     }
 }
 
-// JOIN(r): an entry that holds every variable it claimed is picked (its variables covered by
-// this pass's serial); the others survive to round r + 1.
+// JOIN(r), a workgroup per tile: an entry that holds every variable it claimed is picked (its
+// variables covered by this pass's serial); the others survive to round r + 1.
 template <uint32_t KW>
 __global__ __launch_bounds__(FP_THREADS) void k_fp_join(ClauseView cv, LoopBuffers b, uint32_t r) {
-    RRFpCtl* ctl = b.fp_ctl;
+    const RRFpCtl* ctl = b.fp_ctl;
     if (ctl->state != FP_RUN) return;
+    const uint32_t nu = ctl->nu;
+    __shared__ uint32_t s_cnt;
     const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
+    const uint32_t ntile = (nu + FP_B - 1) / FP_B;
     const uint32_t ep = ctl->ep_base + r, serial = ctl->serial;
-    const uint32_t n = r == 0 ? ctl->nu : ctl->cntC[r];
-    const uint32_t* lin = b.fp_list + b.m;
-    uint32_t* lout = b.fp_list;
-    for (uint32_t j0 = blockIdx.x * blockDim.x; j0 < n; j0 += gridDim.x * blockDim.x) {
-        const uint32_t j = j0 + threadIdx.x;
-        bool keep = false;
-        uint32_t i = 0;
-        if (j < n) {
-            i = r == 0 ? j : lin[j];
-            const uint4 a = U[i].a, v0 = U[i].v0;
-            const unsigned long long key = fp_key(b, ep, b.fp_turn[i], i);
-            bool own = true;
-            fp_for_vars<KW>(cv, U, i, a, v0, [&](uint32_t v) { own &= b.fp_owner[v] == key; });
-            if (own) {
-                fp_for_vars<KW>(cv, U, i, a, v0, [&](uint32_t v) { b.fp_cov[v] = serial; });
-                b.fp_in[i] = (uint8_t)(b.fp_in[i] | 1u);
+    for (uint32_t tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
+        const uint32_t i0 = tile * FP_B;
+        if (threadIdx.x == 0) s_cnt = 0;
+        __syncthreads();
+        const uint32_t n = r == 0 ? min(FP_B, nu - i0) : b.fp_tcnt[(2 * r - 1) * ntile + tile];
+        const uint32_t* lin = b.fp_list + b.m + i0;
+        uint32_t* lout = b.fp_list + i0;
+        for (uint32_t j0 = 0; j0 < n; j0 += blockDim.x) {
+            const uint32_t j = j0 + threadIdx.x;
+            bool keep = false;
+            uint32_t i = 0;
+            if (j < n) {
+                i = r == 0 ? i0 + j : lin[j];
+                const uint4 a = U[i].a, v0 = U[i].v0;
+                const unsigned long long key = fp_key(b, ep, b.fp_turn[i], i);
+                bool own = true;
+                fp_for_vars<KW>(cv, U, i, a, v0, [&](uint32_t v) { own &= b.fp_owner[v] == key; });
+                if (own) {
+                    fp_for_vars<KW>(cv, U, i, a, v0, [&](uint32_t v) { b.fp_cov[v] = serial; });
+                    b.fp_in[i] = (uint8_t)(b.fp_in[i] | 1u);
+                }
+                keep = !own;
             }
-            keep = !own;
+            fp_append(keep, i, &s_cnt, lout);
         }
-        fp_append(keep, i, &ctl->cntJ[r], lout);
+        __syncthreads();
+        if (threadIdx.x == 0) b.fp_tcnt[(2 * r) * ntile + tile] = s_cnt;
+        __syncthreads();
     }
 }
 
@@ -4127,8 +4156,30 @@ __global__ __launch_bounds__(1024) void k_fp_tail(ClauseView cv, LoopBuffers b) 
     uint32_t* la = b.fp_list;
     uint32_t* lb = b.fp_list + b.m;
     const uint32_t serial = ctl->serial, budget = fp_ep_budget(b);
-    uint32_t n = ctl->cntJ[FP_G - 1], ep = ctl->ep_base + FP_G;
+    const uint32_t nu = ctl->nu, ntile = (nu + FP_B - 1) / FP_B;
+    uint32_t ep = ctl->ep_base + FP_G;
     bool failed = false;
+    // the survivors of the last grid round, tile by tile, into one list (lb)
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
+    const uint32_t* tc = b.fp_tcnt + (2 * (FP_G - 1)) * ntile;
+    for (uint32_t t = threadIdx.x >> 6; t < ntile; t += blockDim.x >> 6) {
+        const uint32_t c = tc[t];
+        if (!c) continue;
+        uint32_t base = 0;
+        if ((threadIdx.x & 63) == 0) base = atomicAdd(&s_cnt, c);
+        base = __shfl(base, 0, 64);
+        for (uint32_t j = threadIdx.x & 63; j < c; j += 64) la[b.m + base + j] = la[(uint64_t)t * FP_B + j];
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    uint32_t n = s_cnt;
+    __syncthreads();
+    if (n) {  // back to la (the rounds below read la)
+        for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) la[j] = __hip_atomic_load(&lb[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
     while (n > 0) {
         if (ep >= budget) { failed = true; break; }
         if (threadIdx.x == 0) s_cnt = 0;
@@ -4370,6 +4421,7 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_turn(ClauseView cv, LoopBuffe
     DevState* st = b.state;
     __shared__ uint32_t s_w[FP_THREADS / 64];
     __shared__ uint32_t s_sf[FP_TMAX + 1], s_pf[FP_TMAX + 1], s_nseg[FP_TMAX], s_er[FP_TMAX];
+    __shared__ uint4 s_seg[FP_LDS_SEG_T * FP_LDS_SEG_T];  // the schedule itself when T is small
     const uint32_t nu = ctl->nu, T = b.rr_T, nblk = (nu + FP_B - 1) / FP_B;
     const uint32_t stamp = st->stamp;
     const uint32_t* blkoff = b.fp_blk + (b.m / FP_B + 2);
@@ -4379,7 +4431,11 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_turn(ClauseView cv, LoopBuffe
         s_pf[s] = b.fp_pf[s];
         if (s < T) { s_nseg[s] = b.fp_nseg[s]; s_er[s] = b.fp_erase[s]; }
     }
+    const bool lds_seg = T <= FP_LDS_SEG_T;
+    if (lds_seg)
+        for (uint32_t q = threadIdx.x; q < T * T; q += blockDim.x) s_seg[q] = b.fp_seg[q];
     __syncthreads();
+    const uint4* segs = lds_seg ? s_seg : b.fp_seg;
     for (uint32_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
         const uint32_t i0 = blk * FP_B + threadIdx.x * FP_PER;
         unsigned long long x = 0;
@@ -4393,6 +4449,8 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_turn(ClauseView cv, LoopBuffe
         if (i0 < nu) {
             uint32_t s = fp_set_of(s_sf, T, i0);
             const uint32_t e1 = min(nu - i0, FP_PER);
+            uint32_t st_tile = ~0u, st_n = 0;  // MIS statistics of this thread's picks, per clause tile
+            unsigned long long st_w = 0;
             for (uint32_t e = 0; e < e1; ++e) {
                 const uint32_t i = i0 + e;
                 while (i >= s_sf[s + 1]) ++s;
@@ -4400,7 +4458,7 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_turn(ClauseView cv, LoopBuffe
                 if (!fin || pick) {
                     const uint32_t lev = P - s_pf[s];
                     // last phase record of s whose first level <= lev
-                    const uint4* rec = b.fp_seg + (uint64_t)s * T;
+                    const uint4* rec = segs + (uint64_t)s * T;
                     uint32_t lo = 0, hi = s_nseg[s];
                     while (hi - lo > 1) {
                         const uint32_t mid = (lo + hi) >> 1;
@@ -4422,11 +4480,24 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_turn(ClauseView cv, LoopBuffe
                         b.tmis[turn - a] = ea.x;
                         const uint4 v0 = U[i].v0;
                         fp_for_vars<KW>(cv, U, i, ea, v0, [&](uint32_t v) { b.cover[v] = (uint8_t)stamp; });
-                        atomicAdd(&b.tile_stats[2 * (ea.x / TILE)], 1ull);
-                        atomicAdd(&b.tile_stats[2 * (ea.x / TILE) + 1], (unsigned long long)ea.z);
+                        if (ea.x / TILE != st_tile) {
+                            if (st_n) {
+                                atomicAdd(&b.tile_stats[2 * st_tile], (unsigned long long)st_n);
+                                atomicAdd(&b.tile_stats[2 * st_tile + 1], st_w);
+                            }
+                            st_tile = ea.x / TILE;
+                            st_n = 0;
+                            st_w = 0;
+                        }
+                        st_n += 1;
+                        st_w += ea.z;
                     }
                 }
                 P += pick ? 1u : 0u;
+            }
+            if (st_n) {
+                atomicAdd(&b.tile_stats[2 * st_tile], (unsigned long long)st_n);
+                atomicAdd(&b.tile_stats[2 * st_tile + 1], st_w);
             }
         }
         __syncthreads();
@@ -4732,11 +4803,11 @@ hipError_t launch_rr_mis(const ClauseView& cv, const LoopBuffers& b, hipStream_t
         for (uint32_t p = 0; p < b.fp_max; ++p) {
             for (uint32_t r = 0; r < FP_G; ++r) {
                 if (narrow) {
-                    k_fp_claim<4><<<gl, FP_THREADS, 0, s>>>(cv, b, r);
-                    k_fp_join<4><<<gl, FP_THREADS, 0, s>>>(cv, b, r);
+                    k_fp_claim<4><<<gb, FP_THREADS, 0, s>>>(cv, b, r);
+                    k_fp_join<4><<<gb, FP_THREADS, 0, s>>>(cv, b, r);
                 } else {
-                    k_fp_claim<0><<<gl, FP_THREADS, 0, s>>>(cv, b, r);
-                    k_fp_join<0><<<gl, FP_THREADS, 0, s>>>(cv, b, r);
+                    k_fp_claim<0><<<gb, FP_THREADS, 0, s>>>(cv, b, r);
+                    k_fp_join<0><<<gb, FP_THREADS, 0, s>>>(cv, b, r);
                 }
             }
             if (narrow) k_fp_tail<4><<<1, 1024, 0, s>>>(cv, b);

@@ -3952,7 +3952,9 @@ __global__ __launch_bounds__(64) void k_rr_mw(ClauseView cv, LoopBuffers b) {
 constexpr int FP_THREADS = 256;
 constexpr uint32_t FP_PER = FP_B / FP_THREADS;  // entries per thread in the count / turn passes
 static_assert(FP_PER == 8, "a thread's pick bytes are one 8-byte load");
-constexpr uint32_t FP_LDS_SEG_T = 32;  // k_fp_turn keeps the schedule in LDS up to this many sets
+constexpr uint32_t FP_RT = 256;        // entries per round tile (one per thread): many workgroups per CU
+constexpr uint32_t FP_LDS_SEG_T = 32;     // k_fp_turn keeps the schedule in LDS up to this many sets
+constexpr uint32_t FP_COUNT_GRID = 1024;  // workgroups of k_fp_count / k_fp_turn (grid-stride over blocks)
 
 __device__ __forceinline__ unsigned long long fp_key(const LoopBuffers& b, uint32_t ep, uint32_t turn, uint32_t i) {
     const uint32_t sh = b.fp_tb + b.fp_ib;
@@ -4056,10 +4058,10 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_guess(LoopBuffers b) {
     }
 }
 
-// CLAIM(r), a workgroup per tile of FP_B entries: round 0 takes the tile's entries (and moves
+// CLAIM(r), a workgroup per round tile of FP_RT entries: round 0 takes the tile's entries (and moves
 // the picks of the last pass to bit 1); later rounds take the tile's JOIN(r-1) survivors, drop
 // those a pick of this pass covers, and list the rest.  Lists are per tile (slots
-// [tile * FP_B, +count)), counted in LDS: no global counter.
+// [tile * FP_RT, +count)), counted in LDS: no global counter.
 template <uint32_t KW>
 __global__ __launch_bounds__(FP_THREADS) void k_fp_claim(ClauseView cv, LoopBuffers b, uint32_t r) {
     const RRFpCtl* ctl = b.fp_ctl;
@@ -4067,13 +4069,13 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_claim(ClauseView cv, LoopBuff
     const uint32_t nu = ctl->nu;
     __shared__ uint32_t s_cnt;
     const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
-    const uint32_t ntile = (nu + FP_B - 1) / FP_B;
+    const uint32_t ntile = (nu + FP_RT - 1) / FP_RT;
     const uint32_t ep = ctl->ep_base + r, serial = ctl->serial;
     for (uint32_t tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
-        const uint32_t i0 = tile * FP_B;
+        const uint32_t i0 = tile * FP_RT;
         if (threadIdx.x == 0) s_cnt = 0;
         __syncthreads();
-        const uint32_t n = r == 0 ? min(FP_B, nu - i0) : b.fp_tcnt[(2 * (r - 1)) * ntile + tile];
+        const uint32_t n = r == 0 ? min(FP_RT, nu - i0) : b.fp_tcnt[(2 * (r - 1)) * ntile + tile];
         const uint32_t* lin = b.fp_list + i0;
         uint32_t* lout = b.fp_list + b.m + i0;
         for (uint32_t j0 = 0; j0 < n; j0 += blockDim.x) {
@@ -4107,18 +4109,18 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_claim(ClauseView cv, LoopBuff
 // variables covered by this pass's serial); the others survive to round r + 1.
 template <uint32_t KW>
 __global__ __launch_bounds__(FP_THREADS) void k_fp_join(ClauseView cv, LoopBuffers b, uint32_t r) {
-    const RRFpCtl* ctl = b.fp_ctl;
+    RRFpCtl* ctl = b.fp_ctl;
     if (ctl->state != FP_RUN) return;
     const uint32_t nu = ctl->nu;
     __shared__ uint32_t s_cnt;
     const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
-    const uint32_t ntile = (nu + FP_B - 1) / FP_B;
+    const uint32_t ntile = (nu + FP_RT - 1) / FP_RT;
     const uint32_t ep = ctl->ep_base + r, serial = ctl->serial;
     for (uint32_t tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
-        const uint32_t i0 = tile * FP_B;
+        const uint32_t i0 = tile * FP_RT;
         if (threadIdx.x == 0) s_cnt = 0;
         __syncthreads();
-        const uint32_t n = r == 0 ? min(FP_B, nu - i0) : b.fp_tcnt[(2 * r - 1) * ntile + tile];
+        const uint32_t n = r == 0 ? min(FP_RT, nu - i0) : b.fp_tcnt[(2 * r - 1) * ntile + tile];
         const uint32_t* lin = b.fp_list + b.m + i0;
         uint32_t* lout = b.fp_list + i0;
         for (uint32_t j0 = 0; j0 < n; j0 += blockDim.x) {
@@ -4137,7 +4139,9 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_join(ClauseView cv, LoopBuffe
                 }
                 keep = !own;
             }
-            fp_append(keep, i, &s_cnt, lout);
+            // the last grid round's few survivors go to one list for k_fp_tail
+            if (r + 1 == FP_G) fp_append(keep, i, &ctl->cntJ[r], b.fp_list);
+            else fp_append(keep, i, &s_cnt, lout);
         }
         __syncthreads();
         if (threadIdx.x == 0) b.fp_tcnt[(2 * r) * ntile + tile] = s_cnt;
@@ -4156,30 +4160,9 @@ __global__ __launch_bounds__(1024) void k_fp_tail(ClauseView cv, LoopBuffers b) 
     uint32_t* la = b.fp_list;
     uint32_t* lb = b.fp_list + b.m;
     const uint32_t serial = ctl->serial, budget = fp_ep_budget(b);
-    const uint32_t nu = ctl->nu, ntile = (nu + FP_B - 1) / FP_B;
     uint32_t ep = ctl->ep_base + FP_G;
     bool failed = false;
-    // the survivors of the last grid round, tile by tile, into one list (lb)
-    if (threadIdx.x == 0) s_cnt = 0;
-    __syncthreads();
-    const uint32_t* tc = b.fp_tcnt + (2 * (FP_G - 1)) * ntile;
-    for (uint32_t t = threadIdx.x >> 6; t < ntile; t += blockDim.x >> 6) {
-        const uint32_t c = tc[t];
-        if (!c) continue;
-        uint32_t base = 0;
-        if ((threadIdx.x & 63) == 0) base = atomicAdd(&s_cnt, c);
-        base = __shfl(base, 0, 64);
-        for (uint32_t j = threadIdx.x & 63; j < c; j += 64) la[b.m + base + j] = la[(uint64_t)t * FP_B + j];
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    uint32_t n = s_cnt;
-    __syncthreads();
-    if (n) {  // back to la (the rounds below read la)
-        for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) la[j] = __hip_atomic_load(&lb[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-    }
+    uint32_t n = ctl->cntJ[FP_G - 1];  // the last grid round's survivors, listed in la
     while (n > 0) {
         if (ep >= budget) { failed = true; break; }
         if (threadIdx.x == 0) s_cnt = 0;
@@ -4296,9 +4279,11 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_count(LoopBuffers b, int test
         }
         __syncthreads();
     }
-    if (test) {
+    if (test) {  // per workgroup (k_fp_sched sums them): no contended counter
         for (int o = 32; o > 0; o >>= 1) changed += __shfl_down(changed, o, 64);
-        if ((threadIdx.x & 63) == 0 && changed) atomicAdd(&ctl->changes, changed);
+        if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = changed;
+        __syncthreads();
+        if (threadIdx.x == 0) b.fp_blk[2 * (b.m / FP_B + 2) + blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
     }
 }
 
@@ -4314,8 +4299,12 @@ __global__ __launch_bounds__(1024) void k_fp_sched(LoopBuffers b, int test) {
     __shared__ uint32_t s_w[16];
     __shared__ uint32_t s_n[FP_TMAX], s_done[FP_TMAX], s_live[FP_TMAX], s_nseg[FP_TMAX];
     const uint32_t nu = ctl->nu, T = b.rr_T, nblk = (nu + FP_B - 1) / FP_B;
-    const bool conv = test && ctl->changes == 0;
     uint32_t* blkoff = b.fp_blk + (b.m / FP_B + 2);
+    uint32_t ch = 0;  // picks changed by the last pass (k_fp_count's per-workgroup counts)
+    if (test)
+        for (uint32_t k = threadIdx.x; k < min(nblk, FP_COUNT_GRID); k += blockDim.x) ch += b.fp_blk[2 * (b.m / FP_B + 2) + k];
+    ch = __syncthreads_or(ch != 0);
+    const bool conv = test && ch == 0;
     // exclusive scan of the block counts
     uint32_t carry = 0;
     for (uint32_t k0 = 0; k0 < nblk; k0 += blockDim.x) {
@@ -4787,8 +4776,9 @@ hipError_t launch_rr_mis(const ClauseView& cv, const LoopBuffers& b, hipStream_t
     if (b.fp_ctl) {  // the fixpoint passes; k_rr_mw below only if they do not settle
         if (b.rr_T > FP_TMAX || b.fp_max == 0) return hipErrorInvalidValue;
         const bool narrow = b.rr_k >= 1 && b.rr_k <= 4;
-        const uint32_t gb = (uint32_t)std::min<uint64_t>((b.m + FP_B - 1) / FP_B + 1, 1024);
+        const uint32_t gb = (uint32_t)std::min<uint64_t>((b.m + FP_B - 1) / FP_B + 1, FP_COUNT_GRID);
         const uint32_t gl = (uint32_t)std::min<uint64_t>((b.m + FP_THREADS - 1) / FP_THREADS + 1, 2048);
+        const uint32_t gr = (uint32_t)std::min<uint64_t>((b.m + FP_RT - 1) / FP_RT + 1, 8192);
         hipError_t e = hipMemsetAsync(b.fp_owner, 0xFF, (size_t)b.n_vars * 8, s);
         if (e != hipSuccess) return e;
         k_fp_begin<<<1, 256, 0, s>>>(b);
@@ -4803,11 +4793,11 @@ hipError_t launch_rr_mis(const ClauseView& cv, const LoopBuffers& b, hipStream_t
         for (uint32_t p = 0; p < b.fp_max; ++p) {
             for (uint32_t r = 0; r < FP_G; ++r) {
                 if (narrow) {
-                    k_fp_claim<4><<<gb, FP_THREADS, 0, s>>>(cv, b, r);
-                    k_fp_join<4><<<gb, FP_THREADS, 0, s>>>(cv, b, r);
+                    k_fp_claim<4><<<gr, FP_THREADS, 0, s>>>(cv, b, r);
+                    k_fp_join<4><<<gr, FP_THREADS, 0, s>>>(cv, b, r);
                 } else {
-                    k_fp_claim<0><<<gb, FP_THREADS, 0, s>>>(cv, b, r);
-                    k_fp_join<0><<<gb, FP_THREADS, 0, s>>>(cv, b, r);
+                    k_fp_claim<0><<<gr, FP_THREADS, 0, s>>>(cv, b, r);
+                    k_fp_join<0><<<gr, FP_THREADS, 0, s>>>(cv, b, r);
                 }
             }
             if (narrow) k_fp_tail<4><<<1, 1024, 0, s>>>(cv, b);

@@ -3989,6 +3989,29 @@ __device__ __forceinline__ void fp_for_vars(const ClauseView& cv, const RREnt* U
     }
 }
 
+// the same over the variables another violated clause also holds (bit j of `sole`: slot j's
+// variable has no other claimant this iteration, so it is always owned and never covered by
+// another pick; slots past 8 are always visited)
+template <uint32_t KW, typename F>
+__device__ __forceinline__ void fp_for_shared(const ClauseView& cv, const RREnt* U, uint32_t i, const uint4& a,
+                                              const uint4& v0, uint32_t sole, F&& f) {
+    const uint32_t w = a.z;
+    if (w > 0 && !(sole & 1u)) f(v0.x);
+    if (w > 1 && !(sole & 2u)) f(v0.y);
+    if (w > 2 && !(sole & 4u)) f(v0.z);
+    if (w > 3 && !(sole & 8u)) f(v0.w);
+    if constexpr (KW == 0) {
+        if (w > 4 && (sole & 0xF0u) != 0xF0u) {
+            const uint4 v1 = U[i].v1;
+            if (!(sole & 16u)) f(v1.x);
+            if (w > 5 && !(sole & 32u)) f(v1.y);
+            if (w > 6 && !(sole & 64u)) f(v1.z);
+            if (w > 7 && !(sole & 128u)) f(v1.w);
+        }
+        for (uint32_t j = 8; j < w; ++j) f(lit_var(cv.lits[a.y + j]));
+    }
+}
+
 // largest s < T with sf[s] <= i (sf non-decreasing, sf[0] = 0): the set of entry i < nu
 __device__ __forceinline__ uint32_t fp_set_of(const uint32_t* sf, uint32_t T, uint32_t i) {
     uint32_t lo = 0, hi = T;
@@ -4043,18 +4066,41 @@ __global__ __launch_bounds__(256) void k_fp_begin(LoopBuffers b) {
     }
 }
 
-// The first pass's input: picks spread evenly over every set at density num / den.
-__global__ __launch_bounds__(FP_THREADS) void k_fp_guess(LoopBuffers b) {
+// Violated claimants per variable (fp_deg, zeroed before), for the sole-claimant masks.
+template <uint32_t KW>
+__global__ __launch_bounds__(FP_THREADS) void k_fp_deg(ClauseView cv, LoopBuffers b) {
+    const RRFpCtl* ctl = b.fp_ctl;
+    if (ctl->state != FP_RUN) return;
+    const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
+    const uint32_t nu = ctl->nu;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nu; i += gridDim.x * blockDim.x) {
+        const uint4 a = U[i].a, v0 = U[i].v0;
+        fp_for_vars<KW>(cv, U, i, a, v0, [&](uint32_t v) { atomicAdd(&b.fp_deg[v], 1u); });
+    }
+}
+
+// The first pass's input: picks spread evenly over every set at density num / den; and every
+// entry's sole-claimant mask (bit j: slot j's variable has no other violated claimant).
+template <uint32_t KW>
+__global__ __launch_bounds__(FP_THREADS) void k_fp_guess(ClauseView cv, LoopBuffers b) {
     const RRFpCtl* ctl = b.fp_ctl;
     if (ctl->state != FP_RUN) return;
     __shared__ uint32_t s_sf[FP_TMAX + 1];
     const uint32_t T = b.rr_T, nu = ctl->nu;
     const unsigned long long num = ctl->guess_num, den = ctl->guess_den;
+    const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
     for (uint32_t s = threadIdx.x; s <= T; s += blockDim.x) s_sf[s] = b.fp_sf[s];
     __syncthreads();
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nu; i += gridDim.x * blockDim.x) {
         const unsigned long long pos = i - s_sf[fp_set_of(s_sf, T, i)];
         b.fp_in[i] = (uint8_t)((pos + 1) * num / den > pos * num / den);
+        const uint4 a = U[i].a, v0 = U[i].v0;
+        uint32_t sole = 0, j = 0;
+        fp_for_vars<KW>(cv, U, i, a, v0, [&](uint32_t v) {
+            if (j < 8 && b.fp_deg[v] == 1u) sole |= 1u << j;
+            ++j;
+        });
+        b.fp_sole[i] = (uint8_t)sole;
     }
 }
 
@@ -4085,13 +4131,14 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_claim(ClauseView cv, LoopBuff
             if (j < n) {
                 i = r == 0 ? i0 + j : lin[j];
                 const uint4 a = U[i].a, v0 = U[i].v0;
+                const uint32_t sole = b.fp_sole[i];
                 const uint32_t turn = b.fp_turn[i];
                 bool dead = false;
-                if (r > 0) fp_for_vars<KW>(cv, U, i, a, v0, [&](uint32_t v) { dead |= b.fp_cov[v] == serial; });
+                if (r > 0) fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) { dead |= b.fp_cov[v] == serial; });
                 else b.fp_in[i] = (uint8_t)((b.fp_in[i] & 1u) << 1);
                 if (!dead) {
                     const unsigned long long key = fp_key(b, ep, turn, i);
-                    fp_for_vars<KW>(cv, U, i, a, v0, [&](uint32_t v) { atomicMin(&b.fp_owner[v], key); });
+                    fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) { atomicMin(&b.fp_owner[v], key); });
                     keep = true;
                 }
             }
@@ -4130,11 +4177,12 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_join(ClauseView cv, LoopBuffe
             if (j < n) {
                 i = r == 0 ? i0 + j : lin[j];
                 const uint4 a = U[i].a, v0 = U[i].v0;
+                const uint32_t sole = b.fp_sole[i];
                 const unsigned long long key = fp_key(b, ep, b.fp_turn[i], i);
                 bool own = true;
-                fp_for_vars<KW>(cv, U, i, a, v0, [&](uint32_t v) { own &= b.fp_owner[v] == key; });
+                fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) { own &= b.fp_owner[v] == key; });
                 if (own) {
-                    fp_for_vars<KW>(cv, U, i, a, v0, [&](uint32_t v) { b.fp_cov[v] = serial; });
+                    fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) { b.fp_cov[v] = serial; });
                     b.fp_in[i] = (uint8_t)(b.fp_in[i] | 1u);
                 }
                 keep = !own;
@@ -4174,13 +4222,14 @@ __global__ __launch_bounds__(1024) void k_fp_tail(ClauseView cv, LoopBuffers b) 
             if (j < n) {
                 i = la[j];
                 const uint4 a = U[i].a, v0 = U[i].v0;
+                const uint32_t sole = b.fp_sole[i];
                 bool dead = false;
-                fp_for_vars<KW>(cv, U, i, a, v0, [&](uint32_t v) {
+                fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) {
                     dead |= __hip_atomic_load(&b.fp_cov[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == serial;
                 });
                 if (!dead) {
                     const unsigned long long key = fp_key(b, ep, b.fp_turn[i], i);
-                    fp_for_vars<KW>(cv, U, i, a, v0, [&](uint32_t v) { atomicMin(&b.fp_owner[v], key); });
+                    fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) { atomicMin(&b.fp_owner[v], key); });
                     keep = true;
                 }
             }
@@ -4199,13 +4248,14 @@ __global__ __launch_bounds__(1024) void k_fp_tail(ClauseView cv, LoopBuffers b) 
             if (j < nc) {
                 i = lb[j];
                 const uint4 a = U[i].a, v0 = U[i].v0;
+                const uint32_t sole = b.fp_sole[i];
                 const unsigned long long key = fp_key(b, ep, b.fp_turn[i], i);
                 bool own = true;
-                fp_for_vars<KW>(cv, U, i, a, v0, [&](uint32_t v) {
+                fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) {
                     own &= __hip_atomic_load(&b.fp_owner[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == key;
                 });
                 if (own) {
-                    fp_for_vars<KW>(cv, U, i, a, v0, [&](uint32_t v) {
+                    fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) {
                         __hip_atomic_store(&b.fp_cov[v], serial, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     });
                     b.fp_in[i] = (uint8_t)(b.fp_in[i] | 1u);
@@ -4781,8 +4831,16 @@ hipError_t launch_rr_mis(const ClauseView& cv, const LoopBuffers& b, hipStream_t
         const uint32_t gr = (uint32_t)std::min<uint64_t>((b.m + FP_RT - 1) / FP_RT + 1, 8192);
         hipError_t e = hipMemsetAsync(b.fp_owner, 0xFF, (size_t)b.n_vars * 8, s);
         if (e != hipSuccess) return e;
+        e = hipMemsetAsync(b.fp_deg, 0, (size_t)b.n_vars * 4, s);
+        if (e != hipSuccess) return e;
         k_fp_begin<<<1, 256, 0, s>>>(b);
-        k_fp_guess<<<gl, FP_THREADS, 0, s>>>(b);
+        if (narrow) {
+            k_fp_deg<4><<<gl, FP_THREADS, 0, s>>>(cv, b);
+            k_fp_guess<4><<<gl, FP_THREADS, 0, s>>>(cv, b);
+        } else {
+            k_fp_deg<0><<<gl, FP_THREADS, 0, s>>>(cv, b);
+            k_fp_guess<0><<<gl, FP_THREADS, 0, s>>>(cv, b);
+        }
         auto turns = [&](int test) {
             k_fp_count<<<gb, FP_THREADS, 0, s>>>(b, test);
             k_fp_sched<<<1, 1024, 0, s>>>(b, test);

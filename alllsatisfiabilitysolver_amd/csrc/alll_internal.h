@@ -221,6 +221,9 @@ struct LoopBuffers {
     uint32_t* fp_cov;           // n_vars: serial of the pass whose pick covers the variable
     uint32_t* fp_deg;           // n_vars: violated claimants this iteration
     uint8_t* fp_sole;           // per scan entry: bit j = slot j's variable has no other claimant
+    uint32_t* fp_voff;          // n_vars + 1: list range of every variable (shared variables only)
+    uint32_t* fp_vlist;         // violated claimants of the shared variables (scan entries)
+    uint32_t* fp_vblk;          // block sums / offsets of the list lengths
     uint32_t* fp_blk;           // 2 x blocks: pick counts, then their exclusive prefix
     uint32_t* fp_sf;            // T + 1: first scan entry of every set (entries past the last: nu)
     uint32_t* fp_bnd;           // T + 1: picks before the set's first entry inside its block

@@ -4104,9 +4104,128 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_guess(ClauseView cv, LoopBuff
     }
 }
 
-// CLAIM(r), a workgroup per round tile of FP_RT entries: round 0 takes the tile's entries (and moves
-// the picks of the last pass to bit 1); later rounds take the tile's JOIN(r-1) survivors, drop
-// those a pick of this pass covers, and list the rest.  Lists are per tile (slots
+// Workgroup exclusive scan of one value per thread (blockDim.x <= 1024); returns the total too.
+__device__ __forceinline__ uint32_t fp_block_scan(uint32_t x, uint32_t* s_w, uint32_t& total) {
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    uint32_t incl = x;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o, 64);
+        if ((int)lane >= o) incl += y;
+    }
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    uint32_t before = 0;
+    total = 0;
+    for (uint32_t w = 0; w < nw; ++w) {
+        const uint32_t c = s_w[w];
+        if (w < wave) before += c;
+        total += c;
+    }
+    __syncthreads();
+    return before + incl - x;
+}
+
+// Round 0 without atomics: the violated claimants of every shared variable (two or more) in
+// a CSR built once per iteration (fp_voff / fp_vlist); each pass's round-0 owner of such a
+// variable is then the minimum key over its list (k_fp_vmin, a thread per variable, plain
+// stores), which CLAIM(0)'s atomics computed before.  Block sums of the list lengths:
+__global__ __launch_bounds__(FP_THREADS) void k_fp_vcount(LoopBuffers b) {
+    const RRFpCtl* ctl = b.fp_ctl;
+    if (ctl->state != FP_RUN) return;
+    __shared__ uint32_t s_w[FP_THREADS / 64];
+    const uint32_t nv = b.n_vars, nblk = (nv + FP_B - 1) / FP_B;
+    for (uint32_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+        uint32_t acc = 0;
+        for (uint32_t e = 0; e < FP_PER; ++e) {
+            const uint32_t v = blk * FP_B + e * FP_THREADS + threadIdx.x;
+            const uint32_t d = v < nv ? b.fp_deg[v] : 0u;
+            acc += d >= 2 ? d : 0u;
+        }
+        uint32_t tot;
+        (void)fp_block_scan(acc, s_w, tot);
+        if (threadIdx.x == 0) b.fp_vblk[blk] = tot;
+    }
+}
+
+// exclusive scan of the block sums (one workgroup)
+__global__ __launch_bounds__(1024) void k_fp_vscan(LoopBuffers b) {
+    const RRFpCtl* ctl = b.fp_ctl;
+    if (ctl->state != FP_RUN) return;
+    __shared__ uint32_t s_w[16];
+    const uint32_t nblk = (b.n_vars + FP_B - 1) / FP_B;
+    uint32_t carry = 0;
+    for (uint32_t k0 = 0; k0 < nblk; k0 += blockDim.x) {
+        const uint32_t k = k0 + threadIdx.x;
+        const uint32_t x = k < nblk ? b.fp_vblk[k] : 0u;
+        uint32_t tot;
+        const uint32_t ex = fp_block_scan(x, s_w, tot);
+        if (k < nblk) b.fp_vblk[k] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) b.fp_voff[b.n_vars] = carry;
+}
+
+// list offsets of every variable (shared variables only have non-empty ranges)
+__global__ __launch_bounds__(FP_THREADS) void k_fp_voff(LoopBuffers b) {
+    const RRFpCtl* ctl = b.fp_ctl;
+    if (ctl->state != FP_RUN) return;
+    __shared__ uint32_t s_w[FP_THREADS / 64];
+    const uint32_t nv = b.n_vars, nblk = (nv + FP_B - 1) / FP_B;
+    for (uint32_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
+        const uint32_t v0 = blk * FP_B + threadIdx.x * FP_PER;  // 8 consecutive variables per thread
+        uint32_t d[FP_PER], acc = 0;
+        for (uint32_t e = 0; e < FP_PER; ++e) {
+            const uint32_t v = v0 + e;
+            const uint32_t x = v < nv ? b.fp_deg[v] : 0u;
+            d[e] = x >= 2 ? x : 0u;
+            acc += d[e];
+        }
+        uint32_t tot;
+        uint32_t off = b.fp_vblk[blk] + fp_block_scan(acc, s_w, tot);
+        for (uint32_t e = 0; e < FP_PER; ++e) {
+            if (v0 + e < nv) b.fp_voff[v0 + e] = off;
+            off += d[e];
+        }
+    }
+}
+
+// entries into the lists of their shared variables (fills each list from its end: the degree
+// counts down; the sole masks were taken from it already)
+template <uint32_t KW>
+__global__ __launch_bounds__(FP_THREADS) void k_fp_vfill(ClauseView cv, LoopBuffers b) {
+    const RRFpCtl* ctl = b.fp_ctl;
+    if (ctl->state != FP_RUN) return;
+    const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
+    const uint32_t nu = ctl->nu;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nu; i += gridDim.x * blockDim.x) {
+        const uint4 a = U[i].a, v0 = U[i].v0;
+        fp_for_shared<KW>(cv, U, i, a, v0, b.fp_sole[i], [&](uint32_t v) {
+            const uint32_t o = b.fp_voff[v];
+            if (b.fp_voff[v + 1] - o >= 2) b.fp_vlist[o + atomicSub(&b.fp_deg[v], 1u) - 1u] = i;
+        });
+    }
+}
+
+// round 0 of a pass: the minimum key over every shared variable's claimants
+__global__ __launch_bounds__(FP_THREADS) void k_fp_vmin(LoopBuffers b) {
+    const RRFpCtl* ctl = b.fp_ctl;
+    if (ctl->state != FP_RUN) return;
+    const uint32_t ep = ctl->ep_base, nv = b.n_vars;
+    for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += gridDim.x * blockDim.x) {
+        const uint32_t o0 = b.fp_voff[v], o1 = b.fp_voff[v + 1];
+        if (o1 - o0 < 2) continue;
+        unsigned long long best = ~0ull;
+        for (uint32_t o = o0; o < o1; ++o) {
+            const uint32_t i = b.fp_vlist[o];
+            const unsigned long long k = fp_key(b, ep, b.fp_turn[i], i);
+            best = k < best ? k : best;
+        }
+        b.fp_owner[v] = best;
+    }
+}
+
+// CLAIM(r), r >= 1 (round 0 is k_fp_vmin), a workgroup per round tile of FP_RT entries: the
+// tile's JOIN(r-1) survivors, less those a pick of this pass covers, claim and are listed.  Lists are per tile (slots
 // [tile * FP_RT, +count)), counted in LDS: no global counter.
 template <uint32_t KW>
 __global__ __launch_bounds__(FP_THREADS) void k_fp_claim(ClauseView cv, LoopBuffers b, uint32_t r) {
@@ -4121,7 +4240,7 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_claim(ClauseView cv, LoopBuff
         const uint32_t i0 = tile * FP_RT;
         if (threadIdx.x == 0) s_cnt = 0;
         __syncthreads();
-        const uint32_t n = r == 0 ? min(FP_RT, nu - i0) : b.fp_tcnt[(2 * (r - 1)) * ntile + tile];
+        const uint32_t n = b.fp_tcnt[(2 * (r - 1)) * ntile + tile];
         const uint32_t* lin = b.fp_list + i0;
         uint32_t* lout = b.fp_list + b.m + i0;
         for (uint32_t j0 = 0; j0 < n; j0 += blockDim.x) {
@@ -4129,25 +4248,22 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_claim(ClauseView cv, LoopBuff
             bool keep = false;
             uint32_t i = 0;
             if (j < n) {
-                i = r == 0 ? i0 + j : lin[j];
+                i = lin[j];
                 const uint4 a = U[i].a, v0 = U[i].v0;
                 const uint32_t sole = b.fp_sole[i];
                 const uint32_t turn = b.fp_turn[i];
                 bool dead = false;
-                if (r > 0) fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) { dead |= b.fp_cov[v] == serial; });
-                else b.fp_in[i] = (uint8_t)((b.fp_in[i] & 1u) << 1);
+                fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) { dead |= b.fp_cov[v] == serial; });
                 if (!dead) {
                     const unsigned long long key = fp_key(b, ep, turn, i);
                     fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) { atomicMin(&b.fp_owner[v], key); });
                     keep = true;
                 }
             }
-            if (r > 0) fp_append(keep, i, &s_cnt, lout);
+            fp_append(keep, i, &s_cnt, lout);
         }
-        if (r > 0) {
-            __syncthreads();
-            if (threadIdx.x == 0) b.fp_tcnt[(2 * r - 1) * ntile + tile] = s_cnt;
-        }
+        __syncthreads();
+        if (threadIdx.x == 0) b.fp_tcnt[(2 * r - 1) * ntile + tile] = s_cnt;
         __syncthreads();
     }
 }
@@ -4276,26 +4392,6 @@ __global__ __launch_bounds__(1024) void k_fp_tail(ClauseView cv, LoopBuffers b) 
     }
 }
 
-// Workgroup exclusive scan of one value per thread (blockDim.x <= 1024); returns the total too.
-__device__ __forceinline__ uint32_t fp_block_scan(uint32_t x, uint32_t* s_w, uint32_t& total) {
-    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    uint32_t incl = x;
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(incl, o, 64);
-        if ((int)lane >= o) incl += y;
-    }
-    if (lane == 63) s_w[wave] = incl;
-    __syncthreads();
-    uint32_t before = 0;
-    total = 0;
-    for (uint32_t w = 0; w < nw; ++w) {
-        const uint32_t c = s_w[w];
-        if (w < wave) before += c;
-        total += c;
-    }
-    __syncthreads();
-    return before + incl - x;
-}
 
 // Picks per block of FP_B entries, picks before every set start that falls in the block, and
 // (test) the picks that changed since the previous pass.
@@ -4384,7 +4480,42 @@ __global__ __launch_bounds__(1024) void k_fp_sched(LoopBuffers b, int test) {
     // index x takes its j-th turn of the phase at step + j L + o(x), o(x) = (x - t - 1) mod L;
     // the first set to run out of picks is erased at its next turn E = step + min(r L + o), r =
     // picks left; then t = its index (the reference's t is not decremented).
-    if (threadIdx.x < 64) {
+    if (T <= 64) {
+        // up to 64 sets: lane s keeps set s's state in registers, the live list is a lane mask
+        // (live index = the lanes below it), and a phase is one wave minimum
+        if (threadIdx.x < 64) {
+            const uint32_t lane = threadIdx.x;
+            const uint32_t n = s_n[lane < T ? lane : 0];
+            uint32_t done = 0, nseg = 0, t = 0, step = 0;
+            unsigned long long alive = T == 64 ? ~0ull : (1ull << T) - 1ull;
+            for (uint32_t p = 0; p < T; ++p) {
+                const uint32_t L = (uint32_t)__popcll(alive);
+                const bool live = (alive >> lane) & 1ull;
+                const uint32_t x = (uint32_t)__popcll(alive & ((1ull << lane) - 1ull));
+                const uint32_t o = (x + L - (t % L) - 1) % L;
+                unsigned long long best = live ? (((unsigned long long)(n - done) * L + o) << 6 | lane) : ~0ull;
+                for (int q = 32; q > 0; q >>= 1) {
+                    const unsigned long long y = __shfl_xor(best, q, 64);
+                    best = y < best ? y : best;
+                }
+                const uint32_t ls = (uint32_t)(best & 63u);
+                const unsigned long long d = best >> 6;
+                if (live) {
+                    const uint32_t cnt = lane == ls ? n - done : (d > o ? (uint32_t)((d - o + L - 1) / L) : 0u);
+                    b.fp_seg[(uint64_t)lane * T + nseg] = make_uint4(done, step, L, o);
+                    nseg += 1;
+                    done += cnt;
+                }
+                const uint32_t E = step + (uint32_t)d;
+                if (lane == 0) b.fp_erase[p] = E;
+                t = (uint32_t)__popcll(alive & ((1ull << ls) - 1ull));
+                alive &= ~(1ull << ls);
+                step = E + 1;
+            }
+            if (lane < T) s_nseg[lane] = nseg;
+            if (lane == 0) ctl->n_steps = step;
+        }
+    } else if (threadIdx.x < 64) {
         const uint32_t lane = threadIdx.x;
         uint32_t L = T, t = 0, step = 0;
         for (uint32_t p = 0; p < T; ++p) {
@@ -4485,6 +4616,8 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_turn(ClauseView cv, LoopBuffe
         const unsigned long long b0 = x & 0x0101010101010101ull;
         uint32_t tot;
         uint32_t P = blkoff[blk] + fp_block_scan((uint32_t)__popcll(b0), s_w, tot);
+        // the next pass sets bit 0 of its picks; these become bit 1 (k_fp_count compares them)
+        if (!fin && i0 < nu) *reinterpret_cast<unsigned long long*>(b.fp_in + i0) = b0 << 1;
         if (i0 < nu) {
             uint32_t s = fp_set_of(s_sf, T, i0);
             const uint32_t e1 = min(nu - i0, FP_PER);
@@ -4841,6 +4974,13 @@ hipError_t launch_rr_mis(const ClauseView& cv, const LoopBuffers& b, hipStream_t
             k_fp_deg<0><<<gl, FP_THREADS, 0, s>>>(cv, b);
             k_fp_guess<0><<<gl, FP_THREADS, 0, s>>>(cv, b);
         }
+        const uint32_t gv = (uint32_t)std::min<uint64_t>((b.n_vars + FP_B - 1) / FP_B + 1, FP_COUNT_GRID);
+        const uint32_t gvt = (uint32_t)std::min<uint64_t>((b.n_vars + FP_THREADS - 1) / FP_THREADS + 1, 2048);
+        k_fp_vcount<<<gv, FP_THREADS, 0, s>>>(b);
+        k_fp_vscan<<<1, 1024, 0, s>>>(b);
+        k_fp_voff<<<gv, FP_THREADS, 0, s>>>(b);
+        if (narrow) k_fp_vfill<4><<<gl, FP_THREADS, 0, s>>>(cv, b);
+        else k_fp_vfill<0><<<gl, FP_THREADS, 0, s>>>(cv, b);
         auto turns = [&](int test) {
             k_fp_count<<<gb, FP_THREADS, 0, s>>>(b, test);
             k_fp_sched<<<1, 1024, 0, s>>>(b, test);
@@ -4850,7 +4990,11 @@ hipError_t launch_rr_mis(const ClauseView& cv, const LoopBuffers& b, hipStream_t
         turns(0);
         for (uint32_t p = 0; p < b.fp_max; ++p) {
             for (uint32_t r = 0; r < FP_G; ++r) {
-                if (narrow) {
+                if (r == 0) {
+                    k_fp_vmin<<<gvt, FP_THREADS, 0, s>>>(b);
+                    if (narrow) k_fp_join<4><<<gr, FP_THREADS, 0, s>>>(cv, b, 0);
+                    else k_fp_join<0><<<gr, FP_THREADS, 0, s>>>(cv, b, 0);
+                } else if (narrow) {
                     k_fp_claim<4><<<gr, FP_THREADS, 0, s>>>(cv, b, r);
                     k_fp_join<4><<<gr, FP_THREADS, 0, s>>>(cv, b, r);
                 } else {

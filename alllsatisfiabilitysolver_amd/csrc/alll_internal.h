@@ -78,7 +78,9 @@ struct RRFpCtl {
     uint32_t total;      // picks of the last pass
     uint32_t guess_num, guess_den;  // previous iteration's |M| / |U| (initial pick density)
     uint32_t n_steps;    // schedule length (turns + erasures)
-    uint32_t pad[5];
+    uint32_t tpre;       // entries whose turn is below this keep the last pass's decision
+    uint32_t e0;         // first erasure step of the last schedule
+    uint32_t pad[3];
     uint32_t cntJ[16];   // survivors of JOIN(r)
     uint32_t cntC[16];   // claimers of CLAIM(r)
 };

@@ -4062,6 +4062,8 @@ __global__ __launch_bounds__(256) void k_fp_begin(LoopBuffers b) {
         ctl->changes = 0;
         ctl->ep_base = 0;
         ctl->ep_next = 0;
+        ctl->tpre = 0;
+        ctl->e0 = ~0u;
         if (ctl->guess_den == 0) { ctl->guess_num = 1; ctl->guess_den = 2; }
     }
 }
@@ -4278,7 +4280,7 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_join(ClauseView cv, LoopBuffe
     __shared__ uint32_t s_cnt;
     const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
     const uint32_t ntile = (nu + FP_RT - 1) / FP_RT;
-    const uint32_t ep = ctl->ep_base + r, serial = ctl->serial;
+    const uint32_t ep = ctl->ep_base + r, serial = ctl->serial, tpre = ctl->tpre;
     for (uint32_t tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
         const uint32_t i0 = tile * FP_RT;
         if (threadIdx.x == 0) s_cnt = 0;
@@ -4294,14 +4296,20 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_join(ClauseView cv, LoopBuffe
                 i = r == 0 ? i0 + j : lin[j];
                 const uint4 a = U[i].a, v0 = U[i].v0;
                 const uint32_t sole = b.fp_sole[i];
-                const unsigned long long key = fp_key(b, ep, b.fp_turn[i], i);
-                bool own = true;
-                fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) { own &= b.fp_owner[v] == key; });
+                const uint32_t turn = b.fp_turn[i];
+                bool own = true, pre = false;
+                if (r == 0 && turn < tpre) {  // decided as in the last pass (bit 1)
+                    pre = true;
+                    own = (b.fp_in[i] >> 1) & 1u;
+                } else {
+                    const unsigned long long key = fp_key(b, ep, turn, i);
+                    fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) { own &= b.fp_owner[v] == key; });
+                }
                 if (own) {
                     fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) { b.fp_cov[v] = serial; });
                     b.fp_in[i] = (uint8_t)(b.fp_in[i] | 1u);
                 }
-                keep = !own;
+                keep = !own && !pre;
             }
             // the last grid round's few survivors go to one list for k_fp_tail
             if (r + 1 == FP_G) fp_append(keep, i, &ctl->cntJ[r], b.fp_list);
@@ -4400,7 +4408,7 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_count(LoopBuffers b, int test
     if (ctl->state != FP_RUN) return;
     __shared__ uint32_t s_w[FP_THREADS / 64], s_ex[FP_THREADS], s_bits[FP_THREADS];
     const uint32_t nu = ctl->nu, T = b.rr_T, nblk = (nu + FP_B - 1) / FP_B;
-    uint32_t changed = 0;
+    uint32_t changed = 0, tmin = ~0u;
     for (uint32_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
         const uint32_t i0 = blk * FP_B + threadIdx.x * FP_PER;
         unsigned long long x = 0;
@@ -4411,6 +4419,11 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_count(LoopBuffers b, int test
         const unsigned long long b0 = x & 0x0101010101010101ull, b1 = (x >> 1) & 0x0101010101010101ull;
         const uint32_t cnt = (uint32_t)__popcll(b0);
         changed += (uint32_t)__popcll(b0 ^ b1);
+        if (test && (b0 ^ b1)) {  // the earliest turn (of the last pass) whose decision changed
+            const unsigned long long d = b0 ^ b1;
+            for (uint32_t e = 0; e < FP_PER; ++e)
+                if ((d >> (8 * e)) & 1ull) tmin = min(tmin, b.fp_turn[i0 + e]);
+        }
         uint32_t total;
         const uint32_t ex = fp_block_scan(cnt, s_w, total);
         s_ex[threadIdx.x] = ex;
@@ -4430,6 +4443,12 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_count(LoopBuffers b, int test
         if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = changed;
         __syncthreads();
         if (threadIdx.x == 0) b.fp_blk[2 * (b.m / FP_B + 2) + blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+        for (int o = 32; o > 0; o >>= 1) tmin = min(tmin, (uint32_t)__shfl_down(tmin, o, 64));
+        __syncthreads();
+        if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = tmin;
+        __syncthreads();
+        if (threadIdx.x == 0)
+            b.fp_blk[2 * (b.m / FP_B + 2) + FP_COUNT_GRID + blockIdx.x] = min(min(s_w[0], s_w[1]), min(s_w[2], s_w[3]));
     }
 }
 
@@ -4446,10 +4465,23 @@ __global__ __launch_bounds__(1024) void k_fp_sched(LoopBuffers b, int test) {
     __shared__ uint32_t s_n[FP_TMAX], s_done[FP_TMAX], s_live[FP_TMAX], s_nseg[FP_TMAX];
     const uint32_t nu = ctl->nu, T = b.rr_T, nblk = (nu + FP_B - 1) / FP_B;
     uint32_t* blkoff = b.fp_blk + (b.m / FP_B + 2);
-    uint32_t ch = 0;  // picks changed by the last pass (k_fp_count's per-workgroup counts)
+    uint32_t ch = 0, tmin = ~0u;  // picks changed by the last pass, their earliest turn (per k_fp_count workgroup)
     if (test)
-        for (uint32_t k = threadIdx.x; k < min(nblk, FP_COUNT_GRID); k += blockDim.x) ch += b.fp_blk[2 * (b.m / FP_B + 2) + k];
+        for (uint32_t k = threadIdx.x; k < min(nblk, FP_COUNT_GRID); k += blockDim.x) {
+            ch += b.fp_blk[2 * (b.m / FP_B + 2) + k];
+            tmin = min(tmin, b.fp_blk[2 * (b.m / FP_B + 2) + FP_COUNT_GRID + k]);
+        }
     ch = __syncthreads_or(ch != 0);
+    for (int o = 32; o > 0; o >>= 1) tmin = min(tmin, (uint32_t)__shfl_down(tmin, o, 64));
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = tmin;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (uint32_t w = 1; w < (blockDim.x >> 6); ++w) tmin = min(tmin, s_w[w]);
+        s_w[0] = tmin;
+    }
+    __syncthreads();
+    tmin = s_w[0];
+    __syncthreads();
     const bool conv = test && ch == 0;
     // exclusive scan of the block counts
     uint32_t carry = 0;
@@ -4566,6 +4598,11 @@ __global__ __launch_bounds__(1024) void k_fp_sched(LoopBuffers b, int test) {
     if (threadIdx.x == 0) {
         ctl->total = total;
         ctl->changes = 0;
+        // The next pass keeps the decisions below min(earliest changed turn, both schedules'
+        // first erasure): there the turns did not change, so neither did the sub-problem.
+        const uint32_t e0 = b.fp_erase[0];
+        ctl->tpre = test ? min(tmin, min(e0, ctl->e0)) : 0u;
+        ctl->e0 = e0;
         if (conv) {
             ctl->state = FP_FINAL;
             ctl->guess_num = total;

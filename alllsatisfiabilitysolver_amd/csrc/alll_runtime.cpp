@@ -773,7 +773,7 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
             if ((rc = dalloc(c, &b.fp_voff, (size_t)prob->n_vars + 2))) return bail(rc);
             if ((rc = dalloc(c, &b.fp_vlist, (size_t)L + 1))) return bail(rc);
             if ((rc = dalloc(c, &b.fp_vblk, (size_t)prob->n_vars / FP_B + 2))) return bail(rc);
-            if ((rc = dalloc(c, &b.fp_blk, 2 * nblk + 1024))) return bail(rc);  // sums, offsets, changes
+            if ((rc = dalloc(c, &b.fp_blk, 2 * nblk + 2048))) return bail(rc);  // sums, offsets, changes, earliest changes
             if ((rc = dalloc(c, &b.fp_sf, rr_T + 1))) return bail(rc);
             if ((rc = dalloc(c, &b.fp_bnd, rr_T + 1))) return bail(rc);
             if ((rc = dalloc(c, &b.fp_pf, rr_T + 1))) return bail(rc);

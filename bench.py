@@ -147,6 +147,37 @@ def cpu_baseline(cfg, budget_s):
             "sample": f"oracle serial restatement, {it} iterations on n={ns}, m={ms}; host {cpu_model()}"}
 
 
+def rr_line(args, n, m, k, kind, Solver, generate_ksat, device, warmup=2, steps=10):
+    """GPU resample loop with the reference's n_threads = T round-robin MIS, T = the CPU
+    baseline's thread count."""
+    import torch
+
+    T = cpu_threads()[0]
+    if isinstance(k, tuple):
+        from alllsatisfiabilitysolver_amd import generate_mixed
+
+        offs, lits = generate_mixed(1, n, m, *k)
+    else:
+        offs, lits = generate_ksat(1, n, m, k, kind)
+    with Solver(n, offs, lits, seed=args.seed, device=device, n_threads=T) as r:
+        del offs, lits
+        r.run(warmup)
+        r.synchronize()
+        it0 = r.stats()["n_iterations"]
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        r.run(steps)
+        r.synchronize()
+        torch.cuda.synchronize(device)
+        dt = time.perf_counter() - t0
+        st = r.stats()
+    done = st["n_iterations"] - it0
+    return {"value": m * done / dt if done else None, "unit": "clause-evals/s", "n_threads": T,
+            "resample_iters_per_s": done / dt if done else None, "ms_per_step": dt * 1e3 / done if done else None,
+            "steps": done, "warmup": warmup, "passes_last_iter": st["lfmis_tail_rounds"],
+            "mis": "round robin over T clause chunks (SATInstance.h:414-447), as the cpu_baseline's -p T path"}
+
+
 def launch_ranks(args):
     """--gpus N > 1 without a launcher: start N rank processes (one per GPU) through
     torch.distributed.run and exit with its status.  This process never touches the GPU."""
@@ -179,6 +210,8 @@ def main():
     ap.add_argument("--atomic-claims", action="store_true", help="LFMIS round 0 by global atomics")
     ap.add_argument("--grid-rounds", type=int, default=0, help="full-grid LFMIS rounds (0 = default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-rr-line", action="store_true",
+                    help="skip the GPU run with the CPU baseline's round-robin MIS (n_threads = T)")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--event-iters", type=int, default=10,
                     help="iterations replayed eagerly with HIP events around each phase (cross-check)")
@@ -381,6 +414,14 @@ def main():
             },
         }
     s.close()
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.no_rr_line:
+        # the CPU baseline runs the reference's -p T path, whose MIS is the T-set round robin
+        # (SATInstance.h:414-447), not the one-set LFMIS timed above: the same workload with that
+        # same MIS on the GPU, for a like-for-like ratio
+        try:
+            out["gpu_same_mis_as_cpu_baseline"] = rr_line(args, n, m, k, kind, Solver, generate_ksat, local_rank)
+        except Exception as e:  # reported, never fatal for the GPU number
+            out["gpu_same_mis_as_cpu_baseline"] = {"value": None, "error": str(e)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             out["cpu_baseline"] = cpu_baseline(args.config, args.cpu_budget)

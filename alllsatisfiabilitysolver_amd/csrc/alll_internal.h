@@ -221,7 +221,9 @@ struct LoopBuffers {
     uint32_t* fp_tcnt;          // 2 FP_G x tiles: list lengths per round and tile
     unsigned long long* fp_owner; // n_vars claim keys {epoch | turn | entry}, reset every iteration
     uint32_t* fp_cov;           // n_vars: serial of the pass whose pick covers the variable
-    uint32_t* fp_deg;           // n_vars: violated claimants this iteration
+    uint32_t* fp_deg;           // n_vars: violated claimants this iteration (slots 0..7 of their clauses)
+    uint32_t* fp_deg_hi;        // n_vars: the same from slots past 8 (wide clauses)
+    uint32_t* fp_rank;          // 8 per scan entry: slot j's place in its variable's claimant list
     uint8_t* fp_sole;           // per scan entry: bit j = slot j's variable has no other claimant
     uint32_t* fp_voff;          // n_vars + 1: list range of every variable (shared variables only)
     uint32_t* fp_vlist;         // violated claimants of the shared variables (scan entries)

@@ -4077,32 +4077,32 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_deg(ClauseView cv, LoopBuffer
     const uint32_t nu = ctl->nu;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nu; i += gridDim.x * blockDim.x) {
         const uint4 a = U[i].a, v0 = U[i].v0;
-        fp_for_vars<KW>(cv, U, i, a, v0, [&](uint32_t v) { atomicAdd(&b.fp_deg[v], 1u); });
+        // slots 0..7 keep the rank their count returned (their place in the variable's list);
+        // further slots (wide clauses) are counted apart and placed by a second counter
+        uint32_t rk[8], j = 0;
+        fp_for_vars<KW>(cv, U, i, a, v0, [&](uint32_t v) {
+            if (j < 8) rk[j] = atomicAdd(&b.fp_deg[v], 1u);
+            else atomicAdd(&b.fp_deg_hi[v], 1u);
+            ++j;
+        });
+        uint4* rp = reinterpret_cast<uint4*>(b.fp_rank) + 2 * (uint64_t)i;
+        rp[0] = make_uint4(rk[0], rk[1], rk[2], rk[3]);
+        if (KW == 0 && a.z > 4) rp[1] = make_uint4(rk[4], rk[5], rk[6], rk[7]);
     }
 }
 
-// The first pass's input: picks spread evenly over every set at density num / den; and every
-// entry's sole-claimant mask (bit j: slot j's variable has no other violated claimant).
-template <uint32_t KW>
-__global__ __launch_bounds__(FP_THREADS) void k_fp_guess(ClauseView cv, LoopBuffers b) {
+// The first pass's input: picks spread evenly over every set at density num / den.
+__global__ __launch_bounds__(FP_THREADS) void k_fp_guess(LoopBuffers b) {
     const RRFpCtl* ctl = b.fp_ctl;
     if (ctl->state != FP_RUN) return;
     __shared__ uint32_t s_sf[FP_TMAX + 1];
     const uint32_t T = b.rr_T, nu = ctl->nu;
     const unsigned long long num = ctl->guess_num, den = ctl->guess_den;
-    const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
     for (uint32_t s = threadIdx.x; s <= T; s += blockDim.x) s_sf[s] = b.fp_sf[s];
     __syncthreads();
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nu; i += gridDim.x * blockDim.x) {
         const unsigned long long pos = i - s_sf[fp_set_of(s_sf, T, i)];
         b.fp_in[i] = (uint8_t)((pos + 1) * num / den > pos * num / den);
-        const uint4 a = U[i].a, v0 = U[i].v0;
-        uint32_t sole = 0, j = 0;
-        fp_for_vars<KW>(cv, U, i, a, v0, [&](uint32_t v) {
-            if (j < 8 && b.fp_deg[v] == 1u) sole |= 1u << j;
-            ++j;
-        });
-        b.fp_sole[i] = (uint8_t)sole;
     }
 }
 
@@ -4140,7 +4140,7 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_vcount(LoopBuffers b) {
         uint32_t acc = 0;
         for (uint32_t e = 0; e < FP_PER; ++e) {
             const uint32_t v = blk * FP_B + e * FP_THREADS + threadIdx.x;
-            const uint32_t d = v < nv ? b.fp_deg[v] : 0u;
+            const uint32_t d = v < nv ? b.fp_deg[v] + b.fp_deg_hi[v] : 0u;
             acc += d >= 2 ? d : 0u;
         }
         uint32_t tot;
@@ -4178,7 +4178,7 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_voff(LoopBuffers b) {
         uint32_t d[FP_PER], acc = 0;
         for (uint32_t e = 0; e < FP_PER; ++e) {
             const uint32_t v = v0 + e;
-            const uint32_t x = v < nv ? b.fp_deg[v] : 0u;
+            const uint32_t x = v < nv ? b.fp_deg[v] + b.fp_deg_hi[v] : 0u;
             d[e] = x >= 2 ? x : 0u;
             acc += d[e];
         }
@@ -4191,8 +4191,9 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_voff(LoopBuffers b) {
     }
 }
 
-// entries into the lists of their shared variables (fills each list from its end: the degree
-// counts down; the sole masks were taken from it already)
+// entries into the lists of their shared variables, at the ranks k_fp_deg drew (slots past 8:
+// after the ranked ones, by a second counter), and every entry's sole-claimant mask (bit j:
+// slot j's variable has no other violated claimant, i.e. an empty list)
 template <uint32_t KW>
 __global__ __launch_bounds__(FP_THREADS) void k_fp_vfill(ClauseView cv, LoopBuffers b) {
     const RRFpCtl* ctl = b.fp_ctl;
@@ -4201,10 +4202,22 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_vfill(ClauseView cv, LoopBuff
     const uint32_t nu = ctl->nu;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nu; i += gridDim.x * blockDim.x) {
         const uint4 a = U[i].a, v0 = U[i].v0;
-        fp_for_shared<KW>(cv, U, i, a, v0, b.fp_sole[i], [&](uint32_t v) {
-            const uint32_t o = b.fp_voff[v];
-            if (b.fp_voff[v + 1] - o >= 2) b.fp_vlist[o + atomicSub(&b.fp_deg[v], 1u) - 1u] = i;
+        const uint4* rp = reinterpret_cast<const uint4*>(b.fp_rank) + 2 * (uint64_t)i;
+        const uint4 r0 = rp[0], r1 = (KW == 0 && a.z > 4) ? rp[1] : make_uint4(0, 0, 0, 0);
+        const uint32_t rk[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+        uint32_t sole = 0, j = 0;
+        fp_for_vars<KW>(cv, U, i, a, v0, [&](uint32_t v) {
+            const uint32_t o = b.fp_voff[v], d = b.fp_voff[v + 1] - o;
+            if (d == 0) {
+                if (j < 8) sole |= 1u << j;
+            } else if (j < 8) {
+                b.fp_vlist[o + rk[j]] = i;
+            } else {
+                b.fp_vlist[o + b.fp_deg[v] + atomicSub(&b.fp_deg_hi[v], 1u) - 1u] = i;
+            }
+            ++j;
         });
+        b.fp_sole[i] = (uint8_t)sole;
     }
 }
 
@@ -4998,19 +5011,16 @@ hipError_t launch_rr_mis(const ClauseView& cv, const LoopBuffers& b, hipStream_t
         const bool narrow = b.rr_k >= 1 && b.rr_k <= 4;
         const uint32_t gb = (uint32_t)std::min<uint64_t>((b.m + FP_B - 1) / FP_B + 1, FP_COUNT_GRID);
         const uint32_t gl = (uint32_t)std::min<uint64_t>((b.m + FP_THREADS - 1) / FP_THREADS + 1, 2048);
-        const uint32_t gr = (uint32_t)std::min<uint64_t>((b.m + FP_RT - 1) / FP_RT + 1, 8192);
+        const uint32_t gr = (uint32_t)std::min<uint64_t>((b.m + FP_RT - 1) / FP_RT + 1, 2048);
         hipError_t e = hipMemsetAsync(b.fp_owner, 0xFF, (size_t)b.n_vars * 8, s);
         if (e != hipSuccess) return e;
         e = hipMemsetAsync(b.fp_deg, 0, (size_t)b.n_vars * 4, s);
+        if (e == hipSuccess && !narrow) e = hipMemsetAsync(b.fp_deg_hi, 0, (size_t)b.n_vars * 4, s);
         if (e != hipSuccess) return e;
         k_fp_begin<<<1, 256, 0, s>>>(b);
-        if (narrow) {
-            k_fp_deg<4><<<gl, FP_THREADS, 0, s>>>(cv, b);
-            k_fp_guess<4><<<gl, FP_THREADS, 0, s>>>(cv, b);
-        } else {
-            k_fp_deg<0><<<gl, FP_THREADS, 0, s>>>(cv, b);
-            k_fp_guess<0><<<gl, FP_THREADS, 0, s>>>(cv, b);
-        }
+        if (narrow) k_fp_deg<4><<<gl, FP_THREADS, 0, s>>>(cv, b);
+        else k_fp_deg<0><<<gl, FP_THREADS, 0, s>>>(cv, b);
+        k_fp_guess<<<gl, FP_THREADS, 0, s>>>(b);
         const uint32_t gv = (uint32_t)std::min<uint64_t>((b.n_vars + FP_B - 1) / FP_B + 1, FP_COUNT_GRID);
         const uint32_t gvt = (uint32_t)std::min<uint64_t>((b.n_vars + FP_THREADS - 1) / FP_THREADS + 1, 2048);
         k_fp_vcount<<<gv, FP_THREADS, 0, s>>>(b);

@@ -228,3 +228,24 @@ def test_rr_python_satinstance(gpu, oracle_mod):
     st_o, A_o, _ = o.solve(n, offs, lits, 21, T=T)
     assert stats.n_iterations == st_o["n_iterations"] and stats.n_resamples == st_o["n_resamples"]
     assert inst.verify_validity(chunks)
+
+
+@pytest.mark.parametrize("T", [16, 5])
+def test_rr_full_size_c2_bit_exact(gpu, oracle_mod, rr_kernel, T):
+    """BASELINE config C2 (random 3-SAT, 1M variables / 4M clauses) with the round robin of T
+    sets: two iterations, every violated set, MIS and assignment against the oracle's
+    orc_solve_rr (the fixpoint passes settle on ~500k violated clauses per iteration)."""
+    from alllsatisfiabilitysolver_amd import Solver, generate_ksat
+
+    n, m, seed, K = 1_000_000, 4_000_000, 12, 2
+    offs, lits = generate_ksat(1, n, m, 3)
+    st_o, A_o, rows = oracle_mod.solve(n, offs, lits, seed, max_iters=K + 1, trace=True, T=T)
+    with Solver(n, offs, lits, seed=seed, n_threads=T) as s:
+        for it, nu, nm, dres, A_after in rows[:K]:
+            before = s.stats()
+            s.run(1)
+            after = s.stats()
+            assert after["n_violated"] == nu, f"iter {it}"
+            assert after["sum_mis_size"] - before["sum_mis_size"] == nm, f"iter {it}"
+            assert after["n_resamples"] - before["n_resamples"] == dres, f"iter {it}"
+            np.testing.assert_array_equal(s.assignment_words(), A_after, err_msg=f"A after iter {it}")

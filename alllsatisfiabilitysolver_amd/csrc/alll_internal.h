@@ -220,6 +220,7 @@ struct LoopBuffers {
     uint32_t* fp_list;          // 2 x m: round lists per tile of FP_B entries (JOIN output, CLAIM output)
     uint32_t* fp_tcnt;          // 2 FP_G x tiles: list lengths per round and tile
     unsigned long long* fp_owner; // n_vars claim keys {epoch | turn | entry}, reset every iteration
+    uint32_t* fp_own0;          // n_vars: round-0 winner (entry) of every shared variable
     uint32_t* fp_cov;           // n_vars: serial of the pass whose pick covers the variable
     uint32_t* fp_deg;           // n_vars: violated claimants this iteration (slots 0..7 of their clauses)
     uint32_t* fp_deg_hi;        // n_vars: the same from slots past 8 (wide clauses)

@@ -3954,7 +3954,8 @@ constexpr uint32_t FP_PER = FP_B / FP_THREADS;  // entries per thread in the cou
 static_assert(FP_PER == 8, "a thread's pick bytes are one 8-byte load");
 constexpr uint32_t FP_RT = 256;        // entries per round tile (one per thread): many workgroups per CU
 constexpr uint32_t FP_LDS_SEG_T = 32;     // k_fp_turn keeps the schedule in LDS up to this many sets
-constexpr uint32_t FP_COUNT_GRID = 1024;  // workgroups of k_fp_count / k_fp_turn (grid-stride over blocks)
+constexpr uint32_t FP_COUNT_GRID = 1024;
+constexpr uint32_t FP_SCHED_LDS_BLK = 4096;  // k_fp_sched keeps the block offsets in LDS up to this many blocks  // workgroups of k_fp_count / k_fp_turn (grid-stride over blocks)
 
 __device__ __forceinline__ unsigned long long fp_key(const LoopBuffers& b, uint32_t ep, uint32_t turn, uint32_t i) {
     const uint32_t sh = b.fp_tb + b.fp_ib;
@@ -4235,6 +4236,9 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_vmin(LoopBuffers b) {
             const unsigned long long k = fp_key(b, ep, b.fp_turn[i], i);
             best = k < best ? k : best;
         }
+        // JOIN(0) reads the winning entry from a 4-byte array (half the footprint of the keys);
+        // the later rounds' atomics start from the round-0 key
+        b.fp_own0[v] = (uint32_t)best & ((1u << b.fp_ib) - 1u);
         b.fp_owner[v] = best;
     }
 }
@@ -4314,6 +4318,8 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_join(ClauseView cv, LoopBuffe
                 if (r == 0 && turn < tpre) {  // decided as in the last pass (bit 1)
                     pre = true;
                     own = (b.fp_in[i] >> 1) & 1u;
+                } else if (r == 0) {
+                    fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) { own &= b.fp_own0[v] == i; });
                 } else {
                     const unsigned long long key = fp_key(b, ep, turn, i);
                     fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) { own &= b.fp_owner[v] == key; });
@@ -4466,7 +4472,7 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_count(LoopBuffers b, int test
 }
 
 // One workgroup: convergence, block offsets, picks per set, the schedule, the next pass.
-__global__ __launch_bounds__(1024) void k_fp_sched(LoopBuffers b, int test) {
+__global__ __launch_bounds__(256) void k_fp_sched(LoopBuffers b, int test) {
     RRFpCtl* ctl = b.fp_ctl;
     const uint32_t state = ctl->state;
     if (state == FP_FINAL) {  // the finalizing k_fp_turn has run
@@ -4474,26 +4480,32 @@ __global__ __launch_bounds__(1024) void k_fp_sched(LoopBuffers b, int test) {
         return;
     }
     if (state != FP_RUN) return;
-    __shared__ uint32_t s_w[16];
-    __shared__ uint32_t s_n[FP_TMAX], s_done[FP_TMAX], s_live[FP_TMAX], s_nseg[FP_TMAX];
+    __shared__ uint32_t s_w[16], s_e0;
+    __shared__ uint32_t s_n[FP_TMAX], s_done[FP_TMAX], s_live[FP_TMAX], s_nseg[FP_TMAX], s_pf[FP_TMAX + 1];
+    __shared__ uint32_t s_off[FP_SCHED_LDS_BLK];  // block offsets (when they fit)
     const uint32_t nu = ctl->nu, T = b.rr_T, nblk = (nu + FP_B - 1) / FP_B;
     uint32_t* blkoff = b.fp_blk + (b.m / FP_B + 2);
+    const bool lds_off = nblk <= FP_SCHED_LDS_BLK;
+    // every independent load first (one round trip): change counts and earliest changes, the
+    // first block counts, the set starts and their in-block pick counts
     uint32_t ch = 0, tmin = ~0u;  // picks changed by the last pass, their earliest turn (per k_fp_count workgroup)
     if (test)
         for (uint32_t k = threadIdx.x; k < min(nblk, FP_COUNT_GRID); k += blockDim.x) {
             ch += b.fp_blk[2 * (b.m / FP_B + 2) + k];
             tmin = min(tmin, b.fp_blk[2 * (b.m / FP_B + 2) + FP_COUNT_GRID + k]);
         }
+    uint32_t sf[2], bnd[2];
+    for (uint32_t q = 0; q < 2; ++q) {  // (T + 1 <= 2 * blockDim.x)
+        const uint32_t s = threadIdx.x + q * blockDim.x;
+        sf[q] = s <= T ? b.fp_sf[s] : 0u;
+        bnd[q] = s <= T ? b.fp_bnd[s] : 0u;
+    }
     ch = __syncthreads_or(ch != 0);
     for (int o = 32; o > 0; o >>= 1) tmin = min(tmin, (uint32_t)__shfl_down(tmin, o, 64));
     if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = tmin;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        for (uint32_t w = 1; w < (blockDim.x >> 6); ++w) tmin = min(tmin, s_w[w]);
-        s_w[0] = tmin;
-    }
-    __syncthreads();
     tmin = s_w[0];
+    for (uint32_t w = 1; w < (blockDim.x >> 6); ++w) tmin = min(tmin, s_w[w]);
     __syncthreads();
     const bool conv = test && ch == 0;
     // exclusive scan of the block counts
@@ -4503,19 +4515,26 @@ __global__ __launch_bounds__(1024) void k_fp_sched(LoopBuffers b, int test) {
         const uint32_t x = k < nblk ? b.fp_blk[k] : 0u;
         uint32_t tot;
         const uint32_t ex = fp_block_scan(x, s_w, tot);
-        if (k < nblk) blkoff[k] = carry + ex;
+        if (k < nblk) {
+            blkoff[k] = carry + ex;
+            if (lds_off) s_off[k] = carry + ex;
+        }
         carry += tot;
     }
     __syncthreads();
     const uint32_t total = carry;
     // picks before every set's first entry, picks per set
-    for (uint32_t s = threadIdx.x; s <= T; s += blockDim.x) {
-        const uint32_t f = b.fp_sf[s];
-        b.fp_pf[s] = f >= nu ? total : blkoff[f / FP_B] + b.fp_bnd[s];
+    for (uint32_t q = 0; q < 2; ++q) {
+        const uint32_t s = threadIdx.x + q * blockDim.x;
+        if (s > T) continue;
+        const uint32_t f = sf[q];
+        const uint32_t pf = f >= nu ? total : (lds_off ? s_off[f / FP_B] : blkoff[f / FP_B]) + bnd[q];
+        s_pf[s] = pf;
+        b.fp_pf[s] = pf;
     }
     __syncthreads();
     for (uint32_t s = threadIdx.x; s < T; s += blockDim.x) {
-        s_n[s] = b.fp_pf[s + 1] - b.fp_pf[s];
+        s_n[s] = s_pf[s + 1] - s_pf[s];
         s_done[s] = 0;
         s_live[s] = s;
         s_nseg[s] = 0;
@@ -4552,7 +4571,10 @@ __global__ __launch_bounds__(1024) void k_fp_sched(LoopBuffers b, int test) {
                     done += cnt;
                 }
                 const uint32_t E = step + (uint32_t)d;
-                if (lane == 0) b.fp_erase[p] = E;
+                if (lane == 0) {
+                    b.fp_erase[p] = E;
+                    if (p == 0) s_e0 = E;
+                }
                 t = (uint32_t)__popcll(alive & ((1ull << ls) - 1ull));
                 alive &= ~(1ull << ls);
                 step = E + 1;
@@ -4584,7 +4606,10 @@ __global__ __launch_bounds__(1024) void k_fp_sched(LoopBuffers b, int test) {
                 s_done[s] += cnt;
             }
             const uint32_t E = step + (uint32_t)d;
-            if (lane == 0) b.fp_erase[p] = E;
+            if (lane == 0) {
+                b.fp_erase[p] = E;
+                if (p == 0) s_e0 = E;
+            }
             // erase live index xs (every lane reads before any writes: one wave)
             uint32_t mv[FP_TMAX / 64];
 #pragma unroll
@@ -4613,7 +4638,7 @@ __global__ __launch_bounds__(1024) void k_fp_sched(LoopBuffers b, int test) {
         ctl->changes = 0;
         // The next pass keeps the decisions below min(earliest changed turn, both schedules'
         // first erasure): there the turns did not change, so neither did the sub-problem.
-        const uint32_t e0 = b.fp_erase[0];
+        const uint32_t e0 = s_e0;
         ctl->tpre = test ? min(tmin, min(e0, ctl->e0)) : 0u;
         ctl->e0 = e0;
         if (conv) {
@@ -5030,7 +5055,7 @@ hipError_t launch_rr_mis(const ClauseView& cv, const LoopBuffers& b, hipStream_t
         else k_fp_vfill<0><<<gl, FP_THREADS, 0, s>>>(cv, b);
         auto turns = [&](int test) {
             k_fp_count<<<gb, FP_THREADS, 0, s>>>(b, test);
-            k_fp_sched<<<1, 1024, 0, s>>>(b, test);
+            k_fp_sched<<<1, 256, 0, s>>>(b, test);
             if (narrow) k_fp_turn<4><<<gb, FP_THREADS, 0, s>>>(cv, b);
             else k_fp_turn<0><<<gb, FP_THREADS, 0, s>>>(cv, b);
         };

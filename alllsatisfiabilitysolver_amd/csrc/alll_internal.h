@@ -169,10 +169,6 @@ struct LoopBuffers {
     DevState* state;
     unsigned long long* ktime; // TIME_SLOTS x TIME_FIELDS stamps, nullptr = timing off
     unsigned long long* pairs;  // bucketed round 0: n_runs x run_tiles*TILE*K pairs (nullptr = atomics)
-    uint8_t* sole;              // bucketed round 0 (fixed K, no hot variables): per variable, 1 when one
-                                // violated clause alone claims it this iteration (k_bresolve); round 1
-                                // marks such literals in the entries (bit 31) and no round claims or
-                                // tests them.  nullptr = off (also in iterations with another round 0)
     unsigned long long* runtab; // [bucket][run]: start | count << 32 of the bucket's pairs in the run
     uint32_t* run_pairs;        // pairs per run
     uint32_t* dd_msg;           // dependency-driven LFMIS: one message word per pair position (chain

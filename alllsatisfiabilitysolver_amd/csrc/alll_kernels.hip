@@ -983,11 +983,8 @@ __device__ __forceinline__ void claim_all(const ClauseView& cv, const LoopBuffer
                                           HotTable& ht, bool hot) {
     for (uint32_t j = 0; j < len; ++j) {
         const uint32_t raw = ent_lit<K>(cv, e, lb, j);
-        if (raw & LIT_HOT) {  // hot variable (LDS table), or (no hot variables) a sole claimant: no claim
-            if (hot) ht.claim(lit_var(raw), key);
-        } else {
-            __hip_atomic_fetch_min(&owner[vmix(b, lit_var(raw))], key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        if (hot && (raw & LIT_HOT)) ht.claim(lit_var(raw), key);
+        else __hip_atomic_fetch_min(&owner[vmix(b, lit_var(raw))], key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -1033,23 +1030,7 @@ __global__ __launch_bounds__(ROUND_THREADS) void k_claim(ClauseView cv, LoopBuff
         if (key == ~0u) continue;  // streaming: not yielded this iteration (dropped by JOIN(0))
         if (r > 0) {
             bool killed = false;
-            if (K > 0 && r == 1 && b.sole) {
-                // round 1 after the bucketed round 0: a variable that clause alone claimed this
-                // iteration is its own and cannot be covered by another clause; it is marked in
-                // the entry (bit 31, free without hot variables) and never claimed or tested again
-                uint32_t sole = 0;
-#pragma unroll
-                for (int j = 0; j < (K > 0 ? K : 1); ++j) {
-                    const uint32_t v = lit_var(e.w[1 + j]);
-                    killed |= b.cover[v] == stamp;
-                    sole |= (uint32_t)b.sole[v] << j;
-                }
-#pragma unroll
-                for (int j = 0; j < (K > 0 ? K : 1); ++j)
-                    if ((sole >> j) & 1u) e.w[1 + j] |= LIT_HOT;
-            } else {
-                for (uint32_t j = 0; j < len; ++j) killed |= b.cover[lit_var(ent_lit<K>(cv, e, lb, j))] == stamp;
-            }
+            for (uint32_t j = 0; j < len; ++j) killed |= b.cover[lit_var(ent_lit<K>(cv, e, lb, j))] == stamp;
             if (killed) continue;
         }
         claim_all<K>(cv, b, e, lb, len, keyhi | key, owner, ht, hot);
@@ -1138,15 +1119,11 @@ __global__ __launch_bounds__(JOIN_THREADS) void k_join(ClauseView cv, LoopBuffer
     if (!active || cnt == 0) return;
     const unsigned long long keyhi = (unsigned long long)(~(rbase + r)) << 32;
     const unsigned long long* owner = owner_of(b, rbase + r);
-    const bool hot = cv.n_hot != 0;
     join_tile<K>(cv, b, tile, cnt, in, out, last, stamp, mis0, e0,
                  [&](const Ent<K>& e, uint32_t, uint64_t lb, uint32_t len) {
                      bool own = true;
                      const unsigned long long key = keyhi | prio(b, st, e.w[0]);
-                     for (uint32_t j = 0; j < len; ++j) {
-                         const uint32_t raw = ent_lit<K>(cv, e, lb, j);
-                         if (hot || !(raw & LIT_HOT)) own &= owner[vmix(b, lit_var(raw))] == key;  // (sole: own)
-                     }
+                     for (uint32_t j = 0; j < len; ++j) own &= owner[vmix(b, lit_var(ent_lit<K>(cv, e, lb, j)))] == key;
                      return own;
                  });
 }
@@ -1213,12 +1190,9 @@ __global__ __launch_bounds__(ROUND_THREADS) void k_wclaim(ClauseView cv, LoopBuf
                 if (!killed) {
                     for (uint32_t j = 0; j < len; ++j) {
                         const uint32_t raw = ent_lit<K>(cv, e, lb, j);
-                        if (raw & LIT_HOT) {  // hot (LDS table) or sole (no claim)
-                            if (hot) ht.claim(lit_var(raw), keyhi | key);
-                        } else {
-                            __hip_atomic_fetch_min(&owner[vmix(b, lit_var(raw))], keyhi | key, __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT);
-                        }
+                        if (hot && (raw & LIT_HOT)) ht.claim(lit_var(raw), keyhi | key);
+                        else __hip_atomic_fetch_min(&owner[vmix(b, lit_var(raw))], keyhi | key, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
                     }
                     keep = true;
                 }
@@ -1253,7 +1227,6 @@ __global__ __launch_bounds__(ROUND_THREADS) void k_wjoin(ClauseView cv, LoopBuff
     if (!active) return;
     const uint32_t cnt = __builtin_amdgcn_readfirstlane(cnt0);
     if (cnt == 0) return;
-    const bool hot = cv.n_hot != 0;
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     const unsigned long long keyhi = (unsigned long long)(~(rbase + r)) << 32;
     const unsigned long long* owner = owner_of(b, rbase + r);
@@ -1274,10 +1247,7 @@ __global__ __launch_bounds__(ROUND_THREADS) void k_wjoin(ClauseView cv, LoopBuff
             const uint32_t kc = prio(b, st, e.w[0]);
             if (kc != ~0u) {  // (streaming: a clause not yielded this iteration leaves the list)
                 own = true;
-                for (uint32_t j = 0; j < len; ++j) {
-                    const uint32_t raw = ent_lit<K>(cv, e, lb, j);
-                    if (hot || !(raw & LIT_HOT)) own &= owner[vmix(b, lit_var(raw))] == (keyhi | kc);  // (sole: own)
-                }
+                for (uint32_t j = 0; j < len; ++j) own &= owner[vmix(b, lit_var(ent_lit<K>(cv, e, lb, j)))] == (keyhi | kc);
                 keep = !own;
                 if (own) {
                     for (uint32_t j = 0; j < len; ++j) b.cover[lit_var(ent_lit<K>(cv, e, lb, j))] = (uint8_t)stamp;
@@ -1740,25 +1710,6 @@ __device__ __forceinline__ uint32_t resolve_batch(const LoopBuffers& b, const Re
     return total;
 }
 
-// the pair's claim into its variable's minimum; a claim that finds one already there marks the
-// variable shared (mb: bit per variable, nullptr = not tracked)
-__device__ __forceinline__ void resolve_min(const ResolveLds& L, uint32_t* mb, unsigned long long x) {
-    const uint32_t off = (uint32_t)x & 0x7FFFu;
-    const uint32_t old = atomicMin(&L.min[off], (uint32_t)(x >> 32));
-    if (mb && old != ~0u) atomicOr(&mb[off >> 5], 1u << (off & 31u));
-}
-
-// b.sole of the bucket's variables (owner slots bucket * width + offset): 1 when exactly one
-// violated clause claimed the variable this iteration (round 1 marks it in that clause's entry)
-__device__ __forceinline__ void resolve_sole(const LoopBuffers& b, const ResolveLds& L, const uint32_t* mb,
-                                             uint32_t bv) {
-    const uint64_t base = (uint64_t)blockIdx.x * bv;
-    for (uint32_t off = threadIdx.x; off < bv; off += blockDim.x) {
-        if (base + off >= b.n_vars) break;
-        b.sole[base + off] = (uint8_t)(L.min[off] != ~0u && !((mb[off >> 5] >> (off & 31u)) & 1u));
-    }
-}
-
 __device__ __forceinline__ unsigned long long resolve_mark(const ResolveLds& L, unsigned long long x) {
     return L.min[(uint32_t)x & 0x7FFFu] != (uint32_t)(x >> 32) ? (x | PAIR_LOSE) : x;
 }
@@ -1825,13 +1776,8 @@ __device__ void resolve_bucket(const LoopBuffers& b, uint32_t run_cap) {
     __shared__ uint16_t s_seg[T * U];  // item -> segment of the current sweep
     const uint32_t bv = b.bkt_width;
     ResolveLds L{s_min, s_start, s_pre, s_wsum};
-    // b.sole: a bit per variable of the bucket, set when a second claim arrives (the minimum's
-    // atomic returned a claim), after the dynamic minima
-    uint32_t* mb = b.sole ? s_min + bv : nullptr;
     dbg_stamp(b, 1, 0);
     for (uint32_t i = threadIdx.x; i < bv; i += blockDim.x) L.min[i] = ~0u;
-    if (mb)
-        for (uint32_t i = threadIdx.x; i < (bv + 31) / 32; i += blockDim.x) mb[i] = 0u;
     // items of a wave: f0 + 64 u, f0 = wave * 64 U + lane (+ stride per sweep)
     const uint32_t first = (threadIdx.x >> 6) * 64 * U + (threadIdx.x & 63);
     const uint32_t stride = T * U;
@@ -1855,11 +1801,10 @@ __device__ void resolve_bucket(const LoopBuffers& b, uint32_t run_cap) {
                 for (int u = 0; u < U; ++u) x[u] = b.pairs[pos[u]];
 #pragma unroll
                 for (int u = 0; u < U; ++u)  // (clamped duplicates of the last pair would serialise)
-                    if (first + 64 * u < np) resolve_min(L, mb, x[u]);
+                    if (first + 64 * u < np) atomicMin(&L.min[(uint32_t)x[u] & 0x7FFFu], (uint32_t)(x[u] >> 32));
             }
             dbg_stamp(b, 1, 2);
             __syncthreads();
-            if (mb) resolve_sole(b, L, mb, bv);
             dbg_stamp(b, 1, 3);
             if (np > 0) {
 #pragma unroll
@@ -1889,7 +1834,7 @@ __device__ void resolve_bucket(const LoopBuffers& b, uint32_t run_cap) {
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     if (s0 + first + 64 * u >= np) continue;
-                    if (pass == 0) resolve_min(L, mb, x[u]);
+                    if (pass == 0) atomicMin(&L.min[(uint32_t)x[u] & 0x7FFFu], (uint32_t)(x[u] >> 32));
                     else b.pairs[pos[u]] = resolve_mark(L, x[u]);
                 }
                 __syncthreads();  // the table is rewritten by the next sweep
@@ -1897,7 +1842,6 @@ __device__ void resolve_bucket(const LoopBuffers& b, uint32_t run_cap) {
             // (batch arrays are rewritten next; after pass 0: L.min is final -- the sweep's
             // last barrier orders it)
         }
-        if (pass == 0 && mb) resolve_sole(b, L, mb, bv);
     }
     dbg_stamp(b, 1, 4);
 }
@@ -4986,7 +4930,7 @@ hipError_t launch_round0_buckets(const ClauseView& cv, const LoopBuffers& b, boo
     // buffers as CLAIM(0) + JOIN(0): eval -> stage[0] (ids translated in place); JOIN stage[0] -> stage[1]
     if (b.n_tiles == 0 || cv.k == 0 || !b.pairs) return hipErrorInvalidValue;
     const uint64_t run_cap = (uint64_t)b.run_tiles * TILE * cv.k;
-    const size_t lds = (size_t)4 * b.bkt_width + (b.sole ? (size_t)4 * ((b.bkt_width + 31) / 32) : 0);  // k_bresolve minima (+ shared bits)
+    const size_t lds = (size_t)4 * b.bkt_width;  // k_bresolve minima
     int dev;
     if (cv.k <= (uint32_t)MAX_FIXED_K && attr_pending(ATTR_BUCKETS + cv.k, dev)) {
         hipError_t e = hipFuncSetAttribute((const void*)k_bresolve<BRS_UNROLL_WIDE, BRS_THREADS>,

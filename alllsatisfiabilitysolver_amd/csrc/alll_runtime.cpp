@@ -397,30 +397,26 @@ int enqueue_iteration(alll_ctx* c, hipEvent_t* marks, int variant) {
     } else if (variant == 1 && c->dd) {
         HIP_TRY(launch_lfmis_dd(c->cv, c->b, scatter, fused, s));
     } else {
-        // sole-claimant marks only after the bucketed round 0 (k_bresolve writes them), with
-        // round 1 as a workgroup-per-tile CLAIM and without the fused JOIN+CLAIM rounds
-        LoopBuffers lb = c->b;
-        if (variant != 1 || c->wave_round_min <= 1 || c->fuse_jc) lb.sole = nullptr;
         const uint32_t rounds = variant == 2 ? 1u : c->grid_rounds;
         // rounds [0, f) as separate CLAIM / JOIN launches, then (f + 2 <= G) CLAIM(f), JOIN(r) +
         // CLAIM(r + 1) fused for f <= r < G - 1, and the last JOIN
         const uint32_t f = c->fuse_jc && c->fuse_jc + 2 <= rounds ? c->fuse_jc : rounds;
         for (uint32_t r = 0; r < f; ++r) {
             if (r == 0 && variant == 1)
-                HIP_TRY(launch_round0_buckets(c->cv, lb, rounds == 1, fused, scatter, s));
-            else HIP_TRY(launch_round(c->cv, lb, r, r + 1 == rounds, c->wave_round_min, s));
+                HIP_TRY(launch_round0_buckets(c->cv, c->b, rounds == 1, fused, scatter, s));
+            else HIP_TRY(launch_round(c->cv, c->b, r, r + 1 == rounds, c->wave_round_min, s));
         }
         if (f < rounds) {
             // after JOIN(f-1) the list is in stage[1]: CLAIM(f) -> stage[0], then the fused rounds
             // alternate between the two, and the last JOIN hands the survivors to the tail
-            uint32_t* st2[2] = {lb.stage[0], lb.stage[1]};
-            HIP_TRY(launch_claim_only(c->cv, lb, f, c->wave_round_min, st2[1], st2[0], s));
+            uint32_t* st2[2] = {c->b.stage[0], c->b.stage[1]};
+            HIP_TRY(launch_claim_only(c->cv, c->b, f, c->wave_round_min, st2[1], st2[0], s));
             uint32_t cur = 0;
             for (uint32_t r = f; r + 1 < rounds; ++r, cur ^= 1u)
-                HIP_TRY(launch_join_claim(c->cv, lb, r, st2[cur], st2[cur ^ 1u], s));
-            HIP_TRY(launch_join_only(c->cv, lb, rounds - 1, true, c->wave_round_min, st2[cur], st2[cur ^ 1u], s));
+                HIP_TRY(launch_join_claim(c->cv, c->b, r, st2[cur], st2[cur ^ 1u], s));
+            HIP_TRY(launch_join_only(c->cv, c->b, rounds - 1, true, c->wave_round_min, st2[cur], st2[cur ^ 1u], s));
         }
-        HIP_TRY(launch_tail(c->cv, lb, rounds, s));
+        HIP_TRY(launch_tail(c->cv, c->b, rounds, s));
     }
     if (marks) HIP_TRY(hipEventRecord(marks[3], s));
     if (c->allreduce && xchg) {
@@ -910,11 +906,6 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
             if ((rc = dalloc(c, &b.pairs, (size_t)b.n_runs * run_cap))) return bail(rc);
             if ((rc = dalloc(c, &b.runtab, (size_t)b.n_bkt * b.n_runs))) return bail(rc);
             if ((rc = dalloc(c, &b.run_pairs, b.n_runs))) return bail(rc);
-            // sole-claimant flags (alll_internal.h): no hot variables (bit 31 of the entries is
-            // free), minima + shared bits within k_bresolve's LDS; ALLL_SOLE=0 turns them off
-            bool sole = !n_hot && width <= 16384;
-            if (const char* e = getenv("ALLL_SOLE")) sole = sole && atoi(e) != 0;
-            if (sole && (rc = dalloc(c, &b.sole, (size_t)prob->n_vars + 16))) return bail(rc);
             // below this many violated clauses the atomic round 0 is cheaper (fixed costs)
             c->bucket_min_u = std::max<uint64_t>(65536, m / 64);
             if (const char* e = getenv("ALLL_BUCKET_MIN_U")) c->bucket_min_u = strtoull(e, nullptr, 10);

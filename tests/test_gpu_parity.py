@@ -26,10 +26,6 @@ T1_FIXTURES = sorted(p for p in glob.glob(os.path.join(GOLDEN, "*_T1.npz")))
 LAYOUTS = {"hybrid": (0, {}), "fixed": (1 << 3, {}), "csr": (1 << 2, {}), "atomic_claims": (1 << 5, {}),
            "buckets": (0, {"ALLL_BUCKET_MIN_U": "0"}), "windows": (0, {"ALLL_EVAL_WINDOWS": "1"}),
            "positions": (0, {"ALLL_PACKED_IDS": "0"}),
-           # bucketed round 0 without the sole-claimant marks of round 1 (on by default), and the
-           # marks' off-switch when round 1 is a wave-per-tile round
-           "buckets_no_sole": (0, {"ALLL_BUCKET_MIN_U": "0", "ALLL_SOLE": "0"}),
-           "buckets_wave1": (0, {"ALLL_BUCKET_MIN_U": "0", "ALLL_WAVE_ROUND_MIN": "1"}),
            # hot-variable instances without the owner/bucket spread (identity vmix)
            "no_vmix": (0, {"ALLL_NO_VMIX": "1", "ALLL_BUCKET_MIN_U": "0"}),
            # bucketed round 0 scattered by the evaluation workgroups (no k_bscatter)

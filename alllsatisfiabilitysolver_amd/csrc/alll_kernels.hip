@@ -4583,51 +4583,77 @@ __global__ __launch_bounds__(256) void k_fp_sched(LoopBuffers b, int test) {
             if (lane == 0) ctl->n_steps = step;
         }
     } else if (threadIdx.x < 64) {
+        // up to FP_TMAX sets: lane l keeps sets l, l + 64, l + 128, l + 192 in registers, the
+        // live list is a mask of FP_TMAX / 64 words; a set that is not the phase's winner takes
+        // r* or r* + 1 turns before the erasure (r* L + o* = the winner's key), no division
+        constexpr uint32_t Q = FP_TMAX / 64;
         const uint32_t lane = threadIdx.x;
-        uint32_t L = T, t = 0, step = 0;
+        uint32_t n[Q], done[Q], nseg[Q];
+        unsigned long long alive[Q];
+#pragma unroll
+        for (uint32_t q = 0; q < Q; ++q) {
+            const uint32_t s = lane + 64 * q;
+            n[q] = s < T ? s_n[s] : 0u;
+            done[q] = 0;
+            nseg[q] = 0;
+            alive[q] = T >= 64 * (q + 1) ? ~0ull : (T > 64 * q ? (1ull << (T - 64 * q)) - 1ull : 0ull);
+        }
+        const unsigned long long lt = (1ull << lane) - 1ull;
+        uint32_t t = 0, step = 0;
         for (uint32_t p = 0; p < T; ++p) {
+            uint32_t L = 0;
+#pragma unroll
+            for (uint32_t q = 0; q < Q; ++q) L += (uint32_t)__popcll(alive[q]);
+            const uint32_t tl = t % L;
             unsigned long long best = ~0ull;
-            for (uint32_t x = lane; x < L; x += 64) {
-                const uint32_t s = s_live[x], o = (x + L - (t % L) - 1) % L;
-                const unsigned long long key = ((unsigned long long)(s_n[s] - s_done[s]) * L + o) << 12 | x;
-                best = key < best ? key : best;
+            uint32_t o[Q], below = 0;
+#pragma unroll
+            for (uint32_t q = 0; q < Q; ++q) {
+                const uint32_t x = below + (uint32_t)__popcll(alive[q] & lt);
+                o[q] = (x + L - tl - 1) % L;
+                if ((alive[q] >> lane) & 1ull) {
+                    const unsigned long long key = (((unsigned long long)(n[q] - done[q]) * L + o[q]) << 8) | (lane + 64 * q);
+                    best = key < best ? key : best;
+                }
+                below += (uint32_t)__popcll(alive[q]);
             }
-            for (int o = 32; o > 0; o >>= 1) {
-                const unsigned long long y = __shfl_xor(best, o, 64);
+            for (int sh = 32; sh > 0; sh >>= 1) {
+                const unsigned long long y = __shfl_xor(best, sh, 64);
                 best = y < best ? y : best;
             }
-            const uint32_t xs = (uint32_t)(best & 0xFFFu);
-            const unsigned long long d = best >> 12;  // E - step
-            for (uint32_t x = lane; x < L; x += 64) {
-                const uint32_t s = s_live[x], o = (x + L - (t % L) - 1) % L;
-                const uint32_t cnt = x == xs ? s_n[s] - s_done[s] : (d > o ? (uint32_t)((d - o + L - 1) / L) : 0u);
-                b.fp_seg[(uint64_t)s * T + s_nseg[s]] = make_uint4(s_done[s], step, L, o);
-                s_nseg[s] += 1;
-                s_done[s] += cnt;
+            const uint32_t ls = (uint32_t)(best & 255u);
+            const unsigned long long d = best >> 8;
+            const uint32_t rs = (uint32_t)(d / L), os = (uint32_t)(d - (unsigned long long)rs * L);
+#pragma unroll
+            for (uint32_t q = 0; q < Q; ++q) {
+                if (!((alive[q] >> lane) & 1ull)) continue;
+                const uint32_t s = lane + 64 * q;
+                const uint32_t cnt = s == ls ? n[q] - done[q] : rs + (o[q] < os ? 1u : 0u);
+                b.fp_seg[(uint64_t)s * T + nseg[q]] = make_uint4(done[q], step, L, o[q]);
+                nseg[q] += 1;
+                done[q] += cnt;
             }
             const uint32_t E = step + (uint32_t)d;
             if (lane == 0) {
                 b.fp_erase[p] = E;
                 if (p == 0) s_e0 = E;
             }
-            // erase live index xs (every lane reads before any writes: one wave)
-            uint32_t mv[FP_TMAX / 64];
+            // t = the erased set's live index; then erase it
+            uint32_t ti = 0;
 #pragma unroll
-            for (uint32_t q = 0; q < FP_TMAX / 64; ++q) {
-                const uint32_t x = xs + lane + 64 * q;
-                mv[q] = x + 1 < L ? s_live[x + 1] : 0u;
+            for (uint32_t q = 0; q < Q; ++q) {
+                if ((ls >> 6) > q) ti += (uint32_t)__popcll(alive[q]);
+                else if ((ls >> 6) == q) {
+                    ti += (uint32_t)__popcll(alive[q] & ((1ull << (ls & 63u)) - 1ull));
+                    alive[q] &= ~(1ull << (ls & 63u));
+                }
             }
-            __builtin_amdgcn_wave_barrier();
-#pragma unroll
-            for (uint32_t q = 0; q < FP_TMAX / 64; ++q) {
-                const uint32_t x = xs + lane + 64 * q;
-                if (x + 1 < L) s_live[x] = mv[q];
-            }
-            __builtin_amdgcn_wave_barrier();
-            L -= 1;
-            t = xs;
+            t = ti;
             step = E + 1;
         }
+#pragma unroll
+        for (uint32_t q = 0; q < Q; ++q)
+            if (lane + 64 * q < T) s_nseg[lane + 64 * q] = nseg[q];
         if (lane == 0) ctl->n_steps = step;
     }
     __syncthreads();

@@ -5062,7 +5062,9 @@ hipError_t launch_rr_mis(const ClauseView& cv, const LoopBuffers& b, hipStream_t
         const bool narrow = b.rr_k >= 1 && b.rr_k <= 4;
         const uint32_t gb = (uint32_t)std::min<uint64_t>((b.m + FP_B - 1) / FP_B + 1, FP_COUNT_GRID);
         const uint32_t gl = (uint32_t)std::min<uint64_t>((b.m + FP_THREADS - 1) / FP_THREADS + 1, 2048);
-        const uint32_t gr = (uint32_t)std::min<uint64_t>((b.m + FP_RT - 1) / FP_RT + 1, 2048);
+        uint32_t fp_grid = 2048;  // workgroups of the grid-stride round kernels (ALLL_FP_GRID: A/B)
+        if (const char* ge = getenv("ALLL_FP_GRID")) fp_grid = (uint32_t)std::max(64, atoi(ge));
+        const uint32_t gr = (uint32_t)std::min<uint64_t>((b.m + FP_RT - 1) / FP_RT + 1, fp_grid);
         hipError_t e = hipMemsetAsync(b.fp_owner, 0xFF, (size_t)b.n_vars * 8, s);
         if (e != hipSuccess) return e;
         e = hipMemsetAsync(b.fp_deg, 0, (size_t)b.n_vars * 4, s);
@@ -5073,7 +5075,7 @@ hipError_t launch_rr_mis(const ClauseView& cv, const LoopBuffers& b, hipStream_t
         else k_fp_deg<0><<<gl, FP_THREADS, 0, s>>>(cv, b);
         k_fp_guess<<<gl, FP_THREADS, 0, s>>>(b);
         const uint32_t gv = (uint32_t)std::min<uint64_t>((b.n_vars + FP_B - 1) / FP_B + 1, FP_COUNT_GRID);
-        const uint32_t gvt = (uint32_t)std::min<uint64_t>((b.n_vars + FP_THREADS - 1) / FP_THREADS + 1, 2048);
+        const uint32_t gvt = (uint32_t)std::min<uint64_t>((b.n_vars + FP_THREADS - 1) / FP_THREADS + 1, fp_grid);
         k_fp_vcount<<<gv, FP_THREADS, 0, s>>>(b);
         k_fp_vscan<<<1, 1024, 0, s>>>(b);
         k_fp_voff<<<gv, FP_THREADS, 0, s>>>(b);

@@ -65,6 +65,8 @@ constexpr uint32_t FP_TMAX = 256;          // sets (the schedule keeps T x T pha
 constexpr uint32_t FP_B = 2048;            // entries per block of the count / turn passes
 constexpr uint32_t FP_G = 4;               // grid LFMIS rounds before the one-workgroup tail
 constexpr uint32_t FP_MAX_DEFAULT = 16;    // LFMIS passes per iteration (graph unroll)
+constexpr uint32_t FP_MAX_LONG = 48;       // ... in the long graph variant, used after an iteration
+constexpr uint32_t FP_LONG_AT = 13;        // that needed more than this many passes
 enum : uint32_t { FP_RUN = 0, FP_FINAL = 1, FP_DONE = 2, FP_OFF = 3, FP_FAIL = 4 };
 struct RRFpCtl {
     uint32_t state;      // FP_*: RUN iterating; FINAL the last pass converged (finalize now);
@@ -80,7 +82,8 @@ struct RRFpCtl {
     uint32_t n_steps;    // schedule length (turns + erasures)
     uint32_t tpre;       // entries whose turn is below this keep the last pass's decision
     uint32_t e0;         // first erasure step of the last schedule
-    uint32_t pad[3];
+    uint32_t nheavy;     // variables with more than FP_HEAVY claimants (fp_heavy)
+    uint32_t pad[2];
     uint32_t cntJ[16];   // survivors of JOIN(r)
     uint32_t cntC[16];   // claimers of CLAIM(r)
 };
@@ -229,6 +232,7 @@ struct LoopBuffers {
     uint32_t* fp_voff;          // n_vars + 1: list range of every variable (shared variables only)
     uint32_t* fp_vlist;         // violated claimants of the shared variables (scan entries)
     uint32_t* fp_vblk;          // block sums / offsets of the list lengths
+    uint32_t* fp_heavy;         // variables whose claimant list is long (one wave each in round 0)
     uint32_t* fp_blk;           // 2 x blocks: pick counts, then their exclusive prefix
     uint32_t* fp_sf;            // T + 1: first scan entry of every set (entries past the last: nu)
     uint32_t* fp_bnd;           // T + 1: picks before the set's first entry inside its block

@@ -2985,7 +2985,7 @@ __device__ __forceinline__ bool fp_settled(const LoopBuffers& b) {
 }
 
 struct RREnt {
-    uint4 a;      // {clause id, literal start, width, 0}
+    uint4 a;      // {clause id, literal start, width, hot-variable mask of slots 0..7}
     uint4 v0, v1; // variables 0..RR_KE-1 (RR_EMPTY past the width)
 };
 static_assert(sizeof(RREnt) == 16 + 4 * RR_KE, "scan entry = header + RR_KE variables");
@@ -3028,11 +3028,15 @@ __global__ __launch_bounds__(256) void k_rr_entries(ClauseView cv, LoopBuffers b
     RREnt* out = reinterpret_cast<RREnt*>(b.rr_u) + base;
     for (uint32_t i = tid; i < n; i += 256) {
         const uint32_t c = s_ids[i], lb = cv.offs[c], w = cv.offs[c + 1] - lb;
-        uint32_t v[8];
+        uint32_t v[8], hm = 0;  // hm: slots whose variable is hot (the fixpoint's degree count)
 #pragma unroll
-        for (uint32_t j = 0; j < 8; ++j) v[j] = j < w ? lit_var(cv.lits[lb + j]) : RR_EMPTY;
+        for (uint32_t j = 0; j < 8; ++j) {
+            const uint32_t raw = j < w ? cv.lits[lb + j] : 0u;
+            v[j] = j < w ? lit_var(raw) : RR_EMPTY;
+            hm |= ((raw & LIT_HOT) ? 1u : 0u) << j;
+        }
         RREnt e;
-        e.a = make_uint4(c, lb, w, 0u);
+        e.a = make_uint4(c, lb, w, hm);
         e.v0 = make_uint4(v[0], v[1], v[2], v[3]);
         e.v1 = make_uint4(v[4], v[5], v[6], v[7]);
         out[i] = e;
@@ -3955,6 +3959,9 @@ static_assert(FP_PER == 8, "a thread's pick bytes are one 8-byte load");
 constexpr uint32_t FP_RT = 256;        // entries per round tile (one per thread): many workgroups per CU
 constexpr uint32_t FP_LDS_SEG_T = 32;     // k_fp_turn keeps the schedule in LDS up to this many sets
 constexpr uint32_t FP_COUNT_GRID = 1024;
+constexpr uint32_t FP_HEAVY = 64;         // claimant lists longer than this are reduced by waves
+constexpr uint32_t FP_SEG = 2048;         // claimants per wave of k_fp_vmin_heavy
+constexpr uint32_t FP_HEAVY_GRID = 512;   // workgroups of k_fp_vmin_heavy
 constexpr uint32_t FP_SCHED_LDS_BLK = 4096;  // k_fp_sched keeps the block offsets in LDS up to this many blocks  // workgroups of k_fp_count / k_fp_turn (grid-stride over blocks)
 
 __device__ __forceinline__ unsigned long long fp_key(const LoopBuffers& b, uint32_t ep, uint32_t turn, uint32_t i) {
@@ -4065,30 +4072,72 @@ __global__ __launch_bounds__(256) void k_fp_begin(LoopBuffers b) {
         ctl->ep_next = 0;
         ctl->tpre = 0;
         ctl->e0 = ~0u;
+        ctl->nheavy = 0;
         if (ctl->guess_den == 0) { ctl->guess_num = 1; ctl->guess_den = 2; }
     }
 }
 
-// Violated claimants per variable (fp_deg, zeroed before), for the sole-claimant masks.
+// Violated claimants per variable (fp_deg, zeroed before); each claim of slots 0..7 keeps the
+// rank its count returned (its place in the variable's list; further slots of wide clauses are
+// counted apart).  Claims on hot variables (power-law hubs, flagged by the host) are counted per
+// workgroup in an LDS table first -- one global atomic per (workgroup, hub) instead of one per
+// claim on one address -- and get their ranks in a third phase.
+constexpr uint32_t FP_RANK_LDS = 0x80000000u;  // rank = LDS slot << 20 | rank within the workgroup
 template <uint32_t KW>
 __global__ __launch_bounds__(FP_THREADS) void k_fp_deg(ClauseView cv, LoopBuffers b) {
     const RRFpCtl* ctl = b.fp_ctl;
     if (ctl->state != FP_RUN) return;
+    __shared__ uint32_t s_hk[HOT_SLOTS], s_hc[HOT_SLOTS];
     const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
     const uint32_t nu = ctl->nu;
+    const bool hot = cv.n_hot != 0;
+    if (hot) {
+        for (uint32_t i = threadIdx.x; i < HOT_SLOTS; i += blockDim.x) { s_hk[i] = ~0u; s_hc[i] = 0u; }
+        __syncthreads();
+    }
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nu; i += gridDim.x * blockDim.x) {
         const uint4 a = U[i].a, v0 = U[i].v0;
-        // slots 0..7 keep the rank their count returned (their place in the variable's list);
-        // further slots (wide clauses) are counted apart and placed by a second counter
         uint32_t rk[8], j = 0;
         fp_for_vars<KW>(cv, U, i, a, v0, [&](uint32_t v) {
-            if (j < 8) rk[j] = atomicAdd(&b.fp_deg[v], 1u);
-            else atomicAdd(&b.fp_deg_hi[v], 1u);
+            if (j < 8 && hot && ((a.w >> j) & 1u)) {
+                uint32_t h = (v * 2654435761u) & (HOT_SLOTS - 1);
+                for (;;) {
+                    const uint32_t prev = atomicCAS(&s_hk[h], ~0u, v);
+                    if (prev == ~0u || prev == v) break;
+                    h = (h + 1) & (HOT_SLOTS - 1);
+                }
+                rk[j] = FP_RANK_LDS | (h << 20) | atomicAdd(&s_hc[h], 1u);
+            } else if (j < 8) {
+                rk[j] = atomicAdd(&b.fp_deg[v], 1u);
+            } else {
+                atomicAdd(&b.fp_deg_hi[v], 1u);
+            }
             ++j;
         });
         uint4* rp = reinterpret_cast<uint4*>(b.fp_rank) + 2 * (uint64_t)i;
         rp[0] = make_uint4(rk[0], rk[1], rk[2], rk[3]);
         if (KW == 0 && a.z > 4) rp[1] = make_uint4(rk[4], rk[5], rk[6], rk[7]);
+    }
+    if (!hot) return;
+    __syncthreads();
+    for (uint32_t h = threadIdx.x; h < HOT_SLOTS; h += blockDim.x)  // the workgroup's claims per hub
+        if (s_hk[h] != ~0u) s_hc[h] = atomicAdd(&b.fp_deg[s_hk[h]], s_hc[h]);
+    __syncthreads();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (this thread's rank stores above)
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nu; i += gridDim.x * blockDim.x) {
+        uint4* rp = reinterpret_cast<uint4*>(b.fp_rank) + 2 * (uint64_t)i;
+        const uint32_t w = U[i].a.z;
+        for (uint32_t q = 0; q < (KW == 0 && w > 4 ? 2u : 1u); ++q) {
+            uint4 r = rp[q];
+            uint32_t* x = &r.x;
+            bool any = false;
+            for (uint32_t e = 0; e < 4; ++e)
+                if (4 * q + e < w && (x[e] & FP_RANK_LDS)) {
+                    x[e] = s_hc[(x[e] >> 20) & (HOT_SLOTS - 1)] + (x[e] & 0xFFFFFu);
+                    any = true;
+                }
+            if (any) rp[q] = r;
+        }
     }
 }
 
@@ -4188,6 +4237,13 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_voff(LoopBuffers b) {
         for (uint32_t e = 0; e < FP_PER; ++e) {
             if (v0 + e < nv) b.fp_voff[v0 + e] = off;
             off += d[e];
+            // long lists (hubs of skewed instances): a wave per FP_SEG claimants in k_fp_vmin_heavy
+            if (d[e] > FP_HEAVY) {
+                const uint32_t ns = (d[e] + FP_SEG - 1) / FP_SEG;
+                const uint32_t h0 = atomicAdd(&b.fp_ctl->nheavy, ns);
+                for (uint32_t k = 0; k < ns; ++k)
+                    reinterpret_cast<uint2*>(b.fp_heavy)[h0 + k] = make_uint2(v0 + e, off - d[e] + k * FP_SEG);
+            }
         }
     }
 }
@@ -4222,6 +4278,33 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_vfill(ClauseView cv, LoopBuff
     }
 }
 
+// round 0 of a pass for the variables with more than FP_HEAVY claimants: a wave per segment of
+// FP_SEG claimants, lanes striding it; segments meet in the owner key by atomicMin (keys of this
+// pass are below every earlier one), and JOIN(0) compares keys for such variables (own0 = ~0)
+__global__ __launch_bounds__(FP_THREADS) void k_fp_vmin_heavy(LoopBuffers b) {
+    const RRFpCtl* ctl = b.fp_ctl;
+    if (ctl->state != FP_RUN) return;
+    const uint32_t ep = ctl->ep_base, nh = ctl->nheavy, lane = threadIdx.x & 63;
+    for (uint32_t h = blockIdx.x * (FP_THREADS / 64) + (threadIdx.x >> 6); h < nh; h += gridDim.x * (FP_THREADS / 64)) {
+        const uint2 sg = reinterpret_cast<const uint2*>(b.fp_heavy)[h];
+        const uint32_t v = sg.x, o1 = min(b.fp_voff[v + 1], sg.y + FP_SEG);
+        unsigned long long best = ~0ull;
+        for (uint32_t o = sg.y + lane; o < o1; o += 64) {
+            const uint32_t i = b.fp_vlist[o];
+            const unsigned long long k = fp_key(b, ep, b.fp_turn[i], i);
+            best = k < best ? k : best;
+        }
+        for (int sh = 32; sh > 0; sh >>= 1) {
+            const unsigned long long y = __shfl_xor(best, sh, 64);
+            best = y < best ? y : best;
+        }
+        if (lane == 0) {
+            b.fp_own0[v] = ~0u;
+            atomicMin(&b.fp_owner[v], best);
+        }
+    }
+}
+
 // round 0 of a pass: the minimum key over every shared variable's claimants
 __global__ __launch_bounds__(FP_THREADS) void k_fp_vmin(LoopBuffers b) {
     const RRFpCtl* ctl = b.fp_ctl;
@@ -4229,7 +4312,7 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_vmin(LoopBuffers b) {
     const uint32_t ep = ctl->ep_base, nv = b.n_vars;
     for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += gridDim.x * blockDim.x) {
         const uint32_t o0 = b.fp_voff[v], o1 = b.fp_voff[v + 1];
-        if (o1 - o0 < 2) continue;
+        if (o1 - o0 < 2 || o1 - o0 > FP_HEAVY) continue;
         unsigned long long best = ~0ull;
         for (uint32_t o = o0; o < o1; ++o) {
             const uint32_t i = b.fp_vlist[o];
@@ -4319,7 +4402,10 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_join(ClauseView cv, LoopBuffe
                     pre = true;
                     own = (b.fp_in[i] >> 1) & 1u;
                 } else if (r == 0) {
-                    fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) { own &= b.fp_own0[v] == i; });
+                    fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) {
+                        const uint32_t w = b.fp_own0[v];  // (~0: a long list, reduced into the key)
+                        own &= w == i || (w == ~0u && b.fp_owner[v] == fp_key(b, ep, turn, i));
+                    });
                 } else {
                     const unsigned long long key = fp_key(b, ep, turn, i);
                     fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) { own &= b.fp_owner[v] == key; });
@@ -5092,6 +5178,7 @@ hipError_t launch_rr_mis(const ClauseView& cv, const LoopBuffers& b, hipStream_t
             for (uint32_t r = 0; r < FP_G; ++r) {
                 if (r == 0) {
                     k_fp_vmin<<<gvt, FP_THREADS, 0, s>>>(b);
+                    k_fp_vmin_heavy<<<FP_HEAVY_GRID, FP_THREADS, 0, s>>>(b);
                     if (narrow) k_fp_join<4><<<gr, FP_THREADS, 0, s>>>(cv, b, 0);
                     else k_fp_join<0><<<gr, FP_THREADS, 0, s>>>(cv, b, 0);
                 } else if (narrow) {

@@ -106,6 +106,9 @@ struct alll_ctx {
     // device a batch behind instead of freezing at the last read); an assignment set by the
     // caller makes it unknown (treated as large).
     uint64_t hint_u = ~0ull, hint_iter = 0;
+    uint32_t hint_rounds = 0;     // the last state read's tail_rounds (round robin: fixpoint passes)
+    uint32_t fp_max_long = 0;     // round robin: passes of the long graph variant (iterations that needed many)
+    uint32_t fp_long_at = FP_LONG_AT;  // ... chosen after an iteration with more passes (ALLL_RR_FP_LONG_AT)
     DevState* h_async = nullptr;  // pinned
     hipEvent_t ev_async = nullptr;
     bool async_pending = false;
@@ -285,6 +288,7 @@ int read_state(alll_ctx* c) {
     HIP_TRY(hipStreamSynchronize(c->stream));
     c->hint_u = c->h_state->u_total;
     c->hint_iter = c->h_state->n_iter;
+    c->hint_rounds = c->h_state->tail_rounds;
     c->async_pending = false;  // (the stream is drained: this read is newer)
     if (c->h_state->error == 2)
         return fail(ALLL_ERR_UNSUPPORTED, "a variable has more violated claimants than the dependency-driven "
@@ -343,6 +347,9 @@ int host_exchange(alll_ctx* c, int op, void* dev, size_t bytes, size_t own_off) 
 // skewed instances, see create).
 int round0_variant(const alll_ctx* c) {
     const uint64_t u = c->hint_u;
+    // round robin: the long fixpoint graph (fp_max_long passes) after an iteration that needed
+    // more than FP_LONG_AT passes (or fell back to the batch kernels)
+    if (c->b.rr_T) return c->b.fp_ctl && c->fp_max_long > c->b.fp_max && c->hint_rounds > c->fp_long_at ? 1 : 0;
     if (c->b.pairs && (c->hint_iter == 0 || u >= c->bucket_min_u)) return 1;
     // few violated clauses (the end of a converging solve): round 0 on the grid, the rest in
     // the one-workgroup tail -- 6 launches per iteration instead of 12, each ~4.5 us even
@@ -356,6 +363,7 @@ void refresh_hint(alll_ctx* c) {
     if (!c->async_pending || hipEventQuery(c->ev_async) != hipSuccess) return;
     c->hint_u = c->h_async->u_total;
     c->hint_iter = c->h_async->n_iter;
+    c->hint_rounds = c->h_async->tail_rounds;
     c->async_pending = false;
 }
 
@@ -393,7 +401,9 @@ int enqueue_iteration(alll_ctx* c, hipEvent_t* marks, int variant) {
     const bool fused = c->fuse_reduce && variant == 1 && !xchg && !c->b.rr_T;
     if (!fused) HIP_TRY(launch_reduce(c->b, 0, s));
     if (c->b.rr_T) {
-        HIP_TRY(launch_rr_mis(c->cv, c->b, s));
+        LoopBuffers lb = c->b;
+        if (variant == 1) lb.fp_max = c->fp_max_long;
+        HIP_TRY(launch_rr_mis(c->cv, lb, s));
     } else if (variant == 1 && c->dd) {
         HIP_TRY(launch_lfmis_dd(c->cv, c->b, scatter, fused, s));
     } else {
@@ -776,6 +786,7 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
             if ((rc = dalloc(c, &b.fp_voff, (size_t)prob->n_vars + 2))) return bail(rc);
             if ((rc = dalloc(c, &b.fp_vlist, (size_t)L + 1))) return bail(rc);
             if ((rc = dalloc(c, &b.fp_vblk, (size_t)prob->n_vars / FP_B + 2))) return bail(rc);
+            if ((rc = dalloc(c, &b.fp_heavy, 2 * ((size_t)L / 64 + 2)))) return bail(rc);  // (segments of lists > 64 claims)
             if ((rc = dalloc(c, &b.fp_blk, 2 * nblk + 2048))) return bail(rc);  // sums, offsets, changes, earliest changes
             if ((rc = dalloc(c, &b.fp_sf, rr_T + 1))) return bail(rc);
             if ((rc = dalloc(c, &b.fp_bnd, rr_T + 1))) return bail(rc);
@@ -786,7 +797,10 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
             b.fp_ib = ib;
             b.fp_tb = tb;
             b.fp_max = FP_MAX_DEFAULT;
-            if (const char* e = getenv("ALLL_RR_FP_MAX")) b.fp_max = (uint32_t)std::max(1, std::min(256, atoi(e)));
+            c->fp_max_long = FP_MAX_LONG;
+            if (const char* e = getenv("ALLL_RR_FP_LONG_AT")) c->fp_long_at = (uint32_t)std::max(0, atoi(e));
+            if (const char* e = getenv("ALLL_RR_FP_MAX"))
+                c->fp_max_long = b.fp_max = (uint32_t)std::max(1, std::min(256, atoi(e)));
         }
     }
     if ((rc = dalloc(c, &b.A, b.n_words + 4))) return bail(rc);  // +4: 16-byte tail loads

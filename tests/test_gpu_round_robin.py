@@ -12,7 +12,7 @@ caller's vector<ClauseArray*>), bit-exact:
   * ALLL_FLAG_LFMIS keeps the one-set MIS for T > 1.
 
 Every test runs with each way of deciding the MIS: the fixpoint passes (default, DESIGN.md
-§4.3.2), the same passes capped at one or two per iteration (ALLL_RR_FP_MAX, so that most
+§4.3.2; also in the long graph variant), the same passes capped at one or two per iteration (ALLL_RR_FP_MAX, so that most
 iterations fall back to the batch kernel mid-run), and the batch kernels alone (ALLL_RR_FP=0):
 across workgroups (k_rr_mw) and in one workgroup (k_rr_mis, ALLL_RR_MW=0).
 """
@@ -38,11 +38,13 @@ def gpu(native):
     return True
 
 
-@pytest.fixture(params=["fp", "fp_cap1", "fp_cap2", "mw", "one"], autouse=True)
+@pytest.fixture(params=["fp", "fp_long", "fp_cap1", "fp_cap2", "mw", "one"], autouse=True)
 def rr_kernel(request, monkeypatch):
-    for k in ("ALLL_RR_MW", "ALLL_RR_FP", "ALLL_RR_FP_MAX"):
+    for k in ("ALLL_RR_MW", "ALLL_RR_FP", "ALLL_RR_FP_MAX", "ALLL_RR_FP_LONG_AT"):
         monkeypatch.delenv(k, raising=False)
-    if request.param.startswith("fp_cap"):
+    if request.param == "fp_long":  # the long graph variant (48 passes) from the second launch on
+        monkeypatch.setenv("ALLL_RR_FP_LONG_AT", "0")
+    elif request.param.startswith("fp_cap"):
         monkeypatch.setenv("ALLL_RR_FP_MAX", request.param[-1])
     elif request.param in ("mw", "one"):
         monkeypatch.setenv("ALLL_RR_FP", "0")

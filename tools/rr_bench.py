@@ -13,6 +13,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 CONFIGS = {"M": (2_500_000, 10_000_000, 3, 0), "C2": (1_000_000, 4_000_000, 3, 0),
+           "C3": (4_000_000, 6_000_000, 8, 0), "C5": (2_500_000, 10_000_000, 3, 1),
            "S": (250_000, 1_000_000, 3, 0),
            "R": (25_000, 100_000, 3, 0)}  # bench.py's cpu_baseline sample of the reference -p path
 

@@ -37,11 +37,12 @@ def worker(rank, world, port, spec, flags, out_q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    n, m, k, kind, seed, K = spec
+    n, m, k, kind, seed, K = spec[:6]
+    T = spec[6] if len(spec) > 6 else 1
     offs, lits = generate_ksat(1, n, m, k, kind)
     try:
         with Solver(n, offs, lits, seed=seed, device=0, rank=rank, world=world, flags=flags,
-                    exchange=gloo_exchange()) as s:
+                    exchange=gloo_exchange(), n_threads=T) as s:
             traj = []
             for _ in range(K):
                 s.run(1)
@@ -78,6 +79,9 @@ SPECS = {
     # BASELINE config C2 at full size (1M variables, 4M clauses = 977 tiles, 489 per rank):
     # two iterations, bit-exact on both ranks
     "c2": (1_000_000, 4_000_000, 3, 0, 1, 2),
+    # the round robin of T = 4 / 7 sets (the fixpoint passes) on every rank of the sharded loop
+    "small_rr4": (7000, 28000, 3, 0, 5, 8, 4),
+    "c2_rr7": (1_000_000, 4_000_000, 3, 0, 1, 2, 7),
 }
 
 
@@ -85,13 +89,16 @@ SPECS = {
                                                   (3, "allgather", "small"), (3, "allreduce", "small"),
                                                   (2, "allgather", "windows"), (2, "allgather", "long"),
                                                   (2, "allreduce", "long"), (2, "allgather", "c2"),
-                                                  (2, "allreduce", "c2")])
+                                                  (2, "allreduce", "c2"), (2, "allgather", "small_rr4"),
+                                                  (3, "allreduce", "small_rr4"), (2, "allgather", "c2_rr7")])
 def test_sharded_solver_matches_oracle(oracle_mod, native, world, mode, spec_name):
     o = oracle_mod
-    n, m, k, kind, seed, K = spec = SPECS[spec_name]
+    spec = SPECS[spec_name]
+    n, m, k, kind, seed, K = spec[:6]
+    T = spec[6] if len(spec) > 6 else 1
     flags = native.FLAG_EXCHANGE_ALLREDUCE if mode == "allreduce" else 0
     offs, lits = o.generate_ksat(1, n, m, k, kind)
-    st_o, A_o, rows = o.solve(n, offs, lits, seed, max_iters=K + 1, trace=True)
+    st_o, A_o, rows = o.solve(n, offs, lits, seed, max_iters=K + 1, trace=True, T=T)
     res = run_world(world, spec, flags)
     for rank, traj, st, mis, err in res:
         assert err is None, f"rank {rank}: {err}"

@@ -74,7 +74,7 @@ struct RRFpCtl {
     uint32_t nu;         // violated clauses (scan entries) of the iteration
     uint32_t fp_iter;    // LFMIS passes so far in this iteration
     uint32_t changes;    // picks that differ between the last two passes
-    uint32_t serial;     // cover serial of the current LFMIS pass (fp_cov), never 0
+    uint32_t serial;     // cover serial of the current LFMIS pass (fp_cov, 8-bit, cleared per iteration), never 0
     uint32_t ep_base;    // owner epoch of round 0 of the current pass (owner reset per iteration)
     uint32_t ep_next;    // first epoch after the current pass
     uint32_t total;      // picks of the last pass
@@ -224,7 +224,7 @@ struct LoopBuffers {
     uint32_t* fp_tcnt;          // 2 FP_G x tiles: list lengths per round and tile
     unsigned long long* fp_owner; // n_vars claim keys {epoch | turn | entry}, reset every iteration
     uint32_t* fp_own0;          // n_vars: round-0 winner (entry) of every shared variable
-    uint32_t* fp_cov;           // n_vars: serial of the pass whose pick covers the variable
+    uint8_t* fp_cov;            // n_vars: serial of the pass whose pick covers the variable (cleared per iteration)
     uint32_t* fp_deg;           // n_vars: violated claimants this iteration (slots 0..7 of their clauses)
     uint32_t* fp_deg_hi;        // n_vars: the same from slots past 8 (wide clauses)
     uint32_t* fp_rank;          // 8 per scan entry: slot j's place in its variable's claimant list

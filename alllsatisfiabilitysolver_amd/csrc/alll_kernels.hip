@@ -4070,6 +4070,7 @@ __global__ __launch_bounds__(256) void k_fp_begin(LoopBuffers b) {
         ctl->changes = 0;
         ctl->ep_base = 0;
         ctl->ep_next = 0;
+        ctl->serial = 0;  // (fp_cov was cleared for this iteration)
         ctl->tpre = 0;
         ctl->e0 = ~0u;
         ctl->nheavy = 0;
@@ -4355,7 +4356,7 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_claim(ClauseView cv, LoopBuff
                 const uint32_t sole = b.fp_sole[i];
                 const uint32_t turn = b.fp_turn[i];
                 bool dead = false;
-                fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) { dead |= b.fp_cov[v] == serial; });
+                fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) { dead |= b.fp_cov[v] == (uint8_t)serial; });
                 if (!dead) {
                     const unsigned long long key = fp_key(b, ep, turn, i);
                     fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) { atomicMin(&b.fp_owner[v], key); });
@@ -4411,7 +4412,7 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_join(ClauseView cv, LoopBuffe
                     fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) { own &= b.fp_owner[v] == key; });
                 }
                 if (own) {
-                    fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) { b.fp_cov[v] = serial; });
+                    fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) { b.fp_cov[v] = (uint8_t)serial; });
                     b.fp_in[i] = (uint8_t)(b.fp_in[i] | 1u);
                 }
                 keep = !own && !pre;
@@ -4454,7 +4455,7 @@ __global__ __launch_bounds__(1024) void k_fp_tail(ClauseView cv, LoopBuffers b) 
                 const uint32_t sole = b.fp_sole[i];
                 bool dead = false;
                 fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) {
-                    dead |= __hip_atomic_load(&b.fp_cov[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == serial;
+                    dead |= __hip_atomic_load(&b.fp_cov[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint8_t)serial;
                 });
                 if (!dead) {
                     const unsigned long long key = fp_key(b, ep, b.fp_turn[i], i);
@@ -4485,7 +4486,7 @@ __global__ __launch_bounds__(1024) void k_fp_tail(ClauseView cv, LoopBuffers b) 
                 });
                 if (own) {
                     fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) {
-                        __hip_atomic_store(&b.fp_cov[v], serial, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(&b.fp_cov[v], (uint8_t)serial, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     });
                     b.fp_in[i] = (uint8_t)(b.fp_in[i] | 1u);
                 }
@@ -4760,8 +4761,8 @@ __global__ __launch_bounds__(256) void k_fp_sched(LoopBuffers b, int test) {
         } else {
             if (test) ctl->fp_iter += 1;
             ctl->ep_base = ctl->ep_next;
-            ctl->serial = ctl->serial + 1u ? ctl->serial + 1u : 1u;
-            if (ctl->ep_base + FP_G + 1u >= fp_ep_budget(b)) ctl->state = FP_FAIL;
+            ctl->serial = ctl->serial + 1u;  // 8-bit cover serials: at most 255 passes per iteration
+            if (ctl->ep_base + FP_G + 1u >= fp_ep_budget(b) || ctl->serial > 255u) ctl->state = FP_FAIL;
         }
     }
 }
@@ -5153,7 +5154,8 @@ hipError_t launch_rr_mis(const ClauseView& cv, const LoopBuffers& b, hipStream_t
         const uint32_t gr = (uint32_t)std::min<uint64_t>((b.m + FP_RT - 1) / FP_RT + 1, fp_grid);
         hipError_t e = hipMemsetAsync(b.fp_owner, 0xFF, (size_t)b.n_vars * 8, s);
         if (e != hipSuccess) return e;
-        e = hipMemsetAsync(b.fp_deg, 0, (size_t)b.n_vars * 4, s);
+        e = hipMemsetAsync(b.fp_cov, 0, (size_t)b.n_vars, s);
+        if (e == hipSuccess) e = hipMemsetAsync(b.fp_deg, 0, (size_t)b.n_vars * 4, s);
         if (e == hipSuccess && !narrow) e = hipMemsetAsync(b.fp_deg_hi, 0, (size_t)b.n_vars * 4, s);
         if (e != hipSuccess) return e;
         k_fp_begin<<<1, 256, 0, s>>>(b);

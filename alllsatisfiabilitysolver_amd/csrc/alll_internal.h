@@ -220,6 +220,7 @@ struct LoopBuffers {
     RRFpCtl* fp_ctl;
     uint8_t* fp_in;             // per scan entry: bit 0 picked by the last pass, bit 1 by the one before
     uint32_t* fp_turn;          // per scan entry: turn = LFMIS priority of the next pass
+    uint4* fp_v4;               // per scan entry of narrow instances: its variables (16-byte copy)
     uint32_t* fp_list;          // 2 x m: round lists per tile of FP_B entries (JOIN output, CLAIM output)
     uint32_t* fp_tcnt;          // 2 FP_G x tiles: list lengths per round and tile
     unsigned long long* fp_owner; // n_vars claim keys {epoch | turn | entry}, reset every iteration

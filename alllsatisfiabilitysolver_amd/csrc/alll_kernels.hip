@@ -4020,6 +4020,19 @@ __device__ __forceinline__ void fp_for_shared(const ClauseView& cv, const RREnt*
     }
 }
 
+// an entry's header and first 4 variables in a pass; narrow instances (one width <= 4) read
+// the 16-byte copy k_fp_vfill made (a third of the 48-byte scan entry's lines)
+template <uint32_t KW>
+__device__ __forceinline__ void fp_ent(const LoopBuffers& b, const RREnt* U, uint32_t i, uint4& a, uint4& v0) {
+    if constexpr (KW == 4) {
+        v0 = b.fp_v4[i];
+        a = make_uint4(0u, 0u, b.rr_k, 0u);
+    } else {
+        a = U[i].a;
+        v0 = U[i].v0;
+    }
+}
+
 // largest s < T with sf[s] <= i (sf non-decreasing, sf[0] = 0): the set of entry i < nu
 __device__ __forceinline__ uint32_t fp_set_of(const uint32_t* sf, uint32_t T, uint32_t i) {
     uint32_t lo = 0, hi = T;
@@ -4263,6 +4276,7 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_vfill(ClauseView cv, LoopBuff
         const uint4* rp = reinterpret_cast<const uint4*>(b.fp_rank) + 2 * (uint64_t)i;
         const uint4 r0 = rp[0], r1 = (KW == 0 && a.z > 4) ? rp[1] : make_uint4(0, 0, 0, 0);
         const uint32_t rk[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+        if constexpr (KW == 4) b.fp_v4[i] = v0;
         uint32_t sole = 0, j = 0;
         fp_for_vars<KW>(cv, U, i, a, v0, [&](uint32_t v) {
             const uint32_t o = b.fp_voff[v], d = b.fp_voff[v + 1] - o;
@@ -4352,7 +4366,8 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_claim(ClauseView cv, LoopBuff
             uint32_t i = 0;
             if (j < n) {
                 i = lin[j];
-                const uint4 a = U[i].a, v0 = U[i].v0;
+                uint4 a, v0;
+                fp_ent<KW>(b, U, i, a, v0);
                 const uint32_t sole = b.fp_sole[i];
                 const uint32_t turn = b.fp_turn[i];
                 bool dead = false;
@@ -4395,7 +4410,8 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_join(ClauseView cv, LoopBuffe
             uint32_t i = 0;
             if (j < n) {
                 i = r == 0 ? i0 + j : lin[j];
-                const uint4 a = U[i].a, v0 = U[i].v0;
+                uint4 a, v0;
+                fp_ent<KW>(b, U, i, a, v0);
                 const uint32_t sole = b.fp_sole[i];
                 const uint32_t turn = b.fp_turn[i];
                 bool own = true, pre = false;
@@ -4451,7 +4467,8 @@ __global__ __launch_bounds__(1024) void k_fp_tail(ClauseView cv, LoopBuffers b) 
             uint32_t i = 0;
             if (j < n) {
                 i = la[j];
-                const uint4 a = U[i].a, v0 = U[i].v0;
+                uint4 a, v0;
+                fp_ent<KW>(b, U, i, a, v0);
                 const uint32_t sole = b.fp_sole[i];
                 bool dead = false;
                 fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) {
@@ -4477,7 +4494,8 @@ __global__ __launch_bounds__(1024) void k_fp_tail(ClauseView cv, LoopBuffers b) 
             uint32_t i = 0;
             if (j < nc) {
                 i = lb[j];
-                const uint4 a = U[i].a, v0 = U[i].v0;
+                uint4 a, v0;
+                fp_ent<KW>(b, U, i, a, v0);
                 const uint32_t sole = b.fp_sole[i];
                 const unsigned long long key = fp_key(b, ep, b.fp_turn[i], i);
                 bool own = true;

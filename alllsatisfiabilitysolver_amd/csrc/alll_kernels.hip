@@ -4334,10 +4334,10 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_vmin(LoopBuffers b) {
             const unsigned long long k = fp_key(b, ep, b.fp_turn[i], i);
             best = k < best ? k : best;
         }
-        // JOIN(0) reads the winning entry from a 4-byte array (half the footprint of the keys);
-        // the later rounds' atomics start from the round-0 key
+        // JOIN(0) reads the winning entry from a 4-byte array (half the footprint of the keys).
+        // The owner key itself is not needed: the later rounds' claims are of later epochs,
+        // below any key an earlier pass or round left there
         b.fp_own0[v] = (uint32_t)best & ((1u << b.fp_ib) - 1u);
-        b.fp_owner[v] = best;
     }
 }
 

@@ -84,8 +84,7 @@ struct RRFpCtl {
     uint32_t e0;         // first erasure step of the last schedule
     uint32_t nheavy;     // variables with more than FP_HEAVY claimants (fp_heavy)
     uint32_t pad[2];
-    uint32_t cntJ[16];   // survivors of JOIN(r)
-    uint32_t cntC[16];   // claimers of CLAIM(r)
+    uint32_t cntJ[16];   // survivors of the last grid JOIN (k_fp_tail's list; the rounds count per tile)
 };
 // In-loop kernel timing (ALLL_FLAG_KERNEL_TIMING): per iteration i, slot i % TIME_SLOTS holds
 // device wall-clock stamps (s_memrealtime) {eval start (min over workgroups), eval end (max),

@@ -4075,7 +4075,7 @@ __global__ __launch_bounds__(256) void k_fp_begin(LoopBuffers b) {
         }
         b.fp_sf[s] = s == T ? nu : lo;
     }
-    if (threadIdx.x < 16) { ctl->cntJ[threadIdx.x] = 0; ctl->cntC[threadIdx.x] = 0; }
+    if (threadIdx.x < 16) ctl->cntJ[threadIdx.x] = 0;
     if (threadIdx.x == 0) {
         ctl->state = FP_RUN;
         ctl->nu = nu;
@@ -4586,7 +4586,7 @@ __global__ __launch_bounds__(256) void k_fp_sched(LoopBuffers b, int test) {
     }
     if (state != FP_RUN) return;
     __shared__ uint32_t s_w[16], s_e0;
-    __shared__ uint32_t s_n[FP_TMAX], s_done[FP_TMAX], s_live[FP_TMAX], s_nseg[FP_TMAX], s_pf[FP_TMAX + 1];
+    __shared__ uint32_t s_n[FP_TMAX], s_nseg[FP_TMAX], s_pf[FP_TMAX + 1];
     __shared__ uint32_t s_off[FP_SCHED_LDS_BLK];  // block offsets (when they fit)
     const uint32_t nu = ctl->nu, T = b.rr_T, nblk = (nu + FP_B - 1) / FP_B;
     uint32_t* blkoff = b.fp_blk + (b.m / FP_B + 2);
@@ -4640,8 +4640,6 @@ __global__ __launch_bounds__(256) void k_fp_sched(LoopBuffers b, int test) {
     __syncthreads();
     for (uint32_t s = threadIdx.x; s < T; s += blockDim.x) {
         s_n[s] = s_pf[s + 1] - s_pf[s];
-        s_done[s] = 0;
-        s_live[s] = s;
         s_nseg[s] = 0;
     }
     __syncthreads();
@@ -4763,7 +4761,7 @@ __global__ __launch_bounds__(256) void k_fp_sched(LoopBuffers b, int test) {
     }
     __syncthreads();
     for (uint32_t s = threadIdx.x; s < T; s += blockDim.x) b.fp_nseg[s] = s_nseg[s];
-    if (threadIdx.x < 16) { ctl->cntJ[threadIdx.x] = 0; ctl->cntC[threadIdx.x] = 0; }
+    if (threadIdx.x < 16) ctl->cntJ[threadIdx.x] = 0;
     if (threadIdx.x == 0) {
         ctl->total = total;
         ctl->changes = 0;

@@ -6,7 +6,7 @@ include/alll.h (liballl.so).  This package is the Python front-end of that libra
 """
 from ._native import AlllError, build, lib  # noqa: F401
 from .solver import (Clause, SATInstance, Solver, Statistics, VariablesArray,  # noqa: F401
-                     comm_unique_id, device_count, generate_ksat, generate_mixed, gloo_exchange,
+                     assignment_digest, comm_unique_id, device_count, generate_ksat, generate_mixed, gloo_exchange,
                      parse_dimacs,
                      read_dimacs, shard_plan)
 

@@ -43,7 +43,7 @@ EXPORTED = [
     "alll_comm_unique_id", "alll_create", "alll_destroy", "alll_set_host_exchange", "alll_solve", "alll_run",
     "alll_get_stats", "alll_verify", "alll_get_assignment", "alll_set_assignment",
     "alll_get_assignment_words", "alll_set_assignment_words", "alll_get_violated_mask",
-    "alll_get_mis", "alll_bench_eval", "alll_profile", "alll_loop_times", "alll_debug_phases", "alll_synchronize", "alll_eval_bytes",
+    "alll_get_mis", "alll_bench_eval", "alll_profile", "alll_loop_times", "alll_synchronize", "alll_eval_bytes",
     "alll_layout", "alll_eval_kernel", "alll_comm_size", "alll_uses_graphs", "alll_initial_assignment", "alll_shard_plan", "alll_dimacs_parse", "alll_dimacs_read", "alll_generate_ksat",
 ]
 
@@ -146,8 +146,6 @@ _SIGS = {
     "alll_bench_eval": ([_vp, ctypes.c_int, ctypes.POINTER(ctypes.c_double), _u64p], ctypes.c_int),
     "alll_profile": ([_vp, ctypes.c_uint64, ctypes.POINTER(PhaseTimes)], ctypes.c_int),
     "alll_loop_times": ([_vp, ctypes.c_uint64, ctypes.c_uint64, ctypes.POINTER(PhaseTimes)], ctypes.c_int),
-    "alll_debug_phases": ([_vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint64, ctypes.POINTER(ctypes.c_int)],
-                          ctypes.c_int),
     "alll_synchronize": ([_vp], ctypes.c_int),
     "alll_eval_bytes": ([_vp], ctypes.c_uint64),
     "alll_layout": ([_vp], ctypes.c_int),

@@ -40,19 +40,8 @@ constexpr uint32_t BKT_SHIFT_MIN = 10;
 constexpr uint32_t BKT_SHIFT_MAX = 15;        // LDS minima of k_bresolve: 4 << 15 = 128 KiB
 constexpr uint32_t RUN_TILES_MAX = 16;        // entry index within a run < 16 * TILE = 2^16
 constexpr int BKT_THREADS = 512;
-constexpr uint32_t BKT_RUN_BATCH = 1024;        // runs per segment-table batch of k_bresolve / k_bsort
+constexpr uint32_t BKT_RUN_BATCH = 1024;        // runs per segment-table batch of k_bresolve
 constexpr unsigned long long PAIR_LOSE = 1ull << 31;
-// Dependency-driven LFMIS (one GPU, fixed width, no hot variables, clause-order priorities):
-// k_bsort links every round-0 pair to the next claimant of its variable in clause order, then
-// k_decide (one persistent workgroup per run, all resident) decides every violated clause by
-// messages along those per-variable chains instead of grid rounds.
-constexpr int DDS_THREADS = 1024;        // k_bsort workgroup
-constexpr int DDS_UNROLL = 12;           // items per thread and sweep of k_bsort (12288 per sweep)
-constexpr int DDS_UNROLL_GEN = 8;        // items per thread and sweep of k_bsort_general
-constexpr uint32_t DDS_SUBW = 2048;      // variables per sort sub-range (LDS counters)
-constexpr uint32_t DDS_CAP = 4096;       // pairs sorted in LDS at once (a variable's claimants must fit)
-constexpr int DDD_THREADS = 1024;        // k_decide workgroup (one per CU)
-constexpr uint32_t DD_TIMEOUT = 10000000u;  // k_decide gives up after 100 ms (100 MHz wall clock)
 // Round-robin MIS of T > 1 clause chunks (the reference's n_threads > 1): at most RR_TMAX sets.
 constexpr uint32_t RR_TMAX = 2048;
 constexpr uint32_t RR_MW_GH = 1u << 15;  // k_rr_mw global hash slots
@@ -91,8 +80,6 @@ struct RRFpCtl {
 // reduce start, LFMIS tail end}.
 constexpr uint32_t TIME_SLOTS = 4096;
 constexpr uint32_t TIME_FIELDS = 4;
-// Diagnostics: DBG_KERNELS regions x DBG_BLOCKS workgroups x DBG_FIELDS phase stamps (last iteration).
-constexpr uint32_t DBG_KERNELS = 4, DBG_BLOCKS = 8192, DBG_FIELDS = 8;
 
 // Device-resident loop state.  Written only by the single-block reduce / tail kernels,
 // read by every other kernel at entry (kernel boundaries order the accesses).
@@ -109,7 +96,8 @@ struct DevState {
     uint32_t round_next;   // first unused epoch
     uint32_t tail_rounds;  // rounds the tail kernel needed in the last iteration
     uint32_t max_rounds;   // max total rounds seen in one iteration
-    uint32_t error;        // 1: LFMIS exceeded MAX_TAIL_ROUNDS (loop stopped, done = 3)
+    uint32_t error;        // loop stopped (done = 3): 1 LFMIS exceeded MAX_TAIL_ROUNDS or the round
+                           // robin its batch cap; 4 a k_rr_mw grid barrier timed out
     uint32_t left_cnt;     // undecided entries handed from the last grid round to the tail
     uint32_t tmis_cnt;     // MIS entries decided by the tail kernel (list b.tmis)
     uint64_t win_start;    // streaming solve: generator steps taken before this iteration
@@ -161,9 +149,6 @@ struct LoopBuffers {
     uint32_t* left;         // compact list of undecided entries handed to the tail kernel
     uint32_t* tmis;         // MIS clauses decided by the tail kernel
     unsigned long long* owner; // n_vars 64-bit owner keys (epoch-tagged, never reset)
-    uint64_t owner_alt;        // 0: one owner array for every epoch; else the offset (in keys) of
-                               // a second array that odd epochs use (the fused JOIN(r)+CLAIM(r+1)
-                               // rounds read round r's keys while claiming round r+1's)
     uint8_t* cover;         // per variable: stamp of the iteration whose MIS covers it (the
                             // reduce clears it when the stamp cycles back to 1)
     unsigned long long* tile_stats; // per tile: [2t] sum |MIS|, [2t+1] sum resampled literals
@@ -173,10 +158,6 @@ struct LoopBuffers {
     unsigned long long* pairs;  // bucketed round 0: n_runs x run_tiles*TILE*K pairs (nullptr = atomics)
     unsigned long long* runtab; // [bucket][run]: start | count << 32 of the bucket's pairs in the run
     uint32_t* run_pairs;        // pairs per run
-    uint32_t* dd_msg;           // dependency-driven LFMIS: one message word per pair position (chain
-                                // state of the pair's variable below its clause, tagged with n_iter);
-                                // nullptr = the round-synchronous LFMIS
-    uint32_t dd_senders;        // k_decide: one wave only sends (the others queue in LDS)
     const uint32_t* win_base;   // hybrid eval: per tile, first assignment word of its LDS window
                                 // (nullptr: words [0, win_words) for every tile)
     uint32_t win_words;         // hybrid eval: LDS window size in words (<= LDS_WORDS)
@@ -195,7 +176,6 @@ struct LoopBuffers {
     uint32_t n_runs;
     const uint32_t* run_t0;     // n_runs + 1: first tile of every run (runs split the tile range of
                                 // every evaluation workgroup, so one GPU scatters inside k_eval_hybrid)
-    unsigned long long* kdbg;   // diagnostics (env ALLL_DEBUG_PHASES): per-workgroup phase stamps
     // streaming solve (SATInstance::solve(getEnumeratedClause, ...), T = 1): LFMIS priority =
     // position in the clause generator's yield window (alll_options.stream_batch > 0)
     uint64_t m;                 // clauses
@@ -213,8 +193,8 @@ struct LoopBuffers {
     uint32_t* rr_gmin;
     uint32_t* rr_ptr;
     uint32_t* rr_end;
-    uint32_t rr_mw;             // workgroups of k_rr_mw (0: the one-workgroup k_rr_mis)
-    // round robin by fixpoint (nullptr = off; k_rr_mw / k_rr_mis then decide every iteration,
+    uint32_t rr_mw;             // workgroups of k_rr_mw (one wave each, at most 64)
+    // round robin by fixpoint (nullptr = off; k_rr_mw then decides every iteration,
     // otherwise only those whose fixpoint failed)
     RRFpCtl* fp_ctl;
     uint8_t* fp_in;             // per scan entry: bit 0 picked by the last pass, bit 1 by the one before
@@ -267,23 +247,9 @@ hipError_t launch_round(const ClauseView& cv, const LoopBuffers& b, uint32_t r, 
                         uint32_t wave_from, hipStream_t s);
 hipError_t launch_round0_buckets(const ClauseView& cv, const LoopBuffers& b, bool last, bool fused_reduce,
                                  bool scattered, hipStream_t s);
-// Dependency-driven LFMIS: k_bscatter (unless `scattered`), k_bsort (+ the loop's reduce in
-// workgroup 0 when `fused_reduce`), k_decide.  Replaces round 0 .. tail.
-hipError_t launch_lfmis_dd(const ClauseView& cv, const LoopBuffers& b, bool scattered, bool fused_reduce,
-                           hipStream_t s);
-// LDS bytes of k_bsort / k_decide for these buffers (the host checks them against the CU's LDS)
-size_t dd_sort_lds(const LoopBuffers& b);
-size_t dd_sort_general_lds(const LoopBuffers& b);
-size_t dd_decide_lds(const LoopBuffers& b, uint32_t k);
-hipError_t launch_join_claim(const ClauseView& cv, const LoopBuffers& b, uint32_t r, const uint32_t* in, uint32_t* out,
-                             hipStream_t s);
-hipError_t launch_join_only(const ClauseView& cv, const LoopBuffers& b, uint32_t r, bool last, uint32_t wave_from,
-                            const uint32_t* in, uint32_t* out, hipStream_t s);
-hipError_t launch_claim_only(const ClauseView& cv, const LoopBuffers& b, uint32_t r, uint32_t wave_from,
-                             const uint32_t* in, uint32_t* out, hipStream_t s);
 hipError_t launch_tail(const ClauseView& cv, const LoopBuffers& b, uint32_t first_round,
                        hipStream_t s);
-// round robin: k_rr_entries, the fixpoint passes (when b.fp_ctl), then k_rr_mw / k_rr_mis for
+// round robin: k_rr_entries, the fixpoint passes (when b.fp_ctl), then k_rr_mw for
 // iterations the fixpoint did not settle
 hipError_t launch_rr_mis(const ClauseView& cv, const LoopBuffers& b, hipStream_t s);
 hipError_t launch_resample(const ClauseView& cv, const LoopBuffers& b, uint32_t tile_begin,

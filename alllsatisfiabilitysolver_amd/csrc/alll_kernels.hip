@@ -99,11 +99,6 @@ __device__ __forceinline__ unsigned long long* time_slot(const LoopBuffers& b, u
 __device__ __forceinline__ unsigned long long wall_now() {
     return (unsigned long long)__builtin_amdgcn_s_memrealtime();
 }
-// diagnostics: phase stamp of this workgroup (thread 0) in kernel region `kr`
-__device__ __forceinline__ void dbg_stamp(const LoopBuffers& b, uint32_t kr, uint32_t phase) {
-    if (b.kdbg && threadIdx.x == 0 && blockIdx.x < DBG_BLOCKS)
-        b.kdbg[((uint64_t)kr * DBG_BLOCKS + blockIdx.x) * DBG_FIELDS + phase] = wall_now();
-}
 // one stamp per workgroup (thread 0); only loop evaluations (gated) are timed
 __device__ __forceinline__ void stamp_eval_begin(const LoopBuffers& b, int gated) {
     if (gated && b.ktime && threadIdx.x == 0) atomicMin(time_slot(b, b.state->n_iter), wall_now());
@@ -969,13 +964,6 @@ struct HotTable {
     }
 };
 
-// One owner array for every epoch when JOIN(r) and CLAIM(r+1) are separated by a kernel
-// boundary (or, in the tail, a workgroup barrier): keys of later epochs are always smaller.
-// With the fused JOIN(r)+CLAIM(r+1) rounds (k_wjc) odd epochs use a second array, so that
-// round r's keys stay readable while round r+1 claims.
-__device__ __forceinline__ unsigned long long* owner_of(const LoopBuffers& b, uint32_t epoch) {
-    return b.owner + ((epoch & 1u) ? b.owner_alt : 0ull);
-}
 
 template <int K>
 __device__ __forceinline__ void claim_all(const ClauseView& cv, const LoopBuffers& b, const Ent<K>& e, uint64_t lb,
@@ -1014,7 +1002,7 @@ __global__ __launch_bounds__(ROUND_THREADS) void k_claim(ClauseView cv, LoopBuff
     if (threadIdx.x == 0) s_keep = 0;
     __syncthreads();
     const unsigned long long keyhi = (unsigned long long)(~(rbase + r)) << 32;
-    unsigned long long* owner = owner_of(b, rbase + r);
+    unsigned long long* owner = b.owner;
     uint32_t* lout = out + (uint64_t)tile * TILE * S;
     for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
         Ent<K> e;
@@ -1118,7 +1106,7 @@ __global__ __launch_bounds__(JOIN_THREADS) void k_join(ClauseView cv, LoopBuffer
     spec_fence();
     if (!active || cnt == 0) return;
     const unsigned long long keyhi = (unsigned long long)(~(rbase + r)) << 32;
-    const unsigned long long* owner = owner_of(b, rbase + r);
+    const unsigned long long* owner = b.owner;
     join_tile<K>(cv, b, tile, cnt, in, out, last, stamp, mis0, e0,
                  [&](const Ent<K>& e, uint32_t, uint64_t lb, uint32_t len) {
                      bool own = true;
@@ -1171,7 +1159,7 @@ __global__ __launch_bounds__(ROUND_THREADS) void k_wclaim(ClauseView cv, LoopBuf
     if (cnt == 0 && !hot) return;
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     const unsigned long long keyhi = (unsigned long long)(~(rbase + r)) << 32;
-    unsigned long long* owner = owner_of(b, rbase + r);
+    unsigned long long* owner = b.owner;
     uint32_t* lout = out + (uint64_t)tile * TILE * S;
     uint32_t kept = 0;
     for (uint32_t i0 = 0; i0 < cnt; i0 += 64) {
@@ -1229,7 +1217,7 @@ __global__ __launch_bounds__(ROUND_THREADS) void k_wjoin(ClauseView cv, LoopBuff
     if (cnt == 0) return;
     const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
     const unsigned long long keyhi = (unsigned long long)(~(rbase + r)) << 32;
-    const unsigned long long* owner = owner_of(b, rbase + r);
+    const unsigned long long* owner = b.owner;
     uint32_t* lout = out + (uint64_t)tile * TILE * S;
     const uint32_t m0 = __builtin_amdgcn_readfirstlane(mc0);
     uint32_t* mis = b.mis + (uint64_t)tile * TILE + m0;
@@ -1280,126 +1268,6 @@ __global__ __launch_bounds__(ROUND_THREADS) void k_wjoin(ClauseView cv, LoopBuff
             b.tile_stats[2 * tile] += w;
             b.tile_stats[2 * tile + 1] += lits;
         }
-    }
-}
-
-// JOIN(r) and CLAIM(r+1) in one launch (fixed k, clause-order keys, two owner arrays), a wave
-// per tile.  A clause that holds all its variables joins, as in k_wjoin.  A clause that lost a
-// variable v cannot wait for a boundary to learn whether it was killed in round r, so it
-// decides that itself: the only round-r joiner that can cover one of its variables is that
-// variable's round-r owner d (a joiner held every variable it covers, and the clause claimed v
-// too), and d joined iff it holds all of its own variables -- d's literals (AoS, clause order)
-// and their owner keys, read from round r's array while the survivors' round r+1 claims go to
-// the other one.  Joins of earlier rounds were excluded by the kill tests before round r.
-// Decisions equal JOIN(r) + CLAIM(r+1); one launch and one boundary fewer per round.
-template <int K>
-__global__ __launch_bounds__(ROUND_THREADS) void k_wjc(ClauseView cv, LoopBuffers b, uint32_t r,
-                                                       const uint32_t* in, uint32_t* out) {
-    DevState* st = b.state;
-    constexpr int S = Ent<K>::S;
-    const uint32_t tile = wave_tile();
-    const int lane = threadIdx.x & 63;
-    const bool tv = tile < b.n_tiles;
-    const uint32_t* lin = in + (uint64_t)(tv ? tile : 0u) * TILE * S;
-    // loop state, counts and the first 64 entries (speculatively) in one round trip (k_wclaim)
-    Ent<K> e0;
-    load_ent<K>(e0, lin + (uint64_t)lane * S);
-    const uint32_t cnt0 = b.tile_cnt[tv ? tile : 0u], mc0 = b.mis_cnt[tv ? tile : 0u];
-    const uint32_t active = st->active, stamp = st->stamp, rbase = st->round_base;
-    spec_fence();
-    if (!active) return;
-    const bool hot = cv.n_hot != 0;
-    __shared__ uint32_t s_hk[HOT_SLOTS];
-    __shared__ unsigned long long s_hv[HOT_SLOTS];
-    HotTable ht{s_hk, s_hv};
-    if (hot) {
-        ht.init();
-        __syncthreads();
-    }
-    const uint32_t cnt = tv ? __builtin_amdgcn_readfirstlane(cnt0) : 0u;
-    if (cnt == 0 && !hot) return;
-    const uint64_t lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-    const unsigned long long keyr = (unsigned long long)(~(rbase + r)) << 32;
-    const unsigned long long keyn = (unsigned long long)(~(rbase + r + 1)) << 32;
-    const unsigned long long* own_r = owner_of(b, rbase + r);
-    unsigned long long* own_n = owner_of(b, rbase + r + 1);
-    uint32_t* lout = out + (uint64_t)(tv ? tile : 0u) * TILE * S;
-    const uint32_t m0 = __builtin_amdgcn_readfirstlane(mc0);
-    uint32_t* mis = b.mis + (uint64_t)(tv ? tile : 0u) * TILE + m0;
-    uint32_t kept = 0, joined = 0;
-    unsigned long long lits = 0, w = 0;
-    for (uint32_t i0 = 0; i0 < cnt; i0 += 64) {
-        const uint32_t i = i0 + lane;
-        Ent<K> e;
-        bool join = false, keep = false;
-        if (i < cnt) {
-            if (i0 == 0) e = e0;
-            else load_ent<K>(e, lin + (uint64_t)i * S);
-            const unsigned long long mine = keyr | e.w[0];
-            unsigned long long o[K];
-#pragma unroll
-            for (int j = 0; j < K; ++j) o[j] = own_r[vmix(b, lit_var(e.w[1 + j]))];
-            join = true;
-#pragma unroll
-            for (int j = 0; j < K; ++j) join &= o[j] == mine;
-            if (join) {
-#pragma unroll
-                for (int j = 0; j < K; ++j) b.cover[lit_var(e.w[1 + j])] = (uint8_t)stamp;
-                lits += K;
-                w += 1;
-            } else {
-                // the owners of the lost variables: did one of them join in round r?
-                uint32_t dl[K][K];
-#pragma unroll
-                for (int j = 0; j < K; ++j) {
-                    const bool lost = o[j] != mine;
-#pragma unroll
-                    for (int q = 0; q < K; ++q)
-                        dl[j][q] = lost ? cv.lits[(uint64_t)(uint32_t)o[j] * K + q] : 0u;
-                }
-                bool killed = false;
-#pragma unroll
-                for (int j = 0; j < K; ++j) {
-                    if (o[j] == mine) continue;
-                    bool dj = true;
-#pragma unroll
-                    for (int q = 0; q < K; ++q) dj &= own_r[vmix(b, lit_var(dl[j][q]))] == o[j];
-                    killed |= dj;
-                }
-                if (!killed) {
-                    const unsigned long long kn = keyn | e.w[0];
-#pragma unroll
-                    for (int j = 0; j < K; ++j) {
-                        const uint32_t raw = e.w[1 + j];
-                        if (hot && (raw & LIT_HOT)) ht.claim(lit_var(raw), kn);
-                        else __hip_atomic_fetch_min(&own_n[vmix(b, lit_var(raw))], kn, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT);
-                    }
-                    keep = true;
-                }
-            }
-        }
-        const uint64_t jm = __ballot(join), km = __ballot(keep);
-        if (join) mis[joined + __popcll(jm & lt)] = e.w[0];
-        if (keep) store_ent<K>(lout + (uint64_t)(kept + __popcll(km & lt)) * S, e);
-        joined += (uint32_t)__popcll(jm);
-        kept += (uint32_t)__popcll(km);
-    }
-    for (int o = 32; o > 0; o >>= 1) {
-        lits += __shfl_down(lits, o, 64);
-        w += __shfl_down(w, o, 64);
-    }
-    if (lane == 0 && cnt) {
-        b.tile_cnt[tile] = kept;
-        b.mis_cnt[tile] = m0 + joined;
-        if (joined) {  // (the wave owns the tile: no other writer in this kernel)
-            b.tile_stats[2 * tile] += w;
-            b.tile_stats[2 * tile + 1] += lits;
-        }
-    }
-    if (hot) {
-        __syncthreads();
-        ht.flush(own_n, b);
     }
 }
 
@@ -1497,9 +1365,7 @@ __device__ void scatter_run(const ClauseView& cv, const LoopBuffers& b, uint32_t
     if (hot) ht.init();
     const uint32_t nb = b.n_bkt;
     for (uint32_t i = threadIdx.x; i < nb; i += blockDim.x) s_hist[i] = 0;
-    dbg_stamp(b, 0, 0);
     const uint32_t E = run_prefix(b, t0, nt, s_tc, s_pre);
-    dbg_stamp(b, 0, 1);
     const bool single = E <= blockDim.x * U;
     const unsigned long long keyhi = (unsigned long long)(~epoch) << 32;
     Ent<K> e[U];
@@ -1561,10 +1427,8 @@ __device__ void scatter_run(const ClauseView& cv, const LoopBuffers& b, uint32_t
             }
         }
     }
-    dbg_stamp(b, 0, 2);
     __syncthreads();
-    dbg_stamp(b, 0, 3);
-    if (hot) ht.flush(owner_of(b, epoch), b);
+    if (hot) ht.flush(b.owner, b);
     // exclusive scan of the histogram: run-local start of every bucket
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t per = (nb + blockDim.x - 1) / blockDim.x;
@@ -1592,7 +1456,6 @@ __device__ void scatter_run(const ClauseView& cv, const LoopBuffers& b, uint32_t
     }
     if (threadIdx.x == 0) b.run_pairs[r] = total;
     __syncthreads();
-    dbg_stamp(b, 0, 4);
     // pass 2: pairs grouped by bucket, staged in LDS when they fit so that the run's area is
     // written with whole-line stores
     unsigned long long* gpr = b.pairs + (uint64_t)r * b.run_tiles * TILE * K;
@@ -1624,12 +1487,10 @@ __device__ void scatter_run(const ClauseView& cv, const LoopBuffers& b, uint32_t
             emit();
         }
     }
-    dbg_stamp(b, 0, 5);
     if (staged) {
         __syncthreads();
         for (uint32_t i = threadIdx.x; i < total; i += blockDim.x) gpr[i] = s_pairs[i];
     }
-    dbg_stamp(b, 0, 6);
 }
 
 template <int K>
@@ -1776,7 +1637,6 @@ __device__ void resolve_bucket(const LoopBuffers& b, uint32_t run_cap) {
     __shared__ uint16_t s_seg[T * U];  // item -> segment of the current sweep
     const uint32_t bv = b.bkt_width;
     ResolveLds L{s_min, s_start, s_pre, s_wsum};
-    dbg_stamp(b, 1, 0);
     for (uint32_t i = threadIdx.x; i < bv; i += blockDim.x) L.min[i] = ~0u;
     // items of a wave: f0 + 64 u, f0 = wave * 64 U + lane (+ stride per sweep)
     const uint32_t first = (threadIdx.x >> 6) * 64 * U + (threadIdx.x & 63);
@@ -1785,7 +1645,6 @@ __device__ void resolve_bucket(const LoopBuffers& b, uint32_t run_cap) {
     unsigned long long x[U];
     if (b.n_runs <= BKT_RUN_BATCH) {
         const uint32_t np = resolve_batch(b, L, 0, b.n_runs);  // (its barriers also publish L.min)
-        dbg_stamp(b, 1, 1);
         if (np <= stride) {
             if (np > 0) {
                 // item -> segment table (one LDS read per item instead of a binary search)
@@ -1803,15 +1662,12 @@ __device__ void resolve_bucket(const LoopBuffers& b, uint32_t run_cap) {
                 for (int u = 0; u < U; ++u)  // (clamped duplicates of the last pair would serialise)
                     if (first + 64 * u < np) atomicMin(&L.min[(uint32_t)x[u] & 0x7FFFu], (uint32_t)(x[u] >> 32));
             }
-            dbg_stamp(b, 1, 2);
             __syncthreads();
-            dbg_stamp(b, 1, 3);
             if (np > 0) {
 #pragma unroll
                 for (int u = 0; u < U; ++u)
                     if (first + 64 * u < np) b.pairs[pos[u]] = resolve_mark(L, x[u]);
             }
-            dbg_stamp(b, 1, 4);
             return;
         }
     }
@@ -1843,7 +1699,6 @@ __device__ void resolve_bucket(const LoopBuffers& b, uint32_t run_cap) {
             // last barrier orders it)
         }
     }
-    dbg_stamp(b, 1, 4);
 }
 
 // Workgroup per run: lose marks -> LDS byte per entry; then every entry of the run's tiles in
@@ -1875,9 +1730,7 @@ __global__ __launch_bounds__(BJN_THREADS) void k_bjoin(ClauseView cv, LoopBuffer
         s_lits[threadIdx.x] = 0;
         s_mis0[threadIdx.x] = b.mis_cnt[t0 + threadIdx.x];
     }
-    dbg_stamp(b, 2, 0);
     const uint32_t E = run_prefix(b, t0, nt, s_tc, s_pre);
-    dbg_stamp(b, 2, 1);
     const bool single = E <= blockDim.x * U;
     Ent<K> e[U];
     bool ok[U];
@@ -1897,12 +1750,10 @@ __global__ __launch_bounds__(BJN_THREADS) void k_bjoin(ClauseView cv, LoopBuffer
         for (int u = 0; u < PU; ++u)
             if (x[u] & PAIR_LOSE) lost[(x[u] >> 15) & 0xFFFFu] = 1;
     }
-    dbg_stamp(b, 2, 2);
     __syncthreads();
-    dbg_stamp(b, 2, 3);
     const bool hot = cv.n_hot != 0;
     const unsigned long long keyhi = (unsigned long long)(~rbase) << 32;
-    const unsigned long long* owner = owner_of(b, rbase);
+    const unsigned long long* owner = b.owner;
     auto decide = [&]() {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
@@ -1934,7 +1785,6 @@ __global__ __launch_bounds__(BJN_THREADS) void k_bjoin(ClauseView cv, LoopBuffer
             decide();
         }
     }
-    dbg_stamp(b, 2, 4);
     __syncthreads();
     if (threadIdx.x < nt) {
         const uint32_t tt = threadIdx.x, tile = t0 + tt, kept = s_keep[tt];
@@ -1956,658 +1806,6 @@ __global__ __launch_bounds__(BJN_THREADS) void k_bjoin(ClauseView cv, LoopBuffer
             for (uint32_t i = threadIdx.x; i < kept * S; i += blockDim.x) dst[i] = src[i];
         }
     }
-    dbg_stamp(b, 2, 5);
-}
-
-// ------------------------------------------------------------------------------------
-// Dependency-driven LFMIS (one GPU, fixed width, no hot variables).  After the
-// bucket scatter every violated clause c has one pair per literal {c, its entry in the run, its
-// variable's offset in the bucket}.  For a variable v let c_1 < c_2 < ... be the violated
-// clauses that contain it.  c is in the LFMIS iff no lower clause sharing a variable with it is,
-// and "some c_j < c_i on v is in" = (c_{i-1} is in) or (some c_j < c_{i-1} on v is in).  So every
-// pair passes one bit, "covered below", to the next pair of its variable: an IN clause sends 1 on
-// every pair, an OUT clause forwards what its pair received (0 when it has no predecessor).  A
-// clause that receives a 1 is OUT; one that received 0 on every pair with a predecessor is IN.
-// Every message travels from a lower clause to a higher one, so the lowest undecided clause can
-// always decide: the exchange ends with exactly the LFMIS of SATInstance.h:391-451, without
-// grid rounds (the same decisions as CLAIM/JOIN, in ~12 message hops instead of ~12 launches).
-//
-// k_bsort (workgroup per bucket): the bucket's pairs of every run are counted per variable,
-// placed by variable in LDS, and each pair scans its variable's short segment for its
-// predecessor and successor in clause order; it is written back in place as
-//   {successor pair position:32 (~0: none) | has predecessor:1 | entry in run:16 | inert:1}.
-// A clause holding a variable twice keeps its first pair (lowest position) and marks the other
-// inert.  Variables are handled DDS_SUBW at a time (LDS counters) in pieces whose pairs fit
-// DDS_CAP (the host admits only instances whose variables fit one piece).
-constexpr uint32_t DD_NONE = 0xFFFFFFFFu;
-constexpr uint32_t DD_PRED = 1u << 31;
-constexpr uint32_t DD_INERT = 1u;
-constexpr uint32_t DD_EL_MASK = 0xFFFFu << 15;
-
-// k_bsort (fast kernel): one sweep of at most DDS_THREADS * DDS_UNROLL pairs and a bucket of at
-// most DDS_FAST_W variables: 16-bit per-variable counts turned into their prefix in place, the
-// placed pairs as {clause} + {item index}, and one 16-bit result per item.  Other buckets (more
-// pairs than one sweep: the first iterations of large instances) are left to k_bsort_general
-// (sub-ranges of DDS_SUBW variables, pieces of DDS_CAP pairs, several sweeps).
-constexpr uint32_t DDS_FAST_W = 10240;
-constexpr uint32_t DDS_RES_NONE = 0x3FFFu, DDS_RES_PRED = 1u << 14, DDS_RES_INERT = 1u << 15;
-static_assert(DDS_THREADS * DDS_UNROLL < DDS_RES_NONE, "item indices fit the 14-bit successor field");
-
-struct DdSortLds {
-    uint32_t* start;             // n_runs: segment starts of this bucket
-    uint32_t* pre;               // n_runs + 1: prefix of the segment lengths
-    uint32_t* wsum;              // threads / 64
-    uint16_t* seg;               // threads * unroll: item -> run segment of the current sweep
-    uint16_t* vst16;             // fast: DDS_FAST_W + 1 per-variable counts -> exclusive prefix
-    uint32_t* cl;                // fast: placed pairs' clauses
-    uint16_t* fi;                // fast: placed pairs' item indices
-    uint16_t* res;               // fast: per item {successor item:14 | has predecessor:1 | inert:1}
-    uint16_t* mlist;             // fast: variables with several claimants (at most items / 2)
-    unsigned long long* sorted;  // general: DDS_CAP {clause:32 | pair position:32}
-    uint32_t* cnt;               // general: DDS_SUBW counts, then cursors
-    uint32_t* vst;               // general: DDS_SUBW + 1 exclusive prefix
-};
-
-constexpr size_t dd_align16(size_t x) { return (x + 15) & ~(size_t)15; }
-inline __host__ __device__ size_t dd_sort_common(uint32_t n_runs) {
-    return dd_align16(8ull * (n_runs + 4) + 4ull * (DDS_THREADS / 64) + 2ull * DDS_THREADS * DDS_UNROLL);
-}
-constexpr size_t DD_SORT_FAST = dd_align16(2ull * (DDS_FAST_W + 8)) + 4ull * DDS_THREADS * DDS_UNROLL +
-                                2ull * DDS_THREADS * DDS_UNROLL + 2ull * DDS_THREADS * DDS_UNROLL +
-                                1ull * DDS_THREADS * DDS_UNROLL;
-constexpr size_t DD_SORT_GENERAL = 8ull * DDS_CAP + 4ull * DDS_SUBW + 4ull * (DDS_SUBW + 4);
-
-size_t dd_sort_lds(const LoopBuffers& b) { return dd_sort_common(b.n_runs) + DD_SORT_FAST; }
-size_t dd_sort_general_lds(const LoopBuffers& b) { return dd_sort_common(b.n_runs) + DD_SORT_GENERAL; }
-
-__device__ __forceinline__ DdSortLds dd_carve(void* base, uint32_t n_runs, int T) {
-    DdSortLds L;
-    char* p = static_cast<char*>(base);
-    L.start = reinterpret_cast<uint32_t*>(p); p += 4ull * (n_runs + 4);
-    L.pre = reinterpret_cast<uint32_t*>(p); p += 4ull * (n_runs + 4);
-    L.wsum = reinterpret_cast<uint32_t*>(p); p += 4ull * (T / 64);
-    L.seg = reinterpret_cast<uint16_t*>(p);
-    p = static_cast<char*>(base) + dd_sort_common(n_runs);
-    char* u = p;  // the fast and the general layouts share the rest
-    L.vst16 = reinterpret_cast<uint16_t*>(u); u += dd_align16(2ull * (DDS_FAST_W + 8));
-    L.cl = reinterpret_cast<uint32_t*>(u); u += 4ull * DDS_THREADS * DDS_UNROLL;
-    L.fi = reinterpret_cast<uint16_t*>(u); u += 2ull * DDS_THREADS * DDS_UNROLL;
-    L.res = reinterpret_cast<uint16_t*>(u); u += 2ull * DDS_THREADS * DDS_UNROLL;
-    L.mlist = reinterpret_cast<uint16_t*>(u);
-    L.sorted = reinterpret_cast<unsigned long long*>(p); p += 8ull * DDS_CAP;
-    L.cnt = reinterpret_cast<uint32_t*>(p); p += 4ull * DDS_SUBW;
-    L.vst = reinterpret_cast<uint32_t*>(p);
-    return L;
-}
-
-// Exclusive prefix of a[0, n) into o[0, n] (o[n] = total; a == o allowed), whole workgroup.
-template <typename TA>
-__device__ uint32_t block_excl_scan(const TA* a, TA* o, uint32_t n, uint32_t* wsum) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const uint32_t per = (n + blockDim.x - 1) / blockDim.x;
-    const uint32_t q0 = min(n, threadIdx.x * per), q1 = min(n, q0 + per);
-    uint32_t sum = 0;
-    for (uint32_t q = q0; q < q1; ++q) sum += a[q];
-    uint32_t incl = sum;
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(incl, d, 64);
-        if (lane >= d) incl += y;
-    }
-    if (lane == 63) wsum[wave] = incl;
-    __syncthreads();
-    uint32_t run = incl - sum, total = 0;
-    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
-        if (w < wave) run += wsum[w];
-        total += wsum[w];
-    }
-    for (uint32_t q = q0; q < q1; ++q) {
-        const uint32_t c = a[q];
-        o[q] = (TA)run;
-        run += c;
-    }
-    if (threadIdx.x == 0) o[n] = (TA)total;
-    __syncthreads();
-    return total;
-}
-
-// 16-bit LDS counter i (two per word; counts stay below 2^16): returns its old value
-__device__ __forceinline__ uint32_t lds_inc16(uint16_t* a, uint32_t i) {
-    uint32_t* w = reinterpret_cast<uint32_t*>(a) + (i >> 1);
-    const uint32_t sh = 16 * (i & 1);
-    return (atomicAdd(w, 1u << sh) >> sh) & 0xFFFFu;
-}
-
-__device__ __forceinline__ bool dd_fast_bucket(uint32_t np, uint32_t width) {
-    return np <= (uint32_t)(DDS_THREADS * DDS_UNROLL) && width <= DDS_FAST_W;
-}
-
-template <int U, int T>
-__global__ __launch_bounds__(T) void k_bsort(LoopBuffers b, uint32_t run_cap, int fused_reduce) {
-    extern __shared__ __attribute__((aligned(16))) unsigned long long s_dds[];
-    const DdSortLds L = dd_carve(s_dds, b.n_runs, T);
-    const ResolveLds R{nullptr, L.start, L.pre, L.wsum};
-    const uint32_t nr = b.n_runs;  // <= BKT_RUN_BATCH (checked at create)
-    dbg_stamp(b, 1, 0);
-    const uint32_t np = resolve_batch(b, R, 0, nr);
-    dbg_stamp(b, 1, 1);
-    const uint32_t width = b.bkt_width;
-    if (np && dd_fast_bucket(np, width)) {  // (uniform; the others: k_bsort_general)
-        const uint32_t first = (threadIdx.x >> 6) * 64 * U + (threadIdx.x & 63);
-        resolve_seg_table(R, nr, np, 0, T * U, L.seg);
-        uint32_t* v32 = reinterpret_cast<uint32_t*>(L.vst16);
-        for (uint32_t i = threadIdx.x; i < (width + 2) / 2; i += T) v32[i] = 0;
-        __syncthreads();
-        auto pos_of = [&](uint32_t f) {
-            const uint32_t q = L.seg[f];
-            return q * run_cap + L.start[q] + (f - L.pre[q]);
-        };
-        unsigned long long x[U];
-        uint32_t pos[U], rk[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) pos[u] = pos_of(min(first + 64 * u, np - 1));
-#pragma unroll
-        for (int u = 0; u < U; ++u) x[u] = b.pairs[pos[u]];
-        dbg_stamp(b, 1, 2);
-        // per-variable counts (the atomics' results rank the pairs of a variable)
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (first + 64 * u < np) rk[u] = lds_inc16(L.vst16, (uint32_t)x[u] & 0x7FFFu);
-        __syncthreads();
-        dbg_stamp(b, 1, 4);
-        block_excl_scan<uint16_t>(L.vst16, L.vst16, width, L.wsum);
-        dbg_stamp(b, 1, 5);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (first + 64 * u >= np) continue;
-            const uint32_t slot = L.vst16[(uint32_t)x[u] & 0x7FFFu] + rk[u];
-            L.cl[slot] = (uint32_t)(x[u] >> 32);
-            L.fi[slot] = (uint16_t)(first + 64 * u);
-        }
-        __syncthreads();
-        dbg_stamp(b, 1, 6);
-        // Links of each variable's (short) segment: for each pair, whether a lower clause holds
-        // the variable, whether it is its clause's first pair on the variable, and the first pair
-        // of the next clause.  One claimant: nothing to link.  Several (a quarter of the variables
-        // at 3-SAT ratio 4): listed first, so that each sorting pass runs on full waves.
-        __shared__ uint32_t s_nmulti;
-        if (threadIdx.x == 0) s_nmulti = 0;
-        __syncthreads();
-        for (uint32_t v = threadIdx.x; v < width; v += T) {
-            const uint32_t sa = L.vst16[v], se = L.vst16[v + 1];
-            if (se == sa + 1) L.res[L.fi[sa]] = (uint16_t)DDS_RES_NONE;
-            const bool multi = se > sa + 1;
-            const uint64_t bm = __builtin_amdgcn_ballot_w64(multi);
-            if (!bm) continue;
-            const uint32_t lead = (uint32_t)__builtin_ctzll(bm);
-            uint32_t base = 0;
-            if ((threadIdx.x & 63) == lead) base = atomicAdd(&s_nmulti, (uint32_t)__popcll(bm));
-            base = __shfl(base, lead, 64);
-            if (multi) L.mlist[base + (uint32_t)__popcll(bm & ((1ull << (threadIdx.x & 63)) - 1ull))] = (uint16_t)v;
-        }
-        __syncthreads();
-        const uint32_t nm = s_nmulti;
-        for (uint32_t idx = threadIdx.x; idx < nm; idx += T) {
-            const uint32_t v = L.mlist[idx];
-            const uint32_t sa = L.vst16[v], se = L.vst16[v + 1], n = se - sa;
-            if (n <= 4) {
-                // sort up to four {clause:32 | item:16} keys (a 5-exchange network; missing ones
-                // are ~0 and sort last), then read the links off the neighbours
-                unsigned long long k4[4];
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-                    k4[q] = (uint32_t)q < n ? ((unsigned long long)L.cl[sa + q] << 16) | L.fi[sa + q] : ~0ull;
-                auto cx = [](unsigned long long& a, unsigned long long& c) {
-                    const unsigned long long lo = a < c ? a : c, hi = a < c ? c : a;
-                    a = lo;
-                    c = hi;
-                };
-                cx(k4[0], k4[1]); cx(k4[2], k4[3]); cx(k4[0], k4[2]); cx(k4[1], k4[3]); cx(k4[1], k4[2]);
-                const uint64_t c0 = k4[0] >> 16;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    if ((uint32_t)i >= n) continue;
-                    const uint64_t ci = k4[i] >> 16;
-                    const bool rep = i == 0 || (k4[i - 1] >> 16) != ci;
-                    uint32_t sf = DDS_RES_NONE;
-#pragma unroll
-                    for (int j = 3; j > i; --j)
-                        if ((uint32_t)j < n && (k4[j] >> 16) != ci && (j == i + 1 || (k4[j - 1] >> 16) == ci)) sf = (uint32_t)k4[j] & 0xFFFFu;
-                    L.res[(uint32_t)k4[i] & 0xFFFFu] = (uint16_t)(!rep ? (DDS_RES_INERT | DDS_RES_NONE)
-                                                                       : ((c0 < ci ? DDS_RES_PRED : 0u) | sf));
-                }
-            } else {
-                for (uint32_t i = sa; i < se; ++i) {  // (rare: five or more claimants)
-                    const uint32_t ci = L.cl[i], fi = L.fi[i];
-                    bool rep = true, pred = false;
-                    uint32_t sc = ~0u, sf = DDS_RES_NONE;
-                    for (uint32_t j = sa; j < se; ++j) {
-                        const uint32_t cj = L.cl[j], fj = L.fi[j];
-                        if (cj < ci) pred = true;
-                        else if (cj == ci) rep = rep && !(fj < fi);
-                        else if (cj < sc || (cj == sc && fj < sf)) { sc = cj; sf = fj; }
-                    }
-                    L.res[fi] = (uint16_t)(!rep ? (DDS_RES_INERT | DDS_RES_NONE) : ((pred ? DDS_RES_PRED : 0u) | sf));
-                }
-            }
-        }
-        __syncthreads();
-        dbg_stamp(b, 1, 7);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            if (first + 64 * u >= np) continue;
-            const uint32_t rs = L.res[first + 64 * u], sf = rs & DDS_RES_NONE;
-            uint32_t lw = (uint32_t)x[u] & DD_EL_MASK;
-            if (rs & DDS_RES_INERT) lw |= DD_INERT;
-            else if (rs & DDS_RES_PRED) lw |= DD_PRED;
-            const uint32_t sp = (rs & DDS_RES_INERT) || sf == DDS_RES_NONE ? DD_NONE : pos_of(sf);
-            b.pairs[pos_of(first + 64 * u)] = ((unsigned long long)sp << 32) | lw;  // (pos[] recomputed: registers)
-        }
-    }
-    dbg_stamp(b, 1, 3);
-    if (fused_reduce && blockIdx.x == 0) {  // the loop's reduce (one GPU), as in k_bresolve
-        __syncthreads();
-        if (eval_gate_closed(b.state)) {
-            if (threadIdx.x == 0) b.state->active = 0;
-        } else {
-            reduce_body(b, 0);
-        }
-    }
-}
-
-// k_bsort_general: the buckets k_bsort leaves (more pairs than one sweep, or wider than
-// DDS_FAST_W): variables DDS_SUBW at a time, pieces of DDS_CAP pairs, items reloaded per sweep.
-template <int U, int T>
-__global__ __launch_bounds__(T) void k_bsort_general(LoopBuffers b, uint32_t run_cap) {
-    extern __shared__ __attribute__((aligned(16))) unsigned long long s_ddg[];
-    const DdSortLds L = dd_carve(s_ddg, b.n_runs, T);
-    const ResolveLds R{nullptr, L.start, L.pre, L.wsum};
-    const uint32_t nr = b.n_runs;
-    const uint32_t np = resolve_batch(b, R, 0, nr);
-    const uint32_t width = b.bkt_width;
-    if (np == 0 || dd_fast_bucket(np, width)) return;
-    const uint32_t stride = T * U;
-    const uint32_t first = (threadIdx.x >> 6) * 64 * U + (threadIdx.x & 63);
-    unsigned long long x[U];
-    uint32_t pos[U];
-    bool ok[U];
-    auto load_sweep = [&](uint32_t s0) {
-        resolve_seg_table(R, nr, np, s0, stride, L.seg);
-        __syncthreads();
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t f = s0 + first + 64 * u;
-            ok[u] = f < np;
-            const uint32_t ff = min(f, np - 1);
-            const uint32_t q = L.seg[ff - s0];
-            pos[u] = q * run_cap + L.start[q] + (ff - L.pre[q]);
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) x[u] = b.pairs[pos[u]];
-    };
-    auto voff = [&](int u) { return (uint32_t)x[u] & 0x7FFFu; };
-    for (uint32_t v0 = 0; v0 < width; v0 += DDS_SUBW) {
-        const uint32_t sw = min(DDS_SUBW, width - v0);
-        for (uint32_t i = threadIdx.x; i < sw; i += T) L.cnt[i] = 0;
-        __syncthreads();
-        for (uint32_t s0 = 0; s0 < np; s0 += stride) {
-            load_sweep(s0);
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                const uint32_t v = voff(u) - v0;
-                if (ok[u] && v < sw) atomicAdd(&L.cnt[v], 1u);
-            }
-            __syncthreads();  // (the segment table is rewritten by the next sweep)
-        }
-        const uint32_t tot = block_excl_scan<uint32_t>(L.cnt, L.vst, sw, L.wsum);
-        if (tot == 0) continue;  // (uniform)
-        for (uint32_t i = threadIdx.x; i < sw; i += T) L.cnt[i] = 0;
-        __syncthreads();
-        for (uint32_t a = 0; a < sw;) {
-            // piece [a, e): the largest e whose pairs fit DDS_CAP (at least one variable)
-            uint32_t lo = a + 1, hi = sw;
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi + 1) / 2;
-                if (L.vst[mid] - L.vst[a] <= DDS_CAP) lo = mid; else hi = mid - 1;
-            }
-            const uint32_t e = lo, base = L.vst[a];
-            if (L.vst[e] - base > DDS_CAP && threadIdx.x == 0) b.state->error = 2;  // (host-prevented)
-            for (uint32_t s0 = 0; s0 < np; s0 += stride) {
-                load_sweep(s0);
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const uint32_t v = voff(u) - v0;
-                    if (!ok[u] || v < a || v >= e) continue;
-                    const uint32_t slot = L.vst[v] - base + atomicAdd(&L.cnt[v], 1u);
-                    if (slot < DDS_CAP) L.sorted[slot] = (x[u] & 0xFFFFFFFF00000000ull) | pos[u];
-                }
-                __syncthreads();
-            }
-            for (uint32_t s0 = 0; s0 < np; s0 += stride) {
-                load_sweep(s0);
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const uint32_t v = voff(u) - v0;
-                    if (!ok[u] || v < a || v >= e) continue;
-                    const uint32_t c = (uint32_t)(x[u] >> 32);
-                    const uint32_t sa = L.vst[v] - base, se = min(L.vst[v + 1] - base, DDS_CAP);
-                    bool rep = true, pred = false;
-                    uint32_t sc = ~0u, sp = DD_NONE;
-                    for (uint32_t j = sa; j < se; ++j) {
-                        const unsigned long long y = L.sorted[j];
-                        const uint32_t yc = (uint32_t)(y >> 32), yp = (uint32_t)y;
-                        if (yc < c) pred = true;
-                        else if (yc == c) rep = rep && !(yp < pos[u]);
-                        else if (yc < sc || (yc == sc && yp < sp)) { sc = yc; sp = yp; }
-                    }
-                    uint32_t lw = (uint32_t)x[u] & DD_EL_MASK;
-                    if (!rep) { lw |= DD_INERT; sp = DD_NONE; }
-                    else if (pred) lw |= DD_PRED;
-                    b.pairs[pos[u]] = ((unsigned long long)sp << 32) | lw;
-                }
-                __syncthreads();
-            }
-            __syncthreads();  // (the sorted array is rewritten by the next piece)
-            a = e;
-        }
-    }
-}
-
-// k_decide (one persistent workgroup per run, all runs resident: n_runs <= CUs): the run's pairs
-// are read in blocks of DDD_BLK (lane l of a wave holds pairs 64 k + l, k < DDD_PB, of its
-// blocks: blk = wave, wave + 16, ...; the first one stays in registers) and their state is two
-// LDS words per (block, lane): {finished:16 | received:16}, {received bit:16 | has a
-// predecessor:16}.  Entries: one LDS byte per entry slot of the run's tiles: bits 0-3 pairs still
-// waiting for a 0 from their predecessor, bit 4 IN, bit 5 OUT (LDS atomics; every wave sees them
-// at once).
-// After pass 0 every wave runs on its own, without workgroup barriers, until its pairs have
-// finished: per block it loads the message words of the pairs still waiting (relaxed agent-scope
-// loads of words written by relaxed agent-scope stores, i.e. write-through: the tagged
-// single-store granules of MI355X_MICROARCH.md §visibility; tag = n_iter, so nothing is ever
-// reset); a 1 makes the entry OUT, the last 0 makes it IN, and every open pair whose entry is
-// decided forwards its chain state to its successor and finishes.  A wave that found nothing new
-// sleeps briefly.  IN entries are covered and listed once every wave is done (their entries
-// loaded four at a time).  The wait is bounded by DD_TIMEOUT (state.error = 3; the loop stops).
-constexpr int DDD_PB = 12;
-constexpr uint32_t DDD_BLK = 64 * DDD_PB;
-constexpr uint32_t DDD_ALL = (1u << DDD_PB) - 1u;
-
-constexpr uint32_t DDD_RING = 2048;  // send queue of the sender wave (entries {slot:32 | payload:32})
-
-size_t dd_decide_lds(const LoopBuffers& b, uint32_t k) {
-    const size_t slots = (size_t)b.run_tiles * TILE;
-    const size_t cap = slots * k;
-    return slots + 8 * 64 * ((cap + DDD_BLK - 1) / DDD_BLK) + 8 * DDD_RING;
-}
-
-template <int K>
-__global__ __launch_bounds__(DDD_THREADS) void k_decide(ClauseView cv, LoopBuffers b, const uint32_t* in,
-                                                        uint32_t run_cap) {
-    DevState* st = b.state;
-    constexpr int S = Ent<K>::S;
-    constexpr uint32_t IN_BIT = 0x10u, OUT_BIT = 0x20u;
-    const uint32_t r = blockIdx.x;
-    // the loop state with the run's bounds and pair count (one round trip)
-    const uint32_t t0 = b.run_t0[r], nt = b.run_t0[r + 1] - t0;
-    const uint32_t np = b.run_pairs[r];
-    const uint32_t active = st->active, stamp = st->stamp;
-    const uint32_t tag = (uint32_t)st->n_iter & 0x7FFFFFFFu;  // >= 1 here: never the zero fill
-    spec_fence();
-    if (!active) return;
-    extern __shared__ __attribute__((aligned(16))) uint32_t s_dd[];
-    const uint32_t slots = nt * TILE;
-    uint32_t* entw = s_dd;
-    // (entry states are read as whole LDS words: atomic loads, so a spin never reuses a stale
-    // register copy, and the compiler keeps them ds_ operations)
-    auto ent_get = [&](uint32_t el) -> uint32_t {
-        return (__hip_atomic_load(&entw[el >> 2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >> (8 * (el & 3))) & 0xFFu;
-    };
-    uint2* pst = reinterpret_cast<uint2*>(s_dd + (size_t)b.run_tiles * TILE / 4);
-    const uint32_t nblk = (np + DDD_BLK - 1) / DDD_BLK;
-    const size_t cap_blocks = ((size_t)b.run_tiles * TILE * K + DDD_BLK - 1) / DDD_BLK;
-    unsigned long long* ring = reinterpret_cast<unsigned long long*>(pst + cap_blocks * 64);
-    __shared__ uint32_t s_tc[RUN_TILES_MAX], s_pre[RUN_TILES_MAX + 1], s_join[RUN_TILES_MAX], s_mis0[RUN_TILES_MAX];
-    __shared__ unsigned long long s_lits[RUN_TILES_MAX];
-    __shared__ uint32_t s_passes, s_qtail, s_qhead, s_pdone, s_stop;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    constexpr int NW = DDD_THREADS / 64;
-    // With b.dd_senders the last wave only sends: the others queue their messages in LDS, so
-    // that a poll's wait never includes the completion of the write-through stores.
-    const uint32_t senders = b.dd_senders ? 1u : 0u;
-    const uint32_t NWP = NW - senders;  // polling waves
-    const bool is_sender = senders && (uint32_t)wave == NW - 1;
-    for (uint32_t i = threadIdx.x; i < slots / 4; i += DDD_THREADS) entw[i] = 0;
-    if (threadIdx.x < nt) {
-        s_join[threadIdx.x] = 0;
-        s_lits[threadIdx.x] = 0;
-        s_mis0[threadIdx.x] = b.mis_cnt[t0 + threadIdx.x];
-    }
-    if (threadIdx.x == 0) { s_passes = 0; s_qtail = 0; s_qhead = 0; s_pdone = 0; s_stop = 0; }
-    if (senders)
-        for (uint32_t i = threadIdx.x; i < DDD_RING; i += DDD_THREADS) ring[i] = ~0ull;  // (no slot matches)
-    dbg_stamp(b, 2, 0);
-    const uint32_t E = run_prefix(b, t0, nt, s_tc, s_pre);  // (its barriers publish the zeroing above)
-    dbg_stamp(b, 2, 1);
-    const unsigned long long* pr = b.pairs + (uint64_t)r * run_cap;
-    // message words through buffer descriptors (32-bit offsets; aux 16 = sc1: write-through
-    // stores, loads that bypass L1): the whole array for the sends, this run's part for the polls
-    const auto rs_all = __builtin_amdgcn_make_buffer_rsrc(b.dd_msg, (short)0, (int)(b.n_runs * run_cap * 4u), 0x00020000);
-    const auto rs_run = __builtin_amdgcn_make_buffer_rsrc(b.dd_msg + (uint64_t)r * run_cap, (short)0, (int)(run_cap * 4u),
-                                                          0x00020000);
-    // the pairs of a block, DDD_PB loads in flight together (clamped to the run's last pair)
-    auto load_blk = [&](uint32_t blk, unsigned long long (&x)[DDD_PB]) {
-#pragma unroll
-        for (int k = 0; k < DDD_PB; ++k) x[k] = pr[min(blk * DDD_BLK + k * 64 + lane, np - 1)];
-    };
-    unsigned long long xc[DDD_PB];
-    if (!is_sender && (uint32_t)wave < nblk) load_blk(wave, xc);
-    // fn(blk, pairs) over this (polling) wave's blocks: the first from registers, the rest
-    // reloaded (one copy of fn: the block's pairs are copied or loaded into x)
-    auto for_blocks = [&](auto&& fn) {
-        if (is_sender) return;
-        for (uint32_t blk = wave; blk < nblk; blk += NWP) {
-            unsigned long long x[DDD_PB];
-            if (blk == (uint32_t)wave) {
-#pragma unroll
-                for (int k = 0; k < DDD_PB; ++k) x[k] = xc[k];
-            } else {
-                load_blk(blk, x);
-            }
-            fn(blk, x);
-        }
-    };
-    // pass 0: waiting counts; pairs with nothing to receive and nothing to send finish
-    for_blocks([&](uint32_t blk, unsigned long long (&x)[DDD_PB]) {
-        uint32_t fin = 0, pred = 0;
-#pragma unroll
-        for (int k = 0; k < DDD_PB; ++k) {
-            const uint32_t i = blk * DDD_BLK + k * 64 + lane;
-            const uint32_t lw = (uint32_t)x[k], el = (lw >> 15) & 0xFFFFu;
-            if (i >= np || (lw & DD_INERT)) fin |= 1u << k;
-            else if (lw & DD_PRED) { pred |= 1u << k; atomicAdd(&entw[el >> 2], 1u << (8 * (el & 3))); }
-            else if ((uint32_t)(x[k] >> 32) == DD_NONE) fin |= 1u << k;
-        }
-        pst[blk * 64 + lane] = make_uint2(fin, pred << 16);
-    });
-    __syncthreads();
-    // entries without a predecessor on any variable are IN (flat over the run's entries)
-    for (uint32_t f = threadIdx.x; f < E; f += DDD_THREADS) {
-        const uint32_t tt = run_tile_of(s_pre, nt, f);
-        const uint32_t el = tt * TILE + (f - s_pre[tt]);
-        if (ent_get(el) == 0) atomicOr(&entw[el >> 2], IN_BIT << (8 * (el & 3)));
-    }
-    __syncthreads();
-    dbg_stamp(b, 2, 2);
-    // every wave on its own until its pairs have finished
-    const unsigned long long t_begin = wall_now();
-    uint32_t iters = 0;
-    bool stop = false;
-    if (is_sender) {
-        // drain the queue: slot s holds {s, val << 31 | successor position} once written
-        uint32_t head = 0;
-        for (;;) {
-            const uint32_t tail = __hip_atomic_load(&s_qtail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (tail != head) {
-                const uint32_t n = min(64u, tail - head), slot = head + lane;
-                if ((uint32_t)lane < n) {
-                    unsigned long long e;
-                    do {
-                        e = __hip_atomic_load(&ring[slot % DDD_RING], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    } while ((uint32_t)(e >> 32) != slot);
-                    const uint32_t pl = (uint32_t)e;
-                    __builtin_amdgcn_raw_buffer_store_b32((tag << 1) | (pl >> 31), rs_all, (pl & 0x7FFFFFFFu) * 4u, 0, 16);
-                }
-                head += n;
-                if (lane == 0) __hip_atomic_store(&s_qhead, head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                continue;
-            }
-            if (__hip_atomic_load(&s_pdone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == NWP) {
-                if (__hip_atomic_load(&s_qtail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == head) break;
-                continue;
-            }
-            if (__hip_atomic_load(&s_stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
-            __builtin_amdgcn_s_sleep(1);
-        }
-    }
-    // a polling wave's message: queued for the sender wave (one LDS atomic per wave and slot k),
-    // or stored directly
-    auto send = [&](bool go, uint32_t sp, uint32_t val) {
-        if (!senders) {
-            if (go) __builtin_amdgcn_raw_buffer_store_b32((tag << 1) | val, rs_all, sp * 4u, 0, 16);
-            return;
-        }
-        const uint64_t bm = __builtin_amdgcn_ballot_w64(go);
-        if (!bm) return;
-        uint32_t base = 0;
-        const uint32_t lead = (uint32_t)__builtin_ctzll(bm);
-        if ((uint32_t)lane == lead) base = atomicAdd(&s_qtail, (uint32_t)__popcll(bm));
-        base = __shfl(base, lead, 64);
-        if (!go) return;
-        const uint32_t slot = base + (uint32_t)__popcll(bm & ((1ull << lane) - 1ull));
-        while (slot - __hip_atomic_load(&s_qhead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= DDD_RING)
-            __builtin_amdgcn_s_sleep(1);  // (ring full: the sender drains it independently)
-        __hip_atomic_store(&ring[slot % DDD_RING], ((unsigned long long)slot << 32) | (val << 31) | sp,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    };
-    for (;;) {
-        if (is_sender) break;
-        ++iters;
-        bool open_any = false, moved = false;
-        for_blocks([&](uint32_t blk, unsigned long long (&x)[DDD_PB]) {
-            uint2 w = pst[blk * 64 + lane];
-            const uint32_t open = ~w.x & DDD_ALL;
-            if (!__builtin_amdgcn_ballot_w64(open != 0)) return;  // (wave-uniform skip)
-            const uint32_t want = (w.y >> 16) & open & ~(w.x >> 16);
-            uint32_t m[DDD_PB];
-#pragma unroll
-            for (int k = 0; k < DDD_PB; ++k)
-                m[k] = ((want >> k) & 1u) ? __builtin_amdgcn_raw_buffer_load_b32(rs_run, (blk * DDD_BLK + k * 64 + lane) * 4u,
-                                                                                  0, 16)
-                                          : 0u;
-            // receive: a 1 makes the entry OUT, the last 0 makes it IN
-#pragma unroll
-            for (int k = 0; k < DDD_PB; ++k) {
-                if (!((want >> k) & 1u) || (m[k] >> 1) != tag) continue;
-                const uint32_t v = m[k] & 1u;
-                w.x |= 1u << (16 + k);
-                w.y |= v << k;
-                moved = true;
-                const uint32_t el = ((uint32_t)x[k] >> 15) & 0xFFFFu;
-                const uint32_t sh = 8 * (el & 3);
-                if (v) {
-                    atomicOr(&entw[el >> 2], OUT_BIT << sh);
-                } else {
-                    const uint32_t old = atomicSub(&entw[el >> 2], 1u << sh);
-                    if (((old >> sh) & 0xFFu) == 1u) atomicOr(&entw[el >> 2], IN_BIT << sh);  // the last wait: IN
-                }
-            }
-            // forward the chain state of decided entries
-#pragma unroll
-            for (int k = 0; k < DDD_PB; ++k) {
-                if (!((open >> k) & 1u)) continue;
-                const uint32_t lw = (uint32_t)x[k], sp = (uint32_t)(x[k] >> 32), el = (lw >> 15) & 0xFFFFu;
-                const uint32_t es = ent_get(el);
-                const bool recv = (w.x >> (16 + k)) & 1u;
-                uint32_t fin = 0, val = 2;  // val: the bit to send (2: nothing)
-                if (es & IN_BIT) {
-                    fin = 1;
-                    val = 1;
-                } else if (es & OUT_BIT) {
-                    if (!(lw & DD_PRED)) {  // (a pair with neither neighbour finished at pass 0)
-                        fin = 1;
-                        val = 0;
-                    } else if (recv) {
-                        fin = 1;
-                        val = (w.y >> k) & 1u;
-                    }
-                } else if (recv && sp == DD_NONE) {
-                    fin = 1;  // counted; nothing to pass on
-                }
-                send(val != 2 && sp != DD_NONE, sp, val);
-                w.x |= fin << k;
-                moved |= fin != 0;
-            }
-            pst[blk * 64 + lane] = w;
-            open_any |= (~w.x & DDD_ALL) != 0;
-        });
-        if (!__builtin_amdgcn_ballot_w64(open_any)) break;
-        if (lane == 0 && (iters & 15) == 0 && wall_now() - t_begin > DD_TIMEOUT) stop = true;
-        if (__builtin_amdgcn_readfirstlane(stop ? 1u : 0u)) {
-            if (lane == 0) {
-                st->error = 3;
-                st->done = 3;
-                __hip_atomic_store(&s_stop, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-            break;
-        }
-        if (!__builtin_amdgcn_ballot_w64(moved)) __builtin_amdgcn_s_sleep(2);
-    }
-    if (!is_sender && lane == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // (this wave's queue entries first)
-        atomicAdd(&s_pdone, 1u);
-    }
-    if (lane == 0) atomicMax(&s_passes, iters);
-    __syncthreads();
-    dbg_stamp(b, 2, 3);
-    // IN entries: cover their variables (the resample reads cover) and list them in their tile's
-    // MIS; four entries per thread, loaded together
-    for (uint32_t f0 = threadIdx.x * 4; f0 < E; f0 += DDD_THREADS * 4) {
-        uint32_t el[4];
-        bool is_in[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint32_t f = min(f0 + q, E - 1);
-            const uint32_t tt = run_tile_of(s_pre, nt, f);
-            el[q] = tt * TILE + (f - s_pre[tt]);
-            is_in[q] = f0 + q < E && (ent_get(el[q]) & IN_BIT);
-        }
-        if (!(is_in[0] || is_in[1] || is_in[2] || is_in[3])) continue;
-        Ent<K> e[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) load_ent<K>(e[q], in + ((uint64_t)t0 * TILE + el[q]) * S);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            if (!is_in[q]) continue;
-            const uint32_t tt = el[q] / TILE;
-#pragma unroll
-            for (int j = 0; j < K; ++j) b.cover[lit_var(e[q].w[1 + j])] = (uint8_t)stamp;
-            b.mis[(uint64_t)(t0 + tt) * TILE + s_mis0[tt] + atomicAdd(&s_join[tt], 1u)] = e[q].w[0];
-            atomicAdd(&s_lits[tt], (unsigned long long)K);
-        }
-    }
-    __syncthreads();
-    dbg_stamp(b, 2, 4);
-    if (b.kdbg && threadIdx.x == 0 && blockIdx.x < DBG_BLOCKS)  // (wave iterations, not a stamp)
-        b.kdbg[((uint64_t)2 * DBG_BLOCKS + blockIdx.x) * DBG_FIELDS + 7] = s_passes;
-    if (threadIdx.x < nt) {
-        const uint32_t tt = threadIdx.x, tile = t0 + tt;
-        b.tile_cnt[tile] = 0;
-        b.mis_cnt[tile] = s_mis0[tt] + s_join[tt];
-        if (s_join[tt]) {
-            atomicAdd(&b.tile_stats[2 * tile], (unsigned long long)s_join[tt]);
-            atomicAdd(&b.tile_stats[2 * tile + 1], s_lits[tt]);
-        }
-    }
-    if (threadIdx.x == 0 && b.ktime) atomicMax(time_slot(b, st->n_iter - 1) + 3, wall_now());
 }
 
 // Tail: one workgroup finishes the LFMIS over the compact list handed over by the last grid
@@ -2634,7 +1832,7 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail(ClauseView cv, LoopBuffer
     uint32_t* left = b.left;
     while (n > 0) {
         const unsigned long long keyhi = (unsigned long long)(~epoch) << 32;
-        unsigned long long* owner = owner_of(b, epoch);
+        unsigned long long* owner = b.owner;
         // CLAIM (with the kill test)
         if (threadIdx.x == 0) s_wp = 0;
         __syncthreads();
@@ -2812,113 +2010,22 @@ __global__ void k_apply_delta(LoopBuffers b) {
 // into its sorted list, the front is the first clause at or after it with no covered variable,
 // and the sequence of turns is the whole algorithm.
 //
-// One 1024-thread workgroup runs the turns in speculative batches.  B = min(|sets|, groups)
-// consecutive sets get a lane group each; when every live set has a group, each group also
-// runs D levels (its set's next D turns).  Turn l*B + g belongs to group g, level l.  A group
-// scans its list GS clauses per step (the loads of ST steps in flight together) and
-// picks its next fronts greedily, assuming that only its own picks and the covered variables
-// matter: a step whose live candidates share no variable (an LDS hash per step tells) is
-// taken whole, otherwise lane by lane.  Every pick enters the batch hash (variable -> earliest
-// turn, groups).  The batch is exact up to the first turn whose pick shares a variable with
-// a pick of an earlier turn, and up to the first turn a group could not decide; those turns
-// are committed (cover + MIS), and the first undecided turn of an exhausted set is its
-// erasure.  Skipped clauses before a group's first uncommitted pick are erased for certain
-// (covered by committed picks), so no scan is repeated.
-constexpr int RR_THREADS = 1024;
-constexpr uint32_t RR_HBITS = 12;
-constexpr uint32_t RR_HASH = 1u << RR_HBITS;  // batch hash slots (variable -> earliest turn)
-constexpr uint32_t RR_VCAP = RR_HASH / 2;     // variables of the picks of one batch
-constexpr uint32_t RR_CMAX = 2048;            // picks of one batch
-constexpr uint32_t RR_SHASH = 8192;           // step hash slots {variable:32 | lane:32}, split between groups
+// k_rr_mw (the fallback of the fixpoint passes below) runs the turns in speculative batches.
+// B = min(|sets|, groups) consecutive sets get a group (a one-wave workgroup) each; when every
+// live set has a group, each group also runs D levels (its set's next D turns).  Turn l*B + g
+// belongs to group g, level l.  A group scans its list 64 clauses per step (the loads of ST
+// steps in flight together) and picks its next fronts greedily, assuming that only its own
+// picks and the covered variables matter.  The batch is exact up to the first turn whose pick
+// shares a variable with a pick of an earlier turn, and up to the first turn a group could not
+// decide; those turns are committed (cover + MIS), and the first undecided turn of an exhausted
+// set is its erasure.  Skipped clauses before a group's first uncommitted pick are erased for
+// certain (covered by committed picks), so no scan is repeated.
 constexpr uint32_t RR_KE = 8;                 // variables stored in a scan entry (k_rr_entries)
 constexpr uint32_t RR_ROUNDS = 2;             // rounds of ST scan steps (loads issued together) per group per batch
 constexpr uint32_t RR_EMPTY = 0xFFFFFFFFu;
 constexpr unsigned long long RR_EMPTY64 = ~0ull;
 
-struct RRLds {
-    uint32_t hkey[RR_HASH];
-    uint32_t hmin[RR_HASH];
-    unsigned long long skey[RR_SHASH];
-    uint32_t cc[RR_CMAX];      // group g: [g*cpg, g*cpg + ncand[g]) picked clause ids
-    uint32_t cpos[RR_CMAX];    // their positions in U
-    uint32_t ptr[RR_TMAX];     // per set: position in U of the first clause not known erased
-    uint32_t end[RR_TMAX];     // per set: end of its clauses in U
-    uint16_t live[RR_TMAX];    // live sets in the reference's vector order
-    uint32_t ncand[64], scan_end[64], exh[64];
-    uint32_t n_live, t, conf, tm, wide;
-    uint32_t n_steps, n_rounds;  // diagnostics (ALLL_DEBUG_PHASES)
-    unsigned long long gdur_sum, gdur_max, gdur_spread;
-};
-
 __device__ __forceinline__ uint32_t rr_hash(uint32_t v, uint32_t bits) { return (v * 0x9E3779B1u) >> (32 - bits); }
-
-// batch hash: v picked at turn tau.  A slot keeps the earliest turn; every insert that meets
-// another turn in its slot offers the later of the two to L.conf, so that after the scan
-// L.conf = min over slots of the second-earliest turn = the first pick that shares a variable
-// with a pick of an earlier turn (the batch is exact below it).  A clause that repeats a
-// variable meets its own turn, which is no conflict.
-__device__ __forceinline__ void rr_insert(RRLds& L, uint32_t v, uint32_t tau) {
-    uint32_t h = rr_hash(v, RR_HBITS);
-    while (true) {
-        const uint32_t k = atomicCAS(&L.hkey[h], RR_EMPTY, v);
-        if (k == RR_EMPTY || k == v) {
-            const uint32_t old = atomicMin(&L.hmin[h], tau);
-            if (old != RR_EMPTY && old != tau) atomicMin(&L.conf, old > tau ? old : tau);
-            return;
-        }
-        h = (h + 1) & (RR_HASH - 1);
-    }
-}
-
-// did group g pick a clause with variable v in this batch?  The slot's earliest turn is g's
-// (turn = level * B + g).  When another group's earlier turn holds the slot instead, g's own
-// pick of v conflicts with it and every later turn of g lies beyond the batch's exact prefix,
-// so the answer no longer matters.  (g's own inserts precede this lookup in its wave's LDS
-// order, so a slot g filled is never seen without its turn; slots never empty within a batch.)
-__device__ __forceinline__ bool rr_turn_is(uint32_t m, uint32_t B, uint32_t g) {
-    return m != RR_EMPTY && m % B == g;
-}
-
-__device__ __forceinline__ bool rr_own(const RRLds& L, uint32_t v, uint32_t B, uint32_t g) {
-    uint32_t h = rr_hash(v, RR_HBITS);
-    while (true) {
-        const uint32_t k = L.hkey[h];
-        if (k == v) return rr_turn_is(L.hmin[h], B, g);
-        if (k == RR_EMPTY) return false;
-        h = (h + 1) & (RR_HASH - 1);
-    }
-}
-
-// does group g own any of the variables rv[0..n) (n <= KR) in the batch hash?  The probes
-// of the variables run interleaved so that their LDS latencies overlap.
-template <uint32_t KR>
-__device__ __forceinline__ bool rr_own_any(const RRLds& L, const uint32_t (&rv)[KR], uint32_t n, uint32_t B,
-                                           uint32_t g) {
-    uint32_t h[KR];
-    uint32_t act = 0;
-#pragma unroll
-    for (uint32_t j = 0; j < KR; ++j) {
-        h[j] = rr_hash(rv[j], RR_HBITS);
-        if (j < n) act |= 1u << j;
-    }
-    bool own = false;
-    while (act && !own) {
-#pragma unroll
-        for (uint32_t j = 0; j < KR; ++j) {
-            if (!((act >> j) & 1u)) continue;
-            const uint32_t k = L.hkey[h[j]];
-            if (k == rv[j]) {
-                own |= rr_turn_is(L.hmin[h[j]], B, g);
-                act &= ~(1u << j);
-            } else if (k == RR_EMPTY) {
-                act &= ~(1u << j);
-            } else {
-                h[j] = (h[j] + 1) & (RR_HASH - 1);
-            }
-        }
-    }
-    return own;
-}
 
 // step hash of a group (2^sbits slots): lowest lane holding variable v; returns whether v was
 // already present (another lane of the step holds it)
@@ -2978,8 +2085,8 @@ __device__ __forceinline__ uint32_t rr_step_lane(const unsigned long long* sk, u
 
 // Violated clauses of the iteration in clause order as scan entries {id, literal start, width,
 // variables 0..7} (one 256-thread workgroup per tile; tile offsets from the evaluation's
-// per-tile counts), so that a scan round of k_rr_mis is two dependent loads (entry, cover).
-// the fixpoint passes decided this iteration's MIS (k_rr_mw / k_rr_mis then skip it)
+// per-tile counts), so that a scan round of k_rr_mw is two dependent loads (entry, cover).
+// the fixpoint passes decided this iteration's MIS (k_rr_mw then skips it)
 __device__ __forceinline__ bool fp_settled(const LoopBuffers& b) {
     return b.fp_ctl && (b.fp_ctl->state == FP_FINAL || b.fp_ctl->state == FP_DONE);
 }
@@ -3043,390 +2150,8 @@ __global__ __launch_bounds__(256) void k_rr_entries(ClauseView cv, LoopBuffers b
     }
 }
 
-template <uint32_t KR, uint32_t ST>
-__global__ __launch_bounds__(RR_THREADS) void k_rr_mis(ClauseView cv, LoopBuffers b) {
-    DevState* st = b.state;
-    if (!st->active || fp_settled(b)) return;
-    extern __shared__ __align__(16) unsigned char rr_lds_raw[];
-    RRLds& L = *reinterpret_cast<RRLds*>(rr_lds_raw);
-    const uint32_t stamp = st->stamp;
-    const uint32_t tid = threadIdx.x;
-    const uint32_t lane = tid & 63;
-    const uint32_t T = b.rr_T;
-    const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
-    const auto rsC = __builtin_amdgcn_make_buffer_rsrc(b.cover, (short)0, (int)b.n_vars, 0x00020000);
-    const bool prof = b.kdbg != nullptr;  // diagnostics: phase times of thread 0
-    unsigned long long tp0 = prof ? wall_now() : 0, tacc[4] = {0, 0, 0, 0};
-    unsigned long long gacc[4] = {0, 0, 0, 0};  // diagnostics, group 0 lane 0: loads, steps, rounds, scans
-
-    const uint32_t nu = (uint32_t)st->u_total;  // entries written by k_rr_entries
-    // ---- sets: [lower_bound(start q), lower_bound(start q+1)) of U
-    for (uint32_t q = tid; q < T; q += RR_THREADS) {
-        uint32_t bnd[2];
-        for (int e = 0; e < 2; ++e) {
-            const uint32_t key = b.rr_sets[q + e];
-            uint32_t lo = 0, hi = nu;
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (U[mid].a.x < key) lo = mid + 1; else hi = mid;
-            }
-            bnd[e] = lo;
-        }
-        L.ptr[q] = bnd[0];
-        L.end[q] = bnd[1];
-        L.live[q] = (uint16_t)q;
-    }
-    if (tid == 0) {
-        L.n_live = T; L.t = 0; L.tm = 0; L.wide = 0; L.n_steps = 0; L.n_rounds = 0; L.conf = RR_EMPTY;
-        L.gdur_sum = 0; L.gdur_max = 0; L.gdur_spread = 0;
-    }
-    for (uint32_t i = tid; i < RR_HASH; i += RR_THREADS) { L.hkey[i] = RR_EMPTY; L.hmin[i] = RR_EMPTY; }
-    __syncthreads();
-
-    uint32_t batches = 0;
-    if (prof) { const unsigned long long t1 = wall_now(); tacc[0] += t1 - tp0; tp0 = t1; }
-    while (true) {
-        const uint32_t n_live = L.n_live;
-        if (n_live == 0) break;
-        // every batch commits a turn, erases a set or advances set 0's scan by a full budget
-        if (++batches > 2 * nu + 2 * T + 64) {
-            if (tid == 0) { st->error = 1; st->done = 3; }
-            break;
-        }
-        const uint32_t GS = n_live <= RR_THREADS / 64 ? 64u : 16u;  // lanes per group
-        const uint32_t NG = RR_THREADS / GS;
-        const uint32_t B = n_live < NG ? n_live : NG;
-        const uint32_t vpg = RR_VCAP / B, cpg = RR_CMAX / B;
-        const uint32_t D = (B == n_live) ? cpg : 1u;
-        const uint32_t t0 = L.t;
-        // ---- scan: group g decides the next D turns of set live[(t + 1 + g) % n_live]
-        {
-            const uint32_t g = tid / GS, gl = tid % GS;
-            const uint32_t gshift = lane & ~(GS - 1);
-            const uint64_t gmask = GS == 64 ? ~0ull : ((1ull << GS) - 1ull);
-            const uint64_t below = (1ull << gl) - 1ull;
-            const uint32_t sbits = GS == 64 ? 9u : 7u;  // RR_SHASH / NG slots per group
-            const uint32_t shs = 1u << sbits, wcap = shs / 2;
-            unsigned long long* sk = L.skey + g * shs;
-            if (g < B) {
-                const uint32_t s = L.live[(t0 + 1 + g) % n_live];
-                uint32_t pos = L.ptr[s];
-                const uint32_t end = L.end[s];
-                uint32_t nc = 0, nv = 0, scan_end = pos, exhausted = 0, n_steps = 0, n_rounds = 0;
-                const uint32_t cb = g * cpg;
-                bool stop = false;
-                const bool gprof = prof && tid == 0;
-                const unsigned long long gstart = prof ? wall_now() : 0;
-                for (uint32_t round = 0; round < RR_ROUNDS && !stop; ++round) {
-                    unsigned long long gt0 = gprof ? wall_now() : 0;
-                    // loads of ST steps: clause, width, variables, covered test
-                    uint32_t c[ST], lb[ST], w[ST], rv[ST][KR];
-                    bool alive[ST];
-#pragma unroll
-                    for (uint32_t u = 0; u < ST; ++u) {
-                        const uint32_t i = pos + u * GS + gl;
-                        alive[u] = i < end;
-                        RREnt e;
-                        if (alive[u]) e = U[i];
-                        else { e.a = make_uint4(0u, 0u, 0u, 0u); e.v0 = e.v1 = make_uint4(RR_EMPTY, RR_EMPTY, RR_EMPTY, RR_EMPTY); }
-                        c[u] = e.a.x; lb[u] = e.a.y; w[u] = e.a.z;
-                        const uint32_t ev[8] = {e.v0.x, e.v0.y, e.v0.z, e.v0.w, e.v1.x, e.v1.y, e.v1.z, e.v1.w};
-#pragma unroll
-                        for (uint32_t j = 0; j < KR; ++j) rv[u][j] = ev[j];
-                    }
-                    // cover stamps of all ST steps by write-through (sc1) buffer loads, issued
-                    // together: they see the previous batches' commits (unlike atomic loads they
-                    // are not ordered among themselves); RR_EMPTY past a clause's width is out of
-                    // range and reads 0
-                    uint32_t cs[ST][KR];
-#pragma unroll
-                    for (uint32_t u = 0; u < ST; ++u)
-#pragma unroll
-                        for (uint32_t j = 0; j < KR; ++j) cs[u][j] = __builtin_amdgcn_raw_buffer_load_b8(rsC, rv[u][j], 0, 16);
-#pragma unroll
-                    for (uint32_t u = 0; u < ST; ++u) {
-#pragma unroll
-                        for (uint32_t j = 0; j < KR; ++j) alive[u] &= cs[u][j] != stamp;
-                    }
-#pragma unroll
-                    for (uint32_t u = 0; u < ST; ++u)
-                        for (uint32_t j = KR; j < w[u]; ++j)
-                            alive[u] &= __builtin_amdgcn_raw_buffer_load_b8(rsC, lit_var(cv.lits[lb[u] + j]), 0, 16) != stamp;
-                    if (gprof) {
-                        __builtin_amdgcn_s_waitcnt(0);
-                        const unsigned long long gt1 = wall_now();
-                        gacc[0] += gt1 - gt0;
-                        gt0 = gt1;
-                        ++gacc[2];
-                    }
-#pragma unroll
-                    for (uint32_t u = 0; u < ST; ++u) {
-                        if (stop) break;
-                        const uint32_t pu = pos + u * GS;
-                        if (pu >= end) { exhausted = 1; scan_end = end; stop = true; break; }
-                        const uint32_t i = pu + gl;
-                        bool al = alive[u];
-                        auto var_of = [&](uint32_t j) -> uint32_t {
-                            return j < KR ? rv[u][j] : lit_var(cv.lits[lb[u] + j]);
-                        };
-                        // erased by an earlier pick of this group in the batch
-                        if (al && nc) {
-                            al = !rr_own_any(L, rv[u], w[u] < KR ? w[u] : KR, B, g);
-                            for (uint32_t j = KR; al && j < w[u]; ++j)
-                                if (rr_own(L, var_of(j), B, g)) al = false;
-                        }
-                        uint64_t und = (__ballot(al) >> gshift) & gmask;
-                        if (!und) continue;
-                        ++n_steps;
-                        // greedy (lane order) subset S of the live candidates, by rounds: a lane that
-                        // holds the lowest undecided lane index on every variable is in S, the lanes
-                        // sharing a variable with it are out
-                        uint64_t S = 0;
-                        while (und) {
-                            ++n_rounds;
-                            const bool me = (und >> gl) & 1ull;
-                            uint32_t wsum = me ? w[u] : 0u;
-                            if (b.rr_k) {
-                                wsum = me ? b.rr_k * ((uint32_t)__popcll(und & below) + 1u) : 0u;
-                            } else {
-                                for (uint32_t o = 1; o < GS; o <<= 1) {
-                                    const uint32_t y = __shfl_up(wsum, o, GS);
-                                    if (gl >= o) wsum += y;
-                                }
-                            }
-                            const bool inwin = me && wsum <= wcap;  // lanes whose variables fit the step hash
-                            const uint32_t first = (uint32_t)__builtin_ctzll(und);
-                            bool win = false, dead = false;
-                            const bool wide_first = !((__ballot(inwin) >> gshift >> first) & 1ull);
-                            if (wide_first) {
-                                // the first undecided lane alone is too wide: it is in S; the others
-                                // compare their variables with its variables in memory
-                                win = gl == first;
-                                const uint32_t lb0 = __shfl(lb[u], (int)(gshift + first), 64);
-                                const uint32_t w0 = __shfl(w[u], (int)(gshift + first), 64);
-                                for (uint32_t j0 = 0; j0 < w0; ++j0) {
-                                    const uint32_t v0 = lit_var(cv.lits[lb0 + j0]);
-                                    if (me && !win && !dead)
-                                        for (uint32_t j = 0; j < w[u]; ++j) dead |= var_of(j) == v0;
-                                }
-                            }
-                            uint64_t W;
-                            if (wide_first) {
-                                W = (__ballot(win) >> gshift) & gmask;
-                            } else {
-                                for (uint32_t q = gl; q < shs; q += GS) sk[q] = RR_EMPTY64;
-                                __builtin_amdgcn_wave_barrier();
-                                bool dup = false;
-                                if (inwin)
-                                    for (uint32_t j = 0; j < w[u]; ++j) dup |= rr_step_insert(sk, sbits, var_of(j), gl);
-                                __builtin_amdgcn_wave_barrier();
-                                const uint64_t wm = (__ballot(inwin) >> gshift) & gmask;
-                                if (!((__ballot(dup) >> gshift) & gmask) && wm == und) {
-                                    // no variable shared inside the step: every candidate is in S
-                                    win = me;
-                                    W = und;
-                                } else {
-                                    uint32_t ml[KR];
-                                    rr_step_lanes(sk, sbits, rv[u], me ? (w[u] < KR ? w[u] : KR) : 0u, ml);
-                                    win = inwin;
-#pragma unroll
-                                    for (uint32_t j = 0; j < KR; ++j) win &= j >= w[u] || ml[j] == gl;
-                                    for (uint32_t j = KR; win && j < w[u]; ++j) win = rr_step_lane(sk, sbits, var_of(j)) == gl;
-                                    W = (__ballot(win) >> gshift) & gmask;
-                                    if (me && !win) {
-#pragma unroll
-                                        for (uint32_t j = 0; j < KR; ++j)
-                                            dead |= j < w[u] && ml[j] != RR_EMPTY && ((W >> ml[j]) & 1ull);
-                                        for (uint32_t j = KR; !dead && j < w[u]; ++j) {
-                                            const uint32_t q = rr_step_lane(sk, sbits, var_of(j));
-                                            dead = q != RR_EMPTY && ((W >> q) & 1ull);
-                                        }
-                                    }
-                                }
-                            }
-                            const uint64_t Dm = (__ballot(dead) >> gshift) & gmask;
-                            S |= W;
-                            und &= ~(W | Dm);
-                        }
-                        // S in lane order, up to the level and variable capacities
-                        const bool inS = (S >> gl) & 1ull;
-                        const uint32_t rank = (uint32_t)__popcll(S & below);
-                        uint32_t wincl = inS ? w[u] : 0u;
-                        if (b.rr_k) {
-                            wincl = inS ? b.rr_k * (rank + 1u) : 0u;
-                        } else {
-                            for (uint32_t o = 1; o < GS; o <<= 1) {
-                                const uint32_t y = __shfl_up(wincl, o, GS);
-                                if (gl >= o) wincl += y;
-                            }
-                        }
-                        const bool picked = inS && nc + rank < D && nv + wincl <= vpg;
-                        const uint64_t pm = (__ballot(picked) >> gshift) & gmask;
-                        if (picked) {
-                            const uint32_t idx = nc + rank, tau = idx * B + g;
-                            L.cc[cb + idx] = c[u];
-                            L.cpos[cb + idx] = i;
-                            for (uint32_t j = 0; j < w[u]; ++j) rr_insert(L, var_of(j), tau);
-                        }
-                        const uint32_t np = (uint32_t)__popcll(pm);
-                        if (np) {
-                            const uint32_t lastp = 63u - (uint32_t)__builtin_clzll(pm);
-                            nv += __shfl(wincl, (int)(gshift + lastp), 64);
-                        }
-                        nc += np;
-                        const uint64_t rest = S & ~pm;
-                        if (rest) {
-                            const uint32_t i0 = (uint32_t)__builtin_ctzll(rest);
-                            stop = true;
-                            scan_end = pu + i0;
-                            if (np == 0 && nc == 0 && g == 0) {
-                                // turn 0 is always exact: a pick too wide to record is committed
-                                // alone (its variables are covered from memory)
-                                if (gl == i0) {
-                                    L.cc[cb] = c[u];
-                                    L.cpos[cb] = i;
-                                    L.wide = 1;
-                                }
-                                nc = 1;
-                                scan_end = pu + i0 + 1;
-                            }
-                        } else if (nc == D) {
-                            stop = true;
-                            scan_end = pu + GS < end ? pu + GS : end;
-                        }
-                    }
-                    if (!stop) { pos += ST * GS; scan_end = pos; }
-                    if (gprof) gacc[1] += wall_now() - gt0;
-                }
-                if (gprof) ++gacc[3];
-                if (!stop && pos >= end) { exhausted = 1; scan_end = end; }
-                if (gl == 0) {
-                    L.ncand[g] = nc;
-                    L.scan_end[g] = scan_end;
-                    L.exh[g] = exhausted;
-                    if (prof) {
-                        atomicAdd(&L.n_steps, n_steps); atomicAdd(&L.n_rounds, n_rounds);
-                        const unsigned long long gd = wall_now() - gstart;
-                        atomicAdd(&L.gdur_sum, gd); atomicMax(&L.gdur_spread, gd);
-                    }
-                }
-            }
-        }
-        __syncthreads();
-        if (prof) {
-            const unsigned long long t1 = wall_now();
-            tacc[1] += t1 - tp0;
-            tp0 = t1;
-            if (tid == 0) { L.gdur_max += L.gdur_spread; L.gdur_spread = 0; }
-        }
-        // ---- the batch is exact below the first turn a group did not decide and the first
-        // pick that shares a variable with a pick of an earlier turn (L.conf, from the inserts)
-        if (tid < B) {
-            const uint32_t nc = L.ncand[tid];
-            if (nc < D) atomicMin(&L.conf, nc * B + tid);
-        }
-        __syncthreads();
-        if (prof) { const unsigned long long t1 = wall_now(); tacc[2] += t1 - tp0; tp0 = t1; }
-        const uint32_t trunc = L.wide ? 1u : min(D * B, L.conf);  // (L.conf is reset after the next barrier)
-        // ---- commit turns < trunc: covers, MIS, statistics; reset the batch hash
-        for (uint32_t i = tid; i < RR_HASH; i += RR_THREADS) {
-            const uint32_t k = L.hkey[i];
-            if (k != RR_EMPTY && L.hmin[i] < trunc) __builtin_amdgcn_raw_buffer_store_b8((uint8_t)stamp, rsC, k, 0, 16);
-            L.hkey[i] = RR_EMPTY;
-            L.hmin[i] = RR_EMPTY;
-        }
-        if (L.wide) {
-            const uint32_t c = L.cc[0], lb = cv.offs[c], w = cv.offs[c + 1] - lb;
-            for (uint32_t j = tid; j < w; j += RR_THREADS)
-                __hip_atomic_store(&b.cover[lit_var(cv.lits[lb + j])], (uint8_t)stamp, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-        }
-        for (uint32_t e = tid; e < B * cpg; e += RR_THREADS) {
-            const uint32_t g = e / cpg, l = e - g * cpg;
-            if (l >= L.ncand[g] || l * B + g >= trunc) continue;
-            b.tmis[atomicAdd(&L.tm, 1u)] = L.cc[e];
-        }
-        uint32_t new_ptr = 0, ptr_set = RR_EMPTY;
-        if (tid < B) {
-            const uint32_t g = tid, nc = L.ncand[g];
-            uint32_t a = trunc > g ? (trunc - g + B - 1) / B : 0;
-            if (a > nc) a = nc;
-            ptr_set = L.live[(t0 + 1 + g) % n_live];
-            new_ptr = a < nc ? L.cpos[g * cpg + a] : L.scan_end[g];
-        }
-        __threadfence();
-        __syncthreads();
-        if (ptr_set != RR_EMPTY) L.ptr[ptr_set] = new_ptr;
-        // ---- erasure at turn trunc, or the next turn index
-        bool erase = false;
-        uint32_t idx_e = 0;
-        if (trunc < D * B) {
-            const uint32_t ge = trunc % B, le = trunc / B;
-            erase = (le == L.ncand[ge]) && L.exh[ge];
-            idx_e = (t0 + 1 + trunc) % n_live;
-        }
-        uint16_t moved[RR_TMAX / RR_THREADS];
-#pragma unroll
-        for (uint32_t r = 0; r < RR_TMAX / RR_THREADS; ++r) {
-            const uint32_t i = tid + r * RR_THREADS;
-            moved[r] = (erase && i >= idx_e && i + 1 < n_live) ? L.live[i + 1] : 0;
-        }
-        __syncthreads();
-        if (erase) {
-#pragma unroll
-            for (uint32_t r = 0; r < RR_TMAX / RR_THREADS; ++r) {
-                const uint32_t i = tid + r * RR_THREADS;
-                if (i >= idx_e && i + 1 < n_live) L.live[i] = moved[r];
-            }
-        }
-        if (tid == 0) {
-            L.wide = 0;
-            L.conf = RR_EMPTY;
-            if (erase) {
-                L.n_live = n_live - 1;
-                L.t = idx_e;  // t is not decremented: the next turn skips the moved-up set
-            } else {
-                L.t = (t0 + trunc) % n_live;
-            }
-        }
-        __syncthreads();
-        if (prof) { const unsigned long long t1 = wall_now(); tacc[3] += t1 - tp0; tp0 = t1; }
-    }
-    // statistics of the MIS (per tile, like the LFMIS kernels): |M| and resampled literals
-    const uint32_t tm = L.tm;
-    for (uint32_t i0 = 0; i0 < tm; i0 += 4 * RR_THREADS) {
-        uint32_t cs[4], ws[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint32_t i = i0 + q * RR_THREADS + tid;
-            cs[q] = i < tm ? b.tmis[i] : RR_EMPTY;
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) ws[q] = cs[q] != RR_EMPTY ? cv.offs[cs[q] + 1] - cv.offs[cs[q]] : 0u;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            if (cs[q] == RR_EMPTY) continue;
-            atomicAdd(&b.tile_stats[2 * (cs[q] / TILE)], 1ull);
-            atomicAdd(&b.tile_stats[2 * (cs[q] / TILE) + 1], (unsigned long long)ws[q]);
-        }
-    }
-    if (tid == 0) {
-        st->tmis_cnt = L.tm;
-        st->tail_rounds = batches;
-        if (prof) {
-            unsigned long long* d = b.kdbg + (uint64_t)3 * DBG_BLOCKS * DBG_FIELDS;
-            d[0] = tacc[0]; d[1] = tacc[1]; d[2] = tacc[2]; d[3] = tacc[3];
-            d[4] = batches; d[5] = L.n_steps; d[6] = L.n_rounds; d[7] = L.tm;
-            d[8] = gacc[0]; d[9] = gacc[1]; d[10] = gacc[2]; d[11] = gacc[3];
-            d[12] = L.gdur_sum; d[13] = L.gdur_max;
-        }
-        if (batches > st->max_rounds) st->max_rounds = batches;
-        if (b.ktime) time_slot(b, st->n_iter - 1)[3] = wall_now();
-    }
-}
-
 // ------------------------------------------------------------------------------------
-// Round-robin MIS across workgroups (k_rr_mw): the batches of k_rr_mis with every lane group in
+// Round-robin MIS across workgroups (k_rr_mw): the batches with every lane group in
 // a workgroup of its own (one wave, one CU), so that the groups' scan steps -- chains of
 // dependent LDS hash operations -- no longer share one CU.  What the groups shared in LDS moves
 // to global memory:
@@ -3439,7 +2164,7 @@ __global__ __launch_bounds__(RR_THREADS) void k_rr_mis(ClauseView cv, LoopBuffer
 // Two grid barriers per batch (a monotonic counter per iteration, zeroed by k_rr_entries; every
 // spin bounded by a device-clock timeout).  Every workgroup keeps the same replicated live-set
 // list and turn index and takes the same decisions from the same global words, so the batch
-// sequence, its exact prefix and the set erasures are those of k_rr_mis.
+// sequence, its exact prefix and the set erasures are the same on every workgroup.
 constexpr uint32_t RR_MW_MAX = 64;        // workgroups (groups per batch)
 constexpr uint32_t RR_MW_VPG = 256;       // variables of a group's picks per batch
 constexpr uint32_t RR_MW_CPG = 128;       // picks of a group per batch
@@ -3545,21 +2270,6 @@ __global__ __launch_bounds__(64) void k_rr_mw(ClauseView cv, LoopBuffers b) {
     const uint32_t base = __hip_atomic_load(&ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint32_t nbar = 0;
     bool ok = true;
-    // diagnostics (ALLL_DEBUG_PHASES): workgroup 0's time in scan, hash inserts, first barrier,
-    // commit, second barrier
-    const bool prof = b.kdbg != nullptr && g == 0;
-    unsigned long long pacc[5] = {0, 0, 0, 0, 0}, pt = prof ? wall_now() : 0;
-    unsigned long long sacc[6] = {0, 0, 0, 0, 0, 0}, st0 = 0;  // scan detail: loads, own, greedy, picks, steps, overhead
-    auto sstamp = [&](int k) {
-        if (prof) { const unsigned long long t1 = wall_now(); sacc[k] += t1 - st0; st0 = t1; }
-    };
-    if (prof) {  // cost of one stamp pair
-        const unsigned long long a0 = wall_now(), a1 = wall_now();
-        sacc[5] = a1 - a0;
-    }
-    auto pstamp = [&](int k) {
-        if (prof) { const unsigned long long t1 = wall_now(); pacc[k] += t1 - pt; pt = t1; }
-    };
     // ---- sets: [lower_bound(start q), lower_bound(start q+1)) of U, spread over the workgroups
     for (uint32_t q = g * 64 + lane; q < T; q += NW * 64) {
         uint32_t bnd[2];
@@ -3608,7 +2318,6 @@ __global__ __launch_bounds__(64) void k_rr_mw(ClauseView cv, LoopBuffers b) {
             uint32_t nv = 0, scan_end = pos, exhausted = 0;
             bool stop = false;
             for (uint32_t round = 0; round < RR_ROUNDS && !stop; ++round) {
-                if (prof) st0 = wall_now();
                 uint32_t c[ST], lb[ST], w[ST], rv[ST][KR];
                 bool alive[ST];
 #pragma unroll
@@ -3637,13 +2346,6 @@ __global__ __launch_bounds__(64) void k_rr_mw(ClauseView cv, LoopBuffers b) {
                 for (uint32_t u = 0; u < ST; ++u)
                     for (uint32_t j = KR; j < w[u]; ++j)
                         alive[u] &= __builtin_amdgcn_raw_buffer_load_b8(rsC, lit_var(cv.lits[lb[u] + j]), 0, 16) != stamp;
-                if (prof) {
-                    bool any = false;
-#pragma unroll
-                    for (uint32_t u = 0; u < ST; ++u) any |= alive[u];
-                    if (__ballot(any) == 0x123ull) sacc[5] += 1;  // (consumes the loads before the stamp)
-                    sstamp(0);
-                }
 #pragma unroll
                 for (uint32_t u = 0; u < ST; ++u) {
                     if (stop) break;
@@ -3660,10 +2362,8 @@ __global__ __launch_bounds__(64) void k_rr_mw(ClauseView cv, LoopBuffers b) {
                             if (rr_mw_own(L, var_of(j))) al = false;
                     }
                     uint64_t und = __ballot(al);
-                    sstamp(1);
                     if (!und) continue;
-                    if (prof) sacc[4] += 1;
-                    // greedy (lane order) subset S of the live candidates (as k_rr_mis)
+                    // greedy (lane order) subset S of the live candidates
                     uint64_t S = 0;
                     while (und) {
                         const bool me = (und >> lane) & 1ull;
@@ -3725,7 +2425,6 @@ __global__ __launch_bounds__(64) void k_rr_mw(ClauseView cv, LoopBuffers b) {
                         S |= W;
                         und &= ~(W | Dm);
                     }
-                    sstamp(2);
                     // S in lane order, up to the level and variable capacities
                     const bool inS = (S >> lane) & 1ull;
                     const uint32_t rank = (uint32_t)__popcll(S & below);
@@ -3752,7 +2451,6 @@ __global__ __launch_bounds__(64) void k_rr_mw(ClauseView cv, LoopBuffers b) {
                             rr_mw_own_insert(L, v);
                         }
                     }
-                    if (prof) { __builtin_amdgcn_s_waitcnt(0); sstamp(3); }
                     const uint32_t np = (uint32_t)__popcll(pm);
                     if (np) {
                         const uint32_t lastp = 63u - (uint32_t)__builtin_clzll(pm);
@@ -3780,7 +2478,6 @@ __global__ __launch_bounds__(64) void k_rr_mw(ClauseView cv, LoopBuffers b) {
             }
             if (!stop && pos >= end) { exhausted = 1; scan_end = end; }
             __syncthreads();
-            pstamp(0);
             // ---- the picks' variables into the global hash (turn pick * B + g), RR_MW_VPG / 64
             // per lane, their slot claims issued together, then their minima; an insert that
             // meets another turn offers the later one to ctl->conf
@@ -3836,9 +2533,7 @@ __global__ __launch_bounds__(64) void k_rr_mw(ClauseView cv, LoopBuffers b) {
                 __hip_atomic_store(&ctl->exh[g], exhausted, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             // (the own-pick hash is cleared after the commit)
-            pstamp(1);
             if (!(ok = rr_mw_barrier(ctl, ++nbar * NW))) break;
-            pstamp(2);
             // ---- the exact prefix (identical in every workgroup)
         } else {
             if (!(ok = rr_mw_barrier(ctl, ++nbar * NW))) break;
@@ -3902,12 +2597,10 @@ __global__ __launch_bounds__(64) void k_rr_mw(ClauseView cv, LoopBuffers b) {
         } else {
             t = (t0 + trunc) % n_live;
         }
-        pstamp(3);
         if (!(ok = rr_mw_barrier(ctl, ++nbar * NW))) break;
-        pstamp(4);
     }
-    if (!ok) {
-        if (lane == 0) { st->error = 1; st->done = 3; }
+    if (!ok) {  // a grid barrier timed out: the workgroups were not all resident (error 4)
+        if (lane == 0) { st->error = 4; st->done = 3; }
         return;
     }
     // statistics of the MIS (per tile, like the LFMIS kernels), spread over the workgroups
@@ -3923,13 +2616,6 @@ __global__ __launch_bounds__(64) void k_rr_mw(ClauseView cv, LoopBuffers b) {
         if (batches > st->max_rounds) st->max_rounds = batches;
         __hip_atomic_store(&ctl->epoch, base + batches + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (b.ktime) time_slot(b, st->n_iter - 1)[3] = wall_now();
-        if (prof) {
-            unsigned long long* d = b.kdbg + (uint64_t)3 * DBG_BLOCKS * DBG_FIELDS;
-            d[0] = 0; d[1] = pacc[0] + pacc[1]; d[2] = pacc[2]; d[3] = pacc[3] + pacc[4];
-            d[4] = batches; d[5] = 0; d[6] = 0; d[7] = tm;
-            d[8] = pacc[0]; d[9] = pacc[1]; d[10] = pacc[2]; d[11] = pacc[3]; d[12] = pacc[4];
-            d[13] = sacc[0]; d[14] = sacc[1]; d[15] = sacc[2]; d[16] = sacc[3]; d[17] = sacc[4]; d[18] = sacc[5];
-        }
     }
 }
 
@@ -4923,7 +3609,7 @@ hipError_t launch_eval(const ClauseView& cv, const LoopBuffers& b, uint32_t tile
 // and device records what is set (contexts on several devices may share a process).
 constexpr int ATTR_MAX_DEV = 64;
 static std::atomic<uint32_t> g_attr_done[ATTR_MAX_DEV];
-enum : uint32_t { ATTR_HYBRID = 0, ATTR_BUCKETS = 9, ATTR_RR = 18, ATTR_DD = 19, ATTR_RAGGED = 30 };  // + k for per-width groups
+enum : uint32_t { ATTR_HYBRID = 0, ATTR_BUCKETS = 9, ATTR_RAGGED = 30 };  // + k for per-width groups
 static bool attr_pending(uint32_t bit, int& dev) {
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= ATTR_MAX_DEV) {
         dev = -1;
@@ -5020,40 +3706,6 @@ hipError_t launch_round(const ClauseView& cv, const LoopBuffers& b, uint32_t r, 
     return hipGetLastError();
 }
 
-hipError_t launch_claim_only(const ClauseView& cv, const LoopBuffers& b, uint32_t r, uint32_t wave_from,
-                             const uint32_t* in, uint32_t* out, hipStream_t s) {
-    if (b.n_tiles == 0) return hipSuccess;
-    if (r >= wave_from) {
-        const uint32_t grid = (b.n_tiles + ROUND_THREADS / 64 - 1) / (ROUND_THREADS / 64);
-        ALLL_DISPATCH_K(cv.k, (k_wclaim<K><<<grid, ROUND_THREADS, 0, s>>>(cv, b, r, in, out)));
-    } else {
-        ALLL_DISPATCH_K(cv.k, (k_claim<K><<<b.n_tiles, ROUND_THREADS, 0, s>>>(cv, b, r, const_cast<uint32_t*>(in), out)));
-    }
-    return hipGetLastError();
-}
-
-hipError_t launch_join_only(const ClauseView& cv, const LoopBuffers& b, uint32_t r, bool last, uint32_t wave_from,
-                            const uint32_t* in, uint32_t* out, hipStream_t s) {
-    if (b.n_tiles == 0) return hipSuccess;
-    const int l = last ? 1 : 0;
-    if (r >= wave_from) {
-        const uint32_t grid = (b.n_tiles + ROUND_THREADS / 64 - 1) / (ROUND_THREADS / 64);
-        ALLL_DISPATCH_K(cv.k, (k_wjoin<K><<<grid, ROUND_THREADS, 0, s>>>(cv, b, r, in, out, l)));
-    } else {
-        ALLL_DISPATCH_K(cv.k, (k_join<K><<<b.n_tiles, JOIN_THREADS, 0, s>>>(cv, b, r, in, out, l)));
-    }
-    return hipGetLastError();
-}
-
-hipError_t launch_join_claim(const ClauseView& cv, const LoopBuffers& b, uint32_t r, const uint32_t* in, uint32_t* out,
-                             hipStream_t s) {
-    if (b.n_tiles == 0) return hipSuccess;
-    if (cv.k == 0 || cv.k > (uint32_t)MAX_FIXED_K || !b.owner_alt) return hipErrorInvalidValue;
-    const uint32_t grid = (b.n_tiles + ROUND_THREADS / 64 - 1) / (ROUND_THREADS / 64);
-    ALLL_DISPATCH_K(cv.k, (k_wjc<(K > 0 ? K : 1)><<<grid, ROUND_THREADS, 0, s>>>(cv, b, r, in, out)));
-    return hipGetLastError();
-}
-
 hipError_t launch_round0_buckets(const ClauseView& cv, const LoopBuffers& b, bool last, bool fused_reduce,
                                  bool scattered, hipStream_t s) {
     // buffers as CLAIM(0) + JOIN(0): eval -> stage[0] (ids translated in place); JOIN stage[0] -> stage[1]
@@ -5105,43 +3757,6 @@ hipError_t launch_round0_buckets(const ClauseView& cv, const LoopBuffers& b, boo
     return hipGetLastError();
 }
 
-hipError_t launch_lfmis_dd(const ClauseView& cv, const LoopBuffers& b, bool scattered, bool fused_reduce,
-                           hipStream_t s) {
-    if (b.n_tiles == 0 || cv.k == 0 || cv.k > (uint32_t)MAX_FIXED_K || !b.pairs || !b.dd_msg) return hipErrorInvalidValue;
-    const uint32_t run_cap = b.run_tiles * TILE * cv.k;
-    const size_t lds_sort = dd_sort_lds(b), lds_gen = dd_sort_general_lds(b), lds_dec = dd_decide_lds(b, cv.k);
-    int dev;
-    if (attr_pending(ATTR_DD + cv.k, dev)) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_bsort<DDS_UNROLL, DDS_THREADS>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 512);
-        if (e == hipSuccess)
-            e = hipFuncSetAttribute((const void*)k_bsort_general<DDS_UNROLL_GEN, DDS_THREADS>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 512);
-        if (e != hipSuccess) return e;
-        ALLL_DISPATCH_K(cv.k, (e = hipFuncSetAttribute((const void*)k_decide<(K > 0 ? K : 1)>,
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - 1024)));
-        if (e != hipSuccess) return e;
-        ALLL_DISPATCH_K(cv.k, (e = hipFuncSetAttribute((const void*)k_bscatter<(K > 0 ? K : 1)>,
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                       (int)(BKT_STAGE * 8))));
-        if (e != hipSuccess) return e;
-        attr_mark(ATTR_DD + cv.k, dev);
-    }
-    const int fr = fused_reduce ? 1 : 0;
-    hipError_t e;
-    if (!scattered) {
-        ALLL_DISPATCH_K(cv.k, (k_bscatter<(K > 0 ? K : 1)><<<b.n_runs, BSC_THREADS, BKT_STAGE * 8, s>>>(
-                                  cv, b, b.stage[0], fr)));
-        if ((e = hipGetLastError()) != hipSuccess) return e;
-    }
-    k_bsort<DDS_UNROLL, DDS_THREADS><<<b.n_bkt, DDS_THREADS, lds_sort, s>>>(b, run_cap, fr);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    k_bsort_general<DDS_UNROLL_GEN, DDS_THREADS><<<b.n_bkt, DDS_THREADS, lds_gen, s>>>(b, run_cap);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    ALLL_DISPATCH_K(cv.k, (k_decide<(K > 0 ? K : 1)><<<b.n_runs, DDD_THREADS, lds_dec, s>>>(cv, b, b.stage[0], run_cap)));
-    return hipGetLastError();
-}
-
 hipError_t launch_tail(const ClauseView& cv, const LoopBuffers& b, uint32_t first_round, hipStream_t s) {
     ALLL_DISPATCH_K(cv.k, (k_tail<K><<<1, TAIL_THREADS, 0, s>>>(cv, b, first_round)));
     return hipGetLastError();
@@ -5149,24 +3764,13 @@ hipError_t launch_tail(const ClauseView& cv, const LoopBuffers& b, uint32_t firs
 
 hipError_t launch_rr_mis(const ClauseView& cv, const LoopBuffers& b, hipStream_t s) {
     if (cv.k != 0 || !b.rr_u || b.rr_T < 2 || b.rr_T > RR_TMAX) return hipErrorInvalidValue;
-    int dev;
-    if (attr_pending(ATTR_RR, dev)) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_rr_mis<4, 4>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)sizeof(RRLds));
-        if (e == hipSuccess)
-            e = hipFuncSetAttribute((const void*)k_rr_mis<8, 2>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)sizeof(RRLds));
-        if (e != hipSuccess) return e;
-        attr_mark(ATTR_RR, dev);
-    }
     if (b.n_tiles) k_rr_entries<<<b.n_tiles, 256, 0, s>>>(cv, b);
     if (b.fp_ctl) {  // the fixpoint passes; k_rr_mw below only if they do not settle
         if (b.rr_T > FP_TMAX || b.fp_max == 0) return hipErrorInvalidValue;
         const bool narrow = b.rr_k >= 1 && b.rr_k <= 4;
         const uint32_t gb = (uint32_t)std::min<uint64_t>((b.m + FP_B - 1) / FP_B + 1, FP_COUNT_GRID);
         const uint32_t gl = (uint32_t)std::min<uint64_t>((b.m + FP_THREADS - 1) / FP_THREADS + 1, 2048);
-        uint32_t fp_grid = 2048;  // workgroups of the grid-stride round kernels (ALLL_FP_GRID: A/B)
-        if (const char* ge = getenv("ALLL_FP_GRID")) fp_grid = (uint32_t)std::max(64, atoi(ge));
+        const uint32_t fp_grid = 2048;  // workgroups of the grid-stride round kernels
         const uint32_t gr = (uint32_t)std::min<uint64_t>((b.m + FP_RT - 1) / FP_RT + 1, fp_grid);
         hipError_t e = hipMemsetAsync(b.fp_owner, 0xFF, (size_t)b.n_vars * 8, s);
         if (e != hipSuccess) return e;
@@ -5213,15 +3817,9 @@ hipError_t launch_rr_mis(const ClauseView& cv, const LoopBuffers& b, hipStream_t
         }
     }
     // clause variables held in registers while scanning: 4 for instances of width <= 4
-    if (b.rr_mw) {
-        if (!b.rr_ctl || b.rr_mw > RR_MW_MAX) return hipErrorInvalidValue;
-        if (b.rr_k >= 1 && b.rr_k <= 4) k_rr_mw<4, 4><<<b.rr_mw, 64, sizeof(RRMwLds), s>>>(cv, b);
-        else k_rr_mw<8, 2><<<b.rr_mw, 64, sizeof(RRMwLds), s>>>(cv, b);
-    } else if (b.rr_k >= 1 && b.rr_k <= 4) {
-        k_rr_mis<4, 4><<<1, RR_THREADS, sizeof(RRLds), s>>>(cv, b);
-    } else {
-        k_rr_mis<8, 2><<<1, RR_THREADS, sizeof(RRLds), s>>>(cv, b);
-    }
+    if (!b.rr_ctl || b.rr_mw == 0 || b.rr_mw > RR_MW_MAX) return hipErrorInvalidValue;
+    if (b.rr_k >= 1 && b.rr_k <= 4) k_rr_mw<4, 4><<<b.rr_mw, 64, sizeof(RRMwLds), s>>>(cv, b);
+    else k_rr_mw<8, 2><<<b.rr_mw, 64, sizeof(RRMwLds), s>>>(cv, b);
     return hipGetLastError();
 }
 

@@ -75,17 +75,12 @@ struct alll_ctx {
     LoopBuffers b{};
     uint32_t tiles_per_rank = 0, own_begin = 0, own_end = 0, n_tiles_padded = 0;
     uint32_t grid_rounds = DEFAULT_GRID_ROUNDS;
-    bool fuse_reduce = true;     // env ALLL_FUSE_REDUCE=0: separate k_reduce (tests, A/B)
-    uint32_t fuse_jc = 0;        // env ALLL_FUSE_JC=f >= 1 (fixed k): JOIN(r) + CLAIM(r+1) in one launch
-                                 // for f <= r < G - 1 (k_wjc, two owner arrays); measured no faster
-                                 // (DESIGN.md §7.1), so off by default
     // env ALLL_FUSE_SCATTER=1: the evaluation workgroups scatter their runs themselves (no
     // k_bscatter launch; +2.6% iterations/s at M, but the evaluation kernel's duration then
     // includes the scatter, so its roofline is no longer the evaluation's: off by default)
     bool fuse_scatter = false;
     std::vector<uint32_t> run_t0;  // bucketed round 0: first tile of every run (+ end)
     uint32_t wave_round_min = WAVE_ROUND_MIN;  // first grid round with a wave per tile
-    bool dd = false;             // dependency-driven LFMIS for the bucketed variant
     int rank = 0, world = 1;
     bool allreduce = false;
     ncclComm_t comm = nullptr;
@@ -117,7 +112,6 @@ struct alll_ctx {
     uint64_t bucket_min_u = 0;  // bucketed round 0 when the last pass found at least this many
     hipEvent_t ev[8] = {};
     int n_cu = 256;
-    int eval_wgs = 1;            // hybrid evaluation workgroups per CU (LDS window = LDS_WORDS / eval_wgs)
     bool hybrid = false;
     alll_exchange_fn xfn = nullptr;  // host-staged exchange (instead of RCCL)
     void* xuser = nullptr;
@@ -290,12 +284,9 @@ int read_state(alll_ctx* c) {
     c->hint_iter = c->h_state->n_iter;
     c->hint_rounds = c->h_state->tail_rounds;
     c->async_pending = false;  // (the stream is drained: this read is newer)
-    if (c->h_state->error == 2)
-        return fail(ALLL_ERR_UNSUPPORTED, "a variable has more violated claimants than the dependency-driven "
-                                          "LFMIS sorts at once (%u)", DDS_CAP);
-    if (c->h_state->error == 3)
-        return fail(ALLL_ERR_UNSUPPORTED, "dependency-driven LFMIS: a run did not finish within %u ms",
-                    DD_TIMEOUT / 100000u);
+    if (c->h_state->error == 4)
+        return fail(ALLL_ERR_HIP, "round-robin MIS: a grid barrier of k_rr_mw timed out (its %u workgroups "
+                                  "were not all resident)", c->b.rr_mw);
     if (c->h_state->error)
         return fail(ALLL_ERR_UNSUPPORTED, c->b.rr_T ? "round-robin MIS exceeded its batch cap in one iteration"
                                                     : "LFMIS needed more than %u rounds in one iteration",
@@ -315,11 +306,7 @@ int write_limits(alll_ctx* c, uint64_t limit_eval, uint64_t limit_nores) {
 
 hipError_t eval_launch(alll_ctx* c, uint32_t tb, uint32_t te, bool gated, bool scatter = false) {
     if (c->cv.rg_off) return launch_eval_ragged(c->cv, c->b, tb, te, gated, c->n_cu, c->stream);
-    if (c->hybrid) {
-        int grid = c->n_cu * c->eval_wgs;
-        if (const char* e = getenv("ALLL_EVAL_GRID")) grid = atoi(e);  // tuning experiments
-        return launch_eval_hybrid(c->cv, c->b, tb, te, gated, grid, scatter, c->stream);
-    }
+    if (c->hybrid) return launch_eval_hybrid(c->cv, c->b, tb, te, gated, c->n_cu, scatter, c->stream);
     return launch_eval(c->cv, c->b, tb, te, gated, c->stream);
 }
 
@@ -359,8 +346,17 @@ int round0_variant(const alll_ctx* c) {
 }
 
 // Adopt the asynchronous state copy of the last launch batch once it has landed.
+// Ranks of a sharded run keep the hint of the synchronous state reads only (which they make at
+// the same points of the loop), so that they pick the same graph variants at the same batches
+// and capture their collectives in lockstep.
 void refresh_hint(alll_ctx* c) {
-    if (!c->async_pending || hipEventQuery(c->ev_async) != hipSuccess) return;
+    if (!c->async_pending) return;
+    const hipError_t q = hipEventQuery(c->ev_async);
+    if (q != hipSuccess) {
+        // (hipErrorNotReady would stay the thread's last error and fail the next launch check)
+        if (q == hipErrorNotReady) (void)hipGetLastError();
+        return;
+    }
     c->hint_u = c->h_async->u_total;
     c->hint_iter = c->h_async->n_iter;
     c->hint_rounds = c->h_async->tail_rounds;
@@ -368,6 +364,7 @@ void refresh_hint(alll_ctx* c) {
 }
 
 int post_state_copy(alll_ctx* c) {
+    if (c->world > 1 || c->comm) return ALLL_OK;  // (sharded: synchronous hints only, refresh_hint)
     HIP_TRY(hipMemcpyAsync(c->h_async, c->b.state, sizeof(DevState), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipEventRecord(c->ev_async, c->stream));
     c->async_pending = true;
@@ -380,8 +377,7 @@ int enqueue_iteration(alll_ctx* c, hipEvent_t* marks, int variant) {
     // one GPU, bucketed round 0: the evaluation workgroups scatter their runs' claims
     // themselves (no k_bscatter), before the reduce (pre-reduce epoch)
     const bool xchg = c->world > 1 || c->comm;  // the clause-sharded exchange path
-    const bool scatter = variant == 1 && !xchg && c->hybrid && c->fuse_scatter && c->eval_wgs == 1 &&
-                         !c->b.rr_T && !getenv("ALLL_EVAL_GRID");
+    const bool scatter = variant == 1 && !xchg && c->hybrid && c->fuse_scatter && !c->b.rr_T;
     HIP_TRY(eval_launch(c, c->own_begin, c->own_end, true, scatter));
     if (marks) HIP_TRY(hipEventRecord(marks[1], s));
     if (xchg) {
@@ -398,33 +394,18 @@ int enqueue_iteration(alll_ctx* c, hipEvent_t* marks, int variant) {
     if (marks) HIP_TRY(hipEventRecord(marks[2], s));
     // the bucketed round 0 runs the reduce in an extra k_bscatter workgroup (one GPU, no hot
     // variables, not the round robin): one launch less
-    const bool fused = c->fuse_reduce && variant == 1 && !xchg && !c->b.rr_T;
+    const bool fused = variant == 1 && !xchg && !c->b.rr_T;
     if (!fused) HIP_TRY(launch_reduce(c->b, 0, s));
     if (c->b.rr_T) {
         LoopBuffers lb = c->b;
         if (variant == 1) lb.fp_max = c->fp_max_long;
         HIP_TRY(launch_rr_mis(c->cv, lb, s));
-    } else if (variant == 1 && c->dd) {
-        HIP_TRY(launch_lfmis_dd(c->cv, c->b, scatter, fused, s));
     } else {
         const uint32_t rounds = variant == 2 ? 1u : c->grid_rounds;
-        // rounds [0, f) as separate CLAIM / JOIN launches, then (f + 2 <= G) CLAIM(f), JOIN(r) +
-        // CLAIM(r + 1) fused for f <= r < G - 1, and the last JOIN
-        const uint32_t f = c->fuse_jc && c->fuse_jc + 2 <= rounds ? c->fuse_jc : rounds;
-        for (uint32_t r = 0; r < f; ++r) {
+        for (uint32_t r = 0; r < rounds; ++r) {
             if (r == 0 && variant == 1)
                 HIP_TRY(launch_round0_buckets(c->cv, c->b, rounds == 1, fused, scatter, s));
             else HIP_TRY(launch_round(c->cv, c->b, r, r + 1 == rounds, c->wave_round_min, s));
-        }
-        if (f < rounds) {
-            // after JOIN(f-1) the list is in stage[1]: CLAIM(f) -> stage[0], then the fused rounds
-            // alternate between the two, and the last JOIN hands the survivors to the tail
-            uint32_t* st2[2] = {c->b.stage[0], c->b.stage[1]};
-            HIP_TRY(launch_claim_only(c->cv, c->b, f, c->wave_round_min, st2[1], st2[0], s));
-            uint32_t cur = 0;
-            for (uint32_t r = f; r + 1 < rounds; ++r, cur ^= 1u)
-                HIP_TRY(launch_join_claim(c->cv, c->b, r, st2[cur], st2[cur ^ 1u], s));
-            HIP_TRY(launch_join_only(c->cv, c->b, rounds - 1, true, c->wave_round_min, st2[cur], st2[cur ^ 1u], s));
         }
         HIP_TRY(launch_tail(c->cv, c->b, rounds, s));
     }
@@ -640,21 +621,16 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     // at most HOT_MAX of the highest; flagged in bit 31 of every literal copy the device uses
     std::vector<uint8_t> is_hot;
     uint32_t n_hot = 0;
-    uint32_t max_deg = ~0u;  // most literals of one variable (unknown: ~0)
     if (L && prob->n_vars && prob->n_vars < (1u << 30)) {
         std::vector<uint32_t> deg(prob->n_vars, 0u);
         for (uint64_t j = 0; j < L; ++j) ++deg[prob->literals[j] >> 1];
-        max_deg = *std::max_element(deg.begin(), deg.end());
         const uint64_t thr = std::max<uint64_t>(1024, 32 * (L / prob->n_vars + 1));
         std::vector<std::pair<uint32_t, uint32_t>> hot;
         for (uint32_t v = 0; v < prob->n_vars; ++v)
             if (deg[v] >= thr) hot.push_back({deg[v], v});
         if (!hot.empty()) {
             std::sort(hot.rbegin(), hot.rend());
-            size_t hot_max = HOT_MAX;
-            if (const char* e = getenv("ALLL_HOT_MAX"))  // tuning: fewer hot variables (<= HOT_MAX)
-                hot_max = std::min<size_t>(HOT_MAX, (size_t)std::max(0, atoi(e)));
-            if (hot.size() > hot_max) hot.resize(hot_max);
+            if (hot.size() > HOT_MAX) hot.resize(HOT_MAX);
             is_hot.assign(prob->n_vars, 0);
             for (auto& h : hot) is_hot[h.second] = 1;
             n_hot = (uint32_t)hot.size();
@@ -690,10 +666,7 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     c->grid_rounds = opt.grid_rounds ? opt.grid_rounds : DEFAULT_GRID_ROUNDS;
     c->small_u = SMALL_U_DEFAULT;
     if (const char* e = getenv("ALLL_SMALL_U")) c->small_u = strtoull(e, nullptr, 10);  // tuning, tests
-    if (const char* e = getenv("ALLL_FUSE_REDUCE")) c->fuse_reduce = atoi(e) != 0;
     if (const char* e = getenv("ALLL_FUSE_SCATTER")) c->fuse_scatter = atoi(e) != 0;
-    // (A/B; at least 1: round 0's raw evaluation entries are unpacked only by k_claim / k_bscatter)
-    if (const char* e = getenv("ALLL_WAVE_ROUND_MIN")) c->wave_round_min = (uint32_t)std::max(1, atoi(e));
     auto bail = [&](int rc) { alll_destroy(c); return rc; };
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
         return bail(fail(ALLL_ERR_HIP, "hipStreamCreate failed"));
@@ -717,8 +690,7 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     LoopBuffers& b = c->b;
     b.n_vars = c->n_vars;
     b.n_words = (c->n_vars + 31) / 32;
-    if (const char* e = getenv("ALLL_EVAL_WGS")) c->eval_wgs = std::max(1, std::min(2, atoi(e)));  // tuning
-    b.win_words = LDS_WORDS / c->eval_wgs / 4 * 4;
+    b.win_words = LDS_WORDS;
     if (const char* e = getenv("ALLL_WIN_WORDS"))  // tests: small windows on small instances
         b.win_words = std::max<uint32_t>(16, std::min<uint32_t>(b.win_words, (uint32_t)std::max(0, atoi(e)))) / 8 * 8;
     b.n_cu = (uint32_t)c->n_cu;
@@ -750,17 +722,13 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
         b.rr_sets = d_sets;
         b.rr_T = rr_T;
         b.rr_k = (rr_width >= 1 && rr_width <= 8) ? (uint32_t)rr_width : 0u;
-        // the batches across workgroups (one per lane group, at most 64): ALLL_RR_MW=0 keeps the
-        // one-workgroup kernel
-        uint32_t mw = std::min<uint32_t>(rr_T, 64);
-        if (const char* e = getenv("ALLL_RR_MW")) mw = atoi(e) > 0 ? std::min<uint32_t>(rr_T, std::min(64, atoi(e))) : 0u;
-        if (mw) {
-            if ((rc = dalloc(c, &b.rr_ctl, RR_MW_CTL_WORDS))) return bail(rc);
-            if ((rc = dalloc(c, &b.rr_gkey, RR_MW_GH))) return bail(rc);
-            if ((rc = dalloc(c, &b.rr_gmin, RR_MW_GH, 0xFF))) return bail(rc);
-            if ((rc = dalloc(c, &b.rr_ptr, rr_T))) return bail(rc);
-            if ((rc = dalloc(c, &b.rr_end, rr_T))) return bail(rc);
-        }
+        // the batch kernel (fallback of the fixpoint): one workgroup per lane group, at most 64
+        const uint32_t mw = std::min<uint32_t>(rr_T, 64);
+        if ((rc = dalloc(c, &b.rr_ctl, RR_MW_CTL_WORDS))) return bail(rc);
+        if ((rc = dalloc(c, &b.rr_gkey, RR_MW_GH))) return bail(rc);
+        if ((rc = dalloc(c, &b.rr_gmin, RR_MW_GH, 0xFF))) return bail(rc);
+        if ((rc = dalloc(c, &b.rr_ptr, rr_T))) return bail(rc);
+        if ((rc = dalloc(c, &b.rr_end, rr_T))) return bail(rc);
         b.rr_mw = mw;
         // the fixpoint passes: keys {epoch | turn | entry} need >= 10 epoch
         // bits; ALLL_RR_FP=0 leaves every iteration to the batch kernels, ALLL_RR_FP_MAX sets the
@@ -818,16 +786,13 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     b.vmix_mul = 1u;
     b.vmix_mask = 0xFFFFFFFFu;
     uint64_t vrange = c->n_vars;  // owner slots / bucketed variable keys
-    if (n_hot && !getenv("ALLL_NO_VMIX")) {
+    if (n_hot) {
         vrange = 1024;
         while (vrange < c->n_vars) vrange <<= 1;
         b.vmix_mul = 0x9E3779B1u;
         b.vmix_mask = (uint32_t)(vrange - 1);
     }
-    if (const char* e = getenv("ALLL_FUSE_JC")) c->fuse_jc = (uint32_t)std::max(0, atoi(e));
-    if (fixed_k <= 0) c->fuse_jc = 0;
-    if ((rc = dalloc(c, &b.owner, (size_t)vrange * (c->fuse_jc ? 2 : 1), 0xFF))) return bail(rc);
-    b.owner_alt = c->fuse_jc ? vrange : 0;
+    if ((rc = dalloc(c, &b.owner, (size_t)vrange, 0xFF))) return bail(rc);
     if ((rc = dalloc(c, &b.cover, (size_t)b.n_words * 32))) return bail(rc);  // whole words, zero-padded
     if ((rc = dalloc(c, &b.tile_stats, 2 * (size_t)n_tiles))) return bail(rc);
     if ((rc = dalloc(c, &b.delta, b.n_words))) return bail(rc);
@@ -845,30 +810,14 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
         if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) == hipSuccess && khz > 0)
             c->wall_khz = khz;
     }
-    if (getenv("ALLL_DEBUG_PHASES")) {  // diagnostics only
-        if ((rc = dalloc(c, &b.kdbg, (size_t)DBG_KERNELS * DBG_BLOCKS * DBG_FIELDS))) return bail(rc);
-    }
     // ---- bucketed LFMIS round 0 (fixed width): one bucket per CU when a bucket's minima fit
     // in LDS (else ~300-1000 power-of-2 buckets), runs of up to 16 tiles
     if (fixed_k > 0 && !(opt.flags & ALLL_FLAG_ATOMIC_CLAIMS) && n_tiles > 0 && c->n_vars > 0) {
         uint32_t shift = BKT_SHIFT_MIN;
         while (shift < BKT_SHIFT_MAX && (vrange >> shift) > 384) ++shift;
-        // (one bucket per CU: the dependency-driven LFMIS sorts a bucket's pairs in one sweep of
-        // 12288 when its width is at most 10240 variables; ALLL_DD_BKT_PER_CU to tune)
-        uint32_t per_cu = 1;
-        {
-            bool zid = true;
-            for (int i = 0; i < 128; ++i) zid &= opt.comm_id[i] == 0;
-            const char* e = getenv("ALLL_DD");
-            if (c->world == 1 && zid && !n_hot && !opt.stream_batch && !rr_T && e && atoi(e) != 0) {
-                if (const char* e2 = getenv("ALLL_DD_BKT_PER_CU")) per_cu = (uint32_t)std::max(1, atoi(e2));
-            }
-        }
-        uint64_t width = (vrange + (uint64_t)c->n_cu * per_cu - 1) / ((uint64_t)c->n_cu * per_cu);
+        uint64_t width = (vrange + (uint64_t)c->n_cu - 1) / (uint64_t)c->n_cu;
         width = std::max<uint64_t>(width, 1u << BKT_SHIFT_MIN);
-        if (width > (1u << BKT_SHIFT_MAX) || getenv("ALLL_BKT_POW2")) width = 1u << shift;
-        if (const char* e = getenv("ALLL_BKT_SHIFT"))  // tuning experiments
-            width = 1u << std::min<uint32_t>(BKT_SHIFT_MAX, std::max<uint32_t>(BKT_SHIFT_MIN, (uint32_t)atoi(e)));
+        if (width > (1u << BKT_SHIFT_MAX)) width = 1u << shift;
         const uint64_t nb = (vrange + width - 1) / width;
         // skewed pair load (a literal distribution whose hubs are not all flagged hot): the
         // fullest bucket's workgroup would serialise the round; such instances keep the atomic
@@ -924,29 +873,6 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
             // below this many violated clauses the atomic round 0 is cheaper (fixed costs)
             c->bucket_min_u = std::max<uint64_t>(65536, m / 64);
             if (const char* e = getenv("ALLL_BUCKET_MIN_U")) c->bucket_min_u = strtoull(e, nullptr, 10);
-            // Dependency-driven LFMIS in place of the bucketed rounds: one GPU
-            // without an exchange, clause-order priorities, no hot variables; every run's decide
-            // workgroup resident at once (one per CU), the runs' segment table in one batch, the
-            // LDS of both kernels within a CU's, and every variable's claimants within one sort
-            // piece.  ALLL_DD=0 keeps the round-synchronous LFMIS (tests, A/B).
-            bool zero_id = true;
-            for (int i = 0; i < 128; ++i) zero_id &= opt.comm_id[i] == 0;
-            const uint32_t run_cap32 = b.run_tiles * TILE * (uint32_t)fixed_k;
-            c->dd = c->world == 1 && zero_id && !n_hot && !opt.stream_batch && !rr_T &&
-                    b.n_runs <= (uint32_t)c->n_cu && b.n_runs <= BKT_RUN_BATCH && b.run_tiles <= RUN_TILES_MAX &&
-                    dd_sort_lds(b) <= 160u * 1024 - 512 && dd_sort_general_lds(b) <= 160u * 1024 - 512 && dd_decide_lds(b, (uint32_t)fixed_k) <= 160u * 1024 - 1024 &&
-                    max_deg <= DDS_CAP && (uint64_t)b.n_runs * run_cap32 * 4 < (1ull << 31);  // (buffer offsets)
-            // (opt-in: measured slower than the round-synchronous LFMIS at M)
-            {
-                const char* e = getenv("ALLL_DD");
-                c->dd = c->dd && e && atoi(e) != 0;
-            }
-            if (c->dd) {
-                if ((rc = dalloc(c, &b.dd_msg, (size_t)b.n_runs * run_cap32))) return bail(rc);
-                b.dd_senders = 1;
-                if (const char* e = getenv("ALLL_DD_SENDERS")) b.dd_senders = atoi(e) != 0;  // A/B
-                c->bucket_min_u = 0;  // three launches at any violated count (no small-set variants)
-            }
         }
     }
     // ---- clause storage allocations, then drain the zero-fills before synchronous uploads
@@ -976,7 +902,7 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
             // skewed instances need more rounds before the leftovers are few enough for
             // the single-workgroup tail (power-law 3-SAT at 10M clauses: 10 rounds)
             if (!opt.grid_rounds) c->grid_rounds = SKEWED_GRID_ROUNDS;
-            if (!getenv("ALLL_WAVE_ROUND_MIN")) c->wave_round_min = WAVE_ROUND_MIN_HOT;
+            c->wave_round_min = WAVE_ROUND_MIN_HOT;
         }
         const uint32_t* src = flagged.empty() ? prob->literals : flagged.data();
         if (L && hipMemcpy(d_lits, src, L * 4, hipMemcpyHostToDevice) != hipSuccess)
@@ -1127,7 +1053,7 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
         // ALLL_FLAG_NO_RANGED keeps the clause-order CSR evaluation like GENERIC_CSR)
         const bool ragged = m && !rr_T && !opt.stream_batch &&
                             !(opt.flags & (ALLL_FLAG_GENERIC_CSR | ALLL_FLAG_NO_RANGED)) &&
-                            b.n_words < (1u << 25) && !getenv("ALLL_NO_RAGGED");
+                            b.n_words < (1u << 25);
         if (ragged && (rc = build_ragged(c, prob))) return bail(rc);
     }
 
@@ -1444,17 +1370,6 @@ int alll_loop_times(alll_ctx* c, uint64_t first_iter, uint64_t n_iters, alll_pha
     if (ne) { out->eval_ms = se / ne; out->exchange_ms = sx / ne; }
     if (nm) out->mis_ms = sm / nm;
     if (nt) { out->resample_ms = sr / nt; out->total_ms = st / nt; }
-    return ALLL_OK;
-}
-
-int alll_debug_phases(alll_ctx* c, uint64_t* out, uint64_t n, int* wall_khz) {
-    if (!c || !out) return fail(ALLL_ERR_INVALID_ARG, "null argument");
-    if (!c->b.kdbg) return fail(ALLL_ERR_INVALID_ARG, "created without ALLL_DEBUG_PHASES in the environment");
-    HIP_TRY(hipSetDevice(c->device));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    n = std::min<uint64_t>(n, (uint64_t)DBG_KERNELS * DBG_BLOCKS * DBG_FIELDS);
-    HIP_TRY(hipMemcpy(out, c->b.kdbg, n * 8, hipMemcpyDeviceToHost));
-    if (wall_khz) *wall_khz = c->wall_khz;
     return ALLL_OK;
 }
 

@@ -53,6 +53,15 @@ def generate_mixed(gen_seed: int, n_vars: int, n_clauses: int, w_min: int, w_max
     return offs, (v << np.uint32(1)) | sgn
 
 
+def assignment_digest(words) -> str:
+    """64-bit FNV-1a over the bit-packed assignment's uint32 words (one xor-multiply step per
+    word), as 16 hex digits: the trajectory digest of tests/golden/bench_trajectory.json."""
+    h = 0xCBF29CE484222325
+    for w in np.ascontiguousarray(words, np.uint32).tolist():
+        h = ((h ^ w) * 0x100000001B3) & 0xFFFFFFFFFFFFFFFF
+    return f"{h:016x}"
+
+
 def parse_dimacs(text: bytes):
     """DIMACS text -> (n_vars, offsets, literals) with the reference loader semantics."""
     L = N.lib()

@@ -40,6 +40,7 @@ CONFIGS = {
     "R": (1_000_000, 4_000_000, (2, 12), 0, "mixed widths 2-12 (uniform), 1M vars / 4M clauses"),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+TRAJECTORY_JSON = os.path.join(ROOT, "tests", "golden", "bench_trajectory.json")
 
 
 def log(*a):
@@ -147,6 +148,37 @@ def cpu_baseline(cfg, budget_s):
             "sample": f"oracle serial restatement, {it} iterations on n={ns}, m={ms}; host {cpu_model()}"}
 
 
+def trajectory_check(cfg, T, st, words):
+    """Bit-exactness of the run, checked outside the timed region against the committed data
+    file tests/golden/bench_trajectory.json (oracle trajectories of the same instance and seed,
+    written by tests/golden/make_bench_trajectory.py; no oracle code runs here): after the
+    iteration the GPU reached, the violated count, the cumulative MIS-size and resample counts
+    and a 64-bit FNV-1a digest of the bit-packed assignment."""
+    from alllsatisfiabilitysolver_amd import assignment_digest
+
+    it = int(st["n_iterations"])
+    out = {"iters": it, "n_threads": T, "match": None,
+           "source": "tests/golden/bench_trajectory.json (oracle, SATInstance.h:217-320)"}
+    try:
+        tj = json.load(open(TRAJECTORY_JSON))["trajectories"]
+    except (OSError, ValueError) as e:
+        out["reason"] = f"no trajectory file: {e}"
+        return out
+    tr = tj.get(f"{cfg}_T{T}")
+    if tr is None:
+        out["reason"] = f"no committed trajectory for config {cfg} with n_threads {T}"
+        return out
+    row = next((r for r in tr["rows"] if r[0] == it), None)
+    if row is None:
+        out["reason"] = f"iteration {it} lies beyond the committed {len(tr['rows'])} iterations"
+        return out
+    got = [it, int(st["n_violated"]), int(st["sum_mis_size"]), int(st["n_resamples"]), assignment_digest(words)]
+    out["expected"] = dict(zip(("n_violated", "sum_mis_size", "n_resamples", "digest"), row[1:]))
+    out["got"] = dict(zip(("n_violated", "sum_mis_size", "n_resamples", "digest"), got[1:]))
+    out["match"] = got == list(row)
+    return out
+
+
 def rr_line(args, n, m, k, kind, Solver, generate_ksat, device, warmup=2, steps=10):
     """GPU resample loop with the reference's n_threads = T round-robin MIS, T = the CPU
     baseline's thread count."""
@@ -171,8 +203,9 @@ def rr_line(args, n, m, k, kind, Solver, generate_ksat, device, warmup=2, steps=
         torch.cuda.synchronize(device)
         dt = time.perf_counter() - t0
         st = r.stats()
+        traj = trajectory_check(args.config, T, st, r.assignment_words())
     done = st["n_iterations"] - it0
-    return {"value": m * done / dt if done else None, "unit": "clause-evals/s", "n_threads": T,
+    return {"trajectory_check": traj, "value": m * done / dt if done else None, "unit": "clause-evals/s", "n_threads": T,
             "resample_iters_per_s": done / dt if done else None, "ms_per_step": dt * 1e3 / done if done else None,
             "steps": done, "warmup": warmup, "passes_last_iter": st["lfmis_tail_rounds"],
             "mis": "round robin over T clause chunks (SATInstance.h:414-447), as the cpu_baseline's -p T path"}
@@ -319,6 +352,7 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     st = s.stats()
+    traj = trajectory_check(args.config, 1, st, s.assignment_words()) if rank == 0 else None
     # the timed loop must have replayed the captured graphs; an eager fallback (a capture or an
     # RCCL call under capture that failed) would time a different launch pattern unannounced
     graphs, graph_note = s.uses_graphs()
@@ -384,6 +418,7 @@ def main():
                        "exchange": f"{args.exchange}/{exchange_impl}" if world > 1 or comm_id else "none",
                        "parallelism": f"clause-shard x{world}"},
             "value_kind": vkind,
+            "trajectory_check": traj,
             "graphs": graphs,
             "graph_note": graph_note or None,
             "create_s_max_over_ranks": create_max,
@@ -433,6 +468,12 @@ def main():
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+    bad = [name for name, t in (("T=1 loop", traj), ("round robin", (out or {}).get("gpu_same_mis_as_cpu_baseline", {})
+                                                                 .get("trajectory_check")))
+           if t and t.get("match") is False]
+    if rank == 0 and bad:
+        log(f"[rank 0] FAIL: the {' and '.join(bad)} left a state that differs from the committed oracle trajectory")
+        sys.exit(4)
     if graphs_expected and not graphs:
         log(f"[rank {rank}] FAIL: the loop fell back to eager launches ({graph_note}); the line above "
             f"does not time the graph-replayed loop")

@@ -190,10 +190,6 @@ int alll_profile(alll_ctx* ctx, uint64_t n_iters, alll_phase_times* out);
  * tail end to the next evaluation start; total_ms = evaluation start to the next one.  Only
  * the last 4096 iterations are kept.  (No reference counterpart: measurement) */
 int alll_loop_times(alll_ctx* ctx, uint64_t first_iter, uint64_t n_iters, alll_phase_times* out);
-/* Diagnostics: per-workgroup phase stamps (device wall clock, rate *wall_khz kHz) of the
- * instrumented LFMIS kernels in the last iteration, [kernel][workgroup 0..8191][phase 0..7];
- * only when the context was created with ALLL_DEBUG_PHASES set in the environment. */
-int alll_debug_phases(alll_ctx* ctx, uint64_t* out, uint64_t n, int* wall_khz);
 /* Block the host until all work queued on the solver's stream finished. */
 int alll_synchronize(alll_ctx* ctx);
 /* Bytes the evaluation kernel reads/writes per pass (algorithmic). */

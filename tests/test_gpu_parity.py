@@ -26,24 +26,13 @@ T1_FIXTURES = sorted(p for p in glob.glob(os.path.join(GOLDEN, "*_T1.npz")))
 LAYOUTS = {"hybrid": (0, {}), "fixed": (1 << 3, {}), "csr": (1 << 2, {}), "atomic_claims": (1 << 5, {}),
            "buckets": (0, {"ALLL_BUCKET_MIN_U": "0"}), "windows": (0, {"ALLL_EVAL_WINDOWS": "1"}),
            "positions": (0, {"ALLL_PACKED_IDS": "0"}),
-           # hot-variable instances without the owner/bucket spread (identity vmix)
-           "no_vmix": (0, {"ALLL_NO_VMIX": "1", "ALLL_BUCKET_MIN_U": "0"}),
            # bucketed round 0 scattered by the evaluation workgroups (no k_bscatter)
            "scatter": (0, {"ALLL_FUSE_SCATTER": "1", "ALLL_BUCKET_MIN_U": "0"}),
-           # ... and with the separate k_reduce
-           "no_fusion": (0, {"ALLL_FUSE_SCATTER": "0", "ALLL_FUSE_REDUCE": "0", "ALLL_BUCKET_MIN_U": "0"}),
            # the large-instance evaluation (non-temporal literal loads, exec-masked L2 lookups)
            # with windows
            "nt_windows": (0, {"ALLL_EVAL_NT": "1", "ALLL_EVAL_WINDOWS": "1"}),
            # one grid round + the tail in every iteration after the first (variant 2), and never
            "tail_all": (0, {"ALLL_SMALL_U": str(1 << 62)}), "no_small_u": (0, {"ALLL_SMALL_U": "0"}),
-           # the dependency-driven LFMIS (opt-in) instead of the round-synchronous one
-           "dd": (0, {"ALLL_DD": "1"}),
-           "dd_scatter": (0, {"ALLL_DD": "1", "ALLL_FUSE_SCATTER": "1"}),
-           "dd_no_senders": (0, {"ALLL_DD": "1", "ALLL_DD_SENDERS": "0"}),
-           # JOIN(r) and CLAIM(r+1) fused in one launch (k_wjc, opt-in) from round 1 / round 2 on
-           "fuse_jc": (0, {"ALLL_FUSE_JC": "1"}),
-           "fuse_jc2_atomic": (1 << 5, {"ALLL_FUSE_JC": "2"}),
            # many small LDS windows (64 words: 2048 variables; the C4 layout on small instances),
            # with the cached and with the non-temporal (C4) evaluation
            "small_windows": (0, {"ALLL_EVAL_WINDOWS": "1", "ALLL_WIN_WORDS": "64"}),
@@ -262,37 +251,32 @@ def test_empty_instance(gpu):
         assert st["solved"] == 1 and st["n_iterations"] == 1 and st["n_resamples"] == 0
 
 
-@pytest.mark.parametrize("fuse_jc", ["0", "1", "2"])
 @pytest.mark.parametrize("grid_rounds", [1, 2, 3, 8])
-def test_grid_round_split_is_invisible(gpu, oracle_mod, grid_rounds, fuse_jc, monkeypatch):
+def test_grid_round_split_is_invisible(gpu, oracle_mod, grid_rounds, monkeypatch):
     """The split between full-grid LFMIS rounds and the single-workgroup tail changes
-    nothing, and neither do the fused JOIN(r)+CLAIM(r+1) launches (ALLL_FUSE_JC=f: from round
-    f on): same trajectory as the oracle."""
+    nothing: same trajectory as the oracle."""
     from alllsatisfiabilitysolver_amd import Solver
 
     n, offs, lits = instances()["k5_multi_tile"]
     st_o, A_o, rows = oracle_mod.solve(n, offs, lits, 77, max_iters=12, trace=True)
     monkeypatch.setenv("ALLL_BUCKET_MIN_U", "0")  # round 0 bucketed (incl. last-round hand-off at G=1)
-    monkeypatch.setenv("ALLL_DD", "0")  # (the grid rounds exist only in the round-synchronous LFMIS)
-    monkeypatch.setenv("ALLL_FUSE_JC", fuse_jc)
     with Solver(n, offs, lits, seed=77, max_iters=12, grid_rounds=grid_rounds) as s:
         st = s.solve()
         assert st["n_resamples"] == st_o["n_resamples"]
         np.testing.assert_array_equal(s.assignment_words(), A_o)
 
 
-@pytest.mark.parametrize("fuse", ["0", "1"])
-def test_fused_reduce_is_invisible(gpu, oracle_mod, fuse, monkeypatch):
-    """The loop's reduce runs in an extra workgroup of the bucketed round 0 (default) or as its
-    own kernel (ALLL_FUSE_REDUCE=0): same trajectory, statistics, stop and cap as the oracle."""
+@pytest.mark.parametrize("bucket_min_u", ["0", str(1 << 62)])
+def test_fused_reduce_is_invisible(gpu, oracle_mod, bucket_min_u, monkeypatch):
+    """The loop's reduce runs in an extra workgroup of the bucketed round 0 or as its own kernel
+    (atomic round 0): same trajectory, statistics, stop and cap as the oracle."""
     from alllsatisfiabilitysolver_amd import Solver, generate_ksat
 
     n = 20000
     offs, lits = generate_ksat(3, n, 2 * n, 3, 0)  # ratio 2 over 10 tiles: converges
     st_o, A_o, rows = oracle_mod.solve(n, offs, lits, 5, max_iters=400, trace=True)
     assert st_o["solved"] == 1
-    monkeypatch.setenv("ALLL_FUSE_REDUCE", fuse)
-    monkeypatch.setenv("ALLL_BUCKET_MIN_U", "0")  # the bucketed round 0 in every iteration
+    monkeypatch.setenv("ALLL_BUCKET_MIN_U", bucket_min_u)  # bucketed round 0 in every iteration, or never
     with Solver(n, offs, lits, seed=5, max_iters=400) as s:
         for it, nu, nm, dres, A_after in rows[:6]:
             s.run(1)
@@ -330,24 +314,16 @@ BIG = {
     "C5_atomic_round0": (2_500_000, 10_000_000, 3, 1, {"ALLL_BUCKET_MIN_U": str(1 << 62)}),
     "C5_scatter": (2_500_000, 10_000_000, 3, 1, {"ALLL_FUSE_SCATTER": "1"}),
     "M_scatter": (2_500_000, 10_000_000, 3, 0, {"ALLL_FUSE_SCATTER": "1"}),
-    "C5_no_fusion": (2_500_000, 10_000_000, 3, 1, {"ALLL_FUSE_SCATTER": "0", "ALLL_FUSE_REDUCE": "0"}),
     "W_3sat_4Mvars": (4_000_000, 2_000_000, 3, 0),  # 4 LDS blocks of variables: windowed eval
     "M_no_windows": (2_500_000, 10_000_000, 3, 0, {"ALLL_EVAL_WINDOWS": "0"}),
     "M_positions": (2_500_000, 10_000_000, 3, 0, {"ALLL_PACKED_IDS": "0"}),  # perm translation
-    # 611 power-of-2 buckets (more than CUs): the narrow k_bresolve, two workgroups per CU
-    "M_pow2_buckets": (2_500_000, 10_000_000, 3, 0, {"ALLL_BKT_SHIFT": "12"}),
     # C4 (the north star's 8-GPU instance) on one GPU: 27-bit clause ids do not fit in the
     # literals' spare bits (26-bit literals), so evaluation positions + perm; 26 LDS windows
     "C4_3sat_128M": (32_000_000, 128_000_000, 3, 0),
     # M through the large-instance evaluation variant (C4 takes it by default)
     "M_nt": (2_500_000, 10_000_000, 3, 0, {"ALLL_EVAL_NT": "1"}),
-    # the dependency-driven LFMIS at full size (opt-in; first iteration through k_bsort_general)
-    "M_dd": (2_500_000, 10_000_000, 3, 0, {"ALLL_DD": "1"}),
-    "C2_dd": (1_000_000, 4_000_000, 3, 0, {"ALLL_DD": "1"}),
-    "C3_dd": (4_000_000, 6_000_000, 8, 0, {"ALLL_DD": "1"}),
     # ragged widths 2-12 (bench config R): the chunk-transposed ragged evaluation, CSR LFMIS
     "R_mixed_4M": (1_000_000, 4_000_000, (2, 12), 0),
-    "R_mixed_4M_csr": (1_000_000, 4_000_000, (2, 12), 0, {"ALLL_NO_RAGGED": "1"}),
     # more variables than one LDS window: windowed ragged evaluation
     "R_mixed_windows": (4_000_000, 2_000_000, (1, 9), 0),
 }

@@ -13,8 +13,8 @@ caller's vector<ClauseArray*>), bit-exact:
 
 Every test runs with each way of deciding the MIS: the fixpoint passes (default, DESIGN.md
 §4.3.2; also in the long graph variant), the same passes capped at one or two per iteration (ALLL_RR_FP_MAX, so that most
-iterations fall back to the batch kernel mid-run), and the batch kernels alone (ALLL_RR_FP=0):
-across workgroups (k_rr_mw) and in one workgroup (k_rr_mis, ALLL_RR_MW=0).
+iterations fall back to the batch kernel mid-run), and the batch kernel alone (k_rr_mw,
+ALLL_RR_FP=0).
 """
 import glob
 import os
@@ -38,18 +38,16 @@ def gpu(native):
     return True
 
 
-@pytest.fixture(params=["fp", "fp_long", "fp_cap1", "fp_cap2", "mw", "one"], autouse=True)
+@pytest.fixture(params=["fp", "fp_long", "fp_cap1", "fp_cap2", "mw"], autouse=True)
 def rr_kernel(request, monkeypatch):
-    for k in ("ALLL_RR_MW", "ALLL_RR_FP", "ALLL_RR_FP_MAX", "ALLL_RR_FP_LONG_AT"):
+    for k in ("ALLL_RR_FP", "ALLL_RR_FP_MAX", "ALLL_RR_FP_LONG_AT"):
         monkeypatch.delenv(k, raising=False)
     if request.param == "fp_long":  # the long graph variant (48 passes) from the second launch on
         monkeypatch.setenv("ALLL_RR_FP_LONG_AT", "0")
     elif request.param.startswith("fp_cap"):
         monkeypatch.setenv("ALLL_RR_FP_MAX", request.param[-1])
-    elif request.param in ("mw", "one"):
+    elif request.param == "mw":
         monkeypatch.setenv("ALLL_RR_FP", "0")
-        if request.param == "one":
-            monkeypatch.setenv("ALLL_RR_MW", "0")
     return request.param
 
 
@@ -251,3 +249,23 @@ def test_rr_full_size_c2_bit_exact(gpu, oracle_mod, rr_kernel, T):
             assert after["sum_mis_size"] - before["sum_mis_size"] == nm, f"iter {it}"
             assert after["n_resamples"] - before["n_resamples"] == dres, f"iter {it}"
             np.testing.assert_array_equal(s.assignment_words(), A_after, err_msg=f"A after iter {it}")
+
+
+def test_rr_back_to_back_runs_without_sync(gpu, oracle_mod, monkeypatch):
+    """Several run(1) calls with no stats() or synchronisation in between (the asynchronous
+    state copy of one batch is still in flight when the next picks its graph variant), long
+    graph variant from the second launch on: the same trajectory as the oracle."""
+    from alllsatisfiabilitysolver_amd import Solver, generate_ksat
+
+    monkeypatch.setenv("ALLL_RR_FP_LONG_AT", "0")
+    n, m, T, seed = 6000, 24000, 5, 9
+    offs, lits = generate_ksat(4, n, m, 3, 0)
+    st_o, A_o, rows = oracle_mod.solve(n, offs, lits, seed, max_iters=13, trace=True, T=T)
+    with Solver(n, offs, lits, seed=seed, n_threads=T) as s:
+        for _ in range(12):
+            s.run(1, sync=False)
+        s.synchronize()
+        st = s.stats()
+        assert st["n_iterations"] == 12
+        assert st["n_resamples"] == sum(r[3] for r in rows)
+        np.testing.assert_array_equal(s.assignment_words(), rows[-1][4])

@@ -309,3 +309,46 @@ def test_oracle_solve_stream_semantics(oracle_mod):
     lit = np.array([0 if (A0[0] & 1) else 1], np.uint32)  # the literal of variable 0 that is true
     st, A, rows = o.solve_stream(4, offs1, lit, 2, 8, trace=True)
     assert st == {**st, "n_iterations": 1, "n_resamples": 0, "avg_mis_size": 0, "solved": 1}
+
+
+def test_bench_trajectory_file_regenerates(oracle_mod):
+    """tests/golden/bench_trajectory.json (what bench.py checks its final state against) is the
+    oracle's trajectory of the bench instances: recompute the first iterations of every entry."""
+    import subprocess
+    import sys
+
+    script = os.path.join(os.path.dirname(__file__), "golden", "make_bench_trajectory.py")
+    r = subprocess.run([sys.executable, script, "--check", "4"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_bench_trajectory_check_logic():
+    """bench.trajectory_check: match, mismatch and out-of-range reporting (no GPU)."""
+    import json
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(__file__)))
+    import bench
+
+    tr = json.load(open(bench.TRAJECTORY_JSON))["trajectories"]["C2_T1"]["rows"]
+    it, nu, mis, res, dig = tr[9]
+    st = {"n_iterations": it, "n_violated": nu, "sum_mis_size": mis, "n_resamples": res}
+
+    class W:  # assignment words whose digest is the committed one
+        pass
+
+    import alllsatisfiabilitysolver_amd.solver as S
+
+    orig = S.assignment_digest
+    try:
+        S.assignment_digest = lambda w: dig
+        import alllsatisfiabilitysolver_amd as pkg
+
+        pkg.assignment_digest = S.assignment_digest
+        assert bench.trajectory_check("C2", 1, st, None)["match"] is True
+        assert bench.trajectory_check("C2", 1, {**st, "n_resamples": res + 1}, None)["match"] is False
+        assert bench.trajectory_check("C2", 1, {**st, "n_iterations": 10_000}, None)["match"] is None
+        assert bench.trajectory_check("C3", 1, st, None)["match"] is None
+    finally:
+        S.assignment_digest = orig
+        pkg.assignment_digest = orig

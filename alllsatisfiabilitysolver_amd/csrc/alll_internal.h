@@ -168,6 +168,8 @@ struct LoopBuffers {
     // (mul 1, mask ~0) otherwise.
     uint32_t vmix_mul;
     uint32_t vmix_mask;
+    uint32_t vmix_inv;          // vmix_mul's inverse mod 2^32 (vunmix)
+    uint32_t bkt_span;          // vmix slots [0, bkt_span) that the buckets cover (round robin)
     uint32_t bkt_width;         // bucket = vmix(variable) / bkt_width (<= 2^BKT_SHIFT_MAX)
     uint32_t bkt_magic;         // floor(2^32 / bkt_width): bucket by multiply-high
     uint32_t n_cu;              // compute units of the device
@@ -183,6 +185,9 @@ struct LoopBuffers {
     uint64_t stream_pinv;       // inverse of P mod m (P = 9223372036854775783, ClauseGenerator.h:110)
     // round-robin MIS (T = rr_T > 1 clause chunks, SATInstance.h:414-447; CSR layout)
     uint32_t* rr_u;             // violated clauses in clause order: m scan entries of 12 words
+    uint8_t* rr_flag;           // fixed width (hybrid evaluation): m clause-order violated flags
+                                // (k_rr_mark sets, k_rr_entries clears); nullptr = CSR bitmask
+    uint32_t* rr_tcnt;          // fixed width: violated clauses per clause-order tile
     const uint32_t* rr_sets;    // rr_T + 1 chunk starts (clause ids)
     uint32_t rr_T;
     uint32_t rr_k;              // common clause width (<= 8), 0 = ragged
@@ -203,16 +208,20 @@ struct LoopBuffers {
     uint32_t* fp_list;          // 2 x m: round lists per tile of FP_B entries (JOIN output, CLAIM output)
     uint32_t* fp_tcnt;          // 2 FP_G x tiles: list lengths per round and tile
     unsigned long long* fp_owner; // n_vars claim keys {epoch | turn | entry}, reset every iteration
-    uint32_t* fp_own0;          // n_vars: round-0 winner (entry) of every shared variable
+    uint32_t* fp_own0;          // n_vars: round-0 winner (entry) of every claimed variable (single
+                                // claimants: for the whole iteration, k_fp_bbuild; shared: per pass)
     uint8_t* fp_cov;            // n_vars: serial of the pass whose pick covers the variable (cleared per iteration)
-    uint32_t* fp_deg;           // n_vars: violated claimants this iteration (slots 0..7 of their clauses)
-    uint32_t* fp_deg_hi;        // n_vars: the same from slots past 8 (wide clauses)
-    uint32_t* fp_rank;          // 8 per scan entry: slot j's place in its variable's claimant list
-    uint8_t* fp_sole;           // per scan entry: bit j = slot j's variable has no other claimant
-    uint32_t* fp_voff;          // n_vars + 1: list range of every variable (shared variables only)
-    uint32_t* fp_vlist;         // violated claimants of the shared variables (scan entries)
-    uint32_t* fp_vblk;          // block sums / offsets of the list lengths
-    uint32_t* fp_heavy;         // variables whose claimant list is long (one wave each in round 0)
+    // per-iteration claimant lists (k_fp_bscatter / k_fp_bbuild): variable v's violated
+    // claimants are fp_vlist[fp_soff[v] ..), fp_soff = prefix of the static literal counts
+    const uint32_t* fp_soff;    // n_vars + 1
+    const uint32_t* fp_breg;    // n_bkt + 1: static pair region of every bucket (its literal count)
+    unsigned long long* fp_pairs;  // L pairs {entry, variable} grouped by bucket
+    uint32_t* fp_bfill;         // n_bkt: pairs in each bucket's region (this iteration)
+    uint32_t* fp_one;           // bit vmix(v): v has exactly one violated claimant this iteration
+    uint4* fp_sv;               // per bucket (bkt_width slots): shared variables {list start, count, v}
+    uint32_t* fp_sbcnt;         // n_bkt: shared variables per bucket
+    uint32_t* fp_vlist;         // violated claimants per variable (scan entries)
+    uint32_t* fp_heavy;         // uint4 {v, start, end} segments of long lists (a wave each in round 0)
     uint32_t* fp_blk;           // 2 x blocks: pick counts, then their exclusive prefix
     uint32_t* fp_sf;            // T + 1: first scan entry of every set (entries past the last: nu)
     uint32_t* fp_bnd;           // T + 1: picks before the set's first entry inside its block
@@ -227,6 +236,9 @@ struct LoopBuffers {
     uint32_t n_tiles;       // tiles covering [0, m)
     uint64_t seed;
 };
+
+// LDS of k_fp_bbuild for a bucket of `width` variables: counters, list starts, first claimants
+inline size_t fp_bbuild_lds_bytes(uint32_t width) { return (size_t)12 * width + 16; }
 
 // Launchers (alll_kernels.hip).  All asynchronous on `s`.
 hipError_t launch_init_assignment(const LoopBuffers& b, hipStream_t s);

@@ -932,6 +932,8 @@ __global__ __launch_bounds__(1024) void k_reduce(LoopBuffers b, int mode) {
 // LDS hash table first: one global atomic per hot variable per workgroup (power-law hubs).
 // Owner slot / bucket key of variable v (LoopBuffers::vmix_mul, identity unless skewed).
 __device__ __forceinline__ uint32_t vmix(const LoopBuffers& b, uint32_t v) { return (v * b.vmix_mul) & b.vmix_mask; }
+// inverse of vmix on [0, vmix_mask] (vmix_inv: the multiplier's inverse mod 2^k)
+__device__ __forceinline__ uint32_t vunmix(const LoopBuffers& b, uint32_t x) { return (x * b.vmix_inv) & b.vmix_mask; }
 
 struct HotTable {
     uint32_t* k;
@@ -2097,36 +2099,124 @@ struct RREnt {
 };
 static_assert(sizeof(RREnt) == 16 + 4 * RR_KE, "scan entry = header + RR_KE variables");
 
+// Workgroup exclusive scan of one value per thread (blockDim.x <= 1024); returns the total too.
+__device__ __forceinline__ uint32_t fp_block_scan(uint32_t x, uint32_t* s_w, uint32_t& total) {
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    uint32_t incl = x;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o, 64);
+        if ((int)lane >= o) incl += y;
+    }
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    uint32_t before = 0;
+    total = 0;
+    for (uint32_t w = 0; w < nw; ++w) {
+        const uint32_t c = s_w[w];
+        if (w < wave) before += c;
+        total += c;
+    }
+    __syncthreads();
+    return before + incl - x;
+}
+
+// literal range of clause c: fixed width k (AoS) or the CSR offsets
+__device__ __forceinline__ uint32_t cl_start(const ClauseView& cv, uint32_t c) { return cv.k ? c * cv.k : cv.offs[c]; }
+__device__ __forceinline__ uint32_t cl_width(const ClauseView& cv, uint32_t c) {
+    return cv.k ? cv.k : cv.offs[c + 1] - cv.offs[c];
+}
+
+// Fixed-width layout (the hybrid evaluation writes its violated clauses to per-tile lists in
+// evaluation order): every violated clause sets its byte of the clause-order flag array
+// rr_flag (a wave per evaluation tile; k_rr_entries reads the flags in clause order and clears
+// them), so the scan entries come out in clause order as from the CSR evaluation's bitmask.
+template <int K>
+__global__ __launch_bounds__(256) void k_rr_mark(ClauseView cv, LoopBuffers b) {
+    if (!b.state->active) return;
+    constexpr int S = Ent<K>::S;
+    const uint32_t tile = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (tile >= b.n_tiles) return;
+    const uint32_t cnt = b.tile_cnt[tile];
+    const uint32_t* lin = b.stage[0] + (uint64_t)tile * TILE * S;
+    for (uint32_t i = lane; i < cnt; i += 64) {
+        Ent<K> e;
+        load_ent<K>(e, lin + (uint64_t)i * S);
+        ent_unpack<K>(cv, e);
+        b.rr_flag[e.w[0]] = 1u;
+    }
+}
+
+// violated clauses per clause-order tile (flag mode), a wave per tile
+__global__ __launch_bounds__(256) void k_rr_count(LoopBuffers b) {
+    if (!b.state->active) return;
+    const uint32_t tile = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (tile >= b.n_tiles) return;
+    const uint4* f = reinterpret_cast<const uint4*>(b.rr_flag + (uint64_t)tile * TILE);
+    uint32_t c = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < TILE / 16 / 64; ++q) {  // flags are 0 / 1 bytes
+        const uint4 x = f[q * 64 + lane];
+        c += __popc(x.x) + __popc(x.y) + __popc(x.z) + __popc(x.w);
+    }
+    for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o, 64);
+    if (lane == 0) b.rr_tcnt[tile] = c;
+}
+
 __global__ __launch_bounds__(256) void k_rr_entries(ClauseView cv, LoopBuffers b) {
     if (!b.state->active) return;
     const uint32_t tile = blockIdx.x, tid = threadIdx.x;
     if (tile == 0 && tid < 2 && b.rr_ctl) b.rr_ctl[tid] = 0u;  // k_rr_mw: barrier counter, MIS count
     __shared__ uint32_t s_part[4], s_wpre[TILE_WORDS + 1];
     __shared__ uint32_t s_ids[TILE];
+    // clause-order counts of the earlier tiles: the flag counts (fixed width) or the CSR
+    // evaluation's own tile counts
+    const uint32_t* tcnt = b.rr_flag ? b.rr_tcnt : b.tile_cnt;
     uint32_t acc = 0;
-    for (uint32_t t = tid; t < tile; t += 256) acc += b.tile_cnt[t];
+    for (uint32_t t = tid; t < tile; t += 256) acc += tcnt[t];
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
     if ((tid & 63) == 0) s_part[tid >> 6] = acc;
-    uint64_t x = 0;
-    uint32_t cnt = 0, excl = 0;
-    if (tid < TILE_WORDS) {
-        const uint64_t c0 = (uint64_t)tile * TILE + 64u * tid;
-        x = c0 < cv.m ? b.vmask[(uint64_t)tile * TILE_WORDS + tid] : 0ull;
-        if (c0 < cv.m && cv.m - c0 < 64) x &= (1ull << (cv.m - c0)) - 1ull;
-        cnt = (uint32_t)__popcll(x);
-        uint32_t incl = cnt;
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(incl, o, 64);
-            if ((int)tid >= o) incl += y;
+    if (b.rr_flag) {
+        // 16 flags per thread (one 16-byte load), cleared for the next iteration once read
+        uint4* fp = reinterpret_cast<uint4*>(b.rr_flag + (uint64_t)tile * TILE) + tid;
+        const uint4 f = *fp;
+        const uint32_t fw[4] = {f.x, f.y, f.z, f.w};
+        uint32_t bits = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q)
+#pragma unroll
+            for (uint32_t e = 0; e < 4; ++e) bits |= ((fw[q] >> (8 * e)) & 1u) << (4 * q + e);
+        if (bits) *fp = make_uint4(0u, 0u, 0u, 0u);
+        const uint32_t cnt = (uint32_t)__popc(bits);
+        uint32_t tot;
+        __shared__ uint32_t s_w[4];
+        uint32_t o = fp_block_scan(cnt, s_w, tot);
+        if (tid == 0) s_wpre[TILE_WORDS] = tot;
+        while (bits) {
+            s_ids[o++] = tile * TILE + 16u * tid + (uint32_t)__builtin_ctz(bits);
+            bits &= bits - 1;
         }
-        excl = incl - cnt;
-        if (tid == TILE_WORDS - 1) s_wpre[TILE_WORDS] = incl;
-    }
-    if (tid < TILE_WORDS) {
-        uint32_t o = excl;
-        while (x) {
-            s_ids[o++] = tile * TILE + 64u * tid + (uint32_t)__builtin_ctzll(x);
-            x &= x - 1;
+    } else {
+        uint64_t x = 0;
+        uint32_t cnt = 0, excl = 0;
+        if (tid < TILE_WORDS) {
+            const uint64_t c0 = (uint64_t)tile * TILE + 64u * tid;
+            x = c0 < cv.m ? b.vmask[(uint64_t)tile * TILE_WORDS + tid] : 0ull;
+            if (c0 < cv.m && cv.m - c0 < 64) x &= (1ull << (cv.m - c0)) - 1ull;
+            cnt = (uint32_t)__popcll(x);
+            uint32_t incl = cnt;
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(incl, o, 64);
+                if ((int)tid >= o) incl += y;
+            }
+            excl = incl - cnt;
+            if (tid == TILE_WORDS - 1) s_wpre[TILE_WORDS] = incl;
+        }
+        if (tid < TILE_WORDS) {
+            uint32_t o = excl;
+            while (x) {
+                s_ids[o++] = tile * TILE + 64u * tid + (uint32_t)__builtin_ctzll(x);
+                x &= x - 1;
+            }
         }
     }
     __syncthreads();
@@ -2134,7 +2224,7 @@ __global__ __launch_bounds__(256) void k_rr_entries(ClauseView cv, LoopBuffers b
     const uint32_t n = s_wpre[TILE_WORDS];
     RREnt* out = reinterpret_cast<RREnt*>(b.rr_u) + base;
     for (uint32_t i = tid; i < n; i += 256) {
-        const uint32_t c = s_ids[i], lb = cv.offs[c], w = cv.offs[c + 1] - lb;
+        const uint32_t c = s_ids[i], lb = cl_start(cv, c), w = cl_width(cv, c);
         uint32_t v[8], hm = 0;  // hm: slots whose variable is hot (the fixpoint's degree count)
 #pragma unroll
         for (uint32_t j = 0; j < 8; ++j) {
@@ -2147,10 +2237,10 @@ __global__ __launch_bounds__(256) void k_rr_entries(ClauseView cv, LoopBuffers b
         e.v0 = make_uint4(v[0], v[1], v[2], v[3]);
         e.v1 = make_uint4(v[4], v[5], v[6], v[7]);
         out[i] = e;
+        if (b.rr_k >= 1 && b.rr_k <= 4 && b.fp_ctl) b.fp_v4[base + i] = e.v0;  // (the passes' narrow copy)
     }
 }
 
-// ------------------------------------------------------------------------------------
 // Round-robin MIS across workgroups (k_rr_mw): the batches with every lane group in
 // a workgroup of its own (one wave, one CU), so that the groups' scan steps -- chains of
 // dependent LDS hash operations -- no longer share one CU.  What the groups shared in LDS moves
@@ -2553,7 +2643,7 @@ __global__ __launch_bounds__(64) void k_rr_mw(ClauseView cv, LoopBuffers b) {
             const uint32_t s = L.live[(t0 + 1 + g) % n_live];
             if (wide) {
                 if (a) {
-                    const uint32_t cl = L.cc[0], lbp = cv.offs[cl], wp = cv.offs[cl + 1] - lbp;
+                    const uint32_t cl = L.cc[0], lbp = cl_start(cv, cl), wp = cl_width(cv, cl);
                     for (uint32_t j = lane; j < wp; j += 64)
                         __builtin_amdgcn_raw_buffer_store_b8((uint8_t)stamp, rsC, lit_var(cv.lits[lbp + j]), 0, 16);
                 }
@@ -2608,7 +2698,7 @@ __global__ __launch_bounds__(64) void k_rr_mw(ClauseView cv, LoopBuffers b) {
     for (uint32_t i = g * 64 + lane; i < tm; i += NW * 64) {
         const uint32_t c = b.tmis[i];
         atomicAdd(&b.tile_stats[2 * (c / TILE)], 1ull);
-        atomicAdd(&b.tile_stats[2 * (c / TILE) + 1], (unsigned long long)(cv.offs[c + 1] - cv.offs[c]));
+        atomicAdd(&b.tile_stats[2 * (c / TILE) + 1], (unsigned long long)cl_width(cv, c));
     }
     if (g == 0 && lane == 0) {
         st->tmis_cnt = tm;
@@ -2706,8 +2796,36 @@ __device__ __forceinline__ void fp_for_shared(const ClauseView& cv, const RREnt*
     }
 }
 
+// sole mask of an entry (bit j: slot j's variable has no other violated claimant this
+// iteration; fp_one, in vmix order, k_fp_bbuild): such a variable is always owned by the entry
+// and never covered by another pick, so the claims, ownership and kill tests skip it
+template <uint32_t KW>
+__device__ __forceinline__ uint32_t fp_sole_mask(const LoopBuffers& b, const RREnt* U, uint32_t i, const uint4& a,
+                                                 const uint4& v0) {
+    auto one = [&](uint32_t v) -> uint32_t {
+        const uint32_t x = vmix(b, v);
+        return (b.fp_one[x >> 5] >> (x & 31u)) & 1u;
+    };
+    const uint32_t w = a.z;
+    uint32_t m = 0;
+    if (w > 0) m |= one(v0.x);
+    if (w > 1) m |= one(v0.y) << 1;
+    if (w > 2) m |= one(v0.z) << 2;
+    if (w > 3) m |= one(v0.w) << 3;
+    if constexpr (KW == 0) {
+        if (w > 4) {
+            const uint4 v1 = U[i].v1;
+            m |= one(v1.x) << 4;
+            if (w > 5) m |= one(v1.y) << 5;
+            if (w > 6) m |= one(v1.z) << 6;
+            if (w > 7) m |= one(v1.w) << 7;
+        }
+    }
+    return m;
+}
+
 // an entry's header and first 4 variables in a pass; narrow instances (one width <= 4) read
-// the 16-byte copy k_fp_vfill made (a third of the 48-byte scan entry's lines)
+// the 16-byte copy k_rr_entries made (a third of the 48-byte scan entry's lines)
 template <uint32_t KW>
 __device__ __forceinline__ void fp_ent(const LoopBuffers& b, const RREnt* U, uint32_t i, uint4& a, uint4& v0) {
     if constexpr (KW == 4) {
@@ -2777,70 +2895,6 @@ __global__ __launch_bounds__(256) void k_fp_begin(LoopBuffers b) {
     }
 }
 
-// Violated claimants per variable (fp_deg, zeroed before); each claim of slots 0..7 keeps the
-// rank its count returned (its place in the variable's list; further slots of wide clauses are
-// counted apart).  Claims on hot variables (power-law hubs, flagged by the host) are counted per
-// workgroup in an LDS table first -- one global atomic per (workgroup, hub) instead of one per
-// claim on one address -- and get their ranks in a third phase.
-constexpr uint32_t FP_RANK_LDS = 0x80000000u;  // rank = LDS slot << 20 | rank within the workgroup
-template <uint32_t KW>
-__global__ __launch_bounds__(FP_THREADS) void k_fp_deg(ClauseView cv, LoopBuffers b) {
-    const RRFpCtl* ctl = b.fp_ctl;
-    if (ctl->state != FP_RUN) return;
-    __shared__ uint32_t s_hk[HOT_SLOTS], s_hc[HOT_SLOTS];
-    const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
-    const uint32_t nu = ctl->nu;
-    const bool hot = cv.n_hot != 0;
-    if (hot) {
-        for (uint32_t i = threadIdx.x; i < HOT_SLOTS; i += blockDim.x) { s_hk[i] = ~0u; s_hc[i] = 0u; }
-        __syncthreads();
-    }
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nu; i += gridDim.x * blockDim.x) {
-        const uint4 a = U[i].a, v0 = U[i].v0;
-        uint32_t rk[8], j = 0;
-        fp_for_vars<KW>(cv, U, i, a, v0, [&](uint32_t v) {
-            if (j < 8 && hot && ((a.w >> j) & 1u)) {
-                uint32_t h = (v * 2654435761u) & (HOT_SLOTS - 1);
-                for (;;) {
-                    const uint32_t prev = atomicCAS(&s_hk[h], ~0u, v);
-                    if (prev == ~0u || prev == v) break;
-                    h = (h + 1) & (HOT_SLOTS - 1);
-                }
-                rk[j] = FP_RANK_LDS | (h << 20) | atomicAdd(&s_hc[h], 1u);
-            } else if (j < 8) {
-                rk[j] = atomicAdd(&b.fp_deg[v], 1u);
-            } else {
-                atomicAdd(&b.fp_deg_hi[v], 1u);
-            }
-            ++j;
-        });
-        uint4* rp = reinterpret_cast<uint4*>(b.fp_rank) + 2 * (uint64_t)i;
-        rp[0] = make_uint4(rk[0], rk[1], rk[2], rk[3]);
-        if (KW == 0 && a.z > 4) rp[1] = make_uint4(rk[4], rk[5], rk[6], rk[7]);
-    }
-    if (!hot) return;
-    __syncthreads();
-    for (uint32_t h = threadIdx.x; h < HOT_SLOTS; h += blockDim.x)  // the workgroup's claims per hub
-        if (s_hk[h] != ~0u) s_hc[h] = atomicAdd(&b.fp_deg[s_hk[h]], s_hc[h]);
-    __syncthreads();
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (this thread's rank stores above)
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nu; i += gridDim.x * blockDim.x) {
-        uint4* rp = reinterpret_cast<uint4*>(b.fp_rank) + 2 * (uint64_t)i;
-        const uint32_t w = U[i].a.z;
-        for (uint32_t q = 0; q < (KW == 0 && w > 4 ? 2u : 1u); ++q) {
-            uint4 r = rp[q];
-            uint32_t* x = &r.x;
-            bool any = false;
-            for (uint32_t e = 0; e < 4; ++e)
-                if (4 * q + e < w && (x[e] & FP_RANK_LDS)) {
-                    x[e] = s_hc[(x[e] >> 20) & (HOT_SLOTS - 1)] + (x[e] & 0xFFFFFu);
-                    any = true;
-                }
-            if (any) rp[q] = r;
-        }
-    }
-}
-
 // The first pass's input: picks spread evenly over every set at density num / den.
 __global__ __launch_bounds__(FP_THREADS) void k_fp_guess(LoopBuffers b) {
     const RRFpCtl* ctl = b.fp_ctl;
@@ -2856,127 +2910,155 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_guess(LoopBuffers b) {
     }
 }
 
-// Workgroup exclusive scan of one value per thread (blockDim.x <= 1024); returns the total too.
-__device__ __forceinline__ uint32_t fp_block_scan(uint32_t x, uint32_t* s_w, uint32_t& total) {
-    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    uint32_t incl = x;
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(incl, o, 64);
-        if ((int)lane >= o) incl += y;
-    }
-    if (lane == 63) s_w[wave] = incl;
-    __syncthreads();
-    uint32_t before = 0;
-    total = 0;
-    for (uint32_t w = 0; w < nw; ++w) {
-        const uint32_t c = s_w[w];
-        if (w < wave) before += c;
-        total += c;
-    }
-    __syncthreads();
-    return before + incl - x;
-}
-
 // Round 0 without atomics: the violated claimants of every shared variable (two or more) in
-// a CSR built once per iteration (fp_voff / fp_vlist); each pass's round-0 owner of such a
-// variable is then the minimum key over its list (k_fp_vmin, a thread per variable, plain
-// stores), which CLAIM(0)'s atomics computed before.  Block sums of the list lengths:
-__global__ __launch_bounds__(FP_THREADS) void k_fp_vcount(LoopBuffers b) {
-    const RRFpCtl* ctl = b.fp_ctl;
-    if (ctl->state != FP_RUN) return;
-    __shared__ uint32_t s_w[FP_THREADS / 64];
-    const uint32_t nv = b.n_vars, nblk = (nv + FP_B - 1) / FP_B;
-    for (uint32_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
-        uint32_t acc = 0;
-        for (uint32_t e = 0; e < FP_PER; ++e) {
-            const uint32_t v = blk * FP_B + e * FP_THREADS + threadIdx.x;
-            const uint32_t d = v < nv ? b.fp_deg[v] + b.fp_deg_hi[v] : 0u;
-            acc += d >= 2 ? d : 0u;
-        }
-        uint32_t tot;
-        (void)fp_block_scan(acc, s_w, tot);
-        if (threadIdx.x == 0) b.fp_vblk[blk] = tot;
-    }
+// per-variable lists built once per iteration, by variable buckets (bkt_width variables each,
+// vmix order; as the bucketed round 0 of the one-set LFMIS, §4.1 of DESIGN.md):
+//   k_fp_bscatter (workgroup per FP_BS_ENT scan entries): every claim {entry, variable} is
+//     ranked in an LDS histogram of its bucket, the workgroup reserves its ranges in the
+//     buckets' static pair regions (fp_breg: the bucket's literal occurrences) with one global
+//     atomic per bucket, and the pairs are stored there;
+//   k_fp_bbuild (workgroup per bucket): LDS counters per variable place each claimant in its
+//     variable's static list region (fp_soff: the variable's literal occurrences); then per
+//     variable: the single-claimant bit (fp_one), the single claimant as its round-0 owner
+//     (fp_own0, for the whole iteration), the shared variables' list {start, count, variable}
+//     (fp_sv, per bucket) and the segments of long lists (fp_heavy).
+// Each pass's round-0 owner of a shared variable is then the minimum key over its list
+// (k_fp_vmin, plain stores), which CLAIM(0)'s atomics computed before.
+constexpr uint32_t FP_BS_PER = 8;                          // scan entries per thread of k_fp_bscatter
+constexpr uint32_t FP_BS_ENT = FP_BS_PER * FP_THREADS;     // ... per workgroup
+constexpr int FP_BB_THREADS = 1024;
+
+// slot j < 8 of an entry (narrow instances: the 16-byte copy)
+__device__ __forceinline__ uint32_t fp_slot(const uint4& v0, const uint4& v1, uint32_t j) {
+    const uint32_t v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+    return v[j];
 }
 
-// exclusive scan of the block sums (one workgroup)
-__global__ __launch_bounds__(1024) void k_fp_vscan(LoopBuffers b) {
-    const RRFpCtl* ctl = b.fp_ctl;
-    if (ctl->state != FP_RUN) return;
-    __shared__ uint32_t s_w[16];
-    const uint32_t nblk = (b.n_vars + FP_B - 1) / FP_B;
-    uint32_t carry = 0;
-    for (uint32_t k0 = 0; k0 < nblk; k0 += blockDim.x) {
-        const uint32_t k = k0 + threadIdx.x;
-        const uint32_t x = k < nblk ? b.fp_vblk[k] : 0u;
-        uint32_t tot;
-        const uint32_t ex = fp_block_scan(x, s_w, tot);
-        if (k < nblk) b.fp_vblk[k] = carry + ex;
-        carry += tot;
-    }
-    if (threadIdx.x == 0) b.fp_voff[b.n_vars] = carry;
-}
-
-// list offsets of every variable (shared variables only have non-empty ranges)
-__global__ __launch_bounds__(FP_THREADS) void k_fp_voff(LoopBuffers b) {
-    const RRFpCtl* ctl = b.fp_ctl;
-    if (ctl->state != FP_RUN) return;
-    __shared__ uint32_t s_w[FP_THREADS / 64];
-    const uint32_t nv = b.n_vars, nblk = (nv + FP_B - 1) / FP_B;
-    for (uint32_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
-        const uint32_t v0 = blk * FP_B + threadIdx.x * FP_PER;  // 8 consecutive variables per thread
-        uint32_t d[FP_PER], acc = 0;
-        for (uint32_t e = 0; e < FP_PER; ++e) {
-            const uint32_t v = v0 + e;
-            const uint32_t x = v < nv ? b.fp_deg[v] + b.fp_deg_hi[v] : 0u;
-            d[e] = x >= 2 ? x : 0u;
-            acc += d[e];
-        }
-        uint32_t tot;
-        uint32_t off = b.fp_vblk[blk] + fp_block_scan(acc, s_w, tot);
-        for (uint32_t e = 0; e < FP_PER; ++e) {
-            if (v0 + e < nv) b.fp_voff[v0 + e] = off;
-            off += d[e];
-            // long lists (hubs of skewed instances): a wave per FP_SEG claimants in k_fp_vmin_heavy
-            if (d[e] > FP_HEAVY) {
-                const uint32_t ns = (d[e] + FP_SEG - 1) / FP_SEG;
-                const uint32_t h0 = atomicAdd(&b.fp_ctl->nheavy, ns);
-                for (uint32_t k = 0; k < ns; ++k)
-                    reinterpret_cast<uint2*>(b.fp_heavy)[h0 + k] = make_uint2(v0 + e, off - d[e] + k * FP_SEG);
-            }
-        }
-    }
-}
-
-// entries into the lists of their shared variables, at the ranks k_fp_deg drew (slots past 8:
-// after the ranked ones, by a second counter), and every entry's sole-claimant mask (bit j:
-// slot j's variable has no other violated claimant, i.e. an empty list)
 template <uint32_t KW>
-__global__ __launch_bounds__(FP_THREADS) void k_fp_vfill(ClauseView cv, LoopBuffers b) {
+__global__ __launch_bounds__(FP_THREADS) void k_fp_bscatter(ClauseView cv, LoopBuffers b) {
     const RRFpCtl* ctl = b.fp_ctl;
     if (ctl->state != FP_RUN) return;
+    const uint32_t nu = ctl->nu, nb = b.n_bkt, tid = threadIdx.x;
+    extern __shared__ uint32_t s_bs[];
+    uint32_t* s_h = s_bs;                                   // nb: claims per bucket, then their bases
+    uint32_t* s_breg = s_bs + nb;                           // nb: static pair regions
+    uint16_t* s_rank = reinterpret_cast<uint16_t*>(s_bs + 2 * nb);  // FP_BS_ENT x 8 ranks
     const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
-    const uint32_t nu = ctl->nu;
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < nu; i += gridDim.x * blockDim.x) {
-        const uint4 a = U[i].a, v0 = U[i].v0;
-        const uint4* rp = reinterpret_cast<const uint4*>(b.fp_rank) + 2 * (uint64_t)i;
-        const uint4 r0 = rp[0], r1 = (KW == 0 && a.z > 4) ? rp[1] : make_uint4(0, 0, 0, 0);
-        const uint32_t rk[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
-        if constexpr (KW == 4) b.fp_v4[i] = v0;
-        uint32_t sole = 0, j = 0;
-        fp_for_vars<KW>(cv, U, i, a, v0, [&](uint32_t v) {
-            const uint32_t o = b.fp_voff[v], d = b.fp_voff[v + 1] - o;
-            if (d == 0) {
-                if (j < 8) sole |= 1u << j;
-            } else if (j < 8) {
-                b.fp_vlist[o + rk[j]] = i;
-            } else {
-                b.fp_vlist[o + b.fp_deg[v] + atomicSub(&b.fp_deg_hi[v], 1u) - 1u] = i;
+    uint2* pairs = reinterpret_cast<uint2*>(b.fp_pairs);
+    for (uint32_t k = tid; k < nb; k += FP_THREADS) s_breg[k] = b.fp_breg[k];
+    auto ent = [&](uint32_t i, uint4& a, uint4& v0, uint4& v1) {
+        if constexpr (KW == 4) {
+            v0 = b.fp_v4[i];
+            v1 = make_uint4(RR_EMPTY, RR_EMPTY, RR_EMPTY, RR_EMPTY);
+            a = make_uint4(0u, 0u, b.rr_k, 0u);
+        } else {
+            a = U[i].a;
+            v0 = U[i].v0;
+            v1 = U[i].v1;
+        }
+    };
+    for (uint32_t i0 = blockIdx.x * FP_BS_ENT; i0 < nu; i0 += gridDim.x * FP_BS_ENT) {
+        for (uint32_t k = tid; k < nb; k += FP_THREADS) s_h[k] = 0u;
+        __syncthreads();
+        for (uint32_t e = 0; e < FP_BS_PER; ++e) {  // ranks of slots 0..7 within this chunk
+            const uint32_t i = i0 + e * FP_THREADS + tid;
+            if (i >= nu) break;
+            uint4 a, v0, v1;
+            ent(i, a, v0, v1);
+            const uint32_t w = a.z, w8 = w < 8u ? w : 8u;
+            uint32_t off;
+            for (uint32_t j = 0; j < w8; ++j)
+                s_rank[(e * FP_THREADS + tid) * 8 + j] = (uint16_t)atomicAdd(&s_h[bucket_of(b, fp_slot(v0, v1, j), off)], 1u);
+            if constexpr (KW == 0) {  // slots past 8 of wide clauses (rare): a global rank each
+                for (uint32_t j = 8; j < w; ++j) {
+                    const uint32_t v = lit_var(cv.lits[a.y + j]);
+                    const uint32_t bk = bucket_of(b, v, off);
+                    pairs[s_breg[bk] + atomicAdd(&b.fp_bfill[bk], 1u)] = make_uint2(i, v);
+                }
             }
-            ++j;
-        });
-        b.fp_sole[i] = (uint8_t)sole;
+        }
+        __syncthreads();
+        for (uint32_t k = tid; k < nb; k += FP_THREADS) {  // this chunk's range in every bucket region
+            const uint32_t c = s_h[k];
+            s_h[k] = c ? s_breg[k] + atomicAdd(&b.fp_bfill[k], c) : 0u;
+        }
+        __syncthreads();
+        for (uint32_t e = 0; e < FP_BS_PER; ++e) {
+            const uint32_t i = i0 + e * FP_THREADS + tid;
+            if (i >= nu) break;
+            uint4 a, v0, v1;
+            ent(i, a, v0, v1);
+            const uint32_t w8 = a.z < 8u ? a.z : 8u;
+            uint32_t off;
+            for (uint32_t j = 0; j < w8; ++j) {
+                const uint32_t v = fp_slot(v0, v1, j);
+                pairs[s_h[bucket_of(b, v, off)] + s_rank[(e * FP_THREADS + tid) * 8 + j]] = make_uint2(i, v);
+            }
+        }
+        __syncthreads();  // (s_h is reset for the next chunk)
     }
+}
+
+__global__ __launch_bounds__(FP_BB_THREADS) void k_fp_bbuild(LoopBuffers b) {
+    RRFpCtl* ctl = b.fp_ctl;
+    if (ctl->state != FP_RUN) return;
+    const uint32_t bk = blockIdx.x, W = b.bkt_width, tid = threadIdx.x;
+    const uint32_t xb = bk * W;  // first vmix slot of the bucket
+    const uint32_t nw = min(W, b.bkt_span - xb);  // (vmix slots [0, bkt_span))
+    extern __shared__ uint32_t s_bb[];
+    uint32_t* s_cnt = s_bb;
+    uint32_t* s_off = s_bb + W;
+    uint32_t* s_first = s_bb + 2 * W;
+    __shared__ uint32_t s_ns;
+    const uint32_t n = b.fp_bfill[bk];
+    for (uint32_t w = tid; w < nw; w += FP_BB_THREADS) {
+        const uint32_t v = vunmix(b, xb + w);
+        s_cnt[w] = 0u;
+        s_off[w] = v < b.n_vars ? b.fp_soff[v] : 0u;
+    }
+    if (tid == 0) s_ns = 0;
+    __syncthreads();
+    if (tid == 0) b.fp_bfill[bk] = 0u;  // (read by every thread above; the next iteration's count)
+    const uint2* P = reinterpret_cast<const uint2*>(b.fp_pairs) + b.fp_breg[bk];
+    for (uint32_t k = tid; k < n; k += FP_BB_THREADS) {
+        const uint2 p = P[k];
+        const uint32_t w = vmix(b, p.y) - xb;
+        const uint32_t r = atomicAdd(&s_cnt[w], 1u);
+        if (r == 0) s_first[w] = p.x;
+        b.fp_vlist[s_off[w] + r] = p.x;
+    }
+    __syncthreads();
+    // per variable (vmix slot order): single-claimant bits, the single claimant's ownership, the
+    // shared list and the long lists' segments
+    uint4* sv = reinterpret_cast<uint4*>(b.fp_sv) + (uint64_t)bk * W;
+    const uint32_t lane = tid & 63;
+    for (uint32_t w0 = 0; w0 < nw; w0 += FP_BB_THREADS) {
+        const uint32_t w = w0 + tid;
+        const uint32_t c = w < nw ? s_cnt[w] : 0u;
+        const unsigned long long one = __ballot(c == 1u);
+        // (bucket widths are multiples of 64: the ballot's halves are whole words of fp_one)
+        if (lane == 0 && xb + w0 + tid < b.bkt_span) {
+            uint32_t* ow = b.fp_one + (xb + w0 + tid) / 32;
+            ow[0] = (uint32_t)one;
+            ow[1] = (uint32_t)(one >> 32);
+        }
+        if (c == 0u) continue;
+        const uint32_t v = vunmix(b, xb + w);
+        if (c == 1u) {
+            b.fp_own0[v] = s_first[w];
+        } else {
+            sv[atomicAdd(&s_ns, 1u)] = make_uint4(s_off[w], c, v, 0u);
+            if (c > FP_HEAVY) {  // long lists (hubs of skewed instances): a wave per FP_SEG claimants
+                const uint32_t ns = (c + FP_SEG - 1) / FP_SEG;
+                const uint32_t h0 = atomicAdd(&ctl->nheavy, ns);
+                for (uint32_t k = 0; k < ns; ++k)
+                    reinterpret_cast<uint4*>(b.fp_heavy)[h0 + k] =
+                        make_uint4(v, s_off[w] + k * FP_SEG, s_off[w] + min(c, (k + 1) * FP_SEG), 0u);
+            }
+        }
+    }
+    __syncthreads();
+    if (tid == 0) b.fp_sbcnt[bk] = s_ns;
 }
 
 // round 0 of a pass for the variables with more than FP_HEAVY claimants: a wave per segment of
@@ -2987,10 +3069,9 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_vmin_heavy(LoopBuffers b) {
     if (ctl->state != FP_RUN) return;
     const uint32_t ep = ctl->ep_base, nh = ctl->nheavy, lane = threadIdx.x & 63;
     for (uint32_t h = blockIdx.x * (FP_THREADS / 64) + (threadIdx.x >> 6); h < nh; h += gridDim.x * (FP_THREADS / 64)) {
-        const uint2 sg = reinterpret_cast<const uint2*>(b.fp_heavy)[h];
-        const uint32_t v = sg.x, o1 = min(b.fp_voff[v + 1], sg.y + FP_SEG);
+        const uint4 sg = reinterpret_cast<const uint4*>(b.fp_heavy)[h];
         unsigned long long best = ~0ull;
-        for (uint32_t o = sg.y + lane; o < o1; o += 64) {
+        for (uint32_t o = sg.y + lane; o < sg.z; o += 64) {
             const uint32_t i = b.fp_vlist[o];
             const unsigned long long k = fp_key(b, ep, b.fp_turn[i], i);
             best = k < best ? k : best;
@@ -3000,30 +3081,33 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_vmin_heavy(LoopBuffers b) {
             best = y < best ? y : best;
         }
         if (lane == 0) {
-            b.fp_own0[v] = ~0u;
-            atomicMin(&b.fp_owner[v], best);
+            b.fp_own0[sg.x] = ~0u;
+            atomicMin(&b.fp_owner[sg.x], best);
         }
     }
 }
 
-// round 0 of a pass: the minimum key over every shared variable's claimants
+// round 0 of a pass: the minimum key over every shared variable's claimants (a workgroup per
+// bucket over its shared list)
 __global__ __launch_bounds__(FP_THREADS) void k_fp_vmin(LoopBuffers b) {
     const RRFpCtl* ctl = b.fp_ctl;
     if (ctl->state != FP_RUN) return;
-    const uint32_t ep = ctl->ep_base, nv = b.n_vars;
-    for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += gridDim.x * blockDim.x) {
-        const uint32_t o0 = b.fp_voff[v], o1 = b.fp_voff[v + 1];
-        if (o1 - o0 < 2 || o1 - o0 > FP_HEAVY) continue;
+    const uint32_t ep = ctl->ep_base, bk = blockIdx.x;
+    const uint32_t ns = b.fp_sbcnt[bk];
+    const uint4* sv = reinterpret_cast<const uint4*>(b.fp_sv) + (uint64_t)bk * b.bkt_width;
+    for (uint32_t k = threadIdx.x; k < ns; k += FP_THREADS) {
+        const uint4 e = sv[k];
+        if (e.y > FP_HEAVY) continue;
         unsigned long long best = ~0ull;
-        for (uint32_t o = o0; o < o1; ++o) {
+        for (uint32_t o = e.x; o < e.x + e.y; ++o) {
             const uint32_t i = b.fp_vlist[o];
-            const unsigned long long k = fp_key(b, ep, b.fp_turn[i], i);
-            best = k < best ? k : best;
+            const unsigned long long key = fp_key(b, ep, b.fp_turn[i], i);
+            best = key < best ? key : best;
         }
         // JOIN(0) reads the winning entry from a 4-byte array (half the footprint of the keys).
         // The owner key itself is not needed: the later rounds' claims are of later epochs,
         // below any key an earlier pass or round left there
-        b.fp_own0[v] = (uint32_t)best & ((1u << b.fp_ib) - 1u);
+        b.fp_own0[e.z] = (uint32_t)best & ((1u << b.fp_ib) - 1u);
     }
 }
 
@@ -3054,7 +3138,7 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_claim(ClauseView cv, LoopBuff
                 i = lin[j];
                 uint4 a, v0;
                 fp_ent<KW>(b, U, i, a, v0);
-                const uint32_t sole = b.fp_sole[i];
+                const uint32_t sole = fp_sole_mask<KW>(b, U, i, a, v0);
                 const uint32_t turn = b.fp_turn[i];
                 bool dead = false;
                 fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) { dead |= b.fp_cov[v] == (uint8_t)serial; });
@@ -3098,14 +3182,15 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_join(ClauseView cv, LoopBuffe
                 i = r == 0 ? i0 + j : lin[j];
                 uint4 a, v0;
                 fp_ent<KW>(b, U, i, a, v0);
-                const uint32_t sole = b.fp_sole[i];
+                // (round 0 needs no sole mask: a single claimant owns its variable, fp_own0)
+                const uint32_t sole = r == 0 ? 0u : fp_sole_mask<KW>(b, U, i, a, v0);
                 const uint32_t turn = b.fp_turn[i];
                 bool own = true, pre = false;
                 if (r == 0 && turn < tpre) {  // decided as in the last pass (bit 1)
                     pre = true;
                     own = (b.fp_in[i] >> 1) & 1u;
                 } else if (r == 0) {
-                    fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) {
+                    fp_for_vars<KW>(cv, U, i, a, v0, [&](uint32_t v) {
                         const uint32_t w = b.fp_own0[v];  // (~0: a long list, reduced into the key)
                         own &= w == i || (w == ~0u && b.fp_owner[v] == fp_key(b, ep, turn, i));
                     });
@@ -3155,7 +3240,7 @@ __global__ __launch_bounds__(1024) void k_fp_tail(ClauseView cv, LoopBuffers b) 
                 i = la[j];
                 uint4 a, v0;
                 fp_ent<KW>(b, U, i, a, v0);
-                const uint32_t sole = b.fp_sole[i];
+                const uint32_t sole = fp_sole_mask<KW>(b, U, i, a, v0);
                 bool dead = false;
                 fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) {
                     dead |= __hip_atomic_load(&b.fp_cov[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint8_t)serial;
@@ -3182,7 +3267,7 @@ __global__ __launch_bounds__(1024) void k_fp_tail(ClauseView cv, LoopBuffers b) 
                 i = lb[j];
                 uint4 a, v0;
                 fp_ent<KW>(b, U, i, a, v0);
-                const uint32_t sole = b.fp_sole[i];
+                const uint32_t sole = fp_sole_mask<KW>(b, U, i, a, v0);
                 const unsigned long long key = fp_key(b, ep, b.fp_turn[i], i);
                 bool own = true;
                 fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) {
@@ -3609,7 +3694,7 @@ hipError_t launch_eval(const ClauseView& cv, const LoopBuffers& b, uint32_t tile
 // and device records what is set (contexts on several devices may share a process).
 constexpr int ATTR_MAX_DEV = 64;
 static std::atomic<uint32_t> g_attr_done[ATTR_MAX_DEV];
-enum : uint32_t { ATTR_HYBRID = 0, ATTR_BUCKETS = 9, ATTR_RAGGED = 30 };  // + k for per-width groups
+enum : uint32_t { ATTR_HYBRID = 0, ATTR_BUCKETS = 9, ATTR_FP = 18, ATTR_RAGGED = 30 };  // + k for per-width groups
 static bool attr_pending(uint32_t bit, int& dev) {
     if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= ATTR_MAX_DEV) {
         dev = -1;
@@ -3763,7 +3848,17 @@ hipError_t launch_tail(const ClauseView& cv, const LoopBuffers& b, uint32_t firs
 }
 
 hipError_t launch_rr_mis(const ClauseView& cv, const LoopBuffers& b, hipStream_t s) {
-    if (cv.k != 0 || !b.rr_u || b.rr_T < 2 || b.rr_T > RR_TMAX) return hipErrorInvalidValue;
+    if (!b.rr_u || b.rr_T < 2 || b.rr_T > RR_TMAX) return hipErrorInvalidValue;
+    if (b.rr_flag) {  // fixed width: violated flags in clause order from the evaluation's lists
+        if (cv.k == 0 || !b.rr_tcnt) return hipErrorInvalidValue;
+        const uint32_t gw = (b.n_tiles + 3) / 4;
+        if (gw) {
+            ALLL_DISPATCH_K(cv.k, (k_rr_mark<(K > 0 ? K : 1)><<<gw, 256, 0, s>>>(cv, b)));
+            k_rr_count<<<gw, 256, 0, s>>>(b);
+        }
+    } else if (cv.k != 0) {
+        return hipErrorInvalidValue;
+    }
     if (b.n_tiles) k_rr_entries<<<b.n_tiles, 256, 0, s>>>(cv, b);
     if (b.fp_ctl) {  // the fixpoint passes; k_rr_mw below only if they do not settle
         if (b.rr_T > FP_TMAX || b.fp_max == 0) return hipErrorInvalidValue;
@@ -3772,23 +3867,31 @@ hipError_t launch_rr_mis(const ClauseView& cv, const LoopBuffers& b, hipStream_t
         const uint32_t gl = (uint32_t)std::min<uint64_t>((b.m + FP_THREADS - 1) / FP_THREADS + 1, 2048);
         const uint32_t fp_grid = 2048;  // workgroups of the grid-stride round kernels
         const uint32_t gr = (uint32_t)std::min<uint64_t>((b.m + FP_RT - 1) / FP_RT + 1, fp_grid);
+        if (!b.fp_pairs || !b.fp_soff || b.n_bkt == 0 || b.n_bkt > BKT_MAX) return hipErrorInvalidValue;
+        const size_t lds_bs = 8ull * b.n_bkt + 2ull * FP_BS_ENT * 8;
+        const size_t lds_bb = fp_bbuild_lds_bytes(b.bkt_width);
+        int dev;
+        if (attr_pending(ATTR_FP, dev)) {
+            hipError_t e = hipFuncSetAttribute((const void*)k_fp_bscatter<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               (int)(8ull * BKT_MAX + 2ull * FP_BS_ENT * 8));
+            if (e == hipSuccess)
+                e = hipFuncSetAttribute((const void*)k_fp_bscatter<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)(8ull * BKT_MAX + 2ull * FP_BS_ENT * 8));
+            if (e == hipSuccess)
+                e = hipFuncSetAttribute((const void*)k_fp_bbuild, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        160 * 1024 - 1024);
+            if (e != hipSuccess) return e;
+            attr_mark(ATTR_FP, dev);
+        }
         hipError_t e = hipMemsetAsync(b.fp_owner, 0xFF, (size_t)b.n_vars * 8, s);
-        if (e != hipSuccess) return e;
-        e = hipMemsetAsync(b.fp_cov, 0, (size_t)b.n_vars, s);
-        if (e == hipSuccess) e = hipMemsetAsync(b.fp_deg, 0, (size_t)b.n_vars * 4, s);
-        if (e == hipSuccess && !narrow) e = hipMemsetAsync(b.fp_deg_hi, 0, (size_t)b.n_vars * 4, s);
+        if (e == hipSuccess) e = hipMemsetAsync(b.fp_cov, 0, (size_t)b.n_vars, s);
         if (e != hipSuccess) return e;
         k_fp_begin<<<1, 256, 0, s>>>(b);
-        if (narrow) k_fp_deg<4><<<gl, FP_THREADS, 0, s>>>(cv, b);
-        else k_fp_deg<0><<<gl, FP_THREADS, 0, s>>>(cv, b);
+        const uint32_t gbs = (uint32_t)std::min<uint64_t>((b.m + FP_BS_ENT - 1) / FP_BS_ENT + 1, 512);
+        if (narrow) k_fp_bscatter<4><<<gbs, FP_THREADS, lds_bs, s>>>(cv, b);
+        else k_fp_bscatter<0><<<gbs, FP_THREADS, lds_bs, s>>>(cv, b);
         k_fp_guess<<<gl, FP_THREADS, 0, s>>>(b);
-        const uint32_t gv = (uint32_t)std::min<uint64_t>((b.n_vars + FP_B - 1) / FP_B + 1, FP_COUNT_GRID);
-        const uint32_t gvt = (uint32_t)std::min<uint64_t>((b.n_vars + FP_THREADS - 1) / FP_THREADS + 1, fp_grid);
-        k_fp_vcount<<<gv, FP_THREADS, 0, s>>>(b);
-        k_fp_vscan<<<1, 1024, 0, s>>>(b);
-        k_fp_voff<<<gv, FP_THREADS, 0, s>>>(b);
-        if (narrow) k_fp_vfill<4><<<gl, FP_THREADS, 0, s>>>(cv, b);
-        else k_fp_vfill<0><<<gl, FP_THREADS, 0, s>>>(cv, b);
+        k_fp_bbuild<<<b.n_bkt, FP_BB_THREADS, lds_bb, s>>>(b);
         auto turns = [&](int test) {
             k_fp_count<<<gb, FP_THREADS, 0, s>>>(b, test);
             k_fp_sched<<<1, 256, 0, s>>>(b, test);
@@ -3799,7 +3902,7 @@ hipError_t launch_rr_mis(const ClauseView& cv, const LoopBuffers& b, hipStream_t
         for (uint32_t p = 0; p < b.fp_max; ++p) {
             for (uint32_t r = 0; r < FP_G; ++r) {
                 if (r == 0) {
-                    k_fp_vmin<<<gvt, FP_THREADS, 0, s>>>(b);
+                    k_fp_vmin<<<b.n_bkt, FP_THREADS, 0, s>>>(b);
                     k_fp_vmin_heavy<<<FP_HEAVY_GRID, FP_THREADS, 0, s>>>(b);
                     if (narrow) k_fp_join<4><<<gr, FP_THREADS, 0, s>>>(cv, b, 0);
                     else k_fp_join<0><<<gr, FP_THREADS, 0, s>>>(cv, b, 0);

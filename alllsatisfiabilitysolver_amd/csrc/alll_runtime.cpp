@@ -584,7 +584,8 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     // the streaming solve keeps the clause-order (CSR) layout: its window rule needs the first
     // violated clause index, read from a clause-order bitmask
     // the round-robin MIS of T > 1 chunks (the reference's n_threads > 1) walks clause-order
-    // lists of violated clauses: CSR layout too
+    // lists of violated clauses: fixed widths keep the hybrid evaluation, whose lists are turned
+    // into clause-order flags (k_rr_mark); ragged widths the CSR evaluation
     const uint32_t rr_T = (opt.n_threads > 1 && !(opt.flags & ALLL_FLAG_LFMIS) && !opt.stream_batch)
                               ? (uint32_t)opt.n_threads : 0u;
     if (rr_T > RR_TMAX) return fail(ALLL_ERR_UNSUPPORTED, "n_threads %u > %u chunks", rr_T, RR_TMAX);
@@ -609,7 +610,7 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
         }
     }
     const int rr_width = fixed_k;  // common clause width (-1: no clauses, 0: ragged)
-    if (fixed_k < 1 || fixed_k > MAX_FIXED_K || (opt.flags & ALLL_FLAG_GENERIC_CSR) || opt.stream_batch || rr_T)
+    if (fixed_k < 1 || fixed_k > MAX_FIXED_K || (opt.flags & ALLL_FLAG_GENERIC_CSR) || opt.stream_batch)
         fixed_k = 0;
     const uint64_t lim = 2ull * prob->n_vars;
     for (uint64_t j = 0; j < L; ++j)
@@ -715,6 +716,10 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     if (rr_T) {
         uint32_t* d_sets = nullptr;
         if ((rc = dalloc(c, &b.rr_u, 12 * (size_t)m))) return bail(rc);  // scan entries (k_rr_entries)
+        if (fixed_k > 0) {  // the hybrid evaluation's lists -> clause-order flags (k_rr_mark)
+            if ((rc = dalloc(c, &b.rr_flag, (size_t)n_tiles * TILE))) return bail(rc);
+            if ((rc = dalloc(c, &b.rr_tcnt, n_tiles))) return bail(rc);
+        }
         if ((rc = dalloc(c, &d_sets, rr_T + 1))) return bail(rc);
         if (hipStreamSynchronize(c->stream) != hipSuccess ||
             hipMemcpy(d_sets, rr_sets.data(), (rr_T + 1) * 4ull, hipMemcpyHostToDevice) != hipSuccess)
@@ -748,14 +753,9 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
             if ((rc = dalloc(c, &b.fp_owner, (size_t)prob->n_vars + 1, 0xFF))) return bail(rc);
             if ((rc = dalloc(c, &b.fp_cov, (size_t)prob->n_vars + 16))) return bail(rc);
             if ((rc = dalloc(c, &b.fp_own0, (size_t)prob->n_vars + 1))) return bail(rc);
-            if ((rc = dalloc(c, &b.fp_deg, (size_t)prob->n_vars + 1))) return bail(rc);
-            if ((rc = dalloc(c, &b.fp_deg_hi, (size_t)prob->n_vars + 1))) return bail(rc);
-            if ((rc = dalloc(c, &b.fp_rank, 8 * (size_t)m + 8))) return bail(rc);
-            if ((rc = dalloc(c, &b.fp_sole, m + 1))) return bail(rc);
-            if ((rc = dalloc(c, &b.fp_voff, (size_t)prob->n_vars + 2))) return bail(rc);
             if ((rc = dalloc(c, &b.fp_vlist, (size_t)L + 1))) return bail(rc);
-            if ((rc = dalloc(c, &b.fp_vblk, (size_t)prob->n_vars / FP_B + 2))) return bail(rc);
-            if ((rc = dalloc(c, &b.fp_heavy, 2 * ((size_t)L / 64 + 2)))) return bail(rc);  // (segments of lists > 64 claims)
+            if ((rc = dalloc(c, &b.fp_heavy, 4 * ((size_t)L / 64 + 2)))) return bail(rc);  // (segments of lists > 64 claims)
+            if ((rc = dalloc(c, &b.fp_pairs, (size_t)L + 1))) return bail(rc);
             if ((rc = dalloc(c, &b.fp_blk, 2 * nblk + 2048))) return bail(rc);  // sums, offsets, changes, earliest changes
             if ((rc = dalloc(c, &b.fp_sf, rr_T + 1))) return bail(rc);
             if ((rc = dalloc(c, &b.fp_bnd, rr_T + 1))) return bail(rc);
@@ -793,6 +793,54 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
         b.vmix_mask = (uint32_t)(vrange - 1);
     }
     if ((rc = dalloc(c, &b.owner, (size_t)vrange, 0xFF))) return bail(rc);
+    {
+        uint32_t inv = b.vmix_mul;  // Newton iteration for the inverse mod 2^32 (odd multiplier)
+        for (int it = 0; it < 5; ++it) inv *= 2u - b.vmix_mul * inv;
+        b.vmix_inv = inv;
+    }
+    if (b.fp_ctl) {
+        // round robin: claimant lists by variable buckets (k_fp_bscatter / k_fp_bbuild): bucket =
+        // vmix(v) / width, width a multiple of 64 (whole words of fp_one), one bucket per CU
+        // when the width fits the LDS of k_fp_bbuild
+        const uint64_t span = std::max<uint64_t>(vrange, 1);
+        uint64_t width = (span + (uint64_t)c->n_cu - 1) / (uint64_t)c->n_cu;
+        width = std::max<uint64_t>(1024, (width + 63) / 64 * 64);
+        width = std::min<uint64_t>(width, 12288);
+        uint64_t nb = (span + width - 1) / width;
+        if (nb > BKT_MAX) {
+            width = ((span + BKT_MAX - 1) / BKT_MAX + 63) / 64 * 64;
+            nb = (span + width - 1) / width;
+        }
+        if (fp_bbuild_lds_bytes((uint32_t)width) > 160u * 1024 - 1024)
+            return bail(fail(ALLL_ERR_UNSUPPORTED, "round robin: %u variables exceed the claimant buckets", c->n_vars));
+        b.bkt_width = (uint32_t)width;
+        b.bkt_magic = (uint32_t)((1ull << 32) / width);
+        b.n_bkt = (uint32_t)nb;
+        b.bkt_span = (uint32_t)span;
+        std::vector<uint32_t> soff(c->n_vars + 1, 0u), breg(nb + 1, 0u);
+        for (uint64_t j = 0; j < L; ++j) ++soff[prob->literals[j] >> 1];
+        uint32_t acc = 0;
+        for (uint32_t v = 0; v < c->n_vars; ++v) {
+            const uint32_t d = soff[v];
+            soff[v] = acc;
+            acc += d;
+            breg[((uint64_t)((v * b.vmix_mul) & b.vmix_mask)) / width] += d;
+        }
+        soff[c->n_vars] = acc;
+        acc = 0;
+        for (uint64_t k = 0; k <= nb; ++k) { const uint32_t d = breg[k]; breg[k] = acc; acc += d; }
+        uint32_t *d_soff = nullptr, *d_breg = nullptr;
+        if ((rc = dalloc(c, &d_soff, soff.size())) || (rc = dalloc(c, &d_breg, breg.size())) ||
+            (rc = dalloc(c, &b.fp_bfill, nb)) || (rc = dalloc(c, &b.fp_one, span / 32 + 4)) ||
+            (rc = dalloc(c, &b.fp_sv, (size_t)nb * width)) || (rc = dalloc(c, &b.fp_sbcnt, nb)))
+            return bail(rc);
+        if (hipStreamSynchronize(c->stream) != hipSuccess ||
+            hipMemcpy(d_soff, soff.data(), soff.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(d_breg, breg.data(), breg.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+            return bail(fail(ALLL_ERR_HIP, "claimant bucket upload failed"));
+        b.fp_soff = d_soff;
+        b.fp_breg = d_breg;
+    }
     if ((rc = dalloc(c, &b.cover, (size_t)b.n_words * 32))) return bail(rc);  // whole words, zero-padded
     if ((rc = dalloc(c, &b.tile_stats, 2 * (size_t)n_tiles))) return bail(rc);
     if ((rc = dalloc(c, &b.delta, b.n_words))) return bail(rc);
@@ -812,7 +860,7 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     }
     // ---- bucketed LFMIS round 0 (fixed width): one bucket per CU when a bucket's minima fit
     // in LDS (else ~300-1000 power-of-2 buckets), runs of up to 16 tiles
-    if (fixed_k > 0 && !(opt.flags & ALLL_FLAG_ATOMIC_CLAIMS) && n_tiles > 0 && c->n_vars > 0) {
+    if (fixed_k > 0 && !rr_T && !(opt.flags & ALLL_FLAG_ATOMIC_CLAIMS) && n_tiles > 0 && c->n_vars > 0) {
         uint32_t shift = BKT_SHIFT_MIN;
         while (shift < BKT_SHIFT_MAX && (vrange >> shift) > 384) ++shift;
         uint64_t width = (vrange + (uint64_t)c->n_cu - 1) / (uint64_t)c->n_cu;

@@ -53,9 +53,7 @@ constexpr uint32_t RR_MW_CTL_WORDS = 1024; // k_rr_mw control block (words)
 constexpr uint32_t FP_TMAX = 256;          // sets (the schedule keeps T x T phase records)
 constexpr uint32_t FP_B = 2048;            // entries per block of the count / turn passes
 constexpr uint32_t FP_G = 4;               // grid LFMIS rounds before the one-workgroup tail
-constexpr uint32_t FP_MAX_DEFAULT = 16;    // LFMIS passes per iteration (graph unroll)
-constexpr uint32_t FP_MAX_LONG = 48;       // ... in the long graph variant, used after an iteration
-constexpr uint32_t FP_LONG_AT = 13;        // that needed more than this many passes
+constexpr uint32_t FP_MAX_DEFAULT = 64;    // LFMIS passes per iteration before k_rr_mw decides it
 enum : uint32_t { FP_RUN = 0, FP_FINAL = 1, FP_DONE = 2, FP_OFF = 3, FP_FAIL = 4 };
 struct RRFpCtl {
     uint32_t state;      // FP_*: RUN iterating; FINAL the last pass converged (finalize now);
@@ -261,9 +259,11 @@ hipError_t launch_round0_buckets(const ClauseView& cv, const LoopBuffers& b, boo
                                  bool scattered, hipStream_t s);
 hipError_t launch_tail(const ClauseView& cv, const LoopBuffers& b, uint32_t first_round,
                        hipStream_t s);
-// round robin: k_rr_entries, the fixpoint passes (when b.fp_ctl), then k_rr_mw for
-// iterations the fixpoint did not settle
-hipError_t launch_rr_mis(const ClauseView& cv, const LoopBuffers& b, hipStream_t s);
+// round robin: scan entries and the fixpoint's iteration set-up (when b.fp_ctl); n fixpoint
+// passes; k_rr_mw for an iteration the passes did not settle
+hipError_t launch_rr_prep(const ClauseView& cv, const LoopBuffers& b, hipStream_t s);
+hipError_t launch_rr_passes(const ClauseView& cv, const LoopBuffers& b, uint32_t n, hipStream_t s);
+hipError_t launch_rr_finish(const ClauseView& cv, const LoopBuffers& b, hipStream_t s);
 hipError_t launch_resample(const ClauseView& cv, const LoopBuffers& b, uint32_t tile_begin,
                            uint32_t tile_end, bool to_delta, hipStream_t s);
 hipError_t launch_apply_delta(const LoopBuffers& b, hipStream_t s);

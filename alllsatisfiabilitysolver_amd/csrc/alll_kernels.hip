@@ -392,6 +392,7 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
     // (bit 31 of win_base[t]: the smallest variable of every clause of tile t lies in its
     // window, so slot K-1 is looked up in LDS only)
     auto window = [&](uint32_t t) -> uint32_t { return b.win_base ? b.win_base[t] & 0x7FFFFFFFu : 0u; };
+    auto win_key = [&](uint32_t t) -> uint32_t { return b.win_base ? b.win_base[t] : 0u; };  // (with bit 31)
     // the whole assignment fits the LDS window: every lookup is an LDS read
     const bool all_lds = b.win_base == nullptr && b.n_words <= b.win_words;
     uint32_t wb = window(t0);
@@ -448,6 +449,14 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
             for (int q = 0; q < 4; ++q) gw[q] = 0u;
         }
     };
+    // slot K-1 of a tile whose clauses all have their smallest variable in the window (bit 31 of
+    // win_base): LDS reads only, no range test or L2 path
+    auto lookup4_lds = [&](uint32_t wb4n, const uint32_t (&xs)[4], uint32_t (&lw)[4]) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            lw[q] = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(s_A) +
+                                                       __builtin_amdgcn_ubfe(xs[q], 6u, wbits) * 4u + wb4n);
+    };
     // bit 0: the literal is true (its variable's bit of word w, xor the sign, bit 0 of xs; the
     // other bits are don't-care)
     auto lit_true = [](uint32_t w, uint32_t xs) -> uint32_t { return __builtin_amdgcn_ubfe(w, xs >> 1, 1u) ^ xs; };
@@ -457,7 +466,7 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
     // only then are the lookups consumed; the middle slots follow, each only for the clauses
     // not yet satisfied.  So a wave waits for one literal load and one or two lookup round
     // trips per chunk, not for a chain of them.
-    auto run_chunks_t = [&](auto al, auto nt, uint64_t gbeg, uint64_t gend, uint32_t pt) {
+    auto run_chunks_t = [&](auto al, auto nt, auto kl, uint64_t gbeg, uint64_t gend, uint32_t pt) {
         uint64_t g = gbeg + wave;
         if (g >= gend) return;
         // L2 lookups through a buffer descriptor over the assignment from the window on: its
@@ -493,7 +502,15 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
                 uint32_t ga[4], la[4], gb[4], lb[4];
                 const bool all4[4] = {true, true, true, true};
                 lookup4(al, nt, rsW, wb4n, xa, all4, ga, la);
-                if constexpr (K > 1) lookup4(al, nt, rsW, wb4n, xb, all4, gb, lb);
+                if constexpr (K > 1) {
+                    if constexpr (decltype(kl)::value) {
+                        lookup4_lds(wb4n, xb, lb);
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) gb[q] = 0u;
+                    } else {
+                        lookup4(al, nt, rsW, wb4n, xb, all4, gb, lb);
+                    }
+                }
                 // (scheduling barriers keep the next chunk's loads between the lookups' issue
                 // and their use)
                 __builtin_amdgcn_sched_barrier(0);
@@ -556,20 +573,23 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
             for (int j = 0; j < K; ++j) x[j] = xn[j];
         }
     };
-    auto run_chunks = [&](uint64_t gbeg, uint64_t gend, uint32_t pt) {
-        if (all_lds) run_chunks_t(std::true_type{}, std::false_type{}, gbeg, gend, pt);
-        else if (cv.lits_nt) run_chunks_t(std::false_type{}, std::true_type{}, gbeg, gend, pt);
-        else run_chunks_t(std::false_type{}, std::false_type{}, gbeg, gend, pt);
+    auto run_chunks = [&](uint64_t gbeg, uint64_t gend, uint32_t pt, bool kl) {
+        if (all_lds) run_chunks_t(std::true_type{}, std::false_type{}, std::false_type{}, gbeg, gend, pt);
+        else if (cv.lits_nt && kl) run_chunks_t(std::false_type{}, std::true_type{}, std::true_type{}, gbeg, gend, pt);
+        else if (cv.lits_nt) run_chunks_t(std::false_type{}, std::true_type{}, std::false_type{}, gbeg, gend, pt);
+        else if (kl) run_chunks_t(std::false_type{}, std::false_type{}, std::true_type{}, gbeg, gend, pt);
+        else run_chunks_t(std::false_type{}, std::false_type{}, std::false_type{}, gbeg, gend, pt);
     };
     for (uint32_t pt = t0; pt < t1; pt += HYB_MAX_TILES) {
         const uint32_t pe = min(t1, pt + HYB_MAX_TILES);
         if (threadIdx.x < HYB_MAX_TILES) s_tcnt[threadIdx.x] = 0;
         __syncthreads();  // also publishes the LDS fill
-      // segments of tiles with one window; the LDS is refilled between them
+      // segments of tiles with one window (and one bit 31: slot K-1 in LDS only); the LDS is
+      // refilled between windows
       for (uint32_t sa = pt; sa < pe;) {
-        const uint32_t ws = window(sa);
+        const uint32_t wk = win_key(sa), ws = wk & 0x7FFFFFFFu;
         uint32_t se = sa + 1;
-        while (se < pe && window(se) == ws) ++se;
+        while (se < pe && win_key(se) == wk) ++se;
         if (ws != wb) {
             __syncthreads();  // every wave is done with the old window
             fill(ws);
@@ -580,7 +600,7 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
         const uint64_t gbeg = (uint64_t)sa * (TILE / CHUNK);
         const uint64_t gend = min((uint64_t)se * (TILE / CHUNK), (m + CHUNK - 1) / CHUNK);
         sa = se;
-        run_chunks(gbeg, gend, pt);
+        run_chunks(gbeg, gend, pt, (wk >> 31) != 0u);
       }
         __syncthreads();
         if (threadIdx.x < pe - pt) {
@@ -3847,7 +3867,29 @@ hipError_t launch_tail(const ClauseView& cv, const LoopBuffers& b, uint32_t firs
     return hipGetLastError();
 }
 
-hipError_t launch_rr_mis(const ClauseView& cv, const LoopBuffers& b, hipStream_t s) {
+// grids of the fixpoint kernels
+struct FpGrids {
+    uint32_t gb, gl, gr;
+    bool narrow;
+};
+static FpGrids fp_grids(const LoopBuffers& b) {
+    FpGrids g;
+    g.narrow = b.rr_k >= 1 && b.rr_k <= 4;
+    g.gb = (uint32_t)std::min<uint64_t>((b.m + FP_B - 1) / FP_B + 1, FP_COUNT_GRID);
+    g.gl = (uint32_t)std::min<uint64_t>((b.m + FP_THREADS - 1) / FP_THREADS + 1, 2048);
+    // workgroups of the grid-stride round kernels (2048)
+    g.gr = (uint32_t)std::min<uint64_t>((b.m + FP_RT - 1) / FP_RT + 1, 2048);
+    return g;
+}
+
+static void fp_turns(const ClauseView& cv, const LoopBuffers& b, const FpGrids& g, int test, hipStream_t s) {
+    k_fp_count<<<g.gb, FP_THREADS, 0, s>>>(b, test);
+    k_fp_sched<<<1, 256, 0, s>>>(b, test);
+    if (g.narrow) k_fp_turn<4><<<g.gb, FP_THREADS, 0, s>>>(cv, b);
+    else k_fp_turn<0><<<g.gb, FP_THREADS, 0, s>>>(cv, b);
+}
+
+hipError_t launch_rr_prep(const ClauseView& cv, const LoopBuffers& b, hipStream_t s) {
     if (!b.rr_u || b.rr_T < 2 || b.rr_T > RR_TMAX) return hipErrorInvalidValue;
     if (b.rr_flag) {  // fixed width: violated flags in clause order from the evaluation's lists
         if (cv.k == 0 || !b.rr_tcnt) return hipErrorInvalidValue;
@@ -3860,66 +3902,67 @@ hipError_t launch_rr_mis(const ClauseView& cv, const LoopBuffers& b, hipStream_t
         return hipErrorInvalidValue;
     }
     if (b.n_tiles) k_rr_entries<<<b.n_tiles, 256, 0, s>>>(cv, b);
-    if (b.fp_ctl) {  // the fixpoint passes; k_rr_mw below only if they do not settle
-        if (b.rr_T > FP_TMAX || b.fp_max == 0) return hipErrorInvalidValue;
-        const bool narrow = b.rr_k >= 1 && b.rr_k <= 4;
-        const uint32_t gb = (uint32_t)std::min<uint64_t>((b.m + FP_B - 1) / FP_B + 1, FP_COUNT_GRID);
-        const uint32_t gl = (uint32_t)std::min<uint64_t>((b.m + FP_THREADS - 1) / FP_THREADS + 1, 2048);
-        const uint32_t fp_grid = 2048;  // workgroups of the grid-stride round kernels
-        const uint32_t gr = (uint32_t)std::min<uint64_t>((b.m + FP_RT - 1) / FP_RT + 1, fp_grid);
-        if (!b.fp_pairs || !b.fp_soff || b.n_bkt == 0 || b.n_bkt > BKT_MAX) return hipErrorInvalidValue;
-        const size_t lds_bs = 8ull * b.n_bkt + 2ull * FP_BS_ENT * 8;
-        const size_t lds_bb = fp_bbuild_lds_bytes(b.bkt_width);
-        int dev;
-        if (attr_pending(ATTR_FP, dev)) {
-            hipError_t e = hipFuncSetAttribute((const void*)k_fp_bscatter<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               (int)(8ull * BKT_MAX + 2ull * FP_BS_ENT * 8));
-            if (e == hipSuccess)
-                e = hipFuncSetAttribute((const void*)k_fp_bscatter<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        (int)(8ull * BKT_MAX + 2ull * FP_BS_ENT * 8));
-            if (e == hipSuccess)
-                e = hipFuncSetAttribute((const void*)k_fp_bbuild, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                        160 * 1024 - 1024);
-            if (e != hipSuccess) return e;
-            attr_mark(ATTR_FP, dev);
-        }
-        hipError_t e = hipMemsetAsync(b.fp_owner, 0xFF, (size_t)b.n_vars * 8, s);
-        if (e == hipSuccess) e = hipMemsetAsync(b.fp_cov, 0, (size_t)b.n_vars, s);
+    if (!b.fp_ctl) return hipGetLastError();
+    // the fixpoint passes: iteration set-up, claimant lists, first guess
+    if (b.rr_T > FP_TMAX) return hipErrorInvalidValue;
+    if (!b.fp_pairs || !b.fp_soff || b.n_bkt == 0 || b.n_bkt > BKT_MAX) return hipErrorInvalidValue;
+    const FpGrids g = fp_grids(b);
+    const size_t lds_bs = 8ull * b.n_bkt + 2ull * FP_BS_ENT * 8;
+    const size_t lds_bb = fp_bbuild_lds_bytes(b.bkt_width);
+    int dev;
+    if (attr_pending(ATTR_FP, dev)) {
+        hipError_t e = hipFuncSetAttribute((const void*)k_fp_bscatter<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)(8ull * BKT_MAX + 2ull * FP_BS_ENT * 8));
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute((const void*)k_fp_bscatter<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    (int)(8ull * BKT_MAX + 2ull * FP_BS_ENT * 8));
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute((const void*)k_fp_bbuild, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    160 * 1024 - 1024);
         if (e != hipSuccess) return e;
-        k_fp_begin<<<1, 256, 0, s>>>(b);
-        const uint32_t gbs = (uint32_t)std::min<uint64_t>((b.m + FP_BS_ENT - 1) / FP_BS_ENT + 1, 512);
-        if (narrow) k_fp_bscatter<4><<<gbs, FP_THREADS, lds_bs, s>>>(cv, b);
-        else k_fp_bscatter<0><<<gbs, FP_THREADS, lds_bs, s>>>(cv, b);
-        k_fp_guess<<<gl, FP_THREADS, 0, s>>>(b);
-        k_fp_bbuild<<<b.n_bkt, FP_BB_THREADS, lds_bb, s>>>(b);
-        auto turns = [&](int test) {
-            k_fp_count<<<gb, FP_THREADS, 0, s>>>(b, test);
-            k_fp_sched<<<1, 256, 0, s>>>(b, test);
-            if (narrow) k_fp_turn<4><<<gb, FP_THREADS, 0, s>>>(cv, b);
-            else k_fp_turn<0><<<gb, FP_THREADS, 0, s>>>(cv, b);
-        };
-        turns(0);
-        for (uint32_t p = 0; p < b.fp_max; ++p) {
-            for (uint32_t r = 0; r < FP_G; ++r) {
-                if (r == 0) {
-                    k_fp_vmin<<<b.n_bkt, FP_THREADS, 0, s>>>(b);
-                    k_fp_vmin_heavy<<<FP_HEAVY_GRID, FP_THREADS, 0, s>>>(b);
-                    if (narrow) k_fp_join<4><<<gr, FP_THREADS, 0, s>>>(cv, b, 0);
-                    else k_fp_join<0><<<gr, FP_THREADS, 0, s>>>(cv, b, 0);
-                } else if (narrow) {
-                    k_fp_claim<4><<<gr, FP_THREADS, 0, s>>>(cv, b, r);
-                    k_fp_join<4><<<gr, FP_THREADS, 0, s>>>(cv, b, r);
-                } else {
-                    k_fp_claim<0><<<gr, FP_THREADS, 0, s>>>(cv, b, r);
-                    k_fp_join<0><<<gr, FP_THREADS, 0, s>>>(cv, b, r);
-                }
-            }
-            if (narrow) k_fp_tail<4><<<1, 1024, 0, s>>>(cv, b);
-            else k_fp_tail<0><<<1, 1024, 0, s>>>(cv, b);
-            turns(1);
-        }
+        attr_mark(ATTR_FP, dev);
     }
-    // clause variables held in registers while scanning: 4 for instances of width <= 4
+    hipError_t e = hipMemsetAsync(b.fp_owner, 0xFF, (size_t)b.n_vars * 8, s);
+    if (e == hipSuccess) e = hipMemsetAsync(b.fp_cov, 0, (size_t)b.n_vars, s);
+    if (e != hipSuccess) return e;
+    k_fp_begin<<<1, 256, 0, s>>>(b);
+    const uint32_t gbs = (uint32_t)std::min<uint64_t>((b.m + FP_BS_ENT - 1) / FP_BS_ENT + 1, 512);
+    if (g.narrow) k_fp_bscatter<4><<<gbs, FP_THREADS, lds_bs, s>>>(cv, b);
+    else k_fp_bscatter<0><<<gbs, FP_THREADS, lds_bs, s>>>(cv, b);
+    k_fp_guess<<<g.gl, FP_THREADS, 0, s>>>(b);
+    k_fp_bbuild<<<b.n_bkt, FP_BB_THREADS, lds_bb, s>>>(b);
+    fp_turns(cv, b, g, 0, s);
+    return hipGetLastError();
+}
+
+hipError_t launch_rr_passes(const ClauseView& cv, const LoopBuffers& b, uint32_t n, hipStream_t s) {
+    if (!b.fp_ctl) return hipSuccess;
+    const FpGrids g = fp_grids(b);
+    for (uint32_t p = 0; p < n; ++p) {
+        for (uint32_t r = 0; r < FP_G; ++r) {
+            if (r == 0) {
+                k_fp_vmin<<<b.n_bkt, FP_THREADS, 0, s>>>(b);
+                k_fp_vmin_heavy<<<FP_HEAVY_GRID, FP_THREADS, 0, s>>>(b);
+                if (g.narrow) k_fp_join<4><<<g.gr, FP_THREADS, 0, s>>>(cv, b, 0);
+                else k_fp_join<0><<<g.gr, FP_THREADS, 0, s>>>(cv, b, 0);
+            } else if (g.narrow) {
+                k_fp_claim<4><<<g.gr, FP_THREADS, 0, s>>>(cv, b, r);
+                k_fp_join<4><<<g.gr, FP_THREADS, 0, s>>>(cv, b, r);
+            } else {
+                k_fp_claim<0><<<g.gr, FP_THREADS, 0, s>>>(cv, b, r);
+                k_fp_join<0><<<g.gr, FP_THREADS, 0, s>>>(cv, b, r);
+            }
+        }
+        if (g.narrow) k_fp_tail<4><<<1, 1024, 0, s>>>(cv, b);
+        else k_fp_tail<0><<<1, 1024, 0, s>>>(cv, b);
+        fp_turns(cv, b, g, 1, s);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_rr_finish(const ClauseView& cv, const LoopBuffers& b, hipStream_t s) {
+    // the batch kernel decides an iteration the fixpoint passes did not settle (or every
+    // iteration without them); clause variables held in registers: 4 for widths <= 4
     if (!b.rr_ctl || b.rr_mw == 0 || b.rr_mw > RR_MW_MAX) return hipErrorInvalidValue;
     if (b.rr_k >= 1 && b.rr_k <= 4) k_rr_mw<4, 4><<<b.rr_mw, 64, sizeof(RRMwLds), s>>>(cv, b);
     else k_rr_mw<8, 2><<<b.rr_mw, 64, sizeof(RRMwLds), s>>>(cv, b);

@@ -101,9 +101,15 @@ struct alll_ctx {
     // device a batch behind instead of freezing at the last read); an assignment set by the
     // caller makes it unknown (treated as large).
     uint64_t hint_u = ~0ull, hint_iter = 0;
-    uint32_t hint_rounds = 0;     // the last state read's tail_rounds (round robin: fixpoint passes)
-    uint32_t fp_max_long = 0;     // round robin: passes of the long graph variant (iterations that needed many)
-    uint32_t fp_long_at = FP_LONG_AT;  // ... chosen after an iteration with more passes (ALLL_RR_FP_LONG_AT)
+    // Round robin with the fixpoint passes: every iteration is a graph of the evaluation, the
+    // set-up and rr_p passes, then (host-driven, after reading the pass state) single-pass
+    // graphs until the passes settle (at most fp_max), then the finishing graph (k_rr_mw when
+    // they did not, resample).  rr_p = the passes the last iteration needed.
+    uint32_t rr_p = 8;
+    std::vector<hipGraph_t> rr_graph;         // every captured round-robin graph (destroyed at the end)
+    std::vector<hipGraphExec_t> rr_pre;       // [P]: evaluation .. set-up + P passes
+    hipGraphExec_t rr_more = nullptr, rr_post = nullptr;
+    uint32_t* h_fp = nullptr;                 // pinned copy of RRFpCtl {state, nu, fp_iter}
     DevState* h_async = nullptr;  // pinned
     hipEvent_t ev_async = nullptr;
     bool async_pending = false;
@@ -282,7 +288,6 @@ int read_state(alll_ctx* c) {
     HIP_TRY(hipStreamSynchronize(c->stream));
     c->hint_u = c->h_state->u_total;
     c->hint_iter = c->h_state->n_iter;
-    c->hint_rounds = c->h_state->tail_rounds;
     c->async_pending = false;  // (the stream is drained: this read is newer)
     if (c->h_state->error == 4)
         return fail(ALLL_ERR_HIP, "round-robin MIS: a grid barrier of k_rr_mw timed out (its %u workgroups "
@@ -334,9 +339,7 @@ int host_exchange(alll_ctx* c, int op, void* dev, size_t bytes, size_t own_off) 
 // skewed instances, see create).
 int round0_variant(const alll_ctx* c) {
     const uint64_t u = c->hint_u;
-    // round robin: the long fixpoint graph (fp_max_long passes) after an iteration that needed
-    // more than FP_LONG_AT passes (or fell back to the batch kernels)
-    if (c->b.rr_T) return c->b.fp_ctl && c->fp_max_long > c->b.fp_max && c->hint_rounds > c->fp_long_at ? 1 : 0;
+    if (c->b.rr_T) return 0;  // (round robin: launch_rr_iteration)
     if (c->b.pairs && (c->hint_iter == 0 || u >= c->bucket_min_u)) return 1;
     // few violated clauses (the end of a converging solve): round 0 on the grid, the rest in
     // the one-workgroup tail -- 6 launches per iteration instead of 12, each ~4.5 us even
@@ -359,7 +362,6 @@ void refresh_hint(alll_ctx* c) {
     }
     c->hint_u = c->h_async->u_total;
     c->hint_iter = c->h_async->n_iter;
-    c->hint_rounds = c->h_async->tail_rounds;
     c->async_pending = false;
 }
 
@@ -396,10 +398,9 @@ int enqueue_iteration(alll_ctx* c, hipEvent_t* marks, int variant) {
     // variables, not the round robin): one launch less
     const bool fused = variant == 1 && !xchg && !c->b.rr_T;
     if (!fused) HIP_TRY(launch_reduce(c->b, 0, s));
-    if (c->b.rr_T) {
-        LoopBuffers lb = c->b;
-        if (variant == 1) lb.fp_max = c->fp_max_long;
-        HIP_TRY(launch_rr_mis(c->cv, lb, s));
+    if (c->b.rr_T) {  // (without the fixpoint passes: k_rr_mw decides every iteration)
+        HIP_TRY(launch_rr_prep(c->cv, c->b, s));
+        HIP_TRY(launch_rr_finish(c->cv, c->b, s));
     } else {
         const uint32_t rounds = variant == 2 ? 1u : c->grid_rounds;
         for (uint32_t r = 0; r < rounds; ++r) {
@@ -424,6 +425,123 @@ int enqueue_iteration(alll_ctx* c, hipEvent_t* marks, int variant) {
     }
     if (marks) HIP_TRY(hipEventRecord(marks[4], s));
     return ALLL_OK;
+}
+
+// Round robin with the fixpoint passes: the pieces of one iteration.
+//   pre(P):  evaluation [+ exchange] + reduce + scan entries + set-up + P passes
+//   more:    one pass
+//   post:    k_rr_mw (only if the passes did not settle) + resample
+int enqueue_rr_piece(alll_ctx* c, hipEvent_t* marks, int piece, uint32_t passes) {
+    hipStream_t s = c->stream;
+    const bool xchg = c->world > 1 || c->comm;
+    if (piece == 0) {
+        if (marks) HIP_TRY(hipEventRecord(marks[0], s));
+        HIP_TRY(eval_launch(c, c->own_begin, c->own_end, true));
+        if (marks) HIP_TRY(hipEventRecord(marks[1], s));
+        if (xchg) {
+            const size_t words = (size_t)c->tiles_per_rank * TILE_WORDS;
+            if (c->comm) {
+                NCCL_TRY(ncclAllGather(c->b.vmask + (size_t)c->rank * words, c->b.vmask, words, ncclUint64,
+                                       c->comm, s));
+            } else {
+                int rc = host_exchange(c, ALLL_XCHG_ALLGATHER, c->b.vmask, words * 8, (size_t)c->rank * words * 8);
+                if (rc) return rc;
+            }
+            HIP_TRY(launch_collect(c->cv, c->b, c->own_begin, c->own_end, s));
+        }
+        if (marks) HIP_TRY(hipEventRecord(marks[2], s));
+        HIP_TRY(launch_reduce(c->b, 0, s));
+        HIP_TRY(launch_rr_prep(c->cv, c->b, s));
+        HIP_TRY(launch_rr_passes(c->cv, c->b, passes, s));
+    } else if (piece == 1) {
+        HIP_TRY(launch_rr_passes(c->cv, c->b, passes, s));
+    } else {
+        HIP_TRY(launch_rr_finish(c->cv, c->b, s));
+        if (marks) HIP_TRY(hipEventRecord(marks[3], s));
+        if (c->allreduce && xchg) {
+            HIP_TRY(launch_resample(c->cv, c->b, c->own_begin, c->own_end, true, s));
+            if (c->comm) {
+                NCCL_TRY(ncclAllReduce(c->b.delta, c->b.delta, c->b.n_words, ncclUint32, ncclSum, c->comm, s));
+            } else {
+                int rc = host_exchange(c, ALLL_XCHG_ALLREDUCE_SUM_U32, c->b.delta, (size_t)c->b.n_words * 4, 0);
+                if (rc) return rc;
+            }
+            HIP_TRY(launch_apply_delta(c->b, s));
+        } else {
+            HIP_TRY(launch_resample(c->cv, c->b, c->own_begin, c->own_end, false, s));
+        }
+        if (marks) HIP_TRY(hipEventRecord(marks[4], s));
+    }
+    return ALLL_OK;
+}
+
+// captured once per (piece, passes); nullptr when the loop launches eagerly
+int rr_graph_of(alll_ctx* c, int piece, uint32_t passes, hipGraphExec_t* out) {
+    *out = nullptr;
+    hipGraphExec_t* slot = piece == 0 ? &c->rr_pre[passes] : piece == 1 ? &c->rr_more : &c->rr_post;
+    if (!c->use_graph) return ALLL_OK;
+    if (*slot) { *out = *slot; return ALLL_OK; }
+    hipError_t e = hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal);
+    if (e != hipSuccess) {
+        c->use_graph = false;
+        c->graph_note = std::string("hipStreamBeginCapture: ") + hipGetErrorString(e);
+        (void)hipGetLastError();
+        return ALLL_OK;
+    }
+    const int rc = enqueue_rr_piece(c, nullptr, piece, passes);
+    hipGraph_t g = nullptr;
+    e = hipStreamEndCapture(c->stream, &g);
+    if (rc != ALLL_OK || e != hipSuccess || !g) {
+        if (g) (void)hipGraphDestroy(g);
+        c->graph_note = rc != ALLL_OK ? "capture of the iteration failed: " + g_err
+                                      : std::string("hipStreamEndCapture: ") + hipGetErrorString(e);
+        (void)hipGetLastError();
+        c->use_graph = false;
+        return ALLL_OK;
+    }
+    c->rr_graph.push_back(g);
+    e = hipGraphInstantiate(slot, g, nullptr, nullptr, 0);
+    if (e != hipSuccess) {
+        *slot = nullptr;
+        c->use_graph = false;
+        c->graph_note = std::string("hipGraphInstantiate: ") + hipGetErrorString(e);
+        (void)hipGetLastError();
+        return ALLL_OK;
+    }
+    (void)hipGraphUpload(*slot, c->stream);
+    *out = *slot;
+    return ALLL_OK;
+}
+
+int launch_rr_piece(alll_ctx* c, hipEvent_t* marks, int piece, uint32_t passes) {
+    hipGraphExec_t g = nullptr;
+    int rc;
+    if (!marks && (rc = rr_graph_of(c, piece, passes, &g))) return rc;
+    if (g) {
+        HIP_TRY(hipGraphLaunch(g, c->stream));
+        return ALLL_OK;
+    }
+    return enqueue_rr_piece(c, marks, piece, passes);
+}
+
+// One round-robin iteration with host-driven passes: pre(rr_p), then one pass at a time while
+// the pass state (read back) is still running, at most fp_max in all, then post.  The host
+// reads 12 bytes per decision instead of the GPU running passes after convergence.
+int launch_rr_iteration(alll_ctx* c, hipEvent_t* marks) {
+    const uint32_t cap = c->b.fp_max;
+    uint32_t done = std::min(c->rr_p, cap);
+    int rc;
+    if ((rc = launch_rr_piece(c, marks, 0, done))) return rc;
+    for (;;) {
+        HIP_TRY(hipMemcpyAsync(c->h_fp, c->b.fp_ctl, 12, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        if (c->h_fp[0] != FP_RUN || done >= cap) break;
+        if ((rc = launch_rr_piece(c, marks, 1, 1))) return rc;
+        ++done;
+    }
+    // next iteration: the passes this one needed (fp_iter = passes that changed the picks)
+    if (c->h_fp[0] == FP_FINAL || c->h_fp[0] == FP_DONE) c->rr_p = std::max<uint32_t>(1, std::min(cap, c->h_fp[2] + 1));
+    return launch_rr_piece(c, marks, 2, 0);
 }
 
 int ensure_graph(alll_ctx* c, int variant, int j) {
@@ -463,6 +581,12 @@ int ensure_graph(alll_ctx* c, int variant, int j) {
 
 // n iterations: n / 8 replays of the 8-iteration graph, then one replay per set bit of n % 8
 int launch_iterations(alll_ctx* c, uint64_t n) {
+    if (c->b.rr_T && c->b.fp_ctl) {
+        int rc;
+        for (uint64_t i = 0; i < n; ++i)
+            if ((rc = launch_rr_iteration(c, nullptr))) return rc;
+        return ALLL_OK;
+    }
     refresh_hint(c);
     const int variant = round0_variant(c);
     int rc;
@@ -766,10 +890,11 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
             b.fp_ib = ib;
             b.fp_tb = tb;
             b.fp_max = FP_MAX_DEFAULT;
-            c->fp_max_long = FP_MAX_LONG;
-            if (const char* e = getenv("ALLL_RR_FP_LONG_AT")) c->fp_long_at = (uint32_t)std::max(0, atoi(e));
-            if (const char* e = getenv("ALLL_RR_FP_MAX"))
-                c->fp_max_long = b.fp_max = (uint32_t)std::max(1, std::min(256, atoi(e)));
+            if (const char* e = getenv("ALLL_RR_FP_MAX"))  // tests: iterations left to k_rr_mw mid-run
+                b.fp_max = (uint32_t)std::max(1, std::min(250, atoi(e)));
+            c->rr_p = std::min<uint32_t>(c->rr_p, b.fp_max);
+            c->rr_pre.assign(b.fp_max + 1, nullptr);
+            if (hipHostMalloc((void**)&c->h_fp, 16, 0) != hipSuccess) return bail(fail(ALLL_ERR_OOM, "hipHostMalloc failed"));
         }
     }
     if ((rc = dalloc(c, &b.A, b.n_words + 4))) return bail(rc);  // +4: 16-byte tail loads
@@ -1153,6 +1278,12 @@ int alll_destroy(alll_ctx* c) {
             if (c->graph_exec[v][u]) (void)hipGraphExecDestroy(c->graph_exec[v][u]);
             if (c->graph[v][u]) (void)hipGraphDestroy(c->graph[v][u]);
         }
+    for (auto& g : c->rr_pre)
+        if (g) (void)hipGraphExecDestroy(g);
+    if (c->rr_more) (void)hipGraphExecDestroy(c->rr_more);
+    if (c->rr_post) (void)hipGraphExecDestroy(c->rr_post);
+    for (auto g : c->rr_graph) (void)hipGraphDestroy(g);
+    if (c->h_fp) (void)hipHostFree(c->h_fp);
     if (c->comm) ncclCommDestroy(c->comm);
     for (void* p : c->allocs) (void)hipFree(p);
     for (auto& e : c->ev)
@@ -1360,7 +1491,9 @@ int alll_profile(alll_ctx* c, uint64_t n_iters, alll_phase_times* out) {
     if ((rc = write_limits(c, c->h_state->n_iter + n_iters, ~0ull))) return rc;
     double acc[4] = {0, 0, 0, 0};
     for (uint64_t i = 0; i < n_iters; ++i) {
-        if ((rc = enqueue_iteration(c, c->ev, round0_variant(c)))) return rc;
+        if (c->b.rr_T && c->b.fp_ctl) rc = launch_rr_iteration(c, c->ev);
+        else rc = enqueue_iteration(c, c->ev, round0_variant(c));
+        if (rc) return rc;
         HIP_TRY(hipEventSynchronize(c->ev[4]));
         float t;
         for (int p = 0; p < 4; ++p) {

@@ -12,9 +12,10 @@ caller's vector<ClauseArray*>), bit-exact:
   * ALLL_FLAG_LFMIS keeps the one-set MIS for T > 1.
 
 Every test runs with each way of deciding the MIS: the fixpoint passes (default, DESIGN.md
-§4.3.2; also in the long graph variant), the same passes capped at one or two per iteration (ALLL_RR_FP_MAX, so that most
-iterations fall back to the batch kernel mid-run), and the batch kernel alone (k_rr_mw,
-ALLL_RR_FP=0).
+§4.3.2; host-driven: a first graph with as many passes as the last iteration needed, then one
+pass at a time until they settle), the same passes capped at one or two per iteration
+(ALLL_RR_FP_MAX, so that most iterations fall back to the batch kernel mid-run), and the batch
+kernel alone (k_rr_mw, ALLL_RR_FP=0).
 """
 import glob
 import os
@@ -38,13 +39,11 @@ def gpu(native):
     return True
 
 
-@pytest.fixture(params=["fp", "fp_long", "fp_cap1", "fp_cap2", "mw"], autouse=True)
+@pytest.fixture(params=["fp", "fp_cap1", "fp_cap2", "mw"], autouse=True)
 def rr_kernel(request, monkeypatch):
-    for k in ("ALLL_RR_FP", "ALLL_RR_FP_MAX", "ALLL_RR_FP_LONG_AT"):
+    for k in ("ALLL_RR_FP", "ALLL_RR_FP_MAX"):
         monkeypatch.delenv(k, raising=False)
-    if request.param == "fp_long":  # the long graph variant (48 passes) from the second launch on
-        monkeypatch.setenv("ALLL_RR_FP_LONG_AT", "0")
-    elif request.param.startswith("fp_cap"):
+    if request.param.startswith("fp_cap"):
         monkeypatch.setenv("ALLL_RR_FP_MAX", request.param[-1])
     elif request.param == "mw":
         monkeypatch.setenv("ALLL_RR_FP", "0")
@@ -252,12 +251,10 @@ def test_rr_full_size_c2_bit_exact(gpu, oracle_mod, rr_kernel, T):
 
 
 def test_rr_back_to_back_runs_without_sync(gpu, oracle_mod, monkeypatch):
-    """Several run(1) calls with no stats() or synchronisation in between (the asynchronous
-    state copy of one batch is still in flight when the next picks its graph variant), long
-    graph variant from the second launch on: the same trajectory as the oracle."""
+    """Several run(1) calls with no stats() or synchronisation in between (the pass count of
+    one iteration sizes the next one's first graph): the same trajectory as the oracle."""
     from alllsatisfiabilitysolver_amd import Solver, generate_ksat
 
-    monkeypatch.setenv("ALLL_RR_FP_LONG_AT", "0")
     n, m, T, seed = 6000, 24000, 5, 9
     offs, lits = generate_ksat(4, n, m, 3, 0)
     st_o, A_o, rows = oracle_mod.solve(n, offs, lits, seed, max_iters=13, trace=True, T=T)

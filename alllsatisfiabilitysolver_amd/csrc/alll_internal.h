@@ -137,6 +137,12 @@ struct LoopBuffers {
                             // CSR: bit i of word w = position 64w + i; fixed width: word w = the
                             // ballot of slot w % 4 of chunk w / 4, bit i = position
                             // (w / 4) * CHUNK + 4i + w % 4
+    uint64_t* cmask;        // clause-sharded runs whose evaluation order is not clause order (fixed
+                            // width, ragged): the violated bitmask in clause order, bit c % 64 of
+                            // word c / 64 (k_cmark sets the own shard's bits; the all-gathered
+                            // mask gives the other shards' lists, k_collect); nullptr = vmask
+    uint32_t* xcount;       // clause-sharded verify: the own shard's violated count (u32), summed
+    uint32_t own_begin, own_end;  // this rank's tiles
     uint32_t* tile_cnt;     // undecided violated entries per tile
     uint32_t* stage[2];     // per tile: TILE entries of undecided violated clauses, double
                             // buffered across LFMIS rounds.  Entry = {id, K literals} (fixed
@@ -252,6 +258,8 @@ hipError_t launch_eval_ragged(const ClauseView& cv, const LoopBuffers& b, uint32
                               uint32_t tile_end, bool gated, int n_blocks, hipStream_t s);
 hipError_t launch_collect(const ClauseView& cv, const LoopBuffers& b, uint32_t own_begin,
                           uint32_t own_end, hipStream_t s);
+// clause-sharded: the own shard's violated clauses into cmask (own words cleared first)
+hipError_t launch_cmark(const ClauseView& cv, const LoopBuffers& b, size_t words_per_rank, int rank, hipStream_t s);
 hipError_t launch_reduce(const LoopBuffers& b, int mode, hipStream_t s);
 hipError_t launch_round(const ClauseView& cv, const LoopBuffers& b, uint32_t r, bool last,
                         uint32_t wave_from, hipStream_t s);

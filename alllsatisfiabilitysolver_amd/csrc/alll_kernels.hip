@@ -803,6 +803,26 @@ __global__ __launch_bounds__(EVAL_THREADS) void k_eval_csr(ClauseView cv, LoopBu
     stamp_eval_end(b, gated);
 }
 
+// Clause-sharded, evaluation order != clause order: the own shard's violated clauses set their
+// bits of the clause-order mask (a wave per own tile, from the evaluation's raw entries), which
+// is all-gathered instead of the evaluation-order bitmask.
+template <int K>
+__global__ __launch_bounds__(256) void k_cmark(ClauseView cv, LoopBuffers b) {
+    if (eval_gate_closed(b.state)) return;
+    constexpr int S = Ent<K>::S;
+    const uint32_t tile = b.own_begin + blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (tile >= b.own_end) return;
+    const uint32_t cnt = b.tile_cnt[tile];
+    const uint32_t* lin = b.stage[0] + (uint64_t)tile * TILE * S;
+    for (uint32_t i = lane; i < cnt; i += 64) {
+        Ent<K> e;
+        load_ent<K>(e, lin + (uint64_t)i * S);
+        if constexpr (K > 0) ent_unpack<K>(cv, e);
+        else if (cv.perm) e.w[0] = cv.perm[e.w[0]];
+        atomicOr(reinterpret_cast<unsigned long long*>(&b.cmask[e.w[0] >> 6]), 1ull << (e.w[0] & 63u));
+    }
+}
+
 // Multi-GPU: tiles owned by other ranks get their violated lists from the all-gathered
 // bitmask (evaluation positions; fixed K fetches the literals from the transposed store).
 // Thread t takes 16 bits of word t / 4 of the tile: all bitmask loads are issued at once, a
@@ -819,8 +839,10 @@ __global__ __launch_bounds__(EVAL_THREADS) void k_collect(ClauseView cv, LoopBuf
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint64_t w = (uint64_t)tile * TILE_WORDS + (threadIdx.x >> 2);
     const uint32_t sl = (threadIdx.x & 3u) * 16u;
-    // (bits past m are 0: the evaluation kernels never set them)
-    uint32_t bits = (uint32_t)(b.vmask[w] >> sl) & 0xFFFFu;
+    // (bits past m are 0: the evaluation kernels never set them).  cmask: clause order (the
+    // other ranks' shards are not laid out here: their literals come from the AoS copy)
+    const bool co = b.cmask != nullptr;
+    uint32_t bits = (uint32_t)((co ? b.cmask[w] : b.vmask[w]) >> sl) & 0xFFFFu;
     const uint32_t cnt = (uint32_t)__popc(bits);
     uint32_t incl = cnt;
     for (int o = 1; o < 64; o <<= 1) {
@@ -840,13 +862,20 @@ __global__ __launch_bounds__(EVAL_THREADS) void k_collect(ClauseView cv, LoopBuf
         bits &= bits - 1u;
         // fixed K and ragged: word w of the bitmask holds positions (w / 4) * 256 + 4 * bit +
         // w % 4 (the kernels store their four ballots as they are); CSR: positions 64 * w + bit
-        const uint64_t p = (K > 0 || cv.rg_off) ? (w >> 2) * CHUNK + 4u * i + (w & 3u) : w * 64 + i;
+        const uint64_t p = (!co && (K > 0 || cv.rg_off)) ? (w >> 2) * CHUNK + 4u * i + (w & 3u) : w * 64 + i;
         Ent<K> e;
         if constexpr (K > 0) {
-            const uint32_t* tp = cv.lits_t + (p / CHUNK) * CHUNK * K + (p % CHUNK);
             uint32_t t[K];
+            if (co) {  // clause p: AoS literals with the clause id's pieces packed as the evaluation's
+                const uint32_t idm = cv.id_bits ? (1u << cv.id_bits) - 1u : 0u;
 #pragma unroll
-            for (int j = 0; j < K; ++j) t[j] = tp[j * CHUNK];
+                for (int j = 0; j < K; ++j)
+                    t[j] = cv.lits[p * K + j] | (cv.id_bits ? (((uint32_t)(p >> (j * cv.id_bits)) & idm) << cv.id_shift) : 0u);
+            } else {
+                const uint32_t* tp = cv.lits_t + (p / CHUNK) * CHUNK * K + (p % CHUNK);
+#pragma unroll
+                for (int j = 0; j < K; ++j) t[j] = tp[j * CHUNK];
+            }
             make_ent<K>(e, p, t);
         } else {
             e.w[0] = (uint32_t)p;
@@ -878,7 +907,9 @@ __device__ void reduce_body(const LoopBuffers& b, int mode) {
     }
     unsigned long long acc = 0;
     uint32_t first = ~0u;
-    for (uint32_t t = threadIdx.x; t < b.n_tiles; t += blockDim.x) {
+    // (mode 1, the standalone count: this rank's tiles, the only ones it evaluates)
+    const uint32_t t_lo = mode == 1 ? b.own_begin : 0u, t_hi = mode == 1 ? b.own_end : b.n_tiles;
+    for (uint32_t t = t_lo + threadIdx.x; t < t_hi; t += blockDim.x) {
         const uint32_t cnt = b.tile_cnt[t];
         acc += cnt;
         if (cnt && t < first) first = t;
@@ -889,7 +920,11 @@ __device__ void reduce_body(const LoopBuffers& b, int mode) {
     __syncthreads();
     if (threadIdx.x != 0) return;
     const unsigned long long u = s_sum;
-    if (mode == 1) { st->count_out = u; return; }
+    if (mode == 1) {
+        st->count_out = u;
+        if (b.xcount) b.xcount[0] = (uint32_t)u;  // (summed over the ranks by the host)
+        return;
+    }
     if (b.ktime) {
         unsigned long long* ts = time_slot(b, st->n_iter);
         ts[2] = reduce_t0;
@@ -3780,6 +3815,15 @@ hipError_t launch_collect(const ClauseView& cv, const LoopBuffers& b, uint32_t o
                           uint32_t own_end, hipStream_t s) {
     if (b.n_tiles == 0) return hipSuccess;
     ALLL_DISPATCH_K(cv.k, (k_collect<K><<<b.n_tiles, EVAL_THREADS, 0, s>>>(cv, b, own_begin, own_end)));
+    return hipGetLastError();
+}
+
+hipError_t launch_cmark(const ClauseView& cv, const LoopBuffers& b, size_t words_per_rank, int rank, hipStream_t s) {
+    if (!b.cmask) return hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync(b.cmask + words_per_rank * (size_t)rank, 0, words_per_rank * 8, s);
+    if (e != hipSuccess || b.own_end <= b.own_begin) return e;
+    const uint32_t g = (b.own_end - b.own_begin + 3) / 4;
+    ALLL_DISPATCH_K(cv.k, (k_cmark<K><<<g, 256, 0, s>>>(cv, b)));
     return hipGetLastError();
 }
 

@@ -215,10 +215,12 @@ int build_ragged(alll_ctx* c, const alll_problem* prob) {
         const uint64_t blk = (windows && lo != ~0u) ? std::min<uint64_t>(lo / win_vars, 1023) : 0;
         return {(w << 40) | (blk << 30) | (hi & ((1u << 30) - 1)), (uint32_t)cl};
     };
-    for (int r = 0; r < c->world; ++r) {  // every shard sorted on its own (shards are clause ranges)
-        const uint64_t cb0 = std::min<uint64_t>(m, (uint64_t)r * c->tiles_per_rank * TILE);
-        const uint64_t ce0 = std::min<uint64_t>(m, cb0 + (uint64_t)c->tiles_per_rank * TILE);
-        if (ce0 <= cb0) continue;
+    // the own shard only (a clause range; the other ranks' shards keep clause order here: their
+    // lists come from the all-gathered clause-order mask, k_collect)
+    parallel_for(m, nt, [&](uint64_t i) { perm[i] = (uint32_t)i; });
+    {
+        const uint64_t cb0 = std::min<uint64_t>(m, (uint64_t)c->own_begin * TILE);
+        const uint64_t ce0 = std::min<uint64_t>(m, (uint64_t)c->own_end * TILE);
         std::vector<Key> kv(ce0 - cb0);
         parallel_for(ce0 - cb0, nt, [&](uint64_t i) { kv[i] = key_of(cb0 + i); });
         parallel_sort(kv.data(), kv.size(), [](const Key& x, const Key& y) {
@@ -243,7 +245,10 @@ int build_ragged(alll_ctx* c, const alll_problem* prob) {
     if (b.n_words >= (1u << 25)) return fail(ALLL_ERR_UNSUPPORTED, "ragged layout needs n_words < 2^25");
     const uint32_t false_lit = 64u * b.n_words;  // variable 32 * n_words: its word is out of range
     std::vector<uint32_t> t((size_t)acc * CHUNK, false_lit);
-    parallel_for(m, nt, [&](uint64_t p) {
+    const uint64_t own_p0 = std::min<uint64_t>(m, (uint64_t)c->own_begin * TILE);
+    const uint64_t own_p1 = std::min<uint64_t>(m, (uint64_t)c->own_end * TILE);
+    parallel_for(own_p1 - own_p0, nt, [&](uint64_t q) {
+        const uint64_t p = own_p0 + q;
         const uint64_t cl = perm[p], g = p / CHUNK, r = p % CHUNK;
         const uint64_t w = offs[cl + 1] - offs[cl];
         std::vector<uint32_t> tmp(lits + offs[cl], lits + offs[cl] + w);
@@ -259,7 +264,7 @@ int build_ragged(alll_ctx* c, const alll_problem* prob) {
     if (windows) {
         const uint32_t lds_words = std::min<uint32_t>(b.n_words, b.win_words);
         wb.assign(b.n_tiles, 0u);
-        for (uint32_t tt = 0; tt < b.n_tiles; ++tt) {
+        for (uint32_t tt = c->own_begin; tt < c->own_end; ++tt) {
             const uint64_t p = (uint64_t)tt * TILE;
             if (p >= m) break;
             const uint64_t cl = perm[p];
@@ -332,6 +337,23 @@ int host_exchange(alll_ctx* c, int op, void* dev, size_t bytes, size_t own_off) 
     return ALLL_OK;
 }
 
+// Clause-sharded exchange after the evaluation: the violated bitmask pieces are all-gathered
+// (clause order: cmask, marked from the own lists, when the evaluation order is not clause
+// order; else the evaluation's own bitmask), then the other shards' lists are collected.
+int enqueue_exchange(alll_ctx* c, hipStream_t s) {
+    const size_t words = (size_t)c->tiles_per_rank * TILE_WORDS;
+    uint64_t* mask = c->b.cmask ? c->b.cmask : c->b.vmask;
+    if (c->b.cmask) HIP_TRY(launch_cmark(c->cv, c->b, words, c->rank, s));
+    if (c->comm) {
+        NCCL_TRY(ncclAllGather(mask + (size_t)c->rank * words, mask, words, ncclUint64, c->comm, s));
+    } else {
+        int rc = host_exchange(c, ALLL_XCHG_ALLGATHER, mask, words * 8, (size_t)c->rank * words * 8);
+        if (rc) return rc;
+    }
+    HIP_TRY(launch_collect(c->cv, c->b, c->own_begin, c->own_end, s));
+    return ALLL_OK;
+}
+
 // The launch sequence of one iteration (SATInstance.h:260-311).  Every kernel is gated on
 // the device state, so replaying it after convergence is a no-op.
 // Round-0 variant for the next iterations, from the last state read: the bucketed kernels
@@ -383,15 +405,8 @@ int enqueue_iteration(alll_ctx* c, hipEvent_t* marks, int variant) {
     HIP_TRY(eval_launch(c, c->own_begin, c->own_end, true, scatter));
     if (marks) HIP_TRY(hipEventRecord(marks[1], s));
     if (xchg) {
-        const size_t words = (size_t)c->tiles_per_rank * TILE_WORDS;
-        if (c->comm) {
-            NCCL_TRY(ncclAllGather(c->b.vmask + (size_t)c->rank * words, c->b.vmask, words, ncclUint64,
-                                   c->comm, s));
-        } else {
-            int rc = host_exchange(c, ALLL_XCHG_ALLGATHER, c->b.vmask, words * 8, (size_t)c->rank * words * 8);
-            if (rc) return rc;
-        }
-        HIP_TRY(launch_collect(c->cv, c->b, c->own_begin, c->own_end, s));
+        int rc = enqueue_exchange(c, s);
+        if (rc) return rc;
     }
     if (marks) HIP_TRY(hipEventRecord(marks[2], s));
     // the bucketed round 0 runs the reduce in an extra k_bscatter workgroup (one GPU, no hot
@@ -439,15 +454,8 @@ int enqueue_rr_piece(alll_ctx* c, hipEvent_t* marks, int piece, uint32_t passes)
         HIP_TRY(eval_launch(c, c->own_begin, c->own_end, true));
         if (marks) HIP_TRY(hipEventRecord(marks[1], s));
         if (xchg) {
-            const size_t words = (size_t)c->tiles_per_rank * TILE_WORDS;
-            if (c->comm) {
-                NCCL_TRY(ncclAllGather(c->b.vmask + (size_t)c->rank * words, c->b.vmask, words, ncclUint64,
-                                       c->comm, s));
-            } else {
-                int rc = host_exchange(c, ALLL_XCHG_ALLGATHER, c->b.vmask, words * 8, (size_t)c->rank * words * 8);
-                if (rc) return rc;
-            }
-            HIP_TRY(launch_collect(c->cv, c->b, c->own_begin, c->own_end, s));
+            int rc = enqueue_exchange(c, s);
+            if (rc) return rc;
         }
         if (marks) HIP_TRY(hipEventRecord(marks[2], s));
         HIP_TRY(launch_reduce(c->b, 0, s));
@@ -810,6 +818,8 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     c->n_tiles_padded = c->tiles_per_rank * c->world;
     c->own_begin = std::min<uint32_t>(n_tiles, (uint32_t)c->rank * c->tiles_per_rank);
     c->own_end = std::min<uint32_t>(n_tiles, c->own_begin + c->tiles_per_rank);
+    c->b.own_begin = c->own_begin;
+    c->b.own_end = c->own_end;
 
     int rc;
     LoopBuffers& b = c->b;
@@ -1121,11 +1131,12 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
                 }, nt);
                 parallel_for(kv.size(), nt, [&](uint64_t i) { perm[cb0 + i] = kv[i].id; });
             };
-            for (int r = 0; r < c->world; ++r) {  // every rank lays out every shard (replicated lists)
-                const uint64_t cb0 = std::min<uint64_t>(m, (uint64_t)r * c->tiles_per_rank * TILE);
-                const uint64_t ce0 = std::min<uint64_t>(m, cb0 + (uint64_t)c->tiles_per_rank * TILE);
-                if (ce0 > cb0) sort_range(cb0, ce0);
-            }
+            // the own shard only: the other ranks' shards keep clause order (identity perm; their
+            // violated lists come from the all-gathered clause-order mask and the AoS literals)
+            parallel_for(m, nt, [&](uint64_t i) { perm[i] = (uint32_t)i; });
+            const uint64_t cb0 = std::min<uint64_t>(m, (uint64_t)c->own_begin * TILE);
+            const uint64_t ce0 = std::min<uint64_t>(m, (uint64_t)c->own_end * TILE);
+            if (ce0 > cb0) sort_range(cb0, ce0);
         }
         // Packed clause ids: when the literals leave enough bits below the hot flag, slot j of
         // every clause also carries bits [j * id_bits, (j + 1) * id_bits) of its clause id, so
@@ -1149,7 +1160,10 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
         }
         std::vector<uint32_t> t(real_chunks * CHUNK * fixed_k, 0u);
         const uint32_t id_mask = cv.id_bits ? (1u << cv.id_bits) - 1u : 0u;
-        parallel_for(m, host_threads(), [&](uint64_t p2) {
+        const uint64_t own_p0 = std::min<uint64_t>(m, (uint64_t)c->own_begin * TILE);
+        const uint64_t own_p1 = std::min<uint64_t>(m, (uint64_t)c->own_end * TILE);
+        parallel_for(own_p1 - own_p0, host_threads(), [&](uint64_t q) {  // (the own shard's positions)
+            const uint64_t p2 = own_p0 + q;
             uint32_t tmp[MAX_FIXED_K];
             const uint64_t cl = perm[p2];
             for (int j = 0; j < fixed_k; ++j)
@@ -1185,7 +1199,7 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
         if (windows && m) {  // LDS window of every tile: the block of its first clause's smallest variable
             const uint32_t lds_words = std::min<uint32_t>(b.n_words, b.win_words);
             std::vector<uint32_t> wb(n_tiles, 0u);
-            for (uint32_t tt = 0; tt < n_tiles; ++tt) {
+            for (uint32_t tt = c->own_begin; tt < c->own_end; ++tt) {
                 const uint64_t p = (uint64_t)tt * TILE;
                 if (p >= m) break;
                 const uint64_t cl = perm[p];
@@ -1195,7 +1209,8 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
             }
             // bit 31: every clause of the tile has its smallest variable in the window (all but
             // the tiles at block boundaries), so k_eval_hybrid reads slot K-1 from LDS only
-            parallel_for(n_tiles, host_threads(), [&](uint64_t tt) {
+            parallel_for(c->own_end - c->own_begin, host_threads(), [&](uint64_t q) {
+                const uint64_t tt = c->own_begin + q;
                 bool all_in = true;
                 for (uint64_t p = tt * TILE; p < std::min<uint64_t>(m, (tt + 1) * TILE) && all_in; ++p) {
                     const uint64_t cl = perm[p];
@@ -1244,6 +1259,11 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     // communicator that runs the multi-GPU exchange path on one GPU)
     bool zero_id = true;
     for (int i = 0; i < 128; ++i) zero_id &= opt.comm_id[i] == 0;
+    if ((c->world > 1 || !zero_id) && (cv.k > 0 || cv.rg_off)) {
+        // the exchange's clause-order mask (this rank laid out its own shard only)
+        if ((rc = dalloc(c, &b.cmask, (size_t)c->n_tiles_padded * TILE_WORDS))) return bail(rc);
+    }
+    if (c->world > 1 && (rc = dalloc(c, &b.xcount, 4))) return bail(rc);
     if (c->world > 1 || !zero_id) {
         const bool zero = zero_id;
         if (!zero) {
@@ -1360,13 +1380,28 @@ int alll_synchronize(alll_ctx* c) {
 int alll_verify(alll_ctx* c, int* valid, uint64_t* n_violated) {
     if (!c) return fail(ALLL_ERR_INVALID_ARG, "null context");
     HIP_TRY(hipSetDevice(c->device));
-    // every rank holds the full clause set and the full assignment: evaluate all tiles
-    HIP_TRY(eval_launch(c, 0, c->b.n_tiles, false));
+    // every rank evaluates its own shard (the only one laid out for its evaluation); the
+    // counts are summed over the ranks
+    HIP_TRY(eval_launch(c, c->own_begin, c->own_end, false));
     HIP_TRY(launch_reduce(c->b, 1, c->stream));
+    uint64_t count = 0;
+    if (c->world > 1) {
+        if (c->comm) {
+            NCCL_TRY(ncclAllReduce(c->b.xcount, c->b.xcount, 1, ncclUint32, ncclSum, c->comm, c->stream));
+        } else {
+            int rc = host_exchange(c, ALLL_XCHG_ALLREDUCE_SUM_U32, c->b.xcount, 4, 0);
+            if (rc) return rc;
+        }
+        uint32_t x = 0;
+        HIP_TRY(hipMemcpyAsync(&x, c->b.xcount, 4, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        count = x;
+    }
     int rc = read_state(c);
     if (rc) return rc;
-    if (valid) *valid = c->h_state->count_out == 0;
-    if (n_violated) *n_violated = c->h_state->count_out;
+    if (c->world == 1) count = c->h_state->count_out;
+    if (valid) *valid = count == 0;
+    if (n_violated) *n_violated = count;
     return ALLL_OK;
 }
 
@@ -1417,7 +1452,10 @@ int alll_get_violated_mask(alll_ctx* c, uint64_t* out, uint64_t n_words) {
     if (n_words < need || (!out && need)) return fail(ALLL_ERR_INVALID_ARG, "need %llu words", (unsigned long long)need);
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    if (!c->perm.empty()) {  // fixed width: device bits are chunk ballots in evaluation order
+    if (c->b.cmask && c->world > 1) {  // clause-sharded: the last all-gathered clause-order mask
+        if (need) HIP_TRY(hipMemcpy(out, c->b.cmask, need * 8, hipMemcpyDeviceToHost));
+        if (c->m & 63) out[need - 1] &= (1ull << (c->m & 63)) - 1ull;
+    } else if (!c->perm.empty()) {  // fixed width: device bits are chunk ballots in evaluation order
         std::vector<uint64_t> ev((c->m + CHUNK - 1) / CHUNK * 4);
         HIP_TRY(hipMemcpy(ev.data(), c->b.vmask, ev.size() * 8, hipMemcpyDeviceToHost));
         std::fill(out, out + need, 0ull);

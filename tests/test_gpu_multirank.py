@@ -39,7 +39,7 @@ def worker(rank, world, port, spec, flags, out_q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     n, m, k, kind, seed, K = spec[:6]
     T = spec[6] if len(spec) > 6 else 1
-    offs, lits = generate_ksat(1, n, m, k, kind)
+    offs, lits = make_instance(n, m, k, kind)
     try:
         with Solver(n, offs, lits, seed=seed, device=0, rank=rank, world=world, flags=flags,
                     exchange=gloo_exchange(), n_threads=T) as s:
@@ -56,7 +56,27 @@ def worker(rank, world, port, spec, flags, out_q):
     dist.destroy_process_group()
 
 
-def run_world(world, spec, flags):
+def make_instance(n, m, k, kind):
+    if isinstance(k, tuple):  # mixed widths (the ragged evaluation layout)
+        from alllsatisfiabilitysolver_amd import generate_mixed
+
+        return generate_mixed(1, n, m, *k)
+    from alllsatisfiabilitysolver_amd import generate_ksat
+
+    return generate_ksat(1, n, m, k, kind)
+
+
+def run_world(world, spec, flags, env=None):
+    for key, v in (env or {}).items():  # (inherited by the spawned ranks)
+        os.environ[key] = v
+    try:
+        return _run_world(world, spec, flags)
+    finally:
+        for key in env or {}:
+            del os.environ[key]
+
+
+def _run_world(world, spec, flags):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
@@ -82,7 +102,14 @@ SPECS = {
     # the round robin of T = 4 / 7 sets (the fixpoint passes) on every rank of the sharded loop
     "small_rr4": (7000, 28000, 3, 0, 5, 8, 4),
     "c2_rr7": (1_000_000, 4_000_000, 3, 0, 1, 2, 7),
+    # clause ids not packed into the literals (evaluation positions + perm on the own shard)
+    "small_positions": (7000, 28000, 3, 0, 5, 8),
+    # mixed widths 2-12: the ragged evaluation layout (own shard), CSR LFMIS
+    "ragged": (5000, 20000, (2, 12), 0, 5, 6),
+    # 8-SAT: the wide fixed-width entries
+    "k8": (40000, 60000, 8, 0, 3, 4),
 }
+ENV = {"small_positions": {"ALLL_PACKED_IDS": "0"}}
 
 
 @pytest.mark.parametrize("world,mode,spec_name", [(2, "allgather", "small"), (2, "allreduce", "small"),
@@ -90,16 +117,20 @@ SPECS = {
                                                   (2, "allgather", "windows"), (2, "allgather", "long"),
                                                   (2, "allreduce", "long"), (2, "allgather", "c2"),
                                                   (2, "allreduce", "c2"), (2, "allgather", "small_rr4"),
-                                                  (3, "allreduce", "small_rr4"), (2, "allgather", "c2_rr7")])
+                                                  (3, "allreduce", "small_rr4"), (2, "allgather", "c2_rr7"),
+                                                  (3, "allgather", "small_positions"), (2, "allgather", "ragged"),
+                                                  (3, "allreduce", "ragged"), (2, "allgather", "k8")])
 def test_sharded_solver_matches_oracle(oracle_mod, native, world, mode, spec_name):
+    """Every rank lays out its own shard only; the other shards' violated lists come from the
+    all-gathered clause-order mask and the AoS literals (k_cmark / k_collect)."""
     o = oracle_mod
     spec = SPECS[spec_name]
     n, m, k, kind, seed, K = spec[:6]
     T = spec[6] if len(spec) > 6 else 1
     flags = native.FLAG_EXCHANGE_ALLREDUCE if mode == "allreduce" else 0
-    offs, lits = o.generate_ksat(1, n, m, k, kind)
+    offs, lits = make_instance(n, m, k, kind)
     st_o, A_o, rows = o.solve(n, offs, lits, seed, max_iters=K + 1, trace=True, T=T)
-    res = run_world(world, spec, flags)
+    res = run_world(world, spec, flags, ENV.get(spec_name))
     for rank, traj, st, mis, err in res:
         assert err is None, f"rank {rank}: {err}"
         for i, (it, nu, nm, dres, A_after) in enumerate(rows):

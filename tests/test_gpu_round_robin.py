@@ -266,3 +266,29 @@ def test_rr_back_to_back_runs_without_sync(gpu, oracle_mod, monkeypatch):
         assert st["n_iterations"] == 12
         assert st["n_resamples"] == sum(r[3] for r in rows)
         np.testing.assert_array_equal(s.assignment_words(), rows[-1][4])
+
+
+RR_LAYOUTS = {"positions": {"ALLL_PACKED_IDS": "0"},  # clause ids via perm (k_rr_mark's unpack)
+              "small_windows": {"ALLL_EVAL_WINDOWS": "1", "ALLL_WIN_WORDS": "64"},
+              "nt_windows": {"ALLL_EVAL_WINDOWS": "1", "ALLL_WIN_WORDS": "64", "ALLL_EVAL_NT": "1"}}
+
+
+@pytest.mark.parametrize("layout", list(RR_LAYOUTS))
+@pytest.mark.parametrize("name,T", [("ratio4", 7), ("k5_multi_tile", 16)])
+def test_rr_on_hybrid_eval_layouts(gpu, oracle_mod, name, T, layout, monkeypatch):
+    """The round robin over the fixed-width (hybrid) evaluation: its per-tile lists in
+    evaluation order become clause-order flags (k_rr_mark) under every evaluation layout."""
+    from alllsatisfiabilitysolver_amd import Solver
+
+    n, offs, lits = _instance(name)
+    seed, K = 17, 10
+    st_o, A_o, rows = oracle_mod.solve(n, offs, lits, seed, max_iters=K, trace=True, T=T)
+    for k, v in RR_LAYOUTS[layout].items():
+        monkeypatch.setenv(k, v)
+    with Solver(n, offs, lits, seed=seed, n_threads=T) as s:
+        for k in RR_LAYOUTS[layout]:
+            monkeypatch.delenv(k)
+        for it, nu, nm, dres, A_after in rows:
+            s.run(1)
+            assert s.stats()["n_violated"] == nu, f"iter {it}"
+            np.testing.assert_array_equal(s.assignment_words(), A_after, err_msg=f"A after iter {it}")

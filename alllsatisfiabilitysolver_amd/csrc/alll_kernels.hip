@@ -2791,8 +2791,8 @@ constexpr uint32_t FP_RT = 256;        // entries per round tile (one per thread
 constexpr uint32_t FP_LDS_SEG_T = 32;     // k_fp_turn keeps the schedule in LDS up to this many sets
 constexpr uint32_t FP_COUNT_GRID = 1024;
 constexpr uint32_t FP_HEAVY = 64;         // claimant lists longer than this are reduced by waves
-constexpr uint32_t FP_SEG = 2048;         // claimants per wave of k_fp_vmin_heavy
-constexpr uint32_t FP_HEAVY_GRID = 512;   // workgroups of k_fp_vmin_heavy
+constexpr uint32_t FP_SEG = 2048;         // claimants per wave of k_fp_vmin's long-list workgroups
+constexpr uint32_t FP_HEAVY_GRID = 512;   // ... their number (instances with hot variables)
 constexpr uint32_t FP_SCHED_LDS_BLK = 4096;  // k_fp_sched keeps the block offsets in LDS up to this many blocks  // workgroups of k_fp_count / k_fp_turn (grid-stride over blocks)
 
 __device__ __forceinline__ unsigned long long fp_key(const LoopBuffers& b, uint32_t ep, uint32_t turn, uint32_t i) {
@@ -3116,38 +3116,38 @@ __global__ __launch_bounds__(FP_BB_THREADS) void k_fp_bbuild(LoopBuffers b) {
     if (tid == 0) b.fp_sbcnt[bk] = s_ns;
 }
 
-// round 0 of a pass for the variables with more than FP_HEAVY claimants: a wave per segment of
-// FP_SEG claimants, lanes striding it; segments meet in the owner key by atomicMin (keys of this
-// pass are below every earlier one), and JOIN(0) compares keys for such variables (own0 = ~0)
-__global__ __launch_bounds__(FP_THREADS) void k_fp_vmin_heavy(LoopBuffers b) {
-    const RRFpCtl* ctl = b.fp_ctl;
-    if (ctl->state != FP_RUN) return;
-    const uint32_t ep = ctl->ep_base, nh = ctl->nheavy, lane = threadIdx.x & 63;
-    for (uint32_t h = blockIdx.x * (FP_THREADS / 64) + (threadIdx.x >> 6); h < nh; h += gridDim.x * (FP_THREADS / 64)) {
-        const uint4 sg = reinterpret_cast<const uint4*>(b.fp_heavy)[h];
-        unsigned long long best = ~0ull;
-        for (uint32_t o = sg.y + lane; o < sg.z; o += 64) {
-            const uint32_t i = b.fp_vlist[o];
-            const unsigned long long k = fp_key(b, ep, b.fp_turn[i], i);
-            best = k < best ? k : best;
-        }
-        for (int sh = 32; sh > 0; sh >>= 1) {
-            const unsigned long long y = __shfl_xor(best, sh, 64);
-            best = y < best ? y : best;
-        }
-        if (lane == 0) {
-            b.fp_own0[sg.x] = ~0u;
-            atomicMin(&b.fp_owner[sg.x], best);
-        }
-    }
-}
-
-// round 0 of a pass: the minimum key over every shared variable's claimants (a workgroup per
-// bucket over its shared list)
+// Round 0 of a pass: the minimum key over every shared variable's claimants, a workgroup per
+// bucket over its shared list.  Variables with more than FP_HEAVY claimants (hubs of skewed
+// instances) are left to the workgroups past the buckets: a wave per segment of FP_SEG
+// claimants, lanes striding it; segments meet in the owner key by atomicMin (keys of this pass
+// are below every earlier one), and JOIN(0) compares keys for such variables (own0 = ~0).
 __global__ __launch_bounds__(FP_THREADS) void k_fp_vmin(LoopBuffers b) {
     const RRFpCtl* ctl = b.fp_ctl;
     if (ctl->state != FP_RUN) return;
-    const uint32_t ep = ctl->ep_base, bk = blockIdx.x;
+    const uint32_t ep = ctl->ep_base;
+    if (blockIdx.x >= b.n_bkt) {
+        const uint32_t nh = ctl->nheavy, lane = threadIdx.x & 63, hw = gridDim.x - b.n_bkt;
+        for (uint32_t h = (blockIdx.x - b.n_bkt) * (FP_THREADS / 64) + (threadIdx.x >> 6); h < nh;
+             h += hw * (FP_THREADS / 64)) {
+            const uint4 sg = reinterpret_cast<const uint4*>(b.fp_heavy)[h];
+            unsigned long long best = ~0ull;
+            for (uint32_t o = sg.y + lane; o < sg.z; o += 64) {
+                const uint32_t i = b.fp_vlist[o];
+                const unsigned long long k = fp_key(b, ep, b.fp_turn[i], i);
+                best = k < best ? k : best;
+            }
+            for (int sh = 32; sh > 0; sh >>= 1) {
+                const unsigned long long y = __shfl_xor(best, sh, 64);
+                best = y < best ? y : best;
+            }
+            if (lane == 0) {
+                b.fp_own0[sg.x] = ~0u;
+                atomicMin(&b.fp_owner[sg.x], best);
+            }
+        }
+        return;
+    }
+    const uint32_t bk = blockIdx.x;
     const uint32_t ns = b.fp_sbcnt[bk];
     const uint4* sv = reinterpret_cast<const uint4*>(b.fp_sv) + (uint64_t)bk * b.bkt_width;
     for (uint32_t k = threadIdx.x; k < ns; k += FP_THREADS) {
@@ -3985,8 +3985,8 @@ hipError_t launch_rr_passes(const ClauseView& cv, const LoopBuffers& b, uint32_t
     for (uint32_t p = 0; p < n; ++p) {
         for (uint32_t r = 0; r < FP_G; ++r) {
             if (r == 0) {
-                k_fp_vmin<<<b.n_bkt, FP_THREADS, 0, s>>>(b);
-                k_fp_vmin_heavy<<<FP_HEAVY_GRID, FP_THREADS, 0, s>>>(b);
+                // (instances with hot variables get FP_HEAVY_GRID more workgroups for the long lists)
+                k_fp_vmin<<<b.n_bkt + (cv.n_hot ? FP_HEAVY_GRID : 16u), FP_THREADS, 0, s>>>(b);
                 if (g.narrow) k_fp_join<4><<<g.gr, FP_THREADS, 0, s>>>(cv, b, 0);
                 else k_fp_join<0><<<g.gr, FP_THREADS, 0, s>>>(cv, b, 0);
             } else if (g.narrow) {

@@ -151,6 +151,17 @@ void parallel_for(uint64_t n, unsigned nt, F f) {
     for (auto& x : th) x.join();
 }
 
+// f(t, begin, end) on up to nt threads over contiguous blocks of [0, n); returns the threads used
+template <typename F>
+unsigned parallel_chunks(uint64_t n, unsigned nt, F f) {
+    nt = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(nt, n / 65536 + 1));
+    if (nt <= 1) { f(0u, (uint64_t)0, n); return 1; }
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; ++t) th.emplace_back([&, t] { f(t, n * t / nt, n * (t + 1) / nt); });
+    for (auto& x : th) x.join();
+    return nt;
+}
+
 // std::sort of a[0, n) on nt threads: sorted blocks, then pairwise merges level by level.
 template <typename T, typename Cmp>
 void parallel_sort(T* a, size_t n, Cmp cmp, unsigned nt) {
@@ -706,12 +717,23 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     if (m && prob->offsets[0] != 0) return fail(ALLL_ERR_BAD_INPUT, "offsets[0] != 0");
     if (L && !prob->literals) return fail(ALLL_ERR_INVALID_ARG, "null literals");
     if (L >= 0xFFFFFFFFull) return fail(ALLL_ERR_UNSUPPORTED, "more than 2^32-1 literals");
+    // (host passes over the instance run on the process's threads: at 128M clauses / 384M
+    // literals a serial pass costs ~0.5 s, and every rank of a sharded run makes them)
+    const unsigned hnt = host_threads();
     int fixed_k = -1;
-    for (uint64_t c = 0; c < m; ++c) {
-        if (prob->offsets[c + 1] < prob->offsets[c]) return fail(ALLL_ERR_BAD_INPUT, "offsets decrease at %llu", (unsigned long long)c);
-        const int64_t w = (int64_t)(prob->offsets[c + 1] - prob->offsets[c]);
-        if (fixed_k == -1) fixed_k = (int)std::min<int64_t>(w, 1 << 30);
-        else if (fixed_k != w) fixed_k = 0;
+    if (m) {
+        const uint64_t w0 = prob->offsets[1] - prob->offsets[0];
+        std::vector<uint64_t> bad(hnt, ~0ull);
+        std::vector<uint8_t> ragged(hnt, 0);
+        parallel_chunks(m, hnt, [&](unsigned t, uint64_t c0, uint64_t c1) {
+            for (uint64_t c = c0; c < c1; ++c) {
+                if (prob->offsets[c + 1] < prob->offsets[c]) { bad[t] = c; return; }
+                if (prob->offsets[c + 1] - prob->offsets[c] != w0) ragged[t] = 1;
+            }
+        });
+        const uint64_t first_bad = *std::min_element(bad.begin(), bad.end());
+        if (first_bad != ~0ull) return fail(ALLL_ERR_BAD_INPUT, "offsets decrease at %llu", (unsigned long long)first_bad);
+        fixed_k = *std::max_element(ragged.begin(), ragged.end()) ? 0 : (int)std::min<uint64_t>(w0, 1 << 30);
     }
     // the streaming solve keeps the clause-order (CSR) layout: its window rule needs the first
     // violated clause index, read from a clause-order bitmask
@@ -745,10 +767,17 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     if (fixed_k < 1 || fixed_k > MAX_FIXED_K || (opt.flags & ALLL_FLAG_GENERIC_CSR) || opt.stream_batch)
         fixed_k = 0;
     const uint64_t lim = 2ull * prob->n_vars;
-    for (uint64_t j = 0; j < L; ++j)
-        if (prob->literals[j] >= lim)
+    {
+        std::vector<uint64_t> bad(hnt, ~0ull);
+        parallel_chunks(L, hnt, [&](unsigned t, uint64_t j0, uint64_t j1) {
+            for (uint64_t j = j0; j < j1; ++j)
+                if (prob->literals[j] >= lim) { bad[t] = j; return; }
+        });
+        const uint64_t j = *std::min_element(bad.begin(), bad.end());
+        if (j != ~0ull)
             return fail(ALLL_ERR_LITERAL_RANGE, "literal %u at position %llu exceeds n_vars %u",
                         prob->literals[j], (unsigned long long)j, prob->n_vars);
+    }
 
     // ---- hot variables (skewed degree: power-law hubs): degree >= max(1024, 32 x mean degree),
     // at most HOT_MAX of the highest; flagged in bit 31 of every literal copy the device uses
@@ -756,7 +785,9 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     uint32_t n_hot = 0;
     if (L && prob->n_vars && prob->n_vars < (1u << 30)) {
         std::vector<uint32_t> deg(prob->n_vars, 0u);
-        for (uint64_t j = 0; j < L; ++j) ++deg[prob->literals[j] >> 1];
+        parallel_chunks(L, hnt, [&](unsigned, uint64_t j0, uint64_t j1) {
+            for (uint64_t j = j0; j < j1; ++j) __atomic_fetch_add(&deg[prob->literals[j] >> 1], 1u, __ATOMIC_RELAXED);
+        });
         const uint64_t thr = std::max<uint64_t>(1024, 32 * (L / prob->n_vars + 1));
         std::vector<std::pair<uint32_t, uint32_t>> hot;
         for (uint32_t v = 0; v < prob->n_vars; ++v)
@@ -953,7 +984,9 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
         b.n_bkt = (uint32_t)nb;
         b.bkt_span = (uint32_t)span;
         std::vector<uint32_t> soff(c->n_vars + 1, 0u), breg(nb + 1, 0u);
-        for (uint64_t j = 0; j < L; ++j) ++soff[prob->literals[j] >> 1];
+        parallel_chunks(L, hnt, [&](unsigned, uint64_t j0, uint64_t j1) {
+            for (uint64_t j = j0; j < j1; ++j) __atomic_fetch_add(&soff[prob->literals[j] >> 1], 1u, __ATOMIC_RELAXED);
+        });
         uint32_t acc = 0;
         for (uint32_t v = 0; v < c->n_vars; ++v) {
             const uint32_t d = soff[v];
@@ -1008,13 +1041,21 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
         // remaining high-degree variables of power-law instances over the buckets.
         bool skewed = false;
         if (nb <= BKT_MAX) {
+            std::vector<std::vector<uint64_t>> lt(hnt, std::vector<uint64_t>(nb, 0));
+            std::vector<uint64_t> lp(hnt, 0);
+            const unsigned used = parallel_chunks(L, hnt, [&](unsigned t, uint64_t j0, uint64_t j1) {
+                for (uint64_t j = j0; j < j1; ++j) {
+                    const uint32_t v = prob->literals[j] >> 1;
+                    if (n_hot && is_hot[v]) continue;
+                    ++lt[t][((v * b.vmix_mul) & b.vmix_mask) / width];
+                    ++lp[t];
+                }
+            });
             std::vector<uint64_t> load(nb, 0);
             uint64_t L_pairs = 0;
-            for (uint64_t j = 0; j < L; ++j) {
-                const uint32_t v = prob->literals[j] >> 1;
-                if (n_hot && is_hot[v]) continue;
-                ++load[((v * b.vmix_mul) & b.vmix_mask) / width];
-                ++L_pairs;
+            for (unsigned t = 0; t < used; ++t) {
+                for (uint64_t k = 0; k < nb; ++k) load[k] += lt[t][k];
+                L_pairs += lp[t];
             }
             const uint64_t mx = *std::max_element(load.begin(), load.end());
             skewed = mx > 4 * (L_pairs / nb + 1);

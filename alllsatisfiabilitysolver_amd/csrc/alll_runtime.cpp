@@ -784,14 +784,48 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     std::vector<uint8_t> is_hot;
     uint32_t n_hot = 0;
     if (L && prob->n_vars && prob->n_vars < (1u << 30)) {
-        std::vector<uint32_t> deg(prob->n_vars, 0u);
-        parallel_chunks(L, hnt, [&](unsigned, uint64_t j0, uint64_t j1) {
-            for (uint64_t j = j0; j < j1; ++j) __atomic_fetch_add(&deg[prob->literals[j] >> 1], 1u, __ATOMIC_RELAXED);
-        });
+        // degrees from per-thread 16-bit saturating histograms (4-5x faster than shared atomic
+        // counters at 384M literals), exact recount for the rare saturated candidates
         const uint64_t thr = std::max<uint64_t>(1024, 32 * (L / prob->n_vars + 1));
+        const unsigned dnt = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(hnt, (2ull << 30) / (2ull * prob->n_vars)));
+        std::vector<std::vector<uint16_t>> hist(dnt);
+        const unsigned used = parallel_chunks(L, dnt, [&](unsigned t, uint64_t j0, uint64_t j1) {
+            std::vector<uint16_t>& h = hist[t];
+            h.assign(prob->n_vars, 0);
+            for (uint64_t j = j0; j < j1; ++j) {
+                uint16_t& c = h[prob->literals[j] >> 1];
+                c += c != 0xFFFF;
+            }
+        });
+        std::vector<std::vector<std::pair<uint32_t, uint32_t>>> hot_t(hnt);
+        std::vector<std::vector<uint32_t>> rec_t(hnt);
+        parallel_chunks(prob->n_vars, hnt, [&](unsigned t, uint64_t v0, uint64_t v1) {
+            for (uint64_t v = v0; v < v1; ++v) {
+                uint64_t d = 0;
+                bool sat = false;
+                for (unsigned q = 0; q < used; ++q) { d += hist[q][v]; sat |= hist[q][v] == 0xFFFF; }
+                if (d < thr) continue;
+                if (sat) rec_t[t].push_back((uint32_t)v);
+                else hot_t[t].push_back({(uint32_t)d, (uint32_t)v});
+            }
+        });
+        hist.clear();
         std::vector<std::pair<uint32_t, uint32_t>> hot;
-        for (uint32_t v = 0; v < prob->n_vars; ++v)
-            if (deg[v] >= thr) hot.push_back({deg[v], v});
+        std::vector<uint32_t> recount;  // (ascending: the chunks are in variable order)
+        for (unsigned t = 0; t < hnt; ++t) {
+            hot.insert(hot.end(), hot_t[t].begin(), hot_t[t].end());
+            recount.insert(recount.end(), rec_t[t].begin(), rec_t[t].end());
+        }
+        if (!recount.empty()) {  // (a variable with >= 65535 literals in one thread's range)
+            std::vector<uint64_t> d(recount.size(), 0);
+            for (uint64_t j = 0; j < L; ++j) {
+                const uint32_t v = prob->literals[j] >> 1;
+                const auto it = std::lower_bound(recount.begin(), recount.end(), v);
+                if (it != recount.end() && *it == v) ++d[it - recount.begin()];
+            }
+            for (size_t q = 0; q < recount.size(); ++q)
+                hot.push_back({(uint32_t)std::min<uint64_t>(d[q], 0xFFFFFFFFu), recount[q]});
+        }
         if (!hot.empty()) {
             std::sort(hot.rbegin(), hot.rend());
             if (hot.size() > HOT_MAX) hot.resize(HOT_MAX);

@@ -1233,11 +1233,13 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
                 cv.lit_mask = (1u << lit_bits) - 1u;
             }
         }
-        std::vector<uint32_t> t(real_chunks * CHUNK * fixed_k, 0u);
+        // (the own shard's chunks only: shards are tile-aligned, so they are whole chunks)
         const uint32_t id_mask = cv.id_bits ? (1u << cv.id_bits) - 1u : 0u;
         const uint64_t own_p0 = std::min<uint64_t>(m, (uint64_t)c->own_begin * TILE);
         const uint64_t own_p1 = std::min<uint64_t>(m, (uint64_t)c->own_end * TILE);
-        parallel_for(own_p1 - own_p0, host_threads(), [&](uint64_t q) {  // (the own shard's positions)
+        const uint64_t g0 = own_p0 / CHUNK, g1 = (own_p1 + CHUNK - 1) / CHUNK;
+        std::vector<uint32_t> t((g1 - g0) * CHUNK * fixed_k, 0u);
+        parallel_for(own_p1 - own_p0, host_threads(), [&](uint64_t q) {
             const uint64_t p2 = own_p0 + q;
             uint32_t tmp[MAX_FIXED_K];
             const uint64_t cl = perm[p2];
@@ -1248,13 +1250,13 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
             std::sort(tmp, tmp + fixed_k, [](uint32_t x, uint32_t y) {
                 return ((x & 0x7FFFFFFFu) >> 1) > ((y & 0x7FFFFFFFu) >> 1);
             });
-            const uint64_t g = p2 / CHUNK, r = p2 % CHUNK;
+            const uint64_t g = p2 / CHUNK - g0, r = p2 % CHUNK;
             for (int j = 0; j < fixed_k; ++j) {
                 const uint32_t idp = cv.id_bits ? ((uint32_t)(cl >> (j * cv.id_bits)) & id_mask) << cv.id_shift : 0u;
                 t[(g * fixed_k + j) * CHUNK + r] = tmp[j] | idp;
             }
         });
-        if (!t.empty() && hipMemcpy(d_t, t.data(), t.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
+        if (!t.empty() && hipMemcpy(d_t + g0 * CHUNK * fixed_k, t.data(), t.size() * 4, hipMemcpyHostToDevice) != hipSuccess)
             return bail(fail(ALLL_ERR_HIP, "transposed literal upload failed"));
         if (!cv.id_bits) {
             uint32_t* d_perm = nullptr;

@@ -9,7 +9,7 @@ ARCH ?= gfx950
 PKG := alllsatisfiabilitysolver_amd
 SRC := $(PKG)/csrc
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-result \
-            -Iinclude -I$(SRC) -I$(ROCM)/include
+            -Iinclude -I$(SRC) -I$(ROCM)/include $(EXTRA)
 LIB := $(PKG)/liballl.so
 OBJS := $(SRC)/alll_kernels.o $(SRC)/alll_runtime.o $(SRC)/alll_host.o
 

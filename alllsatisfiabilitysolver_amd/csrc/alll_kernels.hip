@@ -2292,7 +2292,16 @@ __global__ __launch_bounds__(256) void k_rr_entries(ClauseView cv, LoopBuffers b
         e.v0 = make_uint4(v[0], v[1], v[2], v[3]);
         e.v1 = make_uint4(v[4], v[5], v[6], v[7]);
         out[i] = e;
-        if (b.rr_k >= 1 && b.rr_k <= 4 && b.fp_ctl) b.fp_v4[base + i] = e.v0;  // (the passes' narrow copy)
+        if (b.fp_ctl) {  // the passes' narrow copy; sole bytes cleared (k_fp_bbuild sets them)
+            if (b.rr_k >= 1 && b.rr_k <= 4) {
+                b.fp_v4[base + i] = e.v0;
+                reinterpret_cast<uint32_t*>(b.fp_sole)[base + i] = 0u;
+            } else {
+                reinterpret_cast<uint2*>(b.fp_sole)[base + i] = make_uint2(0u, 0u);
+            }
+            b.fp_lost[base + i] = 0u;
+            b.fp_lost[b.m + base + i] = 0u;
+        }
     }
 }
 
@@ -2852,31 +2861,20 @@ __device__ __forceinline__ void fp_for_shared(const ClauseView& cv, const RREnt*
 }
 
 // sole mask of an entry (bit j: slot j's variable has no other violated claimant this
-// iteration; fp_one, in vmix order, k_fp_bbuild): such a variable is always owned by the entry
-// and never covered by another pick, so the claims, ownership and kill tests skip it
+// iteration; the entry's sole bytes, k_fp_bbuild): such a variable is always owned by the entry
+// and never covered by another pick, so the claims, ownership and kill tests skip it.  One load
+// that does not wait for the entry's variables
+__device__ __forceinline__ uint32_t fp_bytes_bits(uint32_t x) {  // bytes 0 / 1 -> bits 0..3
+    return (x & 1u) | ((x >> 7) & 2u) | ((x >> 14) & 4u) | ((x >> 21) & 8u);
+}
 template <uint32_t KW>
-__device__ __forceinline__ uint32_t fp_sole_mask(const LoopBuffers& b, const RREnt* U, uint32_t i, const uint4& a,
-                                                 const uint4& v0) {
-    auto one = [&](uint32_t v) -> uint32_t {
-        const uint32_t x = vmix(b, v);
-        return (b.fp_one[x >> 5] >> (x & 31u)) & 1u;
-    };
-    const uint32_t w = a.z;
-    uint32_t m = 0;
-    if (w > 0) m |= one(v0.x);
-    if (w > 1) m |= one(v0.y) << 1;
-    if (w > 2) m |= one(v0.z) << 2;
-    if (w > 3) m |= one(v0.w) << 3;
-    if constexpr (KW == 0) {
-        if (w > 4) {
-            const uint4 v1 = U[i].v1;
-            m |= one(v1.x) << 4;
-            if (w > 5) m |= one(v1.y) << 5;
-            if (w > 6) m |= one(v1.z) << 6;
-            if (w > 7) m |= one(v1.w) << 7;
-        }
+__device__ __forceinline__ uint32_t fp_sole_mask(const LoopBuffers& b, uint32_t i) {
+    if constexpr (KW == 4) {
+        return fp_bytes_bits(reinterpret_cast<const uint32_t*>(b.fp_sole)[i]);
+    } else {
+        const uint2 x = reinterpret_cast<const uint2*>(b.fp_sole)[i];
+        return fp_bytes_bits(x.x) | (fp_bytes_bits(x.y) << 4);
     }
-    return m;
 }
 
 // an entry's header and first 4 variables in a pass; narrow instances (one width <= 4) read
@@ -2982,6 +2980,10 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_guess(LoopBuffers b) {
 constexpr uint32_t FP_BS_PER = 8;                          // scan entries per thread of k_fp_bscatter
 constexpr uint32_t FP_BS_ENT = FP_BS_PER * FP_THREADS;     // ... per workgroup
 constexpr int FP_BB_THREADS = 1024;
+// a pair's entry word: the entry index (below 2^FP_SLOT_SH) and the claim's slot (8: past the
+// entry's 8 variables) above it
+constexpr uint32_t FP_SLOT_SH = 28;
+constexpr uint32_t FP_IMASK = (1u << FP_SLOT_SH) - 1u;
 
 // slot j < 8 of an entry (narrow instances: the 16-byte copy)
 __device__ __forceinline__ uint32_t fp_slot(const uint4& v0, const uint4& v1, uint32_t j) {
@@ -3012,23 +3014,33 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_bscatter(ClauseView cv, LoopB
             v1 = U[i].v1;
         }
     };
+    constexpr uint32_t FP_JM = KW == 4 ? 4u : 8u;  // slots held in the entry
     for (uint32_t i0 = blockIdx.x * FP_BS_ENT; i0 < nu; i0 += gridDim.x * FP_BS_ENT) {
         for (uint32_t k = tid; k < nb; k += FP_THREADS) s_h[k] = 0u;
+        // the chunk's entries, all loads first, kept in registers for the second phase
+        uint4 ea[FP_BS_PER], e0[FP_BS_PER], e1[FP_BS_PER];
+#pragma unroll
+        for (uint32_t e = 0; e < FP_BS_PER; ++e) {
+            const uint32_t i = i0 + e * FP_THREADS + tid;
+            if (i < nu) ent(i, ea[e], e0[e], e1[e]);
+            else ea[e].z = 0u;
+        }
         __syncthreads();
+#pragma unroll
         for (uint32_t e = 0; e < FP_BS_PER; ++e) {  // ranks of slots 0..7 within this chunk
             const uint32_t i = i0 + e * FP_THREADS + tid;
-            if (i >= nu) break;
-            uint4 a, v0, v1;
-            ent(i, a, v0, v1);
-            const uint32_t w = a.z, w8 = w < 8u ? w : 8u;
+            const uint32_t w = ea[e].z, w8 = w < 8u ? w : 8u;
             uint32_t off;
-            for (uint32_t j = 0; j < w8; ++j)
-                s_rank[(e * FP_THREADS + tid) * 8 + j] = (uint16_t)atomicAdd(&s_h[bucket_of(b, fp_slot(v0, v1, j), off)], 1u);
+#pragma unroll
+            for (uint32_t j = 0; j < FP_JM; ++j)
+                if (j < w8)
+                    s_rank[(e * FP_THREADS + tid) * 8 + j] =
+                        (uint16_t)atomicAdd(&s_h[bucket_of(b, fp_slot(e0[e], e1[e], j), off)], 1u);
             if constexpr (KW == 0) {  // slots past 8 of wide clauses (rare): a global rank each
                 for (uint32_t j = 8; j < w; ++j) {
-                    const uint32_t v = lit_var(cv.lits[a.y + j]);
+                    const uint32_t v = lit_var(cv.lits[ea[e].y + j]);
                     const uint32_t bk = bucket_of(b, v, off);
-                    pairs[s_breg[bk] + atomicAdd(&b.fp_bfill[bk], 1u)] = make_uint2(i, v);
+                    pairs[s_breg[bk] + atomicAdd(&b.fp_bfill[bk], 1u)] = make_uint2(i | (8u << FP_SLOT_SH), v);
                 }
             }
         }
@@ -3038,16 +3050,16 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_bscatter(ClauseView cv, LoopB
             s_h[k] = c ? s_breg[k] + atomicAdd(&b.fp_bfill[k], c) : 0u;
         }
         __syncthreads();
+#pragma unroll
         for (uint32_t e = 0; e < FP_BS_PER; ++e) {
             const uint32_t i = i0 + e * FP_THREADS + tid;
-            if (i >= nu) break;
-            uint4 a, v0, v1;
-            ent(i, a, v0, v1);
-            const uint32_t w8 = a.z < 8u ? a.z : 8u;
+            const uint32_t w8 = ea[e].z < 8u ? ea[e].z : 8u;
             uint32_t off;
-            for (uint32_t j = 0; j < w8; ++j) {
-                const uint32_t v = fp_slot(v0, v1, j);
-                pairs[s_h[bucket_of(b, v, off)] + s_rank[(e * FP_THREADS + tid) * 8 + j]] = make_uint2(i, v);
+#pragma unroll
+            for (uint32_t j = 0; j < FP_JM; ++j) {
+                if (j >= w8) break;
+                const uint32_t v = fp_slot(e0[e], e1[e], j);
+                pairs[s_h[bucket_of(b, v, off)] + s_rank[(e * FP_THREADS + tid) * 8 + j]] = make_uint2(i | (j << FP_SLOT_SH), v);
             }
         }
         __syncthreads();  // (s_h is reset for the next chunk)
@@ -3066,41 +3078,57 @@ __global__ __launch_bounds__(FP_BB_THREADS) void k_fp_bbuild(LoopBuffers b) {
     uint32_t* s_first = s_bb + 2 * W;
     __shared__ uint32_t s_ns;
     const uint32_t n = b.fp_bfill[bk];
-    for (uint32_t w = tid; w < nw; w += FP_BB_THREADS) {
-        const uint32_t v = vunmix(b, xb + w);
-        s_cnt[w] = 0u;
-        s_off[w] = v < b.n_vars ? b.fp_soff[v] : 0u;
+    constexpr uint32_t U4 = 4;  // loads in flight per thread
+    for (uint32_t w0 = tid; w0 < nw; w0 += U4 * FP_BB_THREADS) {
+        uint32_t o[U4];
+#pragma unroll
+        for (uint32_t u = 0; u < U4; ++u) {
+            const uint32_t w = w0 + u * FP_BB_THREADS;
+            const uint32_t v = w < nw ? vunmix(b, xb + w) : ~0u;
+            o[u] = v < b.n_vars ? b.fp_soff[v] : 0u;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < U4; ++u) {
+            const uint32_t w = w0 + u * FP_BB_THREADS;
+            if (w < nw) {
+                s_cnt[w] = 0u;
+                s_off[w] = o[u];
+            }
+        }
     }
     if (tid == 0) s_ns = 0;
     __syncthreads();
     if (tid == 0) b.fp_bfill[bk] = 0u;  // (read by every thread above; the next iteration's count)
     const uint2* P = reinterpret_cast<const uint2*>(b.fp_pairs) + b.fp_breg[bk];
-    for (uint32_t k = tid; k < n; k += FP_BB_THREADS) {
-        const uint2 p = P[k];
-        const uint32_t w = vmix(b, p.y) - xb;
-        const uint32_t r = atomicAdd(&s_cnt[w], 1u);
-        if (r == 0) s_first[w] = p.x;
-        b.fp_vlist[s_off[w] + r] = p.x;
+    for (uint32_t k0 = tid; k0 < n; k0 += U4 * FP_BB_THREADS) {
+        uint2 p[U4];
+#pragma unroll
+        for (uint32_t u = 0; u < U4; ++u) {
+            const uint32_t k = k0 + u * FP_BB_THREADS;
+            p[u] = k < n ? P[k] : make_uint2(0u, ~0u);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < U4; ++u) {
+            if (p[u].y == ~0u) continue;
+            const uint32_t w = vmix(b, p[u].y) - xb;
+            const uint32_t r = atomicAdd(&s_cnt[w], 1u);
+            if (r == 0) s_first[w] = p[u].x;
+            b.fp_vlist[s_off[w] + r] = p[u].x & FP_IMASK;
+        }
     }
     __syncthreads();
-    // per variable (vmix slot order): single-claimant bits, the single claimant's ownership, the
-    // shared list and the long lists' segments
+    // per variable (vmix slot order): the single claimant's ownership and sole byte, the shared
+    // list and the long lists' segments
     uint4* sv = reinterpret_cast<uint4*>(b.fp_sv) + (uint64_t)bk * W;
-    const uint32_t lane = tid & 63;
-    for (uint32_t w0 = 0; w0 < nw; w0 += FP_BB_THREADS) {
-        const uint32_t w = w0 + tid;
-        const uint32_t c = w < nw ? s_cnt[w] : 0u;
-        const unsigned long long one = __ballot(c == 1u);
-        // (bucket widths are multiples of 64: the ballot's halves are whole words of fp_one)
-        if (lane == 0 && xb + w0 + tid < b.bkt_span) {
-            uint32_t* ow = b.fp_one + (xb + w0 + tid) / 32;
-            ow[0] = (uint32_t)one;
-            ow[1] = (uint32_t)(one >> 32);
-        }
+    const uint32_t sw = b.rr_k >= 1 && b.rr_k <= 4 ? 4u : 8u;  // sole bytes per entry
+    for (uint32_t w = tid; w < nw; w += FP_BB_THREADS) {
+        const uint32_t c = s_cnt[w];
         if (c == 0u) continue;
         const uint32_t v = vunmix(b, xb + w);
         if (c == 1u) {
-            b.fp_own0[v] = s_first[w];
+            const uint32_t x = s_first[w], i = x & FP_IMASK, j = x >> FP_SLOT_SH;
+            b.fp_own0[v] = i;
+            if (j < sw) b.fp_sole[(uint64_t)i * sw + j] = 1u;
         } else {
             sv[atomicAdd(&s_ns, 1u)] = make_uint4(s_off[w], c, v, 0u);
             if (c > FP_HEAVY) {  // long lists (hubs of skewed instances): a wave per FP_SEG claimants
@@ -3116,18 +3144,20 @@ __global__ __launch_bounds__(FP_BB_THREADS) void k_fp_bbuild(LoopBuffers b) {
     if (tid == 0) b.fp_sbcnt[bk] = s_ns;
 }
 
-// Round 0 of a pass: the minimum key over every shared variable's claimants, a workgroup per
-// bucket over its shared list.  Variables with more than FP_HEAVY claimants (hubs of skewed
-// instances) are left to the workgroups past the buckets: a wave per segment of FP_SEG
+// Round 0 of a pass: the minimum key over every shared variable's claimants, FP_VS workgroups
+// per bucket striding its shared list.  Variables with more than FP_HEAVY claimants (hubs of
+// skewed instances) are left to the workgroups past the buckets: a wave per segment of FP_SEG
 // claimants, lanes striding it; segments meet in the owner key by atomicMin (keys of this pass
 // are below every earlier one), and JOIN(0) compares keys for such variables (own0 = ~0).
+constexpr uint32_t FP_VS = 8;
 __global__ __launch_bounds__(FP_THREADS) void k_fp_vmin(LoopBuffers b) {
     const RRFpCtl* ctl = b.fp_ctl;
     if (ctl->state != FP_RUN) return;
-    const uint32_t ep = ctl->ep_base;
-    if (blockIdx.x >= b.n_bkt) {
-        const uint32_t nh = ctl->nheavy, lane = threadIdx.x & 63, hw = gridDim.x - b.n_bkt;
-        for (uint32_t h = (blockIdx.x - b.n_bkt) * (FP_THREADS / 64) + (threadIdx.x >> 6); h < nh;
+    const uint32_t ep = ctl->ep_base, nbw = b.n_bkt * FP_VS;
+    if (blockIdx.x >= nbw) {
+        const uint32_t nh = ctl->nheavy, lane = threadIdx.x & 63, hw = gridDim.x - nbw;
+        const uint8_t serial = (uint8_t)ctl->serial;
+        for (uint32_t h = (blockIdx.x - nbw) * (FP_THREADS / 64) + (threadIdx.x >> 6); h < nh;
              h += hw * (FP_THREADS / 64)) {
             const uint4 sg = reinterpret_cast<const uint4*>(b.fp_heavy)[h];
             unsigned long long best = ~0ull;
@@ -3135,6 +3165,7 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_vmin(LoopBuffers b) {
                 const uint32_t i = b.fp_vlist[o];
                 const unsigned long long k = fp_key(b, ep, b.fp_turn[i], i);
                 best = k < best ? k : best;
+                b.fp_lost[b.m + i] = serial;  // (its JOIN(0) compares keys)
             }
             for (int sh = 32; sh > 0; sh >>= 1) {
                 const unsigned long long y = __shfl_xor(best, sh, 64);
@@ -3147,22 +3178,38 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_vmin(LoopBuffers b) {
         }
         return;
     }
-    const uint32_t bk = blockIdx.x;
+    const uint32_t bk = blockIdx.x / FP_VS, sl = blockIdx.x % FP_VS;
+    const uint8_t serial = (uint8_t)ctl->serial;
     const uint32_t ns = b.fp_sbcnt[bk];
     const uint4* sv = reinterpret_cast<const uint4*>(b.fp_sv) + (uint64_t)bk * b.bkt_width;
-    for (uint32_t k = threadIdx.x; k < ns; k += FP_THREADS) {
+    for (uint32_t k = sl * FP_THREADS + threadIdx.x; k < ns; k += FP_VS * FP_THREADS) {
         const uint4 e = sv[k];
         if (e.y > FP_HEAVY) continue;
+        // two claimants at a time (every list here has two or more)
         unsigned long long best = ~0ull;
-        for (uint32_t o = e.x; o < e.x + e.y; ++o) {
+        uint32_t o = e.x;
+        const uint32_t end = e.x + e.y;
+        for (; o + 1 < end; o += 2) {
+            const uint32_t i0 = b.fp_vlist[o], i1 = b.fp_vlist[o + 1];
+            const uint32_t t0 = b.fp_turn[i0], t1 = b.fp_turn[i1];
+            const unsigned long long k0 = fp_key(b, ep, t0, i0), k1 = fp_key(b, ep, t1, i1);
+            const unsigned long long k01 = k0 < k1 ? k0 : k1;
+            best = k01 < best ? k01 : best;
+        }
+        if (o < end) {
             const uint32_t i = b.fp_vlist[o];
             const unsigned long long key = fp_key(b, ep, b.fp_turn[i], i);
             best = key < best ? key : best;
         }
-        // JOIN(0) reads the winning entry from a 4-byte array (half the footprint of the keys).
-        // The owner key itself is not needed: the later rounds' claims are of later epochs,
-        // below any key an earlier pass or round left there
-        b.fp_own0[e.z] = (uint32_t)best & ((1u << b.fp_ib) - 1u);
+        // The losers are marked (JOIN(0) of an entry reads one byte); the winner is kept for
+        // the entries that also hold a long list's variable.  The owner key itself is not
+        // needed: the later rounds' claims are of later epochs, below any key left here
+        const uint32_t win = (uint32_t)best & ((1u << b.fp_ib) - 1u);
+        b.fp_own0[e.z] = win;
+        for (o = e.x; o < end; ++o) {
+            const uint32_t i = b.fp_vlist[o];
+            if (i != win) b.fp_lost[i] = serial;
+        }
     }
 }
 
@@ -3193,7 +3240,7 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_claim(ClauseView cv, LoopBuff
                 i = lin[j];
                 uint4 a, v0;
                 fp_ent<KW>(b, U, i, a, v0);
-                const uint32_t sole = fp_sole_mask<KW>(b, U, i, a, v0);
+                const uint32_t sole = fp_sole_mask<KW>(b, i);
                 const uint32_t turn = b.fp_turn[i];
                 bool dead = false;
                 fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) { dead |= b.fp_cov[v] == (uint8_t)serial; });
@@ -3237,18 +3284,22 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_join(ClauseView cv, LoopBuffe
                 i = r == 0 ? i0 + j : lin[j];
                 uint4 a, v0;
                 fp_ent<KW>(b, U, i, a, v0);
-                // (round 0 needs no sole mask: a single claimant owns its variable, fp_own0)
-                const uint32_t sole = r == 0 ? 0u : fp_sole_mask<KW>(b, U, i, a, v0);
+                // (a sole slot's variable is owned by the entry and covered by no other pick)
+                const uint32_t sole = fp_sole_mask<KW>(b, i);
                 const uint32_t turn = b.fp_turn[i];
                 bool own = true, pre = false;
                 if (r == 0 && turn < tpre) {  // decided as in the last pass (bit 1)
                     pre = true;
                     own = (b.fp_in[i] >> 1) & 1u;
                 } else if (r == 0) {
-                    fp_for_vars<KW>(cv, U, i, a, v0, [&](uint32_t v) {
-                        const uint32_t w = b.fp_own0[v];  // (~0: a long list, reduced into the key)
-                        own &= w == i || (w == ~0u && b.fp_owner[v] == fp_key(b, ep, turn, i));
-                    });
+                    if (b.fp_lost[b.m + i] != (uint8_t)serial) {
+                        own = b.fp_lost[i] != (uint8_t)serial;  // (k_fp_vmin marked the losers)
+                    } else {  // on a long list too: the winners, and the key for the long lists
+                        fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) {
+                            const uint32_t w = b.fp_own0[v];  // (~0: a long list, reduced into the key)
+                            own &= w == i || (w == ~0u && b.fp_owner[v] == fp_key(b, ep, turn, i));
+                        });
+                    }
                 } else {
                     const unsigned long long key = fp_key(b, ep, turn, i);
                     fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) { own &= b.fp_owner[v] == key; });
@@ -3295,7 +3346,7 @@ __global__ __launch_bounds__(1024) void k_fp_tail(ClauseView cv, LoopBuffers b) 
                 i = la[j];
                 uint4 a, v0;
                 fp_ent<KW>(b, U, i, a, v0);
-                const uint32_t sole = fp_sole_mask<KW>(b, U, i, a, v0);
+                const uint32_t sole = fp_sole_mask<KW>(b, i);
                 bool dead = false;
                 fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) {
                     dead |= __hip_atomic_load(&b.fp_cov[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint8_t)serial;
@@ -3322,7 +3373,7 @@ __global__ __launch_bounds__(1024) void k_fp_tail(ClauseView cv, LoopBuffers b) 
                 i = lb[j];
                 uint4 a, v0;
                 fp_ent<KW>(b, U, i, a, v0);
-                const uint32_t sole = fp_sole_mask<KW>(b, U, i, a, v0);
+                const uint32_t sole = fp_sole_mask<KW>(b, i);
                 const unsigned long long key = fp_key(b, ep, b.fp_turn[i], i);
                 bool own = true;
                 fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) {
@@ -3439,21 +3490,21 @@ __global__ __launch_bounds__(256) void k_fp_sched(LoopBuffers b, int test) {
     for (uint32_t w = 1; w < (blockDim.x >> 6); ++w) tmin = min(tmin, s_w[w]);
     __syncthreads();
     const bool conv = test && ch == 0;
-    // exclusive scan of the block counts
-    uint32_t carry = 0;
-    for (uint32_t k0 = 0; k0 < nblk; k0 += blockDim.x) {
-        const uint32_t k = k0 + threadIdx.x;
-        const uint32_t x = k < nblk ? b.fp_blk[k] : 0u;
-        uint32_t tot;
-        const uint32_t ex = fp_block_scan(x, s_w, tot);
-        if (k < nblk) {
-            blkoff[k] = carry + ex;
-            if (lds_off) s_off[k] = carry + ex;
-        }
-        carry += tot;
+    // exclusive scan of the block counts: a contiguous range per thread (independent loads),
+    // one workgroup scan of the range sums
+    const uint32_t per = (nblk + blockDim.x - 1) / blockDim.x;
+    const uint32_t kb = min(nblk, threadIdx.x * per), ke = min(nblk, kb + per);
+    uint32_t rsum = 0;
+    for (uint32_t k = kb; k < ke; ++k) rsum += b.fp_blk[k];
+    uint32_t total;
+    uint32_t ex = fp_block_scan(rsum, s_w, total);
+    for (uint32_t k = kb; k < ke; ++k) {
+        const uint32_t x = b.fp_blk[k];
+        blkoff[k] = ex;
+        if (lds_off) s_off[k] = ex;
+        ex += x;
     }
     __syncthreads();
-    const uint32_t total = carry;
     // picks before every set's first entry, picks per set
     for (uint32_t q = 0; q < 2; ++q) {
         const uint32_t s = threadIdx.x + q * blockDim.x;
@@ -3485,7 +3536,8 @@ __global__ __launch_bounds__(256) void k_fp_sched(LoopBuffers b, int test) {
                 const uint32_t L = (uint32_t)__popcll(alive);
                 const bool live = (alive >> lane) & 1ull;
                 const uint32_t x = (uint32_t)__popcll(alive & ((1ull << lane) - 1ull));
-                const uint32_t o = (x + L - (t % L) - 1) % L;
+                uint32_t o = x + L - (t % L) - 1;  // (x - t - 1) mod L, x < L
+                if (o >= L) o -= L;
                 unsigned long long best = live ? (((unsigned long long)(n - done) * L + o) << 6 | lane) : ~0ull;
                 for (int q = 32; q > 0; q >>= 1) {
                     const unsigned long long y = __shfl_xor(best, q, 64);
@@ -3493,8 +3545,12 @@ __global__ __launch_bounds__(256) void k_fp_sched(LoopBuffers b, int test) {
                 }
                 const uint32_t ls = (uint32_t)(best & 63u);
                 const unsigned long long d = best >> 6;
+                // turns a live set takes before the erasure: r* or r* + 1 (d = r* L + o*), no
+                // per-lane division
+                const uint32_t rs = (d >> 32) ? (uint32_t)(d / L) : (uint32_t)d / L;
+                const uint32_t os = (uint32_t)(d - (unsigned long long)rs * L);
                 if (live) {
-                    const uint32_t cnt = lane == ls ? n - done : (d > o ? (uint32_t)((d - o + L - 1) / L) : 0u);
+                    const uint32_t cnt = lane == ls ? n - done : rs + (o < os ? 1u : 0u);
                     b.fp_seg[(uint64_t)lane * T + nseg] = make_uint4(done, step, L, o);
                     nseg += 1;
                     done += cnt;
@@ -3539,7 +3595,8 @@ __global__ __launch_bounds__(256) void k_fp_sched(LoopBuffers b, int test) {
 #pragma unroll
             for (uint32_t q = 0; q < Q; ++q) {
                 const uint32_t x = below + (uint32_t)__popcll(alive[q] & lt);
-                o[q] = (x + L - tl - 1) % L;
+                o[q] = x + L - tl - 1;  // (x < L)
+                if (o[q] >= L) o[q] -= L;
                 if ((alive[q] >> lane) & 1ull) {
                     const unsigned long long key = (((unsigned long long)(n[q] - done[q]) * L + o[q]) << 8) | (lane + 64 * q);
                     best = key < best ? key : best;
@@ -3552,7 +3609,8 @@ __global__ __launch_bounds__(256) void k_fp_sched(LoopBuffers b, int test) {
             }
             const uint32_t ls = (uint32_t)(best & 255u);
             const unsigned long long d = best >> 8;
-            const uint32_t rs = (uint32_t)(d / L), os = (uint32_t)(d - (unsigned long long)rs * L);
+            const uint32_t rs = (d >> 32) ? (uint32_t)(d / L) : (uint32_t)d / L;
+            const uint32_t os = (uint32_t)(d - (unsigned long long)rs * L);
 #pragma unroll
             for (uint32_t q = 0; q < Q; ++q) {
                 if (!((alive[q] >> lane) & 1ull)) continue;
@@ -3653,6 +3711,10 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_turn(ClauseView cv, LoopBuffe
             const uint32_t e1 = min(nu - i0, FP_PER);
             uint32_t st_tile = ~0u, st_n = 0;  // MIS statistics of this thread's picks, per clause tile
             unsigned long long st_w = 0;
+            // the phase record of the current set: found by binary search at the thread's first
+            // entry of a set, then walked forward (levels do not decrease within a set)
+            uint32_t rs = ~0u, lo = 0, ns = 0;
+            const uint4* rec = segs;
             for (uint32_t e = 0; e < e1; ++e) {
                 const uint32_t i = i0 + e;
                 while (i >= s_sf[s + 1]) ++s;
@@ -3660,12 +3722,19 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_turn(ClauseView cv, LoopBuffe
                 if (!fin || pick) {
                     const uint32_t lev = P - s_pf[s];
                     // last phase record of s whose first level <= lev
-                    const uint4* rec = segs + (uint64_t)s * T;
-                    uint32_t lo = 0, hi = s_nseg[s];
-                    while (hi - lo > 1) {
-                        const uint32_t mid = (lo + hi) >> 1;
-                        if (rec[mid].x <= lev) lo = mid;
-                        else hi = mid;
+                    if (s != rs) {
+                        rs = s;
+                        rec = segs + (uint64_t)s * T;
+                        ns = s_nseg[s];
+                        lo = 0;
+                        uint32_t hi = ns;
+                        while (hi - lo > 1) {
+                            const uint32_t mid = (lo + hi) >> 1;
+                            if (rec[mid].x <= lev) lo = mid;
+                            else hi = mid;
+                        }
+                    } else {
+                        while (lo + 1 < ns && rec[lo + 1].x <= lev) ++lo;
                     }
                     const uint4 g = rec[lo];
                     const uint32_t turn = g.y + (lev - g.x) * g.z + g.w;
@@ -3986,7 +4055,7 @@ hipError_t launch_rr_passes(const ClauseView& cv, const LoopBuffers& b, uint32_t
         for (uint32_t r = 0; r < FP_G; ++r) {
             if (r == 0) {
                 // (instances with hot variables get FP_HEAVY_GRID more workgroups for the long lists)
-                k_fp_vmin<<<b.n_bkt + (cv.n_hot ? FP_HEAVY_GRID : 16u), FP_THREADS, 0, s>>>(b);
+                k_fp_vmin<<<b.n_bkt * FP_VS + (cv.n_hot ? FP_HEAVY_GRID : 16u), FP_THREADS, 0, s>>>(b);
                 if (g.narrow) k_fp_join<4><<<g.gr, FP_THREADS, 0, s>>>(cv, b, 0);
                 else k_fp_join<0><<<g.gr, FP_THREADS, 0, s>>>(cv, b, 0);
             } else if (g.narrow) {

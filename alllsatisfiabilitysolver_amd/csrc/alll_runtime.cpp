@@ -939,7 +939,7 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
         // passes per iteration (graph unroll)
         auto bits_of = [](uint64_t x) { uint32_t k = 1; while (k < 64 && (x >> k)) ++k; return k; };
         const uint32_t ib = bits_of(m), tb = bits_of(m + rr_T + 1);
-        bool fp = rr_T <= FP_TMAX && ib + tb + 10 <= 64;
+        bool fp = rr_T <= FP_TMAX && ib + tb + 10 <= 64 && ib <= 28;  // (28: the claim pairs' slot tags)
         if (const char* e = getenv("ALLL_RR_FP")) fp = fp && atoi(e) != 0;
         if (fp) {
             const size_t nblk = m / FP_B + 2;
@@ -947,6 +947,8 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
             if ((rc = dalloc(c, &b.fp_in, m + FP_B))) return bail(rc);
             if ((rc = dalloc(c, &b.fp_turn, m + 1))) return bail(rc);
             if ((rc = dalloc(c, &b.fp_v4, (rr_width >= 1 && rr_width <= 4) ? m + 1 : 1))) return bail(rc);
+            if ((rc = dalloc(c, &b.fp_lost, 2 * (size_t)m + 16))) return bail(rc);
+            if ((rc = dalloc(c, &b.fp_sole, (size_t)m * ((rr_width >= 1 && rr_width <= 4) ? 4 : 8) + 16))) return bail(rc);
             if ((rc = dalloc(c, &b.fp_list, 2 * (size_t)m + 2))) return bail(rc);
             if ((rc = dalloc(c, &b.fp_tcnt, 2 * FP_G * ((size_t)m / 256 + 2)))) return bail(rc);  // (round tiles of 256)
             if ((rc = dalloc(c, &b.fp_owner, (size_t)prob->n_vars + 1, 0xFF))) return bail(rc);
@@ -1000,7 +1002,7 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     }
     if (b.fp_ctl) {
         // round robin: claimant lists by variable buckets (k_fp_bscatter / k_fp_bbuild): bucket =
-        // vmix(v) / width, width a multiple of 64 (whole words of fp_one), one bucket per CU
+        // vmix(v) / width, width a multiple of 64, one bucket per CU
         // when the width fits the LDS of k_fp_bbuild
         const uint64_t span = std::max<uint64_t>(vrange, 1);
         uint64_t width = (span + (uint64_t)c->n_cu - 1) / (uint64_t)c->n_cu;
@@ -1033,7 +1035,7 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
         for (uint64_t k = 0; k <= nb; ++k) { const uint32_t d = breg[k]; breg[k] = acc; acc += d; }
         uint32_t *d_soff = nullptr, *d_breg = nullptr;
         if ((rc = dalloc(c, &d_soff, soff.size())) || (rc = dalloc(c, &d_breg, breg.size())) ||
-            (rc = dalloc(c, &b.fp_bfill, nb)) || (rc = dalloc(c, &b.fp_one, span / 32 + 4)) ||
+            (rc = dalloc(c, &b.fp_bfill, nb)) ||
             (rc = dalloc(c, &b.fp_sv, (size_t)nb * width)) || (rc = dalloc(c, &b.fp_sbcnt, nb)))
             return bail(rc);
         if (hipStreamSynchronize(c->stream) != hipSuccess ||

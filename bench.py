@@ -17,6 +17,7 @@ fatal; the host-staged gloo exchange is only used with --exchange-impl host.
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config M|C2|C3|C4|C5|R]
 """
 import argparse
+import faulthandler
 import json
 import os
 import platform
@@ -182,8 +183,6 @@ def trajectory_check(cfg, T, st, words):
 def rr_line(args, n, m, k, kind, Solver, generate_ksat, device, warmup=2, steps=10):
     """GPU resample loop with the reference's n_threads = T round-robin MIS, T = the CPU
     baseline's thread count."""
-    import torch
-
     T = cpu_threads()[0]
     if isinstance(k, tuple):
         from alllsatisfiabilitysolver_amd import generate_mixed
@@ -191,24 +190,40 @@ def rr_line(args, n, m, k, kind, Solver, generate_ksat, device, warmup=2, steps=
         offs, lits = generate_mixed(1, n, m, *k)
     else:
         offs, lits = generate_ksat(1, n, m, k, kind)
+    log(f"[rank 0] round-robin line: T={T}, creating the solver")
     with Solver(n, offs, lits, seed=args.seed, device=device, n_threads=T) as r:
         del offs, lits
         r.run(warmup)
         r.synchronize()
+        log(f"[rank 0] round-robin line: {warmup} warmup iterations done, timing {steps}")
         it0 = r.stats()["n_iterations"]
-        torch.cuda.synchronize(device)
         t0 = time.perf_counter()
         r.run(steps)
         r.synchronize()
-        torch.cuda.synchronize(device)
         dt = time.perf_counter() - t0
         st = r.stats()
         traj = trajectory_check(args.config, T, st, r.assignment_words())
+    log(f"[rank 0] round-robin line: {st['n_iterations'] - it0} iterations in {dt:.2f}s")
     done = st["n_iterations"] - it0
     return {"trajectory_check": traj, "value": m * done / dt if done else None, "unit": "clause-evals/s", "n_threads": T,
             "resample_iters_per_s": done / dt if done else None, "ms_per_step": dt * 1e3 / done if done else None,
             "steps": done, "warmup": warmup, "passes_last_iter": st["lfmis_tail_rounds"],
             "mis": "round robin over T clause chunks (SATInstance.h:414-447), as the cpu_baseline's -p T path"}
+
+
+def rr_line_child(args, timeout_s=240):
+    """The round-robin line in a child process (this script with --rr-child): its own HIP
+    context and a time limit, so that it can neither disturb nor stall the main line."""
+    cmd = [sys.executable, os.path.abspath(__file__), "--rr-child", "--config", args.config, "--seed", str(args.seed)]
+    try:
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s)
+    except subprocess.TimeoutExpired:
+        return {"value": None, "error": f"round-robin line did not finish within {timeout_s} s"}
+    sys.stderr.write(p.stderr)
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    if p.returncode != 0 or not lines:
+        return {"value": None, "error": f"round-robin child exited with {p.returncode}"}
+    return json.loads(lines[-1])
 
 
 def launch_ranks(args):
@@ -251,8 +266,15 @@ def main():
     ap.add_argument("--eval-b2b", type=int, default=0,
                     help="also time N back-to-back eval-only launches (reported separately)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_eval_traffic.json"))
+    ap.add_argument("--rr-child", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
 
+    if args.rr_child:  # (rr_line_child): one JSON line on stdout, no torch in this process
+        from alllsatisfiabilitysolver_amd import Solver, generate_ksat
+
+        n, m, k, kind, _ = CONFIGS[args.config]
+        print(json.dumps(rr_line(args, n, m, k, kind, Solver, generate_ksat, 0)), flush=True)
+        return
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -265,14 +287,21 @@ def main():
     # The result is ONE JSON line on stdout: keep a private handle on it and send everything
     # else written to file descriptor 1 (RCCL's version banner at communicator init, library
     # prints) to stderr.
+    # a stalled native call shows where it stalled (stderr), instead of silence
+    faulthandler.dump_traceback_later(120, repeat=True, file=sys.stderr)
     result_out = os.fdopen(os.dup(1), "w")
     sys.stdout.flush()
     os.dup2(2, 1)
 
-    import torch
-
+    # The library (and with it the ROCm runtime it was built against) is loaded before torch:
+    # torch's wheel bundles its own HIP runtime, which the library would otherwise bind to.
+    # torch is used for the rendezvous and the host-side collectives only (gloo); device
+    # synchronisation goes through the library (the solver's stream holds all of its work).
     from alllsatisfiabilitysolver_amd import Solver, comm_unique_id, generate_ksat
     from alllsatisfiabilitysolver_amd import _native as N
+
+    N.lib()
+    import torch
 
     dist = None
     comm_id = None
@@ -327,7 +356,6 @@ def main():
     # warmup (untimed); an RCCL error here is fatal too
     s.run(args.warmup, sync=False)
     s.synchronize()
-    torch.cuda.synchronize(local_rank)
     n_comm = s.comm_size()
     ranks_seen = 1
     if dist is not None:
@@ -339,12 +367,11 @@ def main():
                              f"expected {world}")
 
     barrier()
-    torch.cuda.synchronize(local_rank)
+    s.synchronize()
     it0 = s.stats()["n_iterations"]
     t0 = time.perf_counter()
     s.run(args.steps, sync=False)
     s.synchronize()
-    torch.cuda.synchronize(local_rank)
     barrier()
     dt = time.perf_counter() - t0
     if dist is not None:
@@ -352,6 +379,7 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     st = s.stats()
+    log(f"[rank {rank}] timed {st['n_iterations'] - it0} iterations in {dt:.3f}s")
     traj = trajectory_check(args.config, 1, st, s.assignment_words()) if rank == 0 else None
     # the timed loop must have replayed the captured graphs; an eager fallback (a capture or an
     # RCCL call under capture that failed) would time a different launch pattern unannounced
@@ -454,10 +482,11 @@ def main():
         # (SATInstance.h:414-447), not the one-set LFMIS timed above: the same workload with that
         # same MIS on the GPU, for a like-for-like ratio
         try:
-            out["gpu_same_mis_as_cpu_baseline"] = rr_line(args, n, m, k, kind, Solver, generate_ksat, local_rank)
+            out["gpu_same_mis_as_cpu_baseline"] = rr_line_child(args)
         except Exception as e:  # reported, never fatal for the GPU number
             out["gpu_same_mis_as_cpu_baseline"] = {"value": None, "error": str(e)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log("[rank 0] cpu baseline: the reference's -p path on bounded samples")
         try:
             out["cpu_baseline"] = cpu_baseline(args.config, args.cpu_budget)
         except Exception as e:  # reported, never fatal for the GPU number

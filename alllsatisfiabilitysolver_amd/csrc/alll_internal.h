@@ -52,10 +52,7 @@ constexpr uint32_t RR_MW_CTL_WORDS = 1024; // k_rr_mw control block (words)
 // it.  The pick sets are iterated, LFMIS(turns(P)) -> P, until they repeat.
 constexpr uint32_t FP_TMAX = 256;          // sets (the schedule keeps T x T phase records)
 constexpr uint32_t FP_B = 2048;            // entries per block of the count / turn passes
-#ifndef ALLL_FP_G
-#define ALLL_FP_G 4
-#endif
-constexpr uint32_t FP_G = ALLL_FP_G;       // grid LFMIS rounds before the one-workgroup tail
+constexpr uint32_t FP_G = 4;               // grid LFMIS rounds before the one-workgroup tail (2, 3: slower)
 constexpr uint32_t FP_MAX_DEFAULT = 64;    // LFMIS passes per iteration before k_rr_mw decides it
 enum : uint32_t { FP_RUN = 0, FP_FINAL = 1, FP_DONE = 2, FP_OFF = 3, FP_FAIL = 4 };
 struct RRFpCtl {
@@ -224,8 +221,6 @@ struct LoopBuffers {
     const uint32_t* fp_breg;    // n_bkt + 1: static pair region of every bucket (its literal count)
     unsigned long long* fp_pairs;  // L pairs {entry, variable} grouped by bucket
     uint32_t* fp_bfill;         // n_bkt: pairs in each bucket's region (this iteration)
-    uint8_t* fp_lost;           // per scan entry: [0, m) the serial of the pass in which it lost a round-0
-                                //   variable (k_fp_vmin), [m, 2m) of a pass in which it is on a long list
     uint8_t* fp_sole;           // per scan entry, byte j = 1: slot j's variable has no other violated
                                 //   claimant this iteration (4 bytes per entry when every width <= 4, else 8)
     uint4* fp_sv;               // per bucket (bkt_width slots): shared variables {list start, count, v}

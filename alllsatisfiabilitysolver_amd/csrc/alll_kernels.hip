@@ -2299,8 +2299,6 @@ __global__ __launch_bounds__(256) void k_rr_entries(ClauseView cv, LoopBuffers b
             } else {
                 reinterpret_cast<uint2*>(b.fp_sole)[base + i] = make_uint2(0u, 0u);
             }
-            b.fp_lost[base + i] = 0u;
-            b.fp_lost[b.m + base + i] = 0u;
         }
     }
 }
@@ -3121,16 +3119,23 @@ __global__ __launch_bounds__(FP_BB_THREADS) void k_fp_bbuild(LoopBuffers b) {
     // list and the long lists' segments
     uint4* sv = reinterpret_cast<uint4*>(b.fp_sv) + (uint64_t)bk * W;
     const uint32_t sw = b.rr_k >= 1 && b.rr_k <= 4 ? 4u : 8u;  // sole bytes per entry
-    for (uint32_t w = tid; w < nw; w += FP_BB_THREADS) {
-        const uint32_t c = s_cnt[w];
-        if (c == 0u) continue;
-        const uint32_t v = vunmix(b, xb + w);
+    for (uint32_t w0 = 0; w0 < nw; w0 += FP_BB_THREADS) {  // (every thread runs every step: wave appends)
+        const uint32_t w = w0 + tid;
+        const uint32_t c = w < nw ? s_cnt[w] : 0u;
+        const uint32_t v = c ? vunmix(b, xb + w) : 0u;
+        // shared variables: one LDS atomic per wave for the list positions
+        const bool shared = c > 1u;
+        const unsigned long long bal = __ballot(shared);
+        const uint32_t lane = tid & 63;
+        uint32_t base = 0;
+        if (lane == 0 && bal) base = atomicAdd(&s_ns, (uint32_t)__popcll(bal));
+        base = __shfl(base, 0, 64);
         if (c == 1u) {
             const uint32_t x = s_first[w], i = x & FP_IMASK, j = x >> FP_SLOT_SH;
             b.fp_own0[v] = i;
             if (j < sw) b.fp_sole[(uint64_t)i * sw + j] = 1u;
-        } else {
-            sv[atomicAdd(&s_ns, 1u)] = make_uint4(s_off[w], c, v, 0u);
+        } else if (shared) {
+            sv[base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = make_uint4(s_off[w], c, v, 0u);
             if (c > FP_HEAVY) {  // long lists (hubs of skewed instances): a wave per FP_SEG claimants
                 const uint32_t ns = (c + FP_SEG - 1) / FP_SEG;
                 const uint32_t h0 = atomicAdd(&ctl->nheavy, ns);
@@ -3149,14 +3154,13 @@ __global__ __launch_bounds__(FP_BB_THREADS) void k_fp_bbuild(LoopBuffers b) {
 // skewed instances) are left to the workgroups past the buckets: a wave per segment of FP_SEG
 // claimants, lanes striding it; segments meet in the owner key by atomicMin (keys of this pass
 // are below every earlier one), and JOIN(0) compares keys for such variables (own0 = ~0).
-constexpr uint32_t FP_VS = 8;
+constexpr uint32_t FP_VS = 4;  // (1, 2, 4, 8: 444, 464, 461, 462 iterations/s at M, T = 16)
 __global__ __launch_bounds__(FP_THREADS) void k_fp_vmin(LoopBuffers b) {
     const RRFpCtl* ctl = b.fp_ctl;
     if (ctl->state != FP_RUN) return;
     const uint32_t ep = ctl->ep_base, nbw = b.n_bkt * FP_VS;
     if (blockIdx.x >= nbw) {
         const uint32_t nh = ctl->nheavy, lane = threadIdx.x & 63, hw = gridDim.x - nbw;
-        const uint8_t serial = (uint8_t)ctl->serial;
         for (uint32_t h = (blockIdx.x - nbw) * (FP_THREADS / 64) + (threadIdx.x >> 6); h < nh;
              h += hw * (FP_THREADS / 64)) {
             const uint4 sg = reinterpret_cast<const uint4*>(b.fp_heavy)[h];
@@ -3165,7 +3169,6 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_vmin(LoopBuffers b) {
                 const uint32_t i = b.fp_vlist[o];
                 const unsigned long long k = fp_key(b, ep, b.fp_turn[i], i);
                 best = k < best ? k : best;
-                b.fp_lost[b.m + i] = serial;  // (its JOIN(0) compares keys)
             }
             for (int sh = 32; sh > 0; sh >>= 1) {
                 const unsigned long long y = __shfl_xor(best, sh, 64);
@@ -3178,8 +3181,9 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_vmin(LoopBuffers b) {
         }
         return;
     }
-    const uint32_t bk = blockIdx.x / FP_VS, sl = blockIdx.x % FP_VS;
-    const uint8_t serial = (uint8_t)ctl->serial;
+    // the slices of bucket bk are workgroups bk + k n_bkt: one XCD for the bucket's lists when
+    // n_bkt is a multiple of the 8 XCDs (workgroups are dealt to the XCDs round robin)
+    const uint32_t bk = blockIdx.x % b.n_bkt, sl = blockIdx.x / b.n_bkt;
     const uint32_t ns = b.fp_sbcnt[bk];
     const uint4* sv = reinterpret_cast<const uint4*>(b.fp_sv) + (uint64_t)bk * b.bkt_width;
     for (uint32_t k = sl * FP_THREADS + threadIdx.x; k < ns; k += FP_VS * FP_THREADS) {
@@ -3201,15 +3205,11 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_vmin(LoopBuffers b) {
             const unsigned long long key = fp_key(b, ep, b.fp_turn[i], i);
             best = key < best ? key : best;
         }
-        // The losers are marked (JOIN(0) of an entry reads one byte); the winner is kept for
-        // the entries that also hold a long list's variable.  The owner key itself is not
-        // needed: the later rounds' claims are of later epochs, below any key left here
-        const uint32_t win = (uint32_t)best & ((1u << b.fp_ib) - 1u);
-        b.fp_own0[e.z] = win;
-        for (o = e.x; o < end; ++o) {
-            const uint32_t i = b.fp_vlist[o];
-            if (i != win) b.fp_lost[i] = serial;
-        }
+        // JOIN(0) reads the winning entry from a 4-byte array (half the footprint of the keys;
+        // marking the losers instead, a byte per entry, measured 4% slower).  The owner key
+        // itself is not needed: the later rounds' claims are of later epochs, below any key
+        // left here
+        b.fp_own0[e.z] = (uint32_t)best & ((1u << b.fp_ib) - 1u);
     }
 }
 
@@ -3292,14 +3292,10 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_join(ClauseView cv, LoopBuffe
                     pre = true;
                     own = (b.fp_in[i] >> 1) & 1u;
                 } else if (r == 0) {
-                    if (b.fp_lost[b.m + i] != (uint8_t)serial) {
-                        own = b.fp_lost[i] != (uint8_t)serial;  // (k_fp_vmin marked the losers)
-                    } else {  // on a long list too: the winners, and the key for the long lists
-                        fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) {
-                            const uint32_t w = b.fp_own0[v];  // (~0: a long list, reduced into the key)
-                            own &= w == i || (w == ~0u && b.fp_owner[v] == fp_key(b, ep, turn, i));
-                        });
-                    }
+                    fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) {
+                        const uint32_t w = b.fp_own0[v];  // (~0: a long list, reduced into the key)
+                        own &= w == i || (w == ~0u && b.fp_owner[v] == fp_key(b, ep, turn, i));
+                    });
                 } else {
                     const unsigned long long key = fp_key(b, ep, turn, i);
                     fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) { own &= b.fp_owner[v] == key; });

@@ -947,7 +947,6 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
             if ((rc = dalloc(c, &b.fp_in, m + FP_B))) return bail(rc);
             if ((rc = dalloc(c, &b.fp_turn, m + 1))) return bail(rc);
             if ((rc = dalloc(c, &b.fp_v4, (rr_width >= 1 && rr_width <= 4) ? m + 1 : 1))) return bail(rc);
-            if ((rc = dalloc(c, &b.fp_lost, 2 * (size_t)m + 16))) return bail(rc);
             if ((rc = dalloc(c, &b.fp_sole, (size_t)m * ((rr_width >= 1 && rr_width <= 4) ? 4 : 8) + 16))) return bail(rc);
             if ((rc = dalloc(c, &b.fp_list, 2 * (size_t)m + 2))) return bail(rc);
             if ((rc = dalloc(c, &b.fp_tcnt, 2 * FP_G * ((size_t)m / 256 + 2)))) return bail(rc);  // (round tiles of 256)

@@ -3526,6 +3526,8 @@ __global__ __launch_bounds__(256) void k_fp_sched(LoopBuffers b, int test) {
         if (threadIdx.x < 64) {
             const uint32_t lane = threadIdx.x;
             const uint32_t n = s_n[lane < T ? lane : 0];
+            // every key ((picks left) L + o) << 6 | lane fits 32 bits (a live key is never ~0u)
+            const bool k32 = ((unsigned long long)nu + 1) * T * 64 + 64 < (1ull << 32);
             uint32_t done = 0, nseg = 0, t = 0, step = 0;
             unsigned long long alive = T == 64 ? ~0ull : (1ull << T) - 1ull;
             for (uint32_t p = 0; p < T; ++p) {
@@ -3535,9 +3537,13 @@ __global__ __launch_bounds__(256) void k_fp_sched(LoopBuffers b, int test) {
                 uint32_t o = x + L - (t % L) - 1;  // (x - t - 1) mod L, x < L
                 if (o >= L) o -= L;
                 unsigned long long best = live ? (((unsigned long long)(n - done) * L + o) << 6 | lane) : ~0ull;
-                for (int q = 32; q > 0; q >>= 1) {
-                    const unsigned long long y = __shfl_xor(best, q, 64);
-                    best = y < best ? y : best;
+                if (k32) {  // the wave minimum in 32 bits (DPP reduction)
+                    best = __reduce_min_sync(~0ull, (uint32_t)best);
+                } else {
+                    for (int q = 32; q > 0; q >>= 1) {
+                        const unsigned long long y = __shfl_xor(best, q, 64);
+                        best = y < best ? y : best;
+                    }
                 }
                 const uint32_t ls = (uint32_t)(best & 63u);
                 const unsigned long long d = best >> 6;

@@ -559,6 +559,7 @@ int launch_rr_iteration(alll_ctx* c, hipEvent_t* marks) {
         ++done;
     }
     // next iteration: the passes this one needed (fp_iter = passes that changed the picks)
+    // (one or two passes fewer, with more host-driven passes after them: within noise)
     if (c->h_fp[0] == FP_FINAL || c->h_fp[0] == FP_DONE) c->rr_p = std::max<uint32_t>(1, std::min(cap, c->h_fp[2] + 1));
     return launch_rr_piece(c, marks, 2, 0);
 }
@@ -1004,7 +1005,7 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
         // vmix(v) / width, width a multiple of 64, one bucket per CU
         // when the width fits the LDS of k_fp_bbuild
         const uint64_t span = std::max<uint64_t>(vrange, 1);
-        uint64_t width = (span + (uint64_t)c->n_cu - 1) / (uint64_t)c->n_cu;
+        uint64_t width = (span + (uint64_t)c->n_cu - 1) / (uint64_t)c->n_cu;  // (two per CU: no faster)
         width = std::max<uint64_t>(1024, (width + 63) / 64 * 64);
         width = std::min<uint64_t>(width, 12288);
         uint64_t nb = (span + width - 1) / width;

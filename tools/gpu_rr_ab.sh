@@ -5,10 +5,10 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 T=$1; shift
 O=gpurun_out/$T
 mkdir -p $O
-timeout -k 10 120 python tools/rr_bench.py --config M --threads 16 --iters 10 --warmup 2 > $O/rr_base.json 2> $O/rr_base.err
+timeout -k 10 120 python tools/rr_bench.py --config M --threads 16 --iters 20 --warmup 20 > $O/rr_base.json 2> $O/rr_base.err
 rc=$?; echo "base rc=$rc"; cat $O/rr_base.json; [ $rc -ne 0 ] && exit $rc
 for v in "$@"; do
-  ALLL_LIB_AB=build/ab/liballl_$v.so timeout -k 10 120 python tools/rr_bench.py --config M --threads 16 --iters 10 --warmup 2 > $O/rr_$v.json 2> $O/rr_$v.err
+  ALLL_LIB_AB=build/ab/liballl_$v.so timeout -k 10 120 python tools/rr_bench.py --config M --threads 16 --iters 20 --warmup 20 > $O/rr_$v.json 2> $O/rr_$v.err
   rc=$?; echo "$v rc=$rc"; cat $O/rr_$v.json; [ $rc -ne 0 ] && exit $rc
 done
 exit 0

@@ -787,7 +787,7 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     if (L && prob->n_vars && prob->n_vars < (1u << 30)) {
         // degrees from per-thread 16-bit saturating histograms (4-5x faster than shared atomic
         // counters at 384M literals), exact recount for the rare saturated candidates
-        const uint64_t thr = std::max<uint64_t>(1024, 32 * (L / prob->n_vars + 1));
+        const uint64_t thr = std::max<uint64_t>(HOT_THR_MIN, HOT_MEAN_X * (L / prob->n_vars + 1));
         const unsigned dnt = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(hnt, (2ull << 30) / (2ull * prob->n_vars)));
         std::vector<std::vector<uint16_t>> hist(dnt);
         const unsigned used = parallel_chunks(L, dnt, [&](unsigned t, uint64_t j0, uint64_t j1) {

@@ -275,6 +275,7 @@ hipError_t launch_tail(const ClauseView& cv, const LoopBuffers& b, uint32_t firs
 // round robin: scan entries and the fixpoint's iteration set-up (when b.fp_ctl); n fixpoint
 // passes; k_rr_mw for an iteration the passes did not settle
 hipError_t launch_rr_prep(const ClauseView& cv, const LoopBuffers& b, hipStream_t s);
+hipError_t prepare_kernels(const ClauseView& cv, const LoopBuffers& b);  // attributes, before any capture
 hipError_t launch_rr_passes(const ClauseView& cv, const LoopBuffers& b, uint32_t n, hipStream_t s);
 hipError_t launch_rr_finish(const ClauseView& cv, const LoopBuffers& b, hipStream_t s);
 hipError_t launch_resample(const ClauseView& cv, const LoopBuffers& b, uint32_t tile_begin,

@@ -2799,7 +2799,14 @@ constexpr uint32_t FP_LDS_SEG_T = 32;     // k_fp_turn keeps the schedule in LDS
 constexpr uint32_t FP_COUNT_GRID = 1024;
 constexpr uint32_t FP_HEAVY = 64;         // claimant lists longer than this are reduced by waves
 constexpr uint32_t FP_SEG = 2048;         // claimants per wave of k_fp_vmin's long-list workgroups
-constexpr uint32_t FP_HEAVY_GRID = 512;   // ... their number (instances with hot variables)
+constexpr uint32_t FP_HEAVY_GRID = 512;
+#ifndef ALLL_FP_WGRID
+#define ALLL_FP_WGRID 1024
+#endif
+constexpr uint32_t FP_WGRID = ALLL_FP_WGRID;  // workgroups of the wave-per-tile rounds
+#ifndef ALLL_FP_WAVE
+#define ALLL_FP_WAVE 1
+#endif   // ... their number (instances with hot variables)
 constexpr uint32_t FP_SCHED_LDS_BLK = 4096;  // k_fp_sched keeps the block offsets in LDS up to this many blocks  // workgroups of k_fp_count / k_fp_turn (grid-stride over blocks)
 
 __device__ __forceinline__ unsigned long long fp_key(const LoopBuffers& b, uint32_t ep, uint32_t turn, uint32_t i) {
@@ -3213,8 +3220,55 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_vmin(LoopBuffers b) {
     }
 }
 
-// CLAIM(r), r >= 1 (round 0 is k_fp_vmin), a workgroup per round tile of FP_RT entries: the
-// tile's JOIN(r-1) survivors, less those a pick of this pass covers, claim and are listed.  Lists are per tile (slots
+// One entry of CLAIM(r), r >= 1: out when a pick of this pass covers one of its shared
+// variables, else it claims them (keep).
+template <uint32_t KW>
+__device__ __forceinline__ bool fp_claim_one(const ClauseView& cv, const LoopBuffers& b, const RREnt* U, uint32_t i,
+                                             uint32_t ep, uint32_t serial) {
+    uint4 a, v0;
+    fp_ent<KW>(b, U, i, a, v0);
+    const uint32_t sole = fp_sole_mask<KW>(b, i);
+    const uint32_t turn = b.fp_turn[i];
+    bool dead = false;
+    fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) { dead |= b.fp_cov[v] == (uint8_t)serial; });
+    if (dead) return false;
+    const unsigned long long key = fp_key(b, ep, turn, i);
+    fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) { atomicMin(&b.fp_owner[v], key); });
+    return true;
+}
+
+// One entry of JOIN(r): picked when it holds every variable it claimed (its variables covered
+// by this pass's serial); returns whether it survives to round r + 1.
+template <uint32_t KW>
+__device__ __forceinline__ bool fp_join_one(const ClauseView& cv, const LoopBuffers& b, const RREnt* U, uint32_t i,
+                                            uint32_t r, uint32_t ep, uint32_t serial, uint32_t tpre) {
+    uint4 a, v0;
+    fp_ent<KW>(b, U, i, a, v0);
+    // (a sole slot's variable is owned by the entry and covered by no other pick)
+    const uint32_t sole = fp_sole_mask<KW>(b, i);
+    const uint32_t turn = b.fp_turn[i];
+    bool own = true, pre = false;
+    if (r == 0 && turn < tpre) {  // decided as in the last pass (bit 1)
+        pre = true;
+        own = (b.fp_in[i] >> 1) & 1u;
+    } else if (r == 0) {
+        fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) {
+            const uint32_t w = b.fp_own0[v];  // (~0: a long list, reduced into the key)
+            own &= w == i || (w == ~0u && b.fp_owner[v] == fp_key(b, ep, turn, i));
+        });
+    } else {
+        const unsigned long long key = fp_key(b, ep, turn, i);
+        fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) { own &= b.fp_owner[v] == key; });
+    }
+    if (own) {
+        fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) { b.fp_cov[v] = (uint8_t)serial; });
+        b.fp_in[i] = (uint8_t)(b.fp_in[i] | 1u);
+    }
+    return !own && !pre;
+}
+
+// CLAIM(r), r = 1 (round 0 is k_fp_vmin), a workgroup per round tile of FP_RT entries: the
+// tile's JOIN(r-1) survivors claim, and are listed unless covered.  Lists are per tile (slots
 // [tile * FP_RT, +count)), counted in LDS: no global counter.
 template <uint32_t KW>
 __global__ __launch_bounds__(FP_THREADS) void k_fp_claim(ClauseView cv, LoopBuffers b, uint32_t r) {
@@ -3238,17 +3292,7 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_claim(ClauseView cv, LoopBuff
             uint32_t i = 0;
             if (j < n) {
                 i = lin[j];
-                uint4 a, v0;
-                fp_ent<KW>(b, U, i, a, v0);
-                const uint32_t sole = fp_sole_mask<KW>(b, i);
-                const uint32_t turn = b.fp_turn[i];
-                bool dead = false;
-                fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) { dead |= b.fp_cov[v] == (uint8_t)serial; });
-                if (!dead) {
-                    const unsigned long long key = fp_key(b, ep, turn, i);
-                    fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) { atomicMin(&b.fp_owner[v], key); });
-                    keep = true;
-                }
+                keep = fp_claim_one<KW>(cv, b, U, i, ep, serial);
             }
             fp_append(keep, i, &s_cnt, lout);
         }
@@ -3258,8 +3302,7 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_claim(ClauseView cv, LoopBuff
     }
 }
 
-// JOIN(r), a workgroup per tile: an entry that holds every variable it claimed is picked (its
-// variables covered by this pass's serial); the others survive to round r + 1.
+// JOIN(r), a workgroup per tile (rounds 0 and 1); the survivors go to the tile's list.
 template <uint32_t KW>
 __global__ __launch_bounds__(FP_THREADS) void k_fp_join(ClauseView cv, LoopBuffers b, uint32_t r) {
     RRFpCtl* ctl = b.fp_ctl;
@@ -3282,37 +3325,86 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_join(ClauseView cv, LoopBuffe
             uint32_t i = 0;
             if (j < n) {
                 i = r == 0 ? i0 + j : lin[j];
-                uint4 a, v0;
-                fp_ent<KW>(b, U, i, a, v0);
-                // (a sole slot's variable is owned by the entry and covered by no other pick)
-                const uint32_t sole = fp_sole_mask<KW>(b, i);
-                const uint32_t turn = b.fp_turn[i];
-                bool own = true, pre = false;
-                if (r == 0 && turn < tpre) {  // decided as in the last pass (bit 1)
-                    pre = true;
-                    own = (b.fp_in[i] >> 1) & 1u;
-                } else if (r == 0) {
-                    fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) {
-                        const uint32_t w = b.fp_own0[v];  // (~0: a long list, reduced into the key)
-                        own &= w == i || (w == ~0u && b.fp_owner[v] == fp_key(b, ep, turn, i));
-                    });
-                } else {
-                    const unsigned long long key = fp_key(b, ep, turn, i);
-                    fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) { own &= b.fp_owner[v] == key; });
-                }
-                if (own) {
-                    fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) { b.fp_cov[v] = (uint8_t)serial; });
-                    b.fp_in[i] = (uint8_t)(b.fp_in[i] | 1u);
-                }
-                keep = !own && !pre;
+                keep = fp_join_one<KW>(cv, b, U, i, r, ep, serial, tpre);
             }
-            // the last grid round's few survivors go to one list for k_fp_tail
+            // (the last grid round's survivors go to one list for k_fp_tail)
             if (r + 1 == FP_G) fp_append(keep, i, &ctl->cntJ[r], b.fp_list);
             else fp_append(keep, i, &s_cnt, lout);
         }
         __syncthreads();
         if (threadIdx.x == 0) b.fp_tcnt[(2 * r) * ntile + tile] = s_cnt;
         __syncthreads();
+    }
+}
+
+// Rounds r >= 2 (a few survivors per tile): the same CLAIM / JOIN with a wave per tile, no
+// workgroup barriers; list positions from the wave's ballots.  The last grid round's
+// survivors go to one list for k_fp_tail (one atomic per wave step that has survivors).
+__device__ __forceinline__ uint32_t fp_wave_append(bool keep, uint32_t i, uint32_t kept, uint32_t* out) {
+    const unsigned long long bal = __ballot(keep);
+    const uint32_t lane = threadIdx.x & 63;
+    if (keep) out[kept + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = i;
+    return kept + (uint32_t)__popcll(bal);
+}
+
+template <uint32_t KW>
+__global__ __launch_bounds__(FP_THREADS) void k_fp_wclaim(ClauseView cv, LoopBuffers b, uint32_t r) {
+    const RRFpCtl* ctl = b.fp_ctl;
+    if (ctl->state != FP_RUN) return;
+    const uint32_t nu = ctl->nu, lane = threadIdx.x & 63, wpb = FP_THREADS / 64;
+    const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
+    const uint32_t ntile = (nu + FP_RT - 1) / FP_RT;
+    const uint32_t ep = ctl->ep_base + r, serial = ctl->serial;
+    for (uint32_t tile = blockIdx.x * wpb + (threadIdx.x >> 6); tile < ntile; tile += gridDim.x * wpb) {
+        const uint32_t i0 = tile * FP_RT;
+        const uint32_t n = __builtin_amdgcn_readfirstlane(b.fp_tcnt[(2 * (r - 1)) * ntile + tile]);
+        const uint32_t* lin = b.fp_list + i0;
+        uint32_t* lout = b.fp_list + b.m + i0;
+        uint32_t kept = 0;
+        for (uint32_t j0 = 0; j0 < n; j0 += 64) {
+            const uint32_t j = j0 + lane;
+            bool keep = false;
+            uint32_t i = 0;
+            if (j < n) {
+                i = lin[j];
+                keep = fp_claim_one<KW>(cv, b, U, i, ep, serial);
+            }
+            kept = fp_wave_append(keep, i, kept, lout);
+        }
+        if (lane == 0) b.fp_tcnt[(2 * r - 1) * ntile + tile] = kept;
+    }
+}
+
+template <uint32_t KW>
+__global__ __launch_bounds__(FP_THREADS) void k_fp_wjoin(ClauseView cv, LoopBuffers b, uint32_t r) {
+    RRFpCtl* ctl = b.fp_ctl;
+    if (ctl->state != FP_RUN) return;
+    const uint32_t nu = ctl->nu, lane = threadIdx.x & 63, wpb = FP_THREADS / 64;
+    const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
+    const uint32_t ntile = (nu + FP_RT - 1) / FP_RT;
+    const uint32_t ep = ctl->ep_base + r, serial = ctl->serial, tpre = ctl->tpre;
+    const bool last = r + 1 == FP_G;
+    for (uint32_t tile = blockIdx.x * wpb + (threadIdx.x >> 6); tile < ntile; tile += gridDim.x * wpb) {
+        const uint32_t i0 = tile * FP_RT;
+        const uint32_t n = __builtin_amdgcn_readfirstlane(b.fp_tcnt[(2 * r - 1) * ntile + tile]);
+        const uint32_t* lin = b.fp_list + b.m + i0;
+        uint32_t* lout = b.fp_list + i0;
+        uint32_t kept = 0;
+        for (uint32_t j0 = 0; j0 < n; j0 += 64) {
+            const uint32_t j = j0 + lane;
+            bool keep = false;
+            uint32_t i = 0;
+            if (j < n) {
+                i = lin[j];
+                keep = fp_join_one<KW>(cv, b, U, i, r, ep, serial, tpre);
+            }
+            if (last) {
+                fp_append(keep, i, &ctl->cntJ[r], b.fp_list);
+            } else {
+                kept = fp_wave_append(keep, i, kept, lout);
+            }
+        }
+        if (!last && lane == 0) b.fp_tcnt[(2 * r) * ntile + tile] = kept;
     }
 }
 
@@ -3832,6 +3924,64 @@ static void attr_mark(uint32_t bit, int dev) {
     if (dev >= 0) g_attr_done[dev].fetch_or(1u << bit, std::memory_order_release);
 }
 
+// Kernel attributes of the loop (dynamic LDS above the default), set once per device and
+// kernel group by alll_create, before any stream capture: a capture then holds launches only
+// (the launchers set no attributes; a kernel whose attribute is missing fails its launch).
+hipError_t prepare_kernels(const ClauseView& cv, const LoopBuffers& b) {
+    int dev;
+    if (cv.k >= 1 && cv.k <= (uint32_t)MAX_FIXED_K && attr_pending(ATTR_HYBRID + cv.k, dev)) {
+        hipError_t e = hipSuccess;
+        ALLL_DISPATCH_K(cv.k, (e = hipFuncSetAttribute((const void*)k_eval_hybrid<(K > 0 ? K : 1)>,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       (int)(LDS_WORDS * 4 + 16))));
+        if (e != hipSuccess) return e;
+        attr_mark(ATTR_HYBRID + cv.k, dev);
+    }
+    if (cv.rg_off && attr_pending(ATTR_RAGGED, dev)) {
+        hipError_t e = hipFuncSetAttribute((const void*)k_eval_ragged, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                           (int)(LDS_WORDS * 4 + 16));
+        if (e != hipSuccess) return e;
+        attr_mark(ATTR_RAGGED, dev);
+    }
+    if (b.pairs) {
+        if (cv.k <= (uint32_t)MAX_FIXED_K && attr_pending(ATTR_BUCKETS + cv.k, dev)) {
+            hipError_t e = hipFuncSetAttribute((const void*)k_bresolve<BRS_UNROLL_WIDE, BRS_THREADS>,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)(4u << BKT_SHIFT_MAX));
+            if (e == hipSuccess)
+                e = hipFuncSetAttribute((const void*)k_bresolve<BRS_UNROLL_NARROW, BRS_THREADS>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)(4u << BKT_SHIFT_MAX));
+            if (e == hipSuccess)
+                e = hipFuncSetAttribute((const void*)k_bresolve<BRS_UNROLL_DEEP, BRS_THREADS_DEEP>,
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)(4u << BKT_SHIFT_MAX));
+            if (e != hipSuccess) return e;
+            ALLL_DISPATCH_K(cv.k, (e = hipFuncSetAttribute((const void*)k_bscatter<(K > 0 ? K : 1)>,
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                           (int)(BKT_STAGE * 8))));
+            if (e != hipSuccess) return e;
+            ALLL_DISPATCH_K(cv.k, (e = hipFuncSetAttribute((const void*)k_bjoin<(K > 0 ? K : 1)>,
+                                                           hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                           (int)(RUN_TILES_MAX * TILE))));
+            if (e != hipSuccess) return e;
+            attr_mark(ATTR_BUCKETS + cv.k, dev);
+        }
+    }
+    if (b.fp_ctl) {
+        if (attr_pending(ATTR_FP, dev)) {
+            hipError_t e = hipFuncSetAttribute((const void*)k_fp_bscatter<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               (int)(8ull * BKT_MAX + 2ull * FP_BS_ENT * 8));
+            if (e == hipSuccess)
+                e = hipFuncSetAttribute((const void*)k_fp_bscatter<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)(8ull * BKT_MAX + 2ull * FP_BS_ENT * 8));
+            if (e == hipSuccess)
+                e = hipFuncSetAttribute((const void*)k_fp_bbuild, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        160 * 1024 - 1024);
+            if (e != hipSuccess) return e;
+            attr_mark(ATTR_FP, dev);
+        }
+    }
+    return hipSuccess;
+}
+
 hipError_t launch_eval_hybrid(const ClauseView& cv, const LoopBuffers& b, uint32_t tile_begin,
                               uint32_t tile_end, bool gated, int n_blocks, bool scatter, hipStream_t s) {
     if (tile_end <= tile_begin) return hipSuccess;
@@ -3842,15 +3992,6 @@ hipError_t launch_eval_hybrid(const ClauseView& cv, const LoopBuffers& b, uint32
     size_t lds = ((size_t)(std::min(b.n_words, b.win_words) + 3) / 4 * 4 + 4) * 4;
     if (scatter) lds = std::max(lds, SCATTER_LDS_BYTES);
     const int g = gated ? 1 : 0, sc = scatter ? 1 : 0;
-    int dev;
-    if (cv.k >= 1 && cv.k <= (uint32_t)MAX_FIXED_K && attr_pending(ATTR_HYBRID + cv.k, dev)) {
-        hipError_t e = hipSuccess;
-        ALLL_DISPATCH_K(cv.k, (e = hipFuncSetAttribute((const void*)k_eval_hybrid<(K > 0 ? K : 1)>,
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                       (int)(LDS_WORDS * 4 + 16))));
-        if (e != hipSuccess) return e;
-        attr_mark(ATTR_HYBRID + cv.k, dev);
-    }
     switch (cv.k) {
         case 1: k_eval_hybrid<1><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g, sc); break;
         case 2: k_eval_hybrid<2><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g, sc); break;
@@ -3871,13 +4012,6 @@ hipError_t launch_eval_ragged(const ClauseView& cv, const LoopBuffers& b, uint32
     const uint32_t nt = tile_end - tile_begin;
     const dim3 grid(std::min<uint32_t>(nt, (uint32_t)std::max(1, n_blocks)));
     const size_t lds = ((size_t)(std::min(b.n_words, b.win_words) + 3) / 4 * 4 + 4) * 4;
-    int dev;
-    if (attr_pending(ATTR_RAGGED, dev)) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_eval_ragged, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)(LDS_WORDS * 4 + 16));
-        if (e != hipSuccess) return e;
-        attr_mark(ATTR_RAGGED, dev);
-    }
     k_eval_ragged<<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, gated ? 1 : 0);
     return hipGetLastError();
 }
@@ -3932,27 +4066,6 @@ hipError_t launch_round0_buckets(const ClauseView& cv, const LoopBuffers& b, boo
     if (b.n_tiles == 0 || cv.k == 0 || !b.pairs) return hipErrorInvalidValue;
     const uint64_t run_cap = (uint64_t)b.run_tiles * TILE * cv.k;
     const size_t lds = (size_t)4 * b.bkt_width;  // k_bresolve minima
-    int dev;
-    if (cv.k <= (uint32_t)MAX_FIXED_K && attr_pending(ATTR_BUCKETS + cv.k, dev)) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_bresolve<BRS_UNROLL_WIDE, BRS_THREADS>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)(4u << BKT_SHIFT_MAX));
-        if (e == hipSuccess)
-            e = hipFuncSetAttribute((const void*)k_bresolve<BRS_UNROLL_NARROW, BRS_THREADS>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)(4u << BKT_SHIFT_MAX));
-        if (e == hipSuccess)
-            e = hipFuncSetAttribute((const void*)k_bresolve<BRS_UNROLL_DEEP, BRS_THREADS_DEEP>,
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)(4u << BKT_SHIFT_MAX));
-        if (e != hipSuccess) return e;
-        ALLL_DISPATCH_K(cv.k, (e = hipFuncSetAttribute((const void*)k_bscatter<(K > 0 ? K : 1)>,
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                       (int)(BKT_STAGE * 8))));
-        if (e != hipSuccess) return e;
-        ALLL_DISPATCH_K(cv.k, (e = hipFuncSetAttribute((const void*)k_bjoin<(K > 0 ? K : 1)>,
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                       (int)(RUN_TILES_MAX * TILE))));
-        if (e != hipSuccess) return e;
-        attr_mark(ATTR_BUCKETS + cv.k, dev);
-    }
     // fused_reduce: the loop's reduce has not run; it runs in an extra workgroup of k_bresolve
     // (the scatter uses the pre-reduce epoch).  scattered: k_eval_hybrid has scattered the runs.
     const int fr = fused_reduce ? 1 : 0;
@@ -3984,7 +4097,7 @@ hipError_t launch_tail(const ClauseView& cv, const LoopBuffers& b, uint32_t firs
 
 // grids of the fixpoint kernels
 struct FpGrids {
-    uint32_t gb, gl, gr;
+    uint32_t gb, gl, gr, gw;
     bool narrow;
 };
 static FpGrids fp_grids(const LoopBuffers& b) {
@@ -3994,6 +4107,8 @@ static FpGrids fp_grids(const LoopBuffers& b) {
     g.gl = (uint32_t)std::min<uint64_t>((b.m + FP_THREADS - 1) / FP_THREADS + 1, 2048);
     // workgroups of the grid-stride round kernels (2048)
     g.gr = (uint32_t)std::min<uint64_t>((b.m + FP_RT - 1) / FP_RT + 1, 2048);
+    // wave-per-tile rounds: four tiles per workgroup
+    g.gw = (uint32_t)std::min<uint64_t>(((b.m + FP_RT - 1) / FP_RT + 4) / 4, FP_WGRID);
     return g;
 }
 
@@ -4024,19 +4139,6 @@ hipError_t launch_rr_prep(const ClauseView& cv, const LoopBuffers& b, hipStream_
     const FpGrids g = fp_grids(b);
     const size_t lds_bs = 8ull * b.n_bkt + 2ull * FP_BS_ENT * 8;
     const size_t lds_bb = fp_bbuild_lds_bytes(b.bkt_width);
-    int dev;
-    if (attr_pending(ATTR_FP, dev)) {
-        hipError_t e = hipFuncSetAttribute((const void*)k_fp_bscatter<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)(8ull * BKT_MAX + 2ull * FP_BS_ENT * 8));
-        if (e == hipSuccess)
-            e = hipFuncSetAttribute((const void*)k_fp_bscatter<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    (int)(8ull * BKT_MAX + 2ull * FP_BS_ENT * 8));
-        if (e == hipSuccess)
-            e = hipFuncSetAttribute((const void*)k_fp_bbuild, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    160 * 1024 - 1024);
-        if (e != hipSuccess) return e;
-        attr_mark(ATTR_FP, dev);
-    }
     hipError_t e = hipMemsetAsync(b.fp_owner, 0xFF, (size_t)b.n_vars * 8, s);
     if (e == hipSuccess) e = hipMemsetAsync(b.fp_cov, 0, (size_t)b.n_vars, s);
     if (e != hipSuccess) return e;
@@ -4060,12 +4162,20 @@ hipError_t launch_rr_passes(const ClauseView& cv, const LoopBuffers& b, uint32_t
                 k_fp_vmin<<<b.n_bkt * FP_VS + (cv.n_hot ? FP_HEAVY_GRID : 16u), FP_THREADS, 0, s>>>(b);
                 if (g.narrow) k_fp_join<4><<<g.gr, FP_THREADS, 0, s>>>(cv, b, 0);
                 else k_fp_join<0><<<g.gr, FP_THREADS, 0, s>>>(cv, b, 0);
-            } else if (g.narrow) {
-                k_fp_claim<4><<<g.gr, FP_THREADS, 0, s>>>(cv, b, r);
-                k_fp_join<4><<<g.gr, FP_THREADS, 0, s>>>(cv, b, r);
+            } else if (r == 1 || !ALLL_FP_WAVE) {
+                if (g.narrow) {
+                    k_fp_claim<4><<<g.gr, FP_THREADS, 0, s>>>(cv, b, r);
+                    k_fp_join<4><<<g.gr, FP_THREADS, 0, s>>>(cv, b, r);
+                } else {
+                    k_fp_claim<0><<<g.gr, FP_THREADS, 0, s>>>(cv, b, r);
+                    k_fp_join<0><<<g.gr, FP_THREADS, 0, s>>>(cv, b, r);
+                }
+            } else if (g.narrow) {  // (rounds 2..: a wave per tile)
+                k_fp_wclaim<4><<<g.gw, FP_THREADS, 0, s>>>(cv, b, r);
+                k_fp_wjoin<4><<<g.gw, FP_THREADS, 0, s>>>(cv, b, r);
             } else {
-                k_fp_claim<0><<<g.gr, FP_THREADS, 0, s>>>(cv, b, r);
-                k_fp_join<0><<<g.gr, FP_THREADS, 0, s>>>(cv, b, r);
+                k_fp_wclaim<0><<<g.gw, FP_THREADS, 0, s>>>(cv, b, r);
+                k_fp_wjoin<0><<<g.gw, FP_THREADS, 0, s>>>(cv, b, r);
             }
         }
         if (g.narrow) k_fp_tail<4><<<1, 1024, 0, s>>>(cv, b);

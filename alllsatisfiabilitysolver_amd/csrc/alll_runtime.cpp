@@ -1333,6 +1333,10 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
         return bail(fail(ALLL_ERR_HIP, "state upload failed"));
     if (launch_init_assignment(b, c->stream) != hipSuccess)
         return bail(fail(ALLL_ERR_HIP, "init kernel launch failed"));
+    {  // kernel attributes (dynamic LDS), outside every stream capture
+        const hipError_t e = prepare_kernels(cv, b);
+        if (e != hipSuccess) return bail(fail(ALLL_ERR_HIP, "kernel attributes: %s", hipGetErrorString(e)));
+    }
 
     // ---- RCCL communicator (clause-sharded mode; world 1 with a comm id: a one-rank
     // communicator that runs the multi-GPU exchange path on one GPU)

@@ -8,16 +8,25 @@ reproduce the serial oracle trajectory bit for bit, with per-GPU resample shares
 """
 import os
 import socket
+import sys
 
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# (spawned ranks import this module first: the library's ROCm runtime before torch's)
+sys.path.insert(0, ROOT)
+from alllsatisfiabilitysolver_amd import _native as _alll_native  # noqa: E402
+
+try:
+    _alll_native.lib()
+except Exception:
+    pass
 torch = pytest.importorskip("torch")
 import torch.distributed as dist  # noqa: E402
 import torch.multiprocessing as mp  # noqa: E402
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def free_port():

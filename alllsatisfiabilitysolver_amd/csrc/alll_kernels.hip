@@ -2800,13 +2800,10 @@ constexpr uint32_t FP_COUNT_GRID = 1024;
 constexpr uint32_t FP_HEAVY = 64;         // claimant lists longer than this are reduced by waves
 constexpr uint32_t FP_SEG = 2048;         // claimants per wave of k_fp_vmin's long-list workgroups
 constexpr uint32_t FP_HEAVY_GRID = 512;
-#ifndef ALLL_FP_WGRID
-#define ALLL_FP_WGRID 1024
-#endif
-constexpr uint32_t FP_WGRID = ALLL_FP_WGRID;  // workgroups of the wave-per-tile rounds
-#ifndef ALLL_FP_WAVE
-#define ALLL_FP_WAVE 1
-#endif   // ... their number (instances with hot variables)
+// workgroups of the wave-per-tile rounds (512 / 1024 / 2048: 607 / 627 / 628 iterations/s at
+// M, T = 16; the workgroup-per-tile kernels for these rounds: 605)
+constexpr uint32_t FP_WGRID = 1024;
+   // ... their number (instances with hot variables)
 constexpr uint32_t FP_SCHED_LDS_BLK = 4096;  // k_fp_sched keeps the block offsets in LDS up to this many blocks  // workgroups of k_fp_count / k_fp_turn (grid-stride over blocks)
 
 __device__ __forceinline__ unsigned long long fp_key(const LoopBuffers& b, uint32_t ep, uint32_t turn, uint32_t i) {
@@ -3267,44 +3264,12 @@ __device__ __forceinline__ bool fp_join_one(const ClauseView& cv, const LoopBuff
     return !own && !pre;
 }
 
-// CLAIM(r), r = 1 (round 0 is k_fp_vmin), a workgroup per round tile of FP_RT entries: the
-// tile's JOIN(r-1) survivors claim, and are listed unless covered.  Lists are per tile (slots
-// [tile * FP_RT, +count)), counted in LDS: no global counter.
+// JOIN(0), a workgroup per round tile of FP_RT entries (every entry of the pass): the
+// survivors go to the tile's list (slots [tile * FP_RT, +count), counted in LDS: no global
+// counter).
 template <uint32_t KW>
-__global__ __launch_bounds__(FP_THREADS) void k_fp_claim(ClauseView cv, LoopBuffers b, uint32_t r) {
-    const RRFpCtl* ctl = b.fp_ctl;
-    if (ctl->state != FP_RUN) return;
-    const uint32_t nu = ctl->nu;
-    __shared__ uint32_t s_cnt;
-    const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
-    const uint32_t ntile = (nu + FP_RT - 1) / FP_RT;
-    const uint32_t ep = ctl->ep_base + r, serial = ctl->serial;
-    for (uint32_t tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
-        const uint32_t i0 = tile * FP_RT;
-        if (threadIdx.x == 0) s_cnt = 0;
-        __syncthreads();
-        const uint32_t n = b.fp_tcnt[(2 * (r - 1)) * ntile + tile];
-        const uint32_t* lin = b.fp_list + i0;
-        uint32_t* lout = b.fp_list + b.m + i0;
-        for (uint32_t j0 = 0; j0 < n; j0 += blockDim.x) {
-            const uint32_t j = j0 + threadIdx.x;
-            bool keep = false;
-            uint32_t i = 0;
-            if (j < n) {
-                i = lin[j];
-                keep = fp_claim_one<KW>(cv, b, U, i, ep, serial);
-            }
-            fp_append(keep, i, &s_cnt, lout);
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) b.fp_tcnt[(2 * r - 1) * ntile + tile] = s_cnt;
-        __syncthreads();
-    }
-}
-
-// JOIN(r), a workgroup per tile (rounds 0 and 1); the survivors go to the tile's list.
-template <uint32_t KW>
-__global__ __launch_bounds__(FP_THREADS) void k_fp_join(ClauseView cv, LoopBuffers b, uint32_t r) {
+__global__ __launch_bounds__(FP_THREADS) void k_fp_join0(ClauseView cv, LoopBuffers b) {
+    constexpr uint32_t r = 0;
     RRFpCtl* ctl = b.fp_ctl;
     if (ctl->state != FP_RUN) return;
     const uint32_t nu = ctl->nu;
@@ -3316,30 +3281,28 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_join(ClauseView cv, LoopBuffe
         const uint32_t i0 = tile * FP_RT;
         if (threadIdx.x == 0) s_cnt = 0;
         __syncthreads();
-        const uint32_t n = r == 0 ? min(FP_RT, nu - i0) : b.fp_tcnt[(2 * r - 1) * ntile + tile];
-        const uint32_t* lin = b.fp_list + b.m + i0;
+        const uint32_t n = min(FP_RT, nu - i0);
         uint32_t* lout = b.fp_list + i0;
         for (uint32_t j0 = 0; j0 < n; j0 += blockDim.x) {
             const uint32_t j = j0 + threadIdx.x;
             bool keep = false;
             uint32_t i = 0;
             if (j < n) {
-                i = r == 0 ? i0 + j : lin[j];
+                i = i0 + j;
                 keep = fp_join_one<KW>(cv, b, U, i, r, ep, serial, tpre);
             }
-            // (the last grid round's survivors go to one list for k_fp_tail)
-            if (r + 1 == FP_G) fp_append(keep, i, &ctl->cntJ[r], b.fp_list);
-            else fp_append(keep, i, &s_cnt, lout);
+            fp_append(keep, i, &s_cnt, lout);
         }
         __syncthreads();
-        if (threadIdx.x == 0) b.fp_tcnt[(2 * r) * ntile + tile] = s_cnt;
+        if (threadIdx.x == 0) b.fp_tcnt[tile] = s_cnt;
         __syncthreads();
     }
 }
 
-// Rounds r >= 2 (a few survivors per tile): the same CLAIM / JOIN with a wave per tile, no
-// workgroup barriers; list positions from the wave's ballots.  The last grid round's
-// survivors go to one list for k_fp_tail (one atomic per wave step that has survivors).
+// Rounds r >= 1 (round 1: ~100 of a tile's 256 entries, then a few): CLAIM(r) / JOIN(r) with a
+// wave per tile, no workgroup barriers; list positions from the wave's ballots.  The last grid
+// round's survivors go to one list for k_fp_tail (one atomic per wave step that has
+// survivors).  (A workgroup per tile measured the same in round 1 and 3.5% slower overall.)
 __device__ __forceinline__ uint32_t fp_wave_append(bool keep, uint32_t i, uint32_t kept, uint32_t* out) {
     const unsigned long long bal = __ballot(keep);
     const uint32_t lane = threadIdx.x & 63;
@@ -4156,21 +4119,14 @@ hipError_t launch_rr_passes(const ClauseView& cv, const LoopBuffers& b, uint32_t
     if (!b.fp_ctl) return hipSuccess;
     const FpGrids g = fp_grids(b);
     for (uint32_t p = 0; p < n; ++p) {
-        for (uint32_t r = 0; r < FP_G; ++r) {
-            if (r == 0) {
-                // (instances with hot variables get FP_HEAVY_GRID more workgroups for the long lists)
-                k_fp_vmin<<<b.n_bkt * FP_VS + (cv.n_hot ? FP_HEAVY_GRID : 16u), FP_THREADS, 0, s>>>(b);
-                if (g.narrow) k_fp_join<4><<<g.gr, FP_THREADS, 0, s>>>(cv, b, 0);
-                else k_fp_join<0><<<g.gr, FP_THREADS, 0, s>>>(cv, b, 0);
-            } else if (r == 1 || !ALLL_FP_WAVE) {
-                if (g.narrow) {
-                    k_fp_claim<4><<<g.gr, FP_THREADS, 0, s>>>(cv, b, r);
-                    k_fp_join<4><<<g.gr, FP_THREADS, 0, s>>>(cv, b, r);
-                } else {
-                    k_fp_claim<0><<<g.gr, FP_THREADS, 0, s>>>(cv, b, r);
-                    k_fp_join<0><<<g.gr, FP_THREADS, 0, s>>>(cv, b, r);
-                }
-            } else if (g.narrow) {  // (rounds 2..: a wave per tile)
+        // round 0: the claimant-list minima, then JOIN(0) (a workgroup per tile); rounds 1..:
+        // a wave per tile.  (Instances with hot variables get FP_HEAVY_GRID more k_fp_vmin
+        // workgroups for the long lists.)
+        k_fp_vmin<<<b.n_bkt * FP_VS + (cv.n_hot ? FP_HEAVY_GRID : 16u), FP_THREADS, 0, s>>>(b);
+        if (g.narrow) k_fp_join0<4><<<g.gr, FP_THREADS, 0, s>>>(cv, b);
+        else k_fp_join0<0><<<g.gr, FP_THREADS, 0, s>>>(cv, b);
+        for (uint32_t r = 1; r < FP_G; ++r) {
+            if (g.narrow) {
                 k_fp_wclaim<4><<<g.gw, FP_THREADS, 0, s>>>(cv, b, r);
                 k_fp_wjoin<4><<<g.gw, FP_THREADS, 0, s>>>(cv, b, r);
             } else {

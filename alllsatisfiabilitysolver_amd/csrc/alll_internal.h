@@ -57,6 +57,8 @@ constexpr uint32_t RR_MW_CTL_WORDS = 1024; // k_rr_mw control block (words)
 constexpr uint32_t FP_TMAX = 256;          // sets (the schedule keeps T x T phase records)
 constexpr uint32_t FP_B = 2048;            // entries per block of the count / turn passes
 constexpr uint32_t FP_G = 4;               // grid LFMIS rounds before the one-workgroup tail (2, 3: slower)
+constexpr uint32_t FP_G_HOT = 8;           // ... on instances with hot variables (longer dependency chains)
+constexpr uint32_t FP_G_MAX = 8;
 constexpr uint32_t FP_MAX_DEFAULT = 64;    // LFMIS passes per iteration before k_rr_mw decides it
 enum : uint32_t { FP_RUN = 0, FP_FINAL = 1, FP_DONE = 2, FP_OFF = 3, FP_FAIL = 4 };
 struct RRFpCtl {
@@ -214,7 +216,7 @@ struct LoopBuffers {
     uint32_t* fp_turn;          // per scan entry: turn = LFMIS priority of the next pass
     uint4* fp_v4;               // per scan entry of narrow instances: its variables (16-byte copy)
     uint32_t* fp_list;          // 2 x m: round lists per tile of FP_B entries (JOIN output, CLAIM output)
-    uint32_t* fp_tcnt;          // 2 FP_G x tiles: list lengths per round and tile
+    uint32_t* fp_tcnt;          // 2 FP_G_MAX x tiles: list lengths per round and tile
     unsigned long long* fp_owner; // n_vars claim keys {epoch | turn | entry}, reset every iteration
     uint32_t* fp_own0;          // n_vars: round-0 winner (entry) of every claimed variable (single
                                 // claimants: for the whole iteration, k_fp_bbuild; shared: per pass)
@@ -225,6 +227,8 @@ struct LoopBuffers {
     const uint32_t* fp_breg;    // n_bkt + 1: static pair region of every bucket (its literal count)
     unsigned long long* fp_pairs;  // L pairs {entry, variable} grouped by bucket
     uint32_t* fp_bfill;         // n_bkt: pairs in each bucket's region (this iteration)
+    uint8_t* fp_hv;             // per variable (hot instances): the iteration stamp when it has > FP_HEAVY
+                                //   violated claimants (its round claims are reduced in LDS first)
     uint8_t* fp_sole;           // per scan entry, byte j = 1: slot j's variable has no other violated
                                 //   claimant this iteration (4 bytes per entry when every width <= 4, else 8)
     uint4* fp_sv;               // per bucket (bkt_width slots): shared variables {list start, count, v}
@@ -239,6 +243,7 @@ struct LoopBuffers {
     uint4* fp_seg;              // T x T: {first level, first step, stride, offset} per (set, phase)
     uint32_t* fp_erase;         // T: erasure steps, ascending
     uint32_t fp_ib, fp_tb;      // key bits of the entry index and of the turn
+    uint32_t fp_hot;            // the instance has hot variables (more grid rounds per pass)
     uint32_t fp_max;            // LFMIS passes per iteration
     uint32_t n_vars;
     uint32_t n_words;

@@ -3111,9 +3111,22 @@ __global__ __launch_bounds__(FP_BB_THREADS) void k_fp_bbuild(LoopBuffers b) {
         }
 #pragma unroll
         for (uint32_t u = 0; u < U4; ++u) {
-            if (p[u].y == ~0u) continue;
-            const uint32_t w = vmix(b, p[u].y) - xb;
-            const uint32_t r = atomicAdd(&s_cnt[w], 1u);
+            // ranks by LDS counter; the lanes that share the first valid lane's variable take
+            // theirs from one atomic (a hub's claims would serialise on one LDS word)
+            const bool valid = p[u].y != ~0u;
+            const unsigned long long vb = __ballot(valid);
+            if (!vb) continue;
+            const uint32_t w = valid ? vmix(b, p[u].y) - xb : 0u;
+            const int fl = __ffsll((long long)vb) - 1;
+            const uint32_t wl = __shfl(w, fl, 64);
+            const bool grp = valid && w == wl;
+            const unsigned long long same = __ballot(grp);
+            uint32_t base = 0;
+            if ((int)(tid & 63) == fl) base = atomicAdd(&s_cnt[wl], (uint32_t)__popcll(same));
+            base = __shfl(base, fl, 64);
+            if (!valid) continue;
+            const uint32_t r = grp ? base + (uint32_t)__popcll(same & ((1ull << (tid & 63)) - 1ull))
+                                   : atomicAdd(&s_cnt[w], 1u);
             if (r == 0) s_first[w] = p[u].x;
             b.fp_vlist[s_off[w] + r] = p[u].x & FP_IMASK;
         }
@@ -3141,6 +3154,7 @@ __global__ __launch_bounds__(FP_BB_THREADS) void k_fp_bbuild(LoopBuffers b) {
         } else if (shared) {
             sv[base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = make_uint4(s_off[w], c, v, 0u);
             if (c > FP_HEAVY) {  // long lists (hubs of skewed instances): a wave per FP_SEG claimants
+                if (b.fp_hv) b.fp_hv[v] = (uint8_t)b.state->stamp;
                 const uint32_t ns = (c + FP_SEG - 1) / FP_SEG;
                 const uint32_t h0 = atomicAdd(&ctl->nheavy, ns);
                 for (uint32_t k = 0; k < ns; ++k)
@@ -3219,9 +3233,43 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_vmin(LoopBuffers b) {
 
 // One entry of CLAIM(r), r >= 1: out when a pick of this pass covers one of its shared
 // variables, else it claims them (keep).
+// Claims on the long lists' variables (hot instances) go through a workgroup's LDS table
+// first (bounded probing; a claim that finds no slot goes to memory): a hub's claimants would
+// otherwise serialise on one owner word.  fp_ht_flush sends one claim per variable, and only
+// one that can still lower the owner key (keys only decrease).
+struct FpHotTable {
+    uint32_t* k;
+    unsigned long long* v;
+};
+__device__ __forceinline__ void fp_ht_init(const FpHotTable& t) {
+    for (uint32_t q = threadIdx.x; q < HOT_SLOTS; q += blockDim.x) { t.k[q] = 0xFFFFFFFFu; t.v[q] = ~0ull; }
+}
+__device__ __forceinline__ void fp_ht_claim(const FpHotTable& t, unsigned long long* owner, uint32_t var,
+                                            unsigned long long key) {
+    uint32_t h = (var * 2654435761u) & (HOT_SLOTS - 1);
+    for (int probe = 0; probe < 32; ++probe) {
+        const uint32_t prev = atomicCAS(&t.k[h], 0xFFFFFFFFu, var);
+        if (prev == 0xFFFFFFFFu || prev == var) {
+            __hip_atomic_fetch_min(&t.v[h], key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            return;
+        }
+        h = (h + 1) & (HOT_SLOTS - 1);
+    }
+    atomicMin(&owner[var], key);
+}
+__device__ __forceinline__ void fp_ht_flush(const FpHotTable& t, unsigned long long* owner) {
+    for (uint32_t q = threadIdx.x; q < HOT_SLOTS; q += blockDim.x) {
+        const uint32_t var = t.k[q];
+        if (var == 0xFFFFFFFFu) continue;
+        unsigned long long* o = &owner[var];
+        if (t.v[q] < __hip_atomic_load(o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) atomicMin(o, t.v[q]);
+    }
+}
+
 template <uint32_t KW>
 __device__ __forceinline__ bool fp_claim_one(const ClauseView& cv, const LoopBuffers& b, const RREnt* U, uint32_t i,
-                                             uint32_t ep, uint32_t serial) {
+                                             uint32_t ep, uint32_t serial, uint32_t* hk, unsigned long long* hv,
+                                             uint8_t stamp) {
     uint4 a, v0;
     fp_ent<KW>(b, U, i, a, v0);
     const uint32_t sole = fp_sole_mask<KW>(b, i);
@@ -3230,7 +3278,10 @@ __device__ __forceinline__ bool fp_claim_one(const ClauseView& cv, const LoopBuf
     fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) { dead |= b.fp_cov[v] == (uint8_t)serial; });
     if (dead) return false;
     const unsigned long long key = fp_key(b, ep, turn, i);
-    fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) { atomicMin(&b.fp_owner[v], key); });
+    fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) {
+        if (hk && b.fp_hv[v] == stamp) fp_ht_claim(FpHotTable{hk, hv}, b.fp_owner, v, key);
+        else atomicMin(&b.fp_owner[v], key);
+    });
     return true;
 }
 
@@ -3300,9 +3351,8 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_join0(ClauseView cv, LoopBuff
 }
 
 // Rounds r >= 1 (round 1: ~100 of a tile's 256 entries, then a few): CLAIM(r) / JOIN(r) with a
-// wave per tile, no workgroup barriers; list positions from the wave's ballots.  The last grid
-// round's survivors go to one list for k_fp_tail (one atomic per wave step that has
-// survivors).  (A workgroup per tile measured the same in round 1 and 3.5% slower overall.)
+// wave per tile, no workgroup barriers; list positions from the wave's ballots.  (A workgroup
+// per tile measured the same in round 1 and 3.5% slower overall.)
 __device__ __forceinline__ uint32_t fp_wave_append(bool keep, uint32_t i, uint32_t kept, uint32_t* out) {
     const unsigned long long bal = __ballot(keep);
     const uint32_t lane = threadIdx.x & 63;
@@ -3318,6 +3368,14 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_wclaim(ClauseView cv, LoopBuf
     const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
     const uint32_t ntile = (nu + FP_RT - 1) / FP_RT;
     const uint32_t ep = ctl->ep_base + r, serial = ctl->serial;
+    __shared__ uint32_t s_hk[HOT_SLOTS];
+    __shared__ unsigned long long s_hv[HOT_SLOTS];
+    const bool hot = b.fp_hv != nullptr;
+    const uint8_t stamp = hot ? (uint8_t)b.state->stamp : 0;
+    if (hot) {
+        fp_ht_init(FpHotTable{s_hk, s_hv});
+        __syncthreads();
+    }
     for (uint32_t tile = blockIdx.x * wpb + (threadIdx.x >> 6); tile < ntile; tile += gridDim.x * wpb) {
         const uint32_t i0 = tile * FP_RT;
         const uint32_t n = __builtin_amdgcn_readfirstlane(b.fp_tcnt[(2 * (r - 1)) * ntile + tile]);
@@ -3330,23 +3388,27 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_wclaim(ClauseView cv, LoopBuf
             uint32_t i = 0;
             if (j < n) {
                 i = lin[j];
-                keep = fp_claim_one<KW>(cv, b, U, i, ep, serial);
+                keep = fp_claim_one<KW>(cv, b, U, i, ep, serial, hot ? s_hk : nullptr, s_hv, stamp);
             }
             kept = fp_wave_append(keep, i, kept, lout);
         }
         if (lane == 0) b.fp_tcnt[(2 * r - 1) * ntile + tile] = kept;
     }
+    if (hot) {  // (every wave of the workgroup reaches this barrier)
+        __syncthreads();
+        fp_ht_flush(FpHotTable{s_hk, s_hv}, b.fp_owner);
+    }
 }
 
 template <uint32_t KW>
 __global__ __launch_bounds__(FP_THREADS) void k_fp_wjoin(ClauseView cv, LoopBuffers b, uint32_t r) {
+    // (the last grid round's lists are compacted by k_fp_tail: no contended counter)
     RRFpCtl* ctl = b.fp_ctl;
     if (ctl->state != FP_RUN) return;
     const uint32_t nu = ctl->nu, lane = threadIdx.x & 63, wpb = FP_THREADS / 64;
     const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
     const uint32_t ntile = (nu + FP_RT - 1) / FP_RT;
     const uint32_t ep = ctl->ep_base + r, serial = ctl->serial, tpre = ctl->tpre;
-    const bool last = r + 1 == FP_G;
     for (uint32_t tile = blockIdx.x * wpb + (threadIdx.x >> 6); tile < ntile; tile += gridDim.x * wpb) {
         const uint32_t i0 = tile * FP_RT;
         const uint32_t n = __builtin_amdgcn_readfirstlane(b.fp_tcnt[(2 * r - 1) * ntile + tile]);
@@ -3361,30 +3423,44 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_wjoin(ClauseView cv, LoopBuff
                 i = lin[j];
                 keep = fp_join_one<KW>(cv, b, U, i, r, ep, serial, tpre);
             }
-            if (last) {
-                fp_append(keep, i, &ctl->cntJ[r], b.fp_list);
-            } else {
-                kept = fp_wave_append(keep, i, kept, lout);
-            }
+            kept = fp_wave_append(keep, i, kept, lout);
         }
-        if (!last && lane == 0) b.fp_tcnt[(2 * r) * ntile + tile] = kept;
+        if (lane == 0) b.fp_tcnt[(2 * r) * ntile + tile] = kept;
     }
 }
 
 // The pass's remaining rounds in one workgroup (the lists are short by now).  Reads that other
 // threads' atomics or stores of this launch decide go around L1 (agent-scope loads).
 template <uint32_t KW>
-__global__ __launch_bounds__(1024) void k_fp_tail(ClauseView cv, LoopBuffers b) {
+__global__ __launch_bounds__(1024) void k_fp_tail(ClauseView cv, LoopBuffers b, uint32_t rg) {
     RRFpCtl* ctl = b.fp_ctl;
     if (ctl->state != FP_RUN) return;
     const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
-    __shared__ uint32_t s_cnt;
-    uint32_t* la = b.fp_list;
-    uint32_t* lb = b.fp_list + b.m;
+    __shared__ uint32_t s_cnt, s_w[16];
+    // the last grid round (rg - 1) left its survivors in per-tile lists (fp_list + tile * FP_RT,
+    // counts in fp_tcnt): compacted into the other half of fp_list, a range of tiles per thread
+    uint32_t* la = b.fp_list + b.m;
+    uint32_t* lb = b.fp_list;
+    uint32_t n;
+    {
+        const uint32_t ntile = (ctl->nu + FP_RT - 1) / FP_RT;
+        const uint32_t* tc = b.fp_tcnt + (2 * (rg - 1)) * ntile;
+        const uint32_t per = (ntile + blockDim.x - 1) / blockDim.x;
+        const uint32_t t0 = min(ntile, threadIdx.x * per), t1 = min(ntile, t0 + per);
+        uint32_t sum = 0;
+        for (uint32_t t = t0; t < t1; ++t) sum += tc[t];
+        uint32_t pos = fp_block_scan(sum, s_w, n);
+        for (uint32_t t = t0; t < t1; ++t) {
+            const uint32_t c = tc[t];
+            for (uint32_t k = 0; k < c; ++k) la[pos + k] = lb[t * FP_RT + k];
+            pos += c;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
     const uint32_t serial = ctl->serial, budget = fp_ep_budget(b);
-    uint32_t ep = ctl->ep_base + FP_G;
+    uint32_t ep = ctl->ep_base + rg;
     bool failed = false;
-    uint32_t n = ctl->cntJ[FP_G - 1];  // the last grid round's survivors, listed in la
     while (n > 0) {
         if (ep >= budget) { failed = true; break; }
         if (threadIdx.x == 0) s_cnt = 0;
@@ -3719,7 +3795,7 @@ __global__ __launch_bounds__(256) void k_fp_sched(LoopBuffers b, int test) {
             if (test) ctl->fp_iter += 1;
             ctl->ep_base = ctl->ep_next;
             ctl->serial = ctl->serial + 1u;  // 8-bit cover serials: at most 255 passes per iteration
-            if (ctl->ep_base + FP_G + 1u >= fp_ep_budget(b) || ctl->serial > 255u) ctl->state = FP_FAIL;
+            if (ctl->ep_base + FP_G_MAX + 1u >= fp_ep_budget(b) || ctl->serial > 255u) ctl->state = FP_FAIL;
         }
     }
 }
@@ -4061,11 +4137,13 @@ hipError_t launch_tail(const ClauseView& cv, const LoopBuffers& b, uint32_t firs
 // grids of the fixpoint kernels
 struct FpGrids {
     uint32_t gb, gl, gr, gw;
+    uint32_t rounds;  // grid rounds before the one-workgroup tail
     bool narrow;
 };
 static FpGrids fp_grids(const LoopBuffers& b) {
     FpGrids g;
     g.narrow = b.rr_k >= 1 && b.rr_k <= 4;
+    g.rounds = b.fp_hot ? FP_G_HOT : FP_G;
     g.gb = (uint32_t)std::min<uint64_t>((b.m + FP_B - 1) / FP_B + 1, FP_COUNT_GRID);
     g.gl = (uint32_t)std::min<uint64_t>((b.m + FP_THREADS - 1) / FP_THREADS + 1, 2048);
     // workgroups of the grid-stride round kernels (2048)
@@ -4125,7 +4203,7 @@ hipError_t launch_rr_passes(const ClauseView& cv, const LoopBuffers& b, uint32_t
         k_fp_vmin<<<b.n_bkt * FP_VS + (cv.n_hot ? FP_HEAVY_GRID : 16u), FP_THREADS, 0, s>>>(b);
         if (g.narrow) k_fp_join0<4><<<g.gr, FP_THREADS, 0, s>>>(cv, b);
         else k_fp_join0<0><<<g.gr, FP_THREADS, 0, s>>>(cv, b);
-        for (uint32_t r = 1; r < FP_G; ++r) {
+        for (uint32_t r = 1; r < g.rounds; ++r) {
             if (g.narrow) {
                 k_fp_wclaim<4><<<g.gw, FP_THREADS, 0, s>>>(cv, b, r);
                 k_fp_wjoin<4><<<g.gw, FP_THREADS, 0, s>>>(cv, b, r);
@@ -4134,8 +4212,8 @@ hipError_t launch_rr_passes(const ClauseView& cv, const LoopBuffers& b, uint32_t
                 k_fp_wjoin<0><<<g.gw, FP_THREADS, 0, s>>>(cv, b, r);
             }
         }
-        if (g.narrow) k_fp_tail<4><<<1, 1024, 0, s>>>(cv, b);
-        else k_fp_tail<0><<<1, 1024, 0, s>>>(cv, b);
+        if (g.narrow) k_fp_tail<4><<<1, 1024, 0, s>>>(cv, b, g.rounds);
+        else k_fp_tail<0><<<1, 1024, 0, s>>>(cv, b, g.rounds);
         fp_turns(cv, b, g, 1, s);
     }
     return hipGetLastError();

@@ -559,8 +559,13 @@ int launch_rr_iteration(alll_ctx* c, hipEvent_t* marks) {
         ++done;
     }
     // next iteration: the passes this one needed (fp_iter = passes that changed the picks)
-    // (one or two passes fewer, with more host-driven passes after them: within noise)
-    if (c->h_fp[0] == FP_FINAL || c->h_fp[0] == FP_DONE) c->rr_p = std::max<uint32_t>(1, std::min(cap, c->h_fp[2] + 1));
+#ifndef ALLL_RR_P_LESS
+#define ALLL_RR_P_LESS 0
+#endif
+    if (c->h_fp[0] == FP_FINAL || c->h_fp[0] == FP_DONE) {
+        const uint32_t need = c->h_fp[2] + 1;
+        c->rr_p = std::max<uint32_t>(1, std::min(cap, need > ALLL_RR_P_LESS ? need - ALLL_RR_P_LESS : 1));
+    }
     return launch_rr_piece(c, marks, 2, 0);
 }
 
@@ -950,7 +955,7 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
             if ((rc = dalloc(c, &b.fp_v4, (rr_width >= 1 && rr_width <= 4) ? m + 1 : 1))) return bail(rc);
             if ((rc = dalloc(c, &b.fp_sole, (size_t)m * ((rr_width >= 1 && rr_width <= 4) ? 4 : 8) + 16))) return bail(rc);
             if ((rc = dalloc(c, &b.fp_list, 2 * (size_t)m + 2))) return bail(rc);
-            if ((rc = dalloc(c, &b.fp_tcnt, 2 * FP_G * ((size_t)m / 256 + 2)))) return bail(rc);  // (round tiles of 256)
+            if ((rc = dalloc(c, &b.fp_tcnt, 2 * FP_G_MAX * ((size_t)m / 256 + 2)))) return bail(rc);  // (round tiles of 256)
             if ((rc = dalloc(c, &b.fp_owner, (size_t)prob->n_vars + 1, 0xFF))) return bail(rc);
             if ((rc = dalloc(c, &b.fp_cov, (size_t)prob->n_vars + 16))) return bail(rc);
             if ((rc = dalloc(c, &b.fp_own0, (size_t)prob->n_vars + 1))) return bail(rc);
@@ -966,6 +971,7 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
             if ((rc = dalloc(c, &b.fp_erase, rr_T))) return bail(rc);
             b.fp_ib = ib;
             b.fp_tb = tb;
+            b.fp_hot = 0;  // (set with the hot-variable flags below)
             b.fp_max = FP_MAX_DEFAULT;
             if (const char* e = getenv("ALLL_RR_FP_MAX"))  // tests: iterations left to k_rr_mw mid-run
                 b.fp_max = (uint32_t)std::max(1, std::min(250, atoi(e)));
@@ -1159,6 +1165,10 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
             for (auto& l : flagged)
                 if (is_hot[l >> 1]) l |= 0x80000000u;
             cv.n_hot = n_hot;
+            if (b.fp_ctl) {
+                b.fp_hot = 1;
+                if ((rc = dalloc(c, &b.fp_hv, (size_t)prob->n_vars + 16))) return bail(rc);
+            }
             // skewed instances need more rounds before the leftovers are few enough for
             // the single-workgroup tail (power-law 3-SAT at 10M clauses: 10 rounds)
             if (!opt.grid_rounds) c->grid_rounds = SKEWED_GRID_ROUNDS;

@@ -559,13 +559,9 @@ int launch_rr_iteration(alll_ctx* c, hipEvent_t* marks) {
         ++done;
     }
     // next iteration: the passes this one needed (fp_iter = passes that changed the picks)
-#ifndef ALLL_RR_P_LESS
-#define ALLL_RR_P_LESS 0
-#endif
-    if (c->h_fp[0] == FP_FINAL || c->h_fp[0] == FP_DONE) {
-        const uint32_t need = c->h_fp[2] + 1;
-        c->rr_p = std::max<uint32_t>(1, std::min(cap, need > ALLL_RR_P_LESS ? need - ALLL_RR_P_LESS : 1));
-    }
+    // (two or four passes fewer, with more host-driven passes after them: within noise at M
+    // and C5)
+    if (c->h_fp[0] == FP_FINAL || c->h_fp[0] == FP_DONE) c->rr_p = std::max<uint32_t>(1, std::min(cap, c->h_fp[2] + 1));
     return launch_rr_piece(c, marks, 2, 0);
 }
 

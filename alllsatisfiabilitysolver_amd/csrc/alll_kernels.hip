@@ -2915,6 +2915,27 @@ __device__ __forceinline__ void fp_append(bool keep, uint32_t i, uint32_t* cnt, 
 }
 
 // Iteration start: entry count, set bounds, pass state.  Runs after the reduce.
+// Owner keys and cover serials carry over from iteration to iteration (keys of later epochs
+// are smaller, serials grow), so neither array needs clearing at every iteration: both
+// kernels below decide from the same control words whether this iteration starts over.
+__device__ __forceinline__ bool fp_ep_restart(const LoopBuffers& b, const RRFpCtl* ctl) {
+    return ctl->ep_next >= fp_ep_budget(b) / 2;  // (every iteration gets at least half the epochs)
+}
+__device__ __forceinline__ bool fp_serial_restart(const LoopBuffers& b, const RRFpCtl* ctl) {
+    return ctl->serial + b.fp_max + 2u > 255u;  // (8-bit cover serials, at most fp_max passes)
+}
+// Iteration start, before k_fp_begin: clears the owner keys / cover serials when they restart.
+__global__ __launch_bounds__(256) void k_fp_reset(LoopBuffers b) {
+    const RRFpCtl* ctl = b.fp_ctl;
+    if (!b.state->active) return;
+    const bool ep = fp_ep_restart(b, ctl), ser = fp_serial_restart(b, ctl);
+    if (!ep && !ser) return;
+    for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < b.n_vars; v += gridDim.x * blockDim.x) {
+        if (ep) b.fp_owner[v] = ~0ull;
+        if (ser) b.fp_cov[v] = 0;
+    }
+}
+
 __global__ __launch_bounds__(256) void k_fp_begin(LoopBuffers b) {
     RRFpCtl* ctl = b.fp_ctl;
     const DevState* st = b.state;
@@ -2935,14 +2956,16 @@ __global__ __launch_bounds__(256) void k_fp_begin(LoopBuffers b) {
         b.fp_sf[s] = s == T ? nu : lo;
     }
     if (threadIdx.x < 16) ctl->cntJ[threadIdx.x] = 0;
+    const bool ep0 = fp_ep_restart(b, ctl), ser0 = fp_serial_restart(b, ctl);  // (as k_fp_reset)
+    __syncthreads();  // (every thread has read the control words)
     if (threadIdx.x == 0) {
         ctl->state = FP_RUN;
         ctl->nu = nu;
         ctl->fp_iter = 0;
         ctl->changes = 0;
-        ctl->ep_base = 0;
-        ctl->ep_next = 0;
-        ctl->serial = 0;  // (fp_cov was cleared for this iteration)
+        ctl->ep_base = ep0 ? 0u : ctl->ep_next;
+        ctl->ep_next = ctl->ep_base;
+        if (ser0) ctl->serial = 0;
         ctl->tpre = 0;
         ctl->e0 = ~0u;
         ctl->nheavy = 0;
@@ -3922,6 +3945,10 @@ hipError_t launch_init_assignment(const LoopBuffers& b, hipStream_t s) {
     return hipGetLastError();
 }
 
+__global__ __launch_bounds__(256) void k_clear_u64(uint64_t* p, size_t n) {
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] = 0ull;
+}
+
 __global__ void k_set_limits(DevState* st, uint64_t n) {
     if (threadIdx.x != 0) return;
     st->limit_eval = st->n_iter + n;
@@ -4064,7 +4091,13 @@ hipError_t launch_collect(const ClauseView& cv, const LoopBuffers& b, uint32_t o
 
 hipError_t launch_cmark(const ClauseView& cv, const LoopBuffers& b, size_t words_per_rank, int rank, hipStream_t s) {
     if (!b.cmask) return hipErrorInvalidValue;
-    hipError_t e = hipMemsetAsync(b.cmask + words_per_rank * (size_t)rank, 0, words_per_rank * 8, s);
+    // (a kernel, not a memset node: graphs with memset nodes replayed under the HIP runtime
+    // torch bundles were seen to skip the memset)
+    if (words_per_rank) {
+        uint64_t* w = reinterpret_cast<uint64_t*>(b.cmask) + words_per_rank * (size_t)rank;
+        k_clear_u64<<<(uint32_t)std::min<size_t>((words_per_rank + 255) / 256, 2048), 256, 0, s>>>(w, words_per_rank);
+    }
+    hipError_t e = hipGetLastError();
     if (e != hipSuccess || b.own_end <= b.own_begin) return e;
     const uint32_t g = (b.own_end - b.own_begin + 3) / 4;
     ALLL_DISPATCH_K(cv.k, (k_cmark<K><<<g, 256, 0, s>>>(cv, b)));
@@ -4180,9 +4213,7 @@ hipError_t launch_rr_prep(const ClauseView& cv, const LoopBuffers& b, hipStream_
     const FpGrids g = fp_grids(b);
     const size_t lds_bs = 8ull * b.n_bkt + 2ull * FP_BS_ENT * 8;
     const size_t lds_bb = fp_bbuild_lds_bytes(b.bkt_width);
-    hipError_t e = hipMemsetAsync(b.fp_owner, 0xFF, (size_t)b.n_vars * 8, s);
-    if (e == hipSuccess) e = hipMemsetAsync(b.fp_cov, 0, (size_t)b.n_vars, s);
-    if (e != hipSuccess) return e;
+    k_fp_reset<<<(uint32_t)std::min<uint64_t>(((uint64_t)b.n_vars + 1023) / 1024 + 1, 2048), 256, 0, s>>>(b);
     k_fp_begin<<<1, 256, 0, s>>>(b);
     const uint32_t gbs = (uint32_t)std::min<uint64_t>((b.m + FP_BS_ENT - 1) / FP_BS_ENT + 1, 512);
     if (g.narrow) k_fp_bscatter<4><<<gbs, FP_THREADS, lds_bs, s>>>(cv, b);

@@ -76,8 +76,7 @@ struct RRFpCtl {
     uint32_t tpre;       // entries whose turn is below this keep the last pass's decision
     uint32_t e0;         // first erasure step of the last schedule
     uint32_t nheavy;     // variables with more than FP_HEAVY claimants (fp_heavy)
-    uint32_t ticket;     // workgroups of k_fp_sturn done (the last one advances the pass; reset by it)
-    uint32_t pad[1];
+    uint32_t pad[2];
     uint32_t cntJ[16];   // survivors of the last grid JOIN (k_fp_tail's list; the rounds count per tile)
 };
 // In-loop kernel timing (ALLL_FLAG_KERNEL_TIMING): per iteration i, slot i % TIME_SLOTS holds

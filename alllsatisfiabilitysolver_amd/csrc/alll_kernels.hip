@@ -3948,147 +3948,6 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_turn(ClauseView cv, LoopBuffe
     }
 }
 
-// The schedule and the turns in one kernel (T <= FP_FUSED_T sets, entries <= FP_FUSED_BLK
-// blocks): every workgroup computes the pass's block offsets, set starts and schedule into its
-// own LDS (k_fp_sched's work, redundantly: one launch and two dependent round trips fewer per
-// pass), then turns (or the MIS, when the pass converged) for its blocks; the last workgroup to
-// finish -- every other one has read the control words -- advances the pass state.
-constexpr uint32_t FP_FUSED_T = 32;
-constexpr uint32_t FP_FUSED_BLK = 8192;
-template <uint32_t KW>
-__global__ __launch_bounds__(FP_THREADS) void k_fp_sturn(ClauseView cv, LoopBuffers b, int test) {
-    RRFpCtl* ctl = b.fp_ctl;
-    if (ctl->state != FP_RUN) return;
-    DevState* st = b.state;
-    __shared__ uint32_t s_w[16], s_e0, s_steps, s_last;
-    __shared__ uint32_t s_sf[FP_FUSED_T + 1], s_pf[FP_FUSED_T + 1], s_n[FP_FUSED_T], s_nseg[FP_FUSED_T],
-        s_er[FP_FUSED_T];
-    __shared__ uint4 s_seg[FP_FUSED_T * FP_FUSED_T];
-    __shared__ uint32_t s_off[FP_FUSED_BLK];
-    const uint32_t nu = ctl->nu, T = b.rr_T, nblk = (nu + FP_B - 1) / FP_B;
-    const uint32_t ep_next = ctl->ep_next, serial = ctl->serial, e0_prev = ctl->e0, fp_iter = ctl->fp_iter;
-    const uint32_t stamp = st->stamp;
-    // change counts and earliest changes of the last pass (per k_fp_count workgroup), set
-    // starts and their in-block pick counts: one round trip
-    uint32_t ch = 0, tmin = ~0u;
-    if (test)
-        for (uint32_t k = threadIdx.x; k < min(nblk, FP_COUNT_GRID); k += blockDim.x) {
-            ch += b.fp_blk[2 * (b.m / FP_B + 2) + k];
-            tmin = min(tmin, b.fp_blk[2 * (b.m / FP_B + 2) + FP_COUNT_GRID + k]);
-        }
-    uint32_t sf = 0, bnd = 0;
-    if (threadIdx.x <= T) {
-        sf = b.fp_sf[threadIdx.x];
-        bnd = b.fp_bnd[threadIdx.x];
-        s_sf[threadIdx.x] = sf;
-    }
-    ch = __syncthreads_or(ch != 0);
-    for (int o = 32; o > 0; o >>= 1) tmin = min(tmin, (uint32_t)__shfl_down(tmin, o, 64));
-    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = tmin;
-    __syncthreads();
-    tmin = s_w[0];
-    for (uint32_t w = 1; w < (blockDim.x >> 6); ++w) tmin = min(tmin, s_w[w]);
-    __syncthreads();
-    const bool conv = test && ch == 0;
-    // block offsets (exclusive scan of the block pick counts, a contiguous range per thread)
-    const uint32_t per = (nblk + blockDim.x - 1) / blockDim.x;
-    const uint32_t kb = min(nblk, threadIdx.x * per), ke = min(nblk, kb + per);
-    uint32_t rsum = 0;
-    for (uint32_t k = kb; k < ke; ++k) rsum += b.fp_blk[k];
-    uint32_t total;
-    uint32_t ex = fp_block_scan(rsum, s_w, total);
-    for (uint32_t k = kb; k < ke; ++k) {
-        const uint32_t x = b.fp_blk[k];
-        s_off[k] = ex;
-        ex += x;
-    }
-    __syncthreads();
-    if (threadIdx.x <= T) s_pf[threadIdx.x] = sf >= nu ? total : s_off[sf / FP_B] + bnd;
-    __syncthreads();
-    if (threadIdx.x < T) {
-        s_n[threadIdx.x] = s_pf[threadIdx.x + 1] - s_pf[threadIdx.x];
-        s_nseg[threadIdx.x] = 0;
-    }
-    __syncthreads();
-    // the schedule (wave 0, lane s = set s; as k_fp_sched)
-    if (threadIdx.x < 64) {
-        const uint32_t lane = threadIdx.x;
-        const uint32_t n = s_n[lane < T ? lane : 0];
-        const bool k32 = ((unsigned long long)nu + 1) * T * 64 + 64 < (1ull << 32);
-        uint32_t done = 0, nseg = 0, t = 0, step = 0;
-        unsigned long long alive = (1ull << T) - 1ull;
-        for (uint32_t p = 0; p < T; ++p) {
-            const uint32_t L = (uint32_t)__popcll(alive);
-            const bool live = (alive >> lane) & 1ull;
-            const uint32_t x = (uint32_t)__popcll(alive & ((1ull << lane) - 1ull));
-            uint32_t o = x + L - (t % L) - 1;
-            if (o >= L) o -= L;
-            unsigned long long best = live ? (((unsigned long long)(n - done) * L + o) << 6 | lane) : ~0ull;
-            if (k32) {
-                best = __reduce_min_sync(~0ull, (uint32_t)best);
-            } else {
-                for (int q = 32; q > 0; q >>= 1) {
-                    const unsigned long long y = __shfl_xor(best, q, 64);
-                    best = y < best ? y : best;
-                }
-            }
-            const uint32_t ls = (uint32_t)(best & 63u);
-            const unsigned long long d = best >> 6;
-            const uint32_t rs = (d >> 32) ? (uint32_t)(d / L) : (uint32_t)d / L;
-            const uint32_t os = (uint32_t)(d - (unsigned long long)rs * L);
-            if (live) {
-                const uint32_t cnt = lane == ls ? n - done : rs + (o < os ? 1u : 0u);
-                s_seg[lane * T + nseg] = make_uint4(done, step, L, o);
-                nseg += 1;
-                done += cnt;
-            }
-            const uint32_t E = step + (uint32_t)d;
-            if (lane == 0) {
-                s_er[p] = E;
-                if (p == 0) s_e0 = E;
-            }
-            t = (uint32_t)__popcll(alive & ((1ull << ls) - 1ull));
-            alive &= ~(1ull << ls);
-            step = E + 1;
-        }
-        if (lane < T) s_nseg[lane] = nseg;
-        if (lane == 0) s_steps = step;
-    }
-    __syncthreads();
-    fp_turn_blocks<KW>(cv, b, conv, nu, T, stamp, s_sf, s_pf, s_nseg, s_er, s_seg, s_w,
-                       [&](uint32_t blk) { return s_off[blk]; });
-    // the pass state, by the last workgroup to get here
-    if (threadIdx.x == 0) {
-        __threadfence();
-        s_last = atomicAdd(&ctl->ticket, 1u) == gridDim.x - 1 ? 1u : 0u;
-    }
-    __syncthreads();
-    if (s_last && threadIdx.x == 0) {
-        __threadfence();
-        ctl->ticket = 0;
-        ctl->total = total;
-        ctl->changes = 0;
-        ctl->n_steps = s_steps;
-        // the next pass keeps the decisions below min(earliest changed turn, both schedules'
-        // first erasure): there the turns did not change, so neither did the sub-problem
-        ctl->tpre = test ? min(tmin, min(s_e0, e0_prev)) : 0u;
-        ctl->e0 = s_e0;
-        if (conv) {
-            ctl->state = FP_DONE;
-            ctl->guess_num = total;
-            ctl->guess_den = nu ? nu : 1u;
-            st->tmis_cnt = total;
-            st->tail_rounds = fp_iter;
-            if (fp_iter > st->max_rounds) st->max_rounds = fp_iter;
-            if (b.ktime) time_slot(b, st->n_iter - 1)[3] = wall_now();
-        } else {
-            if (test) ctl->fp_iter = fp_iter + 1;
-            ctl->ep_base = ep_next;
-            ctl->serial = serial + 1u;  // 8-bit cover serials
-            if (ep_next + FP_G_MAX + 1u >= fp_ep_budget(b) || serial + 1u > 255u) ctl->state = FP_FAIL;
-        }
-    }
-}
 
 // ------------------------------------------------------------------------------------
 // Launchers.
@@ -4341,14 +4200,9 @@ static FpGrids fp_grids(const LoopBuffers& b) {
 
 static void fp_turns(const ClauseView& cv, const LoopBuffers& b, const FpGrids& g, int test, hipStream_t s) {
     k_fp_count<<<g.gb, FP_THREADS, 0, s>>>(b, test);
-#ifndef ALLL_FP_FUSED
-#define ALLL_FP_FUSED 1
-#endif
-    if (ALLL_FP_FUSED && b.rr_T <= FP_FUSED_T && (b.m + FP_B - 1) / FP_B <= FP_FUSED_BLK) {  // (every possible entry count)
-        if (g.narrow) k_fp_sturn<4><<<g.gb, FP_THREADS, 0, s>>>(cv, b, test);
-        else k_fp_sturn<0><<<g.gb, FP_THREADS, 0, s>>>(cv, b, test);
-        return;
-    }
+    // (the schedule computed redundantly by every workgroup of the turn kernel, the last one to
+    // finish advancing the pass: 615 -> 527 it/s at M, T = 16; 50 KB of LDS per workgroup and
+    // the schedule's latency in every one of them cost more than the launch saved)
     k_fp_sched<<<1, 256, 0, s>>>(b, test);
     if (g.narrow) k_fp_turn<4><<<g.gb, FP_THREADS, 0, s>>>(cv, b);
     else k_fp_turn<0><<<g.gb, FP_THREADS, 0, s>>>(cv, b);

@@ -77,7 +77,7 @@ struct RRFpCtl {
     uint32_t e0;         // first erasure step of the last schedule
     uint32_t nheavy;     // variables with more than FP_HEAVY claimants (fp_heavy)
     uint32_t pad[2];
-    uint32_t cntJ[16];   // survivors of the last grid JOIN (k_fp_tail's list; the rounds count per tile)
+    uint32_t spare[16];
 };
 // In-loop kernel timing (ALLL_FLAG_KERNEL_TIMING): per iteration i, slot i % TIME_SLOTS holds
 // device wall-clock stamps (s_memrealtime) {eval start (min over workgroups), eval end (max),

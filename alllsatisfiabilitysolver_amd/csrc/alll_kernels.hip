@@ -2955,7 +2955,6 @@ __global__ __launch_bounds__(256) void k_fp_begin(LoopBuffers b) {
         }
         b.fp_sf[s] = s == T ? nu : lo;
     }
-    if (threadIdx.x < 16) ctl->cntJ[threadIdx.x] = 0;
     const bool ep0 = fp_ep_restart(b, ctl), ser0 = fp_serial_restart(b, ctl);  // (as k_fp_reset)
     __syncthreads();  // (every thread has read the control words)
     if (threadIdx.x == 0) {
@@ -2997,7 +2996,7 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_guess(LoopBuffers b) {
 //     atomic per bucket, and the pairs are stored there;
 //   k_fp_bbuild (workgroup per bucket): LDS counters per variable place each claimant in its
 //     variable's static list region (fp_soff: the variable's literal occurrences); then per
-//     variable: the single-claimant bit (fp_one), the single claimant as its round-0 owner
+//     variable: the single claimant as its round-0 owner and its sole byte
 //     (fp_own0, for the whole iteration), the shared variables' list {start, count, variable}
 //     (fp_sv, per bucket) and the segments of long lists (fp_heavy).
 // Each pass's round-0 owner of a shared variable is then the minimum key over its list
@@ -3801,7 +3800,6 @@ __global__ __launch_bounds__(256) void k_fp_sched(LoopBuffers b, int test) {
     }
     __syncthreads();
     for (uint32_t s = threadIdx.x; s < T; s += blockDim.x) b.fp_nseg[s] = s_nseg[s];
-    if (threadIdx.x < 16) ctl->cntJ[threadIdx.x] = 0;
     if (threadIdx.x == 0) {
         ctl->total = total;
         ctl->changes = 0;

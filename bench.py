@@ -180,9 +180,10 @@ def trajectory_check(cfg, T, st, words):
     return out
 
 
-def rr_line(args, n, m, k, kind, Solver, generate_ksat, device, warmup=2, steps=10):
+def rr_line(args, n, m, k, kind, Solver, generate_ksat, device, warmup=20, steps=10):
     """GPU resample loop with the reference's n_threads = T round-robin MIS, T = the CPU
-    baseline's thread count."""
+    baseline's thread count: iterations 21-30 (past the first iterations' larger violated sets,
+    as the T = 1 line skips its first five), checked against the committed oracle trajectory."""
     T = cpu_threads()[0]
     if isinstance(k, tuple):
         from alllsatisfiabilitysolver_amd import generate_mixed

@@ -2193,11 +2193,18 @@ __global__ __launch_bounds__(256) void k_rr_mark(ClauseView cv, LoopBuffers b) {
     if (tile >= b.n_tiles) return;
     const uint32_t cnt = b.tile_cnt[tile];
     const uint32_t* lin = b.stage[0] + (uint64_t)tile * TILE * S;
-    for (uint32_t i = lane; i < cnt; i += 64) {
-        Ent<K> e;
-        load_ent<K>(e, lin + (uint64_t)i * S);
-        ent_unpack<K>(cv, e);
-        b.rr_flag[e.w[0]] = 1u;
+    constexpr uint32_t U = 4;  // entries in flight per lane
+    for (uint32_t i0 = lane; i0 < cnt; i0 += 64 * U) {
+        Ent<K> e[U];
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u)
+            if (i0 + 64 * u < cnt) load_ent<K>(e[u], lin + (uint64_t)(i0 + 64 * u) * S);
+#pragma unroll
+        for (uint32_t u = 0; u < U; ++u) {
+            if (i0 + 64 * u >= cnt) break;
+            ent_unpack<K>(cv, e[u]);
+            b.rr_flag[e[u].w[0]] = 1u;
+        }
     }
 }
 
@@ -2227,7 +2234,11 @@ __global__ __launch_bounds__(256) void k_rr_entries(ClauseView cv, LoopBuffers b
     // evaluation's own tile counts
     const uint32_t* tcnt = b.rr_flag ? b.rr_tcnt : b.tile_cnt;
     uint32_t acc = 0;
-    for (uint32_t t = tid; t < tile; t += 256) acc += tcnt[t];
+    {  // (four independent loads in flight per step, not one load-wait-add per tile)
+        uint32_t t = tid;
+        for (; t + 768 < tile; t += 1024) acc += tcnt[t] + tcnt[t + 256] + tcnt[t + 512] + tcnt[t + 768];
+        for (; t < tile; t += 256) acc += tcnt[t];
+    }
     for (int o = 32; o > 0; o >>= 1) acc += __shfl_down(acc, o, 64);
     if ((tid & 63) == 0) s_part[tid >> 6] = acc;
     if (b.rr_flag) {
@@ -2278,6 +2289,18 @@ __global__ __launch_bounds__(256) void k_rr_entries(ClauseView cv, LoopBuffers b
     const uint32_t base = s_part[0] + s_part[1] + s_part[2] + s_part[3];
     const uint32_t n = s_wpre[TILE_WORDS];
     RREnt* out = reinterpret_cast<RREnt*>(b.rr_u) + base;
+    if (b.fp_ctl)  // the fixpoint's set starts in the entries: those that fall in this tile
+        for (uint32_t s = tid; s < b.rr_T; s += 256) {
+            const uint32_t key = b.rr_sets[s];
+            if (key / TILE != tile || key >= cv.m) continue;
+            uint32_t lo = 0, hi = n;  // this tile's violated clauses below the set start
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (s_ids[mid] < key) lo = mid + 1;
+                else hi = mid;
+            }
+            b.fp_sf[s] = base + lo;
+        }
     for (uint32_t i = tid; i < n; i += 256) {
         const uint32_t c = s_ids[i], lb = cl_start(cv, c), w = cl_width(cv, c);
         uint32_t v[8], hm = 0;  // hm: slots whose variable is hot (the fixpoint's degree count)
@@ -2944,17 +2967,10 @@ __global__ __launch_bounds__(256) void k_fp_begin(LoopBuffers b) {
         return;
     }
     const uint32_t nu = (uint32_t)st->u_total, T = b.rr_T;
-    const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
-    for (uint32_t s = threadIdx.x; s <= T; s += blockDim.x) {  // first entry with id >= set start
-        const uint32_t key = b.rr_sets[s];
-        uint32_t lo = 0, hi = nu;
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (U[mid].a.x < key) lo = mid + 1;
-            else hi = mid;
-        }
-        b.fp_sf[s] = s == T ? nu : lo;
-    }
+    // set starts (first entry with id >= the set's first clause): k_rr_entries wrote those that
+    // fall in a tile; the end and the starts past the last clause are nu
+    for (uint32_t s = threadIdx.x; s <= T; s += blockDim.x)
+        if (s == T || b.rr_sets[s] >= b.m) b.fp_sf[s] = nu;
     const bool ep0 = fp_ep_restart(b, ctl), ser0 = fp_serial_restart(b, ctl);  // (as k_fp_reset)
     __syncthreads();  // (every thread has read the control words)
     if (threadIdx.x == 0) {

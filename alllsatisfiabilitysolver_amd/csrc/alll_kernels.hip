@@ -2821,6 +2821,7 @@ constexpr uint32_t FP_RT = 256;        // entries per round tile (one per thread
 constexpr uint32_t FP_LDS_SEG_T = 32;     // k_fp_turn keeps the schedule in LDS up to this many sets
 constexpr uint32_t FP_COUNT_GRID = 1024;
 constexpr uint32_t FP_HEAVY = 64;         // claimant lists longer than this are reduced by waves
+
 constexpr uint32_t FP_SEG = 2048;         // claimants per wave of k_fp_vmin's long-list workgroups
 constexpr uint32_t FP_HEAVY_GRID = 512;
 // workgroups of the wave-per-tile rounds (512 / 1024 / 2048: 607 / 627 / 628 iterations/s at
@@ -3192,6 +3193,8 @@ __global__ __launch_bounds__(FP_BB_THREADS) void k_fp_bbuild(LoopBuffers b) {
         } else if (shared) {
             sv[base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = make_uint4(s_off[w], c, v, 0u);
             if (c > FP_HEAVY) {  // long lists (hubs of skewed instances): a wave per FP_SEG claimants
+                // (hot instances: their round claims go through LDS; from 16 or 32 claimants on
+                // instead of 64: 173 vs 177 it/s at C5, T = 16)
                 if (b.fp_hv) b.fp_hv[v] = (uint8_t)b.state->stamp;
                 const uint32_t ns = (c + FP_SEG - 1) / FP_SEG;
                 const uint32_t h0 = atomicAdd(&ctl->nheavy, ns);

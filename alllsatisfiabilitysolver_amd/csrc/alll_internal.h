@@ -147,6 +147,8 @@ struct LoopBuffers {
                             // width, ragged): the violated bitmask in clause order, bit c % 64 of
                             // word c / 64 (k_cmark sets the own shard's bits; the all-gathered
                             // mask gives the other shards' lists, k_collect); nullptr = vmask
+    uint8_t* cflag;         // clause-sharded exchange: a byte per clause of this rank's mask words
+                            //   (k_cmark marks, k_cpack packs into cmask and clears)
     uint32_t* xcount;       // clause-sharded verify: the own shard's violated count (u32), summed
     uint32_t own_begin, own_end;  // this rank's tiles
     uint32_t* tile_cnt;     // undecided violated entries per tile

@@ -1351,6 +1351,7 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     if ((c->world > 1 || !zero_id) && (cv.k > 0 || cv.rg_off)) {
         // the exchange's clause-order mask (this rank laid out its own shard only)
         if ((rc = dalloc(c, &b.cmask, (size_t)c->n_tiles_padded * TILE_WORDS))) return bail(rc);
+        if ((rc = dalloc(c, &b.cflag, (size_t)c->tiles_per_rank * TILE + 64))) return bail(rc);
     }
     if (c->world > 1 && (rc = dalloc(c, &b.xcount, 4))) return bail(rc);
     if (c->world > 1 || !zero_id) {

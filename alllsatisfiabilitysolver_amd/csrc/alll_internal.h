@@ -17,7 +17,7 @@ constexpr int JOIN_THREADS = 128;  // k_join: ~230 entries per tile in round 1, 
 constexpr int TAIL_THREADS = 1024;
 // grid rounds from here on run a wave per tile (instances with hot variables: one round later,
 // their round 2 still holds ~10% of the violated clauses)
-constexpr uint32_t WAVE_ROUND_MIN = 2, WAVE_ROUND_MIN_HOT = 3;
+constexpr uint32_t WAVE_ROUND_MIN = 1;  // grid rounds >= 1 run a wave per tile
 constexpr int MAX_FIXED_K = 8;
 // Persistent hybrid evaluation: LDS window of at most LDS_VARS variables' assignment words.
 constexpr uint32_t LDS_WORDS = 38912;              // 152 KiB of LDS
@@ -273,8 +273,7 @@ hipError_t launch_collect(const ClauseView& cv, const LoopBuffers& b, uint32_t o
 // clause-sharded: the own shard's violated clauses into cmask (own words cleared first)
 hipError_t launch_cmark(const ClauseView& cv, const LoopBuffers& b, size_t words_per_rank, int rank, hipStream_t s);
 hipError_t launch_reduce(const LoopBuffers& b, int mode, hipStream_t s);
-hipError_t launch_round(const ClauseView& cv, const LoopBuffers& b, uint32_t r, bool last,
-                        uint32_t wave_from, hipStream_t s);
+hipError_t launch_round(const ClauseView& cv, const LoopBuffers& b, uint32_t r, bool last, hipStream_t s);
 hipError_t launch_round0_buckets(const ClauseView& cv, const LoopBuffers& b, bool last, bool fused_reduce,
                                  bool scattered, hipStream_t s);
 hipError_t launch_tail(const ClauseView& cv, const LoopBuffers& b, uint32_t first_round,

@@ -8,7 +8,8 @@
 //              all-gathered bitmask.
 //   k_reduce   violated count + termination test (check_if_noUNSAT, SATInstance.h:326-338)
 //              and the loop state update.
-//   k_claim0, k_round x G, k_tail   round-synchronous exact lexicographically-first MIS of
+//   round 0 (k_bscatter / k_bresolve / k_bjoin, or k_claim / k_join), rounds 1 .. G-1
+//              (k_wclaim / k_wjoin), k_tail   round-synchronous exact lexicographically-first MIS of
 //              the violated clauses in clause order (populate_mis_parallel with one set,
 //              SATInstance.h:391-451; dependency = shared variable, :369-389).
 //   k_resample_vars  Philox4x32-10 resampling of every variable of every MIS clause
@@ -1059,11 +1060,10 @@ __device__ __forceinline__ void claim_all(const ClauseView& cv, const LoopBuffer
     }
 }
 
-// CLAIM(r).  r == 0: every violated clause claims, in place (evaluation positions become
-// clause ids here).  r > 0: kill test, claim, survivors compacted from `in` to `out`.
+// CLAIM(0) (the atomic round 0): every violated clause of a tile claims its variables, in place
+// (evaluation positions become clause ids here).  Rounds >= 1 run a wave per tile (k_wclaim).
 template <int K>
-__global__ __launch_bounds__(ROUND_THREADS) void k_claim(ClauseView cv, LoopBuffers b, uint32_t r,
-                                                         uint32_t* in, uint32_t* out) {
+__global__ __launch_bounds__(ROUND_THREADS) void k_claim(ClauseView cv, LoopBuffers b, uint32_t* in) {
     const DevState* st = b.state;
     const uint32_t tile = blockIdx.x;
     constexpr int S = Ent<K>::S;
@@ -1073,25 +1073,24 @@ __global__ __launch_bounds__(ROUND_THREADS) void k_claim(ClauseView cv, LoopBuff
     Ent<K> e0;
     load_ent<K>(e0, lin + (uint64_t)threadIdx.x * S);
     const uint32_t cnt = b.tile_cnt[tile];
-    const uint32_t active = st->active, stamp = st->stamp, rbase = st->round_base;
+    const uint32_t active = st->active, rbase = st->round_base;
     spec_fence();
     if (!active || cnt == 0) return;
     __shared__ uint32_t s_hk[HOT_SLOTS];
     __shared__ unsigned long long s_hv[HOT_SLOTS];
-    __shared__ uint32_t s_keep;
     HotTable ht{s_hk, s_hv};
     const bool hot = cv.n_hot != 0;
-    if (hot) ht.init();
-    if (threadIdx.x == 0) s_keep = 0;
-    __syncthreads();
-    const unsigned long long keyhi = (unsigned long long)(~(rbase + r)) << 32;
+    if (hot) {
+        ht.init();
+        __syncthreads();
+    }
+    const unsigned long long keyhi = (unsigned long long)(~rbase) << 32;
     unsigned long long* owner = b.owner;
-    uint32_t* lout = out + (uint64_t)tile * TILE * S;
     for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
         Ent<K> e;
         if (i == threadIdx.x) e = e0;
         else load_ent<K>(e, lin + (uint64_t)i * S);
-        if (r == 0 && (cv.id_bits || cv.perm)) {  // raw entry from the evaluation
+        if (cv.id_bits || cv.perm) {  // raw entry from the evaluation
             ent_unpack<K>(cv, e);
             store_ent<K>(lin + (uint64_t)i * S, e);
         }
@@ -1099,17 +1098,12 @@ __global__ __launch_bounds__(ROUND_THREADS) void k_claim(ClauseView cv, LoopBuff
         const uint32_t len = ent_len<K>(cv, e, lb);
         const uint32_t key = prio(b, st, e.w[0]);
         if (key == ~0u) continue;  // streaming: not yielded this iteration (dropped by JOIN(0))
-        if (r > 0) {
-            bool killed = false;
-            for (uint32_t j = 0; j < len; ++j) killed |= b.cover[lit_var(ent_lit<K>(cv, e, lb, j))] == stamp;
-            if (killed) continue;
-        }
         claim_all<K>(cv, b, e, lb, len, keyhi | key, owner, ht, hot);
-        if (r > 0) store_ent<K>(lout + (uint64_t)atomicAdd(&s_keep, 1u) * S, e);
     }
-    __syncthreads();
-    if (hot) ht.flush(owner, b);
-    if (r > 0 && threadIdx.x == 0) b.tile_cnt[tile] = s_keep;
+    if (hot) {
+        __syncthreads();
+        ht.flush(owner, b);
+    }
 }
 
 // Join one tile's undecided entries: own(e, i) says whether entry i holds every variable it
@@ -4161,15 +4155,14 @@ hipError_t launch_reduce(const LoopBuffers& b, int mode, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_round(const ClauseView& cv, const LoopBuffers& b, uint32_t r, bool last,
-                        uint32_t wave_from, hipStream_t s) {
+hipError_t launch_round(const ClauseView& cv, const LoopBuffers& b, uint32_t r, bool last, hipStream_t s) {
     // buffers: eval -> stage[0]; CLAIM(0) in place; JOIN(r) stage[0] -> stage[1];
     // CLAIM(r>0) stage[1] -> stage[0]
     if (b.n_tiles == 0) return hipSuccess;
     uint32_t* s0 = b.stage[0];
     uint32_t* s1 = b.stage[1];
     const int l = last ? 1 : 0;
-    if (r >= wave_from) {  // late rounds: a wave per tile
+    if (r >= WAVE_ROUND_MIN) {  // rounds >= 1: a wave per tile
         const uint32_t grid = (b.n_tiles + ROUND_THREADS / 64 - 1) / (ROUND_THREADS / 64);
         ALLL_DISPATCH_K(cv.k, (k_wclaim<K><<<grid, ROUND_THREADS, 0, s>>>(cv, b, r, s1, s0)));
         hipError_t e = hipGetLastError();
@@ -4177,7 +4170,7 @@ hipError_t launch_round(const ClauseView& cv, const LoopBuffers& b, uint32_t r, 
         ALLL_DISPATCH_K(cv.k, (k_wjoin<K><<<grid, ROUND_THREADS, 0, s>>>(cv, b, r, s0, s1, l)));
         return hipGetLastError();
     }
-    ALLL_DISPATCH_K(cv.k, (k_claim<K><<<b.n_tiles, ROUND_THREADS, 0, s>>>(cv, b, r, r == 0 ? s0 : s1, s0)));
+    ALLL_DISPATCH_K(cv.k, (k_claim<K><<<b.n_tiles, ROUND_THREADS, 0, s>>>(cv, b, s0)));
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     ALLL_DISPATCH_K(cv.k, (k_join<K><<<b.n_tiles, JOIN_THREADS, 0, s>>>(cv, b, r, s0, s1, l)));

@@ -80,7 +80,6 @@ struct alll_ctx {
     // includes the scatter, so its roofline is no longer the evaluation's: off by default)
     bool fuse_scatter = false;
     std::vector<uint32_t> run_t0;  // bucketed round 0: first tile of every run (+ end)
-    uint32_t wave_round_min = WAVE_ROUND_MIN;  // first grid round with a wave per tile
     int rank = 0, world = 1;
     bool allreduce = false;
     ncclComm_t comm = nullptr;
@@ -432,7 +431,7 @@ int enqueue_iteration(alll_ctx* c, hipEvent_t* marks, int variant) {
         for (uint32_t r = 0; r < rounds; ++r) {
             if (r == 0 && variant == 1)
                 HIP_TRY(launch_round0_buckets(c->cv, c->b, rounds == 1, fused, scatter, s));
-            else HIP_TRY(launch_round(c->cv, c->b, r, r + 1 == rounds, c->wave_round_min, s));
+            else HIP_TRY(launch_round(c->cv, c->b, r, r + 1 == rounds, s));
         }
         HIP_TRY(launch_tail(c->cv, c->b, rounds, s));
     }
@@ -1168,7 +1167,6 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
             // skewed instances need more rounds before the leftovers are few enough for
             // the single-workgroup tail (power-law 3-SAT at 10M clauses: 10 rounds)
             if (!opt.grid_rounds) c->grid_rounds = SKEWED_GRID_ROUNDS;
-            c->wave_round_min = WAVE_ROUND_MIN_HOT;
         }
         const uint32_t* src = flagged.empty() ? prob->literals : flagged.data();
         if (L && hipMemcpy(d_lits, src, L * 4, hipMemcpyHostToDevice) != hipSuccess)

@@ -60,7 +60,7 @@ constexpr uint32_t DEFAULT_GRID_ROUNDS = 4;
 constexpr int GRAPH_SIZES = 4;
 constexpr uint64_t SMALL_U_DEFAULT = 8192;
 constexpr uint32_t GRAPH_UNROLL = 1u << (GRAPH_SIZES - 1);
-constexpr uint32_t SKEWED_GRID_ROUNDS = 6;  // instances with hot variables
+constexpr uint32_t SKEWED_GRID_ROUNDS = 7;  // instances with hot variables
 
 }  // namespace
 

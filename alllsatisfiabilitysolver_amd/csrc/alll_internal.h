@@ -56,9 +56,9 @@ constexpr uint32_t RR_MW_CTL_WORDS = 1024; // k_rr_mw control block (words)
 // it.  The pick sets are iterated, LFMIS(turns(P)) -> P, until they repeat.
 constexpr uint32_t FP_TMAX = 256;          // sets (the schedule keeps T x T phase records)
 constexpr uint32_t FP_B = 2048;            // entries per block of the count / turn passes
-constexpr uint32_t FP_G = 4;               // grid LFMIS rounds before the one-workgroup tail (2, 3: slower)
-constexpr uint32_t FP_G_HOT = 8;           // ... on instances with hot variables (longer dependency chains)
-constexpr uint32_t FP_G_MAX = 8;
+constexpr uint32_t FP_G = 4;       // grid LFMIS rounds before the one-workgroup tail (2, 3, 5: slower)
+constexpr uint32_t FP_G_HOT = 6;   // ... on instances with hot variables (5, 7, 8, 10: slower)
+constexpr uint32_t FP_G_MAX = FP_G_HOT > FP_G ? FP_G_HOT : FP_G;
 constexpr uint32_t FP_MAX_DEFAULT = 64;    // LFMIS passes per iteration before k_rr_mw decides it
 enum : uint32_t { FP_RUN = 0, FP_FINAL = 1, FP_DONE = 2, FP_OFF = 3, FP_FAIL = 4 };
 struct RRFpCtl {

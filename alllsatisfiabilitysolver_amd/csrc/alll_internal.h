@@ -25,7 +25,7 @@ constexpr uint32_t LDS_VARS = LDS_WORDS * 32;      // 1,245,184 variables
 constexpr int HYB_THREADS = 1024;
 constexpr uint32_t HYB_MAX_TILES = 256;            // per-tile LDS counters per pass
 // Hot variables (skewed degree): at most HOT_MAX are flagged; LDS hash slots per claim block.
-constexpr uint32_t HOT_MAX = 512;
+constexpr uint32_t HOT_MAX = 512;  // (256, 128: same C5 throughput)
 constexpr uint32_t HOT_SLOTS = 1024;
 // hot: degree >= max(HOT_THR_MIN, HOT_MEAN_X x mean degree) (round 4 at C5: 1024 hot variables
 // from degree 16 x mean on, 2048 LDS slots: 3508 -> 3437 it/s)

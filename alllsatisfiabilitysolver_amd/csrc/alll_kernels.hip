@@ -2839,16 +2839,15 @@ constexpr uint32_t FP_PER = FP_B / FP_THREADS;  // entries per thread in the cou
 static_assert(FP_PER == 8, "a thread's pick bytes are one 8-byte load");
 constexpr uint32_t FP_RT = 256;        // entries per round tile (one per thread): many workgroups per CU
 constexpr uint32_t FP_LDS_SEG_T = 32;     // k_fp_turn keeps the schedule in LDS up to this many sets
-constexpr uint32_t FP_COUNT_GRID = 1024;
+constexpr uint32_t FP_COUNT_GRID = 1024;  // workgroups of k_fp_count / k_fp_turn (grid-stride over blocks)
 constexpr uint32_t FP_HEAVY = 64;         // claimant lists longer than this are reduced by waves
 
 constexpr uint32_t FP_SEG = 2048;         // claimants per wave of k_fp_vmin's long-list workgroups
-constexpr uint32_t FP_HEAVY_GRID = 512;
+constexpr uint32_t FP_HEAVY_GRID = 512;   // ... their number (instances with hot variables)
 // workgroups of the wave-per-tile rounds (512 / 1024 / 2048: 607 / 627 / 628 iterations/s at
 // M, T = 16; the workgroup-per-tile kernels for these rounds: 605)
 constexpr uint32_t FP_WGRID = 1024;
-   // ... their number (instances with hot variables)
-constexpr uint32_t FP_SCHED_LDS_BLK = 4096;  // k_fp_sched keeps the block offsets in LDS up to this many blocks  // workgroups of k_fp_count / k_fp_turn (grid-stride over blocks)
+constexpr uint32_t FP_SCHED_LDS_BLK = 4096;  // k_fp_sched keeps the block offsets in LDS up to this many blocks
 
 __device__ __forceinline__ unsigned long long fp_key(const LoopBuffers& b, uint32_t ep, uint32_t turn, uint32_t i) {
     const uint32_t sh = b.fp_tb + b.fp_ib;

@@ -67,8 +67,13 @@ struct RRFpCtl {
     uint32_t nu;         // violated clauses (scan entries) of the iteration
     uint32_t fp_iter;    // LFMIS passes so far in this iteration
     uint32_t changes;    // picks that differ between the last two passes
-    uint32_t serial;     // cover serial of the current LFMIS pass (fp_cov, 8-bit, cleared per iteration), never 0
-    uint32_t ep_base;    // owner epoch of round 0 of the current pass (owner reset per iteration)
+    uint32_t serial;     // cover serial of the current LFMIS pass (fp_cov, 8-bit), never 0; carries over
+                         // from iteration to iteration and restarts at 0 (k_fp_reset clears fp_cov)
+                         // only when fewer than fp_max + 2 serials are left (fp_serial_restart)
+    uint32_t ep_base;    // owner epoch of round 0 of the current pass; epochs carry over from iteration
+                         // to iteration (keys of later epochs are smaller, so fp_owner needs no reset)
+                         // and restart at 0 (k_fp_reset clears fp_owner) once half the epoch budget
+                         // is used (fp_ep_restart)
     uint32_t ep_next;    // first epoch after the current pass
     uint32_t total;      // picks of the last pass
     uint32_t guess_num, guess_den;  // previous iteration's |M| / |U| (initial pick density)
@@ -219,10 +224,11 @@ struct LoopBuffers {
     uint4* fp_v4;               // per scan entry of narrow instances: its variables (16-byte copy)
     uint32_t* fp_list;          // 2 x m: round lists per tile of FP_B entries (JOIN output, CLAIM output)
     uint32_t* fp_tcnt;          // 2 FP_G_MAX x tiles: list lengths per round and tile
-    unsigned long long* fp_owner; // n_vars claim keys {epoch | turn | entry}, reset every iteration
+    unsigned long long* fp_owner; // n_vars claim keys {epoch | turn | entry}, cleared only at an epoch restart
     uint32_t* fp_own0;          // n_vars: round-0 winner (entry) of every claimed variable (single
                                 // claimants: for the whole iteration, k_fp_bbuild; shared: per pass)
-    uint8_t* fp_cov;            // n_vars: serial of the pass whose pick covers the variable (cleared per iteration)
+    uint8_t* fp_cov;            // n_vars: serial of the pass whose pick covers the variable (cleared only at a
+                                //   serial restart)
     // per-iteration claimant lists (k_fp_bscatter / k_fp_bbuild): variable v's violated
     // claimants are fp_vlist[fp_soff[v] ..), fp_soff = prefix of the static literal counts
     const uint32_t* fp_soff;    // n_vars + 1
@@ -270,8 +276,10 @@ hipError_t launch_eval_ragged(const ClauseView& cv, const LoopBuffers& b, uint32
                               uint32_t tile_end, bool gated, int n_blocks, hipStream_t s);
 hipError_t launch_collect(const ClauseView& cv, const LoopBuffers& b, uint32_t own_begin,
                           uint32_t own_end, hipStream_t s);
-// clause-sharded: the own shard's violated clauses into cmask (own words cleared first)
-hipError_t launch_cmark(const ClauseView& cv, const LoopBuffers& b, size_t words_per_rank, int rank, hipStream_t s);
+// clause-sharded: the own shard's violated clauses into cmask (own words cleared first); gated: the
+// loop's (skipped once the loop state closes the evaluation), else a standalone pass (alll_verify)
+hipError_t launch_cmark(const ClauseView& cv, const LoopBuffers& b, size_t words_per_rank, int rank, bool gated,
+                        hipStream_t s);
 hipError_t launch_reduce(const LoopBuffers& b, int mode, hipStream_t s);
 hipError_t launch_round(const ClauseView& cv, const LoopBuffers& b, uint32_t r, bool last, hipStream_t s);
 hipError_t launch_round0_buckets(const ClauseView& cv, const LoopBuffers& b, bool last, bool fused_reduce,

@@ -357,10 +357,12 @@ __global__ __launch_bounds__(EVAL_THREADS) void k_eval_fixed(ClauseView cv, Loop
 // per literal slot from the chunk-transposed layout (as k_eval_fixed), so the literal stream
 // is read once, perfectly coalesced.  Violated clauses go to the per-tile lists through
 // per-tile LDS counters.
-template <int K>
-__global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, LoopBuffers b,
-                                                             uint32_t tile_begin, uint32_t tile_end,
-                                                             int gated, int scatter) {
+// SC: the evaluation workgroups also scatter LFMIS round 0's claims of their runs (one GPU,
+// bucketed round 0): k_eval_scatter<K>, a kernel of its own so that profiles and the roofline
+// keep the evaluation alone (k_eval_hybrid<K>) apart from the fused loop kernel.
+template <int K, bool SC>
+__device__ __forceinline__ void eval_hybrid_body(const ClauseView& cv, const LoopBuffers& b, uint32_t tile_begin,
+                                                 uint32_t tile_end, int gated) {
     if (gated && eval_gate_closed(b.state)) return;
     extern __shared__ __attribute__((aligned(16))) uint32_t s_A[];
     __shared__ uint32_t s_tcnt[HYB_MAX_TILES];
@@ -610,7 +612,7 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
         }
     }
     stamp_eval_end(b, gated);
-    if (scatter) {
+    if constexpr (SC) {
         // One GPU, bucketed LFMIS round 0: this workgroup's tiles form runs b.run_t0[r] ..
         // (rpw runs per workgroup), so the workgroup scatters their claims itself, from the
         // lists it has just written (L2-warm) and with the window's LDS, instead of a
@@ -623,6 +625,18 @@ __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, Loop
             __syncthreads();  // (the LDS is reused by the next run)
         }
     }
+}
+
+template <int K>
+__global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, LoopBuffers b, uint32_t tile_begin,
+                                                             uint32_t tile_end, int gated) {
+    eval_hybrid_body<K, false>(cv, b, tile_begin, tile_end, gated);
+}
+
+template <int K>
+__global__ __launch_bounds__(HYB_THREADS) void k_eval_scatter(ClauseView cv, LoopBuffers b, uint32_t tile_begin,
+                                                              uint32_t tile_end, int gated) {
+    eval_hybrid_body<K, true>(cv, b, tile_begin, tile_end, gated);
 }
 
 // Clause evaluation, ragged widths (ClauseView::rg_off): the persistent LDS-window structure
@@ -808,8 +822,8 @@ __global__ __launch_bounds__(EVAL_THREADS) void k_eval_csr(ClauseView cv, LoopBu
 // bits of the clause-order mask (a wave per own tile, from the evaluation's raw entries), which
 // is all-gathered instead of the evaluation-order bitmask.
 template <int K>
-__global__ __launch_bounds__(256) void k_cmark(ClauseView cv, LoopBuffers b, uint64_t base) {
-    if (eval_gate_closed(b.state)) return;
+__global__ __launch_bounds__(256) void k_cmark(ClauseView cv, LoopBuffers b, uint64_t base, int gated) {
+    if (gated && eval_gate_closed(b.state)) return;
     constexpr int S = Ent<K>::S;
     const uint32_t tile = b.own_begin + blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (tile >= b.own_end) return;
@@ -826,8 +840,8 @@ __global__ __launch_bounds__(256) void k_cmark(ClauseView cv, LoopBuffers b, uin
 
 // The rank's clause flags → its words of the clause-order mask (every word written, so no
 // clear), flags cleared once read; a thread per word of 64 clauses.
-__global__ __launch_bounds__(256) void k_cpack(LoopBuffers b, uint64_t* words, uint32_t n_words) {
-    if (eval_gate_closed(b.state)) return;
+__global__ __launch_bounds__(256) void k_cpack(LoopBuffers b, uint64_t* words, uint32_t n_words, int gated) {
+    if (gated && eval_gate_closed(b.state)) return;
     const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
     if (w >= n_words) return;
     uint4* f = reinterpret_cast<uint4*>(b.cflag + (uint64_t)w * 64);
@@ -4045,6 +4059,10 @@ hipError_t prepare_kernels(const ClauseView& cv, const LoopBuffers& b) {
                                                        hipFuncAttributeMaxDynamicSharedMemorySize,
                                                        (int)(LDS_WORDS * 4 + 16))));
         if (e != hipSuccess) return e;
+        ALLL_DISPATCH_K(cv.k, (e = hipFuncSetAttribute((const void*)k_eval_scatter<(K > 0 ? K : 1)>,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       (int)std::max<size_t>(LDS_WORDS * 4 + 16, SCATTER_LDS_BYTES))));
+        if (e != hipSuccess) return e;
         attr_mark(ATTR_HYBRID + cv.k, dev);
     }
     if (cv.rg_off && attr_pending(ATTR_RAGGED, dev)) {
@@ -4101,17 +4119,12 @@ hipError_t launch_eval_hybrid(const ClauseView& cv, const LoopBuffers& b, uint32
     // window words (a multiple of 4) + the zero word (a 16-byte slot); the scatter reuses it
     size_t lds = ((size_t)(std::min(b.n_words, b.win_words) + 3) / 4 * 4 + 4) * 4;
     if (scatter) lds = std::max(lds, SCATTER_LDS_BYTES);
-    const int g = gated ? 1 : 0, sc = scatter ? 1 : 0;
-    switch (cv.k) {
-        case 1: k_eval_hybrid<1><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g, sc); break;
-        case 2: k_eval_hybrid<2><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g, sc); break;
-        case 3: k_eval_hybrid<3><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g, sc); break;
-        case 4: k_eval_hybrid<4><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g, sc); break;
-        case 5: k_eval_hybrid<5><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g, sc); break;
-        case 6: k_eval_hybrid<6><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g, sc); break;
-        case 7: k_eval_hybrid<7><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g, sc); break;
-        case 8: k_eval_hybrid<8><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g, sc); break;
-        default: return hipErrorInvalidValue;
+    const int g = gated ? 1 : 0;
+    if (cv.k < 1 || cv.k > (uint32_t)MAX_FIXED_K) return hipErrorInvalidValue;
+    if (scatter) {
+        ALLL_DISPATCH_K(cv.k, (k_eval_scatter<(K > 0 ? K : 1)><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g)));
+    } else {
+        ALLL_DISPATCH_K(cv.k, (k_eval_hybrid<(K > 0 ? K : 1)><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g)));
     }
     return hipGetLastError();
 }
@@ -4133,18 +4146,19 @@ hipError_t launch_collect(const ClauseView& cv, const LoopBuffers& b, uint32_t o
     return hipGetLastError();
 }
 
-hipError_t launch_cmark(const ClauseView& cv, const LoopBuffers& b, size_t words_per_rank, int rank, hipStream_t s) {
+hipError_t launch_cmark(const ClauseView& cv, const LoopBuffers& b, size_t words_per_rank, int rank, bool gated,
+                        hipStream_t s) {
     if (!b.cmask || !b.cflag || words_per_rank >= (1ull << 32)) return hipErrorInvalidValue;
     // violated clauses → a byte each (k_cmark), packed into this rank's mask words (k_cpack);
     // 64-bit atomicOr per clause instead: 34.6 µs per iteration at M on one rank
     const uint64_t base = (uint64_t)words_per_rank * (uint64_t)rank * 64u;
     if (b.own_end > b.own_begin) {
         const uint32_t g = (b.own_end - b.own_begin + 3) / 4;
-        ALLL_DISPATCH_K(cv.k, (k_cmark<K><<<g, 256, 0, s>>>(cv, b, base)));
+        ALLL_DISPATCH_K(cv.k, (k_cmark<K><<<g, 256, 0, s>>>(cv, b, base, gated ? 1 : 0)));
     }
     if (words_per_rank) {
         uint64_t* w = reinterpret_cast<uint64_t*>(b.cmask) + words_per_rank * (size_t)rank;
-        k_cpack<<<(uint32_t)((words_per_rank + 255) / 256), 256, 0, s>>>(b, w, (uint32_t)words_per_rank);
+        k_cpack<<<(uint32_t)((words_per_rank + 255) / 256), 256, 0, s>>>(b, w, (uint32_t)words_per_rank, gated ? 1 : 0);
     }
     return hipGetLastError();
 }

@@ -75,10 +75,11 @@ struct alll_ctx {
     LoopBuffers b{};
     uint32_t tiles_per_rank = 0, own_begin = 0, own_end = 0, n_tiles_padded = 0;
     uint32_t grid_rounds = DEFAULT_GRID_ROUNDS;
-    // env ALLL_FUSE_SCATTER=1: the evaluation workgroups scatter their runs themselves (no
-    // k_bscatter launch; +2.6% iterations/s at M, but the evaluation kernel's duration then
-    // includes the scatter, so its roofline is no longer the evaluation's: off by default)
-    bool fuse_scatter = false;
+    // One GPU, bucketed round 0: the evaluation workgroups scatter their runs' claims themselves
+    // (k_eval_scatter<K>, no k_bscatter launch; +2.6% iterations/s at M in round 4).  The
+    // evaluation alone keeps its own kernel (k_eval_hybrid<K>: alll_bench_eval, verify, the
+    // other variants) for its roofline.  env ALLL_FUSE_SCATTER=0: the separate k_bscatter
+    bool fuse_scatter = true;
     std::vector<uint32_t> run_t0;  // bucketed round 0: first tile of every run (+ end)
     int rank = 0, world = 1;
     bool allreduce = false;
@@ -353,7 +354,7 @@ int host_exchange(alll_ctx* c, int op, void* dev, size_t bytes, size_t own_off) 
 int enqueue_exchange(alll_ctx* c, hipStream_t s) {
     const size_t words = (size_t)c->tiles_per_rank * TILE_WORDS;
     uint64_t* mask = c->b.cmask ? c->b.cmask : c->b.vmask;
-    if (c->b.cmask) HIP_TRY(launch_cmark(c->cv, c->b, words, c->rank, s));
+    if (c->b.cmask) HIP_TRY(launch_cmark(c->cv, c->b, words, c->rank, true, s));
     if (c->comm) {
         NCCL_TRY(ncclAllGather(mask + (size_t)c->rank * words, mask, words, ncclUint64, c->comm, s));
     } else {
@@ -805,9 +806,10 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
                 uint64_t d = 0;
                 bool sat = false;
                 for (unsigned q = 0; q < used; ++q) { d += hist[q][v]; sat |= hist[q][v] == 0xFFFF; }
-                if (d < thr) continue;
+                // (a saturated count is a lower bound: such a variable is recounted exactly
+                // whatever its sum, the threshold applies to exact sums only)
                 if (sat) rec_t[t].push_back((uint32_t)v);
-                else hot_t[t].push_back({(uint32_t)d, (uint32_t)v});
+                else if (d >= thr) hot_t[t].push_back({(uint32_t)d, (uint32_t)v});
             }
         });
         hist.clear();
@@ -825,7 +827,7 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
                 if (it != recount.end() && *it == v) ++d[it - recount.begin()];
             }
             for (size_t q = 0; q < recount.size(); ++q)
-                hot.push_back({(uint32_t)std::min<uint64_t>(d[q], 0xFFFFFFFFu), recount[q]});
+                if (d[q] >= thr) hot.push_back({(uint32_t)std::min<uint64_t>(d[q], 0xFFFFFFFFu), recount[q]});
         }
         if (!hot.empty()) {
             std::sort(hot.rbegin(), hot.rend());
@@ -1473,6 +1475,20 @@ int alll_verify(alll_ctx* c, int* valid, uint64_t* n_violated) {
     HIP_TRY(eval_launch(c, c->own_begin, c->own_end, false));
     HIP_TRY(launch_reduce(c->b, 1, c->stream));
     uint64_t count = 0;
+    if (c->world > 1) {
+        // the mask alll_get_violated_mask returns on sharded runs (clause order: cmask, or the
+        // CSR evaluation's own bitmask) refreshed from this evaluation: the own shard's piece,
+        // then the other shards' pieces all-gathered
+        const size_t words = (size_t)c->tiles_per_rank * TILE_WORDS;
+        uint64_t* mask = c->b.cmask ? c->b.cmask : c->b.vmask;
+        if (c->b.cmask) HIP_TRY(launch_cmark(c->cv, c->b, words, c->rank, false, c->stream));
+        if (c->comm) {
+            NCCL_TRY(ncclAllGather(mask + (size_t)c->rank * words, mask, words, ncclUint64, c->comm, c->stream));
+        } else {
+            int rc = host_exchange(c, ALLL_XCHG_ALLGATHER, mask, words * 8, (size_t)c->rank * words * 8);
+            if (rc) return rc;
+        }
+    }
     if (c->world > 1) {
         if (c->comm) {
             NCCL_TRY(ncclAllReduce(c->b.xcount, c->b.xcount, 1, ncclUint32, ncclSum, c->comm, c->stream));

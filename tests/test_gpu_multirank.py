@@ -58,6 +58,10 @@ def worker(rank, world, port, spec, flags, out_q):
                 traj.append(s.assignment_words().tolist())
             st = s.stats()
             mis = s.mis().tolist()
+            # a standalone evaluation after the loop: the count summed over the ranks and the
+            # clause-order mask refreshed from it (own shard + all-gathered pieces)
+            st["verify"] = s.verify()
+            st["mask"] = s.violated_mask().tolist()
         out_q.put((rank, traj, st, mis, None))
     except Exception as e:  # surfaced by the parent
         out_q.put((rank, None, None, None, repr(e)))
@@ -108,6 +112,9 @@ SPECS = {
     # BASELINE config C2 at full size (1M variables, 4M clauses = 977 tiles, 489 per rank):
     # two iterations, bit-exact on both ranks
     "c2": (1_000_000, 4_000_000, 3, 0, 1, 2),
+    # BASELINE config C5 at full size (power-law 3-SAT, 2.5M variables / 10M clauses: hot
+    # variables, vmix owner slots, 7 grid rounds), the 8-GPU config's sharded path at world 2
+    "c5": (2_500_000, 10_000_000, 3, 1, 1, 2),
     # the round robin of T = 4 / 7 sets (the fixpoint passes) on every rank of the sharded loop
     "small_rr4": (7000, 28000, 3, 0, 5, 8, 4),
     "c2_rr7": (1_000_000, 4_000_000, 3, 0, 1, 2, 7),
@@ -125,7 +132,8 @@ ENV = {"small_positions": {"ALLL_PACKED_IDS": "0"}}
                                                   (3, "allgather", "small"), (3, "allreduce", "small"),
                                                   (2, "allgather", "windows"), (2, "allgather", "long"),
                                                   (2, "allreduce", "long"), (2, "allgather", "c2"),
-                                                  (2, "allreduce", "c2"), (2, "allgather", "small_rr4"),
+                                                  (2, "allreduce", "c2"), (2, "allgather", "c5"),
+                                                  (2, "allgather", "small_rr4"),
                                                   (3, "allreduce", "small_rr4"), (2, "allgather", "c2_rr7"),
                                                   (3, "allgather", "small_positions"), (2, "allgather", "ragged"),
                                                   (3, "allreduce", "ragged"), (2, "allgather", "k8")])
@@ -148,6 +156,10 @@ def test_sharded_solver_matches_oracle(oracle_mod, native, world, mode, spec_nam
         assert st["sum_mis_size"] == st_o["sum_mis_size"]
         assert st["n_gpus"] == world
         assert sum(st["gpu_resamples"]) == st["n_resamples"]
+        # verify + get_violated_mask after the loop describe the final assignment
+        nv_o, vm_o = o.eval_mask(offs, lits, np.array(traj[-1], np.uint32))
+        assert st["verify"] == (nv_o == 0, nv_o), f"rank {rank}"
+        np.testing.assert_array_equal(np.array(st["mask"], np.uint64), vm_o, err_msg=f"rank {rank} mask")
     # all ranks agree on the last MIS
     assert all(r[3] == res[0][3] for r in res)
 

@@ -26,8 +26,9 @@ T1_FIXTURES = sorted(p for p in glob.glob(os.path.join(GOLDEN, "*_T1.npz")))
 LAYOUTS = {"hybrid": (0, {}), "fixed": (1 << 3, {}), "csr": (1 << 2, {}), "atomic_claims": (1 << 5, {}),
            "buckets": (0, {"ALLL_BUCKET_MIN_U": "0"}), "windows": (0, {"ALLL_EVAL_WINDOWS": "1"}),
            "positions": (0, {"ALLL_PACKED_IDS": "0"}),
-           # bucketed round 0 scattered by the evaluation workgroups (no k_bscatter)
-           "scatter": (0, {"ALLL_FUSE_SCATTER": "1", "ALLL_BUCKET_MIN_U": "0"}),
+           # bucketed round 0 scattered by its own kernel k_bscatter (the default fuses the
+           # scatter into the evaluation workgroups, k_eval_scatter)
+           "bscatter": (0, {"ALLL_FUSE_SCATTER": "0", "ALLL_BUCKET_MIN_U": "0"}),
            # the large-instance evaluation (non-temporal literal loads, exec-masked L2 lookups)
            # with windows
            "nt_windows": (0, {"ALLL_EVAL_NT": "1", "ALLL_EVAL_WINDOWS": "1"}),
@@ -312,8 +313,8 @@ BIG = {
     "C5_powerlaw_10M": (2_500_000, 10_000_000, 3, 1),
     # power-law with the atomic round 0 (the default policy buckets it while |U| is large)
     "C5_atomic_round0": (2_500_000, 10_000_000, 3, 1, {"ALLL_BUCKET_MIN_U": str(1 << 62)}),
-    "C5_scatter": (2_500_000, 10_000_000, 3, 1, {"ALLL_FUSE_SCATTER": "1"}),
-    "M_scatter": (2_500_000, 10_000_000, 3, 0, {"ALLL_FUSE_SCATTER": "1"}),
+    "C5_bscatter": (2_500_000, 10_000_000, 3, 1, {"ALLL_FUSE_SCATTER": "0"}),
+    "M_bscatter": (2_500_000, 10_000_000, 3, 0, {"ALLL_FUSE_SCATTER": "0"}),
     "W_3sat_4Mvars": (4_000_000, 2_000_000, 3, 0),  # 4 LDS blocks of variables: windowed eval
     "M_no_windows": (2_500_000, 10_000_000, 3, 0, {"ALLL_EVAL_WINDOWS": "0"}),
     "M_positions": (2_500_000, 10_000_000, 3, 0, {"ALLL_PACKED_IDS": "0"}),  # perm translation

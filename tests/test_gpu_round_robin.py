@@ -268,27 +268,81 @@ def test_rr_back_to_back_runs_without_sync(gpu, oracle_mod, monkeypatch):
         np.testing.assert_array_equal(s.assignment_words(), rows[-1][4])
 
 
-RR_LAYOUTS = {"positions": {"ALLL_PACKED_IDS": "0"},  # clause ids via perm (k_rr_mark's unpack)
-              "small_windows": {"ALLL_EVAL_WINDOWS": "1", "ALLL_WIN_WORDS": "64"},
-              "nt_windows": {"ALLL_EVAL_WINDOWS": "1", "ALLL_WIN_WORDS": "64", "ALLL_EVAL_NT": "1"}}
+# name: (environment, solver flag): every evaluation the round robin can run over
+RR_LAYOUTS = {"positions": ({"ALLL_PACKED_IDS": "0"}, None),  # clause ids via perm (k_rr_mark's unpack)
+              "small_windows": ({"ALLL_EVAL_WINDOWS": "1", "ALLL_WIN_WORDS": "64"}, None),
+              "nt_windows": ({"ALLL_EVAL_WINDOWS": "1", "ALLL_WIN_WORDS": "64", "ALLL_EVAL_NT": "1"}, None),
+              # the L2-gather evaluation k_eval_fixed writes the lists k_rr_mark reads
+              "fixed": ({}, "FLAG_NO_RANGED"),
+              # the clause-order CSR evaluation (its bitmask feeds k_rr_entries directly)
+              "csr": ({}, "FLAG_GENERIC_CSR")}
 
 
 @pytest.mark.parametrize("layout", list(RR_LAYOUTS))
 @pytest.mark.parametrize("name,T", [("ratio4", 7), ("k5_multi_tile", 16)])
-def test_rr_on_hybrid_eval_layouts(gpu, oracle_mod, name, T, layout, monkeypatch):
-    """The round robin over the fixed-width (hybrid) evaluation: its per-tile lists in
-    evaluation order become clause-order flags (k_rr_mark) under every evaluation layout."""
+def test_rr_on_hybrid_eval_layouts(gpu, oracle_mod, native, name, T, layout, monkeypatch):
+    """The round robin over every fixed-width evaluation: the hybrid kernel's per-tile lists in
+    evaluation order become clause-order flags (k_rr_mark) under every layout; the L2-gather
+    kernel's lists the same way; the CSR evaluation's clause-order bitmask directly."""
     from alllsatisfiabilitysolver_amd import Solver
 
     n, offs, lits = _instance(name)
     seed, K = 17, 10
     st_o, A_o, rows = oracle_mod.solve(n, offs, lits, seed, max_iters=K, trace=True, T=T)
-    for k, v in RR_LAYOUTS[layout].items():
+    env, flag = RR_LAYOUTS[layout]
+    for k, v in env.items():
         monkeypatch.setenv(k, v)
-    with Solver(n, offs, lits, seed=seed, n_threads=T) as s:
-        for k in RR_LAYOUTS[layout]:
+    flags = getattr(native, flag) if flag else 0
+    with Solver(n, offs, lits, seed=seed, n_threads=T, flags=flags) as s:
+        for k in env:
             monkeypatch.delenv(k)
         for it, nu, nm, dres, A_after in rows:
             s.run(1)
             assert s.stats()["n_violated"] == nu, f"iter {it}"
             np.testing.assert_array_equal(s.assignment_words(), A_after, err_msg=f"A after iter {it}")
+
+
+_TORCH_FIRST_CHILD = r"""
+import json, sys
+import numpy as np
+import torch  # first: its wheel's HIP runtime (same soname) then serves the library too
+assert torch.cuda.is_available()
+sys.path.insert(0, sys.argv[1])
+from alllsatisfiabilitysolver_amd import Solver, generate_ksat
+maps = sorted({l.split()[-1] for l in open("/proc/self/maps") if "libamdhip64" in l})
+n, m, T, seed, K = (int(x) for x in sys.argv[3:8])
+offs, lits = generate_ksat(1, n, m, 3)
+with Solver(n, offs, lits, seed=seed, device=0, n_threads=T) as s:
+    for _ in range(K):
+        s.run(1)
+    np.save(sys.argv[2], s.assignment_words())
+    st = s.stats()
+print(json.dumps({"hip_runtime": maps, "n_iterations": st["n_iterations"], "n_resamples": st["n_resamples"],
+                  "sum_mis_size": st["sum_mis_size"]}))
+"""
+
+
+def test_rr_under_torch_runtime(gpu, oracle_mod, tmp_path):
+    """The round robin in a process that imported torch first, so that the library runs on the
+    HIP runtime bundled in torch's wheel (ROCm 7.0; the loop's graphs once stalled there,
+    DESIGN.md §10): K iterations of host-driven pass graphs (every graph replayed several times)
+    in a subprocess under a time limit, bit-exact against the oracle's T-chunk loop."""
+    import json
+    import subprocess
+    import sys
+
+    from alllsatisfiabilitysolver_amd import generate_ksat
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    n, m, T, seed, K = 250_000, 1_000_000, 16, 3, 24
+    out = str(tmp_path / "A.npy")
+    r = subprocess.run([sys.executable, "-c", _TORCH_FIRST_CHILD, root, out] + [str(x) for x in (n, m, T, seed, K)],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert d["hip_runtime"] and all("torch" in p for p in d["hip_runtime"]), d["hip_runtime"]
+    offs, lits = generate_ksat(1, n, m, 3)
+    _, _, rows = oracle_mod.solve(n, offs, lits, seed, max_iters=K + 1, trace=True, T=T)
+    assert d["n_iterations"] == K == len(rows)
+    assert d["n_resamples"] == sum(r[3] for r in rows) and d["sum_mis_size"] == sum(r[2] for r in rows)
+    np.testing.assert_array_equal(np.load(out), rows[-1][4])

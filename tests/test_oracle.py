@@ -345,10 +345,16 @@ def test_bench_trajectory_check_logic():
         import alllsatisfiabilitysolver_amd as pkg
 
         pkg.assignment_digest = S.assignment_digest
-        assert bench.trajectory_check("C2", 1, st, None)["match"] is True
-        assert bench.trajectory_check("C2", 1, {**st, "n_resamples": res + 1}, None)["match"] is False
-        assert bench.trajectory_check("C2", 1, {**st, "n_iterations": 10_000}, None)["match"] is None
-        assert bench.trajectory_check("C3", 1, st, None)["match"] is None
+        assert bench.trajectory_check("C2", 1, st, None, 1)["match"] is True
+        assert bench.trajectory_check("C2", 1, {**st, "n_resamples": res + 1}, None, 1)["match"] is False
+        assert bench.trajectory_check("C2", 1, {**st, "n_iterations": 10_000}, None, 1)["match"] is None
+        assert bench.trajectory_check("C2", 7, st, None, 1)["match"] is None  # no such entry
+        # another solve seed than the committed trajectories': not a mismatch, no check
+        r = bench.trajectory_check("C2", 1, st, None, 2)
+        assert r["match"] is None and "seed" in r["reason"]
+        # the 8-GPU configs and the 8-SAT config have entries (a sharded line checks itself)
+        for cfg in ("C3", "C4", "C5"):
+            assert f"{cfg}_T1" in json.load(open(bench.TRAJECTORY_JSON))["trajectories"]
     finally:
         S.assignment_digest = orig
         pkg.assignment_digest = orig

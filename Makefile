@@ -24,8 +24,10 @@ $(SRC)/alll_runtime.o: $(SRC)/alll_runtime.cpp $(SRC)/alll_internal.h include/al
 $(SRC)/alll_host.o: $(SRC)/alll_host.cpp include/alll.h
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
+# (linked to a temporary name and renamed: a tree snapshot taken meanwhile sees the old or the new library)
 $(LIB): $(OBJS)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $(OBJS) -L$(ROCM)/lib -lrccl -Wl,-rpath,$(ROCM)/lib
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@.tmp $(OBJS) -L$(ROCM)/lib -lrccl -Wl,-rpath,$(ROCM)/lib
+	mv -f $@.tmp $@
 
 cli: tools/alll_main
 

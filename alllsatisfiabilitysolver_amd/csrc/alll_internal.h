@@ -60,6 +60,7 @@ constexpr uint32_t FP_G = 4;       // grid LFMIS rounds before the one-workgroup
 constexpr uint32_t FP_G_HOT = 6;   // ... on instances with hot variables (5, 7, 8, 10: slower)
 constexpr uint32_t FP_G_MAX = FP_G_HOT > FP_G ? FP_G_HOT : FP_G;
 constexpr uint32_t FP_MAX_DEFAULT = 64;    // LFMIS passes per iteration before k_rr_mw decides it
+constexpr uint32_t FP_LOG_PASSES = 64;     // passes of an iteration in the pass log (fp_log)
 enum : uint32_t { FP_RUN = 0, FP_FINAL = 1, FP_DONE = 2, FP_OFF = 3, FP_FAIL = 4 };
 struct RRFpCtl {
     uint32_t state;      // FP_*: RUN iterating; FINAL the last pass converged (finalize now);
@@ -81,9 +82,28 @@ struct RRFpCtl {
     uint32_t tpre;       // entries whose turn is below this keep the last pass's decision
     uint32_t e0;         // first erasure step of the last schedule
     uint32_t nheavy;     // variables with more than FP_HEAVY claimants (fp_heavy)
-    uint32_t pad[2];
-    uint32_t spare[16];
+    // incremental passes: after a full pass, a pass re-decides only the entries
+    // whose blocker no longer lies below them (k_fp_detect) and what their changes reach (k_fp_repair)
+    uint32_t inc;        // the next pass is incremental (1) or a full LFMIS pass (0)
+    uint32_t bail;       // an incremental pass gave up (its dirty set outgrew FP_REP_CAP): the next
+                         // pass is a full one, with no settled prefix (tpre = 0)
+    uint32_t ndirty;     // entries k_fp_detect marked for the repair
+    uint32_t rep_serial; // repair round stamps (fp_dmark), never reset
+    uint32_t rep_rounds; // repair rounds of the iteration (statistics)
+    uint32_t ran;        // the pass's last kernel ran (k_fp_tail or k_fp_repair): k_fp_count / k_fp_sched
+                         // test a pass only then (a pass of the other kind in a graph is a no-op)
+    uint32_t skip;       // k_fp_sched found no pass to test: k_fp_turn leaves the turns as they are
+    uint32_t restart;    // iteration start: bit 0 the owner epochs restart (fp_owner cleared), bit 1 the
+                         // cover serials (fp_cov cleared) -- decided with the reduce, done by k_fp_guess
+    // the wide repair (k_fp_repair_wide, the large early rounds across workgroups) hands over to
+    // the one-workgroup repair: the list (wlist: 0 / 1 of fp_dl, ndirty entries), the change log
+    // length (nlog), the rounds and entries decided; its grid barrier and round counters
+    uint32_t wlist, nlog, wrounds, wwork, wfail;
+    uint32_t wbar;
+    uint32_t wcnt[3];
+    uint32_t spare[1];
 };
+static_assert(sizeof(RRFpCtl) == 128, "RRFpCtl: 32 words");
 // In-loop kernel timing (ALLL_FLAG_KERNEL_TIMING): per iteration i, slot i % TIME_SLOTS holds
 // device wall-clock stamps (s_memrealtime) {eval start (min over workgroups), eval end (max),
 // reduce start, LFMIS tail end}.
@@ -250,6 +270,22 @@ struct LoopBuffers {
     uint32_t* fp_nseg;          // T: schedule phases the set lives through
     uint4* fp_seg;              // T x T: {first level, first step, stride, offset} per (set, phase)
     uint32_t* fp_erase;         // T: erasure steps, ascending
+    // incremental passes (fp_inc != 0; nullptr otherwise)
+    uint32_t* fp_blocker;       // per scan entry out of the last pass's picks: a pick below it that shares a
+                                //   variable with it (the pass's cover of that variable, fp_covby)
+    uint32_t* fp_covby;         // n_vars: the pick that covered the variable in the current pass
+    uint32_t* fp_vcnt;          // n_vars: violated claimants of the variable this iteration (fp_vlist length)
+    uint32_t* fp_lst;           // per scan entry, 4 slots (widths <= 4) or 8: {start, length} of the slot's
+                                //   variable's claimant list (uint2; k_fp_bbuild)
+    uint32_t* fp_dl;            // 3 x m + 16 min(m, 2^16): the repair's dirty lists (two), its change log and
+                                //   its raw push list
+    uint32_t* fp_dmark;         // per scan entry: repair round stamp of its last dirty-list insertion
+    uint8_t* fp_pbits;          // the picks of the last pass, a bit per scan entry (k_fp_turn; the repair
+                                //   keeps them in LDS)
+    uint32_t* fp_log;           // FP_LOG_PASSES x 4: per pass of the current iteration {dirty entries, repair
+                                //   rounds, entries decided, changes} (alll_rr_pass_log; measurement)
+    uint32_t fp_inc;            // incremental passes enabled (no hot variables)
+    uint32_t fp_inc_after;      // full passes of an iteration before the incremental ones
     uint32_t fp_ib, fp_tb;      // key bits of the entry index and of the turn
     uint32_t fp_hot;            // the instance has hot variables (more grid rounds per pass)
     uint32_t fp_max;            // LFMIS passes per iteration
@@ -270,8 +306,10 @@ hipError_t launch_set_limits(const LoopBuffers& b, uint64_t n, hipStream_t s);
 hipError_t launch_eval(const ClauseView& cv, const LoopBuffers& b, uint32_t tile_begin,
                        uint32_t tile_end, bool gated, hipStream_t s);
 // scatter: also the bucket scatter of LFMIS round 0 (one GPU; runs split the workgroups' tiles)
+// flags: the one-GPU round robin's evaluation (clause-order violated flags, no lists)
 hipError_t launch_eval_hybrid(const ClauseView& cv, const LoopBuffers& b, uint32_t tile_begin,
-                              uint32_t tile_end, bool gated, int n_blocks, bool scatter, hipStream_t s);
+                              uint32_t tile_end, bool gated, int n_blocks, bool scatter, hipStream_t s,
+                              bool flags = false);
 hipError_t launch_eval_ragged(const ClauseView& cv, const LoopBuffers& b, uint32_t tile_begin,
                               uint32_t tile_end, bool gated, int n_blocks, hipStream_t s);
 hipError_t launch_collect(const ClauseView& cv, const LoopBuffers& b, uint32_t own_begin,
@@ -288,9 +326,12 @@ hipError_t launch_tail(const ClauseView& cv, const LoopBuffers& b, uint32_t firs
                        hipStream_t s);
 // round robin: scan entries and the fixpoint's iteration set-up (when b.fp_ctl); n fixpoint
 // passes; k_rr_mw for an iteration the passes did not settle
-hipError_t launch_rr_prep(const ClauseView& cv, const LoopBuffers& b, hipStream_t s);
+// marked: the evaluation set the clause-order violated flags itself (k_eval_flags)
+hipError_t launch_rr_prep(const ClauseView& cv, const LoopBuffers& b, bool marked, hipStream_t s);
 hipError_t prepare_kernels(const ClauseView& cv, const LoopBuffers& b);  // attributes, before any capture
-hipError_t launch_rr_passes(const ClauseView& cv, const LoopBuffers& b, uint32_t n, hipStream_t s);
+// n passes: the first full (an LFMIS pass over every entry) when `full`, the others incremental
+// when b.fp_inc (each kernel is gated on the pass kind the device state asks for)
+hipError_t launch_rr_passes(const ClauseView& cv, const LoopBuffers& b, uint32_t n, bool full, hipStream_t s);
 hipError_t launch_rr_finish(const ClauseView& cv, const LoopBuffers& b, hipStream_t s);
 hipError_t launch_resample(const ClauseView& cv, const LoopBuffers& b, uint32_t tile_begin,
                            uint32_t tile_end, bool to_delta, hipStream_t s);

@@ -357,10 +357,13 @@ __global__ __launch_bounds__(EVAL_THREADS) void k_eval_fixed(ClauseView cv, Loop
 // per literal slot from the chunk-transposed layout (as k_eval_fixed), so the literal stream
 // is read once, perfectly coalesced.  Violated clauses go to the per-tile lists through
 // per-tile LDS counters.
-// SC: the evaluation workgroups also scatter LFMIS round 0's claims of their runs (one GPU,
-// bucketed round 0): k_eval_scatter<K>, a kernel of its own so that profiles and the roofline
-// keep the evaluation alone (k_eval_hybrid<K>) apart from the fused loop kernel.
-template <int K, bool SC>
+// MODE: EV_LISTS the violated clauses go to the per-tile lists (k_eval_hybrid<K>); EV_SCATTER the
+// evaluation workgroups also scatter LFMIS round 0's claims of their runs (one GPU, bucketed round
+// 0: k_eval_scatter<K>, a kernel of its own so that profiles and the roofline keep the evaluation
+// alone apart from the fused loop kernel); EV_FLAGS (the one-GPU round robin) each violated clause
+// sets its byte of the clause-order flags rr_flag instead (k_eval_flags<K>: no lists, no k_rr_mark).
+enum : int { EV_LISTS = 0, EV_SCATTER = 1, EV_FLAGS = 2 };
+template <int K, int MODE>
 __device__ __forceinline__ void eval_hybrid_body(const ClauseView& cv, const LoopBuffers& b, uint32_t tile_begin,
                                                  uint32_t tile_end, int gated) {
     if (gated && eval_gate_closed(b.state)) return;
@@ -555,7 +558,24 @@ __device__ __forceinline__ void eval_hybrid_body(const ClauseView& cv, const Loo
             const uint32_t tot = __popcll(b0) + __popcll(b1) + __popcll(b2) + __popcll(b3);
             // (wide clauses are rarely violated: their entries are stored only by chunks that
             // hold violated clauses, with the branching emit4)
-            if (K <= 4 || tot) {
+            if constexpr (MODE == EV_FLAGS) {
+                const uint32_t tile = (uint32_t)(g / (TILE / CHUNK));
+                if (lane == 0 && tot) atomicAdd(&s_tcnt[tile - pt], tot);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    if (!v[q]) continue;
+                    Ent<K> e;
+                    uint32_t t[K];
+#pragma unroll
+                    for (int j = 0; j < K; ++j) {
+                        const uint32_t xs[4] = {x[j].x, x[j].y, x[j].z, x[j].w};
+                        t[j] = xs[q];
+                    }
+                    make_ent<K>(e, c0 + q, t);
+                    ent_unpack<K>(cv, e);
+                    b.rr_flag[e.w[0]] = 1u;
+                }
+            } else if (K <= 4 || tot) {
                 const uint32_t tile = (uint32_t)(g / (TILE / CHUNK));
                 uint32_t base = 0;
                 if (lane == 0) base = atomicAdd(&s_tcnt[tile - pt], tot);
@@ -612,7 +632,7 @@ __device__ __forceinline__ void eval_hybrid_body(const ClauseView& cv, const Loo
         }
     }
     stamp_eval_end(b, gated);
-    if constexpr (SC) {
+    if constexpr (MODE == EV_SCATTER) {
         // One GPU, bucketed LFMIS round 0: this workgroup's tiles form runs b.run_t0[r] ..
         // (rpw runs per workgroup), so the workgroup scatters their claims itself, from the
         // lists it has just written (L2-warm) and with the window's LDS, instead of a
@@ -630,13 +650,19 @@ __device__ __forceinline__ void eval_hybrid_body(const ClauseView& cv, const Loo
 template <int K>
 __global__ __launch_bounds__(HYB_THREADS) void k_eval_hybrid(ClauseView cv, LoopBuffers b, uint32_t tile_begin,
                                                              uint32_t tile_end, int gated) {
-    eval_hybrid_body<K, false>(cv, b, tile_begin, tile_end, gated);
+    eval_hybrid_body<K, EV_LISTS>(cv, b, tile_begin, tile_end, gated);
 }
 
 template <int K>
 __global__ __launch_bounds__(HYB_THREADS) void k_eval_scatter(ClauseView cv, LoopBuffers b, uint32_t tile_begin,
                                                               uint32_t tile_end, int gated) {
-    eval_hybrid_body<K, true>(cv, b, tile_begin, tile_end, gated);
+    eval_hybrid_body<K, EV_SCATTER>(cv, b, tile_begin, tile_end, gated);
+}
+
+template <int K>
+__global__ __launch_bounds__(HYB_THREADS) void k_eval_flags(ClauseView cv, LoopBuffers b, uint32_t tile_begin,
+                                                            uint32_t tile_end, int gated) {
+    eval_hybrid_body<K, EV_FLAGS>(cv, b, tile_begin, tile_end, gated);
 }
 
 // Clause evaluation, ragged widths (ClauseView::rg_off): the persistent LDS-window structure
@@ -1004,12 +1030,72 @@ __device__ void reduce_body(const LoopBuffers& b, int mode) {
     }
 }
 
+// Round robin (fixpoint passes): the iteration's start, run by the reduce's workgroup after the
+// violated count (one launch less than a kernel of its own): entry count, set bounds, pass state.
+// Owner keys and cover serials carry over from iteration to iteration (keys of later epochs are
+// smaller, serials grow), so neither array needs clearing at every iteration; the restart rules
+// below decide when they start over (k_fp_guess clears them then).
+__device__ __forceinline__ uint32_t fp_ep_budget(const LoopBuffers& b);
+__device__ __forceinline__ bool fp_ep_restart(const LoopBuffers& b, const RRFpCtl* ctl) {
+    return ctl->ep_next >= fp_ep_budget(b) / 2;  // (every iteration gets at least half the epochs)
+}
+__device__ __forceinline__ bool fp_serial_restart(const LoopBuffers& b, const RRFpCtl* ctl) {
+    return ctl->serial + b.fp_max + 2u > 255u;  // (8-bit cover serials, at most fp_max passes)
+}
+__device__ void fp_begin_body(const LoopBuffers& b) {
+    RRFpCtl* ctl = b.fp_ctl;
+    __shared__ uint32_t s_act, s_nu;
+    if (threadIdx.x == 0) {
+        s_act = b.state->active;  // (thread 0 wrote the state)
+        s_nu = (uint32_t)b.state->u_total;
+    }
+    __syncthreads();
+    if (!s_act) {
+        if (threadIdx.x == 0) ctl->state = FP_OFF;
+        return;
+    }
+    const uint32_t nu = s_nu, T = b.rr_T;
+    // set starts (first entry with id >= the set's first clause): k_rr_entries writes those that
+    // fall in a tile; the end and the starts past the last clause are nu
+    for (uint32_t s = threadIdx.x; s <= T; s += blockDim.x)
+        if (s == T || b.rr_sets[s] >= b.m) b.fp_sf[s] = nu;
+    if (b.fp_log)
+        for (uint32_t q = threadIdx.x; q < 4 * FP_LOG_PASSES; q += blockDim.x) b.fp_log[q] = 0;
+    if (threadIdx.x == 0) {
+        const bool ep0 = fp_ep_restart(b, ctl), ser0 = fp_serial_restart(b, ctl);
+        ctl->restart = (ep0 ? 1u : 0u) | (ser0 ? 2u : 0u);
+        ctl->state = FP_RUN;
+        ctl->nu = nu;
+        ctl->fp_iter = 0;
+        ctl->changes = 0;
+        ctl->ep_base = ep0 ? 0u : ctl->ep_next;
+        ctl->ep_next = ctl->ep_base;
+        if (ser0) ctl->serial = 0;
+        ctl->tpre = 0;
+        ctl->e0 = ~0u;
+        ctl->nheavy = 0;
+        ctl->inc = 0;  // (the first pass is a full one)
+        ctl->bail = 0;
+        ctl->ran = 0;
+        ctl->skip = 0;
+        ctl->rep_rounds = 0;
+        if (ctl->guess_den == 0) { ctl->guess_num = 1; ctl->guess_den = 2; }
+    }
+}
+
 __global__ __launch_bounds__(1024) void k_reduce(LoopBuffers b, int mode) {
     if (mode == 0 && eval_gate_closed(b.state)) {
-        if (threadIdx.x == 0) b.state->active = 0;
+        if (threadIdx.x == 0) {
+            b.state->active = 0;
+            if (b.fp_ctl) b.fp_ctl->state = FP_OFF;
+        }
         return;
     }
     reduce_body(b, mode);
+    if (mode == 0 && b.fp_ctl) {
+        __syncthreads();  // (thread 0 has written the loop state)
+        fp_begin_body(b);
+    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -2971,61 +3057,15 @@ __device__ __forceinline__ void fp_append(bool keep, uint32_t i, uint32_t* cnt, 
     if (keep) out[base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = i;
 }
 
-// Iteration start: entry count, set bounds, pass state.  Runs after the reduce.
-// Owner keys and cover serials carry over from iteration to iteration (keys of later epochs
-// are smaller, serials grow), so neither array needs clearing at every iteration: both
-// kernels below decide from the same control words whether this iteration starts over.
-__device__ __forceinline__ bool fp_ep_restart(const LoopBuffers& b, const RRFpCtl* ctl) {
-    return ctl->ep_next >= fp_ep_budget(b) / 2;  // (every iteration gets at least half the epochs)
-}
-__device__ __forceinline__ bool fp_serial_restart(const LoopBuffers& b, const RRFpCtl* ctl) {
-    return ctl->serial + b.fp_max + 2u > 255u;  // (8-bit cover serials, at most fp_max passes)
-}
-// Iteration start, before k_fp_begin: clears the owner keys / cover serials when they restart.
-__global__ __launch_bounds__(256) void k_fp_reset(LoopBuffers b) {
-    const RRFpCtl* ctl = b.fp_ctl;
-    if (!b.state->active) return;
-    const bool ep = fp_ep_restart(b, ctl), ser = fp_serial_restart(b, ctl);
-    if (!ep && !ser) return;
-    for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < b.n_vars; v += gridDim.x * blockDim.x) {
-        if (ep) b.fp_owner[v] = ~0ull;
-        if (ser) b.fp_cov[v] = 0;
-    }
-}
-
-__global__ __launch_bounds__(256) void k_fp_begin(LoopBuffers b) {
-    RRFpCtl* ctl = b.fp_ctl;
-    const DevState* st = b.state;
-    if (!st->active) {
-        if (threadIdx.x == 0) ctl->state = FP_OFF;
-        return;
-    }
-    const uint32_t nu = (uint32_t)st->u_total, T = b.rr_T;
-    // set starts (first entry with id >= the set's first clause): k_rr_entries wrote those that
-    // fall in a tile; the end and the starts past the last clause are nu
-    for (uint32_t s = threadIdx.x; s <= T; s += blockDim.x)
-        if (s == T || b.rr_sets[s] >= b.m) b.fp_sf[s] = nu;
-    const bool ep0 = fp_ep_restart(b, ctl), ser0 = fp_serial_restart(b, ctl);  // (as k_fp_reset)
-    __syncthreads();  // (every thread has read the control words)
-    if (threadIdx.x == 0) {
-        ctl->state = FP_RUN;
-        ctl->nu = nu;
-        ctl->fp_iter = 0;
-        ctl->changes = 0;
-        ctl->ep_base = ep0 ? 0u : ctl->ep_next;
-        ctl->ep_next = ctl->ep_base;
-        if (ser0) ctl->serial = 0;
-        ctl->tpre = 0;
-        ctl->e0 = ~0u;
-        ctl->nheavy = 0;
-        if (ctl->guess_den == 0) { ctl->guess_num = 1; ctl->guess_den = 2; }
-    }
-}
-
 // The first pass's input: picks spread evenly over every set at density num / den.
 __global__ __launch_bounds__(FP_THREADS) void k_fp_guess(LoopBuffers b) {
     const RRFpCtl* ctl = b.fp_ctl;
     if (ctl->state != FP_RUN) return;
+    if (const uint32_t rs = ctl->restart)  // (the iteration's restart of owner epochs / cover serials)
+        for (uint32_t v = blockIdx.x * blockDim.x + threadIdx.x; v < b.n_vars; v += gridDim.x * blockDim.x) {
+            if (rs & 1u) b.fp_owner[v] = ~0ull;
+            if (rs & 2u) b.fp_cov[v] = 0;
+        }
     __shared__ uint32_t s_sf[FP_TMAX + 1];
     const uint32_t T = b.rr_T, nu = ctl->nu;
     const unsigned long long num = ctl->guess_num, den = ctl->guess_den;
@@ -3204,6 +3244,26 @@ __global__ __launch_bounds__(FP_BB_THREADS) void k_fp_bbuild(LoopBuffers b) {
         }
     }
     __syncthreads();
+    if (b.fp_lst) {
+        // incremental passes: every claim's list {start, length} at its entry's slot (the repair
+        // reads an entry's lists with its first load; slots past the list rows keep the rolled path)
+        const uint32_t rw = b.rr_k >= 1 && b.rr_k <= 4 ? 4u : 8u;
+        for (uint32_t k0 = tid; k0 < n; k0 += U4 * FP_BB_THREADS) {
+            uint2 p[U4];
+#pragma unroll
+            for (uint32_t u = 0; u < U4; ++u) {
+                const uint32_t k = k0 + u * FP_BB_THREADS;
+                p[u] = k < n ? P[k] : make_uint2(0u, ~0u);
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < U4; ++u) {
+                const uint32_t j = p[u].x >> FP_SLOT_SH;
+                if (p[u].y == ~0u || j >= rw) continue;
+                const uint32_t w = vmix(b, p[u].y) - xb;
+                reinterpret_cast<uint2*>(b.fp_lst)[(uint64_t)(p[u].x & FP_IMASK) * rw + j] = make_uint2(s_off[w], s_cnt[w]);
+            }
+        }
+    }
     // per variable (vmix slot order): the single claimant's ownership and sole byte, the shared
     // list and the long lists' segments
     uint4* sv = reinterpret_cast<uint4*>(b.fp_sv) + (uint64_t)bk * W;
@@ -3219,6 +3279,7 @@ __global__ __launch_bounds__(FP_BB_THREADS) void k_fp_bbuild(LoopBuffers b) {
         uint32_t base = 0;
         if (lane == 0 && bal) base = atomicAdd(&s_ns, (uint32_t)__popcll(bal));
         base = __shfl(base, 0, 64);
+        if (c && b.fp_vcnt) b.fp_vcnt[v] = c;  // (incremental passes: the list's length)
         if (c == 1u) {
             const uint32_t x = s_first[w], i = x & FP_IMASK, j = x >> FP_SLOT_SH;
             b.fp_own0[v] = i;
@@ -3249,7 +3310,7 @@ __global__ __launch_bounds__(FP_BB_THREADS) void k_fp_bbuild(LoopBuffers b) {
 constexpr uint32_t FP_VS = 4;  // (1, 2, 4, 8: 444, 464, 461, 462 iterations/s at M, T = 16)
 __global__ __launch_bounds__(FP_THREADS) void k_fp_vmin(LoopBuffers b) {
     const RRFpCtl* ctl = b.fp_ctl;
-    if (ctl->state != FP_RUN) return;
+    if (ctl->state != FP_RUN || ctl->inc) return;  // (a full pass)
     const uint32_t ep = ctl->ep_base, nbw = b.n_bkt * FP_VS;
     if (blockIdx.x >= nbw) {
         const uint32_t nh = ctl->nheavy, lane = threadIdx.x & 63, hw = gridDim.x - nbw;
@@ -3349,8 +3410,16 @@ __device__ __forceinline__ bool fp_claim_one(const ClauseView& cv, const LoopBuf
     const uint32_t sole = fp_sole_mask<KW>(b, i);
     const uint32_t turn = b.fp_turn[i];
     bool dead = false;
-    fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) { dead |= b.fp_cov[v] == (uint8_t)serial; });
-    if (dead) return false;
+    uint32_t dv = 0;  // a covered variable (its pick is the entry's blocker: incremental passes)
+    fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) {
+        const bool c = b.fp_cov[v] == (uint8_t)serial;
+        if (c && !dead) dv = v;
+        dead |= c;
+    });
+    if (dead) {
+        if (b.fp_blocker) b.fp_blocker[i] = b.fp_covby[dv];
+        return false;
+    }
     const unsigned long long key = fp_key(b, ep, turn, i);
     fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) {
         if (hk && b.fp_hv[v] == stamp) fp_ht_claim(FpHotTable{hk, hv}, b.fp_owner, v, key);
@@ -3383,7 +3452,10 @@ __device__ __forceinline__ bool fp_join_one(const ClauseView& cv, const LoopBuff
         fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) { own &= b.fp_owner[v] == key; });
     }
     if (own) {
-        fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) { b.fp_cov[v] = (uint8_t)serial; });
+        fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) {
+            b.fp_cov[v] = (uint8_t)serial;
+            if (b.fp_covby) b.fp_covby[v] = i;
+        });
         b.fp_in[i] = (uint8_t)(b.fp_in[i] | 1u);
     }
     return !own && !pre;
@@ -3396,7 +3468,7 @@ template <uint32_t KW>
 __global__ __launch_bounds__(FP_THREADS) void k_fp_join0(ClauseView cv, LoopBuffers b) {
     constexpr uint32_t r = 0;
     RRFpCtl* ctl = b.fp_ctl;
-    if (ctl->state != FP_RUN) return;
+    if (ctl->state != FP_RUN || ctl->inc) return;  // (a full pass)
     const uint32_t nu = ctl->nu;
     __shared__ uint32_t s_cnt;
     const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
@@ -3437,7 +3509,7 @@ __device__ __forceinline__ uint32_t fp_wave_append(bool keep, uint32_t i, uint32
 template <uint32_t KW>
 __global__ __launch_bounds__(FP_THREADS) void k_fp_wclaim(ClauseView cv, LoopBuffers b, uint32_t r) {
     const RRFpCtl* ctl = b.fp_ctl;
-    if (ctl->state != FP_RUN) return;
+    if (ctl->state != FP_RUN || ctl->inc) return;  // (a full pass)
     const uint32_t nu = ctl->nu, lane = threadIdx.x & 63, wpb = FP_THREADS / 64;
     const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
     const uint32_t ntile = (nu + FP_RT - 1) / FP_RT;
@@ -3478,7 +3550,7 @@ template <uint32_t KW>
 __global__ __launch_bounds__(FP_THREADS) void k_fp_wjoin(ClauseView cv, LoopBuffers b, uint32_t r) {
     // (the last grid round's lists are compacted by k_fp_tail: no contended counter)
     RRFpCtl* ctl = b.fp_ctl;
-    if (ctl->state != FP_RUN) return;
+    if (ctl->state != FP_RUN || ctl->inc) return;  // (a full pass)
     const uint32_t nu = ctl->nu, lane = threadIdx.x & 63, wpb = FP_THREADS / 64;
     const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
     const uint32_t ntile = (nu + FP_RT - 1) / FP_RT;
@@ -3508,7 +3580,7 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_wjoin(ClauseView cv, LoopBuff
 template <uint32_t KW>
 __global__ __launch_bounds__(1024) void k_fp_tail(ClauseView cv, LoopBuffers b, uint32_t rg) {
     RRFpCtl* ctl = b.fp_ctl;
-    if (ctl->state != FP_RUN) return;
+    if (ctl->state != FP_RUN || ctl->inc) return;  // (a full pass)
     const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
     __shared__ uint32_t s_cnt, s_w[16];
     // the last grid round (rg - 1) left its survivors in per-tile lists (fp_list + tile * FP_RT,
@@ -3549,9 +3621,14 @@ __global__ __launch_bounds__(1024) void k_fp_tail(ClauseView cv, LoopBuffers b, 
                 fp_ent<KW>(b, U, i, a, v0);
                 const uint32_t sole = fp_sole_mask<KW>(b, i);
                 bool dead = false;
+                uint32_t dv = 0;
                 fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) {
-                    dead |= __hip_atomic_load(&b.fp_cov[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint8_t)serial;
+                    const bool c = __hip_atomic_load(&b.fp_cov[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint8_t)serial;
+                    if (c && !dead) dv = v;
+                    dead |= c;
                 });
+                if (dead && b.fp_blocker)
+                    b.fp_blocker[i] = __hip_atomic_load(&b.fp_covby[dv], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if (!dead) {
                     const unsigned long long key = fp_key(b, ep, b.fp_turn[i], i);
                     fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) { atomicMin(&b.fp_owner[v], key); });
@@ -3582,6 +3659,7 @@ __global__ __launch_bounds__(1024) void k_fp_tail(ClauseView cv, LoopBuffers b, 
                 });
                 if (own) {
                     fp_for_shared<KW>(cv, U, i, a, v0, sole, [&](uint32_t v) {
+                        if (b.fp_covby) __hip_atomic_store(&b.fp_covby[v], i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         __hip_atomic_store(&b.fp_cov[v], (uint8_t)serial, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     });
                     b.fp_in[i] = (uint8_t)(b.fp_in[i] | 1u);
@@ -3598,16 +3676,474 @@ __global__ __launch_bounds__(1024) void k_fp_tail(ClauseView cv, LoopBuffers b, 
     }
     if (threadIdx.x == 0) {
         ctl->ep_next = ep;
+        ctl->ran = 1;
         if (failed) ctl->state = FP_FAIL;
     }
 }
+
+// Incremental passes.  A pass takes the last pass's picks P (the LFMIS of the
+// last turns) to the LFMIS of the turns P implies.  The two differ only where the new turns change
+// the order of an entry and a pick below it: every entry out of P keeps a *blocker* (a pick below
+// it sharing a variable: the cover its full pass killed it by, or the pick its repair found), and
+// it stays out for certain while that blocker stays below it and in P.  So the pass
+//   * marks the entries whose blocker is no longer below them (k_fp_detect, every entry), then
+//   * re-decides them in Jacobi rounds (k_fp_repair, one workgroup): an entry is in iff no pick of
+//     the current decisions shares a variable with it and lies below it; a changed decision marks
+//     the entries above it that share a variable with it for the next round.
+// Decisions depend only on entries below, so the rounds end after the longest chain of changes
+// (at M: a few thousand entries in at most ~8 rounds per pass, against ~800k entries and ~10
+// kernels of a full pass).  Instances with hot variables keep the full passes (a hub's claimant
+// list would be scanned per decision).
+constexpr uint32_t FP_REP_CAP = 1u << 16;   // dirty entries per round before the pass gives up (a full pass follows)
+constexpr uint32_t FP_REP_QMAX = 1u << 20;  // entries whose decisions the repair keeps in LDS (128 KiB of bits):
+                                            // iterations with more violated clauses keep the full passes
+constexpr uint32_t FP_REP_MAXR = 4096;      // repair rounds per pass before it gives up
+
+__device__ __forceinline__ unsigned long long fp_order_key(const LoopBuffers& b, uint32_t i) {
+    return ((unsigned long long)b.fp_turn[i] << 32) | i;
+}
+
+__global__ __launch_bounds__(FP_THREADS) void k_fp_detect(LoopBuffers b) {
+    RRFpCtl* ctl = b.fp_ctl;
+    if (ctl->state != FP_RUN || !ctl->inc) return;
+    const uint32_t nu = ctl->nu, stamp = ctl->rep_serial;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // (the wide repair's counters, k_fp_repair_wide)
+        ctl->wlist = 0;
+        ctl->nlog = 0;
+        ctl->wrounds = 0;
+        ctl->wwork = 0;
+        ctl->wfail = 0;
+        ctl->wbar = 0;
+        ctl->wcnt[0] = ctl->wcnt[1] = ctl->wcnt[2] = 0;
+    }
+    for (uint32_t i0 = blockIdx.x * FP_THREADS; i0 < nu; i0 += gridDim.x * FP_THREADS) {
+        const uint32_t i = i0 + threadIdx.x;
+        bool d = false;
+        if (i < nu && !(b.fp_in[i] & 1u)) {
+            const uint32_t bk = b.fp_blocker[i];
+            d = bk >= nu || fp_order_key(b, bk) > fp_order_key(b, i);
+            if (d) b.fp_dmark[i] = stamp;
+        }
+        fp_append(d, i, &ctl->ndirty, b.fp_dl);  // (every lane of the wave calls it)
+    }
+}
+
+// The repair's view of an entry x: the claimant lists of its variables (fp_vlist; the entry's
+// list rows {start, length} in fp_lst) hold its neighbours y != x.  The first FP_RN list slots are
+// gathered into registers level by level for all lists at once -- list rows, list entries, then
+// turns and decisions (LDS bits) -- so a decision costs three dependent round trips, not a chain
+// per neighbour; an entry with more list slots (or wider than its rows) takes a rolled loop.  The
+// kernel is kept small on purpose: a single workgroup runs it, and code larger than the
+// instruction cache made every round several times slower.
+constexpr uint32_t FP_RN = 16;  // list slots gathered together (the entry itself included: ~99.9% of the
+                                // dirty entries at M; 12 left ~4% to the rolled form, which held up whole waves)
+
+// decision of entry y in the repair's LDS bits
+__device__ __forceinline__ uint32_t fp_q(const uint32_t* sq, uint32_t y) { return (sq[y >> 5] >> (y & 31u)) & 1u; }
+__device__ __forceinline__ unsigned long long fp_tkey(uint32_t t, uint32_t y) {
+    return ((unsigned long long)t << 32) | y;
+}
+
+template <uint32_t KW>
+__device__ __forceinline__ bool fp_rep_gather(const ClauseView& cv, const LoopBuffers& b, const RREnt* U, uint32_t x,
+                                              const uint32_t* sq, uint32_t (&id)[FP_RN], uint32_t (&tu)[FP_RN],
+                                              uint32_t& qmask) {
+    // the entry's list rows {start, length} (k_fp_bbuild; a slot whose variable the entry claims
+    // alone is a list of one: the entry itself)
+    constexpr uint32_t RW = KW == 4 ? 4u : 8u;
+    const uint32_t w = KW == 4 ? b.rr_k : U[x].a.z;
+    const uint4* rows = reinterpret_cast<const uint4*>(b.fp_lst) + (uint64_t)x * (RW / 2);
+    uint32_t so[RW], cn[RW];
+#pragma unroll
+    for (uint32_t h = 0; h < RW / 2; ++h) {
+        const uint4 r2 = rows[h];
+        so[2 * h] = r2.x;
+        cn[2 * h] = r2.y;
+        so[2 * h + 1] = r2.z;
+        cn[2 * h + 1] = r2.w;
+    }
+    if (w > RW) return false;
+    uint32_t tot = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < RW; ++k) {
+        if (k >= w) cn[k] = 0;
+        tot += cn[k];
+    }
+    if (tot > FP_RN) return false;
+#pragma unroll
+    for (uint32_t u = 0; u < FP_RN; ++u) {
+        uint32_t r = u, pos = 0;
+        bool found = false;
+#pragma unroll
+        for (uint32_t k = 0; k < RW; ++k) {
+            if (!found && r < cn[k]) {
+                pos = so[k] + r;
+                found = true;
+            } else if (!found) {
+                r -= cn[k];
+            }
+        }
+        id[u] = found ? b.fp_vlist[pos] : x;
+    }
+    qmask = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < FP_RN; ++u) {
+        tu[u] = id[u] != x ? b.fp_turn[id[u]] : 0u;
+        qmask |= (id[u] != x ? fp_q(sq, id[u]) : 0u) << u;
+    }
+    return true;
+}
+
+// the rolled form for the rare entries whose lists exceed the gather: f(y, turn of y) for every
+// neighbour y != x
+template <uint32_t KW, typename F>
+__device__ __forceinline__ void fp_rep_each(const ClauseView& cv, const LoopBuffers& b, const RREnt* U, uint32_t x,
+                                            F f) {
+    uint4 a, v0;
+    fp_ent<KW>(b, U, x, a, v0);
+    const uint32_t sole = fp_sole_mask<KW>(b, x);
+    fp_for_shared<KW>(cv, U, x, a, v0, sole, [&](uint32_t v) {
+        const uint32_t s0 = b.fp_soff[v], c = b.fp_vcnt[v];
+#pragma unroll 1
+        for (uint32_t q = 0; q < c; ++q) {
+            const uint32_t y = b.fp_vlist[s0 + q];
+            if (y != x) f(y, b.fp_turn[y]);
+        }
+    });
+}
+
+struct FpRepBlk {  // the rolled form's decision: a pick below x (~0u: none)
+    const uint32_t* sq;
+    unsigned long long kx;
+    uint32_t* bk;
+    __device__ void operator()(uint32_t y, uint32_t t) const {
+        if (fp_q(sq, y) && fp_tkey(t, y) < kx) *bk = y;
+    }
+};
+constexpr uint32_t FP_RH_BITS = 12;  // LDS dedupe table of a repair round (4096 entry ids)
+constexpr uint32_t FP_RL = 1024;     // dirty entries of a round kept in LDS (more: the global list; 128 + 16 + 8 KiB of LDS)
+
+// entry y into the next round's dirty list once: an LDS hash per round (the global round stamp
+// fp_dmark when its probe window is full); the list itself in LDS up to FP_RL entries, then global
+__device__ __forceinline__ void fp_rep_push(const LoopBuffers& b, uint32_t* hk, uint32_t* nb, uint32_t* lb,
+                                            uint32_t* gb, uint32_t y, uint32_t rid) {
+    uint32_t h = (y * 0x9E3779B1u) >> (32 - FP_RH_BITS);
+    bool fresh = false, found = false;
+#pragma unroll 1
+    for (int probe = 0; probe < 32 && !found; ++probe) {
+        const uint32_t prev = atomicCAS(&hk[h], 0xFFFFFFFFu, y);
+        fresh = prev == 0xFFFFFFFFu;
+        found = fresh || prev == y;
+        h = (h + 1) & ((1u << FP_RH_BITS) - 1u);
+    }
+    if (!found) fresh = atomicExch(&b.fp_dmark[y], rid) != rid;
+    if (!fresh) return;
+    const uint32_t i = atomicAdd(nb, 1u);
+    if (i < FP_RL) lb[i] = y;
+    else gb[i] = y;
+}
+struct FpRepUp {  // the rolled form's propagation: the neighbours above x into the next list
+    const LoopBuffers* b;
+    uint32_t *hk, *nb, *lb, *gb;
+    uint32_t rid;
+    unsigned long long kx;
+    __device__ void operator()(uint32_t y, uint32_t t) const {
+        if (fp_tkey(t, y) > kx) fp_rep_push(*b, hk, nb, lb, gb, y, rid);
+    }
+};
+
+// The large early rounds of a repair across FP_RW_GRID workgroups (a single CU's memory-level
+// parallelism bounds a round of thousands of decisions: ~34 us per 1,000 at M).  The decisions
+// live in the global bits fp_pbits (atomic updates; every round starts after a grid barrier whose
+// acquire fence drops stale L1 lines, within a round stale reads are allowed as in the one-
+// workgroup rounds), the lists in fp_dl, dedup by the round stamps fp_dmark.  The kernel stops
+// once a round holds at most FP_RW_MIN entries and hands the list, the change log and the round
+// stamp over to k_fp_repair; a grid barrier that times out (workgroups not all resident) hands
+// over as well, at a round boundary, so the result is the same either way.
+constexpr uint32_t FP_RW_GRID = 64;   // workgroups of the wide repair (one per CU, all resident)
+constexpr uint32_t FP_RW_MIN = 256;   // rounds this small are left to the one-workgroup repair
+constexpr unsigned long long FP_RW_TIMEOUT = 2000000ull;  // 20 ms at 100 MHz
+
+__device__ __forceinline__ bool fp_rw_barrier(RRFpCtl* ctl, uint32_t target) {
+    __shared__ uint32_t s_ok;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t ok = 1;
+        __threadfence();  // (release: this workgroup's decisions, log and list entries)
+        atomicAdd(&ctl->wbar, 1u);
+        const unsigned long long t0 = wall_now();
+        while (__hip_atomic_load(&ctl->wbar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            if (wall_now() - t0 > FP_RW_TIMEOUT) { ok = 0; break; }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        __threadfence();  // (acquire: the CU's L1 holds no line older than the barrier)
+        s_ok = ok;
+    }
+    __syncthreads();
+    return s_ok != 0;
+}
+
+// cnt (< 32) consecutive slots of a global list for each active lane: one atomic per wave
+// (thousands of lanes appending to one word serialise at the memory side otherwise); the lane's
+// offset in the wave's range from one ballot per bit of cnt.  Returns the lane's first slot.
+__device__ __forceinline__ uint32_t fp_wave_slots(uint32_t* ctr, uint32_t cnt) {
+    const uint32_t lane = threadIdx.x & 63;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    uint32_t excl = 0, tot = 0;
+#pragma unroll
+    for (uint32_t bit = 0; bit < 5; ++bit) {
+        const unsigned long long m = __ballot((cnt >> bit) & 1u);
+        excl += (uint32_t)__popcll(m & below) << bit;
+        tot += (uint32_t)__popcll(m) << bit;
+    }
+    const unsigned long long act = __ballot(true);
+    const uint32_t leader = (uint32_t)__ffsll((long long)act) - 1u;
+    uint32_t base = 0;
+    if (lane == leader && tot) base = atomicAdd(ctr, tot);
+    base = __shfl(base, (int)leader, 64);
+    return base + excl;
+}
+
+template <uint32_t KW>
+__global__ __launch_bounds__(FP_THREADS) void k_fp_repair_wide(ClauseView cv, LoopBuffers b) {
+    RRFpCtl* ctl = b.fp_ctl;
+    if (ctl->state != FP_RUN || !ctl->inc || ctl->nu > FP_REP_QMAX) return;
+    const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
+    uint32_t* Q = reinterpret_cast<uint32_t*>(b.fp_pbits);  // the decisions, a bit per entry
+    uint32_t* Lg = b.fp_dl + 2 * b.m;
+    const uint32_t G = gridDim.x;
+    uint32_t n = ctl->ndirty, rid = ctl->rep_serial, r = 0, cur = 0, work = 0;
+    bool ok = true;
+    while (n > FP_RW_MIN && n <= FP_REP_CAP && ok && r < FP_REP_MAXR) {
+        ++rid;
+        work += n;
+        const uint32_t* A = b.fp_dl + (size_t)cur * b.m;
+        uint32_t* B = b.fp_dl + (size_t)(cur ^ 1) * b.m;
+        uint32_t* nb = &ctl->wcnt[(r + 1) % 3];
+        if (blockIdx.x == 0 && threadIdx.x == 0) ctl->wcnt[(r + 2) % 3] = 0;  // (the round after next)
+        for (uint32_t j = blockIdx.x * FP_THREADS + threadIdx.x; j < n; j += G * FP_THREADS) {
+            const uint32_t x = A[j];
+            const unsigned long long kx = fp_order_key(b, x);
+            uint32_t id[FP_RN], tu[FP_RN], qm;
+            const bool all = fp_rep_gather<KW>(cv, b, U, x, Q, id, tu, qm);
+            uint32_t bk = ~0u;
+            if (all) {
+#pragma unroll
+                for (uint32_t u = 0; u < FP_RN; ++u)
+                    if (((qm >> u) & 1u) && id[u] != x && fp_tkey(tu[u], id[u]) < kx) bk = id[u];
+            } else {
+                fp_rep_each<KW>(cv, b, U, x, FpRepBlk{Q, kx, &bk});
+            }
+            const bool in = bk == ~0u;
+            if (!in) b.fp_blocker[x] = bk;
+            const bool ch = in != (fp_q(Q, x) != 0);
+            if (ch) {
+                if (in) atomicOr(&Q[x >> 5], 1u << (x & 31u));
+                else atomicAnd(&Q[x >> 5], ~(1u << (x & 31u)));
+            }
+            {
+                const uint32_t li = fp_wave_slots(&ctl->nlog, ch ? 1u : 0u);
+                if (ch && li < b.m) Lg[li] = x;  // (a longer log fails the pass: k_fp_repair checks nlog)
+            }
+            // the neighbours above a changed entry into the next round (once: the round stamp);
+            // the stamp exchanges all in flight together, then one list reservation per wave
+            if (all) {
+                uint32_t fresh = 0;
+#pragma unroll
+                for (uint32_t u = 0; u < FP_RN; ++u)
+                    if (ch && id[u] != x && fp_tkey(tu[u], id[u]) > kx)
+                        fresh |= (atomicExch(&b.fp_dmark[id[u]], rid) != rid ? 1u : 0u) << u;
+                uint32_t bi = fp_wave_slots(nb, (uint32_t)__popc(fresh));
+#pragma unroll
+                for (uint32_t u = 0; u < FP_RN; ++u)
+                    if ((fresh >> u) & 1u) B[bi++] = id[u];
+            } else if (ch) {
+                fp_rep_each<KW>(cv, b, U, x, [&](uint32_t y, uint32_t t) {
+                    if (fp_tkey(t, y) > kx && atomicExch(&b.fp_dmark[y], rid) != rid) B[atomicAdd(nb, 1u)] = y;
+                });
+            }
+        }
+        ++r;
+        ok = fp_rw_barrier(ctl, r * G);
+        if (!ok) break;  // (the round is complete on this workgroup; the others may not be: fail)
+        n = __hip_atomic_load(nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        cur ^= 1;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        ctl->wlist = cur;
+        ctl->ndirty = n;
+        ctl->rep_serial = rid;
+        ctl->wrounds = r;
+        ctl->wwork = work;
+        if (!ok) ctl->wfail = 1;
+    }
+}
+
+__device__ __forceinline__ void fp_sched_core(const LoopBuffers& b, RRFpCtl* ctl, int test, bool bail, uint32_t ch,
+                                              uint32_t tmin, uint32_t* s_off);
+
+// The end of an incremental pass: the rounds, then (as k_fp_count + k_fp_sched after a full
+// pass) the pass test and the next pass's schedule, in this same workgroup: the block pick counts
+// and the sets' in-block counts move by the pass's net changes only.
+template <uint32_t KW>
+__global__ __launch_bounds__(1024) void k_fp_repair(ClauseView cv, LoopBuffers b) {
+    RRFpCtl* ctl = b.fp_ctl;
+    const uint32_t state = ctl->state;
+    if (state == FP_FINAL) {  // (as k_fp_sched: the finalizing k_fp_turn has run)
+        if (threadIdx.x == 0) ctl->state = FP_DONE;
+        return;
+    }
+    if (state != FP_RUN) return;
+    if (!ctl->inc) {  // a full pass is due (one of the other kind in the graph): nothing to test
+        if (threadIdx.x == 0) ctl->skip = 1;
+        return;
+    }
+    const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
+    extern __shared__ uint32_t s_q[];  // the current decisions, a bit per entry
+    __shared__ uint32_t s_nb, s_nl;
+    __shared__ uint32_t s_hk[1u << FP_RH_BITS];
+    __shared__ uint32_t s_l[2][FP_RL];  // the rounds' dirty lists (their first FP_RL entries)
+    // global spill of the lists past FP_RL: index i of list c lives at s_l[c][i] or fp_dl[c m + i]
+    uint32_t* Lg = b.fp_dl + 2 * b.m;  // entries whose decision changed (with repeats)
+    const uint32_t nu = ctl->nu, nw = (nu + 31) / 32;
+    // (after the wide rounds: their list, change log, round stamp and statistics)
+    const uint32_t n0 = ctl->ndirty, wl = ctl->wlist;
+    uint32_t n = n0, rid = ctl->rep_serial, rounds = ctl->wrounds, work = ctl->wwork, cur = 0;
+    bool bail = nu > FP_REP_QMAX || ctl->wfail || ctl->nlog > b.m - FP_REP_CAP;
+    if (!bail) {
+        // the last pass's picks (packed by k_fp_turn) into LDS (8 loads in flight per thread: up
+        // to 2^20 entries in one step of the workgroup); k_fp_detect's list into the first list
+        const uint4* src = reinterpret_cast<const uint4*>(b.fp_pbits);
+        const uint32_t n4 = (nw + 3) / 4;
+        for (uint32_t q0 = 0; q0 < n4; q0 += 8 * blockDim.x) {
+            uint4 w[8];
+#pragma unroll
+            for (uint32_t u = 0; u < 8; ++u) {
+                const uint32_t q = q0 + u * blockDim.x + threadIdx.x;
+                w[u] = q < n4 ? src[q] : make_uint4(0u, 0u, 0u, 0u);
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < 8; ++u) {
+                const uint32_t q = q0 + u * blockDim.x + threadIdx.x;
+                const uint32_t e[4] = {w[u].x, w[u].y, w[u].z, w[u].w};
+#pragma unroll
+                for (uint32_t k = 0; k < 4; ++k)
+                    if (4 * q + k < nw) s_q[4 * q + k] = e[k];
+            }
+        }
+        // the list the wide rounds left (list wl of fp_dl) becomes list 0 (LDS part + global part)
+        const uint32_t* src_l = b.fp_dl + (size_t)wl * b.m;
+        for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) {
+            const uint32_t x = src_l[j];
+            if (j < FP_RL) s_l[0][j] = x;
+            else if (wl) b.fp_dl[j] = x;
+        }
+        if (threadIdx.x == 0) s_nl = ctl->nlog;
+    }
+    // Rounds over the dirty entries.  An entry's new decision is stored at once (the others of
+    // the round may read it or the old one): whatever it read, an entry is dirty again in the
+    // next round after any change of a neighbour below it, and decisions depend only on the
+    // entries below, so the rounds settle on the exact LFMIS (the lowest dirty entry is final
+    // after its first decision, and so on up).
+    while (n > 0 && !bail) {
+        if (n > FP_REP_CAP || rounds >= FP_REP_MAXR) { bail = true; break; }
+        ++rounds;
+        ++rid;
+        work += n;
+        for (uint32_t q = threadIdx.x; q < (1u << FP_RH_BITS); q += blockDim.x) s_hk[q] = 0xFFFFFFFFu;
+        if (threadIdx.x == 0) s_nb = 0;
+        __syncthreads();
+        const uint32_t* la = s_l[cur];
+        const uint32_t* ga = b.fp_dl + (size_t)cur * b.m;
+        uint32_t* lb = s_l[cur ^ 1];
+        uint32_t* gb = b.fp_dl + (size_t)(cur ^ 1) * b.m;
+        for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) {
+            const uint32_t x = j < FP_RL ? la[j] : ga[j];
+            const unsigned long long kx = fp_order_key(b, x);
+            uint32_t id[FP_RN], tu[FP_RN], qm;
+            const bool all = fp_rep_gather<KW>(cv, b, U, x, s_q, id, tu, qm);
+            uint32_t bk = ~0u;
+            if (all) {
+#pragma unroll
+                for (uint32_t u = 0; u < FP_RN; ++u)
+                    if (((qm >> u) & 1u) && id[u] != x && fp_tkey(tu[u], id[u]) < kx) bk = id[u];
+            } else {
+                fp_rep_each<KW>(cv, b, U, x, FpRepBlk{s_q, kx, &bk});
+            }
+            const bool in = bk == ~0u;
+            if (!in) b.fp_blocker[x] = bk;
+            if (in == (fp_q(s_q, x) != 0)) continue;
+            if (in) atomicOr(&s_q[x >> 5], 1u << (x & 31u));
+            else atomicAnd(&s_q[x >> 5], ~(1u << (x & 31u)));
+            Lg[atomicAdd(&s_nl, 1u)] = x;
+            // the neighbours above x are dirty in the next round
+            if (all) {
+#pragma unroll
+                for (uint32_t u = 0; u < FP_RN; ++u)
+                    if (id[u] != x && fp_tkey(tu[u], id[u]) > kx) fp_rep_push(b, s_hk, &s_nb, lb, gb, id[u], rid);
+            } else {
+                fp_rep_each<KW>(cv, b, U, x, FpRepUp{&b, s_hk, &s_nb, lb, gb, rid, kx});
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        n = s_nb;
+        if (s_nl > b.m - FP_REP_CAP) bail = true;  // (the change log is full: give up)
+        cur ^= 1;
+        __syncthreads();  // (the counters and the table are reset at the top of the next round)
+    }
+    // The net changes (logged entries whose decision differs from the last pass's, once each: a
+    // fresh round stamp) into bit 0 of fp_in, the block pick counts and the in-block counts of the
+    // set starts behind them in their block; then the test and the next schedule.
+    __shared__ uint32_t s_ch, s_tmin;
+    if (threadIdx.x == 0) { s_ch = 0; s_tmin = ~0u; }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (!bail) {
+        ++rid;
+        const uint32_t T = b.rr_T;
+        for (uint32_t j = threadIdx.x; j < s_nl; j += blockDim.x) {
+            const uint32_t x = Lg[j];
+            if (atomicExch(&b.fp_dmark[x], rid) == rid) continue;
+            const uint32_t q = fp_q(s_q, x), old = b.fp_in[x];
+            if (q == ((old >> 1) & 1u)) {  // (changed back: bit 0 is still the last pass's)
+                continue;
+            }
+            b.fp_in[x] = (uint8_t)((old & 0xFEu) | q);
+            const uint32_t d = q ? 1u : 0xFFFFFFFFu;  // (+1 / -1)
+            const uint32_t blk = x / FP_B;
+            atomicAdd(&b.fp_blk[blk], d);
+            for (uint32_t st = fp_set_of(b.fp_sf, T, x) + 1; st <= T && b.fp_sf[st] / FP_B == blk; ++st)
+                if (b.fp_sf[st] < ctl->nu) atomicAdd(&b.fp_bnd[st], d);
+            atomicAdd(&s_ch, 1u);
+            atomicMin(&s_tmin, b.fp_turn[x]);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        ctl->rep_serial = rid + 1;
+        ctl->rep_rounds += rounds;
+        if (bail) ctl->bail = 1;
+        if (b.fp_log && ctl->fp_iter < FP_LOG_PASSES) {
+            uint32_t* lg = b.fp_log + 4 * ctl->fp_iter;
+            lg[0] = n0;
+            lg[1] = bail ? 0xFFFFFFFFu : rounds;
+            lg[2] = work;
+            lg[3] = bail ? 0u : s_ch;
+        }
+    }
+    fp_sched_core(b, ctl, 1, bail, threadIdx.x == 0 ? s_ch : 0u, s_tmin, nullptr);
+}
+
 
 
 // Picks per block of FP_B entries, picks before every set start that falls in the block, and
 // (test) the picks that changed since the previous pass.
 __global__ __launch_bounds__(FP_THREADS) void k_fp_count(LoopBuffers b, int test) {
     RRFpCtl* ctl = b.fp_ctl;
-    if (ctl->state != FP_RUN) return;
+    if (ctl->state != FP_RUN || (test && !ctl->ran)) return;  // (no pass ran: nothing to test)
     __shared__ uint32_t s_w[FP_THREADS / 64], s_ex[FP_THREADS], s_bits[FP_THREADS];
     const uint32_t nu = ctl->nu, T = b.rr_T, nblk = (nu + FP_B - 1) / FP_B;
     uint32_t changed = 0, tmin = ~0u;
@@ -3655,28 +4191,18 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_count(LoopBuffers b, int test
 }
 
 // One workgroup: convergence, block offsets, picks per set, the schedule, the next pass.
-__global__ __launch_bounds__(256) void k_fp_sched(LoopBuffers b, int test) {
-    RRFpCtl* ctl = b.fp_ctl;
-    const uint32_t state = ctl->state;
-    if (state == FP_FINAL) {  // the finalizing k_fp_turn has run
-        if (threadIdx.x == 0) ctl->state = FP_DONE;
-        return;
-    }
-    if (state != FP_RUN) return;
+// The schedule of the next pass from the block pick counts (fp_blk) and the set starts' in-block
+// counts (fp_bnd), with the pass test: ch / tmin = this thread's share of the picks the pass
+// changed and their earliest turn (OR / min over the workgroup here).  One workgroup; k_fp_sched
+// (after k_fp_count) or the end of k_fp_repair (which updates the counts itself).  s_off: LDS
+// for the block offsets (FP_SCHED_LDS_BLK words) or nullptr.
+__device__ __forceinline__ void fp_sched_core(const LoopBuffers& b, RRFpCtl* ctl, int test, bool bail, uint32_t ch,
+                                              uint32_t tmin, uint32_t* s_off) {
     __shared__ uint32_t s_w[16], s_e0;
     __shared__ uint32_t s_n[FP_TMAX], s_nseg[FP_TMAX], s_pf[FP_TMAX + 1];
-    __shared__ uint32_t s_off[FP_SCHED_LDS_BLK];  // block offsets (when they fit)
     const uint32_t nu = ctl->nu, T = b.rr_T, nblk = (nu + FP_B - 1) / FP_B;
     uint32_t* blkoff = b.fp_blk + (b.m / FP_B + 2);
-    const bool lds_off = nblk <= FP_SCHED_LDS_BLK;
-    // every independent load first (one round trip): change counts and earliest changes, the
-    // first block counts, the set starts and their in-block pick counts
-    uint32_t ch = 0, tmin = ~0u;  // picks changed by the last pass, their earliest turn (per k_fp_count workgroup)
-    if (test)
-        for (uint32_t k = threadIdx.x; k < min(nblk, FP_COUNT_GRID); k += blockDim.x) {
-            ch += b.fp_blk[2 * (b.m / FP_B + 2) + k];
-            tmin = min(tmin, b.fp_blk[2 * (b.m / FP_B + 2) + FP_COUNT_GRID + k]);
-        }
+    const bool lds_off = s_off && nblk <= FP_SCHED_LDS_BLK;
     uint32_t sf[2], bnd[2];
     for (uint32_t q = 0; q < 2; ++q) {  // (T + 1 <= 2 * blockDim.x)
         const uint32_t s = threadIdx.x + q * blockDim.x;
@@ -3690,7 +4216,7 @@ __global__ __launch_bounds__(256) void k_fp_sched(LoopBuffers b, int test) {
     tmin = s_w[0];
     for (uint32_t w = 1; w < (blockDim.x >> 6); ++w) tmin = min(tmin, s_w[w]);
     __syncthreads();
-    const bool conv = test && ch == 0;
+    const bool conv = test && ch == 0 && !bail;
     // exclusive scan of the block counts: a contiguous range per thread (independent loads),
     // one workgroup scan of the range sums
     const uint32_t per = (nblk + blockDim.x - 1) / blockDim.x;
@@ -3858,8 +4384,14 @@ __global__ __launch_bounds__(256) void k_fp_sched(LoopBuffers b, int test) {
         // The next pass keeps the decisions below min(earliest changed turn, both schedules'
         // first erasure): there the turns did not change, so neither did the sub-problem.
         const uint32_t e0 = s_e0;
-        ctl->tpre = test ? min(tmin, min(e0, ctl->e0)) : 0u;
+        ctl->tpre = test && !bail ? min(tmin, min(e0, ctl->e0)) : 0u;
         ctl->e0 = e0;
+        // the next pass: incremental once a full pass has run (test), unless this one gave up
+        ctl->inc = test && b.fp_inc && !bail && nu <= FP_REP_QMAX && ctl->fp_iter + 1 >= b.fp_inc_after ? 1u : 0u;
+        ctl->bail = 0;
+        ctl->ndirty = 0;
+        ctl->ran = 0;
+        ctl->skip = 0;
         if (conv) {
             ctl->state = FP_FINAL;
             ctl->guess_num = total;
@@ -3873,11 +4405,38 @@ __global__ __launch_bounds__(256) void k_fp_sched(LoopBuffers b, int test) {
     }
 }
 
+// One workgroup after k_fp_count: convergence, block offsets, picks per set, the schedule, the
+// next pass.
+__global__ __launch_bounds__(256) void k_fp_sched(LoopBuffers b, int test) {
+    RRFpCtl* ctl = b.fp_ctl;
+    const uint32_t state = ctl->state;
+    if (state == FP_FINAL) {  // the finalizing k_fp_turn has run
+        if (threadIdx.x == 0) ctl->state = FP_DONE;
+        return;
+    }
+    if (state != FP_RUN) return;
+    if (test && !ctl->ran) {  // no pass ran (one of the other kind in the graph): nothing to test
+        if (threadIdx.x == 0) ctl->skip = 1;
+        return;
+    }
+    const bool bail = test && ctl->bail;  // the incremental pass gave up: its picks are no fixpoint test
+    __shared__ uint32_t s_off[FP_SCHED_LDS_BLK];  // block offsets (when they fit)
+    const uint32_t nblk = (ctl->nu + FP_B - 1) / FP_B;
+    // change counts and earliest changes of the k_fp_count workgroups
+    uint32_t ch = 0, tmin = ~0u;
+    if (test)
+        for (uint32_t k = threadIdx.x; k < min(nblk, FP_COUNT_GRID); k += blockDim.x) {
+            ch += b.fp_blk[2 * (b.m / FP_B + 2) + k];
+            tmin = min(tmin, b.fp_blk[2 * (b.m / FP_B + 2) + FP_COUNT_GRID + k]);
+        }
+    fp_sched_core(b, ctl, test, bail, ch, tmin, s_off);
+}
+
 // Turns of every block of entries (grid-stride) for the next pass, or (fin) the MIS: picks in
 // step order into tmis (step minus the erasures before it), their variables covered with the
 // iteration's stamp, and the statistics of k_rr_mw.  blk_off(blk): picks before block blk.
 template <uint32_t KW, typename BlkOff>
-__device__ __forceinline__ void fp_turn_blocks(const ClauseView& cv, const LoopBuffers& b, bool fin, uint32_t nu,
+__device__ __forceinline__ void fp_turn_blocks(const ClauseView& cv, const LoopBuffers& b, bool fin, bool inc, uint32_t nu,
                                                uint32_t T, uint32_t stamp, const uint32_t* s_sf,
                                                const uint32_t* s_pf, const uint32_t* s_nseg, const uint32_t* s_er,
                                                const uint4* segs, uint32_t* s_w, BlkOff blk_off) {
@@ -3893,8 +4452,12 @@ __device__ __forceinline__ void fp_turn_blocks(const ClauseView& cv, const LoopB
         const unsigned long long b0 = x & 0x0101010101010101ull;
         uint32_t tot;
         uint32_t P = blk_off(blk) + fp_block_scan((uint32_t)__popcll(b0), s_w, tot);
-        // the next pass sets bit 0 of its picks; these become bit 1 (k_fp_count compares them)
-        if (!fin && i0 < nu) *reinterpret_cast<unsigned long long*>(b.fp_in + i0) = b0 << 1;
+        // the next pass sets bit 0 of its picks; these become bit 1 (k_fp_count compares them); an
+        // incremental pass starts from them (bit 0 too) and repairs bit 0
+        if (!fin && i0 < nu) {
+            *reinterpret_cast<unsigned long long*>(b.fp_in + i0) = (b0 << 1) | (inc ? b0 : 0ull);
+            if (inc) b.fp_pbits[i0 / 8] = (uint8_t)((b0 * 0x0102040810204080ull) >> 56);  // (FP_PER == 8: a byte)
+        }
         if (i0 < nu) {
             uint32_t s = fp_set_of(s_sf, T, i0);
             const uint32_t e1 = min(nu - i0, FP_PER);
@@ -3971,6 +4534,7 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_turn(ClauseView cv, LoopBuffe
     const RRFpCtl* ctl = b.fp_ctl;
     const uint32_t state = ctl->state;
     if (state != FP_RUN && state != FP_FINAL) return;
+    if (state == FP_RUN && ctl->skip) return;  // (k_fp_sched found no pass to test)
     const bool fin = state == FP_FINAL;
     DevState* st = b.state;
     __shared__ uint32_t s_w[FP_THREADS / 64];
@@ -3988,7 +4552,7 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_turn(ClauseView cv, LoopBuffe
     if (lds_seg)
         for (uint32_t q = threadIdx.x; q < T * T; q += blockDim.x) s_seg[q] = b.fp_seg[q];
     __syncthreads();
-    fp_turn_blocks<KW>(cv, b, fin, nu, T, stamp, s_sf, s_pf, s_nseg, s_er, lds_seg ? s_seg : b.fp_seg, s_w,
+    fp_turn_blocks<KW>(cv, b, fin, ctl->inc != 0, nu, T, stamp, s_sf, s_pf, s_nseg, s_er, lds_seg ? s_seg : b.fp_seg, s_w,
                        [&](uint32_t blk) { return blkoff[blk]; });
     if (fin && blockIdx.x == 0 && threadIdx.x == 0) {
         st->tmis_cnt = ctl->total;
@@ -4063,6 +4627,10 @@ hipError_t prepare_kernels(const ClauseView& cv, const LoopBuffers& b) {
                                                        hipFuncAttributeMaxDynamicSharedMemorySize,
                                                        (int)std::max<size_t>(LDS_WORDS * 4 + 16, SCATTER_LDS_BYTES))));
         if (e != hipSuccess) return e;
+        ALLL_DISPATCH_K(cv.k, (e = hipFuncSetAttribute((const void*)k_eval_flags<(K > 0 ? K : 1)>,
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                       (int)(LDS_WORDS * 4 + 16))));
+        if (e != hipSuccess) return e;
         attr_mark(ATTR_HYBRID + cv.k, dev);
     }
     if (cv.rg_off && attr_pending(ATTR_RAGGED, dev)) {
@@ -4103,6 +4671,12 @@ hipError_t prepare_kernels(const ClauseView& cv, const LoopBuffers& b) {
             if (e == hipSuccess)
                 e = hipFuncSetAttribute((const void*)k_fp_bbuild, hipFuncAttributeMaxDynamicSharedMemorySize,
                                         160 * 1024 - 1024);
+            if (e == hipSuccess)
+                e = hipFuncSetAttribute((const void*)k_fp_repair<4>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)(FP_REP_QMAX / 8));
+            if (e == hipSuccess)
+                e = hipFuncSetAttribute((const void*)k_fp_repair<0>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        (int)(FP_REP_QMAX / 8));
             if (e != hipSuccess) return e;
             attr_mark(ATTR_FP, dev);
         }
@@ -4111,7 +4685,8 @@ hipError_t prepare_kernels(const ClauseView& cv, const LoopBuffers& b) {
 }
 
 hipError_t launch_eval_hybrid(const ClauseView& cv, const LoopBuffers& b, uint32_t tile_begin,
-                              uint32_t tile_end, bool gated, int n_blocks, bool scatter, hipStream_t s) {
+                              uint32_t tile_end, bool gated, int n_blocks, bool scatter, hipStream_t s, bool flags) {
+    if (flags && (scatter || !b.rr_flag)) return hipErrorInvalidValue;
     if (tile_end <= tile_begin) return hipSuccess;
     const uint32_t nt = tile_end - tile_begin;
     const dim3 grid(std::min<uint32_t>(nt, (uint32_t)std::max(1, n_blocks)));
@@ -4123,6 +4698,8 @@ hipError_t launch_eval_hybrid(const ClauseView& cv, const LoopBuffers& b, uint32
     if (cv.k < 1 || cv.k > (uint32_t)MAX_FIXED_K) return hipErrorInvalidValue;
     if (scatter) {
         ALLL_DISPATCH_K(cv.k, (k_eval_scatter<(K > 0 ? K : 1)><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g)));
+    } else if (flags) {
+        ALLL_DISPATCH_K(cv.k, (k_eval_flags<(K > 0 ? K : 1)><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g)));
     } else {
         ALLL_DISPATCH_K(cv.k, (k_eval_hybrid<(K > 0 ? K : 1)><<<grid, HYB_THREADS, lds, s>>>(cv, b, tile_begin, tile_end, g)));
     }
@@ -4254,13 +4831,14 @@ static void fp_turns(const ClauseView& cv, const LoopBuffers& b, const FpGrids& 
     else k_fp_turn<0><<<g.gb, FP_THREADS, 0, s>>>(cv, b);
 }
 
-hipError_t launch_rr_prep(const ClauseView& cv, const LoopBuffers& b, hipStream_t s) {
+hipError_t launch_rr_prep(const ClauseView& cv, const LoopBuffers& b, bool marked, hipStream_t s) {
     if (!b.rr_u || b.rr_T < 2 || b.rr_T > RR_TMAX) return hipErrorInvalidValue;
     if (b.rr_flag) {  // fixed width: violated flags in clause order from the evaluation's lists
         if (cv.k == 0 || !b.rr_tcnt) return hipErrorInvalidValue;
         const uint32_t gw = (b.n_tiles + 3) / 4;
         if (gw) {
-            ALLL_DISPATCH_K(cv.k, (k_rr_mark<(K > 0 ? K : 1)><<<gw, 256, 0, s>>>(cv, b)));
+            // (marked: the evaluation set the flags itself, k_eval_flags)
+            if (!marked) ALLL_DISPATCH_K(cv.k, (k_rr_mark<(K > 0 ? K : 1)><<<gw, 256, 0, s>>>(cv, b)));
             k_rr_count<<<gw, 256, 0, s>>>(b);
         }
     } else if (cv.k != 0) {
@@ -4274,8 +4852,7 @@ hipError_t launch_rr_prep(const ClauseView& cv, const LoopBuffers& b, hipStream_
     const FpGrids g = fp_grids(b);
     const size_t lds_bs = 8ull * b.n_bkt + 2ull * FP_BS_ENT * 8;
     const size_t lds_bb = fp_bbuild_lds_bytes(b.bkt_width);
-    k_fp_reset<<<(uint32_t)std::min<uint64_t>(((uint64_t)b.n_vars + 1023) / 1024 + 1, 2048), 256, 0, s>>>(b);
-    k_fp_begin<<<1, 256, 0, s>>>(b);
+    // (the iteration's start ran with the reduce: fp_begin_body; the owner / cover restart runs in k_fp_guess)
     const uint32_t gbs = (uint32_t)std::min<uint64_t>((b.m + FP_BS_ENT - 1) / FP_BS_ENT + 1, 512);
     if (g.narrow) k_fp_bscatter<4><<<gbs, FP_THREADS, lds_bs, s>>>(cv, b);
     else k_fp_bscatter<0><<<gbs, FP_THREADS, lds_bs, s>>>(cv, b);
@@ -4285,10 +4862,24 @@ hipError_t launch_rr_prep(const ClauseView& cv, const LoopBuffers& b, hipStream_
     return hipGetLastError();
 }
 
-hipError_t launch_rr_passes(const ClauseView& cv, const LoopBuffers& b, uint32_t n, hipStream_t s) {
+hipError_t launch_rr_passes(const ClauseView& cv, const LoopBuffers& b, uint32_t n, bool full, hipStream_t s) {
     if (!b.fp_ctl) return hipSuccess;
     const FpGrids g = fp_grids(b);
     for (uint32_t p = 0; p < n; ++p) {
+        if (b.fp_inc && !(full && p == 0)) {
+            // an incremental pass (its kernels run only when the device state asks for one)
+            k_fp_detect<<<g.gl, FP_THREADS, 0, s>>>(b);
+            const size_t lq = ((size_t)std::min<uint64_t>(b.m, FP_REP_QMAX) + 127) / 128 * 16;  // (uint4 rows)
+            const uint32_t gw = std::min<uint32_t>(FP_RW_GRID, std::max<uint32_t>(1, b.n_cu));  // (all resident)
+            if (g.narrow) k_fp_repair_wide<4><<<gw, FP_THREADS, 0, s>>>(cv, b);
+            else k_fp_repair_wide<0><<<gw, FP_THREADS, 0, s>>>(cv, b);
+            if (g.narrow) k_fp_repair<4><<<1, 1024, lq, s>>>(cv, b);
+            else k_fp_repair<0><<<1, 1024, lq, s>>>(cv, b);
+            // (the repair ran the pass test and the schedule: the turns follow)
+            if (g.narrow) k_fp_turn<4><<<g.gb, FP_THREADS, 0, s>>>(cv, b);
+            else k_fp_turn<0><<<g.gb, FP_THREADS, 0, s>>>(cv, b);
+            continue;
+        }
         // round 0: the claimant-list minima, then JOIN(0) (a workgroup per tile); rounds 1..:
         // a wave per tile.  (Instances with hot variables get FP_HEAVY_GRID more k_fp_vmin
         // workgroups for the long lists.)

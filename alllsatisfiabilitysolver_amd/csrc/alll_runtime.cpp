@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <cstdarg>
+#include <cstddef>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
@@ -108,8 +109,8 @@ struct alll_ctx {
     uint32_t rr_p = 8;
     std::vector<hipGraph_t> rr_graph;         // every captured round-robin graph (destroyed at the end)
     std::vector<hipGraphExec_t> rr_pre;       // [P]: evaluation .. set-up + P passes
-    hipGraphExec_t rr_more = nullptr, rr_post = nullptr;
-    uint32_t* h_fp = nullptr;                 // pinned copy of RRFpCtl {state, nu, fp_iter}
+    hipGraphExec_t rr_more = nullptr, rr_full = nullptr, rr_post = nullptr;
+    uint32_t* h_fp = nullptr;                 // pinned copy of RRFpCtl's first words {state, nu, fp_iter, .., inc}
     DevState* h_async = nullptr;  // pinned
     hipEvent_t ev_async = nullptr;
     bool async_pending = false;
@@ -325,9 +326,9 @@ int write_limits(alll_ctx* c, uint64_t limit_eval, uint64_t limit_nores) {
     return ALLL_OK;
 }
 
-hipError_t eval_launch(alll_ctx* c, uint32_t tb, uint32_t te, bool gated, bool scatter = false) {
+hipError_t eval_launch(alll_ctx* c, uint32_t tb, uint32_t te, bool gated, bool scatter = false, bool flags = false) {
     if (c->cv.rg_off) return launch_eval_ragged(c->cv, c->b, tb, te, gated, c->n_cu, c->stream);
-    if (c->hybrid) return launch_eval_hybrid(c->cv, c->b, tb, te, gated, c->n_cu, scatter, c->stream);
+    if (c->hybrid) return launch_eval_hybrid(c->cv, c->b, tb, te, gated, c->n_cu, scatter, c->stream, flags);
     return launch_eval(c->cv, c->b, tb, te, gated, c->stream);
 }
 
@@ -425,7 +426,7 @@ int enqueue_iteration(alll_ctx* c, hipEvent_t* marks, int variant) {
     const bool fused = variant == 1 && !xchg && !c->b.rr_T;
     if (!fused) HIP_TRY(launch_reduce(c->b, 0, s));
     if (c->b.rr_T) {  // (without the fixpoint passes: k_rr_mw decides every iteration)
-        HIP_TRY(launch_rr_prep(c->cv, c->b, s));
+        HIP_TRY(launch_rr_prep(c->cv, c->b, false, s));
         HIP_TRY(launch_rr_finish(c->cv, c->b, s));
     } else {
         const uint32_t rounds = variant == 2 ? 1u : c->grid_rounds;
@@ -460,9 +461,11 @@ int enqueue_iteration(alll_ctx* c, hipEvent_t* marks, int variant) {
 int enqueue_rr_piece(alll_ctx* c, hipEvent_t* marks, int piece, uint32_t passes) {
     hipStream_t s = c->stream;
     const bool xchg = c->world > 1 || c->comm;
+    // one GPU, hybrid evaluation: the evaluation writes the clause-order violated flags itself
+    const bool flags = !xchg && c->hybrid && c->b.rr_flag;
     if (piece == 0) {
         if (marks) HIP_TRY(hipEventRecord(marks[0], s));
-        HIP_TRY(eval_launch(c, c->own_begin, c->own_end, true));
+        HIP_TRY(eval_launch(c, c->own_begin, c->own_end, true, false, flags));
         if (marks) HIP_TRY(hipEventRecord(marks[1], s));
         if (xchg) {
             int rc = enqueue_exchange(c, s);
@@ -470,10 +473,10 @@ int enqueue_rr_piece(alll_ctx* c, hipEvent_t* marks, int piece, uint32_t passes)
         }
         if (marks) HIP_TRY(hipEventRecord(marks[2], s));
         HIP_TRY(launch_reduce(c->b, 0, s));
-        HIP_TRY(launch_rr_prep(c->cv, c->b, s));
-        HIP_TRY(launch_rr_passes(c->cv, c->b, passes, s));
-    } else if (piece == 1) {
-        HIP_TRY(launch_rr_passes(c->cv, c->b, passes, s));
+        HIP_TRY(launch_rr_prep(c->cv, c->b, flags, s));
+        HIP_TRY(launch_rr_passes(c->cv, c->b, passes, true, s));
+    } else if (piece == 1 || piece == 3) {  // one incremental (1) or full (3) pass
+        HIP_TRY(launch_rr_passes(c->cv, c->b, passes, piece == 3, s));
     } else {
         HIP_TRY(launch_rr_finish(c->cv, c->b, s));
         if (marks) HIP_TRY(hipEventRecord(marks[3], s));
@@ -497,7 +500,8 @@ int enqueue_rr_piece(alll_ctx* c, hipEvent_t* marks, int piece, uint32_t passes)
 // captured once per (piece, passes); nullptr when the loop launches eagerly
 int rr_graph_of(alll_ctx* c, int piece, uint32_t passes, hipGraphExec_t* out) {
     *out = nullptr;
-    hipGraphExec_t* slot = piece == 0 ? &c->rr_pre[passes] : piece == 1 ? &c->rr_more : &c->rr_post;
+    hipGraphExec_t* slot = piece == 0 ? &c->rr_pre[passes] : piece == 1 ? &c->rr_more : piece == 3 ? &c->rr_full
+                                                                                               : &c->rr_post;
     if (!c->use_graph) return ALLL_OK;
     if (*slot) { *out = *slot; return ALLL_OK; }
     hipError_t e = hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal);
@@ -543,19 +547,23 @@ int launch_rr_piece(alll_ctx* c, hipEvent_t* marks, int piece, uint32_t passes) 
     return enqueue_rr_piece(c, marks, piece, passes);
 }
 
-// One round-robin iteration with host-driven passes: pre(rr_p), then one pass at a time while
-// the pass state (read back) is still running, at most fp_max in all, then post.  The host
-// reads 12 bytes per decision instead of the GPU running passes after convergence.
+// One round-robin iteration with host-driven passes: pre(rr_p) (a full pass, then incremental
+// ones), then one pass at a time while the pass state (read back) is still running -- an
+// incremental one, or a full one after an incremental pass gave up -- at most fp_max in all, then
+// post.  The host reads the pass state per decision instead of the GPU running passes after
+// convergence.
 int launch_rr_iteration(alll_ctx* c, hipEvent_t* marks) {
     const uint32_t cap = c->b.fp_max;
     uint32_t done = std::min(c->rr_p, cap);
     int rc;
     if ((rc = launch_rr_piece(c, marks, 0, done))) return rc;
+    constexpr size_t ctl_words = offsetof(RRFpCtl, inc) / 4 + 1;  // {state, nu, fp_iter, ..., inc}
     for (;;) {
-        HIP_TRY(hipMemcpyAsync(c->h_fp, c->b.fp_ctl, 12, hipMemcpyDeviceToHost, c->stream));
+        HIP_TRY(hipMemcpyAsync(c->h_fp, c->b.fp_ctl, ctl_words * 4, hipMemcpyDeviceToHost, c->stream));
         HIP_TRY(hipStreamSynchronize(c->stream));
         if (c->h_fp[0] != FP_RUN || done >= cap) break;
-        if ((rc = launch_rr_piece(c, marks, 1, 1))) return rc;
+        const bool inc = c->h_fp[offsetof(RRFpCtl, inc) / 4] != 0;
+        if ((rc = launch_rr_piece(c, marks, inc ? 1 : 3, 1))) return rc;
         ++done;
     }
     // next iteration: the passes this one needed (fp_iter = passes that changed the picks)
@@ -974,7 +982,23 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
                 b.fp_max = (uint32_t)std::max(1, std::min(250, atoi(e)));
             c->rr_p = std::min<uint32_t>(c->rr_p, b.fp_max);
             c->rr_pre.assign(b.fp_max + 1, nullptr);
-            if (hipHostMalloc((void**)&c->h_fp, 16, 0) != hipSuccess) return bail(fail(ALLL_ERR_OOM, "hipHostMalloc failed"));
+            if (hipHostMalloc((void**)&c->h_fp, sizeof(RRFpCtl), 0) != hipSuccess)
+                return bail(fail(ALLL_ERR_OOM, "hipHostMalloc failed"));
+            // incremental passes on instances without hot variables
+            // (ALLL_RR_INC=0: full passes only; tests, A/B)
+            bool inc = n_hot == 0;
+            if (const char* e = getenv("ALLL_RR_INC")) inc = inc && atoi(e) != 0;
+            if (inc) {
+                if ((rc = dalloc(c, &b.fp_blocker, m + 1, 0xFF)) || (rc = dalloc(c, &b.fp_covby, (size_t)prob->n_vars + 1)) ||
+                    (rc = dalloc(c, &b.fp_vcnt, (size_t)prob->n_vars + 1)) || (rc = dalloc(c, &b.fp_dl, 3 * (size_t)m + 16 * std::min<size_t>(m, 1u << 16) + 64)) ||
+                    (rc = dalloc(c, &b.fp_dmark, m + 1)) || (rc = dalloc(c, &b.fp_pbits, m / 8 + 64)) ||
+                    (rc = dalloc(c, &b.fp_log, 4 * FP_LOG_PASSES)) ||
+                    (rc = dalloc(c, &b.fp_lst, 2 * (size_t)m * ((rr_width >= 1 && rr_width <= 4) ? 4 : 8) + 16)))
+                    return bail(rc);
+                b.fp_inc = 1;
+                b.fp_inc_after = 1;
+                if (const char* e = getenv("ALLL_RR_INC_AFTER")) b.fp_inc_after = (uint32_t)std::max(1, atoi(e));
+            }
         }
     }
     if ((rc = dalloc(c, &b.A, b.n_words + 4))) return bail(rc);  // +4: 16-byte tail loads
@@ -1391,6 +1415,7 @@ int alll_destroy(alll_ctx* c) {
     for (auto& g : c->rr_pre)
         if (g) (void)hipGraphExecDestroy(g);
     if (c->rr_more) (void)hipGraphExecDestroy(c->rr_more);
+    if (c->rr_full) (void)hipGraphExecDestroy(c->rr_full);
     if (c->rr_post) (void)hipGraphExecDestroy(c->rr_post);
     for (auto g : c->rr_graph) (void)hipGraphDestroy(g);
     if (c->h_fp) (void)hipHostFree(c->h_fp);
@@ -1722,6 +1747,17 @@ uint64_t alll_eval_bytes(alll_ctx* c) {
 }
 
 int alll_layout(alll_ctx* c) { return c ? (int)c->cv.k : -1; }
+
+int alll_rr_pass_log(alll_ctx* c, uint32_t* out, uint32_t n_words) {
+    if (!c || (!out && n_words)) return fail(ALLL_ERR_INVALID_ARG, "null argument");
+    HIP_TRY(hipSetDevice(c->device));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    const uint32_t have = c->b.fp_log ? 4 * FP_LOG_PASSES : 0;
+    const uint32_t nw = std::min(n_words, have);
+    if (nw) HIP_TRY(hipMemcpy(out, c->b.fp_log, nw * 4ull, hipMemcpyDeviceToHost));
+    for (uint32_t i = nw; i < n_words; ++i) out[i] = 0;
+    return (int)nw;
+}
 
 int alll_comm_size(alll_ctx* c) {
     if (!c) return -1;

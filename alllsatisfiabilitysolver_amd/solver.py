@@ -261,6 +261,15 @@ class Solver:
         r = int(self._L.alll_uses_graphs(self._ctx, ctypes.byref(why)))
         return r == 1, (why.value or b"").decode()
 
+    def rr_pass_log(self):
+        """Round robin: per pass of the last iteration (dirty entries, repair rounds, entries
+        decided, decisions changed) of its incremental passes (measurement)."""
+        out = np.zeros(256, np.uint32)
+        n = self._L.alll_rr_pass_log(self._ctx, _p(out, _u32p), out.size)
+        if n < 0:
+            N.check(n, "rr_pass_log")
+        return out[:n].reshape(-1, 4)
+
     def comm_size(self) -> int:
         """Ranks in the solve: the RCCL communicator's count (or world with a host exchange)."""
         n = int(self._L.alll_comm_size(self._ctx))

@@ -203,6 +203,11 @@ const char* alll_eval_kernel(alll_ctx* ctx);
  * eager launches with the same results); *why (may be NULL) names the reason.  -1: null ctx.
  * (No reference counterpart: measurement honesty of the benchmark) */
 int alll_uses_graphs(alll_ctx* ctx, const char** why);
+/* Round robin (n_threads > 1): the pass log of the last iteration, 4 words per pass {dirty
+ * entries, repair rounds (0xFFFFFFFF: the incremental pass gave up), entries decided, decisions
+ * changed} for the incremental passes (zeros for full ones), at most 64 passes; returns the words
+ * written (0 without incremental passes).  (No reference counterpart: measurement) */
+int alll_rr_pass_log(alll_ctx* ctx, uint32_t* out, uint32_t n_words);
 /* Ranks taking part in the clause-sharded solve: ncclCommCount of the RCCL communicator, or
  * alll_options.world with a host-staged exchange (1 on one GPU); -1 on failure.  (The
  * reference counterpart is the thread count of the -p path, example/main.cpp:76-84.) */

@@ -12,7 +12,7 @@ starts = [i for i, s in enumerate(seq) if s[0].startswith("k_eval")]
 i0 = starts[-1]
 line, tot, t_first = [], 0.0, seq[i0][2]
 for n, d, t in seq[i0:]:
-    if n.startswith("k_fp_vmin") and line:
+    if (n.startswith("k_fp_vmin") or n.startswith("k_fp_detect")) and line:
         print(f"{tot:7.1f} | " + " ".join(line))
         line, tot = [], 0.0
     line.append(f"{n.replace('k_fp_', '').replace('<4u>', '')}:{d:.1f}")

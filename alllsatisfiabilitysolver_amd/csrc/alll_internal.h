@@ -61,6 +61,11 @@ constexpr uint32_t FP_G_HOT = 6;   // ... on instances with hot variables (5, 7,
 constexpr uint32_t FP_G_MAX = FP_G_HOT > FP_G ? FP_G_HOT : FP_G;
 constexpr uint32_t FP_MAX_DEFAULT = 64;    // LFMIS passes per iteration before k_rr_mw decides it
 constexpr uint32_t FP_LOG_PASSES = 64;     // passes of an iteration in the pass log (fp_log)
+constexpr uint32_t FP_LOG_RW = 64;         // words per pass of the timing log behind it: {detect, wide, repair,
+                                           //   rounds end, repair end, LDS loaded, schedule, phases} clock
+                                           //   stamps, {round entries, stamp} pairs (24 rounds), then the
+                                           //   first 4 wide rounds' pre-barrier stamps (words 56, 58, 60, 62)
+constexpr uint32_t FP_LOG_WORDS = 4 * FP_LOG_PASSES + FP_LOG_RW * FP_LOG_PASSES;
 enum : uint32_t { FP_RUN = 0, FP_FINAL = 1, FP_DONE = 2, FP_OFF = 3, FP_FAIL = 4 };
 struct RRFpCtl {
     uint32_t state;      // FP_*: RUN iterating; FINAL the last pass converged (finalize now);
@@ -96,12 +101,13 @@ struct RRFpCtl {
     uint32_t restart;    // iteration start: bit 0 the owner epochs restart (fp_owner cleared), bit 1 the
                          // cover serials (fp_cov cleared) -- decided with the reduce, done by k_fp_guess
     // the wide repair (k_fp_repair_wide, the large early rounds across workgroups) hands over to
-    // the one-workgroup repair: the list (wlist: 0 / 1 of fp_dl, ndirty entries), the change log
-    // length (nlog), the rounds and entries decided; its grid barrier and round counters
-    uint32_t wlist, nlog, wrounds, wwork, wfail;
+    // the one-workgroup repair: the list (wlist: 0 / 1 of fp_dl, ndirty entries), the rounds and
+    // entries decided; its grid barrier
+    uint32_t wlist, wrounds, wwork, wfail;
     uint32_t wbar;
-    uint32_t wcnt[3];
-    uint32_t spare[1];
+    uint32_t pbsrc;      // the last pass was incremental: its picks are the bits fp_pbits (k_fp_turn reads
+                         // them there), not bit 0 of fp_in
+    uint32_t spare[4];
 };
 static_assert(sizeof(RRFpCtl) == 128, "RRFpCtl: 32 words");
 // In-loop kernel timing (ALLL_FLAG_KERNEL_TIMING): per iteration i, slot i % TIME_SLOTS holds
@@ -280,10 +286,12 @@ struct LoopBuffers {
     uint32_t* fp_dl;            // 3 x m + 16 min(m, 2^16): the repair's dirty lists (two), its change log and
                                 //   its raw push list
     uint32_t* fp_dmark;         // per scan entry: repair round stamp of its last dirty-list insertion
-    uint8_t* fp_pbits;          // the picks of the last pass, a bit per scan entry (k_fp_turn; the repair
-                                //   keeps them in LDS)
+    uint8_t* fp_pbits;          // 2 x (m / 8 + 80) bytes: the picks, a bit per scan entry -- the working copy
+                                //   (k_fp_turn writes it, the wide repair updates it, the repair keeps it in LDS
+                                //   and writes its result back) and the last pass's picks behind it
     uint32_t* fp_log;           // FP_LOG_PASSES x 4: per pass of the current iteration {dirty entries, repair
-                                //   rounds, entries decided, changes} (alll_rr_pass_log; measurement)
+                                //   rounds, entries decided, changes}, then the timing log (FP_LOG_RW per
+                                //   pass; alll_rr_pass_log; measurement)
     uint32_t fp_inc;            // incremental passes enabled (no hot variables)
     uint32_t fp_inc_after;      // full passes of an iteration before the incremental ones
     uint32_t fp_ib, fp_tb;      // key bits of the entry index and of the turn

@@ -68,6 +68,34 @@ __device__ __forceinline__ uint32_t abit(const uint32_t* __restrict__ A, uint32_
 // the compiler may not sink a load past it, so the loads are in flight together (no wait).
 __device__ __forceinline__ void spec_fence() { asm volatile("" ::: "memory"); }
 
+// Wave-wide (64 lanes, all active) reductions and scans by DPP moves: a few cycles per step
+// where a shuffle (ds_bpermute) costs an LDS round trip.  dpp<CTRL, ROWS>(v, old): v moved by the
+// DPP control CTRL in the rows ROWS, old where a lane has no source (or its row is masked off).
+template <int CTRL, int ROWS = 0xF>
+__device__ __forceinline__ uint32_t dpp(uint32_t v, uint32_t old) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, ROWS, 0xF, false);
+}
+// the minimum over the wave, in every lane
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+    v = min(v, dpp<0xB1>(v, v));        // quad_perm [1,0,3,2]
+    v = min(v, dpp<0x4E>(v, v));        // quad_perm [2,3,0,1]
+    v = min(v, dpp<0x124>(v, v));       // row_ror:4
+    v = min(v, dpp<0x128>(v, v));       // row_ror:8: every lane holds its row's minimum
+    v = min(v, dpp<0x142, 0xA>(v, v));  // row_bcast:15 into rows 1, 3
+    v = min(v, dpp<0x143, 0xC>(v, v));  // row_bcast:31 into rows 2, 3: lane 63 holds the minimum
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+// inclusive prefix sum over the wave's lanes
+__device__ __forceinline__ uint32_t wave_incl_add(uint32_t v) {
+    v += dpp<0x111>(v, 0u);        // row_shr:1
+    v += dpp<0x112>(v, 0u);        // row_shr:2
+    v += dpp<0x114>(v, 0u);        // row_shr:4
+    v += dpp<0x118>(v, 0u);        // row_shr:8: prefix within the row
+    v += dpp<0x142, 0xA>(v, 0u);   // row_bcast:15: row 0's total into row 1, row 2's into row 3
+    v += dpp<0x143, 0xC>(v, 0u);   // row_bcast:31: rows 0 + 1 into rows 2, 3
+    return v;
+}
+
 __device__ __forceinline__ bool eval_gate_closed(const DevState* st) {
     return st->done != 0 || st->n_iter >= st->limit_eval;
 }
@@ -1060,7 +1088,7 @@ __device__ void fp_begin_body(const LoopBuffers& b) {
     for (uint32_t s = threadIdx.x; s <= T; s += blockDim.x)
         if (s == T || b.rr_sets[s] >= b.m) b.fp_sf[s] = nu;
     if (b.fp_log)
-        for (uint32_t q = threadIdx.x; q < 4 * FP_LOG_PASSES; q += blockDim.x) b.fp_log[q] = 0;
+        for (uint32_t q = threadIdx.x; q < FP_LOG_WORDS; q += blockDim.x) b.fp_log[q] = 0;
     if (threadIdx.x == 0) {
         const bool ep0 = fp_ep_restart(b, ctl), ser0 = fp_serial_restart(b, ctl);
         ctl->restart = (ep0 ? 1u : 0u) | (ser0 ? 2u : 0u);
@@ -1075,6 +1103,7 @@ __device__ void fp_begin_body(const LoopBuffers& b) {
         ctl->e0 = ~0u;
         ctl->nheavy = 0;
         ctl->inc = 0;  // (the first pass is a full one)
+        ctl->pbsrc = 0;
         ctl->bail = 0;
         ctl->ran = 0;
         ctl->skip = 0;
@@ -2277,11 +2306,7 @@ static_assert(sizeof(RREnt) == 16 + 4 * RR_KE, "scan entry = header + RR_KE vari
 // Workgroup exclusive scan of one value per thread (blockDim.x <= 1024); returns the total too.
 __device__ __forceinline__ uint32_t fp_block_scan(uint32_t x, uint32_t* s_w, uint32_t& total) {
     const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-    uint32_t incl = x;
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(incl, o, 64);
-        if ((int)lane >= o) incl += y;
-    }
+    const uint32_t incl = wave_incl_add(x);
     if (lane == 63) s_w[wave] = incl;
     __syncthreads();
     uint32_t before = 0;
@@ -3703,18 +3728,28 @@ __device__ __forceinline__ unsigned long long fp_order_key(const LoopBuffers& b,
     return ((unsigned long long)b.fp_turn[i] << 32) | i;
 }
 
+// the timing log of pass p (FP_LOG_RW words; nullptr past FP_LOG_PASSES) and its round records
+__device__ __forceinline__ uint32_t* fp_tlog(const LoopBuffers& b, uint32_t p) {
+    return b.fp_log && p < FP_LOG_PASSES ? b.fp_log + 4 * FP_LOG_PASSES + FP_LOG_RW * p : nullptr;
+}
+__device__ __forceinline__ void fp_tround(uint32_t* t, uint32_t r, uint32_t n) {
+    if (t && r < FP_LOG_RW / 2 - 8) {
+        t[8 + 2 * r] = n;
+        t[9 + 2 * r] = (uint32_t)wall_now();
+    }
+}
+
 __global__ __launch_bounds__(FP_THREADS) void k_fp_detect(LoopBuffers b) {
     RRFpCtl* ctl = b.fp_ctl;
     if (ctl->state != FP_RUN || !ctl->inc) return;
     const uint32_t nu = ctl->nu, stamp = ctl->rep_serial;
     if (blockIdx.x == 0 && threadIdx.x == 0) {  // (the wide repair's counters, k_fp_repair_wide)
+        if (uint32_t* t = fp_tlog(b, ctl->fp_iter)) t[0] = (uint32_t)wall_now();
         ctl->wlist = 0;
-        ctl->nlog = 0;
         ctl->wrounds = 0;
         ctl->wwork = 0;
         ctl->wfail = 0;
         ctl->wbar = 0;
-        ctl->wcnt[0] = ctl->wcnt[1] = ctl->wcnt[2] = 0;
     }
     for (uint32_t i0 = blockIdx.x * FP_THREADS; i0 < nu; i0 += gridDim.x * FP_THREADS) {
         const uint32_t i = i0 + threadIdx.x;
@@ -3729,50 +3764,59 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_detect(LoopBuffers b) {
 }
 
 // The repair's view of an entry x: the claimant lists of its variables (fp_vlist; the entry's
-// list rows {start, length} in fp_lst) hold its neighbours y != x.  The first FP_RN list slots are
-// gathered into registers level by level for all lists at once -- list rows, list entries, then
-// turns and decisions (LDS bits) -- so a decision costs three dependent round trips, not a chain
-// per neighbour; an entry with more list slots (or wider than its rows) takes a rolled loop.  The
-// kernel is kept small on purpose: a single workgroup runs it, and code larger than the
-// instruction cache made every round several times slower.
-constexpr uint32_t FP_RN = 16;  // list slots gathered together (the entry itself included: ~99.9% of the
-                                // dirty entries at M; 12 left ~4% to the rolled form, which held up whole waves)
+// list rows {start, length} in fp_lst) hold its neighbours y != x.  A group of FP_RN lanes decides
+// one entry: lane u takes slot u of the concatenated lists, so a decision is three dependent
+// round trips (the list rows and x's turn, the list slot, its turn and decision) and a few dozen
+// instructions per lane; the rare entry with more slots (or wider than its rows) has its group
+// stride every list in turn.  (One lane per entry with all FP_RN slots unrolled ran ~4x the
+// instructions: a one-entry round took ~5 us.)
+constexpr uint32_t FP_RN = 16;  // lanes per entry (the entry's own slots included: ~99.9% of the dirty
+                                // entries at M fit)
 
-// decision of entry y in the repair's LDS bits
+// decision of entry y in the repair's bits
 __device__ __forceinline__ uint32_t fp_q(const uint32_t* sq, uint32_t y) { return (sq[y >> 5] >> (y & 31u)) & 1u; }
 __device__ __forceinline__ unsigned long long fp_tkey(uint32_t t, uint32_t y) {
     return ((unsigned long long)t << 32) | y;
 }
 
-template <uint32_t KW>
-__device__ __forceinline__ bool fp_rep_gather(const ClauseView& cv, const LoopBuffers& b, const RREnt* U, uint32_t x,
-                                              const uint32_t* sq, uint32_t (&id)[FP_RN], uint32_t (&tu)[FP_RN],
-                                              uint32_t& qmask) {
-    // the entry's list rows {start, length} (k_fp_bbuild; a slot whose variable the entry claims
-    // alone is a list of one: the entry itself)
+// One entry per group of FP_RN lanes (x == ~0u: an idle group; every lane of the wave calls it).
+// Decides x against the current decisions (pol.q), records its blocker, stores a changed
+// decision (pol.set) and pushes the neighbours above a changed entry
+// (pol.push, pol.push1: the next round's list).  Policies: FpPolLds (one workgroup, LDS bits and
+// lists), FpPolWide (the wide rounds, global bits).
+template <uint32_t KW, typename P>
+__device__ __forceinline__ void fp_grp_step(const ClauseView& cv, const LoopBuffers& b, const RREnt* U, uint32_t x,
+                                            P& pol) {
     constexpr uint32_t RW = KW == 4 ? 4u : 8u;
-    const uint32_t w = KW == 4 ? b.rr_k : U[x].a.z;
-    const uint4* rows = reinterpret_cast<const uint4*>(b.fp_lst) + (uint64_t)x * (RW / 2);
-    uint32_t so[RW], cn[RW];
+    const uint32_t lane = threadIdx.x & 63, gl = lane & (FP_RN - 1), g0 = lane & ~(FP_RN - 1);
+    const bool act = x != ~0u;
+    unsigned long long kx = 0;
+    uint32_t w = 0, tot = 0, so[RW], cn[RW];
 #pragma unroll
-    for (uint32_t h = 0; h < RW / 2; ++h) {
-        const uint4 r2 = rows[h];
-        so[2 * h] = r2.x;
-        cn[2 * h] = r2.y;
-        so[2 * h + 1] = r2.z;
-        cn[2 * h + 1] = r2.w;
+    for (uint32_t k = 0; k < RW; ++k) so[k] = cn[k] = 0;
+    if (act) {
+        kx = fp_tkey(b.fp_turn[x], x);
+        w = KW == 4 ? b.rr_k : U[x].a.z;
+        const uint4* rows = reinterpret_cast<const uint4*>(b.fp_lst) + (uint64_t)x * (RW / 2);
+#pragma unroll
+        for (uint32_t h = 0; h < RW / 2; ++h) {
+            const uint4 r2 = rows[h];
+            so[2 * h] = r2.x;
+            cn[2 * h] = r2.y;
+            so[2 * h + 1] = r2.z;
+            cn[2 * h + 1] = r2.w;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < RW; ++k) {
+            if (k >= w) cn[k] = 0;
+            tot += cn[k];
+        }
     }
-    if (w > RW) return false;
-    uint32_t tot = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < RW; ++k) {
-        if (k >= w) cn[k] = 0;
-        tot += cn[k];
-    }
-    if (tot > FP_RN) return false;
-#pragma unroll
-    for (uint32_t u = 0; u < FP_RN; ++u) {
-        uint32_t r = u, pos = 0;
+    const bool fast = act && w <= RW && tot <= FP_RN, slow = act && !fast;
+    // fast: slot gl of the lists
+    uint32_t y = ~0u;
+    if (fast && gl < tot) {
+        uint32_t r = gl, pos = 0;
         bool found = false;
 #pragma unroll
         for (uint32_t k = 0; k < RW; ++k) {
@@ -3783,50 +3827,57 @@ __device__ __forceinline__ bool fp_rep_gather(const ClauseView& cv, const LoopBu
                 r -= cn[k];
             }
         }
-        id[u] = found ? b.fp_vlist[pos] : x;
+        y = b.fp_vlist[pos];
     }
-    qmask = 0;
-#pragma unroll
-    for (uint32_t u = 0; u < FP_RN; ++u) {
-        tu[u] = id[u] != x ? b.fp_turn[id[u]] : 0u;
-        qmask |= (id[u] != x ? fp_q(sq, id[u]) : 0u) << u;
+    bool below = false, above = false;
+    if (y != ~0u && y != x) {
+        const unsigned long long ky = fp_tkey(b.fp_turn[y], y);
+        below = ky < kx && pol.q(y);
+        above = ky > kx;
     }
-    return true;
-}
-
-// the rolled form for the rare entries whose lists exceed the gather: f(y, turn of y) for every
-// neighbour y != x
-template <uint32_t KW, typename F>
-__device__ __forceinline__ void fp_rep_each(const ClauseView& cv, const LoopBuffers& b, const RREnt* U, uint32_t x,
-                                            F f) {
-    uint4 a, v0;
-    fp_ent<KW>(b, U, x, a, v0);
-    const uint32_t sole = fp_sole_mask<KW>(b, x);
-    fp_for_shared<KW>(cv, U, x, a, v0, sole, [&](uint32_t v) {
-        const uint32_t s0 = b.fp_soff[v], c = b.fp_vcnt[v];
+    uint32_t by = below ? y : ~0u;  // a pick below x sharing a variable (this lane's)
+    // slow: the group strides every list of the entry
+    auto each = [&](auto f) {
+        uint4 a, v0;
+        fp_ent<KW>(b, U, x, a, v0);
+        fp_for_vars<KW>(cv, U, x, a, v0, [&](uint32_t v) {
+            const uint32_t s0 = b.fp_soff[v], c = b.fp_vcnt[v];
 #pragma unroll 1
-        for (uint32_t q = 0; q < c; ++q) {
-            const uint32_t y = b.fp_vlist[s0 + q];
-            if (y != x) f(y, b.fp_turn[y]);
-        }
-    });
+            for (uint32_t q = gl; q < c; q += FP_RN) {
+                const uint32_t z = b.fp_vlist[s0 + q];
+                if (z != x) f(z, fp_tkey(b.fp_turn[z], z));
+            }
+        });
+    };
+    if (slow)
+        each([&](uint32_t z, unsigned long long kz) {
+            if (kz < kx && pol.q(z)) by = z;
+        });
+    const uint32_t gm = (uint32_t)(__ballot(by != ~0u) >> g0) & ((1u << FP_RN) - 1u);
+    const bool in = gm == 0;
+    const uint32_t bky = __shfl(by, (int)(g0 + (gm ? (uint32_t)__ffs(gm) - 1u : 0u)), 64);
+    bool ch = false;
+    if (act && gl == 0) {
+        if (!in) b.fp_blocker[x] = bky;
+        ch = in != (pol.q(x) != 0);
+        if (ch) pol.set(x, in);
+    }
+    const bool gch = (__ballot(ch) >> g0) & 1ull;
+    pol.push(gch && above, y);
+    if (__ballot(gch && slow))
+        if (gch && slow)
+            each([&](uint32_t z, unsigned long long kz) {
+                if (kz > kx) pol.push1(z);
+            });
 }
 
-struct FpRepBlk {  // the rolled form's decision: a pick below x (~0u: none)
-    const uint32_t* sq;
-    unsigned long long kx;
-    uint32_t* bk;
-    __device__ void operator()(uint32_t y, uint32_t t) const {
-        if (fp_q(sq, y) && fp_tkey(t, y) < kx) *bk = y;
-    }
-};
 constexpr uint32_t FP_RH_BITS = 12;  // LDS dedupe table of a repair round (4096 entry ids)
 constexpr uint32_t FP_RL = 1024;     // dirty entries of a round kept in LDS (more: the global list; 128 + 16 + 8 KiB of LDS)
 
-// entry y into the next round's dirty list once: an LDS hash per round (the global round stamp
-// fp_dmark when its probe window is full); the list itself in LDS up to FP_RL entries, then global
-__device__ __forceinline__ void fp_rep_push(const LoopBuffers& b, uint32_t* hk, uint32_t* nb, uint32_t* lb,
-                                            uint32_t* gb, uint32_t y, uint32_t rid) {
+// true for the first caller with y since the table hk was cleared: an LDS hash (linear probing,
+// slots only ever filled, so every caller with y sees the same window), the global stamp fp_dmark
+// (rid) when y's probe window is full
+__device__ __forceinline__ bool fp_rep_first(const LoopBuffers& b, uint32_t* hk, uint32_t y, uint32_t rid) {
     uint32_t h = (y * 0x9E3779B1u) >> (32 - FP_RH_BITS);
     bool fresh = false, found = false;
 #pragma unroll 1
@@ -3837,54 +3888,10 @@ __device__ __forceinline__ void fp_rep_push(const LoopBuffers& b, uint32_t* hk, 
         h = (h + 1) & ((1u << FP_RH_BITS) - 1u);
     }
     if (!found) fresh = atomicExch(&b.fp_dmark[y], rid) != rid;
-    if (!fresh) return;
-    const uint32_t i = atomicAdd(nb, 1u);
-    if (i < FP_RL) lb[i] = y;
-    else gb[i] = y;
-}
-struct FpRepUp {  // the rolled form's propagation: the neighbours above x into the next list
-    const LoopBuffers* b;
-    uint32_t *hk, *nb, *lb, *gb;
-    uint32_t rid;
-    unsigned long long kx;
-    __device__ void operator()(uint32_t y, uint32_t t) const {
-        if (fp_tkey(t, y) > kx) fp_rep_push(*b, hk, nb, lb, gb, y, rid);
-    }
-};
-
-// The large early rounds of a repair across FP_RW_GRID workgroups (a single CU's memory-level
-// parallelism bounds a round of thousands of decisions: ~34 us per 1,000 at M).  The decisions
-// live in the global bits fp_pbits (atomic updates; every round starts after a grid barrier whose
-// acquire fence drops stale L1 lines, within a round stale reads are allowed as in the one-
-// workgroup rounds), the lists in fp_dl, dedup by the round stamps fp_dmark.  The kernel stops
-// once a round holds at most FP_RW_MIN entries and hands the list, the change log and the round
-// stamp over to k_fp_repair; a grid barrier that times out (workgroups not all resident) hands
-// over as well, at a round boundary, so the result is the same either way.
-constexpr uint32_t FP_RW_GRID = 64;   // workgroups of the wide repair (one per CU, all resident)
-constexpr uint32_t FP_RW_MIN = 256;   // rounds this small are left to the one-workgroup repair
-constexpr unsigned long long FP_RW_TIMEOUT = 2000000ull;  // 20 ms at 100 MHz
-
-__device__ __forceinline__ bool fp_rw_barrier(RRFpCtl* ctl, uint32_t target) {
-    __shared__ uint32_t s_ok;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t ok = 1;
-        __threadfence();  // (release: this workgroup's decisions, log and list entries)
-        atomicAdd(&ctl->wbar, 1u);
-        const unsigned long long t0 = wall_now();
-        while (__hip_atomic_load(&ctl->wbar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-            if (wall_now() - t0 > FP_RW_TIMEOUT) { ok = 0; break; }
-            __builtin_amdgcn_s_sleep(1);
-        }
-        __threadfence();  // (acquire: the CU's L1 holds no line older than the barrier)
-        s_ok = ok;
-    }
-    __syncthreads();
-    return s_ok != 0;
+    return fresh;
 }
 
-// cnt (< 32) consecutive slots of a global list for each active lane: one atomic per wave
+// cnt (< 32) consecutive slots of a list (LDS or global counter) for each active lane: one atomic per wave
 // (thousands of lanes appending to one word serialise at the memory side otherwise); the lane's
 // offset in the wave's range from one ballot per bit of cnt.  Returns the lane's first slot.
 __device__ __forceinline__ uint32_t fp_wave_slots(uint32_t* ctr, uint32_t cnt) {
@@ -3905,73 +3912,178 @@ __device__ __forceinline__ uint32_t fp_wave_slots(uint32_t* ctr, uint32_t cnt) {
     return base + excl;
 }
 
+struct FpPolLds {  // the one-workgroup rounds: decisions in LDS bits, LDS dedupe table and lists
+    const LoopBuffers* b;
+    uint32_t *sq, *hk, *nb, *lb, *gb;
+    uint32_t rid;
+    bool sp;  // (a push went to the global part of the list, read next round once this wave's stores completed)
+    __device__ uint32_t q(uint32_t y) const { return fp_q(sq, y); }
+    __device__ void set(uint32_t x, bool in) {
+        if (in) atomicOr(&sq[x >> 5], 1u << (x & 31u));
+        else atomicAnd(&sq[x >> 5], ~(1u << (x & 31u)));
+    }
+    __device__ void put(uint32_t i, uint32_t y) {
+        if (i < FP_RL) {
+            lb[i] = y;
+        } else {
+            gb[i] = y;
+            sp = true;
+        }
+    }
+    __device__ void push(bool c, uint32_t y) {  // (wave op)
+        const bool f = c && fp_rep_first(*b, hk, y, rid);
+        const uint32_t i = fp_wave_slots(nb, f ? 1u : 0u);
+        if (f) put(i, y);
+    }
+    __device__ void push1(uint32_t y) {
+        if (fp_rep_first(*b, hk, y, rid)) put(atomicAdd(nb, 1u), y);
+    }
+};
+
+struct FpPolWide {  // the wide rounds: decisions in global bits; per workgroup an LDS dedupe table
+                    // and its own segment of the next list
+    const LoopBuffers* b;
+    uint32_t *qg, *hk, *nb, *seg;
+    uint32_t rid, cap;
+    bool over;  // (the segment is full: the pass fails over to a full one)
+    __device__ uint32_t q(uint32_t y) const { return fp_q(qg, y); }
+    __device__ void set(uint32_t x, bool in) {
+        if (in) atomicOr(&qg[x >> 5], 1u << (x & 31u));
+        else atomicAnd(&qg[x >> 5], ~(1u << (x & 31u)));
+    }
+    __device__ void put(uint32_t i, uint32_t y) {
+        if (i < cap) seg[i] = y;
+        else over = true;
+    }
+    __device__ void push(bool c, uint32_t y) {  // (wave op)
+        const bool f = c && fp_rep_first(*b, hk, y, rid);
+        const uint32_t i = fp_wave_slots(nb, f ? 1u : 0u);
+        if (f) put(i, y);
+    }
+    __device__ void push1(uint32_t y) {
+        if (fp_rep_first(*b, hk, y, rid)) put(atomicAdd(nb, 1u), y);
+    }
+};
+
+// the last pass's picks behind the working bits of fp_pbits (16-byte aligned)
+__device__ __forceinline__ uint8_t* fp_pold(const LoopBuffers& b) {
+    return b.fp_pbits + ((b.m / 8 + 64 + 15) & ~15u);
+}
+
+// The large early rounds of a repair across FP_RW_GRID workgroups (a single CU's memory-level
+// parallelism bounds a round of thousands of decisions: ~34 us per 1,000 at M).  The decisions
+// live in the global bits fp_pbits (atomic updates; every round starts after a grid barrier whose
+// acquire fence drops stale L1 lines, within a round stale reads are allowed as in the one-
+// workgroup rounds), the lists in fp_dl, dedup by the round stamps fp_dmark.  The kernel stops
+// once a round holds at most FP_RW_MIN entries and hands the list, the change log and the round
+// stamp over to k_fp_repair; a grid barrier that times out (workgroups not all resident) hands
+// over as well, at a round boundary, so the result is the same either way.
+constexpr uint32_t FP_RW_GRID = 64;   // workgroups of the wide repair (one per CU, all resident)
+constexpr uint32_t FP_RW_MIN = 256;   // rounds this small are left to the one-workgroup repair
+constexpr unsigned long long FP_RW_TIMEOUT = 2000000ull;  // 20 ms at 100 MHz
+
+__device__ __forceinline__ bool fp_rw_barrier(RRFpCtl* ctl, uint32_t target) {
+    __shared__ uint32_t s_ok;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t ok = 1;
+        __threadfence();  // (release: this workgroup's decisions, log and list entries)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the write-back completes before the arrival)
+        atomicAdd(&ctl->wbar, 1u);
+        const unsigned long long t0 = wall_now();
+        while (__hip_atomic_load(&ctl->wbar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            if (wall_now() - t0 > FP_RW_TIMEOUT) { ok = 0; break; }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        __threadfence();  // (acquire: the CU's L1 holds no line older than the barrier)
+        s_ok = ok;
+    }
+    __syncthreads();
+    return s_ok != 0;
+}
+
 template <uint32_t KW>
 __global__ __launch_bounds__(FP_THREADS) void k_fp_repair_wide(ClauseView cv, LoopBuffers b) {
     RRFpCtl* ctl = b.fp_ctl;
     if (ctl->state != FP_RUN || !ctl->inc || ctl->nu > FP_REP_QMAX) return;
     const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
     uint32_t* Q = reinterpret_cast<uint32_t*>(b.fp_pbits);  // the decisions, a bit per entry
-    uint32_t* Lg = b.fp_dl + 2 * b.m;
-    const uint32_t G = gridDim.x;
+    uint32_t* cnts = b.fp_dl + 3 * (size_t)b.m;  // [2][FP_RW_GRID]: the segments' lengths of a list
+    const uint32_t G = gridDim.x, g = blockIdx.x, cap = b.m / G;  // (segment g of a list: cap entries at g cap)
+    __shared__ uint32_t s_hk[1u << FP_RH_BITS];
+    __shared__ uint32_t s_pre[FP_RW_GRID + 1];  // the current list's segment starts (round 0: one list)
+    __shared__ uint32_t s_nb, s_over;
     uint32_t n = ctl->ndirty, rid = ctl->rep_serial, r = 0, cur = 0, work = 0;
     bool ok = true;
+    uint32_t* tl = g == 0 && threadIdx.x == 0 ? fp_tlog(b, ctl->fp_iter) : nullptr;
+    if (tl) tl[1] = (uint32_t)wall_now();
+    if (threadIdx.x == 0) s_over = 0;
     while (n > FP_RW_MIN && n <= FP_REP_CAP && ok && r < FP_REP_MAXR) {
         ++rid;
         work += n;
         const uint32_t* A = b.fp_dl + (size_t)cur * b.m;
         uint32_t* B = b.fp_dl + (size_t)(cur ^ 1) * b.m;
-        uint32_t* nb = &ctl->wcnt[(r + 1) % 3];
-        if (blockIdx.x == 0 && threadIdx.x == 0) ctl->wcnt[(r + 2) % 3] = 0;  // (the round after next)
-        for (uint32_t j = blockIdx.x * FP_THREADS + threadIdx.x; j < n; j += G * FP_THREADS) {
-            const uint32_t x = A[j];
-            const unsigned long long kx = fp_order_key(b, x);
-            uint32_t id[FP_RN], tu[FP_RN], qm;
-            const bool all = fp_rep_gather<KW>(cv, b, U, x, Q, id, tu, qm);
-            uint32_t bk = ~0u;
-            if (all) {
-#pragma unroll
-                for (uint32_t u = 0; u < FP_RN; ++u)
-                    if (((qm >> u) & 1u) && id[u] != x && fp_tkey(tu[u], id[u]) < kx) bk = id[u];
-            } else {
-                fp_rep_each<KW>(cv, b, U, x, FpRepBlk{Q, kx, &bk});
+        for (uint32_t q = threadIdx.x; q < (1u << FP_RH_BITS); q += FP_THREADS) s_hk[q] = 0xFFFFFFFFu;
+        if (threadIdx.x == 0) s_nb = 0;
+        __syncthreads();
+        // a group of FP_RN lanes per entry (fp_grp_step); every lane runs every step
+        FpPolWide pol{&b, Q, s_hk, &s_nb, B + (size_t)g * cap, rid, cap, false};
+        const uint32_t ng = G * (FP_THREADS / FP_RN);
+        for (uint32_t j0 = 0; j0 < n; j0 += ng) {
+            const uint32_t j = j0 + g * (FP_THREADS / FP_RN) + threadIdx.x / FP_RN;
+            uint32_t x = ~0u;
+            if (j < n) {
+                if (r == 0) {
+                    x = A[j];  // (k_fp_detect's list)
+                } else {       // entry j of the segmented list
+                    uint32_t lo = 0, hi = G;
+                    while (hi - lo > 1) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if (s_pre[mid] <= j) lo = mid;
+                        else hi = mid;
+                    }
+                    x = A[(size_t)lo * cap + (j - s_pre[lo])];
+                }
             }
-            const bool in = bk == ~0u;
-            if (!in) b.fp_blocker[x] = bk;
-            const bool ch = in != (fp_q(Q, x) != 0);
-            if (ch) {
-                if (in) atomicOr(&Q[x >> 5], 1u << (x & 31u));
-                else atomicAnd(&Q[x >> 5], ~(1u << (x & 31u)));
-            }
-            {
-                const uint32_t li = fp_wave_slots(&ctl->nlog, ch ? 1u : 0u);
-                if (ch && li < b.m) Lg[li] = x;  // (a longer log fails the pass: k_fp_repair checks nlog)
-            }
-            // the neighbours above a changed entry into the next round (once: the round stamp);
-            // the stamp exchanges all in flight together, then one list reservation per wave
-            if (all) {
-                uint32_t fresh = 0;
-#pragma unroll
-                for (uint32_t u = 0; u < FP_RN; ++u)
-                    if (ch && id[u] != x && fp_tkey(tu[u], id[u]) > kx)
-                        fresh |= (atomicExch(&b.fp_dmark[id[u]], rid) != rid ? 1u : 0u) << u;
-                uint32_t bi = fp_wave_slots(nb, (uint32_t)__popc(fresh));
-#pragma unroll
-                for (uint32_t u = 0; u < FP_RN; ++u)
-                    if ((fresh >> u) & 1u) B[bi++] = id[u];
-            } else if (ch) {
-                fp_rep_each<KW>(cv, b, U, x, [&](uint32_t y, uint32_t t) {
-                    if (fp_tkey(t, y) > kx && atomicExch(&b.fp_dmark[y], rid) != rid) B[atomicAdd(nb, 1u)] = y;
-                });
-            }
+            fp_grp_step<KW>(cv, b, U, x, pol);
         }
+        if (pol.over) s_over = 1;
+        __syncthreads();
+        if (threadIdx.x == 0) cnts[(size_t)((r + 1) & 1) * FP_RW_GRID + g] = s_over ? 0xFFFFFFFFu : s_nb;
+        if (tl && r < 4) tl[56 + 2 * r] = (uint32_t)wall_now();  // (the round's decisions issued: measurement)
         ++r;
         ok = fp_rw_barrier(ctl, r * G);
+        fp_tround(tl, r - 1, n);
         if (!ok) break;  // (the round is complete on this workgroup; the others may not be: fail)
-        n = __hip_atomic_load(nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        // the next list's segment starts (a full segment fails the pass)
+        if (threadIdx.x < 64) {
+            const uint32_t c = threadIdx.x < G ? cnts[(size_t)(r & 1) * FP_RW_GRID + threadIdx.x] : 0u;
+            const bool bad = __ballot(c == 0xFFFFFFFFu) != 0;
+            const uint32_t incl = wave_incl_add(bad ? 0u : c);
+            if (threadIdx.x < G) s_pre[threadIdx.x + 1] = incl;
+            if (threadIdx.x == 0) {
+                s_pre[0] = 0;
+                if (bad) s_over = 2;
+            }
+        }
+        __syncthreads();
+        if (s_over == 2) { ok = false; break; }
+        n = s_pre[G];
         cur ^= 1;
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        ctl->wlist = cur;
+    // the list the rounds left (segments of list cur) into list cur ^ 1 as one list for
+    // k_fp_repair (the detect list as it is when no round ran)
+    uint32_t wl = 0;
+    if (r > 0 && ok) {
+        const uint32_t* A = b.fp_dl + (size_t)cur * b.m;
+        uint32_t* C = b.fp_dl + (size_t)(cur ^ 1) * b.m;
+        const uint32_t c0 = s_pre[g], c = s_pre[g + 1] - c0;
+        for (uint32_t i = threadIdx.x; i < c && c0 + i < b.m; i += FP_THREADS) C[c0 + i] = A[(size_t)g * cap + i];
+        wl = cur ^ 1;
+    }
+    if (g == 0 && threadIdx.x == 0) {
+        ctl->wlist = wl;
         ctl->ndirty = n;
         ctl->rep_serial = rid;
         ctl->wrounds = r;
@@ -3981,7 +4093,8 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_repair_wide(ClauseView cv, Lo
 }
 
 __device__ __forceinline__ void fp_sched_core(const LoopBuffers& b, RRFpCtl* ctl, int test, bool bail, uint32_t ch,
-                                              uint32_t tmin, uint32_t* s_off);
+                                              uint32_t tmin, uint32_t* s_off, const uint32_t* sfp,
+                                              const uint32_t* bndp, const uint32_t* blkp, uint32_t* tl);
 
 // The end of an incremental pass: the rounds, then (as k_fp_count + k_fp_sched after a full
 // pass) the pass test and the next pass's schedule, in this same workgroup: the block pick counts
@@ -4001,19 +4114,30 @@ __global__ __launch_bounds__(1024) void k_fp_repair(ClauseView cv, LoopBuffers b
     }
     const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
     extern __shared__ uint32_t s_q[];  // the current decisions, a bit per entry
-    __shared__ uint32_t s_nb, s_nl;
+    __shared__ uint32_t s_nb;
     __shared__ uint32_t s_hk[1u << FP_RH_BITS];
     __shared__ uint32_t s_l[2][FP_RL];  // the rounds' dirty lists (their first FP_RL entries)
     // global spill of the lists past FP_RL: index i of list c lives at s_l[c][i] or fp_dl[c m + i]
-    uint32_t* Lg = b.fp_dl + 2 * b.m;  // entries whose decision changed (with repeats)
     const uint32_t nu = ctl->nu, nw = (nu + 31) / 32;
-    // (after the wide rounds: their list, change log, round stamp and statistics)
+    // (after the wide rounds: their list, round stamp and statistics)
     const uint32_t n0 = ctl->ndirty, wl = ctl->wlist;
     uint32_t n = n0, rid = ctl->rep_serial, rounds = ctl->wrounds, work = ctl->wwork, cur = 0;
-    bool bail = nu > FP_REP_QMAX || ctl->wfail || ctl->nlog > b.m - FP_REP_CAP;
+    bool bail = nu > FP_REP_QMAX || ctl->wfail;
+    uint32_t* tl = threadIdx.x == 0 ? fp_tlog(b, ctl->fp_iter) : nullptr;
+    if (tl) tl[2] = (uint32_t)wall_now();
+    // the block pick counts, set starts and their in-block counts (one each per thread: nblk <=
+    // FP_REP_QMAX / FP_B, T < blockDim.x), loaded now, kept in LDS for the write-back and schedule
+    const uint32_t T = b.rr_T, nblk = (nu + FP_B - 1) / FP_B;
+    const bool lds_cnt = nu <= FP_REP_QMAX;
+    uint32_t r_blk = 0, r_sf = 0, r_bnd = 0;
+    if (lds_cnt) {
+        if (threadIdx.x < nblk) r_blk = b.fp_blk[threadIdx.x];
+        if (threadIdx.x <= T) { r_sf = b.fp_sf[threadIdx.x]; r_bnd = b.fp_bnd[threadIdx.x]; }
+    }
     if (!bail) {
-        // the last pass's picks (packed by k_fp_turn) into LDS (8 loads in flight per thread: up
-        // to 2^20 entries in one step of the workgroup); k_fp_detect's list into the first list
+        // the decisions (the last pass's picks as packed by k_fp_turn, updated by the wide rounds)
+        // into LDS (8 loads in flight per thread: up to 2^20 entries in one step of the
+        // workgroup); k_fp_detect's list into the first list
         const uint4* src = reinterpret_cast<const uint4*>(b.fp_pbits);
         const uint32_t n4 = (nw + 3) / 4;
         for (uint32_t q0 = 0; q0 < n4; q0 += 8 * blockDim.x) {
@@ -4039,7 +4163,8 @@ __global__ __launch_bounds__(1024) void k_fp_repair(ClauseView cv, LoopBuffers b
             if (j < FP_RL) s_l[0][j] = x;
             else if (wl) b.fp_dl[j] = x;
         }
-        if (threadIdx.x == 0) s_nl = ctl->nlog;
+        __syncthreads();
+        if (tl) tl[5] = (uint32_t)wall_now();
     }
     // Rounds over the dirty entries.  An entry's new decision is stored at once (the others of
     // the round may read it or the old one): whatever it read, an entry is dirty again in the
@@ -4058,74 +4183,120 @@ __global__ __launch_bounds__(1024) void k_fp_repair(ClauseView cv, LoopBuffers b
         const uint32_t* ga = b.fp_dl + (size_t)cur * b.m;
         uint32_t* lb = s_l[cur ^ 1];
         uint32_t* gb = b.fp_dl + (size_t)(cur ^ 1) * b.m;
-        for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) {
-            const uint32_t x = j < FP_RL ? la[j] : ga[j];
-            const unsigned long long kx = fp_order_key(b, x);
-            uint32_t id[FP_RN], tu[FP_RN], qm;
-            const bool all = fp_rep_gather<KW>(cv, b, U, x, s_q, id, tu, qm);
-            uint32_t bk = ~0u;
-            if (all) {
-#pragma unroll
-                for (uint32_t u = 0; u < FP_RN; ++u)
-                    if (((qm >> u) & 1u) && id[u] != x && fp_tkey(tu[u], id[u]) < kx) bk = id[u];
-            } else {
-                fp_rep_each<KW>(cv, b, U, x, FpRepBlk{s_q, kx, &bk});
-            }
-            const bool in = bk == ~0u;
-            if (!in) b.fp_blocker[x] = bk;
-            if (in == (fp_q(s_q, x) != 0)) continue;
-            if (in) atomicOr(&s_q[x >> 5], 1u << (x & 31u));
-            else atomicAnd(&s_q[x >> 5], ~(1u << (x & 31u)));
-            Lg[atomicAdd(&s_nl, 1u)] = x;
-            // the neighbours above x are dirty in the next round
-            if (all) {
-#pragma unroll
-                for (uint32_t u = 0; u < FP_RN; ++u)
-                    if (id[u] != x && fp_tkey(tu[u], id[u]) > kx) fp_rep_push(b, s_hk, &s_nb, lb, gb, id[u], rid);
-            } else {
-                fp_rep_each<KW>(cv, b, U, x, FpRepUp{&b, s_hk, &s_nb, lb, gb, rid, kx});
-            }
+        // a group of FP_RN lanes per entry (fp_grp_step); every lane runs every step
+        FpPolLds pol{&b, s_q, s_hk, &s_nb, lb, gb, rid, false};
+        constexpr uint32_t NG = 1024 / FP_RN;
+        for (uint32_t j0 = 0; j0 < n; j0 += NG) {
+            const uint32_t j = j0 + threadIdx.x / FP_RN;
+            fp_grp_step<KW>(cv, b, U, j < n ? (j < FP_RL ? la[j] : ga[j]) : ~0u, pol);
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const bool sp = pol.sp;
+        // (only the next list's global part crosses waves within the rounds: the blockers are
+        // read by the next pass)
+        if (__ballot(sp)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        fp_tround(tl, rounds - 1, n);
         n = s_nb;
-        if (s_nl > b.m - FP_REP_CAP) bail = true;  // (the change log is full: give up)
         cur ^= 1;
         __syncthreads();  // (the counters and the table are reset at the top of the next round)
     }
-    // The net changes (logged entries whose decision differs from the last pass's, once each: a
-    // fresh round stamp) into bit 0 of fp_in, the block pick counts and the in-block counts of the
-    // set starts behind them in their block; then the test and the next schedule.
-    __shared__ uint32_t s_ch, s_tmin;
-    if (threadIdx.x == 0) { s_ch = 0; s_tmin = ~0u; }
+    // The net changes, word by word against the last pass's picks (the copy behind the working
+    // bits); the blocks they fall in recounted from the decisions, with the in-block counts of
+    // the set starts in them (LDS; the lists' space is free now); the decisions back into the
+    // working bits, where k_fp_turn reads the picks (ctl->pbsrc); then the test and the next
+    // schedule from the counts.
+    __shared__ uint32_t s_ch;
+    if (tl) tl[3] = (uint32_t)wall_now();
+    uint32_t* s_blk = s_l[0];
+    uint32_t* s_sf = s_l[1];
+    uint32_t* s_bnd = s_l[1] + 512;  // (T + 1 <= 257)
+    __shared__ uint8_t s_touch[FP_REP_QMAX / FP_B];  // blocks with changed decisions
+    __syncthreads();  // (the last round's lists are read)
+    if (threadIdx.x == 0) s_ch = 0;
+    if (lds_cnt) {
+        if (threadIdx.x < nblk) s_blk[threadIdx.x] = r_blk;
+        if (threadIdx.x <= T) { s_sf[threadIdx.x] = r_sf; s_bnd[threadIdx.x] = r_bnd; }
+    }
+    for (uint32_t k = threadIdx.x; k < nblk; k += blockDim.x) s_touch[k] = 0;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (!bail) {
-        ++rid;
-        const uint32_t T = b.rr_T;
-        for (uint32_t j = threadIdx.x; j < s_nl; j += blockDim.x) {
-            const uint32_t x = Lg[j];
-            if (atomicExch(&b.fp_dmark[x], rid) == rid) continue;
-            const uint32_t q = fp_q(s_q, x), old = b.fp_in[x];
-            if (q == ((old >> 1) & 1u)) {  // (changed back: bit 0 is still the last pass's)
-                continue;
+        const uint4* old4 = reinterpret_cast<const uint4*>(fp_pold(b));
+        uint4* wk4 = reinterpret_cast<uint4*>(b.fp_pbits);
+        const uint32_t n4 = (nw + 3) / 4, tail = (nu & 31u) ? (1u << (nu & 31u)) - 1u : ~0u;
+        uint32_t my_ch = 0;
+        for (uint32_t q0 = 0; q0 < n4; q0 += 8 * blockDim.x) {  // (8 loads in flight per thread)
+            uint4 o[8];
+#pragma unroll
+            for (uint32_t u = 0; u < 8; ++u) {
+                const uint32_t q = q0 + u * blockDim.x + threadIdx.x;
+                o[u] = q < n4 ? old4[q] : make_uint4(0u, 0u, 0u, 0u);
             }
-            b.fp_in[x] = (uint8_t)((old & 0xFEu) | q);
-            const uint32_t d = q ? 1u : 0xFFFFFFFFu;  // (+1 / -1)
-            const uint32_t blk = x / FP_B;
-            atomicAdd(&b.fp_blk[blk], d);
-            for (uint32_t st = fp_set_of(b.fp_sf, T, x) + 1; st <= T && b.fp_sf[st] / FP_B == blk; ++st)
-                if (b.fp_sf[st] < ctl->nu) atomicAdd(&b.fp_bnd[st], d);
-            atomicAdd(&s_ch, 1u);
-            atomicMin(&s_tmin, b.fp_turn[x]);
+            // (stores after every load is consumed: a store between them made each step wait for
+            // the previous store to complete)
+            uint4 nqs[8];
+#pragma unroll
+            for (uint32_t u = 0; u < 8; ++u) {
+                const uint32_t q = q0 + u * blockDim.x + threadIdx.x;
+                nqs[u] = make_uint4(0u, 0u, 0u, 0u);
+                if (q >= n4) continue;
+                // (a 16-byte group of words lies in one block: FP_B / 32 == 64 words)
+                uint4 nq = make_uint4(s_q[4 * q], s_q[4 * q + 1], s_q[4 * q + 2], s_q[4 * q + 3]), oq = o[u];
+                if (4 * q + 3 >= nw - 1) {  // (the last group: words past the entries masked)
+                    const uint32_t m0 = 4 * q < nw - 1 ? ~0u : (4 * q == nw - 1 ? tail : 0u);
+                    const uint32_t m1 = 4 * q + 1 < nw - 1 ? ~0u : (4 * q + 1 == nw - 1 ? tail : 0u);
+                    const uint32_t m2 = 4 * q + 2 < nw - 1 ? ~0u : (4 * q + 2 == nw - 1 ? tail : 0u);
+                    const uint32_t m3 = 4 * q + 3 == nw - 1 ? tail : 0u;
+                    nq = make_uint4(nq.x & m0, nq.y & m1, nq.z & m2, nq.w & m3);
+                    oq = make_uint4(oq.x & m0, oq.y & m1, oq.z & m2, oq.w & m3);
+                }
+                const uint4 d = make_uint4(nq.x ^ oq.x, nq.y ^ oq.y, nq.z ^ oq.z, nq.w ^ oq.w);
+                if (d.x | d.y | d.z | d.w) {
+                    s_touch[q / (FP_B / 128)] = 1;
+                    my_ch += (uint32_t)(__popc(d.x) + __popc(d.y) + __popc(d.z) + __popc(d.w));
+                }
+                nqs[u] = nq;
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < 8; ++u) {
+                const uint32_t q = q0 + u * blockDim.x + threadIdx.x;
+                if (q < n4) wk4[q] = nqs[u];
+            }
         }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t wch = wave_incl_add(my_ch);
+        if ((threadIdx.x & 63) == 63 && wch) atomicAdd(&s_ch, wch);
         __syncthreads();
+        // the marked blocks' pick counts recounted from the decisions (a wave per block), then the
+        // in-block counts of the set starts in them
+        const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        for (uint32_t k0 = 64 * wave; k0 < nblk; k0 += blockDim.x) {  // (64 blocks per wave and step)
+            unsigned long long tb = __ballot(k0 + lane < nblk && s_touch[k0 + lane]);
+            while (tb) {
+                const uint32_t k = k0 + (uint32_t)__ffsll((long long)tb) - 1u;
+                tb &= tb - 1ull;
+                const uint32_t wd = k * (FP_B / 32) + lane;  // (FP_B / 32 == 64 words per block)
+                uint32_t bits = wd < nw ? s_q[wd] : 0u;
+                if (wd == nw - 1) bits &= tail;
+                const uint32_t c = wave_incl_add((uint32_t)__popc(bits));
+                if (lane == 63) s_blk[k] = c;
+            }
+        }
+        if (threadIdx.x <= T) {
+            const uint32_t f = s_sf[threadIdx.x];
+            if (f < nu && s_touch[f / FP_B]) {
+                uint32_t c = 0;
+                for (uint32_t wd = (f / FP_B) * (FP_B / 32); wd < f / 32; ++wd) c += (uint32_t)__popc(s_q[wd]);
+                if (f & 31u) c += (uint32_t)__popc(s_q[f / 32] & ((1u << (f & 31u)) - 1u));
+                s_bnd[threadIdx.x] = c;
+            }
+        }
+        __syncthreads();  // (the working bits' stores are for the next kernels: no wait)
     }
     if (threadIdx.x == 0) {
         ctl->rep_serial = rid + 1;
         ctl->rep_rounds += rounds;
         if (bail) ctl->bail = 1;
+        ctl->pbsrc = bail ? 0u : 1u;
         if (b.fp_log && ctl->fp_iter < FP_LOG_PASSES) {
             uint32_t* lg = b.fp_log + 4 * ctl->fp_iter;
             lg[0] = n0;
@@ -4134,7 +4305,17 @@ __global__ __launch_bounds__(1024) void k_fp_repair(ClauseView cv, LoopBuffers b
             lg[3] = bail ? 0u : s_ch;
         }
     }
-    fp_sched_core(b, ctl, 1, bail, threadIdx.x == 0 ? s_ch : 0u, s_tmin, nullptr);
+    if (lds_cnt) {
+        // (tmin 0: an incremental pass is followed by another, or by a full one after giving up; the
+        // earliest changed turn serves full passes only)
+        fp_sched_core(b, ctl, 1, bail, threadIdx.x == 0 ? s_ch : 0u, 0u, s_hk, s_sf, s_bnd, s_blk, tl);
+        // (the counts for the next repair / k_fp_count's successor passes)
+        if (threadIdx.x < nblk) b.fp_blk[threadIdx.x] = s_blk[threadIdx.x];
+        if (threadIdx.x <= T) b.fp_bnd[threadIdx.x] = s_bnd[threadIdx.x];
+    } else {
+        fp_sched_core(b, ctl, 1, bail, threadIdx.x == 0 ? s_ch : 0u, 0u, nullptr, b.fp_sf, b.fp_bnd, b.fp_blk, tl);
+    }
+    if (tl) tl[4] = (uint32_t)wall_now();
 }
 
 
@@ -4195,9 +4376,11 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_count(LoopBuffers b, int test
 // counts (fp_bnd), with the pass test: ch / tmin = this thread's share of the picks the pass
 // changed and their earliest turn (OR / min over the workgroup here).  One workgroup; k_fp_sched
 // (after k_fp_count) or the end of k_fp_repair (which updates the counts itself).  s_off: LDS
-// for the block offsets (FP_SCHED_LDS_BLK words) or nullptr.
+// for the block offsets (FP_SCHED_LDS_BLK words) or nullptr; sfp / bndp / blkp: the set starts,
+// their in-block counts and the block counts (fp_sf, fp_bnd, fp_blk or LDS copies of them).
 __device__ __forceinline__ void fp_sched_core(const LoopBuffers& b, RRFpCtl* ctl, int test, bool bail, uint32_t ch,
-                                              uint32_t tmin, uint32_t* s_off) {
+                                              uint32_t tmin, uint32_t* s_off, const uint32_t* sfp,
+                                              const uint32_t* bndp, const uint32_t* blkp, uint32_t* tl) {
     __shared__ uint32_t s_w[16], s_e0;
     __shared__ uint32_t s_n[FP_TMAX], s_nseg[FP_TMAX], s_pf[FP_TMAX + 1];
     const uint32_t nu = ctl->nu, T = b.rr_T, nblk = (nu + FP_B - 1) / FP_B;
@@ -4206,8 +4389,8 @@ __device__ __forceinline__ void fp_sched_core(const LoopBuffers& b, RRFpCtl* ctl
     uint32_t sf[2], bnd[2];
     for (uint32_t q = 0; q < 2; ++q) {  // (T + 1 <= 2 * blockDim.x)
         const uint32_t s = threadIdx.x + q * blockDim.x;
-        sf[q] = s <= T ? b.fp_sf[s] : 0u;
-        bnd[q] = s <= T ? b.fp_bnd[s] : 0u;
+        sf[q] = s <= T ? sfp[s] : 0u;
+        bnd[q] = s <= T ? bndp[s] : 0u;
     }
     ch = __syncthreads_or(ch != 0);
     for (int o = 32; o > 0; o >>= 1) tmin = min(tmin, (uint32_t)__shfl_down(tmin, o, 64));
@@ -4222,11 +4405,11 @@ __device__ __forceinline__ void fp_sched_core(const LoopBuffers& b, RRFpCtl* ctl
     const uint32_t per = (nblk + blockDim.x - 1) / blockDim.x;
     const uint32_t kb = min(nblk, threadIdx.x * per), ke = min(nblk, kb + per);
     uint32_t rsum = 0;
-    for (uint32_t k = kb; k < ke; ++k) rsum += b.fp_blk[k];
+    for (uint32_t k = kb; k < ke; ++k) rsum += blkp[k];
     uint32_t total;
     uint32_t ex = fp_block_scan(rsum, s_w, total);
     for (uint32_t k = kb; k < ke; ++k) {
-        const uint32_t x = b.fp_blk[k];
+        const uint32_t x = blkp[k];
         blkoff[k] = ex;
         if (lds_off) s_off[k] = ex;
         ex += x;
@@ -4247,6 +4430,7 @@ __device__ __forceinline__ void fp_sched_core(const LoopBuffers& b, RRFpCtl* ctl
         s_nseg[s] = 0;
     }
     __syncthreads();
+    if (tl) tl[6] = (uint32_t)wall_now();
     // schedule (wave 0): phases between erasures.  With L live sets and the turn index t, live
     // index x takes its j-th turn of the phase at step + j L + o(x), o(x) = (x - t - 1) mod L;
     // the first set to run out of picks is erased at its next turn E = step + min(r L + o), r =
@@ -4265,25 +4449,28 @@ __device__ __forceinline__ void fp_sched_core(const LoopBuffers& b, RRFpCtl* ctl
                 const uint32_t L = (uint32_t)__popcll(alive);
                 const bool live = (alive >> lane) & 1ull;
                 const uint32_t x = (uint32_t)__popcll(alive & ((1ull << lane) - 1ull));
-                uint32_t o = x + L - (t % L) - 1;  // (x - t - 1) mod L, x < L
+                // o = (x - t - 1) mod L, x < L; t <= L (the erased set's index among L + 1)
+                uint32_t o = x + L - (t == L ? 0u : t) - 1;
                 if (o >= L) o -= L;
-                unsigned long long best = live ? (((unsigned long long)(n - done) * L + o) << 6 | lane) : ~0ull;
-                if (k32) {  // the wave minimum in 32 bits (DPP reduction)
-                    best = __reduce_min_sync(~0ull, (uint32_t)best);
+                const uint32_t left = n - done;
+                uint32_t ls;
+                if (k32) {  // the wave minimum in 32 bits (DPP moves)
+                    ls = wave_min_u32(live ? ((left * L + o) << 6 | lane) : ~0u) & 63u;
                 } else {
+                    unsigned long long best = live ? (((unsigned long long)left * L + o) << 6 | lane) : ~0ull;
                     for (int q = 32; q > 0; q >>= 1) {
                         const unsigned long long y = __shfl_xor(best, q, 64);
                         best = y < best ? y : best;
                     }
+                    ls = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(best & 63u));
                 }
-                const uint32_t ls = (uint32_t)(best & 63u);
-                const unsigned long long d = best >> 6;
-                // turns a live set takes before the erasure: r* or r* + 1 (d = r* L + o*), no
-                // per-lane division
-                const uint32_t rs = (d >> 32) ? (uint32_t)(d / L) : (uint32_t)d / L;
-                const uint32_t os = (uint32_t)(d - (unsigned long long)rs * L);
+                // the first set out: picks left r*, offset o*; it is erased at step + r* L + o*,
+                // every other live set takes r* or r* + 1 turns before (no division)
+                const uint32_t rs = (uint32_t)__builtin_amdgcn_readlane((int)left, (int)ls);
+                const uint32_t os = (uint32_t)__builtin_amdgcn_readlane((int)o, (int)ls);
+                const unsigned long long d = (unsigned long long)rs * L + os;
                 if (live) {
-                    const uint32_t cnt = lane == ls ? n - done : rs + (o < os ? 1u : 0u);
+                    const uint32_t cnt = lane == ls ? left : rs + (o < os ? 1u : 0u);
                     b.fp_seg[(uint64_t)lane * T + nseg] = make_uint4(done, step, L, o);
                     nseg += 1;
                     done += cnt;
@@ -4377,6 +4564,7 @@ __device__ __forceinline__ void fp_sched_core(const LoopBuffers& b, RRFpCtl* ctl
         if (lane == 0) ctl->n_steps = step;
     }
     __syncthreads();
+    if (tl) tl[7] = (uint32_t)wall_now();
     for (uint32_t s = threadIdx.x; s < T; s += blockDim.x) b.fp_nseg[s] = s_nseg[s];
     if (threadIdx.x == 0) {
         ctl->total = total;
@@ -4420,6 +4608,7 @@ __global__ __launch_bounds__(256) void k_fp_sched(LoopBuffers b, int test) {
         return;
     }
     const bool bail = test && ctl->bail;  // the incremental pass gave up: its picks are no fixpoint test
+    if (threadIdx.x == 0) ctl->pbsrc = 0;  // (a full pass: its picks are bit 0 of fp_in)
     __shared__ uint32_t s_off[FP_SCHED_LDS_BLK];  // block offsets (when they fit)
     const uint32_t nblk = (ctl->nu + FP_B - 1) / FP_B;
     // change counts and earliest changes of the k_fp_count workgroups
@@ -4429,14 +4618,14 @@ __global__ __launch_bounds__(256) void k_fp_sched(LoopBuffers b, int test) {
             ch += b.fp_blk[2 * (b.m / FP_B + 2) + k];
             tmin = min(tmin, b.fp_blk[2 * (b.m / FP_B + 2) + FP_COUNT_GRID + k]);
         }
-    fp_sched_core(b, ctl, test, bail, ch, tmin, s_off);
+    fp_sched_core(b, ctl, test, bail, ch, tmin, s_off, b.fp_sf, b.fp_bnd, b.fp_blk, nullptr);
 }
 
 // Turns of every block of entries (grid-stride) for the next pass, or (fin) the MIS: picks in
 // step order into tmis (step minus the erasures before it), their variables covered with the
 // iteration's stamp, and the statistics of k_rr_mw.  blk_off(blk): picks before block blk.
 template <uint32_t KW, typename BlkOff>
-__device__ __forceinline__ void fp_turn_blocks(const ClauseView& cv, const LoopBuffers& b, bool fin, bool inc, uint32_t nu,
+__device__ __forceinline__ void fp_turn_blocks(const ClauseView& cv, const LoopBuffers& b, bool fin, bool inc, bool pb, uint32_t nu,
                                                uint32_t T, uint32_t stamp, const uint32_t* s_sf,
                                                const uint32_t* s_pf, const uint32_t* s_nseg, const uint32_t* s_er,
                                                const uint4* segs, uint32_t* s_w, BlkOff blk_off) {
@@ -4446,17 +4635,28 @@ __device__ __forceinline__ void fp_turn_blocks(const ClauseView& cv, const LoopB
         const uint32_t i0 = blk * FP_B + threadIdx.x * FP_PER;
         unsigned long long x = 0;
         if (i0 < nu) {
-            x = *reinterpret_cast<const unsigned long long*>(b.fp_in + i0);
+            if (pb) {  // (after an incremental pass: its picks are bits; byte -> bit 0 of 8 bytes)
+                const uint32_t by = b.fp_pbits[i0 / 8];
+                x = (unsigned long long)(((by & 15u) * 0x00204081u) & 0x01010101u) |
+                    ((unsigned long long)(((by >> 4) * 0x00204081u) & 0x01010101u) << 32);
+            } else {
+                x = *reinterpret_cast<const unsigned long long*>(b.fp_in + i0);
+            }
             if (nu - i0 < FP_PER) x &= (1ull << (8 * (nu - i0))) - 1ull;
         }
         const unsigned long long b0 = x & 0x0101010101010101ull;
         uint32_t tot;
         uint32_t P = blk_off(blk) + fp_block_scan((uint32_t)__popcll(b0), s_w, tot);
         // the next pass sets bit 0 of its picks; these become bit 1 (k_fp_count compares them); an
-        // incremental pass starts from them (bit 0 too) and repairs bit 0
+        // incremental pass starts from them (bit 0 too), packed: the working bits it repairs and
+        // the copy its net changes are taken against
         if (!fin && i0 < nu) {
             *reinterpret_cast<unsigned long long*>(b.fp_in + i0) = (b0 << 1) | (inc ? b0 : 0ull);
-            if (inc) b.fp_pbits[i0 / 8] = (uint8_t)((b0 * 0x0102040810204080ull) >> 56);  // (FP_PER == 8: a byte)
+            if (inc) {
+                const uint8_t by = (uint8_t)((b0 * 0x0102040810204080ull) >> 56);  // (FP_PER == 8: a byte)
+                b.fp_pbits[i0 / 8] = by;
+                fp_pold(b)[i0 / 8] = by;
+            }
         }
         if (i0 < nu) {
             uint32_t s = fp_set_of(s_sf, T, i0);
@@ -4552,7 +4752,7 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_turn(ClauseView cv, LoopBuffe
     if (lds_seg)
         for (uint32_t q = threadIdx.x; q < T * T; q += blockDim.x) s_seg[q] = b.fp_seg[q];
     __syncthreads();
-    fp_turn_blocks<KW>(cv, b, fin, ctl->inc != 0, nu, T, stamp, s_sf, s_pf, s_nseg, s_er, lds_seg ? s_seg : b.fp_seg, s_w,
+    fp_turn_blocks<KW>(cv, b, fin, ctl->inc != 0, ctl->pbsrc != 0, nu, T, stamp, s_sf, s_pf, s_nseg, s_er, lds_seg ? s_seg : b.fp_seg, s_w,
                        [&](uint32_t blk) { return blkoff[blk]; });
     if (fin && blockIdx.x == 0 && threadIdx.x == 0) {
         st->tmis_cnt = ctl->total;

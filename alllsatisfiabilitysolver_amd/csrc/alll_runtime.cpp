@@ -991,8 +991,8 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
             if (inc) {
                 if ((rc = dalloc(c, &b.fp_blocker, m + 1, 0xFF)) || (rc = dalloc(c, &b.fp_covby, (size_t)prob->n_vars + 1)) ||
                     (rc = dalloc(c, &b.fp_vcnt, (size_t)prob->n_vars + 1)) || (rc = dalloc(c, &b.fp_dl, 3 * (size_t)m + 16 * std::min<size_t>(m, 1u << 16) + 64)) ||
-                    (rc = dalloc(c, &b.fp_dmark, m + 1)) || (rc = dalloc(c, &b.fp_pbits, m / 8 + 64)) ||
-                    (rc = dalloc(c, &b.fp_log, 4 * FP_LOG_PASSES)) ||
+                    (rc = dalloc(c, &b.fp_dmark, m + 1)) || (rc = dalloc(c, &b.fp_pbits, 2 * ((size_t)m / 8 + 80))) ||
+                    (rc = dalloc(c, &b.fp_log, FP_LOG_WORDS)) ||
                     (rc = dalloc(c, &b.fp_lst, 2 * (size_t)m * ((rr_width >= 1 && rr_width <= 4) ? 4 : 8) + 16)))
                     return bail(rc);
                 b.fp_inc = 1;
@@ -1752,7 +1752,7 @@ int alll_rr_pass_log(alll_ctx* c, uint32_t* out, uint32_t n_words) {
     if (!c || (!out && n_words)) return fail(ALLL_ERR_INVALID_ARG, "null argument");
     HIP_TRY(hipSetDevice(c->device));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    const uint32_t have = c->b.fp_log ? 4 * FP_LOG_PASSES : 0;
+    const uint32_t have = c->b.fp_log ? FP_LOG_WORDS : 0;
     const uint32_t nw = std::min(n_words, have);
     if (nw) HIP_TRY(hipMemcpy(out, c->b.fp_log, nw * 4ull, hipMemcpyDeviceToHost));
     for (uint32_t i = nw; i < n_words; ++i) out[i] = 0;

@@ -264,11 +264,20 @@ class Solver:
     def rr_pass_log(self):
         """Round robin: per pass of the last iteration (dirty entries, repair rounds, entries
         decided, decisions changed) of its incremental passes (measurement)."""
-        out = np.zeros(256, np.uint32)
+        return self._rr_log()[0]
+
+    def rr_round_log(self):
+        """Round robin: per pass of the last iteration, the repair's clock stamps (100 MHz;
+        detect, wide repair, repair, rounds end, repair end, LDS loaded) and its rounds
+        {entries, stamp} (measurement; rows of 64 words, zeros where not reached)."""
+        return self._rr_log()[1]
+
+    def _rr_log(self):
+        out = np.zeros(256 + 64 * 64, np.uint32)
         n = self._L.alll_rr_pass_log(self._ctx, _p(out, _u32p), out.size)
         if n < 0:
             N.check(n, "rr_pass_log")
-        return out[:n].reshape(-1, 4)
+        return out[:min(n, 256)].reshape(-1, 4), out[256:max(n, 256)].reshape(-1, 64)
 
     def comm_size(self) -> int:
         """Ranks in the solve: the RCCL communicator's count (or world with a host exchange)."""

@@ -205,7 +205,9 @@ const char* alll_eval_kernel(alll_ctx* ctx);
 int alll_uses_graphs(alll_ctx* ctx, const char** why);
 /* Round robin (n_threads > 1): the pass log of the last iteration, 4 words per pass {dirty
  * entries, repair rounds (0xFFFFFFFF: the incremental pass gave up), entries decided, decisions
- * changed} for the incremental passes (zeros for full ones), at most 64 passes; returns the words
+ * changed} for the incremental passes (zeros for full ones), at most 64 passes, then 64 words per
+ * pass of repair clock stamps (100 MHz; words 0..5: detect, wide repair, repair, rounds end,
+ * repair end, decisions loaded; from word 8 {round entries, stamp} pairs); returns the words
  * written (0 without incremental passes).  (No reference counterpart: measurement) */
 int alll_rr_pass_log(alll_ctx* ctx, uint32_t* out, uint32_t n_words);
 /* Ranks taking part in the clause-sharded solve: ncclCommCount of the RCCL communicator, or

@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--iters", type=int, default=6)
     ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--rounds", action="store_true", help="the repair rounds' clock stamps too")
     a = ap.parse_args()
     from alllsatisfiabilitysolver_amd import Solver, generate_ksat
     from rr_bench import CONFIGS
@@ -33,6 +34,19 @@ def main():
             rows = [tuple(int(x) for x in r) for r in lg if r.any()]
             print(f"iter {st['n_iterations']}: {1e3 * dt:.3f} ms, |U| {st['n_violated']}, passes {st['lfmis_tail_rounds']}: "
                   + " ".join(f"[d{r[0]} r{r[1] if r[1] != 0xFFFFFFFF else 'BAIL'} w{r[2]} c{r[3]}]" for r in rows), flush=True)
+            if a.rounds:
+                tl = s.rr_round_log()
+                for p, t in enumerate(tl):
+                    if not t.any():
+                        continue
+                    t0 = int(t[0])
+                    us = lambda x: (int(x) - t0) % (1 << 32) / 100.0  # 100 MHz ticks -> us
+                    rr = [(int(t[8 + 2 * q]), us(t[9 + 2 * q])) for q in range(24) if t[9 + 2 * q]]
+                    wb = [us(t[56 + 2 * q]) for q in range(4) if t[56 + 2 * q]]
+                    print(f"  pass {p}: wide@{us(t[1]):.1f} rep@{us(t[2]):.1f} lds@{us(t[5]):.1f} "
+                          f"rounds_end@{us(t[3]):.1f} sched@{us(t[6]):.1f} phases@{us(t[7]):.1f} end@{us(t[4]):.1f} | "
+                          + " ".join(f"{n}@{x:.1f}" for n, x in rr)
+                          + (" | wide pre-barrier " + " ".join(f"{x:.1f}" for x in wb) if wb else ""), flush=True)
 
 
 if __name__ == "__main__":

@@ -280,9 +280,10 @@ struct LoopBuffers {
     uint32_t* fp_blocker;       // per scan entry out of the last pass's picks: a pick below it that shares a
                                 //   variable with it (the pass's cover of that variable, fp_covby)
     uint32_t* fp_covby;         // n_vars: the pick that covered the variable in the current pass
-    uint32_t* fp_vcnt;          // n_vars: violated claimants of the variable this iteration (fp_vlist length)
     uint32_t* fp_lst;           // per scan entry, 4 slots (widths <= 4) or 8: {start, length} of the slot's
                                 //   variable's claimant list (uint2; k_fp_bbuild)
+    uint2* fp_sc;               // n_vars: {fp_soff, violated claimants this iteration}: a variable's claimant
+                                //   list (written for the claimed variables only)
     uint32_t* fp_dl;            // 3 x m + 16 min(m, 2^16): the repair's dirty lists (two), its change log and
                                 //   its raw push list
     uint32_t* fp_dmark;         // per scan entry: repair round stamp of its last dirty-list insertion

@@ -2320,6 +2320,17 @@ __device__ __forceinline__ uint32_t fp_block_scan(uint32_t x, uint32_t* s_w, uin
     return before + incl - x;
 }
 
+// the timing log of pass p (FP_LOG_RW words; nullptr past FP_LOG_PASSES) and its round records
+__device__ __forceinline__ uint32_t* fp_tlog(const LoopBuffers& b, uint32_t p) {
+    return b.fp_log && p < FP_LOG_PASSES ? b.fp_log + 4 * FP_LOG_PASSES + FP_LOG_RW * p : nullptr;
+}
+__device__ __forceinline__ void fp_tround(uint32_t* t, uint32_t r, uint32_t n) {
+    if (t && r < FP_LOG_RW / 2 - 8) {
+        t[8 + 2 * r] = n;
+        t[9 + 2 * r] = (uint32_t)wall_now();
+    }
+}
+
 // literal range of clause c: fixed width k (AoS) or the CSR offsets
 __device__ __forceinline__ uint32_t cl_start(const ClauseView& cv, uint32_t c) { return cv.k ? c * cv.k : cv.offs[c]; }
 __device__ __forceinline__ uint32_t cl_width(const ClauseView& cv, uint32_t c) {
@@ -2455,18 +2466,21 @@ __global__ __launch_bounds__(256) void k_rr_entries(ClauseView cv, LoopBuffers b
             v[j] = j < w ? lit_var(raw) : RR_EMPTY;
             hm |= ((raw & LIT_HOT) ? 1u : 0u) << j;
         }
-        RREnt e;
-        e.a = make_uint4(c, lb, w, hm);
-        e.v0 = make_uint4(v[0], v[1], v[2], v[3]);
-        e.v1 = make_uint4(v[4], v[5], v[6], v[7]);
-        out[i] = e;
-        if (b.fp_ctl) {  // the passes' narrow copy; sole bytes cleared (k_fp_bbuild sets them)
-            if (b.rr_k >= 1 && b.rr_k <= 4) {
-                b.fp_v4[base + i] = e.v0;
-                reinterpret_cast<uint32_t*>(b.fp_sole)[base + i] = 0u;
-            } else {
-                reinterpret_cast<uint2*>(b.fp_sole)[base + i] = make_uint2(0u, 0u);
-            }
+        const uint4 a = make_uint4(c, lb, w, hm), v0 = make_uint4(v[0], v[1], v[2], v[3]);
+        if (b.fp_ctl && b.rr_k >= 1 && b.rr_k <= 4) {
+            // narrow instances with the passes: the header, and the variables in the 16-byte copy
+            // only (every reader of a narrow entry's variables takes them there); sole bytes
+            // cleared (k_fp_bbuild sets them)
+            out[i].a = a;
+            b.fp_v4[base + i] = v0;
+            reinterpret_cast<uint32_t*>(b.fp_sole)[base + i] = 0u;
+        } else {
+            RREnt e;
+            e.a = a;
+            e.v0 = v0;
+            e.v1 = make_uint4(v[4], v[5], v[6], v[7]);
+            out[i] = e;
+            if (b.fp_ctl) reinterpret_cast<uint2*>(b.fp_sole)[base + i] = make_uint2(0u, 0u);
         }
     }
 }
@@ -2585,6 +2599,7 @@ __global__ __launch_bounds__(64) void k_rr_mw(ClauseView cv, LoopBuffers b) {
     const uint32_t NW = gridDim.x, g = blockIdx.x;
     const uint32_t T = b.rr_T;
     const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
+    const bool v4 = b.fp_ctl && b.rr_k >= 1 && b.rr_k <= 4;  // (k_rr_entries: variables in fp_v4)
     const auto rsC = __builtin_amdgcn_make_buffer_rsrc(b.cover, (short)0, (int)b.n_vars, 0x00020000);
     const uint32_t nu = (uint32_t)st->u_total;
     const uint32_t base = __hip_atomic_load(&ctl->epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2645,8 +2660,17 @@ __global__ __launch_bounds__(64) void k_rr_mw(ClauseView cv, LoopBuffers b) {
                     const uint32_t i = pos + u * 64 + lane;
                     alive[u] = i < end;
                     RREnt e;
-                    if (alive[u]) e = U[i];
-                    else { e.a = make_uint4(0u, 0u, 0u, 0u); e.v0 = e.v1 = make_uint4(RR_EMPTY, RR_EMPTY, RR_EMPTY, RR_EMPTY); }
+                    if (alive[u]) {
+                        if (KR == 4 && v4) {  // (narrow entries keep their variables in fp_v4 only)
+                            e.a = U[i].a;
+                            e.v0 = b.fp_v4[i];
+                        } else {
+                            e = U[i];
+                        }
+                    } else {
+                        e.a = make_uint4(0u, 0u, 0u, 0u);
+                        e.v0 = e.v1 = make_uint4(RR_EMPTY, RR_EMPTY, RR_EMPTY, RR_EMPTY);
+                    }
                     c[u] = e.a.x; lb[u] = e.a.y; w[u] = e.a.z;
                     const uint32_t ev[8] = {e.v0.x, e.v0.y, e.v0.z, e.v0.w, e.v1.x, e.v1.y, e.v1.z, e.v1.w};
 #pragma unroll
@@ -3218,28 +3242,34 @@ __global__ __launch_bounds__(FP_BB_THREADS) void k_fp_bbuild(LoopBuffers b) {
     __shared__ uint32_t s_ns;
     const uint32_t n = b.fp_bfill[bk];
     constexpr uint32_t U4 = 4;  // loads in flight per thread
-    for (uint32_t w0 = tid; w0 < nw; w0 += U4 * FP_BB_THREADS) {
-        uint32_t o[U4];
-#pragma unroll
-        for (uint32_t u = 0; u < U4; ++u) {
-            const uint32_t w = w0 + u * FP_BB_THREADS;
-            const uint32_t v = w < nw ? vunmix(b, xb + w) : ~0u;
-            o[u] = v < b.n_vars ? b.fp_soff[v] : 0u;
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < U4; ++u) {
-            const uint32_t w = w0 + u * FP_BB_THREADS;
-            if (w < nw) {
-                s_cnt[w] = 0u;
-                s_off[w] = o[u];
-            }
-        }
-    }
+    uint32_t* tlb = bk == 0 && tid == 0 ? fp_tlog(b, FP_LOG_PASSES - 1) : nullptr;  // (phase stamps: measurement)
+    if (tlb) tlb[0] = (uint32_t)wall_now();
+    for (uint32_t w = tid; w < nw; w += FP_BB_THREADS) s_cnt[w] = 0u;
     if (tid == 0) s_ns = 0;
     __syncthreads();
+    if (tlb) tlb[1] = (uint32_t)wall_now();
     if (tid == 0) b.fp_bfill[bk] = 0u;  // (read by every thread above; the next iteration's count)
     const uint2* P = reinterpret_cast<const uint2*>(b.fp_pairs) + b.fp_breg[bk];
-    for (uint32_t k0 = tid; k0 < n; k0 += U4 * FP_BB_THREADS) {
+    // The bucket's lists packed at the start of its region (the pairs' region bounds: fp_breg):
+    // claims counted per variable, the counts scanned into list starts, then every claim placed.
+    // (At static per-variable offsets -- every literal occurrence's slot -- the lists were sparse
+    // and each claim's store a line of its own: the placement cost three times as much.)
+    // rank / place: the lanes that share the first valid lane's variable take theirs from one
+    // atomic (a hub's claims would serialise on one LDS word)
+    auto grouped_add = [&](uint32_t* ctr, bool valid, uint32_t w) -> uint32_t {
+        const unsigned long long vb = __ballot(valid);
+        if (!vb) return 0u;
+        const int fl = __ffsll((long long)vb) - 1;
+        const uint32_t wl = __shfl(w, fl, 64);
+        const bool grp = valid && w == wl;
+        const unsigned long long same = __ballot(grp);
+        uint32_t base = 0;
+        if ((int)(tid & 63) == fl) base = atomicAdd(&ctr[wl], (uint32_t)__popcll(same));
+        base = __shfl(base, fl, 64);
+        if (!valid) return 0u;
+        return grp ? base + (uint32_t)__popcll(same & ((1ull << (tid & 63)) - 1ull)) : atomicAdd(&ctr[w], 1u);
+    };
+    for (uint32_t k0 = tid; k0 < n; k0 += U4 * FP_BB_THREADS) {  // counts, first claimants
         uint2 p[U4];
 #pragma unroll
         for (uint32_t u = 0; u < U4; ++u) {
@@ -3248,27 +3278,46 @@ __global__ __launch_bounds__(FP_BB_THREADS) void k_fp_bbuild(LoopBuffers b) {
         }
 #pragma unroll
         for (uint32_t u = 0; u < U4; ++u) {
-            // ranks by LDS counter; the lanes that share the first valid lane's variable take
-            // theirs from one atomic (a hub's claims would serialise on one LDS word)
             const bool valid = p[u].y != ~0u;
-            const unsigned long long vb = __ballot(valid);
-            if (!vb) continue;
             const uint32_t w = valid ? vmix(b, p[u].y) - xb : 0u;
-            const int fl = __ffsll((long long)vb) - 1;
-            const uint32_t wl = __shfl(w, fl, 64);
-            const bool grp = valid && w == wl;
-            const unsigned long long same = __ballot(grp);
-            uint32_t base = 0;
-            if ((int)(tid & 63) == fl) base = atomicAdd(&s_cnt[wl], (uint32_t)__popcll(same));
-            base = __shfl(base, fl, 64);
-            if (!valid) continue;
-            const uint32_t r = grp ? base + (uint32_t)__popcll(same & ((1ull << (tid & 63)) - 1ull))
-                                   : atomicAdd(&s_cnt[w], 1u);
-            if (r == 0) s_first[w] = p[u].x;
-            b.fp_vlist[s_off[w] + r] = p[u].x & FP_IMASK;
+            const uint32_t r = grouped_add(s_cnt, valid, w);
+            if (valid && r == 0) s_first[w] = p[u].x;
         }
     }
     __syncthreads();
+    {  // list starts: a contiguous range of variables per thread, one workgroup scan
+        const uint32_t per = (nw + FP_BB_THREADS - 1) / FP_BB_THREADS;
+        const uint32_t w0 = min(nw, tid * per), w1 = min(nw, w0 + per);
+        uint32_t sum = 0;
+        for (uint32_t w = w0; w < w1; ++w) sum += s_cnt[w];
+        __shared__ uint32_t s_sw[FP_BB_THREADS / 64];
+        uint32_t tot;
+        uint32_t o = b.fp_breg[bk] + fp_block_scan(sum, s_sw, tot);
+        for (uint32_t w = w0; w < w1; ++w) {
+            s_off[w] = o;
+            o += s_cnt[w];
+        }
+    }
+    __syncthreads();
+    for (uint32_t k0 = tid; k0 < n; k0 += U4 * FP_BB_THREADS) {  // placement
+        uint2 p[U4];
+#pragma unroll
+        for (uint32_t u = 0; u < U4; ++u) {
+            const uint32_t k = k0 + u * FP_BB_THREADS;
+            p[u] = k < n ? P[k] : make_uint2(0u, ~0u);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < U4; ++u) {
+            const bool valid = p[u].y != ~0u;
+            const uint32_t w = valid ? vmix(b, p[u].y) - xb : 0u;
+            const uint32_t pos = grouped_add(s_off, valid, w);
+            if (valid) b.fp_vlist[pos] = p[u].x & FP_IMASK;
+        }
+    }
+    __syncthreads();
+    for (uint32_t w = tid; w < nw; w += FP_BB_THREADS) s_off[w] -= s_cnt[w];  // (back to the starts)
+    __syncthreads();
+    if (tlb) tlb[2] = (uint32_t)wall_now();
     if (b.fp_lst) {
         // incremental passes: every claim's list {start, length} at its entry's slot (the repair
         // reads an entry's lists with its first load; slots past the list rows keep the rolled path)
@@ -3289,6 +3338,7 @@ __global__ __launch_bounds__(FP_BB_THREADS) void k_fp_bbuild(LoopBuffers b) {
             }
         }
     }
+    if (tlb) tlb[3] = (uint32_t)wall_now();
     // per variable (vmix slot order): the single claimant's ownership and sole byte, the shared
     // list and the long lists' segments
     uint4* sv = reinterpret_cast<uint4*>(b.fp_sv) + (uint64_t)bk * W;
@@ -3304,7 +3354,7 @@ __global__ __launch_bounds__(FP_BB_THREADS) void k_fp_bbuild(LoopBuffers b) {
         uint32_t base = 0;
         if (lane == 0 && bal) base = atomicAdd(&s_ns, (uint32_t)__popcll(bal));
         base = __shfl(base, 0, 64);
-        if (c && b.fp_vcnt) b.fp_vcnt[v] = c;  // (incremental passes: the list's length)
+        if (c && b.fp_sc) b.fp_sc[v] = make_uint2(s_off[w], c);  // (incremental passes: the list)
         if (c == 1u) {
             const uint32_t x = s_first[w], i = x & FP_IMASK, j = x >> FP_SLOT_SH;
             b.fp_own0[v] = i;
@@ -3324,6 +3374,7 @@ __global__ __launch_bounds__(FP_BB_THREADS) void k_fp_bbuild(LoopBuffers b) {
         }
     }
     __syncthreads();
+    if (tlb) tlb[4] = (uint32_t)wall_now();
     if (tid == 0) b.fp_sbcnt[bk] = s_ns;
 }
 
@@ -3728,17 +3779,6 @@ __device__ __forceinline__ unsigned long long fp_order_key(const LoopBuffers& b,
     return ((unsigned long long)b.fp_turn[i] << 32) | i;
 }
 
-// the timing log of pass p (FP_LOG_RW words; nullptr past FP_LOG_PASSES) and its round records
-__device__ __forceinline__ uint32_t* fp_tlog(const LoopBuffers& b, uint32_t p) {
-    return b.fp_log && p < FP_LOG_PASSES ? b.fp_log + 4 * FP_LOG_PASSES + FP_LOG_RW * p : nullptr;
-}
-__device__ __forceinline__ void fp_tround(uint32_t* t, uint32_t r, uint32_t n) {
-    if (t && r < FP_LOG_RW / 2 - 8) {
-        t[8 + 2 * r] = n;
-        t[9 + 2 * r] = (uint32_t)wall_now();
-    }
-}
-
 __global__ __launch_bounds__(FP_THREADS) void k_fp_detect(LoopBuffers b) {
     RRFpCtl* ctl = b.fp_ctl;
     if (ctl->state != FP_RUN || !ctl->inc) return;
@@ -3764,10 +3804,11 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_detect(LoopBuffers b) {
 }
 
 // The repair's view of an entry x: the claimant lists of its variables (fp_vlist; the entry's
-// list rows {start, length} in fp_lst) hold its neighbours y != x.  A group of FP_RN lanes decides
-// one entry: lane u takes slot u of the concatenated lists, so a decision is three dependent
-// round trips (the list rows and x's turn, the list slot, its turn and decision) and a few dozen
-// instructions per lane; the rare entry with more slots (or wider than its rows) has its group
+// list rows {start, length} in fp_lst, k_fp_bbuild) hold its neighbours y != x.  A group of FP_RN
+// lanes decides one entry: lane u takes slot u of the concatenated lists, so a decision is three
+// dependent round trips (x's turn and list rows, the list slot, its turn and decision) and a few
+// dozen instructions per lane (the rows loaded per decision from the variables and fp_sc instead:
+// one more round trip, the same iteration time as the rows' scattered stores in k_fp_bbuild); the rare entry with more slots (or wider than its rows) has its group
 // stride every list in turn.  (One lane per entry with all FP_RN slots unrolled ran ~4x the
 // instructions: a one-entry round took ~5 us.)
 constexpr uint32_t FP_RN = 16;  // lanes per entry (the entry's own slots included: ~99.9% of the dirty
@@ -3795,6 +3836,7 @@ __device__ __forceinline__ void fp_grp_step(const ClauseView& cv, const LoopBuff
 #pragma unroll
     for (uint32_t k = 0; k < RW; ++k) so[k] = cn[k] = 0;
     if (act) {
+        // x's turn and list rows (every lane of the group loads the same words)
         kx = fp_tkey(b.fp_turn[x], x);
         w = KW == 4 ? b.rr_k : U[x].a.z;
         const uint4* rows = reinterpret_cast<const uint4*>(b.fp_lst) + (uint64_t)x * (RW / 2);
@@ -3841,7 +3883,8 @@ __device__ __forceinline__ void fp_grp_step(const ClauseView& cv, const LoopBuff
         uint4 a, v0;
         fp_ent<KW>(b, U, x, a, v0);
         fp_for_vars<KW>(cv, U, x, a, v0, [&](uint32_t v) {
-            const uint32_t s0 = b.fp_soff[v], c = b.fp_vcnt[v];
+            const uint2 sc = b.fp_sc[v];
+            const uint32_t s0 = sc.x, c = sc.y;
 #pragma unroll 1
             for (uint32_t q = gl; q < c; q += FP_RN) {
                 const uint32_t z = b.fp_vlist[s0 + q];
@@ -4125,6 +4168,23 @@ __global__ __launch_bounds__(1024) void k_fp_repair(ClauseView cv, LoopBuffers b
     bool bail = nu > FP_REP_QMAX || ctl->wfail;
     uint32_t* tl = threadIdx.x == 0 ? fp_tlog(b, ctl->fp_iter) : nullptr;
     if (tl) tl[2] = (uint32_t)wall_now();
+    if (n0 == 0 && rounds == 0 && !bail) {
+        // nothing to repair: the picks repeat, the pass converged, and the counts and the
+        // schedule (k_fp_turn finalizes with it) are the last pass's
+        if (threadIdx.x == 0) {
+            ctl->state = FP_FINAL;
+            ctl->guess_num = ctl->total;
+            ctl->guess_den = nu ? nu : 1u;
+            ctl->changes = 0;
+            ctl->pbsrc = 1;
+            if (b.fp_log && ctl->fp_iter < FP_LOG_PASSES) {
+                uint32_t* lg = b.fp_log + 4 * ctl->fp_iter;
+                lg[0] = lg[1] = lg[2] = lg[3] = 0;
+            }
+            if (tl) tl[4] = (uint32_t)wall_now();
+        }
+        return;
+    }
     // the block pick counts, set starts and their in-block counts (one each per thread: nblk <=
     // FP_REP_QMAX / FP_B, T < blockDim.x), loaded now, kept in LDS for the write-back and schedule
     const uint32_t T = b.rr_T, nblk = (nu + FP_B - 1) / FP_B;
@@ -4621,6 +4681,19 @@ __global__ __launch_bounds__(256) void k_fp_sched(LoopBuffers b, int test) {
     fp_sched_core(b, ctl, test, bail, ch, tmin, s_off, b.fp_sf, b.fp_bnd, b.fp_blk, nullptr);
 }
 
+// a thread's MIS statistics of one clause tile into the block's LDS tally (tiles s_t0 ..
+// s_t0 + 63; others straight to tile_stats)
+__device__ __forceinline__ void fp_stat_add(const LoopBuffers& b, uint32_t t0, uint32_t* sn, uint32_t* sw, uint32_t tile,
+                                            uint32_t n, unsigned long long w) {
+    if (tile >= t0 && tile - t0 < 64 && w < (1ull << 31)) {
+        atomicAdd(&sn[tile - t0], n);
+        atomicAdd(&sw[tile - t0], (uint32_t)w);
+    } else {
+        atomicAdd(&b.tile_stats[2 * tile], (unsigned long long)n);
+        atomicAdd(&b.tile_stats[2 * tile + 1], w);
+    }
+}
+
 // Turns of every block of entries (grid-stride) for the next pass, or (fin) the MIS: picks in
 // step order into tmis (step minus the erasures before it), their variables covered with the
 // iteration's stamp, and the statistics of k_rr_mw.  blk_off(blk): picks before block blk.
@@ -4631,8 +4704,16 @@ __device__ __forceinline__ void fp_turn_blocks(const ClauseView& cv, const LoopB
                                                const uint4* segs, uint32_t* s_w, BlkOff blk_off) {
     const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
     const uint32_t nblk = (nu + FP_B - 1) / FP_B;
+    // (fin: the block's MIS statistics per clause tile in LDS -- its entries span a few
+    // consecutive tiles from s_t0 on -- then one global add per tile; past FP_ST_TILES, direct)
+    constexpr uint32_t FP_ST_TILES = 64;
+    __shared__ uint32_t s_t0, s_stn[FP_ST_TILES], s_stw[FP_ST_TILES];
     for (uint32_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
         const uint32_t i0 = blk * FP_B + threadIdx.x * FP_PER;
+        if (fin) {
+            if (threadIdx.x == 0) s_t0 = U[blk * FP_B].a.x / TILE;
+            if (threadIdx.x < FP_ST_TILES) s_stn[threadIdx.x] = s_stw[threadIdx.x] = 0;
+        }
         unsigned long long x = 0;
         if (i0 < nu) {
             if (pb) {  // (after an incremental pass: its picks are bits; byte -> bit 0 of 8 bytes)
@@ -4701,13 +4782,10 @@ __device__ __forceinline__ void fp_turn_blocks(const ClauseView& cv, const LoopB
                         }
                         const uint4 ea = U[i].a;
                         b.tmis[turn - a] = ea.x;
-                        const uint4 v0 = U[i].v0;
+                        const uint4 v0 = KW == 4 ? b.fp_v4[i] : U[i].v0;
                         fp_for_vars<KW>(cv, U, i, ea, v0, [&](uint32_t v) { b.cover[v] = (uint8_t)stamp; });
                         if (ea.x / TILE != st_tile) {
-                            if (st_n) {
-                                atomicAdd(&b.tile_stats[2 * st_tile], (unsigned long long)st_n);
-                                atomicAdd(&b.tile_stats[2 * st_tile + 1], st_w);
-                            }
+                            if (st_n) fp_stat_add(b, s_t0, s_stn, s_stw, st_tile, st_n, st_w);
                             st_tile = ea.x / TILE;
                             st_n = 0;
                             st_w = 0;
@@ -4718,12 +4796,16 @@ __device__ __forceinline__ void fp_turn_blocks(const ClauseView& cv, const LoopB
                 }
                 P += pick ? 1u : 0u;
             }
-            if (st_n) {
-                atomicAdd(&b.tile_stats[2 * st_tile], (unsigned long long)st_n);
-                atomicAdd(&b.tile_stats[2 * st_tile + 1], st_w);
-            }
+            if (st_n) fp_stat_add(b, s_t0, s_stn, s_stw, st_tile, st_n, st_w);
         }
         __syncthreads();
+        if (fin) {
+            if (threadIdx.x < FP_ST_TILES && s_stn[threadIdx.x]) {
+                atomicAdd(&b.tile_stats[2 * (s_t0 + threadIdx.x)], (unsigned long long)s_stn[threadIdx.x]);
+                atomicAdd(&b.tile_stats[2 * (s_t0 + threadIdx.x) + 1], (unsigned long long)s_stw[threadIdx.x]);
+            }
+            __syncthreads();  // (s_t0 and the tally are rewritten for the next block)
+        }
     }
 }
 

@@ -990,7 +990,7 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
             if (const char* e = getenv("ALLL_RR_INC")) inc = inc && atoi(e) != 0;
             if (inc) {
                 if ((rc = dalloc(c, &b.fp_blocker, m + 1, 0xFF)) || (rc = dalloc(c, &b.fp_covby, (size_t)prob->n_vars + 1)) ||
-                    (rc = dalloc(c, &b.fp_vcnt, (size_t)prob->n_vars + 1)) || (rc = dalloc(c, &b.fp_dl, 3 * (size_t)m + 16 * std::min<size_t>(m, 1u << 16) + 64)) ||
+                    (rc = dalloc(c, &b.fp_sc, (size_t)prob->n_vars + 1)) || (rc = dalloc(c, &b.fp_dl, 3 * (size_t)m + 16 * std::min<size_t>(m, 1u << 16) + 64)) ||
                     (rc = dalloc(c, &b.fp_dmark, m + 1)) || (rc = dalloc(c, &b.fp_pbits, 2 * ((size_t)m / 8 + 80))) ||
                     (rc = dalloc(c, &b.fp_log, FP_LOG_WORDS)) ||
                     (rc = dalloc(c, &b.fp_lst, 2 * (size_t)m * ((rr_width >= 1 && rr_width <= 4) ? 4 : 8) + 16)))

@@ -39,6 +39,10 @@ def main():
                 for p, t in enumerate(tl):
                     if not t.any():
                         continue
+                    if p == len(tl) - 1:  # k_fp_bbuild's phases (workgroup 0)
+                        t0 = int(t[0])
+                        print("  bbuild wg0: " + " ".join(f"{(int(t[q]) - t0) % (1 << 32) / 100.0:.1f}" for q in range(1, 5)), flush=True)
+                        continue
                     t0 = int(t[0])
                     us = lambda x: (int(x) - t0) % (1 << 32) / 100.0  # 100 MHz ticks -> us
                     rr = [(int(t[8 + 2 * q]), us(t[9 + 2 * q])) for q in range(24) if t[9 + 2 * q]]

@@ -3783,7 +3783,7 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_detect(LoopBuffers b) {
     RRFpCtl* ctl = b.fp_ctl;
     if (ctl->state != FP_RUN || !ctl->inc) return;
     const uint32_t nu = ctl->nu, stamp = ctl->rep_serial;
-    if (blockIdx.x == 0 && threadIdx.x == 0) {  // (the wide repair's counters, k_fp_repair_wide)
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // (the wide rounds' barrier counter, k_fp_repair)
         if (uint32_t* t = fp_tlog(b, ctl->fp_iter)) t[0] = (uint32_t)wall_now();
         ctl->wlist = 0;
         ctl->wrounds = 0;
@@ -4046,20 +4046,21 @@ __device__ __forceinline__ bool fp_rw_barrier(RRFpCtl* ctl, uint32_t target) {
     return s_ok != 0;
 }
 
+// The wide rounds, by every workgroup of k_fp_repair's grid (groups of FP_RN lanes, per-workgroup
+// list segments; see above).  In: n, the detect list's length (list 0 of fp_dl); out: n, the
+// rounds' last list (segments of list `cur`, starts s_pre) or the detect list when no round ran,
+// the round stamp, rounds and entries decided.  Returns false when a barrier timed out or a
+// segment overflowed (the pass gives up).
 template <uint32_t KW>
-__global__ __launch_bounds__(FP_THREADS) void k_fp_repair_wide(ClauseView cv, LoopBuffers b) {
-    RRFpCtl* ctl = b.fp_ctl;
-    if (ctl->state != FP_RUN || !ctl->inc || ctl->nu > FP_REP_QMAX) return;
+__device__ bool fp_wide_rounds(const ClauseView& cv, const LoopBuffers& b, RRFpCtl* ctl, uint32_t* s_hk, uint32_t* s_pre,
+                               uint32_t& n, uint32_t& rid, uint32_t& r, uint32_t& work, uint32_t& cur, uint32_t* tl) {
     const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
     uint32_t* Q = reinterpret_cast<uint32_t*>(b.fp_pbits);  // the decisions, a bit per entry
     uint32_t* cnts = b.fp_dl + 3 * (size_t)b.m;  // [2][FP_RW_GRID]: the segments' lengths of a list
     const uint32_t G = gridDim.x, g = blockIdx.x, cap = b.m / G;  // (segment g of a list: cap entries at g cap)
-    __shared__ uint32_t s_hk[1u << FP_RH_BITS];
-    __shared__ uint32_t s_pre[FP_RW_GRID + 1];  // the current list's segment starts (round 0: one list)
+    const uint32_t gpw = blockDim.x / FP_RN;  // groups per workgroup
     __shared__ uint32_t s_nb, s_over;
-    uint32_t n = ctl->ndirty, rid = ctl->rep_serial, r = 0, cur = 0, work = 0;
     bool ok = true;
-    uint32_t* tl = g == 0 && threadIdx.x == 0 ? fp_tlog(b, ctl->fp_iter) : nullptr;
     if (tl) tl[1] = (uint32_t)wall_now();
     if (threadIdx.x == 0) s_over = 0;
     while (n > FP_RW_MIN && n <= FP_REP_CAP && ok && r < FP_REP_MAXR) {
@@ -4067,14 +4068,14 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_repair_wide(ClauseView cv, Lo
         work += n;
         const uint32_t* A = b.fp_dl + (size_t)cur * b.m;
         uint32_t* B = b.fp_dl + (size_t)(cur ^ 1) * b.m;
-        for (uint32_t q = threadIdx.x; q < (1u << FP_RH_BITS); q += FP_THREADS) s_hk[q] = 0xFFFFFFFFu;
+        for (uint32_t q = threadIdx.x; q < (1u << FP_RH_BITS); q += blockDim.x) s_hk[q] = 0xFFFFFFFFu;
         if (threadIdx.x == 0) s_nb = 0;
         __syncthreads();
         // a group of FP_RN lanes per entry (fp_grp_step); every lane runs every step
         FpPolWide pol{&b, Q, s_hk, &s_nb, B + (size_t)g * cap, rid, cap, false};
-        const uint32_t ng = G * (FP_THREADS / FP_RN);
+        const uint32_t ng = G * gpw;
         for (uint32_t j0 = 0; j0 < n; j0 += ng) {
-            const uint32_t j = j0 + g * (FP_THREADS / FP_RN) + threadIdx.x / FP_RN;
+            const uint32_t j = j0 + g * gpw + threadIdx.x / FP_RN;
             uint32_t x = ~0u;
             if (j < n) {
                 if (r == 0) {
@@ -4115,24 +4116,7 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_repair_wide(ClauseView cv, Lo
         n = s_pre[G];
         cur ^= 1;
     }
-    // the list the rounds left (segments of list cur) into list cur ^ 1 as one list for
-    // k_fp_repair (the detect list as it is when no round ran)
-    uint32_t wl = 0;
-    if (r > 0 && ok) {
-        const uint32_t* A = b.fp_dl + (size_t)cur * b.m;
-        uint32_t* C = b.fp_dl + (size_t)(cur ^ 1) * b.m;
-        const uint32_t c0 = s_pre[g], c = s_pre[g + 1] - c0;
-        for (uint32_t i = threadIdx.x; i < c && c0 + i < b.m; i += FP_THREADS) C[c0 + i] = A[(size_t)g * cap + i];
-        wl = cur ^ 1;
-    }
-    if (g == 0 && threadIdx.x == 0) {
-        ctl->wlist = wl;
-        ctl->ndirty = n;
-        ctl->rep_serial = rid;
-        ctl->wrounds = r;
-        ctl->wwork = work;
-        if (!ok) ctl->wfail = 1;
-    }
+    return ok;
 }
 
 __device__ __forceinline__ void fp_sched_core(const LoopBuffers& b, RRFpCtl* ctl, int test, bool bail, uint32_t ch,
@@ -4142,17 +4126,21 @@ __device__ __forceinline__ void fp_sched_core(const LoopBuffers& b, RRFpCtl* ctl
 // The end of an incremental pass: the rounds, then (as k_fp_count + k_fp_sched after a full
 // pass) the pass test and the next pass's schedule, in this same workgroup: the block pick counts
 // and the sets' in-block counts move by the pass's net changes only.
+// One launch of FP_RW_GRID workgroups (all resident: one per CU by its LDS): every workgroup
+// takes part in the wide rounds (fp_wide_rounds), then workgroup 0 alone runs the small rounds,
+// the write-back, the pass test and the schedule.  (The wide rounds as a kernel of their own cost
+// a launch per pass even when there was nothing for them: ~4.5 us.)
 template <uint32_t KW>
 __global__ __launch_bounds__(1024) void k_fp_repair(ClauseView cv, LoopBuffers b) {
     RRFpCtl* ctl = b.fp_ctl;
     const uint32_t state = ctl->state;
     if (state == FP_FINAL) {  // (as k_fp_sched: the finalizing k_fp_turn has run)
-        if (threadIdx.x == 0) ctl->state = FP_DONE;
+        if (blockIdx.x == 0 && threadIdx.x == 0) ctl->state = FP_DONE;
         return;
     }
     if (state != FP_RUN) return;
     if (!ctl->inc) {  // a full pass is due (one of the other kind in the graph): nothing to test
-        if (threadIdx.x == 0) ctl->skip = 1;
+        if (blockIdx.x == 0 && threadIdx.x == 0) ctl->skip = 1;
         return;
     }
     const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
@@ -4160,13 +4148,17 @@ __global__ __launch_bounds__(1024) void k_fp_repair(ClauseView cv, LoopBuffers b
     __shared__ uint32_t s_nb;
     __shared__ uint32_t s_hk[1u << FP_RH_BITS];
     __shared__ uint32_t s_l[2][FP_RL];  // the rounds' dirty lists (their first FP_RL entries)
+    __shared__ uint32_t s_pre[FP_RW_GRID + 1];  // (the wide rounds' list segments)
     // global spill of the lists past FP_RL: index i of list c lives at s_l[c][i] or fp_dl[c m + i]
     const uint32_t nu = ctl->nu, nw = (nu + 31) / 32;
-    // (after the wide rounds: their list, round stamp and statistics)
-    const uint32_t n0 = ctl->ndirty, wl = ctl->wlist;
-    uint32_t n = n0, rid = ctl->rep_serial, rounds = ctl->wrounds, work = ctl->wwork, cur = 0;
-    bool bail = nu > FP_REP_QMAX || ctl->wfail;
-    uint32_t* tl = threadIdx.x == 0 ? fp_tlog(b, ctl->fp_iter) : nullptr;
+    const uint32_t n0 = ctl->ndirty;
+    uint32_t n = n0, rid = ctl->rep_serial, rounds = 0, work = 0, cur = 0, wcur = 0;
+    uint32_t* tl = blockIdx.x == 0 && threadIdx.x == 0 ? fp_tlog(b, ctl->fp_iter) : nullptr;
+    bool bail = nu > FP_REP_QMAX;
+    if (!bail) bail = !fp_wide_rounds<KW>(cv, b, ctl, s_hk, s_pre, n, rid, rounds, work, wcur, tl);
+    if (blockIdx.x != 0) return;
+    // (a wide round leaves at most FP_RW_MIN entries unless the pass gives up: all in LDS below)
+    if (rounds > 0 && n > FP_RL) bail = true;
     if (tl) tl[2] = (uint32_t)wall_now();
     if (n0 == 0 && rounds == 0 && !bail) {
         // nothing to repair: the picks repeat, the pass converged, and the counts and the
@@ -4216,12 +4208,22 @@ __global__ __launch_bounds__(1024) void k_fp_repair(ClauseView cv, LoopBuffers b
                     if (4 * q + k < nw) s_q[4 * q + k] = e[k];
             }
         }
-        // the list the wide rounds left (list wl of fp_dl) becomes list 0 (LDS part + global part)
-        const uint32_t* src_l = b.fp_dl + (size_t)wl * b.m;
-        for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) {
-            const uint32_t x = src_l[j];
-            if (j < FP_RL) s_l[0][j] = x;
-            else if (wl) b.fp_dl[j] = x;
+        // the list the wide rounds left (segments of list wcur) or k_fp_detect's (list 0) becomes
+        // list 0 (LDS part + global part)
+        if (rounds > 0) {
+            const uint32_t* A = b.fp_dl + (size_t)wcur * b.m;
+            const uint32_t G = gridDim.x, cap = b.m / G;
+            for (uint32_t j = threadIdx.x; j < n; j += blockDim.x) {
+                uint32_t lo = 0, hi = G;
+                while (hi - lo > 1) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (s_pre[mid] <= j) lo = mid;
+                    else hi = mid;
+                }
+                s_l[0][j] = A[(size_t)lo * cap + (j - s_pre[lo])];  // (n <= FP_RL)
+            }
+        } else {
+            for (uint32_t j = threadIdx.x; j < n && j < FP_RL; j += blockDim.x) s_l[0][j] = b.fp_dl[j];
         }
         __syncthreads();
         if (tl) tl[5] = (uint32_t)wall_now();
@@ -5152,11 +5154,10 @@ hipError_t launch_rr_passes(const ClauseView& cv, const LoopBuffers& b, uint32_t
             // an incremental pass (its kernels run only when the device state asks for one)
             k_fp_detect<<<g.gl, FP_THREADS, 0, s>>>(b);
             const size_t lq = ((size_t)std::min<uint64_t>(b.m, FP_REP_QMAX) + 127) / 128 * 16;  // (uint4 rows)
-            const uint32_t gw = std::min<uint32_t>(FP_RW_GRID, std::max<uint32_t>(1, b.n_cu));  // (all resident)
-            if (g.narrow) k_fp_repair_wide<4><<<gw, FP_THREADS, 0, s>>>(cv, b);
-            else k_fp_repair_wide<0><<<gw, FP_THREADS, 0, s>>>(cv, b);
-            if (g.narrow) k_fp_repair<4><<<1, 1024, lq, s>>>(cv, b);
-            else k_fp_repair<0><<<1, 1024, lq, s>>>(cv, b);
+            // (all resident: one workgroup per CU by its LDS)
+            const uint32_t gw = std::min<uint32_t>(FP_RW_GRID, std::max<uint32_t>(1, b.n_cu));
+            if (g.narrow) k_fp_repair<4><<<gw, 1024, lq, s>>>(cv, b);
+            else k_fp_repair<0><<<gw, 1024, lq, s>>>(cv, b);
             // (the repair ran the pass test and the schedule: the turns follow)
             if (g.narrow) k_fp_turn<4><<<g.gb, FP_THREADS, 0, s>>>(cv, b);
             else k_fp_turn<0><<<g.gb, FP_THREADS, 0, s>>>(cv, b);

@@ -423,6 +423,10 @@ def main():
         tj = json.load(open(args.traffic_json))
         if tj.get("config") == args.config and tj.get("n_gpus", 1) == world:
             traffic = tj.get("hbm_bytes_per_launch")
+            # (the roofline prices the evaluation alone: its own kernel's counters when recorded)
+            for k, v in (tj.get("per_kernel") or {}).items():
+                if s.eval_kernel() in k.split("(")[0] and "hbm_bytes_per_launch" in v:
+                    traffic = v["hbm_bytes_per_launch"]
     except (OSError, ValueError):
         pass
 

@@ -46,9 +46,14 @@ for k, v in res.items():
     if "TCC_HIT_sum" in v:
         v["l2_hit_rate"] = v["TCC_HIT_sum"] / max(1.0, v["TCC_HIT_sum"] + v["TCC_MISS_sum"])
         print(f"   L2 hit rate {v['l2_hit_rate']:.3f}")
-# bench-format record (bench.py --traffic-json): the dominant eval kernel of this config
+# bench-format record (bench.py --traffic-json): the roofline's kernel, the evaluation alone
+# (k_eval_hybrid / k_eval_ragged / ...: not the fused k_eval_scatter, whose bytes include the
+# round-0 scatter); the other kernels stay under per_kernel
 out = {"config": config, "n_gpus": 1, "per_kernel": res}
 main = [k for k in res if "hbm_bytes_per_launch" in res[k]]
+alone = [k for k in main if "k_eval_scatter" not in k]
+if alone:
+    main = alone
 if main:
     k = max(main, key=lambda k: res[k]["hbm_bytes_per_launch"])
     out.update(kernel=k, hbm_bytes_per_launch=res[k]["hbm_bytes_per_launch"],

@@ -2473,14 +2473,14 @@ __global__ __launch_bounds__(256) void k_rr_entries(ClauseView cv, LoopBuffers b
             // cleared (k_fp_bbuild sets them)
             out[i].a = a;
             b.fp_v4[base + i] = v0;
-            reinterpret_cast<uint32_t*>(b.fp_sole)[base + i] = 0u;
+            if (!b.fp_lst) reinterpret_cast<uint32_t*>(b.fp_sole)[base + i] = 0u;
         } else {
             RREnt e;
             e.a = a;
             e.v0 = v0;
             e.v1 = make_uint4(v[4], v[5], v[6], v[7]);
             out[i] = e;
-            if (b.fp_ctl) reinterpret_cast<uint2*>(b.fp_sole)[base + i] = make_uint2(0u, 0u);
+            if (b.fp_ctl && !b.fp_lst) reinterpret_cast<uint2*>(b.fp_sole)[base + i] = make_uint2(0u, 0u);
         }
     }
 }
@@ -3063,6 +3063,21 @@ __device__ __forceinline__ uint32_t fp_bytes_bits(uint32_t x) {  // bytes 0 / 1 
 }
 template <uint32_t KW>
 __device__ __forceinline__ uint32_t fp_sole_mask(const LoopBuffers& b, uint32_t i) {
+    if (b.fp_lst) {
+        // incremental passes: a sole slot is a claimant list of one (the entry itself), read from
+        // the entry's list rows (k_fp_bbuild writes them anyway; the sole bytes would be another
+        // scattered store per single-claimant variable).  Bits past the width are don't-care.
+        constexpr uint32_t RW = KW == 4 ? 4u : 8u;
+        const uint4* rows = reinterpret_cast<const uint4*>(b.fp_lst) + (uint64_t)i * (RW / 2);
+        uint32_t m = 0;
+#pragma unroll
+        for (uint32_t h = 0; h < RW / 2; ++h) {
+            const uint4 r2 = rows[h];
+            m |= (r2.y == 1u ? 1u : 0u) << (2 * h);
+            m |= (r2.w == 1u ? 1u : 0u) << (2 * h + 1);
+        }
+        return m;
+    }
     if constexpr (KW == 4) {
         return fp_bytes_bits(reinterpret_cast<const uint32_t*>(b.fp_sole)[i]);
     } else {
@@ -3356,9 +3371,11 @@ __global__ __launch_bounds__(FP_BB_THREADS) void k_fp_bbuild(LoopBuffers b) {
         base = __shfl(base, 0, 64);
         if (c && b.fp_sc) b.fp_sc[v] = make_uint2(s_off[w], c);  // (incremental passes: the list)
         if (c == 1u) {
+            // (the ownership is read for slots past the sole bytes only: wide entries; the sole
+            // byte, when there are no list rows to tell it: fp_sole_mask)
             const uint32_t x = s_first[w], i = x & FP_IMASK, j = x >> FP_SLOT_SH;
-            b.fp_own0[v] = i;
-            if (j < sw) b.fp_sole[(uint64_t)i * sw + j] = 1u;
+            if (sw == 8u) b.fp_own0[v] = i;
+            if (j < sw && !b.fp_lst) b.fp_sole[(uint64_t)i * sw + j] = 1u;
         } else if (shared) {
             sv[base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull))] = make_uint4(s_off[w], c, v, 0u);
             if (c > FP_HEAVY) {  // long lists (hubs of skewed instances): a wave per FP_SEG claimants

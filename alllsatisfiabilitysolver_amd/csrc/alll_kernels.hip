@@ -4048,7 +4048,10 @@ __device__ __forceinline__ bool fp_rw_barrier(RRFpCtl* ctl, uint32_t target) {
     __syncthreads();
     if (threadIdx.x == 0) {
         uint32_t ok = 1;
-        __threadfence();  // (release: this workgroup's decisions, log and list entries)
+        // release (the XCD L2's dirty lines written back: this workgroup's decisions and list
+        // entries), then the arrival; acquire (the CU's L1 invalidated) after the poll.  (Two
+        // __threadfence() -- each both -- cost more per round.)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the write-back completes before the arrival)
         atomicAdd(&ctl->wbar, 1u);
         const unsigned long long t0 = wall_now();
@@ -4056,7 +4059,8 @@ __device__ __forceinline__ bool fp_rw_barrier(RRFpCtl* ctl, uint32_t target) {
             if (wall_now() - t0 > FP_RW_TIMEOUT) { ok = 0; break; }
             __builtin_amdgcn_s_sleep(1);
         }
-        __threadfence();  // (acquire: the CU's L1 holds no line older than the barrier)
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the invalidate completes before the barrier below)
         s_ok = ok;
     }
     __syncthreads();

@@ -3821,15 +3821,20 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_detect(LoopBuffers b) {
 }
 
 // The repair's view of an entry x: the claimant lists of its variables (fp_vlist; the entry's
-// list rows {start, length} in fp_lst, k_fp_bbuild) hold its neighbours y != x.  A group of FP_RN
-// lanes decides one entry: lane u takes slot u of the concatenated lists, so a decision is three
-// dependent round trips (x's turn and list rows, the list slot, its turn and decision) and a few
-// dozen instructions per lane (the rows loaded per decision from the variables and fp_sc instead:
-// one more round trip, the same iteration time as the rows' scattered stores in k_fp_bbuild); the rare entry with more slots (or wider than its rows) has its group
-// stride every list in turn.  (One lane per entry with all FP_RN slots unrolled ran ~4x the
-// instructions: a one-entry round took ~5 us.)
-constexpr uint32_t FP_RN = 16;  // lanes per entry (the entry's own slots included: ~99.9% of the dirty
-                                // entries at M fit)
+// list rows {start, length} in fp_lst, k_fp_bbuild) hold its neighbours y != x.  A group of
+// FP_LPE lanes decides one entry: lane u takes slots u and u + FP_LPE of the concatenated lists
+// (FP_RN slots in all), so a decision is three dependent round trips (x's turn and list rows,
+// the list slots, their turns and decisions) and a few dozen instructions per lane; the rare
+// entry with more slots (or wider than its rows) has its group stride every list in turn.
+// (One lane per entry with all FP_RN slots unrolled ran ~4x the instructions: a one-entry
+// round took ~5 us; 16 lanes of one slot each: half the entries per step of a workgroup.  The
+// rows loaded per decision from the variables and fp_sc instead of fp_lst: one more round trip,
+// the same iteration time as the rows' scattered stores in k_fp_bbuild.)
+constexpr uint32_t FP_RN = 16;   // list slots decided at once (the entry's own included: ~99.9% of the
+                                 // dirty entries at M fit)
+constexpr uint32_t FP_LPE = 8;        // lanes per entry in the one-workgroup rounds (2 slots per lane)
+constexpr uint32_t FP_LPE_WIDE = 16;  // ... in the wide rounds (one step of the grid holds a round anyway;
+                                      // 8 lanes per entry: ~1 us slower per wide round)
 
 // decision of entry y in the repair's bits
 __device__ __forceinline__ uint32_t fp_q(const uint32_t* sq, uint32_t y) { return (sq[y >> 5] >> (y & 31u)) & 1u; }
@@ -3837,16 +3842,17 @@ __device__ __forceinline__ unsigned long long fp_tkey(uint32_t t, uint32_t y) {
     return ((unsigned long long)t << 32) | y;
 }
 
-// One entry per group of FP_RN lanes (x == ~0u: an idle group; every lane of the wave calls it).
+// One entry per group of FP_LPE lanes (x == ~0u: an idle group; every lane of the wave calls it).
 // Decides x against the current decisions (pol.q), records its blocker, stores a changed
 // decision (pol.set) and pushes the neighbours above a changed entry
 // (pol.push, pol.push1: the next round's list).  Policies: FpPolLds (one workgroup, LDS bits and
 // lists), FpPolWide (the wide rounds, global bits).
-template <uint32_t KW, typename P>
+template <uint32_t KW, uint32_t LPE, typename P>
 __device__ __forceinline__ void fp_grp_step(const ClauseView& cv, const LoopBuffers& b, const RREnt* U, uint32_t x,
                                             P& pol) {
     constexpr uint32_t RW = KW == 4 ? 4u : 8u;
-    const uint32_t lane = threadIdx.x & 63, gl = lane & (FP_RN - 1), g0 = lane & ~(FP_RN - 1);
+    constexpr uint32_t FP_SPL = FP_RN / LPE;  // slots per lane
+    const uint32_t lane = threadIdx.x & 63, gl = lane & (LPE - 1), g0 = lane & ~(LPE - 1);
     const bool act = x != ~0u;
     unsigned long long kx = 0;
     uint32_t w = 0, tot = 0, so[RW], cn[RW];
@@ -3872,29 +3878,38 @@ __device__ __forceinline__ void fp_grp_step(const ClauseView& cv, const LoopBuff
         }
     }
     const bool fast = act && w <= RW && tot <= FP_RN, slow = act && !fast;
-    // fast: slot gl of the lists
-    uint32_t y = ~0u;
-    if (fast && gl < tot) {
-        uint32_t r = gl, pos = 0;
-        bool found = false;
+    // fast: slots gl + t FP_LPE of the lists (all loads of a level in flight together)
+    uint32_t y[FP_SPL];
 #pragma unroll
-        for (uint32_t k = 0; k < RW; ++k) {
-            if (!found && r < cn[k]) {
-                pos = so[k] + r;
-                found = true;
-            } else if (!found) {
-                r -= cn[k];
+    for (uint32_t t = 0; t < FP_SPL; ++t) {
+        const uint32_t u = gl + t * LPE;
+        y[t] = ~0u;
+        if (fast && u < tot) {
+            uint32_t r = u, pos = 0;
+            bool found = false;
+#pragma unroll
+            for (uint32_t k = 0; k < RW; ++k) {
+                if (!found && r < cn[k]) {
+                    pos = so[k] + r;
+                    found = true;
+                } else if (!found) {
+                    r -= cn[k];
+                }
             }
+            y[t] = b.fp_vlist[pos];
         }
-        y = b.fp_vlist[pos];
     }
-    bool below = false, above = false;
-    if (y != ~0u && y != x) {
-        const unsigned long long ky = fp_tkey(b.fp_turn[y], y);
-        below = ky < kx && pol.q(y);
-        above = ky > kx;
+    bool above[FP_SPL];
+    uint32_t by = ~0u;  // a pick below x sharing a variable (this lane's)
+#pragma unroll
+    for (uint32_t t = 0; t < FP_SPL; ++t) {
+        above[t] = false;
+        if (y[t] != ~0u && y[t] != x) {
+            const unsigned long long ky = fp_tkey(b.fp_turn[y[t]], y[t]);
+            if (ky < kx && pol.q(y[t])) by = y[t];
+            above[t] = ky > kx;
+        }
     }
-    uint32_t by = below ? y : ~0u;  // a pick below x sharing a variable (this lane's)
     // slow: the group strides every list of the entry
     auto each = [&](auto f) {
         uint4 a, v0;
@@ -3903,7 +3918,7 @@ __device__ __forceinline__ void fp_grp_step(const ClauseView& cv, const LoopBuff
             const uint2 sc = b.fp_sc[v];
             const uint32_t s0 = sc.x, c = sc.y;
 #pragma unroll 1
-            for (uint32_t q = gl; q < c; q += FP_RN) {
+            for (uint32_t q = gl; q < c; q += LPE) {
                 const uint32_t z = b.fp_vlist[s0 + q];
                 if (z != x) f(z, fp_tkey(b.fp_turn[z], z));
             }
@@ -3913,7 +3928,7 @@ __device__ __forceinline__ void fp_grp_step(const ClauseView& cv, const LoopBuff
         each([&](uint32_t z, unsigned long long kz) {
             if (kz < kx && pol.q(z)) by = z;
         });
-    const uint32_t gm = (uint32_t)(__ballot(by != ~0u) >> g0) & ((1u << FP_RN) - 1u);
+    const uint32_t gm = (uint32_t)(__ballot(by != ~0u) >> g0) & ((1u << LPE) - 1u);
     const bool in = gm == 0;
     const uint32_t bky = __shfl(by, (int)(g0 + (gm ? (uint32_t)__ffs(gm) - 1u : 0u)), 64);
     bool ch = false;
@@ -3923,7 +3938,8 @@ __device__ __forceinline__ void fp_grp_step(const ClauseView& cv, const LoopBuff
         if (ch) pol.set(x, in);
     }
     const bool gch = (__ballot(ch) >> g0) & 1ull;
-    pol.push(gch && above, y);
+#pragma unroll
+    for (uint32_t t = 0; t < FP_SPL; ++t) pol.push(gch && above[t], y[t]);
     if (__ballot(gch && slow))
         if (gch && slow)
             each([&](uint32_t z, unsigned long long kz) {
@@ -4067,7 +4083,7 @@ __device__ __forceinline__ bool fp_rw_barrier(RRFpCtl* ctl, uint32_t target) {
     return s_ok != 0;
 }
 
-// The wide rounds, by every workgroup of k_fp_repair's grid (groups of FP_RN lanes, per-workgroup
+// The wide rounds, by every workgroup of k_fp_repair's grid (groups of FP_LPE lanes, per-workgroup
 // list segments; see above).  In: n, the detect list's length (list 0 of fp_dl); out: n, the
 // rounds' last list (segments of list `cur`, starts s_pre) or the detect list when no round ran,
 // the round stamp, rounds and entries decided.  Returns false when a barrier timed out or a
@@ -4079,7 +4095,7 @@ __device__ bool fp_wide_rounds(const ClauseView& cv, const LoopBuffers& b, RRFpC
     uint32_t* Q = reinterpret_cast<uint32_t*>(b.fp_pbits);  // the decisions, a bit per entry
     uint32_t* cnts = b.fp_dl + 3 * (size_t)b.m;  // [2][FP_RW_GRID]: the segments' lengths of a list
     const uint32_t G = gridDim.x, g = blockIdx.x, cap = b.m / G;  // (segment g of a list: cap entries at g cap)
-    const uint32_t gpw = blockDim.x / FP_RN;  // groups per workgroup
+    const uint32_t gpw = blockDim.x / FP_LPE_WIDE;  // groups per workgroup
     __shared__ uint32_t s_nb, s_over;
     bool ok = true;
     if (tl) tl[1] = (uint32_t)wall_now();
@@ -4092,11 +4108,11 @@ __device__ bool fp_wide_rounds(const ClauseView& cv, const LoopBuffers& b, RRFpC
         for (uint32_t q = threadIdx.x; q < (1u << FP_RH_BITS); q += blockDim.x) s_hk[q] = 0xFFFFFFFFu;
         if (threadIdx.x == 0) s_nb = 0;
         __syncthreads();
-        // a group of FP_RN lanes per entry (fp_grp_step); every lane runs every step
+        // a group of FP_LPE_WIDE lanes per entry (fp_grp_step); every lane runs every step
         FpPolWide pol{&b, Q, s_hk, &s_nb, B + (size_t)g * cap, rid, cap, false};
         const uint32_t ng = G * gpw;
         for (uint32_t j0 = 0; j0 < n; j0 += ng) {
-            const uint32_t j = j0 + g * gpw + threadIdx.x / FP_RN;
+            const uint32_t j = j0 + g * gpw + threadIdx.x / FP_LPE_WIDE;
             uint32_t x = ~0u;
             if (j < n) {
                 if (r == 0) {
@@ -4111,7 +4127,7 @@ __device__ bool fp_wide_rounds(const ClauseView& cv, const LoopBuffers& b, RRFpC
                     x = A[(size_t)lo * cap + (j - s_pre[lo])];
                 }
             }
-            fp_grp_step<KW>(cv, b, U, x, pol);
+            fp_grp_step<KW, FP_LPE_WIDE>(cv, b, U, x, pol);
         }
         if (pol.over) s_over = 1;
         __syncthreads();
@@ -4266,12 +4282,12 @@ __global__ __launch_bounds__(1024) void k_fp_repair(ClauseView cv, LoopBuffers b
         const uint32_t* ga = b.fp_dl + (size_t)cur * b.m;
         uint32_t* lb = s_l[cur ^ 1];
         uint32_t* gb = b.fp_dl + (size_t)(cur ^ 1) * b.m;
-        // a group of FP_RN lanes per entry (fp_grp_step); every lane runs every step
+        // a group of FP_LPE lanes per entry (fp_grp_step); every lane runs every step
         FpPolLds pol{&b, s_q, s_hk, &s_nb, lb, gb, rid, false};
-        constexpr uint32_t NG = 1024 / FP_RN;
+        constexpr uint32_t NG = 1024 / FP_LPE;
         for (uint32_t j0 = 0; j0 < n; j0 += NG) {
-            const uint32_t j = j0 + threadIdx.x / FP_RN;
-            fp_grp_step<KW>(cv, b, U, j < n ? (j < FP_RL ? la[j] : ga[j]) : ~0u, pol);
+            const uint32_t j = j0 + threadIdx.x / FP_LPE;
+            fp_grp_step<KW, FP_LPE>(cv, b, U, j < n ? (j < FP_RL ? la[j] : ga[j]) : ~0u, pol);
         }
         const bool sp = pol.sp;
         // (only the next list's global part crosses waves within the rounds: the blockers are

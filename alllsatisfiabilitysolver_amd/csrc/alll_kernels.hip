@@ -4317,8 +4317,7 @@ __global__ __launch_bounds__(1024) void k_fp_repair(ClauseView cv, LoopBuffers b
         if (threadIdx.x <= T) { s_sf[threadIdx.x] = r_sf; s_bnd[threadIdx.x] = r_bnd; }
     }
     for (uint32_t k = threadIdx.x; k < nblk; k += blockDim.x) s_touch[k] = 0;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    __syncthreads();  // (the rounds' blocker stores are for the next pass: no wait)
     if (!bail) {
         const uint4* old4 = reinterpret_cast<const uint4*>(fp_pold(b));
         uint4* wk4 = reinterpret_cast<uint4*>(b.fp_pbits);
@@ -4365,31 +4364,41 @@ __global__ __launch_bounds__(1024) void k_fp_repair(ClauseView cv, LoopBuffers b
         const uint32_t wch = wave_incl_add(my_ch);
         if ((threadIdx.x & 63) == 63 && wch) atomicAdd(&s_ch, wch);
         __syncthreads();
-        // the marked blocks' pick counts recounted from the decisions (a wave per block), then the
-        // in-block counts of the set starts in them
-        const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-        for (uint32_t k0 = 64 * wave; k0 < nblk; k0 += blockDim.x) {  // (64 blocks per wave and step)
-            unsigned long long tb = __ballot(k0 + lane < nblk && s_touch[k0 + lane]);
-            while (tb) {
-                const uint32_t k = k0 + (uint32_t)__ffsll((long long)tb) - 1u;
-                tb &= tb - 1ull;
-                const uint32_t wd = k * (FP_B / 32) + lane;  // (FP_B / 32 == 64 words per block)
+        if (tl) tl[57] = (uint32_t)wall_now();  // (measurement: the comparison done)
+        // the marked blocks' pick counts recounted from the decisions (a thread per block, its 64
+        // words read in an order rotated by the block index so the threads' LDS reads spread over
+        // the banks), and the in-block counts of the set starts in them (a thread per set, from the
+        // top of the workgroup)
+        for (uint32_t k = threadIdx.x; k < nblk; k += blockDim.x) {
+            if (!s_touch[k]) continue;
+            const uint32_t w0 = k * (FP_B / 32);  // (FP_B / 32 == 64 words per block)
+            uint32_t c = 0;
+#pragma unroll 8
+            for (uint32_t i = 0; i < FP_B / 32; ++i) {
+                const uint32_t wd = w0 + ((i + k) & (FP_B / 32 - 1u));
                 uint32_t bits = wd < nw ? s_q[wd] : 0u;
                 if (wd == nw - 1) bits &= tail;
-                const uint32_t c = wave_incl_add((uint32_t)__popc(bits));
-                if (lane == 63) s_blk[k] = c;
+                c += (uint32_t)__popc(bits);
             }
+            s_blk[k] = c;
         }
-        if (threadIdx.x <= T) {
-            const uint32_t f = s_sf[threadIdx.x];
+        const uint32_t ts = blockDim.x - 1u - threadIdx.x;
+        if (ts <= T) {
+            const uint32_t f = s_sf[ts];
             if (f < nu && s_touch[f / FP_B]) {
+                const uint32_t w0 = (f / FP_B) * (FP_B / 32), we = f / 32;
                 uint32_t c = 0;
-                for (uint32_t wd = (f / FP_B) * (FP_B / 32); wd < f / 32; ++wd) c += (uint32_t)__popc(s_q[wd]);
-                if (f & 31u) c += (uint32_t)__popc(s_q[f / 32] & ((1u << (f & 31u)) - 1u));
-                s_bnd[threadIdx.x] = c;
+#pragma unroll 8
+                for (uint32_t i = 0; i < FP_B / 32; ++i) {
+                    const uint32_t wd = w0 + ((i + ts) & (FP_B / 32 - 1u));
+                    if (wd < we) c += (uint32_t)__popc(s_q[wd]);
+                }
+                if (f & 31u) c += (uint32_t)__popc(s_q[we] & ((1u << (f & 31u)) - 1u));
+                s_bnd[ts] = c;
             }
         }
         __syncthreads();  // (the working bits' stores are for the next kernels: no wait)
+        if (tl) tl[59] = (uint32_t)wall_now();  // (measurement: the recount done)
     }
     if (threadIdx.x == 0) {
         ctl->rep_serial = rid + 1;

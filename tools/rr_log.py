@@ -46,9 +46,9 @@ def main():
                     t0 = int(t[0])
                     us = lambda x: (int(x) - t0) % (1 << 32) / 100.0  # 100 MHz ticks -> us
                     rr = [(int(t[8 + 2 * q]), us(t[9 + 2 * q])) for q in range(24) if t[9 + 2 * q]]
-                    wb = [us(t[56 + 2 * q]) for q in range(4) if t[56 + 2 * q]]
+                    wb = [us(t[56 + 2 * q]) for q in range(4) if t[56 + 2 * q] and (q == 0 or t[56 + 2 * q] != t[57])]
                     print(f"  pass {p}: wide@{us(t[1]):.1f} rep@{us(t[2]):.1f} lds@{us(t[5]):.1f} "
-                          f"rounds_end@{us(t[3]):.1f} sched@{us(t[6]):.1f} phases@{us(t[7]):.1f} end@{us(t[4]):.1f} | "
+                          f"rounds_end@{us(t[3]):.1f} cmp@{us(t[57]):.1f} recount@{us(t[59]):.1f} sched@{us(t[6]):.1f} phases@{us(t[7]):.1f} end@{us(t[4]):.1f} | "
                           + " ".join(f"{n}@{x:.1f}" for n, x in rr)
                           + (" | wide pre-barrier " + " ".join(f"{x:.1f}" for x in wb) if wb else ""), flush=True)
 

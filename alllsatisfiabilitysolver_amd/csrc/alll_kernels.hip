@@ -3798,8 +3798,18 @@ __device__ __forceinline__ unsigned long long fp_order_key(const LoopBuffers& b,
 
 __global__ __launch_bounds__(FP_THREADS) void k_fp_detect(LoopBuffers b) {
     RRFpCtl* ctl = b.fp_ctl;
-    if (ctl->state != FP_RUN || !ctl->inc) return;
-    const uint32_t nu = ctl->nu, stamp = ctl->rep_serial;
+    // (the first entry's pick byte, blocker and turn loaded before the state is read -- in bounds
+    // of their buffers, independent of each other: one round trip less per pass)
+    const uint32_t i1 = blockIdx.x * FP_THREADS + threadIdx.x;
+    uint32_t p_in = 1, p_bk = 0, p_t = 0;
+    if (i1 < b.m) {  // (the kernel runs with incremental passes only: fp_blocker exists)
+        p_in = b.fp_in[i1];
+        p_bk = b.fp_blocker[i1];
+        p_t = b.fp_turn[i1];
+    }
+    // (the control words read together: no chain of scalar loads behind the branches)
+    const uint32_t state = ctl->state, inc = ctl->inc, nu = ctl->nu, stamp = ctl->rep_serial;
+    if ((state != FP_RUN) | (inc == 0)) return;
     if (blockIdx.x == 0 && threadIdx.x == 0) {  // (the wide rounds' barrier counter, k_fp_repair)
         if (uint32_t* t = fp_tlog(b, ctl->fp_iter)) t[0] = (uint32_t)wall_now();
         ctl->wlist = 0;
@@ -3810,10 +3820,12 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_detect(LoopBuffers b) {
     }
     for (uint32_t i0 = blockIdx.x * FP_THREADS; i0 < nu; i0 += gridDim.x * FP_THREADS) {
         const uint32_t i = i0 + threadIdx.x;
+        const bool first = i == i1;
         bool d = false;
-        if (i < nu && !(b.fp_in[i] & 1u)) {
-            const uint32_t bk = b.fp_blocker[i];
-            d = bk >= nu || fp_order_key(b, bk) > fp_order_key(b, i);
+        if (i < nu && !((first ? p_in : b.fp_in[i]) & 1u)) {
+            const uint32_t bk = first ? p_bk : b.fp_blocker[i];
+            const unsigned long long ki = ((unsigned long long)(first ? p_t : b.fp_turn[i]) << 32) | i;
+            d = bk >= nu || fp_order_key(b, bk) > ki;
             if (d) b.fp_dmark[i] = stamp;
         }
         fp_append(d, i, &ctl->ndirty, b.fp_dl);  // (every lane of the wave calls it)
@@ -4745,11 +4757,19 @@ __device__ __forceinline__ void fp_stat_add(const LoopBuffers& b, uint32_t t0, u
 // Turns of every block of entries (grid-stride) for the next pass, or (fin) the MIS: picks in
 // step order into tmis (step minus the erasures before it), their variables covered with the
 // iteration's stamp, and the statistics of k_rr_mw.  blk_off(blk): picks before block blk.
+// the first block's words of a thread (its picks both ways and the block's offset), loaded by
+// k_fp_turn before it reads the state
+struct FpTurnPre {
+    unsigned long long in;
+    uint32_t by, off;
+    bool ok;
+};
+
 template <uint32_t KW, typename BlkOff>
 __device__ __forceinline__ void fp_turn_blocks(const ClauseView& cv, const LoopBuffers& b, bool fin, bool inc, bool pb, uint32_t nu,
                                                uint32_t T, uint32_t stamp, const uint32_t* s_sf,
                                                const uint32_t* s_pf, const uint32_t* s_nseg, const uint32_t* s_er,
-                                               const uint4* segs, uint32_t* s_w, BlkOff blk_off) {
+                                               const uint4* segs, uint32_t* s_w, BlkOff blk_off, FpTurnPre pre) {
     const RREnt* U = reinterpret_cast<const RREnt*>(b.rr_u);
     const uint32_t nblk = (nu + FP_B - 1) / FP_B;
     // (fin: the block's MIS statistics per clause tile in LDS -- its entries span a few
@@ -4762,20 +4782,21 @@ __device__ __forceinline__ void fp_turn_blocks(const ClauseView& cv, const LoopB
             if (threadIdx.x == 0) s_t0 = U[blk * FP_B].a.x / TILE;
             if (threadIdx.x < FP_ST_TILES) s_stn[threadIdx.x] = s_stw[threadIdx.x] = 0;
         }
+        const bool first = pre.ok && blk == blockIdx.x;
         unsigned long long x = 0;
         if (i0 < nu) {
             if (pb) {  // (after an incremental pass: its picks are bits; byte -> bit 0 of 8 bytes)
-                const uint32_t by = b.fp_pbits[i0 / 8];
+                const uint32_t by = first ? pre.by : b.fp_pbits[i0 / 8];
                 x = (unsigned long long)(((by & 15u) * 0x00204081u) & 0x01010101u) |
                     ((unsigned long long)(((by >> 4) * 0x00204081u) & 0x01010101u) << 32);
             } else {
-                x = *reinterpret_cast<const unsigned long long*>(b.fp_in + i0);
+                x = first ? pre.in : *reinterpret_cast<const unsigned long long*>(b.fp_in + i0);
             }
             if (nu - i0 < FP_PER) x &= (1ull << (8 * (nu - i0))) - 1ull;
         }
         const unsigned long long b0 = x & 0x0101010101010101ull;
         uint32_t tot;
-        uint32_t P = blk_off(blk) + fp_block_scan((uint32_t)__popcll(b0), s_w, tot);
+        uint32_t P = (first ? pre.off : blk_off(blk)) + fp_block_scan((uint32_t)__popcll(b0), s_w, tot);
         // the next pass sets bit 0 of its picks; these become bit 1 (k_fp_count compares them); an
         // incremental pass starts from them (bit 0 too), packed: the working bits it repairs and
         // the copy its net changes are taken against
@@ -4862,28 +4883,64 @@ __device__ __forceinline__ void fp_turn_blocks(const ClauseView& cv, const LoopB
 template <uint32_t KW>
 __global__ __launch_bounds__(FP_THREADS) void k_fp_turn(ClauseView cv, LoopBuffers b) {
     const RRFpCtl* ctl = b.fp_ctl;
-    const uint32_t state = ctl->state;
-    if (state != FP_RUN && state != FP_FINAL) return;
-    if (state == FP_RUN && ctl->skip) return;  // (k_fp_sched found no pass to test)
-    const bool fin = state == FP_FINAL;
+    const uint32_t T = b.rr_T;
+    const uint32_t* blkoff = b.fp_blk + (b.m / FP_B + 2);
+    // The first block's words and the schedule's tables are loaded before the state is read (each
+    // load within its buffer, none depending on another): one round trip before the first block
+    // instead of three.
+    FpTurnPre pre{0ull, 0u, 0u, false};
+    if (blockIdx.x < (b.m + FP_B - 1) / FP_B) {
+        const uint32_t i1 = blockIdx.x * FP_B + threadIdx.x * FP_PER;
+        pre.in = *reinterpret_cast<const unsigned long long*>(b.fp_in + i1);  // (fp_in: m + FP_B bytes)
+        pre.by = b.fp_pbits && i1 < b.m ? b.fp_pbits[i1 / 8] : 0u;  // (fp_pbits: incremental passes only)
+        pre.off = blkoff[blockIdx.x];
+        pre.ok = true;
+    }
+    const uint32_t s1 = threadIdx.x;  // (set s1 <= T; sets past FP_THREADS below)
+    uint32_t t_sf = 0, t_pf = 0, t_ns = 0, t_er = 0;
+    if (s1 <= T) {
+        t_sf = b.fp_sf[s1];
+        t_pf = b.fp_pf[s1];
+        if (s1 < T) { t_ns = b.fp_nseg[s1]; t_er = b.fp_erase[s1]; }
+    }
+    const bool lds_seg = T <= FP_LDS_SEG_T;
+    constexpr uint32_t SEG_PT = FP_LDS_SEG_T * FP_LDS_SEG_T / FP_THREADS;  // phase records per thread
+    uint4 t_seg[SEG_PT];
+#pragma unroll
+    for (uint32_t u = 0; u < SEG_PT; ++u) {
+        const uint32_t q = threadIdx.x + u * FP_THREADS;
+        t_seg[u] = lds_seg && q < T * T ? b.fp_seg[q] : make_uint4(0u, 0u, 0u, 0u);
+    }
     DevState* st = b.state;
+    // (the control words read together: no chain of scalar loads behind the branches)
+    const uint32_t state = ctl->state, skip = ctl->skip, nu = ctl->nu, inc = ctl->inc, pbsrc = ctl->pbsrc;
+    const uint32_t stamp = st->stamp;
+    if ((state != FP_RUN) & (state != FP_FINAL)) return;
+    if ((state == FP_RUN) & (skip != 0)) return;  // (k_fp_sched found no pass to test)
+    const bool fin = state == FP_FINAL;
     __shared__ uint32_t s_w[FP_THREADS / 64];
     __shared__ uint32_t s_sf[FP_TMAX + 1], s_pf[FP_TMAX + 1], s_nseg[FP_TMAX], s_er[FP_TMAX];
     __shared__ uint4 s_seg[FP_LDS_SEG_T * FP_LDS_SEG_T];  // the schedule itself when T is small
-    const uint32_t nu = ctl->nu, T = b.rr_T;
-    const uint32_t stamp = st->stamp;
-    const uint32_t* blkoff = b.fp_blk + (b.m / FP_B + 2);
-    for (uint32_t s = threadIdx.x; s <= T; s += blockDim.x) {
+    if (s1 <= T) {
+        s_sf[s1] = t_sf;
+        s_pf[s1] = t_pf;
+        if (s1 < T) { s_nseg[s1] = t_ns; s_er[s1] = t_er; }
+    }
+    for (uint32_t s = threadIdx.x + blockDim.x; s <= T; s += blockDim.x) {
         s_sf[s] = b.fp_sf[s];
         s_pf[s] = b.fp_pf[s];
         if (s < T) { s_nseg[s] = b.fp_nseg[s]; s_er[s] = b.fp_erase[s]; }
     }
-    const bool lds_seg = T <= FP_LDS_SEG_T;
-    if (lds_seg)
-        for (uint32_t q = threadIdx.x; q < T * T; q += blockDim.x) s_seg[q] = b.fp_seg[q];
+    if (lds_seg) {
+#pragma unroll
+        for (uint32_t u = 0; u < SEG_PT; ++u) {
+            const uint32_t q = threadIdx.x + u * FP_THREADS;
+            if (q < T * T) s_seg[q] = t_seg[u];
+        }
+    }
     __syncthreads();
-    fp_turn_blocks<KW>(cv, b, fin, ctl->inc != 0, ctl->pbsrc != 0, nu, T, stamp, s_sf, s_pf, s_nseg, s_er, lds_seg ? s_seg : b.fp_seg, s_w,
-                       [&](uint32_t blk) { return blkoff[blk]; });
+    fp_turn_blocks<KW>(cv, b, fin, inc != 0, pbsrc != 0, nu, T, stamp, s_sf, s_pf, s_nseg, s_er, lds_seg ? s_seg : b.fp_seg, s_w,
+                       [&](uint32_t blk) { return blkoff[blk]; }, pre);
     if (fin && blockIdx.x == 0 && threadIdx.x == 0) {
         st->tmis_cnt = ctl->total;
         st->tail_rounds = ctl->fp_iter;

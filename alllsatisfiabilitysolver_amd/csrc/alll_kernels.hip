@@ -4760,10 +4760,14 @@ __device__ __forceinline__ void fp_stat_add(const LoopBuffers& b, uint32_t t0, u
 // the first block's words of a thread (its picks both ways and the block's offset), loaded by
 // k_fp_turn before it reads the state
 struct FpTurnPre {
-    unsigned long long in;
-    uint32_t by, off;
+    uint32_t in, by, off;
     bool ok;
 };
+
+// k_fp_turn: FP_TPER entries per thread (half the count kernel's: twice the threads per block,
+// half the per-thread chain of set and phase lookups)
+constexpr uint32_t FP_TPER = 4;
+constexpr int FP_TURN_THREADS = FP_B / FP_TPER;
 
 template <uint32_t KW, typename BlkOff>
 __device__ __forceinline__ void fp_turn_blocks(const ClauseView& cv, const LoopBuffers& b, bool fin, bool inc, bool pb, uint32_t nu,
@@ -4777,40 +4781,44 @@ __device__ __forceinline__ void fp_turn_blocks(const ClauseView& cv, const LoopB
     constexpr uint32_t FP_ST_TILES = 64;
     __shared__ uint32_t s_t0, s_stn[FP_ST_TILES], s_stw[FP_ST_TILES];
     for (uint32_t blk = blockIdx.x; blk < nblk; blk += gridDim.x) {
-        const uint32_t i0 = blk * FP_B + threadIdx.x * FP_PER;
+        const uint32_t i0 = blk * FP_B + threadIdx.x * FP_TPER;
         if (fin) {
             if (threadIdx.x == 0) s_t0 = U[blk * FP_B].a.x / TILE;
             if (threadIdx.x < FP_ST_TILES) s_stn[threadIdx.x] = s_stw[threadIdx.x] = 0;
         }
         const bool first = pre.ok && blk == blockIdx.x;
-        unsigned long long x = 0;
+        static_assert(FP_TPER == 4, "a nibble of pick bits, 4 bytes of fp_in per thread");
+        uint32_t x = 0;
         if (i0 < nu) {
-            if (pb) {  // (after an incremental pass: its picks are bits; byte -> bit 0 of 8 bytes)
+            if (pb) {  // (after an incremental pass: its picks are bits; nibble -> bit 0 of 4 bytes)
                 const uint32_t by = first ? pre.by : b.fp_pbits[i0 / 8];
-                x = (unsigned long long)(((by & 15u) * 0x00204081u) & 0x01010101u) |
-                    ((unsigned long long)(((by >> 4) * 0x00204081u) & 0x01010101u) << 32);
+                x = (((by >> (i0 & 4u)) & 15u) * 0x00204081u) & 0x01010101u;
             } else {
-                x = first ? pre.in : *reinterpret_cast<const unsigned long long*>(b.fp_in + i0);
+                x = first ? pre.in : *reinterpret_cast<const uint32_t*>(b.fp_in + i0);
             }
-            if (nu - i0 < FP_PER) x &= (1ull << (8 * (nu - i0))) - 1ull;
+            if (nu - i0 < FP_TPER) x &= (1u << (8 * (nu - i0))) - 1u;
         }
-        const unsigned long long b0 = x & 0x0101010101010101ull;
+        const unsigned long long b0 = x & 0x01010101u;
         uint32_t tot;
         uint32_t P = (first ? pre.off : blk_off(blk)) + fp_block_scan((uint32_t)__popcll(b0), s_w, tot);
         // the next pass sets bit 0 of its picks; these become bit 1 (k_fp_count compares them); an
         // incremental pass starts from them (bit 0 too), packed: the working bits it repairs and
         // the copy its net changes are taken against
-        if (!fin && i0 < nu) {
-            *reinterpret_cast<unsigned long long*>(b.fp_in + i0) = (b0 << 1) | (inc ? b0 : 0ull);
-            if (inc) {
-                const uint8_t by = (uint8_t)((b0 * 0x0102040810204080ull) >> 56);  // (FP_PER == 8: a byte)
-                b.fp_pbits[i0 / 8] = by;
-                fp_pold(b)[i0 / 8] = by;
+        if (!fin) {
+            if (i0 < nu) *reinterpret_cast<uint32_t*>(b.fp_in + i0) = (uint32_t)((b0 << 1) | (inc ? b0 : 0ull));
+            if (inc) {  // (the even thread of a pair stores the byte of both nibbles)
+                const uint32_t nib = (uint32_t)((b0 * 0x0102040810204080ull) >> 56) & 15u;
+                const uint32_t hi = (uint32_t)__shfl_xor((int)nib, 1, 64);
+                if (!(threadIdx.x & 1u) && i0 < nu) {
+                    const uint8_t by = (uint8_t)(nib | (hi << 4));
+                    b.fp_pbits[i0 / 8] = by;
+                    fp_pold(b)[i0 / 8] = by;
+                }
             }
         }
         if (i0 < nu) {
             uint32_t s = fp_set_of(s_sf, T, i0);
-            const uint32_t e1 = min(nu - i0, FP_PER);
+            const uint32_t e1 = min(nu - i0, FP_TPER);
             uint32_t st_tile = ~0u, st_n = 0;  // MIS statistics of this thread's picks, per clause tile
             unsigned long long st_w = 0;
             // the phase record of the current set: found by binary search at the thread's first
@@ -4881,22 +4889,22 @@ __device__ __forceinline__ void fp_turn_blocks(const ClauseView& cv, const LoopB
 // Turns of every entry for the next pass (RUN), or, after the converged pass (FINAL), the MIS
 // (fp_turn_blocks), from the schedule k_fp_sched wrote.
 template <uint32_t KW>
-__global__ __launch_bounds__(FP_THREADS) void k_fp_turn(ClauseView cv, LoopBuffers b) {
+__global__ __launch_bounds__(FP_TURN_THREADS) void k_fp_turn(ClauseView cv, LoopBuffers b) {
     const RRFpCtl* ctl = b.fp_ctl;
     const uint32_t T = b.rr_T;
     const uint32_t* blkoff = b.fp_blk + (b.m / FP_B + 2);
     // The first block's words and the schedule's tables are loaded before the state is read (each
     // load within its buffer, none depending on another): one round trip before the first block
     // instead of three.
-    FpTurnPre pre{0ull, 0u, 0u, false};
+    FpTurnPre pre{0u, 0u, 0u, false};
     if (blockIdx.x < (b.m + FP_B - 1) / FP_B) {
-        const uint32_t i1 = blockIdx.x * FP_B + threadIdx.x * FP_PER;
-        pre.in = *reinterpret_cast<const unsigned long long*>(b.fp_in + i1);  // (fp_in: m + FP_B bytes)
+        const uint32_t i1 = blockIdx.x * FP_B + threadIdx.x * FP_TPER;
+        pre.in = *reinterpret_cast<const uint32_t*>(b.fp_in + i1);  // (fp_in: m + FP_B bytes)
         pre.by = b.fp_pbits && i1 < b.m ? b.fp_pbits[i1 / 8] : 0u;  // (fp_pbits: incremental passes only)
         pre.off = blkoff[blockIdx.x];
         pre.ok = true;
     }
-    const uint32_t s1 = threadIdx.x;  // (set s1 <= T; sets past FP_THREADS below)
+    const uint32_t s1 = threadIdx.x;  // (set s1 <= T; sets past the block below)
     uint32_t t_sf = 0, t_pf = 0, t_ns = 0, t_er = 0;
     if (s1 <= T) {
         t_sf = b.fp_sf[s1];
@@ -4904,11 +4912,11 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_turn(ClauseView cv, LoopBuffe
         if (s1 < T) { t_ns = b.fp_nseg[s1]; t_er = b.fp_erase[s1]; }
     }
     const bool lds_seg = T <= FP_LDS_SEG_T;
-    constexpr uint32_t SEG_PT = FP_LDS_SEG_T * FP_LDS_SEG_T / FP_THREADS;  // phase records per thread
+    constexpr uint32_t SEG_PT = FP_LDS_SEG_T * FP_LDS_SEG_T / FP_TURN_THREADS;  // phase records per thread
     uint4 t_seg[SEG_PT];
 #pragma unroll
     for (uint32_t u = 0; u < SEG_PT; ++u) {
-        const uint32_t q = threadIdx.x + u * FP_THREADS;
+        const uint32_t q = threadIdx.x + u * FP_TURN_THREADS;
         t_seg[u] = lds_seg && q < T * T ? b.fp_seg[q] : make_uint4(0u, 0u, 0u, 0u);
     }
     DevState* st = b.state;
@@ -4918,7 +4926,7 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_turn(ClauseView cv, LoopBuffe
     if ((state != FP_RUN) & (state != FP_FINAL)) return;
     if ((state == FP_RUN) & (skip != 0)) return;  // (k_fp_sched found no pass to test)
     const bool fin = state == FP_FINAL;
-    __shared__ uint32_t s_w[FP_THREADS / 64];
+    __shared__ uint32_t s_w[FP_TURN_THREADS / 64];
     __shared__ uint32_t s_sf[FP_TMAX + 1], s_pf[FP_TMAX + 1], s_nseg[FP_TMAX], s_er[FP_TMAX];
     __shared__ uint4 s_seg[FP_LDS_SEG_T * FP_LDS_SEG_T];  // the schedule itself when T is small
     if (s1 <= T) {
@@ -4934,7 +4942,7 @@ __global__ __launch_bounds__(FP_THREADS) void k_fp_turn(ClauseView cv, LoopBuffe
     if (lds_seg) {
 #pragma unroll
         for (uint32_t u = 0; u < SEG_PT; ++u) {
-            const uint32_t q = threadIdx.x + u * FP_THREADS;
+            const uint32_t q = threadIdx.x + u * FP_TURN_THREADS;
             if (q < T * T) s_seg[q] = t_seg[u];
         }
     }
@@ -5214,8 +5222,8 @@ static void fp_turns(const ClauseView& cv, const LoopBuffers& b, const FpGrids& 
     // finish advancing the pass: 615 -> 527 it/s at M, T = 16; 50 KB of LDS per workgroup and
     // the schedule's latency in every one of them cost more than the launch saved)
     k_fp_sched<<<1, 256, 0, s>>>(b, test);
-    if (g.narrow) k_fp_turn<4><<<g.gb, FP_THREADS, 0, s>>>(cv, b);
-    else k_fp_turn<0><<<g.gb, FP_THREADS, 0, s>>>(cv, b);
+    if (g.narrow) k_fp_turn<4><<<g.gb, FP_TURN_THREADS, 0, s>>>(cv, b);
+    else k_fp_turn<0><<<g.gb, FP_TURN_THREADS, 0, s>>>(cv, b);
 }
 
 hipError_t launch_rr_prep(const ClauseView& cv, const LoopBuffers& b, bool marked, hipStream_t s) {
@@ -5262,8 +5270,8 @@ hipError_t launch_rr_passes(const ClauseView& cv, const LoopBuffers& b, uint32_t
             if (g.narrow) k_fp_repair<4><<<gw, 1024, lq, s>>>(cv, b);
             else k_fp_repair<0><<<gw, 1024, lq, s>>>(cv, b);
             // (the repair ran the pass test and the schedule: the turns follow)
-            if (g.narrow) k_fp_turn<4><<<g.gb, FP_THREADS, 0, s>>>(cv, b);
-            else k_fp_turn<0><<<g.gb, FP_THREADS, 0, s>>>(cv, b);
+            if (g.narrow) k_fp_turn<4><<<g.gb, FP_TURN_THREADS, 0, s>>>(cv, b);
+            else k_fp_turn<0><<<g.gb, FP_TURN_THREADS, 0, s>>>(cv, b);
             continue;
         }
         // round 0: the claimant-list minima, then JOIN(0) (a workgroup per tile); rounds 1..:

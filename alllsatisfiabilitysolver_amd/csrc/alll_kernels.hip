@@ -4765,7 +4765,8 @@ struct FpTurnPre {
 };
 
 // k_fp_turn: FP_TPER entries per thread (half the count kernel's: twice the threads per block,
-// half the per-thread chain of set and phase lookups)
+// half the per-thread chain of set and phase lookups; 10.1 -> 9.1 us per pass at M.  Two per
+// thread, 1024-thread blocks: 13 us)
 constexpr uint32_t FP_TPER = 4;
 constexpr int FP_TURN_THREADS = FP_B / FP_TPER;
 
@@ -4787,14 +4788,16 @@ __device__ __forceinline__ void fp_turn_blocks(const ClauseView& cv, const LoopB
             if (threadIdx.x < FP_ST_TILES) s_stn[threadIdx.x] = s_stw[threadIdx.x] = 0;
         }
         const bool first = pre.ok && blk == blockIdx.x;
-        static_assert(FP_TPER == 4, "a nibble of pick bits, 4 bytes of fp_in per thread");
+        static_assert(FP_TPER == 2 || FP_TPER == 4, "FP_TPER pick bits and bytes of fp_in per thread");
+        constexpr uint32_t TMASK = (1u << FP_TPER) - 1u;
         uint32_t x = 0;
         if (i0 < nu) {
-            if (pb) {  // (after an incremental pass: its picks are bits; nibble -> bit 0 of 4 bytes)
+            if (pb) {  // (after an incremental pass: its picks are bits; bits -> bit 0 of FP_TPER bytes)
                 const uint32_t by = first ? pre.by : b.fp_pbits[i0 / 8];
-                x = (((by >> (i0 & 4u)) & 15u) * 0x00204081u) & 0x01010101u;
+                x = (((by >> (i0 & 7u)) & TMASK) * 0x00204081u) & 0x01010101u;
             } else {
-                x = first ? pre.in : *reinterpret_cast<const uint32_t*>(b.fp_in + i0);
+                x = first ? pre.in : (FP_TPER == 4 ? *reinterpret_cast<const uint32_t*>(b.fp_in + i0)
+                                                   : (uint32_t)*reinterpret_cast<const uint16_t*>(b.fp_in + i0));
             }
             if (nu - i0 < FP_TPER) x &= (1u << (8 * (nu - i0))) - 1u;
         }
@@ -4805,14 +4808,19 @@ __device__ __forceinline__ void fp_turn_blocks(const ClauseView& cv, const LoopB
         // incremental pass starts from them (bit 0 too), packed: the working bits it repairs and
         // the copy its net changes are taken against
         if (!fin) {
-            if (i0 < nu) *reinterpret_cast<uint32_t*>(b.fp_in + i0) = (uint32_t)((b0 << 1) | (inc ? b0 : 0ull));
-            if (inc) {  // (the even thread of a pair stores the byte of both nibbles)
-                const uint32_t nib = (uint32_t)((b0 * 0x0102040810204080ull) >> 56) & 15u;
-                const uint32_t hi = (uint32_t)__shfl_xor((int)nib, 1, 64);
-                if (!(threadIdx.x & 1u) && i0 < nu) {
-                    const uint8_t by = (uint8_t)(nib | (hi << 4));
-                    b.fp_pbits[i0 / 8] = by;
-                    fp_pold(b)[i0 / 8] = by;
+            const uint32_t fv = (uint32_t)((b0 << 1) | (inc ? b0 : 0ull));
+            if (i0 < nu) {
+                if (FP_TPER == 4) *reinterpret_cast<uint32_t*>(b.fp_in + i0) = fv;
+                else *reinterpret_cast<uint16_t*>(b.fp_in + i0) = (uint16_t)fv;
+            }
+            if (inc) {  // (the first thread of each 8 entries stores their byte, OR-ed over the lanes)
+                constexpr uint32_t TPB = 8 / FP_TPER;  // threads per byte
+                uint32_t v = ((uint32_t)((b0 * 0x0102040810204080ull) >> 56) & TMASK) << (FP_TPER * (threadIdx.x % TPB));
+#pragma unroll
+                for (uint32_t o = 1; o < TPB; o <<= 1) v |= (uint32_t)__shfl_xor((int)v, (int)o, 64);
+                if (threadIdx.x % TPB == 0 && i0 < nu) {
+                    b.fp_pbits[i0 / 8] = (uint8_t)v;
+                    fp_pold(b)[i0 / 8] = (uint8_t)v;
                 }
             }
         }
@@ -4899,7 +4907,8 @@ __global__ __launch_bounds__(FP_TURN_THREADS) void k_fp_turn(ClauseView cv, Loop
     FpTurnPre pre{0u, 0u, 0u, false};
     if (blockIdx.x < (b.m + FP_B - 1) / FP_B) {
         const uint32_t i1 = blockIdx.x * FP_B + threadIdx.x * FP_TPER;
-        pre.in = *reinterpret_cast<const uint32_t*>(b.fp_in + i1);  // (fp_in: m + FP_B bytes)
+        pre.in = FP_TPER == 4 ? *reinterpret_cast<const uint32_t*>(b.fp_in + i1)  // (fp_in: m + FP_B bytes)
+                              : (uint32_t)*reinterpret_cast<const uint16_t*>(b.fp_in + i1);
         pre.by = b.fp_pbits && i1 < b.m ? b.fp_pbits[i1 / 8] : 0u;  // (fp_pbits: incremental passes only)
         pre.off = blkoff[blockIdx.x];
         pre.ok = true;

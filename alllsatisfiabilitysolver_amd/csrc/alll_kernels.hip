@@ -4833,7 +4833,22 @@ __device__ __forceinline__ void fp_turn_blocks(const ClauseView& cv, const LoopB
             // entry of a set, then walked forward (levels do not decrease within a set)
             uint32_t rs = ~0u, lo = 0, ns = 0;
             const uint4* rec = segs;
-            for (uint32_t e = 0; e < e1; ++e) {
+            // (fin: the picks' headers and variables loaded together up front, not one pick's
+            // chain after the other)
+            uint4 pa[FP_TPER], pv[FP_TPER];
+            if (fin) {
+#pragma unroll
+                for (uint32_t e = 0; e < FP_TPER; ++e) {
+                    pa[e] = pv[e] = make_uint4(0u, 0u, 0u, 0u);
+                    if (e < e1 && ((b0 >> (8 * e)) & 1ull)) {
+                        pa[e] = U[i0 + e].a;
+                        pv[e] = KW == 4 ? b.fp_v4[i0 + e] : U[i0 + e].v0;
+                    }
+                }
+            }
+#pragma unroll
+            for (uint32_t e = 0; e < FP_TPER; ++e) {
+                if (e >= e1) break;
                 const uint32_t i = i0 + e;
                 while (i >= s_sf[s + 1]) ++s;
                 const bool pick = (b0 >> (8 * e)) & 1ull;
@@ -4865,9 +4880,9 @@ __device__ __forceinline__ void fp_turn_blocks(const ClauseView& cv, const LoopB
                             if (s_er[mid] < turn) a = mid + 1;
                             else z = mid;
                         }
-                        const uint4 ea = U[i].a;
+                        const uint4 ea = pa[e];
                         b.tmis[turn - a] = ea.x;
-                        const uint4 v0 = KW == 4 ? b.fp_v4[i] : U[i].v0;
+                        const uint4 v0 = pv[e];
                         fp_for_vars<KW>(cv, U, i, ea, v0, [&](uint32_t v) { b.cover[v] = (uint8_t)stamp; });
                         if (ea.x / TILE != st_tile) {
                             if (st_n) fp_stat_add(b, s_t0, s_stn, s_stw, st_tile, st_n, st_w);

@@ -364,6 +364,28 @@ def test_baseline_sizes_bit_exact_steps(gpu, oracle_mod, name, monkeypatch):
         assert nv == oracle_mod.eval_mask(offs, lits, A)[0]
 
 
+@pytest.mark.slow
+@pytest.mark.parametrize("name", ["C2_3sat_4M", "M_3sat_10M"])
+def test_full_size_long_run_bit_exact(gpu, oracle_mod, name):
+    """C2 and M at full size over 8 consecutive iterations, every one against the oracle's
+    (violated count, MIS list, resampled assignment): the full-size cases above check 2
+    iterations, the bench digests only the end state of a longer run."""
+    from alllsatisfiabilitysolver_amd import Solver, generate_ksat
+
+    n, m, k, kind = BIG[name]
+    offs, lits = generate_ksat(1, n, m, k, kind)
+    seed = 1
+    with Solver(n, offs, lits, seed=seed) as s:
+        A = s.assignment_words()
+        for it in range(8):
+            nu, vm, M, A_next = _oracle_step(oracle_mod, n, offs, lits, A, seed, it)
+            s.run(1)
+            assert s.stats()["n_violated"] == nu, f"iteration {it}"
+            np.testing.assert_array_equal(s.mis(), M, err_msg=f"iteration {it}")
+            A = s.assignment_words()
+            np.testing.assert_array_equal(A, A_next, err_msg=f"iteration {it}")
+
+
 def test_bench_helpers(gpu, oracle_mod):
     from alllsatisfiabilitysolver_amd import Solver, generate_ksat
 

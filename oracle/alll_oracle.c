@@ -386,6 +386,144 @@ int orc_solve_stream(uint32_t n_vars, uint64_t m, const uint64_t* offs, const ui
 }
 
 /* ------------------------------------------------------------------------- */
+/* Streaming solve with T > 1 threads (SATInstance.h:70-153).                  */
+/*  - T generators (:74-86): generator t owns clauses [t*tn, t*tn + n_t),      */
+/*    tn = m / T, the last one the remainder; each walks its own range with    */
+/*    c <- (c + P) % n_t from c = 0 (ClauseGenerator.h:44-47), never reset;    */
+/*  - a batch step (:98-125) asks every generator for a batch                  */
+/*    (yieldRandomUNSATClauseBatch, ClauseGenerator.h:32-71: a finished        */
+/*    generator first resets n_yielded to 0; min(batch, n_t - n_yielded)      */
+/*    steps; finished when n_yielded == n_t) and keeps the violated ones;      */
+/*    populate_mis_parallel (:391-451) then drops every set's clauses that     */
+/*    share a variable with the MIS accumulated so far and runs the T-set      */
+/*    round robin from t = 0 (first turn: set 1), extending the MIS; the       */
+/*    batch steps repeat until every generator finished at the same step,      */
+/*    then the MIS is resampled (parallel_solve resample = finishedYielding);  */
+/*  - avg_mis_size accumulates the MIS size after every batch step;            */
+/*  - the end-of-iteration check (:129-147) runs T threads over their ranges   */
+/*    in index order sharing one `solved` flag, so where each thread stops is  */
+/*    a race in the reference.  Restated with the lock-step schedule: step k   */
+/*    checks clause base_t + k of every generator with k < n_t, and the steps  */
+/*    stop after the first one that finds a violated clause (f = the smallest  */
+/*    first-violated offset over the generators); generator t is left at       */
+/*    n_yielded = min(n_t, f + 1), finished iff that is n_t.  With T = 1 this  */
+/*    is the one-thread window rule of orc_solve_stream.                       */
+/* An empty clause is refused (-2): it is violated forever and, never sharing */
+/* a variable, joins the MIS at every batch step.  A loop whose generators    */
+/* never finish together (the reference would not return) stops at step_cap   */
+/* batch steps in one iteration (-1).  Returns 0 solved, 1 capped.             */
+/* ------------------------------------------------------------------------- */
+typedef struct { uint64_t base, n, c, ny; int fin; } orc_sgen;
+
+static uint64_t sgen_yield(orc_sgen* g, uint64_t batch, const uint64_t* vmask, uint32_t* out) {
+    if (g->fin) { g->ny = 0; g->fin = 0; }  /* ClauseGenerator.h:33-35 (reset) */
+    const uint64_t n = (g->ny + batch >= g->n) ? g->n - g->ny : batch;
+    uint64_t k = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        g->c = (g->c + ORC_STREAM_P) % g->n;  /* c < n_t < 2^32: no overflow */
+        const uint64_t cl = g->base + g->c;
+        if ((vmask[cl >> 6] >> (cl & 63)) & 1ull) out[k++] = (uint32_t)cl;
+        g->ny++;
+    }
+    if (g->ny == g->n) g->fin = 1;
+    return k;
+}
+
+int orc_solve_stream_rr(uint32_t n_vars, uint64_t m, const uint64_t* offs, const uint32_t* lits, uint64_t seed,
+                        uint64_t max_iters, uint64_t batch, uint32_t T, uint64_t step_cap, uint32_t* A,
+                        orc_stats* st, orc_iter_cb cb, void* cb_user) {
+    memset(st, 0, sizeof(*st));
+    if (T < 1) T = 1;
+    if (batch == 0) batch = 1;
+    for (uint64_t c = 0; c < m; ++c)
+        if (offs[c + 1] == offs[c]) return -2;
+    const uint64_t nw = (m + 63) / 64, tn = m / T;
+    orc_sgen* g = (orc_sgen*)calloc(T, sizeof(orc_sgen));
+    uint64_t *seg = (uint64_t*)malloc(sizeof(uint64_t) * (T + 1)), *cnt = (uint64_t*)malloc(sizeof(uint64_t) * T),
+             *head = (uint64_t*)malloc(sizeof(uint64_t) * T);
+    uint32_t* live = (uint32_t*)malloc(sizeof(uint32_t) * T);
+    uint64_t* vmask = (uint64_t*)calloc(nw ? nw : 1, sizeof(uint64_t));
+    uint8_t* used = (uint8_t*)calloc(n_vars ? n_vars : 1, 1);
+    uint32_t* M = (uint32_t*)malloc(sizeof(uint32_t) * (m ? m : 1));
+    seg[0] = 0;
+    for (uint32_t t = 0; t < T; ++t) {  /* SATInstance.h:74-86 */
+        g[t].base = (uint64_t)t * tn;
+        g[t].n = (t == T - 1) ? m - g[t].base : tn;
+        seg[t + 1] = seg[t] + (g[t].n < batch ? g[t].n : batch);  /* a batch holds at most this many */
+    }
+    uint32_t* lists = (uint32_t*)malloc(sizeof(uint32_t) * (seg[T] ? seg[T] : 1));
+    uint64_t weighted = 0, nu = orc_eval(m, offs, lits, A, vmask);
+    int rc = 0;
+    for (;;) {
+        st->n_iterations += 1;
+        st->last_violated = nu;
+        uint64_t nm = 0, steps = 0;
+        int all_fin = 0;
+        while (!all_fin) {
+            if (++steps > step_cap) { rc = -1; goto out; }
+            all_fin = 1;
+            for (uint32_t t = 0; t < T; ++t) {
+                cnt[t] = sgen_yield(&g[t], batch, vmask, lists + seg[t]);
+                head[t] = 0;
+                live[t] = t;
+                all_fin &= g[t].fin;
+            }
+            /* populate_mis_parallel: the filter against the MIS so far and the erasures of the
+               round robin are both lazy (a front touching a used variable is skipped) */
+            uint32_t nlive = T, t = 0;
+            while (nlive > 0) {
+                t = (t + 1) % nlive;
+                const uint32_t s = live[t];
+                const uint32_t* L = lists + seg[s];
+                while (head[s] < cnt[s] && touches(offs, lits, used, L[head[s]])) ++head[s];
+                if (head[s] == cnt[s]) {
+                    for (uint32_t q = t; q + 1 < nlive; ++q) live[q] = live[q + 1];
+                    --nlive;
+                    continue;
+                }
+                const uint32_t c = L[head[s]++];
+                M[nm++] = c;
+                mark(offs, lits, used, c, 1);
+            }
+            weighted += nm;  /* SATInstance.h:113-114 (avg_mis_size after every batch) */
+        }
+        uint64_t dres = 0;
+        const uint64_t iter = st->n_iterations - 1;
+        for (uint64_t i = 0; i < nm; ++i) {
+            const uint32_t cl = M[i];
+            for (uint64_t j = offs[cl]; j < offs[cl + 1]; ++j) {
+                const uint32_t v = lits[j] >> 1;
+                const uint32_t bb = orc_resample_bit(seed, iter, v);
+                A[v >> 5] = (A[v >> 5] & ~(1u << (v & 31))) | (bb << (v & 31));
+                used[v] = 0;
+            }
+            dres += offs[cl + 1] - offs[cl];
+        }
+        st->n_resamples += dres;
+        if (cb) cb(cb_user, st->n_iterations, nu, nm, dres, A);
+        nu = orc_eval(m, offs, lits, A, vmask);
+        if (nu == 0) { st->solved = 1; st->last_violated = 0; break; }
+        if (max_iters && st->n_iterations >= max_iters) { st->last_violated = nu; rc = 1; break; }
+        /* lock-step check: f = smallest first-violated offset over the generators */
+        uint64_t f = ~0ull;
+        for (uint32_t t = 0; t < T; ++t)
+            for (uint64_t k = 0; k < g[t].n && k < f; ++k) {
+                const uint64_t cl = g[t].base + k;
+                if ((vmask[cl >> 6] >> (cl & 63)) & 1ull) { f = k; break; }
+            }
+        for (uint32_t t = 0; t < T; ++t) {
+            g[t].ny = g[t].n < f + 1 ? g[t].n : f + 1;
+            g[t].fin = g[t].ny == g[t].n;
+        }
+    }
+out:
+    st->sum_mis_size = weighted;
+    st->avg_mis_size = st->n_iterations ? weighted / st->n_iterations : 0;
+    free(g); free(seg); free(cnt); free(head); free(live); free(vmask); free(used); free(M); free(lists);
+    return rc;
+}
+
+/* ------------------------------------------------------------------------- */
 /* DIMACS semantics of cnf_header_read / cnf_data_read (example/cnf_io/        */
 /* cnf_io.cpp:487-705, 126-328) plus the encoding of example/main.cpp:157-178. */
 /* Restated over an in-memory buffer:                                          */

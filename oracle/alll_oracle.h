@@ -44,6 +44,9 @@ void orc_stream_order(uint64_t m, uint32_t* order);
 int orc_solve_stream(uint32_t n_vars, uint64_t m, const uint64_t* offs, const uint32_t* lits, uint64_t seed,
                      uint64_t max_iters, uint64_t batch, uint32_t* A, orc_stats* st, orc_iter_cb cb,
                      void* cb_user);
+int orc_solve_stream_rr(uint32_t n_vars, uint64_t m, const uint64_t* offs, const uint32_t* lits, uint64_t seed,
+                        uint64_t max_iters, uint64_t batch, uint32_t T, uint64_t step_cap, uint32_t* A,
+                        orc_stats* st, orc_iter_cb cb, void* cb_user);
 int orc_dimacs_parse(const char* buf, uint64_t len, uint32_t* v_num, uint64_t* c_num, uint64_t* offs,
                      uint32_t* lits, uint64_t* l_num);
 

@@ -82,6 +82,10 @@ def lib():
                                        ctypes.c_uint64, ctypes.c_uint64, _u32p, ctypes.POINTER(OrcStats),
                                        ITER_CB, ctypes.c_void_p]
         L.orc_solve_stream.restype = ctypes.c_int
+        L.orc_solve_stream_rr.argtypes = [ctypes.c_uint32, ctypes.c_uint64, _u64p, _u32p, ctypes.c_uint64,
+                                          ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
+                                          _u32p, ctypes.POINTER(OrcStats), ITER_CB, ctypes.c_void_p]
+        L.orc_solve_stream_rr.restype = ctypes.c_int
         L.orc_dimacs_parse.argtypes = [ctypes.c_char_p, ctypes.c_uint64, _u32p, _u64p, _u64p,
                                        _u32p, _u64p]
         L.orc_dimacs_parse.restype = ctypes.c_int
@@ -292,6 +296,105 @@ def solve_stream(n_vars, offs, lits, seed, batch, max_iters=0, A0=None, trace=Fa
     return stats, A, rows
 
 
+def solve_stream_rr(n_vars, offs, lits, seed, batch, T, max_iters=0, A0=None, trace=False, step_cap=1 << 24):
+    """Streaming solve with T > 1 threads (SATInstance.h:70-153; orc_solve_stream_rr) with
+    Philox.  Returns (rc, stats dict, final A words, per-iteration rows (it, |U|, |M|, dres,
+    A after)); rc 0 solved, 1 capped, -1 step cap, -2 empty clause."""
+    m = len(offs) - 1
+    A = init_assignment(seed, n_vars) if A0 is None else np.array(A0, np.uint32)
+    st = OrcStats()
+    rows = []
+
+    def cb(user, it, nu, nm, dres, Ap):
+        if trace:
+            rows.append((int(it), int(nu), int(nm), int(dres),
+                         np.ctypeslib.as_array(Ap, shape=(A.size,)).copy()))
+
+    cbf = ITER_CB(cb)
+    rc = lib().orc_solve_stream_rr(n_vars, m, _p(offs, _u64p), _p(lits, _u32p), seed, max_iters, batch, T,
+                                   step_cap, _p(A, _u32p), ctypes.byref(st), cbf, None)
+    stats = {k: int(getattr(st, k)) for k, _ in OrcStats._fields_ if k != "pad"}
+    return int(rc), stats, A, rows
+
+
+# Pure-Python restatement of one streaming iteration with T threads (small cases; the maps the
+# golden stream-rr fixtures pin, and the reference for orc_solve_stream_rr in tests/test_oracle.py).
+STREAM_P = 9223372036854775783
+
+
+def stream_gens(m, T):
+    """The T ClauseGenerators of SATInstance.h:74-86: {base, n, c, ny, fin}."""
+    tn = m // T
+    return [dict(base=t * tn, n=(m - t * tn) if t == T - 1 else tn, c=0, ny=0, fin=False) for t in range(T)]
+
+
+def stream_yield(g, bits, batch):
+    """ClauseGenerator::yieldRandomUNSATClauseBatch (ClauseGenerator.h:32-71): the violated
+    clauses of the next batch in yield order."""
+    if g["fin"]:
+        g["ny"], g["fin"] = 0, False
+    n = g["n"] - g["ny"] if g["ny"] + batch >= g["n"] else batch
+    out = []
+    for _ in range(n):
+        g["c"] = (g["c"] + STREAM_P) % g["n"]
+        cl = g["base"] + g["c"]
+        if bits[cl]:
+            out.append(cl)
+        g["ny"] += 1
+    if g["ny"] == g["n"]:
+        g["fin"] = True
+    return out
+
+
+def stream_rr_iteration(n_vars, offs, lits, A, batch, gens):
+    """The batch loop of one streaming iteration (SATInstance.h:98-125) from generator states
+    `gens` (updated in place): returns (per step the T violated lists, the MIS in pick order,
+    the MIS size after every step)."""
+    m = len(offs) - 1
+    _, vm = eval_mask(offs, lits, A)
+    bits = np.unpackbits(vm.view(np.uint8), bitorder="little")[:m]
+    used = np.zeros(max(1, n_vars), bool)
+    T = len(gens)
+    steps, M, cum = [], [], []
+    while True:
+        lists = [stream_yield(g, bits, batch) for g in gens]
+        steps.append(lists)
+        fin = all(g["fin"] for g in gens)
+        head, live, t = [0] * T, list(range(T)), 0   # populate_mis_parallel, SATInstance.h:391-451
+        while live:
+            t = (t + 1) % len(live)
+            s = live[t]
+            L = lists[s]
+            while head[s] < len(L) and used[lits[int(offs[L[head[s]]]):int(offs[L[head[s]] + 1])] >> 1].any():
+                head[s] += 1
+            if head[s] == len(L):
+                live.pop(t)
+                continue
+            c = L[head[s]]
+            head[s] += 1
+            M.append(c)
+            used[lits[int(offs[c]):int(offs[c + 1])] >> 1] = True
+        cum.append(len(M))
+        if fin:
+            return steps, np.array(M, np.uint32), cum
+
+
+def stream_rr_check(offs, lits, A, gens):
+    """End-of-iteration check (SATInstance.h:129-147) in lock step: True when solved, else the
+    generators are left where the check stopped (min(n_t, f + 1) clauses yielded)."""
+    m = len(offs) - 1
+    nu, vm = eval_mask(offs, lits, A)
+    if nu == 0:
+        return True
+    bits = np.unpackbits(vm.view(np.uint8), bitorder="little")[:m]
+    f = min((int(np.argmax(bits[g["base"]:g["base"] + g["n"]])) for g in gens
+             if g["n"] and bits[g["base"]:g["base"] + g["n"]].any()))
+    for g in gens:
+        g["ny"] = min(g["n"], f + 1)
+        g["fin"] = g["ny"] == g["n"]
+    return False
+
+
 def stream_mis(n_vars, offs, lits, A, order):
     """Greedy MIS of the violated clauses in the given order (pick order)."""
     nu, vm = eval_mask(offs, lits, A)
@@ -365,6 +468,56 @@ def read_stream_trace(path):
     return dict(n_vars=n_vars, m=m, batch=batch, iters=iters,
                 stats=dict(n_iterations=n_it, n_resamples=n_res, avg_mis_size=avg), A_final=Af,
                 solve_stats=dict(n_iterations=s_it, n_resamples=s_res, avg_mis_size=s_avg), solve_A=As)
+
+
+def read_stream_rr_trace(path):
+    """Parse oracle/_ref/ref_probe `stream-rr` output (streaming solve, T > 1 threads)."""
+    with open(path, "rb") as f:
+        data = f.read()
+    assert data[:4] == b"ALRQ"
+    n_vars, batch, T, _ = struct.unpack_from("<IIII", data, 4)
+    (m,) = struct.unpack_from("<Q", data, 20)
+    p = 28
+    iters = []
+
+    def u64(p):
+        return struct.unpack_from("<Q", data, p)[0], p + 8
+
+    def gens(p):
+        g = np.frombuffer(data, np.uint64, 3 * T, p).reshape(T, 3).copy()
+        return g, p + 24 * T
+
+    while True:
+        it, p = u64(p)
+        if it == 0xFFFFFFFFFFFFFFFF:
+            break
+        A = np.frombuffer(data, np.uint8, n_vars, p).copy()
+        p += n_vars
+        G, p = gens(p)
+        ns, p = u64(p)
+        steps, cum = [], []
+        for _ in range(ns):
+            lists = []
+            for _ in range(T):
+                n, p = u64(p)
+                lists.append(np.frombuffer(data, np.uint32, n, p).copy())
+                p += 4 * n
+            steps.append(lists)
+            c, p = u64(p)
+            cum.append(c)
+        nm, p = u64(p)
+        M = np.frombuffer(data, np.uint32, nm, p).copy()
+        p += 4 * nm
+        dres, p = u64(p)
+        solved, p = u64(p)
+        iters.append(dict(it=it, A=A, G=G, steps=steps, cum=cum, M=M, dres=dres, solved=solved))
+    n_it, n_res, avg = struct.unpack_from("<QQQ", data, p)
+    p += 24
+    Af = np.frombuffer(data, np.uint8, n_vars, p).copy()
+    p += n_vars
+    Gf, p = gens(p)
+    return dict(n_vars=n_vars, m=m, batch=batch, T=T, iters=iters,
+                stats=dict(n_iterations=n_it, n_resamples=n_res, avg_mis_size=avg), A_final=Af, G_final=Gf)
 
 
 # ----------------------------------------------------------------- reference run

@@ -410,6 +410,140 @@ static int cmd_stream(int argc, char** argv) {
     return 0;
 }
 
+// ---- streaming solve (SATInstance.h:70-153) with T > 1 threads ------------------------------
+// The loop of SATInstance::solve(getEnumeratedClause, n_clauses, batch_size) with the reference's
+// own ClauseGenerators (:74-86), populate_mis_parallel and resample_clauses, recording per
+// iteration A, every generator's state {n_yielded, finished, c}, per batch step the violated list
+// of every generator (yield order) and the MIS size after the step, then the MIS (pick order).
+// Two parts are restated: (1) the batches are requested generator by generator on this thread
+// (the reference asks all generators at once, :105-108; they are independent, so the lists are
+// the same, and the callback's index map needs no lock); (2) the end-of-iteration check
+// (:129-147) shares one `solved` flag between T threads, so where each thread stops is a race in
+// the reference: it is run here in lock step (step k yields clause k of every generator with
+// k < n_t; the steps stop after the first that finds a violated clause), the schedule
+// oracle/alll_oracle.c restates.  The real solve() is not run for T > 1: its check is racy.
+//   stream-rr <cnf> <batch> <T> <rd_seed> <out.bin>
+static int cmd_stream_rr(int argc, char** argv) {
+    std::string path = argv[2];
+    const UINT_T batch = (UINT_T)strtoul(argv[3], 0, 10);
+    const int T = atoi(argv[4]);
+    const unsigned long long rd_seed = strtoull(argv[5], 0, 10);
+    FILE* f = fopen(argv[6], "wb");
+    Loaded L = load(path, 1);
+    g_stream = &L;
+    const UINT_T n_clauses = (UINT_T)L.c_num;
+    wr(f, "ALRQ", 4);
+    uint32_t hdr[4] = {(uint32_t)L.v_num, (uint32_t)batch, (uint32_t)T, 0u};
+    wr(f, hdr, 16);
+    wr64(f, (uint64_t)L.c_num);
+    g_rd_state = rd_seed;
+    auto S = new SATInstance<UINT_T>(new VariablesArray<UINT_T>(L.v_num), T);
+    omp_set_num_threads(T);
+    auto statistics = new Statistics;
+    for (int t = 0; t < T; t++) statistics->n_thread_resamples.push_back(0);
+    S->n_clauses = n_clauses;
+    // SATInstance.h:74-86
+    UINT_T t_n_clauses = (UINT_T)n_clauses / T;
+    std::vector<ClauseGenerator<UINT_T>*> gens;
+    for (int t = 0; t < T; t++) {
+        UINT_T offset = (UINT_T)t * t_n_clauses;
+        if (t == T - 1) t_n_clauses = n_clauses - offset;
+        gens.push_back(new ClauseGenerator<UINT_T>(stream_clause, (unsigned short)t, t_n_clauses, offset, batch));
+    }
+    auto wr_gens = [&]() {
+        for (auto g : gens) {
+            wr64(f, (uint64_t)g->n_yielded_clauses);
+            wr64(f, g->finished_yielding ? 1ull : 0ull);
+            wr64(f, (uint64_t)g->c);
+        }
+    };
+    std::vector<uint8_t> A(L.v_num);
+    bool solved = false;
+    while (!solved) {
+        solved = true;
+        statistics->n_iterations += 1;
+        for (int v = 0; v < L.v_num; ++v) A[v] = S->var_arr->vars[v] ? 1 : 0;
+        wr64(f, statistics->n_iterations);
+        wr(f, A.data(), A.size());
+        wr_gens();
+        auto mis = new ClauseArray();
+        std::vector<uint32_t> M;
+        std::vector<std::vector<uint32_t>> step_lists;  // T lists per step
+        std::vector<uint64_t> cum;
+        bool finished = false;
+        ull dres = 0;
+        while (!finished) {
+            auto clauses = new std::vector<ClauseArray*>;
+            for (int t = 0; t < T; t++) clauses->push_back(gens[t]->yieldRandomUNSATClauseBatch(S->var_arr->vars));
+            for (int t = 0; t < T; t++) {
+                std::vector<uint32_t> u;
+                for (auto c : *clauses->at(t)) u.push_back(g_copy_index[c]);
+                step_lists.push_back(u);
+            }
+            finished = true;
+            for (int t = 0; t < T; t++)
+                if (!gens[t]->has_finished_yielding()) { finished = false; break; }
+            // parallel_solve(clauses, mis, stream = true, resample = finished), SATInstance.h:217-320
+            auto result = new Statistics;
+            for (int t = 0; t < T; t++) result->n_thread_resamples.push_back(0);
+            result->n_iterations = 1;
+            S->populate_mis_parallel(clauses, mis, true);
+            result->avg_mis_size += mis->size();
+            cum.push_back(mis->size());
+            if (finished) {
+                for (auto c : *mis) M.push_back(g_copy_index[c]);
+                S->resample_clauses(mis, result);
+                mis->clear();  // (the reference also frees the clauses; ids recorded above)
+            }
+            for (int t = 0; t < T; t++) result->n_resamples += result->n_thread_resamples.at(t);
+            statistics->avg_mis_size += result->avg_mis_size;
+            statistics->n_resamples += result->n_resamples;
+            dres += result->n_resamples;
+            delete result;
+            if (step_lists.size() > 4000000) { fprintf(stderr, "probe step cap\n"); return 1; }
+        }
+        delete mis;
+        wr64(f, cum.size());
+        for (size_t s = 0; s < cum.size(); ++s) {
+            for (int t = 0; t < T; t++) {
+                const auto& u = step_lists[s * T + t];
+                wr64(f, u.size());
+                wr(f, u.data(), u.size() * 4);
+            }
+            wr64(f, cum[s]);
+        }
+        wr64(f, M.size());
+        wr(f, M.data(), M.size() * 4);
+        wr64(f, dres);
+        // check (SATInstance.h:129-147) in lock step
+        uint64_t maxn = 0;
+        for (auto g : gens) maxn = std::max<uint64_t>(maxn, g->n_clauses);
+        for (uint64_t k = 0; k < maxn && solved; ++k) {
+            bool found = false;
+            for (int t = 0; t < T; t++) {
+                if (k >= (uint64_t)gens[t]->n_clauses) continue;
+                auto c = gens[t]->yieldNextClause();
+                if (c->is_not_satisfied(S->var_arr->vars)) found = true;
+                delete c->literals;
+                delete c;
+            }
+            if (found) solved = false;
+        }
+        wr64(f, solved ? 1ull : 0ull);
+        if (statistics->n_iterations >= 2000) break;  // (probe safety cap)
+    }
+    statistics->avg_mis_size /= statistics->n_iterations;
+    wr64(f, ~0ull);
+    wr64(f, statistics->n_iterations);
+    wr64(f, statistics->n_resamples);
+    wr64(f, statistics->avg_mis_size);
+    for (int v = 0; v < L.v_num; ++v) A[v] = S->var_arr->vars[v] ? 1 : 0;
+    wr(f, A.data(), A.size());
+    wr_gens();
+    fclose(f);
+    return 0;
+}
+
 int main(int argc, char** argv) {
     if (argc < 3) {
         fprintf(stderr, "usage: ref_probe trace|solve|bench|cnf ...\n");
@@ -422,6 +556,7 @@ int main(int argc, char** argv) {
     if (cmd == "bench-gen" && argc >= 10) return cmd_bench_gen(argc, argv);
     if (cmd == "cnf") return cmd_cnf(argc, argv);
     if (cmd == "stream" && argc >= 6) return cmd_stream(argc, argv);
+    if (cmd == "stream-rr" && argc >= 7) return cmd_stream_rr(argc, argv);
     fprintf(stderr, "bad arguments\n");
     return 2;
 }

@@ -129,7 +129,78 @@ def stream_fixtures(tmp):
     return out
 
 
+def stream_rr_fixtures(tmp, keep):
+    """Streaming solve with T > 1 threads (ref_probe `stream-rr`): per iteration A_i, every
+    generator's state {n_yielded, finished, c} at its start, per batch step the violated list of
+    every generator and the MIS size after the step, the MIS in pick order, delta n_resamples and
+    the check's verdict.  Not reproducible (T > 1 resampling, see the module docstring): an
+    existing fixture is kept unless --rewrite-rr."""
+    specs = [
+        # name, instance, [(T, batch)]
+        ("r2_3sat_200_400", (200, 400, 3, 0), [(2, 1), (2, 64), (3, 7), (4, 37)]),
+        ("r2_3sat_2000_4000", (2000, 4000, 3, 0), [(2, 256), (4, 100)]),
+        ("k8_4000_6000", (4000, 6000, 8, 0), [(4, 500)]),
+        ("edge", None, [(3, 6), (5, 1), (20, 3)]),
+    ]
+    out = []
+    for name, inst, runs in specs:
+        if inst is None:
+            n, (offs, lits) = edge_instance()
+        else:
+            n, m, k, kind = inst
+            offs, lits = o.generate_ksat(1, n, m, k, kind)
+        cnf = os.path.join(tmp, name + "_q.cnf")
+        with open(cnf, "w") as f:
+            f.write(o.to_dimacs(n, offs, lits))
+        for T, bs in runs:
+            fx = f"streamrr_{name}_T{T}_b{bs}"
+            if keep(fx):
+                continue
+            path = os.path.join(tmp, "q.bin")
+            subprocess.run([o.REF_PROBE, "stream-rr", cnf, str(bs), str(T), str(RD_SEED), path], check=True)
+            tr = o.read_stream_rr_trace(path)
+            it = tr["iters"]
+            flat = [l for r in it for lists in r["steps"] for l in lists]
+            st = tr["stats"]
+            np.savez_compressed(
+                os.path.join(HERE, fx + ".npz"), n_vars=np.uint32(n), offs=offs, lits=lits,
+                batch=np.uint64(bs), T=np.uint32(T), A=np.stack([o.pack_bools(r["A"]) for r in it]),
+                G=np.stack([r["G"] for r in it]).astype(np.uint64),
+                nsteps=np.array([len(r["steps"]) for r in it], np.uint64),
+                L=(np.concatenate(flat) if flat else np.zeros(0)).astype(np.uint32),
+                L_ptr=np.cumsum([0] + [l.size for l in flat]).astype(np.uint64),
+                cum=np.array([c for r in it for c in r["cum"]], np.uint64),
+                M=np.concatenate([r["M"] for r in it]).astype(np.uint32),
+                M_ptr=np.cumsum([0] + [r["M"].size for r in it]).astype(np.uint64),
+                dres=np.array([r["dres"] for r in it], np.uint64),
+                solved=np.array([r["solved"] for r in it], np.uint64),
+                stats=np.array([st["n_iterations"], st["n_resamples"], st["avg_mis_size"]], np.uint64),
+                A_final=o.pack_bools(tr["A_final"]), G_final=tr["G_final"].astype(np.uint64))
+            out.append(dict(fixture=fx, n_vars=n, n_clauses=len(offs) - 1, T=T, batch=bs, iters=len(it),
+                            reproducible=False))
+    return out
+
+
 def main():
+    if "--stream-rr-only" in sys.argv:
+        tmp = tempfile.mkdtemp()
+        mf = os.path.join(HERE, "manifest.json")
+        man = json.load(open(mf))
+        old = {e["fixture"]: e for e in man.get("stream_rr_fixtures", [])}
+        kept = []
+
+        def keep(fx):
+            if "--rewrite-rr" in sys.argv or fx not in old or not os.path.exists(os.path.join(HERE, fx + ".npz")):
+                return False
+            kept.append(old[fx])
+            return True
+
+        sm = stream_rr_fixtures(tmp, keep)
+        man["stream_rr_fixtures"] = kept + sm
+        with open(mf, "w") as f:
+            json.dump(man, f, indent=1)
+        print("wrote", len(sm), "streaming T > 1 fixtures, kept", len(kept))
+        return
     if "--stream-only" in sys.argv:
         tmp = tempfile.mkdtemp()
         sm = stream_fixtures(tmp)
@@ -227,9 +298,21 @@ def main():
     with open(os.path.join(HERE, "dimacs_cases.json"), "w") as f:
         json.dump(loader, f, indent=1)
     sm = stream_fixtures(tmp)
+    old_q = {}
+    if os.path.exists(mf_path):
+        old_q = {e["fixture"]: e for e in json.load(open(mf_path)).get("stream_rr_fixtures", [])}
+    kept_q = []
+
+    def keep_q(fx):
+        if rewrite_rr or fx not in old_q or not os.path.exists(os.path.join(HERE, fx + ".npz")):
+            return False
+        kept_q.append(old_q[fx])
+        return True
+
+    sq = stream_rr_fixtures(tmp, keep_q)
     with open(os.path.join(HERE, "manifest.json"), "w") as f:
         json.dump(dict(rd_seed=RD_SEED, generator="oracle.generate_ksat(gen_seed=1, ...)",
-                       fixtures=manifest, stream_fixtures=sm), f, indent=1)
+                       fixtures=manifest, stream_fixtures=sm, stream_rr_fixtures=kept_q + sq), f, indent=1)
     print("wrote", len(manifest), "trajectory fixtures and", len(loader), "loader cases")
 
 

@@ -27,7 +27,8 @@ from conftest import GOLDEN
 
 pytestmark = pytest.mark.gpu
 
-RR_FIXTURES = sorted(p for p in glob.glob(os.path.join(GOLDEN, "*_T*.npz")) if not p.endswith("_T1.npz"))
+RR_FIXTURES = sorted(p for p in glob.glob(os.path.join(GOLDEN, "*_T*.npz"))
+                     if not p.endswith("_T1.npz") and not os.path.basename(p).startswith("stream"))
 
 
 @pytest.fixture(scope="module")

@@ -17,7 +17,7 @@ import pytest
 from conftest import GOLDEN
 
 FIXTURES = sorted(p for p in glob.glob(os.path.join(GOLDEN, "*.npz"))
-                  if not os.path.basename(p).startswith("stream_"))
+                  if not os.path.basename(p).startswith("stream"))
 STREAM_FIXTURES = sorted(glob.glob(os.path.join(GOLDEN, "stream_*.npz")))
 
 
@@ -309,6 +309,126 @@ def test_oracle_solve_stream_semantics(oracle_mod):
     lit = np.array([0 if (A0[0] & 1) else 1], np.uint32)  # the literal of variable 0 that is true
     st, A, rows = o.solve_stream(4, offs1, lit, 2, 8, trace=True)
     assert st == {**st, "n_iterations": 1, "n_resamples": 0, "avg_mis_size": 0, "solved": 1}
+
+
+# ---------------------------------------------------------------------------------------------
+# Streaming solve with T > 1 threads: fixtures from the reference's own ClauseGenerators,
+# populate_mis_parallel and resample_clauses (ref_probe `stream-rr`; its end-of-iteration check
+# runs in lock step, see oracle/ref_probe.cpp).  Per iteration: set A_i and the generators'
+# recorded state, replay the batch loop, compare every step's violated lists, the MIS (pick
+# order), its size after every step; then the check's verdict and the generators it leaves.
+STREAM_RR_FIXTURES = sorted(glob.glob(os.path.join(GOLDEN, "streamrr_*.npz")))
+
+
+def test_stream_rr_fixtures_present():
+    assert len(STREAM_RR_FIXTURES) >= 8
+    Ts = {int(load(p)["T"]) for p in STREAM_RR_FIXTURES}
+    assert {2, 4} <= Ts
+
+
+def _gens_from(G, m, T):
+    import oracle as o
+    gens = o.stream_gens(m, T)
+    for g, row in zip(gens, G):
+        g["ny"], g["fin"], g["c"] = int(row[0]), bool(row[1]), int(row[2])
+    return gens
+
+
+def _gens_state(gens):
+    return np.array([[g["ny"], int(g["fin"]), g["c"]] for g in gens], np.uint64)
+
+
+@pytest.mark.parametrize("path", STREAM_RR_FIXTURES, ids=lambda p: os.path.basename(p)[:-4])
+def test_oracle_matches_reference_stream_rr(oracle_mod, path):
+    o = oracle_mod
+    f = load(path)
+    n, offs, lits, bs, T = int(f["n_vars"]), f["offs"], f["lits"], int(f["batch"]), int(f["T"])
+    m = offs.size - 1
+    n_it = f["A"].shape[0]
+    # the generators start fresh (SATInstance.h:74-86)
+    np.testing.assert_array_equal(f["G"][0], _gens_state(o.stream_gens(m, T)))
+    assert [g["n"] for g in o.stream_gens(m, T)] == [m // T] * (T - 1) + [m - (T - 1) * (m // T)]
+    step0, total_w = 0, 0
+    for i in range(n_it):
+        gens = _gens_from(f["G"][i], m, T)
+        steps, M, cum = o.stream_rr_iteration(n, offs, lits, f["A"][i], bs, gens)
+        ns = int(f["nsteps"][i])
+        assert len(steps) == ns, f"iteration {i}: batch steps"
+        for s in range(ns):
+            for t in range(T):
+                q = (step0 + s) * T + t
+                ref = f["L"][int(f["L_ptr"][q]):int(f["L_ptr"][q + 1])]
+                np.testing.assert_array_equal(np.array(steps[s][t], np.uint32), ref,
+                                              err_msg=f"iteration {i} step {s} generator {t}")
+        np.testing.assert_array_equal(cum, f["cum"][step0:step0 + ns], err_msg=f"iteration {i}: MIS sizes")
+        np.testing.assert_array_equal(M, f["M"][int(f["M_ptr"][i]):int(f["M_ptr"][i + 1])],
+                                      err_msg=f"iteration {i}: MIS")
+        assert int(f["dres"][i]) == int(np.sum(offs[M.astype(np.int64) + 1] - offs[M.astype(np.int64)]))
+        total_w += int(np.sum(cum))
+        step0 += ns
+        # the check under the next assignment, and where it leaves the generators
+        A_next = f["A"][i + 1] if i + 1 < n_it else f["A_final"]
+        solved = o.stream_rr_check(offs, lits, A_next, gens)
+        assert solved == bool(f["solved"][i])
+        if not solved:
+            G_next = f["G"][i + 1] if i + 1 < n_it else f["G_final"]
+            np.testing.assert_array_equal(_gens_state(gens), G_next, err_msg=f"iteration {i}: check")
+        if i + 1 < n_it:  # only MIS variables changed
+            M64 = M.astype(np.int64)
+            idx = [np.arange(offs[c], offs[c + 1]) for c in M64] or [np.zeros(0, np.int64)]
+            vars_m = np.unique(lits[np.concatenate(idx).astype(np.int64)] >> 1)
+            changed = np.nonzero(o.unpack_words(f["A"][i], n) != o.unpack_words(f["A"][i + 1], n))[0]
+            assert np.isin(changed, vars_m).all()
+    st = f["stats"]
+    assert int(st[0]) == n_it
+    assert int(st[1]) == int(f["dres"].sum())
+    assert int(st[2]) == total_w // n_it
+
+
+def test_oracle_solve_stream_rr_semantics(oracle_mod):
+    """orc_solve_stream_rr (C, Philox) follows the fixture-pinned Python restatement: every
+    iteration's MIS size, delta n_resamples and resampled assignment, and the statistics."""
+    o = oracle_mod
+    cases = [
+        (o.generate_ksat(3, 300, 800, 3), 300, [(2, 1), (2, 50), (3, 133), (4, 1000), (7, 57)]),
+        (o.generate_ksat(5, 900, 2000, 4), 900, [(4, 64), (16, 5)]),
+        (o.generate_ksat(6, 40, 30, 3), 40, [(32, 2), (5, 1)]),  # m < T: empty generators
+    ]
+    for (offs, lits), n, runs in cases:
+        m = offs.size - 1
+        for T, bs in runs:
+            seed = 17 + T
+            rc, st, A_end, rows = o.solve_stream_rr(n, offs, lits, seed, bs, T, trace=True)
+            assert rc == 0 and st["solved"] == 1 and o.eval_mask(offs, lits, A_end)[0] == 0
+            gens = o.stream_gens(m, T)
+            A = o.init_assignment(seed, n)
+            w_total = 0
+            for it, nu, nm, dres, A_after in rows:
+                steps, M, cum = o.stream_rr_iteration(n, offs, lits, A, bs, gens)
+                assert (nu, nm) == (o.eval_mask(offs, lits, A)[0], M.size), (T, bs, it)
+                assert dres == int(np.sum(offs[M.astype(np.int64) + 1] - offs[M.astype(np.int64)]))
+                w_total += sum(cum)
+                np.testing.assert_array_equal(
+                    o.resample_words(A.copy(), seed, it - 1, o.clause_vars(offs, lits, M)), A_after)
+                A = A_after
+                if o.stream_rr_check(offs, lits, A, gens):
+                    break
+            assert st["n_iterations"] == len(rows)
+            assert st["sum_mis_size"] == w_total and st["avg_mis_size"] == w_total // len(rows)
+    # T = 1 is the one-thread window rule
+    offs, lits = o.generate_ksat(3, 300, 800, 3)
+    for bs in (1, 77):
+        a = o.solve_stream(300, offs, lits, 5, bs)
+        b = o.solve_stream_rr(300, offs, lits, 5, bs, 1)
+        assert a[0] == b[1] and np.array_equal(a[1], b[2])
+    # refusals: an empty clause; generators that never finish together (the reference loops)
+    offs_e, lits_e = o.csr_from_lists([[0, 2], [], [4]])
+    assert o.solve_stream_rr(3, offs_e, lits_e, 1, 1, 2)[0] == -2
+    # m = 800, T = 3: generators of 266, 266 and 268 clauses, batches of 9 (30 per walk each):
+    # after a check that leaves them at 266 - r and 268 - r unyielded, the first two finish at
+    # steps ceil((266 - r) / 9) + 30 j, the last at ceil((268 - r) / 9) + 30 j -- never together
+    offs, lits = o.generate_ksat(3, 300, 800, 3)
+    assert o.solve_stream_rr(300, offs, lits, 20, 9, 3, step_cap=10000)[0] == -1
 
 
 def test_bench_trajectory_file_regenerates(oracle_mod):

@@ -110,6 +110,34 @@ struct RRFpCtl {
     uint32_t spare[4];
 };
 static_assert(sizeof(RRFpCtl) == 128, "RRFpCtl: 32 words");
+// Streaming solve with T > 1 threads (SATInstance::solve(getEnumeratedClause, n, batch),
+// SATInstance.h:70-153).  The host plans every iteration from the generators'
+// states (alll_runtime.cpp, srr_plan); the device lists each generator's violated clauses in walk
+// order (k_srr_count / k_srr_scan / k_srr_fill) and runs the batch steps' round robins
+// (k_srr_mis).  Generator t of an iteration:
+struct SrrGen {
+    uint64_t base;    // first clause of its range
+    uint64_t n;       // clauses in its range (0: it yields nothing)
+    uint64_t pt;      // P mod n (P = 9223372036854775783, ClauseGenerator.h:109)
+    uint64_t c0;      // walk position c at the iteration start (ClauseGenerator.h:110, never reset)
+    uint64_t r;       // walk steps of its first batches: n - n_yielded, or n after a reset
+    uint64_t b;       // batch steps of those, ceil(r / batch) (it finishes at step b)
+    uint64_t p;       // batch steps of a whole walk, ceil(n / batch) (it finishes every p steps after)
+    uint64_t yields;  // its walk steps in the iteration's materialised batch steps
+    uint64_t vblk;    // its first virtual block of SRR_BLK walk steps (entry T: the block count)
+    uint64_t e0;      // first entry of its violated list (k_srr_scan)
+};
+struct SrrPlan {
+    uint32_t T;
+    uint32_t nblk;    // virtual blocks
+    uint64_t batch;
+    uint64_t steps;   // materialised batch steps (every generator has walked its whole range by then)
+    uint64_t extra;   // later batch steps, up to the one where all generators finish together: they
+                      // re-yield only clauses already seen, so each adds the MIS size to the statistic
+};
+constexpr uint32_t SRR_BLK = 4096;      // walk steps per virtual block (k_srr_count / k_srr_fill)
+constexpr uint32_t SRR_ENT_WORDS = 12;  // list entry {clause id, width, literal start, 0, 8 variables}
+
 // In-loop kernel timing (ALLL_FLAG_KERNEL_TIMING): per iteration i, slot i % TIME_SLOTS holds
 // device wall-clock stamps (s_memrealtime) {eval start (min over workgroups), eval end (max),
 // reduce start, LFMIS tail end}.
@@ -132,7 +160,8 @@ struct DevState {
     uint32_t tail_rounds;  // rounds the tail kernel needed in the last iteration
     uint32_t max_rounds;   // max total rounds seen in one iteration
     uint32_t error;        // loop stopped (done = 3): 1 LFMIS exceeded MAX_TAIL_ROUNDS or the round
-                           // robin its batch cap; 4 a k_rr_mw grid barrier timed out
+                           // robin its batch cap; 4 a k_rr_mw grid barrier timed out; 5 an incremental
+                           // round-robin pass kernel found its buffers missing
     uint32_t left_cnt;     // undecided entries handed from the last grid round to the tail
     uint32_t tmis_cnt;     // MIS entries decided by the tail kernel (list b.tmis)
     uint64_t win_start;    // streaming solve: generator steps taken before this iteration
@@ -298,6 +327,15 @@ struct LoopBuffers {
     uint32_t fp_ib, fp_tb;      // key bits of the entry index and of the turn
     uint32_t fp_hot;            // the instance has hot variables (more grid rounds per pass)
     uint32_t fp_max;            // LFMIS passes per iteration
+    // streaming solve with T > 1 threads (srr_T > 0; nullptr otherwise)
+    uint32_t srr_T;
+    SrrGen* srr_gen;            // srr_T + 1 generator plans of the iteration
+    SrrPlan* srr_plan;
+    unsigned long long* srr_first; // srr_T: first violated offset in every generator's range (~0: none)
+    uint32_t* srr_bcnt;         // 2 x virtual blocks: violated walk steps per block, then their exclusive prefix
+    uint32_t* srr_ent;          // violated walk steps of every generator in walk order (SRR_ENT_WORDS each)
+    uint32_t* srr_step;         // (steps + 1) x srr_T: first entry of generator t's batch at step s; row
+                                // `steps` = the ends of the lists
     uint32_t n_vars;
     uint32_t n_words;
     uint32_t n_tiles;       // tiles covering [0, m)
@@ -345,5 +383,10 @@ hipError_t launch_rr_finish(const ClauseView& cv, const LoopBuffers& b, hipStrea
 hipError_t launch_resample(const ClauseView& cv, const LoopBuffers& b, uint32_t tile_begin,
                            uint32_t tile_end, bool to_delta, hipStream_t s);
 hipError_t launch_apply_delta(const LoopBuffers& b, hipStream_t s);
+// streaming solve with T > 1 threads (alll_stream.hip): the check's first violated offset of every
+// generator (gated on the loop state), then the iteration's lists and round robins (b.srr_plan)
+hipError_t launch_srr_first(const LoopBuffers& b, hipStream_t s);
+hipError_t launch_srr_lists(const ClauseView& cv, const LoopBuffers& b, uint32_t nblk, hipStream_t s);
+hipError_t launch_srr_mis(const ClauseView& cv, const LoopBuffers& b, hipStream_t s);
 
 }  // namespace alll

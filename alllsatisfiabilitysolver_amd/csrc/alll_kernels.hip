@@ -2381,8 +2381,19 @@ __global__ __launch_bounds__(256) void k_rr_count(LoopBuffers b) {
 }
 
 __global__ __launch_bounds__(256) void k_rr_entries(ClauseView cv, LoopBuffers b) {
-    if (!b.state->active) return;
     const uint32_t tile = blockIdx.x, tid = threadIdx.x;
+    if (!b.state->active) {
+        // The evaluation sets the flags before the reduce decides whether the iteration runs
+        // (k_eval_flags): the last pass of a loop that stops here (solved, or capped by max_iters)
+        // leaves its flags set.  Cleared now, so that a later run (alll_set_assignment + alll_run)
+        // starts from clean flags.
+        if (b.rr_flag) {
+            uint4* fp = reinterpret_cast<uint4*>(b.rr_flag + (uint64_t)tile * TILE) + tid;
+            const uint4 f = *fp;
+            if (f.x | f.y | f.z | f.w) *fp = make_uint4(0u, 0u, 0u, 0u);
+        }
+        return;
+    }
     if (tile == 0 && tid < 2 && b.rr_ctl) b.rr_ctl[tid] = 0u;  // k_rr_mw: barrier counter, MIS count
     __shared__ uint32_t s_part[4], s_wpre[TILE_WORDS + 1];
     __shared__ uint32_t s_ids[TILE];
@@ -3796,8 +3807,25 @@ __device__ __forceinline__ unsigned long long fp_order_key(const LoopBuffers& b,
     return ((unsigned long long)b.fp_turn[i] << 32) | i;
 }
 
+// The incremental passes' buffers exist (alll_create allocates them only for instances without hot
+// variables, b.fp_inc).  k_fp_detect and k_fp_repair load from them before they read the pass state
+// (one round trip less): without them they stop the loop (state error 5, reported by the host)
+// instead of dereferencing a null buffer.  (Round 5's fault: a hoisted fp_pbits load of k_fp_turn
+// without its null test, on a power-law instance)
+__device__ __forceinline__ bool fp_inc_buffers(const LoopBuffers& b) {
+    return b.fp_inc && b.fp_blocker && b.fp_covby && b.fp_sc && b.fp_dl && b.fp_dmark && b.fp_pbits && b.fp_lst;
+}
+__device__ __forceinline__ void fp_inc_missing(const LoopBuffers& b) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        b.state->error = 5;
+        b.state->done = 3;
+        b.fp_ctl->state = FP_FAIL;
+    }
+}
+
 __global__ __launch_bounds__(FP_THREADS) void k_fp_detect(LoopBuffers b) {
     RRFpCtl* ctl = b.fp_ctl;
+    if (!fp_inc_buffers(b)) { fp_inc_missing(b); return; }  // (kernel arguments: a uniform branch)
     // (the first entry's pick byte, blocker and turn loaded before the state is read -- in bounds
     // of their buffers, independent of each other: one round trip less per pass)
     const uint32_t i1 = blockIdx.x * FP_THREADS + threadIdx.x;
@@ -4182,6 +4210,7 @@ __device__ __forceinline__ void fp_sched_core(const LoopBuffers& b, RRFpCtl* ctl
 template <uint32_t KW>
 __global__ __launch_bounds__(1024) void k_fp_repair(ClauseView cv, LoopBuffers b) {
     RRFpCtl* ctl = b.fp_ctl;
+    if (!fp_inc_buffers(b)) { fp_inc_missing(b); return; }
     const uint32_t state = ctl->state;
     if (state == FP_FINAL) {  // (as k_fp_sched: the finalizing k_fp_turn has run)
         if (blockIdx.x == 0 && threadIdx.x == 0) ctl->state = FP_DONE;
@@ -4971,7 +5000,9 @@ __global__ __launch_bounds__(FP_TURN_THREADS) void k_fp_turn(ClauseView cv, Loop
         }
     }
     __syncthreads();
-    fp_turn_blocks<KW>(cv, b, fin, inc != 0, pbsrc != 0, nu, T, stamp, s_sf, s_pf, s_nseg, s_er, lds_seg ? s_seg : b.fp_seg, s_w,
+    // (the incremental passes' picks live in fp_pbits, which exists only with b.fp_inc)
+    const bool has_pb = b.fp_pbits != nullptr;
+    fp_turn_blocks<KW>(cv, b, fin, inc != 0 && has_pb, pbsrc != 0 && has_pb, nu, T, stamp, s_sf, s_pf, s_nseg, s_er, lds_seg ? s_seg : b.fp_seg, s_w,
                        [&](uint32_t blk) { return blkoff[blk]; }, pre);
     if (fin && blockIdx.x == 0 && threadIdx.x == 0) {
         st->tmis_cnt = ctl->total;
@@ -5284,6 +5315,9 @@ hipError_t launch_rr_prep(const ClauseView& cv, const LoopBuffers& b, bool marke
 hipError_t launch_rr_passes(const ClauseView& cv, const LoopBuffers& b, uint32_t n, bool full, hipStream_t s) {
     if (!b.fp_ctl) return hipSuccess;
     const FpGrids g = fp_grids(b);
+    // (the incremental kernels need their buffers: never enqueued without them)
+    if (b.fp_inc && (!b.fp_blocker || !b.fp_covby || !b.fp_sc || !b.fp_dl || !b.fp_dmark || !b.fp_pbits || !b.fp_lst))
+        return hipErrorInvalidValue;
     for (uint32_t p = 0; p < n; ++p) {
         if (b.fp_inc && !(full && p == 0)) {
             // an incremental pass (its kernels run only when the device state asks for one)

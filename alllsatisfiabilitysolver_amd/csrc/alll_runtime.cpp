@@ -126,6 +126,17 @@ struct alll_ctx {
     std::vector<uint32_t> perm;  // evaluation position -> clause id (fixed-k layout)
     std::string eval_name;
     int wall_khz = 100000;       // s_memrealtime rate (ALLL_FLAG_KERNEL_TIMING)
+    // Streaming solve with T > 1 threads (b.srr_T > 0): the reference's
+    // ClauseGenerator states (ClauseGenerator.h:104-113) between iterations, the plan of the next
+    // one (pinned, uploaded per iteration) and the device lists, grown on demand
+    struct SGen { uint64_t base = 0, n = 0, c = 0, ny = 0; bool fin = false; };
+    std::vector<SGen> sgen;
+    bool srr_started = false;   // an iteration ran: the next one starts where its check stopped
+    uint64_t srr_batch = 1;
+    SrrGen* h_srr = nullptr;
+    SrrPlan* h_plan = nullptr;
+    unsigned long long* h_first = nullptr;
+    size_t srr_cap_blk = 0, srr_cap_ent = 0, srr_cap_step = 0;
 };
 
 namespace {
@@ -309,6 +320,8 @@ int read_state(alll_ctx* c) {
     if (c->h_state->error == 4)
         return fail(ALLL_ERR_HIP, "round-robin MIS: a grid barrier of k_rr_mw timed out (its %u workgroups "
                                   "were not all resident)", c->b.rr_mw);
+    if (c->h_state->error == 5)
+        return fail(ALLL_ERR_HIP, "round-robin MIS: an incremental-pass kernel ran without its buffers (DESIGN.md §10)");
     if (c->h_state->error)
         return fail(ALLL_ERR_UNSUPPORTED, c->b.rr_T ? "round-robin MIS exceeded its batch cap in one iteration"
                                                     : "LFMIS needed more than %u rounds in one iteration",
@@ -573,6 +586,152 @@ int launch_rr_iteration(alll_ctx* c, hipEvent_t* marks) {
     return launch_rr_piece(c, marks, 2, 0);
 }
 
+// ---- streaming solve with T > 1 threads ------------------------------------
+// Device lists grown on demand (the stream is drained: the caller has just read the state).
+int srr_grow(alll_ctx* c, uint32_t** p, size_t& cap, size_t need) {
+    if (need <= cap) return ALLL_OK;
+    need = std::max<size_t>(need + need / 4, 1024);
+    if (*p) { (void)hipFree(*p); *p = nullptr; cap = 0; }
+    void* q = nullptr;
+    const hipError_t e = hipMalloc(&q, need * 4);
+    if (e != hipSuccess) return fail(ALLL_ERR_OOM, "hipMalloc(%zu bytes) failed: %s", need * 4, hipGetErrorString(e));
+    *p = static_cast<uint32_t*>(q);
+    cap = need;
+    return ALLL_OK;
+}
+
+// smallest s >= 1 with s = b_t (mod p_t) for every generator: the batch step at which all of them
+// finish together (1 <= b_t <= p_t); false when there is none, or it lies beyond 2^62
+bool srr_common_finish(const std::vector<uint64_t>& bs, const std::vector<uint64_t>& ps, uint64_t* S) {
+    __int128 a = 0, mod = 1;  // s = a (mod mod)
+    for (size_t t = 0; t < bs.size(); ++t) {
+        const __int128 n2 = ps[t], a2 = bs[t] % ps[t];
+        // a + mod k = a2 (mod n2)
+        __int128 r0 = mod, r1 = n2, x0 = 1, x1 = 0;  // extended Euclid: x0 mod = r0 (mod n2)
+        while (r1) {
+            const __int128 q = r0 / r1, r = r0 - q * r1, x = x0 - q * x1;
+            r0 = r1; r1 = r; x0 = x1; x1 = x;
+        }
+        const __int128 g = r0, d = a2 - a;
+        if (d % g != 0) return false;
+        const __int128 n2g = n2 / g;
+        __int128 k = ((d / g) % n2g) * (x0 % n2g) % n2g;
+        if (k < 0) k += n2g;
+        a = a + mod * k;
+        mod = mod * n2g;
+        if (mod > ((__int128)1 << 62)) return false;
+        a %= mod;
+    }
+    *S = a == 0 ? (uint64_t)mod : (uint64_t)a;
+    return true;
+}
+
+// One iteration: evaluation + reduce (the previous iteration's check) + the check's stop offsets;
+// then, while the loop is active, the plan from the generators' states, the lists, the round robins
+// and the resample.  Host-synchronous (one state read per iteration).
+int launch_srr_iteration(alll_ctx* c, hipEvent_t* marks) {
+    hipStream_t s = c->stream;
+    LoopBuffers& b = c->b;
+    const uint32_t T = b.srr_T;
+    if (marks) HIP_TRY(hipEventRecord(marks[0], s));
+    HIP_TRY(eval_launch(c, c->own_begin, c->own_end, true));
+    if (marks) { HIP_TRY(hipEventRecord(marks[1], s)); HIP_TRY(hipEventRecord(marks[2], s)); }
+    HIP_TRY(launch_reduce(b, 0, s));
+    HIP_TRY(launch_srr_first(b, s));
+    HIP_TRY(hipMemcpyAsync(c->h_first, b.srr_first, T * 8ull, hipMemcpyDeviceToHost, s));
+    int rc = read_state(c);
+    if (rc) return rc;
+    if (!c->h_state->active) {
+        if (marks) { HIP_TRY(hipEventRecord(marks[3], s)); HIP_TRY(hipEventRecord(marks[4], s)); }
+        return ALLL_OK;
+    }
+    std::vector<alll_ctx::SGen>& gens = c->sgen;
+    if (c->srr_started) {
+        // the lock-step check stopped after its first step that found a violated clause: every
+        // generator has yielded min(n_t, f + 1) clauses (oracle/alll_oracle.c orc_solve_stream_rr)
+        unsigned long long f = ~0ull;
+        for (uint32_t t = 0; t < T; ++t) f = std::min(f, c->h_first[t]);
+        for (auto& g : gens) {
+            g.ny = std::min<uint64_t>(g.n, f + 1);
+            g.fin = g.ny == g.n;
+        }
+    }
+    // ---- plan: every generator's first window (r steps, finished at batch step b) and walks (p
+    // steps each); the step S at which all finish together; the lists stop at the step by which
+    // every generator has walked its whole range (later steps re-yield seen clauses only)
+    const uint64_t B = c->srr_batch;
+    std::vector<uint64_t> bs(T), ps(T), zs(T);
+    for (uint32_t t = 0; t < T; ++t) {
+        const auto& g = gens[t];
+        SrrGen& d = c->h_srr[t];
+        d.base = g.base;
+        d.n = g.n;
+        d.pt = g.n ? 9223372036854775783ull % g.n : 0;
+        d.c0 = g.c;
+        if (g.n == 0) { d.r = 0; d.b = 1; d.p = 1; zs[t] = 1; }
+        else {
+            d.r = g.fin ? g.n : g.n - g.ny;
+            d.b = (d.r + B - 1) / B;
+            d.p = (g.n + B - 1) / B;
+            zs[t] = d.r == g.n ? d.b : d.b + d.p;
+        }
+        bs[t] = d.b;
+        ps[t] = d.p;
+    }
+    uint64_t S = 0;
+    if (!srr_common_finish(bs, ps, &S))
+        return fail(ALLL_ERR_UNSUPPORTED, "streaming solve, %u threads: the generators never finish at the same "
+                                          "batch step (the reference's loop, SATInstance.h:98-125, would not end)", T);
+    const uint64_t steps = std::min<uint64_t>(S, *std::max_element(zs.begin(), zs.end()));
+    uint64_t nblk = 0, total = 0;
+    for (uint32_t t = 0; t < T; ++t) {
+        SrrGen& d = c->h_srr[t];
+        uint64_t y = 0;
+        if (d.n) {
+            if (steps <= d.b) y = std::min<uint64_t>(d.r, steps * B);
+            else {
+                const uint64_t q = steps - d.b;
+                y = d.r + (q / d.p) * d.n + std::min<uint64_t>(d.n, (q % d.p) * B);
+            }
+        }
+        d.yields = y;
+        d.vblk = nblk;
+        d.e0 = 0;
+        nblk += (y + SRR_BLK - 1) / SRR_BLK;
+        total += y;
+    }
+    c->h_srr[T] = SrrGen{};
+    c->h_srr[T].vblk = nblk;
+    if (total >= 0xFFFFFFFFull || nblk >= (1ull << 31) || (steps + 1) * T >= (1ull << 40))
+        return fail(ALLL_ERR_UNSUPPORTED, "streaming solve: %llu walk steps in one iteration (limit 2^32)",
+                    (unsigned long long)total);
+    *c->h_plan = SrrPlan{T, (uint32_t)nblk, B, steps, S - steps};
+    if ((rc = srr_grow(c, &b.srr_bcnt, c->srr_cap_blk, 2 * nblk + 1)) ||
+        (rc = srr_grow(c, &b.srr_ent, c->srr_cap_ent, std::max<uint64_t>(total, 1) * SRR_ENT_WORDS)) ||
+        (rc = srr_grow(c, &b.srr_step, c->srr_cap_step, (steps + 1) * T)))
+        return rc;
+    HIP_TRY(hipMemcpyAsync(b.srr_gen, c->h_srr, (T + 1) * sizeof(SrrGen), hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(b.srr_plan, c->h_plan, sizeof(SrrPlan), hipMemcpyHostToDevice, s));
+    HIP_TRY(launch_srr_lists(c->cv, b, (uint32_t)nblk, s));
+    HIP_TRY(launch_srr_mis(c->cv, b, s));
+    if (marks) HIP_TRY(hipEventRecord(marks[3], s));
+    HIP_TRY(launch_resample(c->cv, b, c->own_begin, c->own_end, false, s));
+    if (marks) HIP_TRY(hipEventRecord(marks[4], s));
+    // after the batch loop every generator has finished (n_yielded = n_t) at walk position
+    // c0 + (its walk steps in all S batch steps) P: r + whole walks, i.e. c0 + r P (mod n_t)
+    for (uint32_t t = 0; t < T; ++t) {
+        auto& g = gens[t];
+        const SrrGen& d = c->h_srr[t];
+        if (g.n) g.c = (uint64_t)(((unsigned __int128)(d.r % g.n) * d.pt + g.c) % g.n);
+        g.ny = g.n;
+        g.fin = true;
+    }
+    c->srr_started = true;
+    // (the pinned plan is read by the copies above; the next iteration drains the stream in its
+    // state read before it rewrites the plan)
+    return ALLL_OK;
+}
+
 int ensure_graph(alll_ctx* c, int variant, int j) {
     if (!c->use_graph || c->graph_exec[variant][j]) return ALLL_OK;
     hipError_t e = hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal);
@@ -609,7 +768,15 @@ int ensure_graph(alll_ctx* c, int variant, int j) {
 }
 
 // n iterations: n / 8 replays of the 8-iteration graph, then one replay per set bit of n % 8
+int launch_srr_iteration(alll_ctx* c, hipEvent_t* marks);
+
 int launch_iterations(alll_ctx* c, uint64_t n) {
+    if (c->b.srr_T) {
+        int rc;
+        for (uint64_t i = 0; i < n; ++i)
+            if ((rc = launch_srr_iteration(c, nullptr))) return rc;
+        return ALLL_OK;
+    }
     if (c->b.rr_T && c->b.fp_ctl) {
         int rc;
         for (uint64_t i = 0; i < n; ++i)
@@ -649,7 +816,7 @@ int fill_stats(alll_ctx* c, alll_stats* st) {
         const uint32_t r = c->tiles_per_rank ? t / c->tiles_per_rank : 0;
         if (r < ALLL_MAX_GPU_STATS) st->gpu_resamples[r] += ts[2 * t + 1];
     }
-    if (c->b.stream_batch && st->n_iterations) {
+    if (c->opt.stream_batch && st->n_iterations) {
         // a stream iteration is evaluation + MIS + resample + the full check (SATInstance.h:
         // 91-147); the check is the next evaluation pass, so the stream iterations are the
         // resample rounds: every pass but a final non-resampling one (solved or capped), and
@@ -753,6 +920,21 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     const uint32_t rr_T = (opt.n_threads > 1 && !(opt.flags & ALLL_FLAG_LFMIS) && !opt.stream_batch)
                               ? (uint32_t)opt.n_threads : 0u;
     if (rr_T > RR_TMAX) return fail(ALLL_ERR_UNSUPPORTED, "n_threads %u > %u chunks", rr_T, RR_TMAX);
+    // the streaming solve with n_threads > 1: T clause generators and the per-batch round robin
+    // (SATInstance.h:70-153)
+    const uint32_t srr_T = (opt.n_threads > 1 && !(opt.flags & ALLL_FLAG_LFMIS) && opt.stream_batch)
+                               ? (uint32_t)opt.n_threads : 0u;
+    if (srr_T) {
+        if (srr_T > RR_TMAX) return fail(ALLL_ERR_UNSUPPORTED, "streaming solve: n_threads %u > %u", srr_T, RR_TMAX);
+        if (opt.world > 1) return fail(ALLL_ERR_UNSUPPORTED, "streaming solve with n_threads > 1 runs on one GPU");
+        // an empty clause is violated forever and, sharing no variable, joins the MIS at every batch
+        // step; the reference never returns on it (as with one thread), and here its repeats past the
+        // materialised steps would be miscounted: refused
+        for (uint64_t c = 0; c < m; ++c)
+            if (prob->offsets[c + 1] == prob->offsets[c])
+                return fail(ALLL_ERR_UNSUPPORTED, "streaming solve with n_threads > 1: clause %llu is empty",
+                            (unsigned long long)c);
+    }
     std::vector<uint32_t> rr_sets;
     if (rr_T) {
         rr_sets.resize(rr_T + 1);
@@ -907,7 +1089,7 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     b.n_cu = (uint32_t)c->n_cu;
     b.n_tiles = n_tiles;
     b.m = m;
-    if (opt.stream_batch && m) {
+    if (opt.stream_batch && m && !srr_T) {
         // key of the streaming solve: position in the generator sequence j*P mod m, so the
         // inverse of P mod m (P is prime, so it exists for every m < P)
         const uint64_t p = 9223372036854775783ull % m;
@@ -1000,6 +1182,27 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
                 if (const char* e = getenv("ALLL_RR_INC_AFTER")) b.fp_inc_after = (uint32_t)std::max(1, atoi(e));
             }
         }
+    }
+    if (srr_T) {
+        if ((rc = dalloc(c, &b.srr_gen, srr_T + 1)) || (rc = dalloc(c, &b.srr_plan, 1)) ||
+            (rc = dalloc(c, &b.srr_first, srr_T)))
+            return bail(rc);
+        if (hipHostMalloc((void**)&c->h_srr, (srr_T + 1) * sizeof(SrrGen), 0) != hipSuccess ||
+            hipHostMalloc((void**)&c->h_plan, sizeof(SrrPlan), 0) != hipSuccess ||
+            hipHostMalloc((void**)&c->h_first, srr_T * 8ull, 0) != hipSuccess)
+            return bail(fail(ALLL_ERR_OOM, "hipHostMalloc failed"));
+        b.srr_T = srr_T;
+        c->srr_batch = opt.stream_batch;
+        // the generators of SATInstance.h:74-86 (T t_n_clauses = n_clauses / n_threads, the last
+        // one takes the remainder), fresh
+        c->sgen.resize(srr_T);
+        const uint64_t tn = m / srr_T;
+        for (uint32_t t = 0; t < srr_T; ++t) {
+            c->sgen[t].base = (uint64_t)t * tn;
+            c->sgen[t].n = t == srr_T - 1 ? m - c->sgen[t].base : tn;
+        }
+        c->use_graph = false;
+        c->graph_note = "streaming solve with n_threads > 1: host-planned iterations (eager launches)";
     }
     if ((rc = dalloc(c, &b.A, b.n_words + 4))) return bail(rc);  // +4: 16-byte tail loads
     if ((rc = dalloc(c, &b.vmask, (size_t)c->n_tiles_padded * TILE_WORDS))) return bail(rc);
@@ -1419,6 +1622,11 @@ int alll_destroy(alll_ctx* c) {
     if (c->rr_post) (void)hipGraphExecDestroy(c->rr_post);
     for (auto g : c->rr_graph) (void)hipGraphDestroy(g);
     if (c->h_fp) (void)hipHostFree(c->h_fp);
+    if (c->h_srr) (void)hipHostFree(c->h_srr);
+    if (c->h_plan) (void)hipHostFree(c->h_plan);
+    if (c->h_first) (void)hipHostFree(c->h_first);
+    for (uint32_t* p : {c->b.srr_bcnt, c->b.srr_ent, c->b.srr_step})
+        if (p) (void)hipFree(p);
     if (c->comm) ncclCommDestroy(c->comm);
     for (void* p : c->allocs) (void)hipFree(p);
     for (auto& e : c->ev)
@@ -1447,7 +1655,7 @@ int alll_solve(alll_ctx* c, alll_stats* st) {
     if (rc) return rc;
     // (streaming solve: max_iters counts stream iterations; the last one's check is one more
     // evaluation pass, which does not resample)
-    const uint64_t cap = c->opt.max_iters ? c->opt.max_iters + (c->b.stream_batch ? 1 : 0) : ~0ull;
+    const uint64_t cap = c->opt.max_iters ? c->opt.max_iters + (c->opt.stream_batch ? 1 : 0) : ~0ull;
     if (c->h_state->done != 1) {
         if ((rc = write_limits(c, cap, cap))) return rc;
         uint64_t batch = 1;
@@ -1658,7 +1866,8 @@ int alll_profile(alll_ctx* c, uint64_t n_iters, alll_phase_times* out) {
     if ((rc = write_limits(c, c->h_state->n_iter + n_iters, ~0ull))) return rc;
     double acc[4] = {0, 0, 0, 0};
     for (uint64_t i = 0; i < n_iters; ++i) {
-        if (c->b.rr_T && c->b.fp_ctl) rc = launch_rr_iteration(c, c->ev);
+        if (c->b.srr_T) rc = launch_srr_iteration(c, c->ev);
+        else if (c->b.rr_T && c->b.fp_ctl) rc = launch_rr_iteration(c, c->ev);
         else rc = enqueue_iteration(c, c->ev, round0_variant(c));
         if (rc) return rc;
         HIP_TRY(hipEventSynchronize(c->ev[4]));

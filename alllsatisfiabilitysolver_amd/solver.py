@@ -376,7 +376,11 @@ class SATInstance:
         lits = np.fromiter((l for c in flat for l in c.literals), np.uint32, int(offs[-1]))
         return offs, lits
 
-    def solve(self, clauses) -> Statistics:  # SATInstance.h:60-66
+    def solve(self, clauses, n_clauses: Optional[int] = None, batch_size: Optional[int] = None) -> Statistics:
+        """solve(clauses) -- SATInstance.h:60-66; solve(getEnumeratedClause, n_clauses, batch_size)
+        -- the streaming overload, SATInstance.h:70-153 (getEnumeratedClause(index, t_id) -> Clause)."""
+        if callable(clauses):
+            return self._solve_stream(clauses, int(n_clauses), int(batch_size))
         self.n_clauses += sum(len(c) for c in clauses)
         offs, lits = self._flatten(clauses)
         starts = None
@@ -392,6 +396,41 @@ class SATInstance:
         thr = [0] * self.n_threads
         thr[0] = d["n_resamples"]
         return Statistics(d["n_iterations"], d["n_resamples"], d["avg_mis_size"], thr)
+
+    def _generated(self, fn, n_clauses: int):
+        """Clauses 0 .. n-1 from the callback, each with the t_id of the generator whose range
+        holds it (SATInstance.h:74-86: n / T each, the last one the remainder)."""
+        T = self.n_threads
+        per = n_clauses // T
+        out = []
+        for i in range(n_clauses):
+            t = min(i // per, T - 1) if per else T - 1
+            cl = fn(i, t)
+            if cl is None:
+                raise ValueError(f"clause generator returned None for index {i}")
+            out.append(cl)
+        return out
+
+    def _solve_stream(self, fn, n_clauses: int, batch_size: int) -> Statistics:
+        self.n_clauses = n_clauses
+        offs, lits = self._flatten([self._generated(fn, n_clauses)])
+        with Solver(self.n_vars, offs, lits, seed=self._seed, device=self._device, n_threads=self.n_threads,
+                    max_iters=self._max_iters, stream_batch=max(1, batch_size)) as s:
+            d = s.solve()
+            self.var_arr.vars[:] = s.assignment().astype(np.bool_)
+        thr = [0] * self.n_threads
+        thr[0] = d["n_resamples"]
+        return Statistics(d["n_iterations"], d["n_resamples"], d["avg_mis_size"], thr)
+
+    def writeDIMACS(self, fn, n_clauses: int, out_f) -> None:  # SATInstance.h:175-203
+        self.n_clauses = n_clauses
+        out_f.write(f"p cnf {self.n_vars} {n_clauses}\n")
+        for i in range(n_clauses):
+            cl = fn(i, 0)
+            if cl is None:
+                raise ValueError(f"clause generator returned None for index {i}")
+            toks = [str(-(l >> 1) - 1) if (l & 1) else str((l >> 1) + 1) for l in cl.literals]
+            out_f.write("".join(" " + x for x in toks) + " 0\n")
 
     def verify_validity(self, clauses) -> bool:  # SATInstance.h:156-173
         v = self.var_arr.vars

@@ -80,11 +80,20 @@ typedef struct alll_options {
     uint32_t grid_rounds;   /* full-grid LFMIS rounds before the tail kernel (0 = default) */
     uint64_t stream_batch;  /* 0: SATInstance::solve(vector<ClauseArray*>*) semantics.  > 0: the
                                streaming solve SATInstance::solve(getEnumeratedClause, n_clauses,
-                               batch_size) (SATInstance.h:70-153) with one thread and this batch
-                               size: the MIS follows the clause generator's yield order
-                               (ClauseGenerator.h:33-70) and alll_stats reports its statistics
-                               (n_iterations = stream iterations, avg_mis_size summed per batch);
-                               max_iters then caps stream iterations */
+                               batch_size) (SATInstance.h:70-153) with this batch size and
+                               n_threads clause generators (ClauseGenerator.h:32-71): with one
+                               thread the MIS follows the generator's yield order; with n_threads
+                               = T > 1 every batch step runs the T-set round robin over the T
+                               generators' violated lists, filtered by the MIS so far
+                               (SATInstance.h:98-125, 391-447), and the end-of-iteration check
+                               runs in lock step.  T > 1 returns
+                               ALLL_ERR_UNSUPPORTED for an empty clause, for world > 1, and from
+                               alll_solve / alll_run at an iteration whose generators would never
+                               finish at the same batch step (the reference's loop does not end
+                               there).  ALLL_FLAG_LFMIS keeps the one-thread order for any T.
+                               alll_stats reports the reference's statistics (n_iterations =
+                               stream iterations, avg_mis_size summed per batch step); max_iters
+                               then caps stream iterations */
     const uint64_t* set_starts; /* n_threads > 1: n_threads + 1 non-decreasing clause indices,
                                chunk q = [set_starts[q], set_starts[q+1]), set_starts[0] = 0,
                                set_starts[n_threads] = n_clauses (the sizes of the caller's

@@ -70,18 +70,20 @@ class SATInstance {
     }
 
     // Streaming solve (reference SATInstance.h:70-153): clauses come from a callback by index.
-    // With 288 GB of HBM the instance is materialised once (callback order and t_id as the
-    // reference's per-thread generators would use) and the GPU runs the streaming semantics of
-    // one thread: the MIS follows the generator's yield order, batch by batch
-    // (alll_options.stream_batch); a batch size of 0 is taken as 1.
+    // With 288 GB of HBM the instance is materialised once (each index with the t_id of the
+    // generator whose range holds it, SATInstance.h:74-86) and the GPU runs the streaming
+    // semantics of n_threads generators (alll_options.stream_batch): one thread's MIS follows the
+    // generator's yield order, T > 1 threads' MIS is the per-batch round robin over the T
+    // generators.  A batch size of 0 is taken as 1 (the reference's generators never finish).
+    // T > 1 throws std::runtime_error where the reference would not return (alll.h).
     Statistics* solve(Clause<T>* (*getEnumeratedClause)(T, unsigned short int), ull n_clauses, T batch_size) {
         this->n_clauses = n_clauses;
         vector<uint64_t> offs(1, 0);
         vector<uint32_t> lits;
         const int nt = n_threads_ > 0 ? n_threads_ : 1;
-        const ull per = n_clauses / (ull)nt;
+        const ull per = n_clauses / (ull)nt;  // (T t_n_clauses, SATInstance.h:74; the last takes the rest)
         for (ull i = 0; i < n_clauses; ++i) {
-            const unsigned short t = (unsigned short)(per ? std::min<ull>(i / per, (ull)nt - 1) : 0);
+            const unsigned short t = (unsigned short)(per ? std::min<ull>(i / per, (ull)nt - 1) : (ull)nt - 1);
             Clause<T>* cl = getEnumeratedClause((T)i, t);
             if (!cl) throw std::runtime_error("alll: clause generator returned nullptr");
             for (auto l : *cl->literals) lits.push_back((uint32_t)l);

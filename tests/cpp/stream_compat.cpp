@@ -1,6 +1,6 @@
 // Test driver (not product code): the compatibility SATInstance API's streaming solve and
 // writeDIMACS, compiled against include/alll_compat exactly like a reference consumer.
-//   stream_compat <cnf-in> <batch> <dimacs-out>
+//   stream_compat <cnf-in> <batch> <dimacs-out> [n_threads]
 //   stream_compat order <m> <batch>   yield order of ClauseGenerator over m always-violated clauses
 // loads a DIMACS file (one clause per line) into a table served by the clause callback, runs
 // solve(getEnumeratedClause, n_clauses, batch), prints the statistics and the assignment as
@@ -64,8 +64,14 @@ int main(int argc, char** argv) {
         g_clauses.push_back(cl);
     }
     auto var_arr = new VariablesArray<UINT_T>((UINT_T)n_vars);
-    SATInstance<UINT_T> S(var_arr, 1);
-    Statistics* st = S.solve(enumerated, (ull)g_clauses.size(), (UINT_T)atol(argv[2]));
+    SATInstance<UINT_T> S(var_arr, argc > 4 ? atoi(argv[4]) : 1);
+    Statistics* st = nullptr;
+    try {
+        st = S.solve(enumerated, (ull)g_clauses.size(), (UINT_T)atol(argv[2]));
+    } catch (const std::exception& e) {
+        printf("{\"error\": \"%s\"}\n", e.what());
+        return 3;
+    }
     printf("{\"n_iterations\": %llu, \"n_resamples\": %llu, \"avg_mis_size\": %llu, \"threads\": %zu, \"assignment\": \"",
            st->n_iterations, st->n_resamples, st->avg_mis_size, st->n_thread_resamples.size());
     for (long v = 0; v < n_vars; ++v) putchar(var_arr->vars[v] ? '1' : '0');

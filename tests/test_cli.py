@@ -95,8 +95,10 @@ def test_compat_stream_api_compiles(native, tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("batch", [1, 50, 100000])
-def test_compat_stream_solve_matches_oracle(oracle_mod, native, tmp_path, batch):
+@pytest.mark.parametrize("batch,T", [(1, 1), (50, 1), (100000, 1), (1, 2), (50, 2), (7, 4), (100000, 4)])
+def test_compat_stream_solve_matches_oracle(oracle_mod, native, tmp_path, batch, T):
+    """solve(getEnumeratedClause, n, batch) of the compatibility SATInstance with n_threads = T
+    (SATInstance.h:70-153): statistics and assignment equal the oracle's streaming solve."""
     o = oracle_mod
     exe = _build_stream_driver(tmp_path)
     n, m, seed = 300, 600, 17
@@ -105,10 +107,15 @@ def test_compat_stream_solve_matches_oracle(oracle_mod, native, tmp_path, batch)
     cnf.write_text(o.to_dimacs(n, offs, lits))
     out = tmp_path / "w.cnf"
     env = dict(os.environ, ALLL_SEED=str(seed))
-    r = subprocess.run([exe, str(cnf), str(batch), str(out)], capture_output=True, text=True, env=env)
-    assert r.returncode == 0, r.stderr
+    r = subprocess.run([exe, str(cnf), str(batch), str(out), str(T)], capture_output=True, text=True, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
     got = json.loads(r.stdout)
-    st, A, _ = o.solve_stream(n, offs, lits, seed, batch)
+    if T == 1:
+        st, A, _ = o.solve_stream(n, offs, lits, seed, batch)
+    else:
+        rc, st, A, _ = o.solve_stream_rr(n, offs, lits, seed, batch, T)
+        assert rc == 0
+        assert got["threads"] == T
     assert st["solved"] == 1
     for key in ("n_iterations", "n_resamples", "avg_mis_size"):
         assert got[key] == st[key], key
@@ -123,6 +130,23 @@ def test_compat_stream_solve_matches_oracle(oracle_mod, native, tmp_path, batch)
     np.testing.assert_array_equal(lits2, lits)
 
 
+@pytest.mark.gpu
+def test_compat_stream_threads_refuses_what_never_ends(oracle_mod, native, tmp_path):
+    """n_threads = 3 over 800 clauses (generators of 266, 266, 268), batches of 9: after the first
+    check the generators never finish at the same batch step, the reference's loop would not end;
+    the compatibility solve throws (no silent fallback to another order)."""
+    o = oracle_mod
+    exe = _build_stream_driver(tmp_path)
+    offs, lits = o.generate_ksat(3, 300, 800, 3)
+    assert o.solve_stream_rr(300, offs, lits, 20, 9, 3, step_cap=10000)[0] == -1
+    cnf = tmp_path / "x.cnf"
+    cnf.write_text(o.to_dimacs(300, offs, lits))
+    env = dict(os.environ, ALLL_SEED="20")
+    r = subprocess.run([exe, str(cnf), "9", str(tmp_path / "w.cnf"), "3"], capture_output=True, text=True, env=env)
+    assert r.returncode == 3, r.stdout + r.stderr
+    assert "never finish" in json.loads(r.stdout)["error"]
+
+
 def test_compat_clause_generator_order(oracle_mod, native, tmp_path):
     """The compatibility ClauseGenerator walks clauses in the reference generator's order
     (ClauseGenerator.h:47), continuing across passes."""
@@ -133,3 +157,22 @@ def test_compat_clause_generator_order(oracle_mod, native, tmp_path):
         got = json.loads(r.stdout)
         order = oracle_mod.stream_order(m)
         np.testing.assert_array_equal(got, np.concatenate([order, order]))
+
+
+def test_python_write_dimacs(oracle_mod):
+    """SATInstance.writeDIMACS of the Python mirror (SATInstance.h:175-203): same text layout,
+    parsed back to the same instance."""
+    import io
+
+    from alllsatisfiabilitysolver_amd.solver import Clause, SATInstance, VariablesArray
+
+    offs, lits = oracle_mod.generate_ksat(2, 50, 120, 3)
+    S = SATInstance(VariablesArray(50), 2)
+    buf = io.StringIO()
+    S.writeDIMACS(lambda i, t: Clause(lits[int(offs[i]):int(offs[i + 1])].tolist(), t), 120, buf)
+    text = buf.getvalue()
+    assert text.startswith("p cnf 50 120\n") and text.splitlines()[1].startswith(" ")
+    rc, (v, offs2, lits2) = oracle_mod.dimacs_parse(text.encode())
+    assert rc == 0 and v == 50
+    np.testing.assert_array_equal(offs2, offs)
+    np.testing.assert_array_equal(lits2, lits)

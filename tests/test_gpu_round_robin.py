@@ -347,3 +347,26 @@ def test_rr_under_torch_runtime(gpu, oracle_mod, tmp_path):
     assert d["n_iterations"] == K == len(rows)
     assert d["n_resamples"] == sum(r[3] for r in rows) and d["sum_mis_size"] == sum(r[2] for r in rows)
     np.testing.assert_array_equal(np.load(out), rows[-1][4])
+
+
+def test_rr_flags_cleared_when_the_loop_stops(gpu, oracle_mod):
+    """The evaluation sets the clause-order violated flags before the reduce decides whether the
+    iteration runs (k_eval_flags): a loop stopped by max_iters leaves them set unless cleared
+    (ADVICE r5).  solve(max_iters) -> set_assignment -> run(1) must pick the oracle's MIS of the
+    new assignment, and resample exactly its variables."""
+    from alllsatisfiabilitysolver_amd import Solver, generate_ksat
+
+    n, m, T = 2000, 8000, 4  # ratio 4: not solved within the cap
+    offs, lits = generate_ksat(4, n, m, 3)
+    A_new = oracle_mod.init_assignment(77, n)
+    with Solver(n, offs, lits, seed=3, n_threads=T, max_iters=3) as s:
+        st = s.solve()
+        assert st["solved"] == 0 and st["n_violated"] > 0
+        s.set_assignment_words(A_new)
+        s.run(1)
+        nu, vm = oracle_mod.eval_mask(offs, lits, A_new)
+        M = oracle_mod.rr_mis(n, offs, lits, mask_to_list(vm, m), T)
+        np.testing.assert_array_equal(s.mis(), np.sort(M))
+        it = s.stats()["n_iterations"] - 1
+        A_exp = oracle_mod.resample_words(A_new.copy(), 3, it, oracle_mod.clause_vars(offs, lits, M))
+        np.testing.assert_array_equal(s.assignment_words(), A_exp)

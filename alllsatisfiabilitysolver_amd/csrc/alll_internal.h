@@ -60,12 +60,19 @@ constexpr uint32_t FP_G = 4;       // grid LFMIS rounds before the one-workgroup
 constexpr uint32_t FP_G_HOT = 6;   // ... on instances with hot variables (5, 7, 8, 10: slower)
 constexpr uint32_t FP_G_MAX = FP_G_HOT > FP_G ? FP_G_HOT : FP_G;
 constexpr uint32_t FP_MAX_DEFAULT = 64;    // LFMIS passes per iteration before k_rr_mw decides it
+// incremental passes: defaults of LoopBuffers::fp_rep_cap / fp_rw_min / fp_rw_timeout
+constexpr uint32_t FP_REP_CAP = 1u << 16;   // dirty entries per round before the pass gives up (a full pass follows)
+constexpr uint32_t FP_RW_GRID = 64;         // workgroups of the wide repair (one per CU, all resident)
+constexpr uint32_t FP_RW_MIN = 256;         // rounds this small are left to the one-workgroup repair
+constexpr unsigned long long FP_RW_TIMEOUT = 2000000ull;  // wide-round barrier timeout: 20 ms at 100 MHz
 constexpr uint32_t FP_LOG_PASSES = 64;     // passes of an iteration in the pass log (fp_log)
 constexpr uint32_t FP_LOG_RW = 64;         // words per pass of the timing log behind it: {detect, wide, repair,
                                            //   rounds end, repair end, LDS loaded, schedule, phases} clock
                                            //   stamps, {round entries, stamp} pairs (24 rounds), then the
                                            //   first 4 wide rounds' pre-barrier stamps (words 56, 58, 60, 62)
-constexpr uint32_t FP_LOG_WORDS = 4 * FP_LOG_PASSES + FP_LOG_RW * FP_LOG_PASSES;
+// (one timing row per pass and one more for k_fp_bbuild's phase stamps; the rows are written and
+// cleared only with ALLL_FLAG_KERNEL_TIMING, the per-pass counts always)
+constexpr uint32_t FP_LOG_WORDS = 4 * FP_LOG_PASSES + FP_LOG_RW * (FP_LOG_PASSES + 1);
 enum : uint32_t { FP_RUN = 0, FP_FINAL = 1, FP_DONE = 2, FP_OFF = 3, FP_FAIL = 4 };
 struct RRFpCtl {
     uint32_t state;      // FP_*: RUN iterating; FINAL the last pass converged (finalize now);
@@ -107,7 +114,8 @@ struct RRFpCtl {
     uint32_t wbar;
     uint32_t pbsrc;      // the last pass was incremental: its picks are the bits fp_pbits (k_fp_turn reads
                          // them there), not bit 0 of fp_in
-    uint32_t spare[4];
+    uint32_t rw_timeouts;  // wide-round grid barriers that timed out (never reset; alll_rr_barrier_timeouts)
+    uint32_t spare[3];
 };
 static_assert(sizeof(RRFpCtl) == 128, "RRFpCtl: 32 words");
 // Streaming solve with T > 1 threads (SATInstance::solve(getEnumeratedClause, n, batch),
@@ -323,6 +331,10 @@ struct LoopBuffers {
                                 //   rounds, entries decided, changes}, then the timing log (FP_LOG_RW per
                                 //   pass; alll_rr_pass_log; measurement)
     uint32_t fp_inc;            // incremental passes enabled (no hot variables)
+    uint32_t fp_rep_cap;        // dirty entries per repair round before the pass gives up (FP_REP_CAP; tests lower it)
+    uint32_t fp_rw_min;         // wide repair rounds run while a round holds more entries than this (FP_RW_MIN;
+                                // ~0u: no wide rounds, e.g. when its workgroups cannot all be resident)
+    unsigned long long fp_rw_timeout;  // wide-round grid barrier timeout, 100 MHz ticks (FP_RW_TIMEOUT; tests)
     uint32_t fp_inc_after;      // full passes of an iteration before the incremental ones
     uint32_t fp_ib, fp_tb;      // key bits of the entry index and of the turn
     uint32_t fp_hot;            // the instance has hot variables (more grid rounds per pass)
@@ -336,6 +348,7 @@ struct LoopBuffers {
     uint32_t* srr_ent;          // violated walk steps of every generator in walk order (SRR_ENT_WORDS each)
     uint32_t* srr_step;         // (steps + 1) x srr_T: first entry of generator t's batch at step s; row
                                 // `steps` = the ends of the lists
+    uint32_t tail_chunked;      // k_tail always takes its chunked passes (env ALLL_TAIL_CHUNKED=1; tests, A/B)
     uint32_t n_vars;
     uint32_t n_words;
     uint32_t n_tiles;       // tiles covering [0, m)
@@ -383,6 +396,8 @@ hipError_t launch_rr_finish(const ClauseView& cv, const LoopBuffers& b, hipStrea
 hipError_t launch_resample(const ClauseView& cv, const LoopBuffers& b, uint32_t tile_begin,
                            uint32_t tile_end, bool to_delta, hipStream_t s);
 hipError_t launch_apply_delta(const LoopBuffers& b, hipStream_t s);
+// resident workgroups of k_fp_repair per CU (its wide rounds need all FP_RW_GRID of them at once)
+hipError_t fp_repair_occupancy(const ClauseView& cv, const LoopBuffers& b, int* blocks_per_cu);
 // streaming solve with T > 1 threads (alll_stream.hip): the check's first violated offset of every
 // generator (gated on the loop state), then the iteration's lists and round robins (b.srr_plan)
 hipError_t launch_srr_first(const LoopBuffers& b, hipStream_t s);

@@ -1087,8 +1087,8 @@ __device__ void fp_begin_body(const LoopBuffers& b) {
     // fall in a tile; the end and the starts past the last clause are nu
     for (uint32_t s = threadIdx.x; s <= T; s += blockDim.x)
         if (s == T || b.rr_sets[s] >= b.m) b.fp_sf[s] = nu;
-    if (b.fp_log)
-        for (uint32_t q = threadIdx.x; q < FP_LOG_WORDS; q += blockDim.x) b.fp_log[q] = 0;
+    if (b.fp_log)  // (the per-pass counts; the timing rows only when they are written)
+        for (uint32_t q = threadIdx.x; q < (b.ktime ? FP_LOG_WORDS : 4 * FP_LOG_PASSES); q += blockDim.x) b.fp_log[q] = 0;
     if (threadIdx.x == 0) {
         const bool ep0 = fp_ep_restart(b, ctl), ser0 = fp_serial_restart(b, ctl);
         ctl->restart = (ep0 ? 1u : 0u) | (ser0 ? 2u : 0u);
@@ -2015,10 +2015,138 @@ __global__ __launch_bounds__(BJN_THREADS) void k_bjoin(ClauseView cv, LoopBuffer
 }
 
 // Tail: one workgroup finishes the LFMIS over the compact list handed over by the last grid
-// round (CLAIM / barrier / JOIN passes until no undecided clause is left).  Entries are
-// processed in chunks of one per thread; survivors are compacted in place (a write position
-// never passes the chunk being read).  owner / cover are accessed with agent-scope relaxed
-// atomics so no stale L1 line is read across the barriers.
+// round (CLAIM / barrier / JOIN passes until no undecided clause is left).  owner / cover are
+// accessed with agent-scope relaxed atomics so no stale L1 line is read across the barriers.
+//
+// Up to TAIL_REG_PER(K) x 1024 entries (the common case) the entries stay in registers for the
+// whole tail (thread t holds entries t, t + 1024, ...): a round is one kill test + claim pass and
+// one ownership pass over every thread's entries at once, its loads all in flight together, and
+// no list is rewritten.  (Round 6: chunks of one entry per thread with a barrier per chunk made a
+// round cost one dependent chain per 1024 entries, so the tail could not take over from the grid
+// rounds before only a few hundred entries were left.)  Longer lists take the chunked passes.
+template <int K>
+constexpr uint32_t tail_reg_per() { return K > 4 ? 4u : (K == 4 ? 8u : 12u); }
+constexpr uint32_t TAIL_GROUP = 4;  // entries whose loads are in flight together (registers)
+
+template <int K>
+__device__ __forceinline__ void tail_regs(const ClauseView& cv, const LoopBuffers& b, DevState* st, uint32_t first_round,
+                                          const Ent<K>& e0, uint32_t n0, uint32_t stamp, uint32_t rbase) {
+    constexpr int S = Ent<K>::S;
+    constexpr uint32_t E = tail_reg_per<K>();
+    __shared__ uint32_t s_live[2], s_tm;
+    Ent<K> e[E];
+    uint32_t alive = 0;  // bit q: entry threadIdx.x + q * TAIL_THREADS is undecided
+#pragma unroll
+    for (uint32_t q = 0; q < E; ++q) {
+        const uint32_t i = threadIdx.x + q * TAIL_THREADS;
+        if (i < n0) {
+            if (q == 0) e[q] = e0;
+            else load_ent<K>(e[q], b.left + (uint64_t)i * S);
+            alive |= 1u << q;
+        }
+    }
+    if (threadIdx.x == 0) { s_tm = 0; s_live[0] = 0; s_live[1] = 0; }
+    __syncthreads();
+    uint32_t n = n0, epoch = rbase + first_round, rounds = 0;
+    unsigned long long* owner = b.owner;
+    while (n > 0) {
+        // (the entry words made opaque each round: otherwise the compiler hoists every entry's
+        // cover / owner addresses out of the round loop and keeps them all live -- 128 VGPRs and
+        // spills)
+#pragma unroll
+        for (uint32_t q = 0; q < E; ++q)
+#pragma unroll
+            for (int w = 0; w < S; ++w) asm volatile("" : "+v"(e[q].w[w]));
+        const unsigned long long keyhi = (unsigned long long)(~epoch) << 32;
+        // CLAIM: kill tests (the cover loads of TAIL_GROUP entries in flight together), then the
+        // claims of the survivors
+#pragma unroll
+        for (uint32_t g = 0; g < E; g += TAIL_GROUP) {
+            uint32_t killed = 0;
+#pragma unroll
+            for (uint32_t q = g; q < g + TAIL_GROUP && q < E; ++q) {
+                if (!((alive >> q) & 1u)) continue;
+                uint64_t lb;
+                const uint32_t len = ent_len<K>(cv, e[q], lb);
+                bool k = false;
+                for (uint32_t j = 0; j < len; ++j)
+                    k |= __hip_atomic_load(&b.cover[lit_var(ent_lit<K>(cv, e[q], lb, j))], __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT) == stamp;
+                killed |= (uint32_t)k << q;
+            }
+            alive &= ~killed;
+#pragma unroll
+            for (uint32_t q = g; q < g + TAIL_GROUP && q < E; ++q) {
+                if (!((alive >> q) & 1u)) continue;
+                uint64_t lb;
+                const uint32_t len = ent_len<K>(cv, e[q], lb);
+                const unsigned long long key = keyhi | prio(b, st, e[q].w[0]);
+                for (uint32_t j = 0; j < len; ++j)
+                    __hip_atomic_fetch_min(&owner[vmix(b, lit_var(ent_lit<K>(cv, e[q], lb, j)))], key,
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            spec_fence();
+        }
+        __syncthreads();
+        // JOIN: a claimer holding every variable it claimed joins.  (Its own claims were this
+        // round's, and a round's keys are below every older key, so the owner key's low word --
+        // the winner's priority -- decides.)
+#pragma unroll
+        for (uint32_t g = 0; g < E; g += TAIL_GROUP) {
+            uint32_t joined = 0;
+#pragma unroll
+            for (uint32_t q = g; q < g + TAIL_GROUP && q < E; ++q) {
+                if (!((alive >> q) & 1u)) continue;
+                uint64_t lb;
+                const uint32_t len = ent_len<K>(cv, e[q], lb);
+                const uint32_t kc = prio(b, st, e[q].w[0]);
+                bool own = true;
+                for (uint32_t j = 0; j < len; ++j)
+                    own &= __hip_atomic_load(reinterpret_cast<const uint32_t*>(&owner[vmix(b, lit_var(ent_lit<K>(cv, e[q], lb, j)))]),
+                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == kc;
+                joined |= (uint32_t)own << q;
+            }
+#pragma unroll
+            for (uint32_t q = g; q < g + TAIL_GROUP && q < E; ++q) {
+                if (!((joined >> q) & 1u)) continue;
+                uint64_t lb;
+                const uint32_t len = ent_len<K>(cv, e[q], lb);
+                const uint32_t c = e[q].w[0];
+                for (uint32_t j = 0; j < len; ++j)
+                    __hip_atomic_store(&b.cover[lit_var(ent_lit<K>(cv, e[q], lb, j))], (uint8_t)stamp, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                b.tmis[atomicAdd(&s_tm, 1u)] = c;
+                atomicAdd(&b.tile_stats[2 * (c / TILE)], mis_weight(b, st, prio(b, st, c)));
+                atomicAdd(&b.tile_stats[2 * (c / TILE) + 1], (unsigned long long)len);
+            }
+            alive &= ~joined;
+            spec_fence();
+        }
+        uint32_t cnt = (uint32_t)__popc(alive);
+        for (int o = 32; o > 0; o >>= 1) cnt += __shfl_down(cnt, o, 64);
+        if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(&s_live[rounds & 1], cnt);
+        __syncthreads();
+        n = s_live[rounds & 1];
+        // (the other slot was last read before this round's first barrier: reset for the next round)
+        if (threadIdx.x == 0) s_live[(rounds + 1) & 1] = 0;
+        ++rounds;
+        ++epoch;
+        if (rounds >= MAX_TAIL_ROUNDS && n > 0) {
+            if (threadIdx.x == 0) { st->error = 1; st->done = 3; }
+            break;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (epoch > st->round_next) st->round_next = epoch;
+        st->tail_rounds = rounds;
+        st->tmis_cnt = s_tm;
+        const uint32_t total = first_round + rounds;
+        if (total > st->max_rounds) st->max_rounds = total;
+        if (b.ktime) time_slot(b, st->n_iter - 1)[3] = wall_now();
+    }
+}
+
 template <int K>
 __global__ __launch_bounds__(TAIL_THREADS) void k_tail(ClauseView cv, LoopBuffers b, uint32_t first_round) {
     DevState* st = b.state;
@@ -2030,6 +2158,12 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail(ClauseView cv, LoopBuffer
     const uint32_t active = st->active, stamp = st->stamp, n0 = st->left_cnt, rbase = st->round_base;
     spec_fence();
     if (!active) return;
+    if (n0 <= tail_reg_per<K>() * TAIL_THREADS && !b.tail_chunked) {
+        tail_regs<K>(cv, b, st, first_round, e0, n0, stamp, rbase);
+        return;
+    }
+    // chunked passes: entries in chunks of one per thread; survivors compacted in place (a write
+    // position never passes the chunk being read)
     __shared__ uint32_t s_wp, s_tm;
     uint32_t n = n0;
     uint32_t epoch = rbase + first_round;
@@ -2322,7 +2456,12 @@ __device__ __forceinline__ uint32_t fp_block_scan(uint32_t x, uint32_t* s_w, uin
 
 // the timing log of pass p (FP_LOG_RW words; nullptr past FP_LOG_PASSES) and its round records
 __device__ __forceinline__ uint32_t* fp_tlog(const LoopBuffers& b, uint32_t p) {
-    return b.fp_log && p < FP_LOG_PASSES ? b.fp_log + 4 * FP_LOG_PASSES + FP_LOG_RW * p : nullptr;
+    // (measurement: only with ALLL_FLAG_KERNEL_TIMING)
+    return b.fp_log && b.ktime && p < FP_LOG_PASSES ? b.fp_log + 4 * FP_LOG_PASSES + FP_LOG_RW * p : nullptr;
+}
+// k_fp_bbuild's phase stamps: the row after the passes' rows
+__device__ __forceinline__ uint32_t* fp_tlog_bbuild(const LoopBuffers& b) {
+    return b.fp_log && b.ktime ? b.fp_log + 4 * FP_LOG_PASSES + FP_LOG_RW * FP_LOG_PASSES : nullptr;
 }
 __device__ __forceinline__ void fp_tround(uint32_t* t, uint32_t r, uint32_t n) {
     if (t && r < FP_LOG_RW / 2 - 8) {
@@ -3268,7 +3407,7 @@ __global__ __launch_bounds__(FP_BB_THREADS) void k_fp_bbuild(LoopBuffers b) {
     __shared__ uint32_t s_ns;
     const uint32_t n = b.fp_bfill[bk];
     constexpr uint32_t U4 = 4;  // loads in flight per thread
-    uint32_t* tlb = bk == 0 && tid == 0 ? fp_tlog(b, FP_LOG_PASSES - 1) : nullptr;  // (phase stamps: measurement)
+    uint32_t* tlb = bk == 0 && tid == 0 ? fp_tlog_bbuild(b) : nullptr;  // (phase stamps: measurement)
     if (tlb) tlb[0] = (uint32_t)wall_now();
     for (uint32_t w = tid; w < nw; w += FP_BB_THREADS) s_cnt[w] = 0u;
     if (tid == 0) s_ns = 0;
@@ -3798,7 +3937,6 @@ __global__ __launch_bounds__(1024) void k_fp_tail(ClauseView cv, LoopBuffers b, 
 // (at M: a few thousand entries in at most ~8 rounds per pass, against ~800k entries and ~10
 // kernels of a full pass).  Instances with hot variables keep the full passes (a hub's claimant
 // list would be scanned per decision).
-constexpr uint32_t FP_REP_CAP = 1u << 16;   // dirty entries per round before the pass gives up (a full pass follows)
 constexpr uint32_t FP_REP_QMAX = 1u << 20;  // entries whose decisions the repair keeps in LDS (128 KiB of bits):
                                             // iterations with more violated clauses keep the full passes
 constexpr uint32_t FP_REP_MAXR = 4096;      // repair rounds per pass before it gives up
@@ -4094,11 +4232,8 @@ __device__ __forceinline__ uint8_t* fp_pold(const LoopBuffers& b) {
 // once a round holds at most FP_RW_MIN entries and hands the list, the change log and the round
 // stamp over to k_fp_repair; a grid barrier that times out (workgroups not all resident) hands
 // over as well, at a round boundary, so the result is the same either way.
-constexpr uint32_t FP_RW_GRID = 64;   // workgroups of the wide repair (one per CU, all resident)
-constexpr uint32_t FP_RW_MIN = 256;   // rounds this small are left to the one-workgroup repair
-constexpr unsigned long long FP_RW_TIMEOUT = 2000000ull;  // 20 ms at 100 MHz
 
-__device__ __forceinline__ bool fp_rw_barrier(RRFpCtl* ctl, uint32_t target) {
+__device__ __forceinline__ bool fp_rw_barrier(const LoopBuffers& b, RRFpCtl* ctl, uint32_t target) {
     __shared__ uint32_t s_ok;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -4112,11 +4247,12 @@ __device__ __forceinline__ bool fp_rw_barrier(RRFpCtl* ctl, uint32_t target) {
         atomicAdd(&ctl->wbar, 1u);
         const unsigned long long t0 = wall_now();
         while (__hip_atomic_load(&ctl->wbar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-            if (wall_now() - t0 > FP_RW_TIMEOUT) { ok = 0; break; }
+            if (wall_now() - t0 > b.fp_rw_timeout) { ok = 0; break; }
             __builtin_amdgcn_s_sleep(1);
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the invalidate completes before the barrier below)
+        if (!ok) atomicAdd(&ctl->rw_timeouts, 1u);  // (a slowdown the host can report: the pass gives up)
         s_ok = ok;
     }
     __syncthreads();
@@ -4140,7 +4276,7 @@ __device__ bool fp_wide_rounds(const ClauseView& cv, const LoopBuffers& b, RRFpC
     bool ok = true;
     if (tl) tl[1] = (uint32_t)wall_now();
     if (threadIdx.x == 0) s_over = 0;
-    while (n > FP_RW_MIN && n <= FP_REP_CAP && ok && r < FP_REP_MAXR) {
+    while (n > b.fp_rw_min && n <= b.fp_rep_cap && ok && r < FP_REP_MAXR) {
         ++rid;
         work += n;
         const uint32_t* A = b.fp_dl + (size_t)cur * b.m;
@@ -4174,7 +4310,7 @@ __device__ bool fp_wide_rounds(const ClauseView& cv, const LoopBuffers& b, RRFpC
         if (threadIdx.x == 0) cnts[(size_t)((r + 1) & 1) * FP_RW_GRID + g] = s_over ? 0xFFFFFFFFu : s_nb;
         if (tl && r < 4) tl[56 + 2 * r] = (uint32_t)wall_now();  // (the round's decisions issued: measurement)
         ++r;
-        ok = fp_rw_barrier(ctl, r * G);
+        ok = fp_rw_barrier(b, ctl, r * G);
         fp_tround(tl, r - 1, n);
         if (!ok) break;  // (the round is complete on this workgroup; the others may not be: fail)
         // the next list's segment starts (a full segment fails the pass)
@@ -4235,7 +4371,7 @@ __global__ __launch_bounds__(1024) void k_fp_repair(ClauseView cv, LoopBuffers b
     bool bail = nu > FP_REP_QMAX;
     if (!bail) bail = !fp_wide_rounds<KW>(cv, b, ctl, s_hk, s_pre, n, rid, rounds, work, wcur, tl);
     if (blockIdx.x != 0) return;
-    // (a wide round leaves at most FP_RW_MIN entries unless the pass gives up: all in LDS below)
+    // (a wide round leaves at most fp_rw_min (<= FP_RL) entries unless the pass gives up: all in LDS below)
     if (rounds > 0 && n > FP_RL) bail = true;
     if (tl) tl[2] = (uint32_t)wall_now();
     if (n0 == 0 && rounds == 0 && !bail) {
@@ -4312,7 +4448,7 @@ __global__ __launch_bounds__(1024) void k_fp_repair(ClauseView cv, LoopBuffers b
     // entries below, so the rounds settle on the exact LFMIS (the lowest dirty entry is final
     // after its first decision, and so on up).
     while (n > 0 && !bail) {
-        if (n > FP_REP_CAP || rounds >= FP_REP_MAXR) { bail = true; break; }
+        if (n > b.fp_rep_cap || rounds >= FP_REP_MAXR) { bail = true; break; }
         ++rounds;
         ++rid;
         work += n;
@@ -5375,6 +5511,13 @@ hipError_t launch_resample(const ClauseView& cv, const LoopBuffers& b, uint32_t 
     if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
     k_resample_vars<<<(uint32_t)blocks, 256, 0, s>>>(b);
     return hipGetLastError();
+}
+
+hipError_t fp_repair_occupancy(const ClauseView& cv, const LoopBuffers& b, int* blocks_per_cu) {
+    const size_t lq = ((size_t)std::min<uint64_t>(b.m, FP_REP_QMAX) + 127) / 128 * 16;
+    const bool narrow = b.rr_k >= 1 && b.rr_k <= 4;
+    return narrow ? hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k_fp_repair<4>, 1024, lq)
+                  : hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k_fp_repair<0>, 1024, lq);
 }
 
 hipError_t launch_apply_delta(const LoopBuffers& b, hipStream_t s) {

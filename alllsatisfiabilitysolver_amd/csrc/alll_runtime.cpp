@@ -1105,6 +1105,7 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
         b.stream_batch = opt.stream_batch;
     }
     b.seed = opt.seed;
+    if (const char* e = getenv("ALLL_TAIL_CHUNKED")) b.tail_chunked = atoi(e) != 0;  // (tests, A/B)
     if (rr_T) {
         uint32_t* d_sets = nullptr;
         if ((rc = dalloc(c, &b.rr_u, 12 * (size_t)m))) return bail(rc);  // scan entries (k_rr_entries)
@@ -1179,6 +1180,14 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
                     return bail(rc);
                 b.fp_inc = 1;
                 b.fp_inc_after = 1;
+                // the repair's limits (tests lower them to force the fallbacks: a pass that gives
+                // up, wide rounds on small instances, barriers that time out)
+                b.fp_rep_cap = FP_REP_CAP;
+                b.fp_rw_min = FP_RW_MIN;
+                b.fp_rw_timeout = FP_RW_TIMEOUT;
+                if (const char* e = getenv("ALLL_RR_REP_CAP")) b.fp_rep_cap = (uint32_t)std::max(1, atoi(e));
+                if (const char* e = getenv("ALLL_RR_RW_MIN")) b.fp_rw_min = (uint32_t)std::max(0, atoi(e));
+                if (const char* e = getenv("ALLL_RR_RW_TIMEOUT")) b.fp_rw_timeout = strtoull(e, nullptr, 10);
                 if (const char* e = getenv("ALLL_RR_INC_AFTER")) b.fp_inc_after = (uint32_t)std::max(1, atoi(e));
             }
         }
@@ -1569,6 +1578,17 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     {  // kernel attributes (dynamic LDS), outside every stream capture
         const hipError_t e = prepare_kernels(cv, b);
         if (e != hipSuccess) return bail(fail(ALLL_ERR_HIP, "kernel attributes: %s", hipGetErrorString(e)));
+    }
+    if (b.fp_inc) {
+        // the wide repair rounds synchronise their workgroups by a grid barrier: all of them must be
+        // resident at once, else every incremental pass would wait for the barrier's timeout and
+        // give up; without that guarantee the repair keeps to its one-workgroup rounds
+        int per_cu = 0;
+        const uint32_t gw = std::min<uint32_t>(FP_RW_GRID, std::max(1, c->n_cu));
+        if (fp_repair_occupancy(cv, b, &per_cu) != hipSuccess || (uint64_t)per_cu * (uint64_t)c->n_cu < gw) {
+            (void)hipGetLastError();
+            b.fp_rw_min = ~0u;
+        }
     }
 
     // ---- RCCL communicator (clause-sharded mode; world 1 with a comm id: a one-rank
@@ -1966,6 +1986,15 @@ int alll_rr_pass_log(alll_ctx* c, uint32_t* out, uint32_t n_words) {
     if (nw) HIP_TRY(hipMemcpy(out, c->b.fp_log, nw * 4ull, hipMemcpyDeviceToHost));
     for (uint32_t i = nw; i < n_words; ++i) out[i] = 0;
     return (int)nw;
+}
+
+int64_t alll_rr_barrier_timeouts(alll_ctx* c) {
+    if (!c) return -1;
+    if (!c->b.fp_ctl) return 0;
+    if (hipSetDevice(c->device) != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess) return -1;
+    RRFpCtl ctl;
+    if (hipMemcpy(&ctl, c->b.fp_ctl, sizeof ctl, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    return ctl.rw_timeouts;
 }
 
 int alll_comm_size(alll_ctx* c) {

@@ -269,15 +269,23 @@ class Solver:
     def rr_round_log(self):
         """Round robin: per pass of the last iteration, the repair's clock stamps (100 MHz;
         detect, wide repair, repair, rounds end, repair end, LDS loaded) and its rounds
-        {entries, stamp} (measurement; rows of 64 words, zeros where not reached)."""
+        {entries, stamp}, then a row of k_fp_bbuild's phase stamps (measurement, written only
+        with FLAG_KERNEL_TIMING; rows of 64 words, zeros where not reached)."""
         return self._rr_log()[1]
 
     def _rr_log(self):
-        out = np.zeros(256 + 64 * 64, np.uint32)
+        out = np.zeros(256 + 64 * 65, np.uint32)
         n = self._L.alll_rr_pass_log(self._ctx, _p(out, _u32p), out.size)
         if n < 0:
             N.check(n, "rr_pass_log")
         return out[:min(n, 256)].reshape(-1, 4), out[256:max(n, 256)].reshape(-1, 64)
+
+    def rr_barrier_timeouts(self) -> int:
+        """Round robin: wide-repair grid barriers that timed out since create (measurement)."""
+        n = int(self._L.alll_rr_barrier_timeouts(self._ctx))
+        if n < 0:
+            raise N.AlllError(N.ALLL_ERR_HIP, "alll_rr_barrier_timeouts failed")
+        return n
 
     def comm_size(self) -> int:
         """Ranks in the solve: the RCCL communicator's count (or world with a host exchange)."""

@@ -214,11 +214,18 @@ const char* alll_eval_kernel(alll_ctx* ctx);
 int alll_uses_graphs(alll_ctx* ctx, const char** why);
 /* Round robin (n_threads > 1): the pass log of the last iteration, 4 words per pass {dirty
  * entries, repair rounds (0xFFFFFFFF: the incremental pass gave up), entries decided, decisions
- * changed} for the incremental passes (zeros for full ones), at most 64 passes, then 64 words per
- * pass of repair clock stamps (100 MHz; words 0..5: detect, wide repair, repair, rounds end,
- * repair end, decisions loaded; from word 8 {round entries, stamp} pairs); returns the words
- * written (0 without incremental passes).  (No reference counterpart: measurement) */
+ * changed} for the incremental passes (zeros for full ones), at most 64 passes, then -- written
+ * only with ALLL_FLAG_KERNEL_TIMING, zeros otherwise -- 64 words per pass of repair clock stamps
+ * (100 MHz; words 0..5: detect, wide repair, repair, rounds end, repair end, decisions loaded;
+ * from word 8 {round entries, stamp} pairs) and one 64-word row of k_fp_bbuild's phase stamps;
+ * returns the words written (0 without incremental passes).  (No reference counterpart:
+ * measurement) */
 int alll_rr_pass_log(alll_ctx* ctx, uint32_t* out, uint32_t n_words);
+/* Round robin: grid barriers of the incremental passes' wide repair rounds that timed out since
+ * alll_create (each makes its pass give up and a full pass follow: correct, slower); -1 on failure.
+ * Non-zero means the repair's workgroups were not all resident (the GPU shared with other work).
+ * (No reference counterpart: measurement) */
+int64_t alll_rr_barrier_timeouts(alll_ctx* ctx);
 /* Ranks taking part in the clause-sharded solve: ncclCommCount of the RCCL communicator, or
  * alll_options.world with a host-staged exchange (1 on one GPU); -1 on failure.  (The
  * reference counterpart is the thread count of the -p path, example/main.cpp:76-84.) */

@@ -124,6 +124,10 @@ SPECS = {
     "ragged": (5000, 20000, (2, 12), 0, 5, 6),
     # 8-SAT: the wide fixed-width entries
     "k8": (40000, 60000, 8, 0, 3, 4),
+    # the 8-way split of the BASELINE 8-GPU configs (C4, C5) at a small size: 16 tiles, two per
+    # rank; and 9 tiles over 8 ranks (two per rank: ranks 5-7 own no clause)
+    "small8": (16000, 64000, 3, 0, 5, 6),
+    "uneven8": (9000, 36000, 3, 0, 5, 6),
 }
 ENV = {"small_positions": {"ALLL_PACKED_IDS": "0"}}
 
@@ -136,7 +140,9 @@ ENV = {"small_positions": {"ALLL_PACKED_IDS": "0"}}
                                                   (2, "allgather", "small_rr4"),
                                                   (3, "allreduce", "small_rr4"), (2, "allgather", "c2_rr7"),
                                                   (3, "allgather", "small_positions"), (2, "allgather", "ragged"),
-                                                  (3, "allreduce", "ragged"), (2, "allgather", "k8")])
+                                                  (3, "allreduce", "ragged"), (2, "allgather", "k8"),
+                                                  (8, "allgather", "small8"), (8, "allreduce", "small8"),
+                                                  (8, "allgather", "uneven8")])
 def test_sharded_solver_matches_oracle(oracle_mod, native, world, mode, spec_name):
     """Every rank lays out its own shard only; the other shards' violated lists come from the
     all-gathered clause-order mask and the AoS literals (k_cmark / k_collect)."""

@@ -37,7 +37,10 @@ LAYOUTS = {"hybrid": (0, {}), "fixed": (1 << 3, {}), "csr": (1 << 2, {}), "atomi
            # many small LDS windows (64 words: 2048 variables; the C4 layout on small instances),
            # with the cached and with the non-temporal (C4) evaluation
            "small_windows": (0, {"ALLL_EVAL_WINDOWS": "1", "ALLL_WIN_WORDS": "64"}),
-           "small_windows_nt": (0, {"ALLL_EVAL_WINDOWS": "1", "ALLL_WIN_WORDS": "64", "ALLL_EVAL_NT": "1"})}
+           "small_windows_nt": (0, {"ALLL_EVAL_WINDOWS": "1", "ALLL_WIN_WORDS": "64", "ALLL_EVAL_NT": "1"}),
+           # the tail's chunked passes (the default keeps up to 12 x 1024 entries in registers),
+           # with the tail in every iteration after the first
+           "tail_chunked": (0, {"ALLL_TAIL_CHUNKED": "1", "ALLL_SMALL_U": str(1 << 62)})}
 
 
 def make_solver(layout, monkeypatch, *args, **kw):
@@ -365,11 +368,11 @@ def test_baseline_sizes_bit_exact_steps(gpu, oracle_mod, name, monkeypatch):
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("name", ["C2_3sat_4M", "M_3sat_10M"])
+@pytest.mark.parametrize("name", ["C2_3sat_4M", "M_3sat_10M", "C3_8sat_6M", "C5_powerlaw_10M", "C4_3sat_128M"])
 def test_full_size_long_run_bit_exact(gpu, oracle_mod, name):
-    """C2 and M at full size over 8 consecutive iterations, every one against the oracle's
-    (violated count, MIS list, resampled assignment): the full-size cases above check 2
-    iterations, the bench digests only the end state of a longer run."""
+    """Every BASELINE config on the GPU at full size over 8 consecutive iterations, every one
+    against the oracle's (violated count, MIS list, resampled assignment): the full-size cases
+    above check 2 iterations, the bench digests only the end state of a longer run."""
     from alllsatisfiabilitysolver_amd import Solver, generate_ksat
 
     n, m, k, kind = BIG[name]

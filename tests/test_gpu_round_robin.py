@@ -370,3 +370,44 @@ def test_rr_flags_cleared_when_the_loop_stops(gpu, oracle_mod):
         it = s.stats()["n_iterations"] - 1
         A_exp = oracle_mod.resample_words(A_new.copy(), 3, it, oracle_mod.clause_vars(offs, lits, M))
         np.testing.assert_array_equal(s.assignment_words(), A_exp)
+
+
+@pytest.mark.parametrize("knobs", [{"ALLL_RR_INC": "0"}, {"ALLL_RR_REP_CAP": "4"}, {"ALLL_RR_RW_MIN": "4"},
+                                   {"ALLL_RR_RW_MIN": "4", "ALLL_RR_RW_TIMEOUT": "0"}],
+                         ids=["full_passes_only", "repair_gives_up", "wide_rounds_small", "wide_barrier_timeout"])
+def test_rr_incremental_pass_fallbacks(gpu, oracle_mod, rr_kernel, knobs, monkeypatch):
+    """The incremental passes' fallbacks stay exact: full passes only
+    (ALLL_RR_INC=0); a repair whose dirty set outgrows its cap gives up and a full pass follows;
+    the wide (multi-workgroup) repair rounds on a small instance; wide rounds whose grid barrier
+    times out (the pass gives up, counted by alll_rr_barrier_timeouts).  Trajectory against the
+    oracle after every iteration, and the pass log shows the fallback happened."""
+    from alllsatisfiabilitysolver_amd import Solver, generate_ksat
+    from alllsatisfiabilitysolver_amd import _native as N
+
+    if rr_kernel != "fp":
+        pytest.skip("incremental passes: the default fixpoint mode")
+    n, m, T, seed, K = 20000, 80000, 8, 3, 6
+    offs, lits = generate_ksat(9, n, m, 3)
+    st_o, A_o, rows = oracle_mod.solve(n, offs, lits, seed, max_iters=K + 1, trace=True, T=T)
+    for k, v in knobs.items():
+        monkeypatch.setenv(k, v)
+    logs, wide = [], 0
+    with Solver(n, offs, lits, seed=seed, n_threads=T, flags=N.FLAG_KERNEL_TIMING) as s:
+        for k in knobs:
+            monkeypatch.delenv(k)
+        for it, nu, nm, dres, A_after in rows[:K]:
+            s.run(1)
+            np.testing.assert_array_equal(s.assignment_words(), A_after, err_msg=f"iter {it}")
+            logs.append(s.rr_pass_log().copy())
+            wide += int((s.rr_round_log()[:64, 56] != 0).sum())  # a wide round's stamp per pass
+        timeouts = s.rr_barrier_timeouts()
+    inc = [r for lg in logs for r in lg if r.any()]
+    bails = [r for r in inc if r[1] == 0xFFFFFFFF]
+    if "ALLL_RR_INC" in knobs:
+        assert not inc and timeouts == 0
+    elif "ALLL_RR_REP_CAP" in knobs:
+        assert bails, "no incremental pass gave up"
+    elif "ALLL_RR_RW_TIMEOUT" in knobs:
+        assert timeouts > 0 and bails
+    else:
+        assert wide > 0 and timeouts == 0, "no wide repair round ran"

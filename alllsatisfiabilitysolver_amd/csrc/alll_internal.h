@@ -348,7 +348,6 @@ struct LoopBuffers {
     uint32_t* srr_ent;          // violated walk steps of every generator in walk order (SRR_ENT_WORDS each)
     uint32_t* srr_step;         // (steps + 1) x srr_T: first entry of generator t's batch at step s; row
                                 // `steps` = the ends of the lists
-    uint32_t tail_chunked;      // k_tail always takes its chunked passes (env ALLL_TAIL_CHUNKED=1; tests, A/B)
     uint32_t n_vars;
     uint32_t n_words;
     uint32_t n_tiles;       // tiles covering [0, m)

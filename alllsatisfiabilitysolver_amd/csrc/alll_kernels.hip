@@ -2015,138 +2015,13 @@ __global__ __launch_bounds__(BJN_THREADS) void k_bjoin(ClauseView cv, LoopBuffer
 }
 
 // Tail: one workgroup finishes the LFMIS over the compact list handed over by the last grid
-// round (CLAIM / barrier / JOIN passes until no undecided clause is left).  owner / cover are
-// accessed with agent-scope relaxed atomics so no stale L1 line is read across the barriers.
-//
-// Up to TAIL_REG_PER(K) x 1024 entries (the common case) the entries stay in registers for the
-// whole tail (thread t holds entries t, t + 1024, ...): a round is one kill test + claim pass and
-// one ownership pass over every thread's entries at once, its loads all in flight together, and
-// no list is rewritten.  (Round 6: chunks of one entry per thread with a barrier per chunk made a
-// round cost one dependent chain per 1024 entries, so the tail could not take over from the grid
-// rounds before only a few hundred entries were left.)  Longer lists take the chunked passes.
-template <int K>
-constexpr uint32_t tail_reg_per() { return K > 4 ? 4u : (K == 4 ? 8u : 12u); }
-constexpr uint32_t TAIL_GROUP = 4;  // entries whose loads are in flight together (registers)
-
-template <int K>
-__device__ __forceinline__ void tail_regs(const ClauseView& cv, const LoopBuffers& b, DevState* st, uint32_t first_round,
-                                          const Ent<K>& e0, uint32_t n0, uint32_t stamp, uint32_t rbase) {
-    constexpr int S = Ent<K>::S;
-    constexpr uint32_t E = tail_reg_per<K>();
-    __shared__ uint32_t s_live[2], s_tm;
-    Ent<K> e[E];
-    uint32_t alive = 0;  // bit q: entry threadIdx.x + q * TAIL_THREADS is undecided
-#pragma unroll
-    for (uint32_t q = 0; q < E; ++q) {
-        const uint32_t i = threadIdx.x + q * TAIL_THREADS;
-        if (i < n0) {
-            if (q == 0) e[q] = e0;
-            else load_ent<K>(e[q], b.left + (uint64_t)i * S);
-            alive |= 1u << q;
-        }
-    }
-    if (threadIdx.x == 0) { s_tm = 0; s_live[0] = 0; s_live[1] = 0; }
-    __syncthreads();
-    uint32_t n = n0, epoch = rbase + first_round, rounds = 0;
-    unsigned long long* owner = b.owner;
-    while (n > 0) {
-        // (the entry words made opaque each round: otherwise the compiler hoists every entry's
-        // cover / owner addresses out of the round loop and keeps them all live -- 128 VGPRs and
-        // spills)
-#pragma unroll
-        for (uint32_t q = 0; q < E; ++q)
-#pragma unroll
-            for (int w = 0; w < S; ++w) asm volatile("" : "+v"(e[q].w[w]));
-        const unsigned long long keyhi = (unsigned long long)(~epoch) << 32;
-        // CLAIM: kill tests (the cover loads of TAIL_GROUP entries in flight together), then the
-        // claims of the survivors
-#pragma unroll
-        for (uint32_t g = 0; g < E; g += TAIL_GROUP) {
-            uint32_t killed = 0;
-#pragma unroll
-            for (uint32_t q = g; q < g + TAIL_GROUP && q < E; ++q) {
-                if (!((alive >> q) & 1u)) continue;
-                uint64_t lb;
-                const uint32_t len = ent_len<K>(cv, e[q], lb);
-                bool k = false;
-                for (uint32_t j = 0; j < len; ++j)
-                    k |= __hip_atomic_load(&b.cover[lit_var(ent_lit<K>(cv, e[q], lb, j))], __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT) == stamp;
-                killed |= (uint32_t)k << q;
-            }
-            alive &= ~killed;
-#pragma unroll
-            for (uint32_t q = g; q < g + TAIL_GROUP && q < E; ++q) {
-                if (!((alive >> q) & 1u)) continue;
-                uint64_t lb;
-                const uint32_t len = ent_len<K>(cv, e[q], lb);
-                const unsigned long long key = keyhi | prio(b, st, e[q].w[0]);
-                for (uint32_t j = 0; j < len; ++j)
-                    __hip_atomic_fetch_min(&owner[vmix(b, lit_var(ent_lit<K>(cv, e[q], lb, j)))], key,
-                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            spec_fence();
-        }
-        __syncthreads();
-        // JOIN: a claimer holding every variable it claimed joins.  (Its own claims were this
-        // round's, and a round's keys are below every older key, so the owner key's low word --
-        // the winner's priority -- decides.)
-#pragma unroll
-        for (uint32_t g = 0; g < E; g += TAIL_GROUP) {
-            uint32_t joined = 0;
-#pragma unroll
-            for (uint32_t q = g; q < g + TAIL_GROUP && q < E; ++q) {
-                if (!((alive >> q) & 1u)) continue;
-                uint64_t lb;
-                const uint32_t len = ent_len<K>(cv, e[q], lb);
-                const uint32_t kc = prio(b, st, e[q].w[0]);
-                bool own = true;
-                for (uint32_t j = 0; j < len; ++j)
-                    own &= __hip_atomic_load(reinterpret_cast<const uint32_t*>(&owner[vmix(b, lit_var(ent_lit<K>(cv, e[q], lb, j)))]),
-                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == kc;
-                joined |= (uint32_t)own << q;
-            }
-#pragma unroll
-            for (uint32_t q = g; q < g + TAIL_GROUP && q < E; ++q) {
-                if (!((joined >> q) & 1u)) continue;
-                uint64_t lb;
-                const uint32_t len = ent_len<K>(cv, e[q], lb);
-                const uint32_t c = e[q].w[0];
-                for (uint32_t j = 0; j < len; ++j)
-                    __hip_atomic_store(&b.cover[lit_var(ent_lit<K>(cv, e[q], lb, j))], (uint8_t)stamp, __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                b.tmis[atomicAdd(&s_tm, 1u)] = c;
-                atomicAdd(&b.tile_stats[2 * (c / TILE)], mis_weight(b, st, prio(b, st, c)));
-                atomicAdd(&b.tile_stats[2 * (c / TILE) + 1], (unsigned long long)len);
-            }
-            alive &= ~joined;
-            spec_fence();
-        }
-        uint32_t cnt = (uint32_t)__popc(alive);
-        for (int o = 32; o > 0; o >>= 1) cnt += __shfl_down(cnt, o, 64);
-        if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(&s_live[rounds & 1], cnt);
-        __syncthreads();
-        n = s_live[rounds & 1];
-        // (the other slot was last read before this round's first barrier: reset for the next round)
-        if (threadIdx.x == 0) s_live[(rounds + 1) & 1] = 0;
-        ++rounds;
-        ++epoch;
-        if (rounds >= MAX_TAIL_ROUNDS && n > 0) {
-            if (threadIdx.x == 0) { st->error = 1; st->done = 3; }
-            break;
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        if (epoch > st->round_next) st->round_next = epoch;
-        st->tail_rounds = rounds;
-        st->tmis_cnt = s_tm;
-        const uint32_t total = first_round + rounds;
-        if (total > st->max_rounds) st->max_rounds = total;
-        if (b.ktime) time_slot(b, st->n_iter - 1)[3] = wall_now();
-    }
-}
-
+// round (CLAIM / barrier / JOIN passes until no undecided clause is left).  Entries are
+// processed in chunks of one per thread; survivors are compacted in place (a write position
+// never passes the chunk being read).  owner / cover are accessed with agent-scope relaxed
+// atomics so no stale L1 line is read across the barriers.  (Round 6: the entries held in
+// registers across the rounds, up to 12 per thread with their loads in flight together, was
+// 6-7 us slower per iteration at M and C5 and no faster on longer lists, DESIGN.md §7.1: one
+// CU's memory-level parallelism, not the chunk barriers, bounds a round of the tail.)
 template <int K>
 __global__ __launch_bounds__(TAIL_THREADS) void k_tail(ClauseView cv, LoopBuffers b, uint32_t first_round) {
     DevState* st = b.state;
@@ -2158,12 +2033,6 @@ __global__ __launch_bounds__(TAIL_THREADS) void k_tail(ClauseView cv, LoopBuffer
     const uint32_t active = st->active, stamp = st->stamp, n0 = st->left_cnt, rbase = st->round_base;
     spec_fence();
     if (!active) return;
-    if (n0 <= tail_reg_per<K>() * TAIL_THREADS && !b.tail_chunked) {
-        tail_regs<K>(cv, b, st, first_round, e0, n0, stamp, rbase);
-        return;
-    }
-    // chunked passes: entries in chunks of one per thread; survivors compacted in place (a write
-    // position never passes the chunk being read)
     __shared__ uint32_t s_wp, s_tm;
     uint32_t n = n0;
     uint32_t epoch = rbase + first_round;

@@ -1105,7 +1105,6 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
         b.stream_batch = opt.stream_batch;
     }
     b.seed = opt.seed;
-    if (const char* e = getenv("ALLL_TAIL_CHUNKED")) b.tail_chunked = atoi(e) != 0;  // (tests, A/B)
     if (rr_T) {
         uint32_t* d_sets = nullptr;
         if ((rc = dalloc(c, &b.rr_u, 12 * (size_t)m))) return bail(rc);  // scan entries (k_rr_entries)

@@ -37,10 +37,7 @@ LAYOUTS = {"hybrid": (0, {}), "fixed": (1 << 3, {}), "csr": (1 << 2, {}), "atomi
            # many small LDS windows (64 words: 2048 variables; the C4 layout on small instances),
            # with the cached and with the non-temporal (C4) evaluation
            "small_windows": (0, {"ALLL_EVAL_WINDOWS": "1", "ALLL_WIN_WORDS": "64"}),
-           "small_windows_nt": (0, {"ALLL_EVAL_WINDOWS": "1", "ALLL_WIN_WORDS": "64", "ALLL_EVAL_NT": "1"}),
-           # the tail's chunked passes (the default keeps up to 12 x 1024 entries in registers),
-           # with the tail in every iteration after the first
-           "tail_chunked": (0, {"ALLL_TAIL_CHUNKED": "1", "ALLL_SMALL_U": str(1 << 62)})}
+           "small_windows_nt": (0, {"ALLL_EVAL_WINDOWS": "1", "ALLL_WIN_WORDS": "64", "ALLL_EVAL_NT": "1"})}
 
 
 def make_solver(layout, monkeypatch, *args, **kw):

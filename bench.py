@@ -87,12 +87,12 @@ def cpu_threads():
     return max(1, n), ", ".join(why)
 
 
-def _probe(probe, n, m, k, kind, threads, budget, eval_reps):
+def _probe(probe, n, m, k, kind, threads, budget, eval_reps, timeout=None):
     cmd = [probe, "bench-gen", str(n), str(m), str(k), str(kind), "1", str(threads), str(budget), str(eval_reps)]
-    return json.loads(subprocess.run(cmd, check=True, capture_output=True, text=True).stdout)
+    return json.loads(subprocess.run(cmd, check=True, capture_output=True, text=True, timeout=timeout).stdout)
 
 
-def cpu_baseline(cfg, budget_s):
+def cpu_baseline(cfg, budget_s, full_iteration_cap_s=0.0):
     """The reference's own -p OpenMP path (oracle/_ref/ref_probe, compiled from the reference
     sources) on the host cores: full resample iterations on bounded samples of the same
     generator (BASELINE.md "CPU-baseline plan"), plus the eval-phase rate at the full size."""
@@ -119,6 +119,22 @@ def cpu_baseline(cfg, budget_s):
                                         "iters_per_s": q["iters"] / q["iters_s"] if q["iters_s"] else 0.0}
         # eval phase (P1, SATInstance.h:273-280) at the full size, best of 3
         e = _probe(probe, n, m, k, kind, threads, 0, 3)
+        # the plan's wall-capped single iteration at the full size: ~1e3 s, so only
+        # on request (--cpu-full-iteration SECONDS)
+        if full_iteration_cap_s > 0:
+            t0 = time.perf_counter()
+            try:
+                q = _probe(probe, n, m, k, kind, threads, 1e-3, 0, timeout=full_iteration_cap_s)
+                full = {"measured": True, "iters": q["iters"], "s": q["iters_s"], "load_s": q["load_s"]}
+            except subprocess.TimeoutExpired:
+                full = {"measured": False, "why": f"one iteration did not finish within the {full_iteration_cap_s:.0f} s cap",
+                        "s_lower_bound": time.perf_counter() - t0}
+        else:
+            full = {"measured": False,
+                    "why": ("one reference iteration at the full size takes ~1e3 s (its populate_mis_parallel is "
+                            "quadratic in |U|: 158 s at m=4M on 8 threads, BASELINE.md), beyond the default "
+                            "line's few-minute budget; bench.py --cpu-full-iteration SECONDS runs it wall-capped")}
+        points[f"m={m}"] = full
         return {
             "value": loop_rate,
             "unit": "clause-evals/s",
@@ -267,6 +283,8 @@ def main():
     ap.add_argument("--no-rr-line", action="store_true",
                     help="skip the GPU run with the CPU baseline's round-robin MIS (n_threads = T)")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--cpu-full-iteration", type=float, default=0.0,
+                    help="also time one reference iteration at the full size, capped at this many seconds")
     ap.add_argument("--event-iters", type=int, default=10,
                     help="iterations replayed eagerly with HIP events around each phase (cross-check)")
     ap.add_argument("--eval-b2b", type=int, default=20,
@@ -484,6 +502,13 @@ def main():
                 "kernel": s.eval_kernel(),
                 "algorithmic_bytes_per_launch": eval_bytes,
                 "eval_ms": eval_ms,
+                # (named for what it is -- the eval-only kernel's launches over the loop's
+                # final assignment; the committed rocprof summaries, profiles/r*_<cfg>/, average the
+                # same eval-only launches of bench_eval, and the in-loop figure is eval_ms_in_loop)
+                "eval_ms_b2b_fixed_assignment": eval_ms,
+                "traffic_source": (f"{os.path.relpath(args.traffic_json, ROOT)}: PMC FETCH_SIZE x2 + WRITE_SIZE of "
+                                   f"{s.eval_kernel()} per launch (committed, not measured in this run)"
+                                   if traffic is not None else None),
                 "timing": (f"HIP events on the solver's stream around {max(args.eval_b2b, 20)} back-to-back "
                            f"launches of the evaluation kernel alone ({s.eval_kernel()}, alll_bench_eval), "
                            f"after the timed region"),
@@ -507,7 +532,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("[rank 0] cpu baseline: the reference's -p path on bounded samples")
         try:
-            out["cpu_baseline"] = cpu_baseline(args.config, args.cpu_budget)
+            out["cpu_baseline"] = cpu_baseline(args.config, args.cpu_budget, args.cpu_full_iteration)
         except Exception as e:  # reported, never fatal for the GPU number
             out["cpu_baseline"] = {"value": None, "error": str(e)}
     if rank == 0:

@@ -410,4 +410,4 @@ def test_rr_incremental_pass_fallbacks(gpu, oracle_mod, rr_kernel, knobs, monkey
     elif "ALLL_RR_RW_TIMEOUT" in knobs:
         assert timeouts > 0 and bails
     else:
-        assert wide > 0 and timeouts == 0, "no wide repair round ran"
+        assert wide > 0 and timeouts == 0, f"no wide repair round ran: passes {[tuple(map(int, r)) for r in inc][:12]}"

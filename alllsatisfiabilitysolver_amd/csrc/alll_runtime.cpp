@@ -137,6 +137,7 @@ struct alll_ctx {
     SrrPlan* h_plan = nullptr;
     unsigned long long* h_first = nullptr;
     size_t srr_cap_blk = 0, srr_cap_ent = 0, srr_cap_step = 0;
+    int rw_occupancy = 0;       // resident k_fp_repair workgroups per CU found at create (-1: query failed)
 };
 
 namespace {
@@ -1582,12 +1583,14 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
         // the wide repair rounds synchronise their workgroups by a grid barrier: all of them must be
         // resident at once, else every incremental pass would wait for the barrier's timeout and
         // give up; without that guarantee the repair keeps to its one-workgroup rounds
+        // (a failed query keeps the wide rounds: their barriers time out safely, and are counted)
         int per_cu = 0;
         const uint32_t gw = std::min<uint32_t>(FP_RW_GRID, std::max(1, c->n_cu));
-        if (fp_repair_occupancy(cv, b, &per_cu) != hipSuccess || (uint64_t)per_cu * (uint64_t)c->n_cu < gw) {
-            (void)hipGetLastError();
-            b.fp_rw_min = ~0u;
-        }
+        (void)hipGetLastError();
+        const hipError_t e = fp_repair_occupancy(cv, b, &per_cu);
+        if (e == hipSuccess && (uint64_t)per_cu * (uint64_t)c->n_cu < gw) b.fp_rw_min = ~0u;
+        if (e != hipSuccess) (void)hipGetLastError();
+        c->rw_occupancy = e == hipSuccess ? per_cu : -1;
     }
 
     // ---- RCCL communicator (clause-sharded mode; world 1 with a comm id: a one-rank

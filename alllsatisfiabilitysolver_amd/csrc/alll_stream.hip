@@ -299,6 +299,10 @@ __global__ __launch_bounds__(SRR_THREADS) void k_srr_mis(ClauseView cv, LoopBuff
                 b.tmis[nm] = h.x;
                 s_lits += h.y;
                 s_ptr[g] = front + 1;
+                // the stamps must have reached the L2 before any wave's next cover load: the
+                // barrier below does not wait for this thread's outstanding stores (a missed stamp
+                // lets a later front share a variable with this pick -- seen once in 550 cases)
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
             ++nm;
             __syncthreads();

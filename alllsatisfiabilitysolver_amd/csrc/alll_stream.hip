@@ -308,6 +308,9 @@ __global__ __launch_bounds__(SRR_THREADS) void k_srr_mis(ClauseView cv, LoopBuff
             __syncthreads();
         }
         weighted += nm;
+        // (a step can end with a turn that passed no barrier -- the last set erased without a scan:
+        // every thread must be done reading this step's set bounds before they are rewritten)
+        __syncthreads();
     }
     weighted += (unsigned long long)nm * pl.extra;
     __syncthreads();

@@ -1583,14 +1583,19 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
         // the wide repair rounds synchronise their workgroups by a grid barrier: all of them must be
         // resident at once, else every incremental pass would wait for the barrier's timeout and
         // give up; without that guarantee the repair keeps to its one-workgroup rounds
-        // (a failed query keeps the wide rounds: their barriers time out safely, and are counted)
+        // (a failed query, or one that reports no resident workgroup at all -- seen in processes that
+        // had imported torch, whose bundled HIP runtime answers it differently -- keeps the wide
+        // rounds: their barriers time out safely, and are counted)
         int per_cu = 0;
         const uint32_t gw = std::min<uint32_t>(FP_RW_GRID, std::max(1, c->n_cu));
         (void)hipGetLastError();
         const hipError_t e = fp_repair_occupancy(cv, b, &per_cu);
-        if (e == hipSuccess && (uint64_t)per_cu * (uint64_t)c->n_cu < gw) b.fp_rw_min = ~0u;
+        if (e == hipSuccess && per_cu > 0 && (uint64_t)per_cu * (uint64_t)c->n_cu < gw) b.fp_rw_min = ~0u;
         if (e != hipSuccess) (void)hipGetLastError();
         c->rw_occupancy = e == hipSuccess ? per_cu : -1;
+        if (getenv("ALLL_DEBUG_OCCUPANCY"))  // (diagnostics)
+            fprintf(stderr, "alll: k_fp_repair occupancy query %s, %d per CU, %d CUs, wide rounds %s\n",
+                    hipGetErrorString(e), per_cu, c->n_cu, b.fp_rw_min == ~0u ? "off" : "on");
     }
 
     // ---- RCCL communicator (clause-sharded mode; world 1 with a comm id: a one-rank

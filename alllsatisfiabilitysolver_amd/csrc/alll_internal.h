@@ -169,7 +169,8 @@ struct DevState {
     uint32_t max_rounds;   // max total rounds seen in one iteration
     uint32_t error;        // loop stopped (done = 3): 1 LFMIS exceeded MAX_TAIL_ROUNDS or the round
                            // robin its batch cap; 4 a k_rr_mw grid barrier timed out; 5 an incremental
-                           // round-robin pass kernel found its buffers missing
+                           // round-robin pass kernel found its buffers missing; 6 the streaming
+                           // round robin exceeded its gather bound
     uint32_t left_cnt;     // undecided entries handed from the last grid round to the tail
     uint32_t tmis_cnt;     // MIS entries decided by the tail kernel (list b.tmis)
     uint64_t win_start;    // streaming solve: generator steps taken before this iteration

@@ -323,6 +323,8 @@ int read_state(alll_ctx* c) {
                                   "were not all resident)", c->b.rr_mw);
     if (c->h_state->error == 5)
         return fail(ALLL_ERR_HIP, "round-robin MIS: an incremental-pass kernel ran without its buffers (DESIGN.md §10)");
+    if (c->h_state->error == 6)
+        return fail(ALLL_ERR_HIP, "streaming round robin: k_srr_mis made no progress (DESIGN.md §4.2.1)");
     if (c->h_state->error)
         return fail(ALLL_ERR_UNSUPPORTED, c->b.rr_T ? "round-robin MIS exceeded its batch cap in one iteration"
                                                     : "LFMIS needed more than %u rounds in one iteration",

@@ -213,15 +213,41 @@ __global__ __launch_bounds__(256) void k_srr_fill(ClauseView cv, LoopBuffers b) 
 }
 
 namespace {
-// entry i has a variable covered by the MIS of this iteration (cover stamps read at agent scope: the
-// picks of this workgroup's earlier turns are stored the same way)
-__device__ __forceinline__ bool srr_covered(const ClauseView& cv, const LoopBuffers& b, uint32_t i, uint32_t stamp) {
-    const uint4* d = reinterpret_cast<const uint4*>(b.srr_ent + (uint64_t)i * SRR_ENT_WORDS);
-    const uint4 h = d[0], x = d[1], y = d[2];
+constexpr uint32_t SRR_WAVES = SRR_THREADS / 64;
+constexpr uint32_t SRR_CAND = 512;          // candidate slots of one gather (all sets)
+constexpr uint32_t SRR_KMAX = 256;          // candidates per set
+constexpr uint32_t SRR_HASH = 8192;         // >= 2 x SRR_CAND x 8 variables: never more than half full
+constexpr uint32_t SRR_COMPLETE = 1u << 31; // (s_cnt) the set's list holds every uncovered entry left
+constexpr uint32_t SRR_NONE = ~0u;
+
+__device__ __forceinline__ uint32_t srr_hslot(uint32_t v) { return (v * 2654435761u) >> 19; }
+
+// the variable's first sequence position this cycle (inserting p)
+__device__ __forceinline__ void srr_hins(uint32_t* key, uint32_t* pos, uint32_t v, uint32_t p) {
+    uint32_t h = srr_hslot(v);
+    for (;;) {
+        const uint32_t k = atomicCAS(&key[h], SRR_NONE, v);
+        if (k == SRR_NONE || k == v) { atomicMin(&pos[h], p); return; }
+        h = (h + 1) & (SRR_HASH - 1);
+    }
+}
+__device__ __forceinline__ uint32_t srr_hget(const uint32_t* key, const uint32_t* pos, uint32_t v) {
+    uint32_t h = srr_hslot(v);
+    for (;;) {
+        const uint32_t k = key[h];
+        if (k == v) return pos[h];
+        if (k == SRR_NONE) return SRR_NONE;
+        h = (h + 1) & (SRR_HASH - 1);
+    }
+}
+
+// list entry {id, width, literal start, 0, 8 variables} has a variable covered by this iteration's
+// MIS (cover stamps read at agent scope: the commits of this workgroup store them the same way)
+__device__ __forceinline__ bool srr_covered(const ClauseView& cv, const LoopBuffers& b, const uint4& h,
+                                            const uint32_t (&v)[8], uint32_t stamp) {
     const uint32_t wd = h.y;
     bool cov = false;
     if (wd <= 8) {
-        const uint32_t v[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
 #pragma unroll
         for (int q = 0; q < 8; ++q)
             if ((uint32_t)q < wd)
@@ -232,6 +258,12 @@ __device__ __forceinline__ bool srr_covered(const ClauseView& cv, const LoopBuff
     }
     return cov;
 }
+
+__device__ __forceinline__ uint32_t srr_wave_min(uint32_t x) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x = min(x, (uint32_t)__shfl_xor((int)x, o, 64));
+    return x;
+}
 }  // namespace
 
 // The batch steps of the iteration in order; in each, the round robin of populate_mis_parallel
@@ -239,80 +271,236 @@ __device__ __forceinline__ bool srr_covered(const ClauseView& cv, const LoopBuff
 // left whose variables are all uncovered is erased (t is not decremented, so the set moving into
 // its place loses its turn), else its first such entry joins the MIS and stamps its variables.
 // The MIS size after every step adds to the statistic (SATInstance.h:113-114), then `extra` times more.
+//
+// The turns run a cycle at a time instead of one by one:
+//   gather   every live set's first uncovered entries (up to K; the sets in turn order from the next
+//            turn share SRR_CAND slots), with a flag when the list holds all of them;
+//   segment  were no turn to find its candidate covered by an earlier pick of the cycle, the turns
+//            would take the sets' candidates in order until the first set out of candidates (E
+//            turns, closed form over the live list).  The candidates' variables go into an LDS hash
+//            with the first sequence position using them; the first turn q* whose candidate has a
+//            variable used earlier is where that assumption breaks.  Turns [0, min(q*, E)) are
+//            exactly the reference's (each candidate was uncovered at the gather and shares nothing
+//            with the cycle's earlier picks, and entries the gather skipped were covered): their picks
+//            are committed in order.  At q* the cycle ends (the turn re-runs after a new gather,
+//            where the candidate is covered); at E the set out of candidates is erased when its list
+//            was complete (then the next segment follows on the same gather) or a new gather runs.
+// A clause wider than 8 variables is a candidate only as the first turn of a cycle, alone.
 __global__ __launch_bounds__(SRR_THREADS) void k_srr_mis(ClauseView cv, LoopBuffers b) {
     DevState* st = b.state;
     if (!st->active) return;
     const SrrPlan pl = *b.srr_plan;
     const uint32_t T = pl.T, stamp = st->stamp;
     __shared__ uint32_t s_live[RR_TMAX], s_ptr[RR_TMAX], s_end[RR_TMAX];
-    __shared__ uint32_t s_wmin[SRR_THREADS / 64];
+    __shared__ uint32_t s_base[RR_TMAX], s_cnt[RR_TMAX], s_use[RR_TMAX];  // per set id, this gather
+    __shared__ uint32_t s_cent[SRR_CAND], s_cid[SRR_CAND], s_cw[SRR_CAND], s_cv[SRR_CAND * 8];
+    __shared__ uint32_t s_hkey[SRR_HASH], s_hpos[SRR_HASH];
+    __shared__ uint32_t s_gcur[SRR_WAVES], s_gcnt[SRR_WAVES], s_gst[SRR_WAVES];
+    __shared__ uint32_t s_wc[SRR_WAVES], s_wwide[SRR_WAVES];
+    __shared__ uint32_t s_red[2], s_wide, s_tot[2];
     __shared__ unsigned long long s_lits;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    if (tid == 0) s_lits = 0;
+    const unsigned long long lt_mask = (1ull << lane) - 1ull;
+    if (tid == 0) { s_lits = 0; s_tot[0] = 0; }
+    __syncthreads();
     uint32_t nm = 0;
-    unsigned long long weighted = 0;
+    unsigned long long weighted = 0, lits = 0;
     for (uint64_t s = 0; s < pl.steps; ++s) {
+        uint32_t ent = 0;
         for (uint32_t t = tid; t < T; t += SRR_THREADS) {
             s_ptr[t] = b.srr_step[s * T + t];
             s_end[t] = b.srr_step[(s + 1) * T + t];
             s_live[t] = t;
+            ent += s_end[t] - s_ptr[t];
         }
+        if (ent) atomicAdd(&s_tot[s & 1], ent);
+        if (tid == 0) s_tot[(s + 1) & 1] = 0;
+        uint32_t sz = T, tt = 0;  // block-uniform
         __syncthreads();
-        uint32_t size = T, tt = 0;
-        while (size > 0) {
-            tt = (tt + 1) % size;
-            const uint32_t g = s_live[tt];
-            const uint32_t e = s_end[g];
-            uint32_t p0 = s_ptr[g], front = ~0u;
-            while (p0 < e) {
-                const uint32_t i = p0 + tid;
-                const bool alive = i < e && !srr_covered(cv, b, i, stamp);
-                const unsigned long long bal = __ballot(alive);
-                if (lane == 0) s_wmin[wave] = bal ? p0 + wave * 64u + (uint32_t)__builtin_ctzll(bal) : ~0u;
+        // every gather is followed by a pick or an erasure, or by one at the next gather: a step
+        // needs at most 2 (entries + T) gathers (a guard against a wrong plan, error 6)
+        const uint64_t max_gathers = 2ull * ((uint64_t)s_tot[s & 1] + T) + 8;
+        uint64_t gathers = 0;
+        while (sz > 0) {
+            if (++gathers > max_gathers) {
+                if (tid == 0) { st->error = 6; st->done = 3; }
+                return;
+            }
+            // ---- gather
+            const uint32_t t0 = (tt + 1) % sz;
+            const uint32_t K = max(1u, min(SRR_KMAX, SRR_CAND / sz));
+            const uint32_t nsl = min(sz, SRR_CAND / K);  // sets with slots: turn-order offsets [0, nsl)
+            for (uint32_t i = tid; i < sz; i += SRR_THREADS) {
+                const uint32_t g = s_live[i], d = (i + sz - t0) % sz;
+                s_base[g] = d * K;
+                s_cnt[g] = 0;
+                s_use[g] = 0;
+            }
+            for (uint32_t h = tid; h < SRR_HASH; h += SRR_THREADS) { s_hkey[h] = SRR_NONE; s_hpos[h] = SRR_NONE; }
+            if (tid == 0) s_wide = 0;
+            const uint32_t wps = nsl >= SRR_WAVES ? 1u : SRR_WAVES / nsl;  // waves per set
+            const uint32_t G = SRR_WAVES / wps;                             // sets per pass
+            const uint32_t h = wave / wps, sub = wave % wps;
+            for (uint32_t d0 = 0; d0 < nsl; d0 += G) {
+                const uint32_t d = d0 + h;
+                const bool mine = h < G && d < nsl;
+                const uint32_t g = mine ? s_live[(t0 + d) % sz] : 0u;
+                const uint32_t e = mine ? s_end[g] : 0u;
+                __syncthreads();  // (the previous pass's last "more" reads)
+                if (mine && sub == 0 && lane == 0) { s_gcur[h] = s_ptr[g]; s_gcnt[h] = 0; s_gst[h] = 0; }
                 __syncthreads();
-                uint32_t f = ~0u;
+                for (;;) {
+                    const bool active = mine && s_gst[h] == 0;
+                    const uint32_t i = (active ? s_gcur[h] : 0u) + sub * 64u + lane;
+                    bool alive = false;
+                    uint4 hd = make_uint4(0, 0, 0, 0);
+                    uint32_t v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+                    if (active && i < e) {
+                        const uint4* dp = reinterpret_cast<const uint4*>(b.srr_ent + (uint64_t)i * SRR_ENT_WORDS);
+                        hd = dp[0];
+                        const uint4 x = dp[1], y = dp[2];
+                        v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w; v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
+                        alive = !srr_covered(cv, b, hd, v, stamp);
+                    }
+                    const unsigned long long bal = __ballot(alive), wb = __ballot(alive && hd.y > 8);
+                    if (lane == 0) {
+                        s_wc[wave] = (uint32_t)__popcll(bal);
+                        s_wwide[wave] = wb ? (uint32_t)__popcll(bal & ((1ull << __builtin_ctzll(wb)) - 1ull)) : SRR_NONE;
+                    }
+                    __syncthreads();
+                    if (active) {
+                        // this wave's first candidate index, the group's first wide one, the group total
+                        uint32_t pre = s_gcnt[h], off = 0, fw = SRR_NONE;
+                        for (uint32_t u = 0; u < wps; ++u) {
+                            const uint32_t wv = h * wps + u;
+                            if (u == sub) off = pre;
+                            if (fw == SRR_NONE && s_wwide[wv] != SRR_NONE) fw = pre + s_wwide[wv];
+                            pre += s_wc[wv];
+                        }
+                        const bool takewide = fw == 0 && d == 0;
+                        const uint32_t lim = takewide ? 1u : min(K, fw);
+                        if (alive) {
+                            const uint32_t r = off + (uint32_t)__popcll(bal & lt_mask);
+                            if (r < lim) {
+                                const uint32_t slot = d * K + r;
+                                s_cent[slot] = i;
+                                s_cid[slot] = hd.x;
+                                s_cw[slot] = hd.y;
+                                if (hd.y <= 8) {
 #pragma unroll
-                for (int w = 0; w < SRR_THREADS / 64; ++w) f = min(f, s_wmin[w]);
-                __syncthreads();
-                if (f != ~0u) { front = f; break; }
-                p0 += SRR_THREADS;
-            }
-            if (front == ~0u) {  // erase live[tt]
-                for (uint32_t q0 = tt; q0 + 1 < size; q0 += SRR_THREADS) {
-                    const uint32_t q = q0 + tid;
-                    const uint32_t x = q + 1 < size ? s_live[q + 1] : 0u;
+                                    for (int q = 0; q < 8; ++q) s_cv[slot * 8 + q] = v[q];
+                                } else {
+                                    s_cv[slot * 8] = hd.z;
+                                }
+                            }
+                        }
+                        if (sub == 0 && lane == 0) {
+                            const uint32_t cur = s_gcur[h] + wps * 64u, n = min(pre, lim);
+                            uint32_t stt = 0;
+                            if (fw != SRR_NONE || pre > K) stt = 2;        // truncated
+                            else if (cur >= e) stt = 1;                    // complete
+                            else if (pre == K) stt = 2;
+                            if (takewide) s_wide = 1;
+                            s_gcnt[h] = n;
+                            s_gcur[h] = cur;
+                            s_gst[h] = stt;
+                            if (stt) s_cnt[g] = n | (stt == 1 ? SRR_COMPLETE : 0u);
+                        }
+                    }
                     __syncthreads();
-                    if (q + 1 < size) s_live[q] = x;
-                    __syncthreads();
+                    bool more = false;
+                    for (uint32_t u = 0; u < G && d0 + u < nsl; ++u) more |= s_gst[u] == 0;
+                    if (!more) break;
                 }
-                --size;
-                continue;
             }
-            if (tid == front - p0) {
-                const uint4* d = reinterpret_cast<const uint4*>(b.srr_ent + (uint64_t)front * SRR_ENT_WORDS);
-                const uint4 h = d[0], x = d[1], y = d[2];
-                const uint32_t v[8] = {x.x, x.y, x.z, x.w, y.x, y.y, y.z, y.w};
-                for (uint32_t q = 0; q < h.y; ++q) {
-                    const uint32_t var = q < 8 ? v[q] : s_var(cv.lits[h.z + q]);
-                    __hip_atomic_store(&b.cover[var], (uint8_t)stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-                b.tmis[nm] = h.x;
-                s_lits += h.y;
-                s_ptr[g] = front + 1;
-                // the stamps must have reached the L2 before any wave's next cover load: the
-                // barrier below does not wait for this thread's outstanding stores (a missed stamp
-                // lets a later front share a variable with this pick -- seen once in 550 cases)
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            }
-            ++nm;
             __syncthreads();
+            if (s_wide) {  // a wide first candidate runs alone: every other set stops at its turn
+                for (uint32_t i = tid; i < sz; i += SRR_THREADS)
+                    if (i != t0) s_cnt[s_live[i]] = 0;
+                __syncthreads();
+            }
+            // ---- segments on this gather
+            uint32_t qb = 0;
+            for (;;) {
+                const uint32_t ts = (tt + 1) % sz;
+                if (tid == 0) { s_red[0] = SRR_NONE; s_red[1] = SRR_NONE; }
+                __syncthreads();
+                uint32_t em = SRR_NONE;
+                for (uint32_t i = tid; i < sz; i += SRR_THREADS) {
+                    const uint32_t g = s_live[i], d = (i + sz - ts) % sz;
+                    em = min(em, d + ((s_cnt[g] & ~SRR_COMPLETE) - s_use[g]) * sz);
+                }
+                em = srr_wave_min(em);
+                if (lane == 0 && em != SRR_NONE) atomicMin(&s_red[0], em);
+                __syncthreads();
+                const uint32_t E = s_red[0];
+                for (uint32_t j = tid; j < E; j += SRR_THREADS) {
+                    const uint32_t g = s_live[(ts + j) % sz], slot = s_base[g] + s_use[g] + j / sz;
+                    const uint32_t w = s_cw[slot];
+                    if (w <= 8)
+                        for (uint32_t q = 0; q < w; ++q) srr_hins(s_hkey, s_hpos, s_cv[slot * 8 + q], qb + j);
+                }
+                __syncthreads();
+                uint32_t qm = SRR_NONE;
+                for (uint32_t j = tid; j < E; j += SRR_THREADS) {
+                    const uint32_t g = s_live[(ts + j) % sz], slot = s_base[g] + s_use[g] + j / sz;
+                    const uint32_t w = s_cw[slot];
+                    bool clash = false;
+                    if (w <= 8)
+                        for (uint32_t q = 0; q < w; ++q) clash |= srr_hget(s_hkey, s_hpos, s_cv[slot * 8 + q]) < qb + j;
+                    if (clash) qm = min(qm, j);
+                }
+                qm = srr_wave_min(qm);
+                if (lane == 0 && qm != SRR_NONE) atomicMin(&s_red[1], qm);
+                __syncthreads();
+                const uint32_t A = min(s_red[1], E);  // turns taken in this segment
+                for (uint32_t j = tid; j < A; j += SRR_THREADS) {
+                    const uint32_t g = s_live[(ts + j) % sz], slot = s_base[g] + s_use[g] + j / sz;
+                    const uint32_t w = s_cw[slot];
+                    for (uint32_t q = 0; q < w; ++q) {
+                        const uint32_t var = w <= 8 ? s_cv[slot * 8 + q] : s_var(cv.lits[s_cv[slot * 8] + q]);
+                        __hip_atomic_store(&b.cover[var], (uint8_t)stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                    b.tmis[nm + j] = s_cid[slot];
+                    lits += w;
+                }
+                __syncthreads();  // (the commits read s_use)
+                for (uint32_t i = tid; i < sz; i += SRR_THREADS) {
+                    const uint32_t d = (i + sz - ts) % sz;
+                    if (A > d) {
+                        const uint32_t g = s_live[i], u = s_use[g] + (A - d + sz - 1) / sz;
+                        s_use[g] = u;
+                        s_ptr[g] = s_cent[s_base[g] + u - 1] + 1;
+                    }
+                }
+                // every stamp must have reached the L2 before the next gather's cover loads: the
+                // barrier does not wait for outstanding stores
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                nm += A;
+                qb += A;
+                if (A > 0) tt = (ts + A - 1) % sz;
+                if (A < E) break;  // a covered candidate: new gather
+                const uint32_t te = (tt + 1) % sz, ge = s_live[te];
+                if (!(s_cnt[ge] & SRR_COMPLETE)) break;  // out of gathered candidates: new gather
+                // the set has no uncovered entry left: erase live[te]
+                for (uint32_t q0 = te; q0 + 1 < sz; q0 += SRR_THREADS) {
+                    const uint32_t q = q0 + tid;
+                    const uint32_t x = q + 1 < sz ? s_live[q + 1] : 0u;
+                    __syncthreads();
+                    if (q + 1 < sz) s_live[q] = x;
+                }
+                __syncthreads();
+                --sz;
+                tt = te;
+                if (sz == 0) break;
+            }
         }
         weighted += nm;
-        // (a step can end with a turn that passed no barrier -- the last set erased without a scan:
-        // every thread must be done reading this step's set bounds before they are rewritten)
         __syncthreads();
     }
     weighted += (unsigned long long)nm * pl.extra;
+    if (lits) atomicAdd(&s_lits, lits);
     __syncthreads();
     if (tid == 0) {
         st->tmis_cnt = nm;

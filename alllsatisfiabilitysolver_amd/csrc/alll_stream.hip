@@ -303,7 +303,7 @@ __global__ __launch_bounds__(SRR_THREADS) void k_srr_mis(ClauseView cv, LoopBuff
     const unsigned long long lt_mask = (1ull << lane) - 1ull;
     if (tid == 0) { s_lits = 0; s_tot[0] = 0; }
     __syncthreads();
-    uint32_t nm = 0;
+    uint32_t nm = 0, all_gathers = 0;
     unsigned long long weighted = 0, lits = 0;
     for (uint64_t s = 0; s < pl.steps; ++s) {
         uint32_t ent = 0;
@@ -322,6 +322,7 @@ __global__ __launch_bounds__(SRR_THREADS) void k_srr_mis(ClauseView cv, LoopBuff
         const uint64_t max_gathers = 2ull * ((uint64_t)s_tot[s & 1] + T) + 8;
         uint64_t gathers = 0;
         while (sz > 0) {
+            ++all_gathers;
             if (++gathers > max_gathers) {
                 if (tid == 0) { st->error = 6; st->done = 3; }
                 return;
@@ -504,6 +505,8 @@ __global__ __launch_bounds__(SRR_THREADS) void k_srr_mis(ClauseView cv, LoopBuff
     __syncthreads();
     if (tid == 0) {
         st->tmis_cnt = nm;
+        st->tail_rounds = all_gathers;  // (the statistics' lfmis_tail_rounds: gathers of the iteration)
+        if (all_gathers > st->max_rounds) st->max_rounds = all_gathers;
         b.tile_stats[0] += weighted;
         b.tile_stats[1] += s_lits;
     }

@@ -233,6 +233,52 @@ def rr_line(args, n, m, k, kind, Solver, generate_ksat, device, warmup=20, steps
             "mis": "round robin over T clause chunks (SATInstance.h:414-447), as the cpu_baseline's -p T path"}
 
 
+def stream_line(args, n, m, k, kind, T, bs, check_iters=2, warmup=3, steps=10):
+    """The streaming solve with T > 1 generators, SATInstance::solve(getEnumeratedClause, n_clauses,
+    batch) (SATInstance.h:70-153), on the bench instance: GPU iterations/s over
+    `steps` iterations, and as its cpu_baseline the oracle's serial restatement
+    (orc_solve_stream_rr) timed over the first `check_iters` iterations, whose statistics and
+    assignment the GPU's must equal bit for bit (checked outside the timed region)."""
+    from alllsatisfiabilitysolver_amd import Solver, assignment_digest, generate_ksat
+
+    if isinstance(k, tuple):
+        return {"value": None, "error": "the stream line runs on the fixed-width configurations"}
+    offs, lits = generate_ksat(1, n, m, k, kind)
+    log(f"[rank 0] stream line: T={T}, batch={bs}")
+    with Solver(n, offs, lits, seed=args.seed, stream_batch=bs, n_threads=T) as s:
+        s.run(check_iters)
+        st_k = s.stats()
+        words = s.assignment_words().copy()
+        s.run(warmup)
+        s.synchronize()
+        it0 = s.stats()["n_iterations"]
+        t0 = time.perf_counter()
+        s.run(steps)
+        s.synchronize()
+        dt = time.perf_counter() - t0
+        done = s.stats()["n_iterations"] - it0
+    out = {"n_threads": T, "batch": bs, "steps": done, "warmup": warmup + check_iters,
+           "resample_iters_per_s": done / dt if done else None,
+           "value": m * done / dt if done else None, "unit": "clause-evals/s",
+           "ms_per_step": dt * 1e3 / done if done else None}
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle
+
+    t0 = time.perf_counter()
+    rc, st_o, A_o, _ = oracle.solve_stream_rr(n, offs, lits, args.seed, bs, T, max_iters=check_iters)
+    dtc = time.perf_counter() - t0
+    keys = ("n_iterations", "n_resamples", "sum_mis_size", "avg_mis_size", "solved")
+    match = rc in (0, 1) and all(int(st_k[q]) == int(st_o[q]) for q in keys) and \
+        assignment_digest(words) == assignment_digest(A_o)
+    out["check"] = {"iters": check_iters, "match": bool(match),
+                    "gpu": {q: int(st_k[q]) for q in keys}, "oracle": {q: int(st_o[q]) for q in keys}}
+    out["cpu_baseline"] = {"value": m * check_iters / dtc, "unit": "clause-evals/s", "cores": 1, "kind": "port",
+                           "resample_iters_per_s": check_iters / dtc,
+                           "sample": f"oracle serial restatement (orc_solve_stream_rr), the first {check_iters} "
+                                     f"iterations of the same instance and seed; host {cpu_model()}"}
+    return out
+
+
 def rr_line_child(args, timeout_s=240):
     """The round-robin line in a child process (this script with --rr-child): its own HIP
     context and a time limit, so that it can neither disturb nor stall the main line."""
@@ -291,6 +337,9 @@ def main():
                     help="back-to-back eval-only launches timed with HIP events for the roofline (at least 20)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_eval_traffic.json"))
     ap.add_argument("--rr-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--stream-line", default="",
+                    help="T:BATCH -- also run the streaming solve with T generators of BATCH clauses "
+                         "(GPU rate, and the oracle's first iterations as its CPU baseline and check)")
     args = ap.parse_args()
 
     if args.rr_child:  # (rr_line_child): one JSON line on stdout, no torch in this process
@@ -529,6 +578,13 @@ def main():
             out["gpu_same_mis_as_cpu_baseline"] = rr_line_child(args)
         except Exception as e:  # reported, never fatal for the GPU number
             out["gpu_same_mis_as_cpu_baseline"] = {"value": None, "error": str(e)}
+    if rank == 0 and world == 1 and args.stream_line:
+        try:
+            st_T, st_b = (int(x) for x in args.stream_line.split(":"))
+            n0, m0, k0, kind0, _ = CONFIGS[args.config]
+            out["stream_line"] = stream_line(args, n0, m0, k0, kind0, st_T, st_b)
+        except Exception as e:  # reported, never fatal for the GPU number
+            out["stream_line"] = {"value": None, "error": str(e)}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("[rank 0] cpu baseline: the reference's -p path on bounded samples")
         try:
@@ -542,7 +598,8 @@ def main():
         dist.barrier()
         dist.destroy_process_group()
     rr = (out or {}).get("gpu_same_mis_as_cpu_baseline") or {}
-    bad = [name for name, t in (("T=1 loop", traj), ("round robin", rr.get("trajectory_check")))
+    bad = [name for name, t in (("T=1 loop", traj), ("round robin", rr.get("trajectory_check")),
+                                ("streaming solve", ((out or {}).get("stream_line") or {}).get("check")))
            if t and t.get("match") is False]
     if rank == 0 and bad:
         log(f"[rank 0] FAIL: the {' and '.join(bad)} left a state that differs from the committed oracle trajectory")

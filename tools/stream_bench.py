@@ -42,7 +42,8 @@ def main():
                                       "iters_per_s": it / dt if dt > 0 else None,
                                       "clause_evals_per_s": m * it / dt if dt > 0 else None,
                                       "violated_last": st["n_violated"], "avg_mis_size": st["avg_mis_size"],
-                                      "solved": st["solved"]}), flush=True)
+                                      "solved": st["solved"], "mis_last": int(s.mis().size),
+                                      "gathers_last": st["lfmis_tail_rounds"]}), flush=True)
             except Exception as e:  # e.g. generators that never finish together (the reference hangs)
                 print(json.dumps({"config": a.config, "n_threads": T, "batch": bs, "error": str(e)}), flush=True)
 

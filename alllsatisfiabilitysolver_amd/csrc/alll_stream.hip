@@ -14,10 +14,12 @@
 //                 lists every generator's violated walk steps in walk order (a thread per 16 steps,
 //                 violated bits from the clause-order bitmask of k_eval_csr), with each clause's
 //                 variables inline, and the first list entry of every (batch step, generator);
-//   k_srr_mis     runs the batch steps' round robins in order, one 1024-thread workgroup: a turn is
-//                 one parallel scan of the set's next entries against the cover stamps (the filter
-//                 against the MIS so far and the round robin's erasures are both the "first entry
-//                 with no covered variable" rule), the pick stamps its variables.
+//   k_srr_mis     runs the batch steps' round robins in order, one 1024-thread workgroup, a cycle
+//                 of turns at a time: every set's next uncovered entries are gathered, the turn
+//                 sequence they would give is laid out in closed form, and an LDS hash of first
+//                 uses finds the first turn whose candidate an earlier pick covers; the turns
+//                 before it are the reference's (the filter against the MIS so far and the round
+//                 robin's erasures are both the "first entry with no covered variable" rule).
 // k_resample_vars (alll_kernels.hip) then resamples the covered variables.  Integer work, latency
 // bound: no MFMA.
 #include "alll_internal.h"

@@ -221,44 +221,58 @@ constexpr uint32_t SRR_KMAX = 256;          // candidates per set
 constexpr uint32_t SRR_HASH = 8192;         // >= 2 x SRR_CAND x 8 variables: never more than half full
 constexpr uint32_t SRR_COMPLETE = 1u << 31; // (s_cnt) the set's list holds every uncovered entry left
 constexpr uint32_t SRR_NONE = ~0u;
+constexpr int SRR_GU = 1;                   // list entries per lane in a gather's window (2: 5.8 vs 3.5 us per window, 4% slower overall)
 
 __device__ __forceinline__ uint32_t srr_hslot(uint32_t v) { return (v * 2654435761u) >> 19; }
 
-// the variable's first sequence position this cycle (inserting p)
-__device__ __forceinline__ void srr_hins(uint32_t* key, uint32_t* pos, uint32_t v, uint32_t p) {
+// Inserts variable v used at sequence position p; returns a position that shares v with an
+// earlier one, or SRR_NONE.  The minimum over every insert of a segment is exactly the first
+// position q* with a variable some earlier position uses: for a variable with users p1 < p2 < ...,
+// whichever of p1, p2 arrives second finds the other (or a larger user) as the slot's minimum and
+// reports max(old, p) = p2; every report is the later of two users.  (A clause repeating a
+// variable finds its own position: not a conflict.)
+__device__ __forceinline__ uint32_t srr_hins(uint32_t* key, uint32_t* pos, uint32_t v, uint32_t p) {
     uint32_t h = srr_hslot(v);
     for (;;) {
         const uint32_t k = atomicCAS(&key[h], SRR_NONE, v);
-        if (k == SRR_NONE || k == v) { atomicMin(&pos[h], p); return; }
-        h = (h + 1) & (SRR_HASH - 1);
-    }
-}
-__device__ __forceinline__ uint32_t srr_hget(const uint32_t* key, const uint32_t* pos, uint32_t v) {
-    uint32_t h = srr_hslot(v);
-    for (;;) {
-        const uint32_t k = key[h];
-        if (k == v) return pos[h];
-        if (k == SRR_NONE) return SRR_NONE;
+        if (k == SRR_NONE || k == v) {
+            const uint32_t old = atomicMin(&pos[h], p);
+            return old == SRR_NONE || old == p ? SRR_NONE : max(old, p);
+        }
         h = (h + 1) & (SRR_HASH - 1);
     }
 }
 
-// list entry {id, width, literal start, 0, 8 variables} has a variable covered by this iteration's
-// MIS (cover stamps read at agent scope: the commits of this workgroup store them the same way)
-__device__ __forceinline__ bool srr_covered(const ClauseView& cv, const LoopBuffers& b, const uint4& h,
-                                            const uint32_t (&v)[8], uint32_t stamp) {
-    const uint32_t wd = h.y;
-    bool cov = false;
-    if (wd <= 8) {
+// The cover stamps of list entries {id, width, literal start, 0, 8 variables}.  Every stamp read
+// here was stored either before this launch or by a wave of this workgroup (one CU), which waits
+// for its stores (vmcnt(0)) ahead of the barrier before a gather: workgroup scope, so plain loads
+// and stores (no sc1: agent-scope stores drop the cover lines from L2, agent-scope loads bypass
+// L1 and were waited one by one).  All of a lane's loads are issued before the first is used, and
+// only slots below the wave's widest clause are loaded (each lane's scattered byte load costs the
+// CU's address unit a cycle; a 3-SAT list needs 3 of the 8).
+template <int U>
+__device__ __forceinline__ void srr_cover_test(const ClauseView& cv, const LoopBuffers& b, const uint4 (&hd)[U],
+                                               const uint32_t (&v)[U][8], uint32_t stamp, bool (&alive)[U]) {
+    uint32_t wmax = 0;
 #pragma unroll
-        for (int q = 0; q < 8; ++q)
-            if ((uint32_t)q < wd)
-                cov |= __hip_atomic_load(&b.cover[v[q]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == stamp;
-    } else {
-        for (uint32_t q = 0; q < wd && !cov; ++q)
-            cov = __hip_atomic_load(&b.cover[s_var(cv.lits[h.z + q])], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == stamp;
+    for (int u = 0; u < U; ++u) wmax = max(wmax, alive[u] ? min(hd[u].y, 8u) : 0u);
+    for (int o = 32; o > 0; o >>= 1) wmax = max(wmax, (uint32_t)__shfl_xor((int)wmax, o, 64));
+    uint8_t cs[U][8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+        if ((uint32_t)q < wmax) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) cs[u][q] = alive[u] && (uint32_t)q < hd[u].y ? b.cover[v[u][q]] : (uint8_t)0;
+        }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        bool cov = false;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) cov |= (uint32_t)q < wmax && cs[u][q] == stamp;
+        for (uint32_t q = 8; alive[u] && q < hd[u].y && !cov; ++q)  // (clauses wider than 8: rare)
+            cov = b.cover[s_var(cv.lits[hd[u].z + q])] == stamp;
+        alive[u] &= !cov;
     }
-    return cov;
 }
 
 __device__ __forceinline__ uint32_t srr_wave_min(uint32_t x) {
@@ -294,19 +308,33 @@ __global__ __launch_bounds__(SRR_THREADS) void k_srr_mis(ClauseView cv, LoopBuff
     const SrrPlan pl = *b.srr_plan;
     const uint32_t T = pl.T, stamp = st->stamp;
     __shared__ uint32_t s_live[RR_TMAX], s_ptr[RR_TMAX], s_end[RR_TMAX];
-    __shared__ uint32_t s_base[RR_TMAX], s_cnt[RR_TMAX], s_use[RR_TMAX];  // per set id, this gather
+    __shared__ uint32_t s_base[RR_TMAX], s_cnt[RR_TMAX];  // per set id, this gather
+    __shared__ uint32_t s_use[2][RR_TMAX];  // candidates consumed: by segment parity
     __shared__ uint32_t s_cent[SRR_CAND], s_cid[SRR_CAND], s_cw[SRR_CAND], s_cv[SRR_CAND * 8];
     __shared__ uint32_t s_hkey[SRR_HASH], s_hpos[SRR_HASH];
     __shared__ uint32_t s_gcur[SRR_WAVES], s_gcnt[SRR_WAVES], s_gst[SRR_WAVES];
     __shared__ uint32_t s_wc[SRR_WAVES], s_wwide[SRR_WAVES];
-    __shared__ uint32_t s_red[2], s_wide, s_tot[2];
+    __shared__ uint32_t s_red[4], s_wide, s_tot[2];  // (s_red: {E, q*} by segment parity)
     __shared__ unsigned long long s_lits;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const unsigned long long lt_mask = (1ull << lane) - 1ull;
-    if (tid == 0) { s_lits = 0; s_tot[0] = 0; }
+    if (tid == 0) {
+        s_lits = 0;
+        s_tot[0] = 0;
+        for (int q = 0; q < 4; ++q) s_red[q] = SRR_NONE;
+    }
     __syncthreads();
+    uint32_t seg = 0;  // segments so far (parity: s_red, s_use)
     uint32_t nm = 0, all_gathers = 0;
     unsigned long long weighted = 0, lits = 0;
+#ifdef SRR_PROFILE  // (development: phase clocks of thread 0, printed at the end)
+    unsigned long long p_t0 = __builtin_amdgcn_s_memrealtime(), p_g = 0, p_x;
+    uint32_t p_segs = 0, p_conf = 0, p_wit = 0;
+    unsigned long long p_a = 0, p_b = 0, p_y, p_ph[5] = {0, 0, 0, 0, 0}, p_z;
+#define SRR_PH(k) { const unsigned long long z_ = __builtin_amdgcn_s_memrealtime(); p_ph[k] += z_ - p_z; p_z = z_; }
+#else
+#define SRR_PH(k)
+#endif
     for (uint64_t s = 0; s < pl.steps; ++s) {
         uint32_t ent = 0;
         for (uint32_t t = tid; t < T; t += SRR_THREADS) {
@@ -330,6 +358,9 @@ __global__ __launch_bounds__(SRR_THREADS) void k_srr_mis(ClauseView cv, LoopBuff
                 return;
             }
             // ---- gather
+#ifdef SRR_PROFILE
+            p_x = __builtin_amdgcn_s_memrealtime();
+#endif
             const uint32_t t0 = (tt + 1) % sz;
             const uint32_t K = max(1u, min(SRR_KMAX, SRR_CAND / sz));
             const uint32_t nsl = min(sz, SRR_CAND / K);  // sets with slots: turn-order offsets [0, nsl)
@@ -337,38 +368,68 @@ __global__ __launch_bounds__(SRR_THREADS) void k_srr_mis(ClauseView cv, LoopBuff
                 const uint32_t g = s_live[i], d = (i + sz - t0) % sz;
                 s_base[g] = d * K;
                 s_cnt[g] = 0;
-                s_use[g] = 0;
+                s_use[seg & 1][g] = 0;
             }
             for (uint32_t h = tid; h < SRR_HASH; h += SRR_THREADS) { s_hkey[h] = SRR_NONE; s_hpos[h] = SRR_NONE; }
             if (tid == 0) s_wide = 0;
             const uint32_t wps = nsl >= SRR_WAVES ? 1u : SRR_WAVES / nsl;  // waves per set
             const uint32_t G = SRR_WAVES / wps;                             // sets per pass
             const uint32_t h = wave / wps, sub = wave % wps;
+#ifdef SRR_PROFILE
+            p_y = __builtin_amdgcn_s_memrealtime();
+            p_a += p_y - p_x;
+#endif
             for (uint32_t d0 = 0; d0 < nsl; d0 += G) {
                 const uint32_t d = d0 + h;
                 const bool mine = h < G && d < nsl;
                 const uint32_t g = mine ? s_live[(t0 + d) % sz] : 0u;
                 const uint32_t e = mine ? s_end[g] : 0u;
-                __syncthreads();  // (the previous pass's last "more" reads)
+                // (the previous pass's last "more" reads; and every commit's cover stamps must
+                // have reached the L2 before the cover loads below: a barrier does not wait for
+                // outstanding stores)
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
                 if (mine && sub == 0 && lane == 0) { s_gcur[h] = s_ptr[g]; s_gcnt[h] = 0; s_gst[h] = 0; }
                 __syncthreads();
+#ifdef SRR_PROFILE
+                { const unsigned long long z = __builtin_amdgcn_s_memrealtime(); p_b += z - p_y; p_y = z; }
+#endif
                 for (;;) {
                     const bool active = mine && s_gst[h] == 0;
-                    const uint32_t i = (active ? s_gcur[h] : 0u) + sub * 64u + lane;
-                    bool alive = false;
-                    uint4 hd = make_uint4(0, 0, 0, 0);
-                    uint32_t v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-                    if (active && i < e) {
-                        const uint4* dp = reinterpret_cast<const uint4*>(b.srr_ent + (uint64_t)i * SRR_ENT_WORDS);
-                        hd = dp[0];
-                        const uint4 x = dp[1], y = dp[2];
-                        v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w; v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
-                        alive = !srr_covered(cv, b, hd, v, stamp);
+                    const uint32_t i0 = (active ? s_gcur[h] : 0u) + sub * (64u * SRR_GU) + lane;
+                    bool alive[SRR_GU];
+                    uint4 hd[SRR_GU];
+                    uint32_t v[SRR_GU][8];
+#pragma unroll
+                    for (int u = 0; u < SRR_GU; ++u) {
+                        const uint32_t i = i0 + 64u * u;
+                        alive[u] = active && i < e;
+                        hd[u] = make_uint4(0, 0, 0, 0);
+                        uint4 x = make_uint4(0, 0, 0, 0), y = x;
+                        if (alive[u]) {
+                            const uint4* dp = reinterpret_cast<const uint4*>(b.srr_ent + (uint64_t)i * SRR_ENT_WORDS);
+                            hd[u] = dp[0];
+                            x = dp[1];
+                            y = dp[2];
+                        }
+                        v[u][0] = x.x; v[u][1] = x.y; v[u][2] = x.z; v[u][3] = x.w;
+                        v[u][4] = y.x; v[u][5] = y.y; v[u][6] = y.z; v[u][7] = y.w;
                     }
-                    const unsigned long long bal = __ballot(alive), wb = __ballot(alive && hd.y > 8);
+                    srr_cover_test<SRR_GU>(cv, b, hd, v, stamp, alive);
+                    // candidate order: entry u = 0's 64 lanes, then u = 1's
+                    unsigned long long bal[SRR_GU];
+                    uint32_t wcnt = 0, wwide = SRR_NONE;
+#pragma unroll
+                    for (int u = 0; u < SRR_GU; ++u) {
+                        bal[u] = __ballot(alive[u]);
+                        const unsigned long long wb = __ballot(alive[u] && hd[u].y > 8);
+                        if (wb && wwide == SRR_NONE)
+                            wwide = wcnt + (uint32_t)__popcll(bal[u] & ((1ull << __builtin_ctzll(wb)) - 1ull));
+                        wcnt += (uint32_t)__popcll(bal[u]);
+                    }
                     if (lane == 0) {
-                        s_wc[wave] = (uint32_t)__popcll(bal);
-                        s_wwide[wave] = wb ? (uint32_t)__popcll(bal & ((1ull << __builtin_ctzll(wb)) - 1ull)) : SRR_NONE;
+                        s_wc[wave] = wcnt;
+                        s_wwide[wave] = wwide;
                     }
                     __syncthreads();
                     if (active) {
@@ -382,23 +443,26 @@ __global__ __launch_bounds__(SRR_THREADS) void k_srr_mis(ClauseView cv, LoopBuff
                         }
                         const bool takewide = fw == 0 && d == 0;
                         const uint32_t lim = takewide ? 1u : min(K, fw);
-                        if (alive) {
-                            const uint32_t r = off + (uint32_t)__popcll(bal & lt_mask);
-                            if (r < lim) {
-                                const uint32_t slot = d * K + r;
-                                s_cent[slot] = i;
-                                s_cid[slot] = hd.x;
-                                s_cw[slot] = hd.y;
-                                if (hd.y <= 8) {
+                        uint32_t r = off;
 #pragma unroll
-                                    for (int q = 0; q < 8; ++q) s_cv[slot * 8 + q] = v[q];
+                        for (int u = 0; u < SRR_GU; ++u) {
+                            const uint32_t ru = r + (uint32_t)__popcll(bal[u] & lt_mask);
+                            if (alive[u] && ru < lim) {
+                                const uint32_t slot = d * K + ru;
+                                s_cent[slot] = i0 + 64u * u;
+                                s_cid[slot] = hd[u].x;
+                                s_cw[slot] = hd[u].y;
+                                if (hd[u].y <= 8) {
+#pragma unroll
+                                    for (int q = 0; q < 8; ++q) s_cv[slot * 8 + q] = v[u][q];
                                 } else {
-                                    s_cv[slot * 8] = hd.z;
+                                    s_cv[slot * 8] = hd[u].z;
                                 }
                             }
+                            r += (uint32_t)__popcll(bal[u]);
                         }
                         if (sub == 0 && lane == 0) {
-                            const uint32_t cur = s_gcur[h] + wps * 64u, n = min(pre, lim);
+                            const uint32_t cur = s_gcur[h] + wps * 64u * SRR_GU, n = min(pre, lim);
                             uint32_t stt = 0;
                             if (fw != SRR_NONE || pre > K) stt = 2;        // truncated
                             else if (cur >= e) stt = 1;                    // complete
@@ -411,6 +475,9 @@ __global__ __launch_bounds__(SRR_THREADS) void k_srr_mis(ClauseView cv, LoopBuff
                         }
                     }
                     __syncthreads();
+#ifdef SRR_PROFILE
+                    ++p_wit;
+#endif
                     bool more = false;
                     for (uint32_t u = 0; u < G && d0 + u < nsl; ++u) more |= s_gst[u] == 0;
                     if (!more) break;
@@ -423,65 +490,67 @@ __global__ __launch_bounds__(SRR_THREADS) void k_srr_mis(ClauseView cv, LoopBuff
                 __syncthreads();
             }
             // ---- segments on this gather
+#ifdef SRR_PROFILE
+            { const unsigned long long y = __builtin_amdgcn_s_memrealtime(); p_g += y - p_x; p_x = y; }
+#endif
             uint32_t qb = 0;
             for (;;) {
-                const uint32_t ts = (tt + 1) % sz;
-                if (tid == 0) { s_red[0] = SRR_NONE; s_red[1] = SRR_NONE; }
-                __syncthreads();
+#ifdef SRR_PROFILE
+                p_z = __builtin_amdgcn_s_memrealtime();
+#endif
+                const uint32_t ts = (tt + 1) % sz, pr = seg & 1u;
+                uint32_t* use = s_use[pr];
+                uint32_t* red = s_red + 2 * pr;  // (reset during the previous segment)
                 uint32_t em = SRR_NONE;
                 for (uint32_t i = tid; i < sz; i += SRR_THREADS) {
                     const uint32_t g = s_live[i], d = (i + sz - ts) % sz;
-                    em = min(em, d + ((s_cnt[g] & ~SRR_COMPLETE) - s_use[g]) * sz);
+                    em = min(em, d + ((s_cnt[g] & ~SRR_COMPLETE) - use[g]) * sz);
                 }
                 em = srr_wave_min(em);
-                if (lane == 0 && em != SRR_NONE) atomicMin(&s_red[0], em);
+                if (lane == 0 && em != SRR_NONE) atomicMin(&red[0], em);
                 __syncthreads();
-                const uint32_t E = s_red[0];
+                const uint32_t E = red[0];
+                SRR_PH(0)
+                if (tid == 0) { s_red[2 * (pr ^ 1u)] = SRR_NONE; s_red[2 * (pr ^ 1u) + 1] = SRR_NONE; }
+                uint32_t qm = SRR_NONE;  // (positions are relative to the cycle: qb + j)
                 for (uint32_t j = tid; j < E; j += SRR_THREADS) {
-                    const uint32_t g = s_live[(ts + j) % sz], slot = s_base[g] + s_use[g] + j / sz;
+                    const uint32_t g = s_live[(ts + j) % sz], slot = s_base[g] + use[g] + j / sz;
                     const uint32_t w = s_cw[slot];
                     if (w <= 8)
-                        for (uint32_t q = 0; q < w; ++q) srr_hins(s_hkey, s_hpos, s_cv[slot * 8 + q], qb + j);
+                        for (uint32_t q = 0; q < w; ++q) qm = min(qm, srr_hins(s_hkey, s_hpos, s_cv[slot * 8 + q], qb + j));
                 }
-                __syncthreads();
-                uint32_t qm = SRR_NONE;
-                for (uint32_t j = tid; j < E; j += SRR_THREADS) {
-                    const uint32_t g = s_live[(ts + j) % sz], slot = s_base[g] + s_use[g] + j / sz;
-                    const uint32_t w = s_cw[slot];
-                    bool clash = false;
-                    if (w <= 8)
-                        for (uint32_t q = 0; q < w; ++q) clash |= srr_hget(s_hkey, s_hpos, s_cv[slot * 8 + q]) < qb + j;
-                    if (clash) qm = min(qm, j);
-                }
+                SRR_PH(1)
                 qm = srr_wave_min(qm);
-                if (lane == 0 && qm != SRR_NONE) atomicMin(&s_red[1], qm);
+                if (lane == 0 && qm != SRR_NONE) atomicMin(&red[1], qm - qb);
                 __syncthreads();
-                const uint32_t A = min(s_red[1], E);  // turns taken in this segment
+                const uint32_t A = min(red[1], E);  // turns taken in this segment
+                SRR_PH(2)
                 for (uint32_t j = tid; j < A; j += SRR_THREADS) {
-                    const uint32_t g = s_live[(ts + j) % sz], slot = s_base[g] + s_use[g] + j / sz;
+                    const uint32_t g = s_live[(ts + j) % sz], slot = s_base[g] + use[g] + j / sz;
                     const uint32_t w = s_cw[slot];
                     for (uint32_t q = 0; q < w; ++q) {
                         const uint32_t var = w <= 8 ? s_cv[slot * 8 + q] : s_var(cv.lits[s_cv[slot * 8] + q]);
-                        __hip_atomic_store(&b.cover[var], (uint8_t)stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        b.cover[var] = (uint8_t)stamp;  // (workgroup scope: srr_cover_test)
                     }
                     b.tmis[nm + j] = s_cid[slot];
                     lits += w;
                 }
-                __syncthreads();  // (the commits read s_use)
+                // consumed counts into the other parity (the commits above still read this one)
                 for (uint32_t i = tid; i < sz; i += SRR_THREADS) {
-                    const uint32_t d = (i + sz - ts) % sz;
-                    if (A > d) {
-                        const uint32_t g = s_live[i], u = s_use[g] + (A - d + sz - 1) / sz;
-                        s_use[g] = u;
-                        s_ptr[g] = s_cent[s_base[g] + u - 1] + 1;
-                    }
+                    const uint32_t d = (i + sz - ts) % sz, g = s_live[i];
+                    const uint32_t u = use[g] + (A > d ? (A - d + sz - 1) / sz : 0u);
+                    s_use[pr ^ 1u][g] = u;
+                    if (A > d) s_ptr[g] = s_cent[s_base[g] + u - 1] + 1;
                 }
-                // every stamp must have reached the L2 before the next gather's cover loads: the
-                // barrier does not wait for outstanding stores
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __syncthreads();
+                SRR_PH(3)
+                ++seg;
                 nm += A;
                 qb += A;
+#ifdef SRR_PROFILE
+                ++p_segs;
+                p_conf += A < E;
+#endif
                 if (A > 0) tt = (ts + A - 1) % sz;
                 if (A < E) break;  // a covered candidate: new gather
                 const uint32_t te = (tt + 1) % sz, ge = s_live[te];
@@ -496,12 +565,19 @@ __global__ __launch_bounds__(SRR_THREADS) void k_srr_mis(ClauseView cv, LoopBuff
                 __syncthreads();
                 --sz;
                 tt = te;
+                SRR_PH(4)
                 if (sz == 0) break;
             }
         }
         weighted += nm;
         __syncthreads();
     }
+#ifdef SRR_PROFILE
+    if (tid == 0)
+        printf("srr_prof T %u steps %llu picks %u gathers %u window_iters %u segs %u conflicts %u ticks total %llu gather %llu reset %llu firstbar %llu seg E %llu ins %llu det %llu com %llu erase %llu\n",
+               T, (unsigned long long)pl.steps, nm, all_gathers, p_wit, p_segs, p_conf,
+               __builtin_amdgcn_s_memrealtime() - p_t0, p_g, p_a, p_b, p_ph[0], p_ph[1], p_ph[2], p_ph[3], p_ph[4]);
+#endif
     weighted += (unsigned long long)nm * pl.extra;
     if (lits) atomicAdd(&s_lits, lits);
     __syncthreads();

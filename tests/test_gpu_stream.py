@@ -73,6 +73,12 @@ STREAM_RR_CASES = {
     "k8_T4_b500": (4000, 6000, 8, 0, 500, 4),
     "mixed_T3_b40": (600, 900, (1, 12), 0, 40, 3),
     "tiny_T32_b2": (40, 30, 3, 0, 2, 32),
+    # k_srr_mis's large-T paths: more sets than candidate slots (512: the sets past them wait
+    # for the next gather), more sets than threads, wide clauses among many sets
+    "u3_T600_b20": (20000, 60000, 3, 0, 20, 600),
+    "u3_T1100_b7": (20000, 55000, 3, 0, 7, 1100),
+    "mixed_T40_b30": (3000, 6000, (1, 12), 0, 30, 40),
+    "k8_T700_b3": (4000, 5600, 8, 0, 3, 700),
 }
 
 

@@ -337,9 +337,10 @@ def main():
                     help="back-to-back eval-only launches timed with HIP events for the roofline (at least 20)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_eval_traffic.json"))
     ap.add_argument("--rr-child", action="store_true", help=argparse.SUPPRESS)
-    ap.add_argument("--stream-line", default="",
+    ap.add_argument("--stream-line", default="4:100000",
                     help="T:BATCH -- also run the streaming solve with T generators of BATCH clauses "
-                         "(GPU rate, and the oracle's first iterations as its CPU baseline and check)")
+                         "(GPU rate, and the oracle's first iterations as its CPU baseline and check); "
+                         "'none' skips it")
     args = ap.parse_args()
 
     if args.rr_child:  # (rr_line_child): one JSON line on stdout, no torch in this process
@@ -578,7 +579,7 @@ def main():
             out["gpu_same_mis_as_cpu_baseline"] = rr_line_child(args)
         except Exception as e:  # reported, never fatal for the GPU number
             out["gpu_same_mis_as_cpu_baseline"] = {"value": None, "error": str(e)}
-    if rank == 0 and world == 1 and args.stream_line:
+    if rank == 0 and world == 1 and args.stream_line and args.stream_line != "none" and not args.rccl_self:
         try:
             st_T, st_b = (int(x) for x in args.stream_line.split(":"))
             n0, m0, k0, kind0, _ = CONFIGS[args.config]

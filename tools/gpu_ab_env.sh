@@ -10,7 +10,7 @@ for rep in $(seq 1 $REPS); do
   for c in $CFGS; do
     for v in $VARS; do
       if [ "$v" = "-" ]; then E=(); else E=("$v"); fi
-      env "${E[@]}" timeout -k 10 200 python bench.py --config $c --no-cpu-baseline --no-rr-line --event-iters 0 $EXTRA \
+      env "${E[@]}" timeout -k 10 200 python bench.py --config $c --no-cpu-baseline --no-rr-line --stream-line none --event-iters 0 $EXTRA \
           > $O/ab_${c}_${v}_$rep.json 2> $O/ab_${c}_${v}_$rep.err
       rc=$?; [ $rc -eq 0 ] || { echo "$c $v rc=$rc"; tail -3 $O/ab_${c}_${v}_$rep.err; exit $rc; }
       python3 -c "

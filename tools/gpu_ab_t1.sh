@@ -5,5 +5,5 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 R=${1:-2}
 for cfg in M C5; do
   echo "== $cfg"
-  bash tools/ab_bench.sh $R --config $cfg --no-rr-line --event-iters 0 || exit $?
+  bash tools/ab_bench.sh $R --config $cfg --no-rr-line --stream-line none --event-iters 0 || exit $?
 done

@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 run() {
   local cfg=$1 g=$2 i=$3
-  timeout -k 10 200 python bench.py --no-cpu-baseline --no-rr-line --event-iters 0 --config $cfg --grid-rounds $g \
+  timeout -k 10 200 python bench.py --no-cpu-baseline --no-rr-line --stream-line none --event-iters 0 --config $cfg --grid-rounds $g \
       > gpurun_out/rounds_${cfg}_${g}_$i.json 2> gpurun_out/rounds_${cfg}_${g}_$i.err || exit $?
   python3 -c "
 import json; d=json.load(open('gpurun_out/rounds_${cfg}_${g}_$i.json'))

@@ -8,6 +8,6 @@ from ._native import AlllError, build, lib  # noqa: F401
 from .solver import (Clause, SATInstance, Solver, Statistics, VariablesArray,  # noqa: F401
                      assignment_digest, comm_unique_id, device_count, generate_ksat, generate_mixed, gloo_exchange,
                      parse_dimacs,
-                     read_dimacs, shard_plan)
+                     read_dimacs, shard_plan, plan_multi_gpu)
 
 __version__ = "0.1.0"

@@ -10,6 +10,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdarg>
 #include <cstddef>
 #include <cstdlib>
@@ -1970,6 +1971,36 @@ int alll_shard_plan(uint64_t n_clauses, int world, int rank, uint64_t* clause_be
     if (clause_begin) *clause_begin = std::min<uint64_t>(n_clauses, tb * TILE);
     if (clause_end) *clause_end = std::min<uint64_t>(n_clauses, te * TILE);
     if (mask_words_per_rank) *mask_words_per_rank = tpr * TILE_WORDS;
+    return ALLL_OK;
+}
+
+int alll_plan_multi_gpu(uint64_t n_clauses, uint64_t n_literals, uint32_t n_vars, int world,
+                        alll_multi_plan* out) {
+    if (!out || world < 1) return fail(ALLL_ERR_INVALID_ARG, "bad arguments");
+    memset(out, 0, sizeof(*out));
+    const double m = (double)n_clauses, G = (double)world;
+    const double k_avg = n_clauses ? (double)n_literals / m : 0.0;
+    // evaluation: the literal stream + assignment + bitmask bytes (alll_eval_bytes) at the rate
+    // the evaluation kernel reaches on one MI355X: 4.3 TB/s while the stream fits the 256 MB
+    // Infinity Cache (M: 121.6 MB in 28 us), 3.3 TB/s beyond it (C4: 1,556 MB in 467 us)
+    const double bytes = 4.0 * (double)n_literals + (double)n_vars / 8.0 + m / 8.0;
+    const double eval_us = bytes / (bytes <= 200e6 ? 4.3e6 : 3.3e6);
+    // violated clauses: a uniform assignment violates a k-clause with probability 2^-k
+    const double u = m * std::pow(2.0, -k_avg);
+    out->eval_us_1gpu = eval_us;
+    out->eval_saved_us = eval_us * (1.0 - 1.0 / G);
+    out->violated_est = u;
+    if (world > 1) {
+        // own shard's marking (k_cmark: 14.4 us for 0.75M violated clauses; k_cpack: 7.4 us per
+        // 10M clauses), the in-graph all-gather (15 us latency + m/8 bytes at ~300 GB/s), the
+        // other shards' violated clauses collected (4.5 us + a 64-byte line each at ~6 TB/s),
+        // the round-0 scatter and reduce the exchange path runs unfused (2.6 + 4.6 us)
+        const double mark = 14.4 * (u / G) / 0.75e6 + 7.4 * (m / G) / 10e6;
+        const double gather = 15.0 + (m / 8.0) / 300e3;
+        const double collect = 4.5 + u * (G - 1.0) / G * 64.0 / 6e6;
+        out->exchange_us = mark + gather + collect + 2.6 + 4.6;
+    }
+    out->plan = world > 1 && out->eval_saved_us > out->exchange_us ? ALLL_PLAN_SHARD : ALLL_PLAN_REPLICATE;
     return ALLL_OK;
 }
 

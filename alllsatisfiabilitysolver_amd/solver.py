@@ -307,6 +307,21 @@ def shard_plan(n_clauses: int, world: int, rank: int):
     return int(b.value), int(e.value), int(w.value)
 
 
+class _MultiPlan(ctypes.Structure):
+    _fields_ = [("eval_us_1gpu", ctypes.c_double), ("eval_saved_us", ctypes.c_double),
+                ("exchange_us", ctypes.c_double), ("violated_est", ctypes.c_double),
+                ("plan", ctypes.c_int), ("pad", ctypes.c_int)]
+
+
+def plan_multi_gpu(n_clauses: int, n_literals: int, n_vars: int, world: int) -> dict:
+    """alll_plan_multi_gpu: {"plan": "shard" | "replicate", and the model's predicted
+    microseconds} for one instance on `world` GPUs."""
+    p = _MultiPlan()
+    N.check(N.lib().alll_plan_multi_gpu(n_clauses, n_literals, n_vars, world, ctypes.byref(p)), "plan_multi_gpu")
+    return {"plan": "shard" if p.plan == 1 else "replicate", "eval_us_1gpu": p.eval_us_1gpu,
+            "eval_saved_us": p.eval_saved_us, "exchange_us": p.exchange_us, "violated_est": p.violated_est}
+
+
 def gloo_exchange(group=None):
     """Host exchange over torch.distributed (gloo) for Solver(exchange=...)."""
     import torch

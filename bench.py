@@ -279,6 +279,44 @@ def stream_line(args, n, m, k, kind, T, bs, check_iters=2, warmup=3, steps=10):
     return out
 
 
+def shard_line(args, n, offs, lits, kw, rank, world, exchange_impl, comm_id, dist, barrier, torch, warmup=3, steps=20):
+    """N>1 with the replicated plan: the clause-sharded loop (alll_shard_plan, the violated-bitmask
+    exchange every iteration) on the same instance, `steps` iterations timed as the main line
+    (barrier + max over ranks), checked against the committed oracle trajectory."""
+    from alllsatisfiabilitysolver_amd import Solver
+
+    kw = dict(kw, rank=rank, world=world)
+    if exchange_impl == "host":
+        from alllsatisfiabilitysolver_amd import gloo_exchange
+
+        s = Solver(n, offs, lits, exchange=gloo_exchange(), **kw)
+    else:
+        s = Solver(n, offs, lits, comm_id=comm_id, **kw)
+    try:
+        s.run(warmup)
+        s.synchronize()
+        barrier()
+        it0 = s.stats()["n_iterations"]
+        t0 = time.perf_counter()
+        s.run(steps, sync=False)
+        s.synchronize()
+        barrier()
+        dt = time.perf_counter() - t0
+        tt = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dt = float(tt.item())
+        st = s.stats()
+        done = st["n_iterations"] - it0
+        traj = trajectory_check(args.config, 1, st, s.assignment_words(), args.seed) if rank == 0 else None
+        m = len(offs) - 1
+        return {"value": m * done / dt if done else None, "unit": "clause-evals/s", "exchange": exchange_impl,
+                "n_comm": s.comm_size(), "steps": done, "warmup": warmup,
+                "resample_iters_per_s": done / dt if done else None,
+                "ms_per_step": dt * 1e3 / done if done else None, "trajectory_check": traj}
+    finally:
+        s.close()
+
+
 def rr_line_child(args, timeout_s=240):
     """The round-robin line in a child process (this script with --rr-child): its own HIP
     context and a time limit, so that it can neither disturb nor stall the main line."""
@@ -337,6 +375,11 @@ def main():
                     help="back-to-back eval-only launches timed with HIP events for the roofline (at least 20)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_eval_traffic.json"))
     ap.add_argument("--rr-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--plan", default="auto", choices=["auto", "shard", "replicate"],
+                    help="N>1: clause-sharded loop with the per-iteration exchange, or every rank the whole "
+                         "one-GPU loop; auto = alll_plan_multi_gpu's cost model (DESIGN.md §5.2)")
+    ap.add_argument("--no-shard-line", action="store_true",
+                    help="N>1 with the replicated plan: skip the secondary run of the sharded (exchange) path")
     ap.add_argument("--stream-line", default="4:100000",
                     help="T:BATCH -- also run the streaming solve with T generators of BATCH clauses "
                          "(GPU rate, and the oracle's first iterations as its CPU baseline and check); "
@@ -403,6 +446,14 @@ def main():
     else:
         offs, lits = generate_ksat(1, n, m, k, kind)
     t_gen = time.perf_counter() - t0
+    from alllsatisfiabilitysolver_amd import plan_multi_gpu
+
+    mplan = plan_multi_gpu(m, int(len(lits)), n, world)
+    plan = mplan["plan"] if args.plan == "auto" else args.plan
+    if world == 1:
+        plan = "single"
+    log(f"[rank {rank}] multi-GPU plan: {plan} (model: evaluation {mplan['eval_us_1gpu']:.1f} us on one GPU, "
+        f"sharding saves {mplan['eval_saved_us']:.1f}, exchange costs {mplan['exchange_us']:.1f})")
     flags = N.FLAG_KERNEL_TIMING  # kernels stamp device wall-clock times of every iteration
     if args.exchange == "allreduce":
         flags |= N.FLAG_EXCHANGE_ALLREDUCE
@@ -412,13 +463,19 @@ def main():
         flags |= N.FLAG_ATOMIC_CLAIMS
     t0 = time.perf_counter()
     kw = dict(seed=args.seed, device=local_rank, rank=rank, world=world, flags=flags, grid_rounds=args.grid_rounds)
-    if exchange_impl == "host":
+    if plan == "replicate":
+        # every rank runs the whole one-GPU loop on its own device: no exchange, the same
+        # trajectory on every rank (the sharded path runs afterwards as a secondary line)
+        kw.update(rank=0, world=1)
+        s = Solver(n, offs, lits, **kw)
+    elif exchange_impl == "host":
         from alllsatisfiabilitysolver_amd import gloo_exchange
 
         s = Solver(n, offs, lits, exchange=gloo_exchange(), **kw)
     else:
         s = Solver(n, offs, lits, comm_id=comm_id, **kw)  # RCCL failure raises: fatal
-    del offs, lits
+    if not (plan == "replicate" and not args.no_shard_line):
+        del offs, lits
     t_create = time.perf_counter() - t0
     log(f"[rank {rank}] generated {m} clauses in {t_gen:.2f}s, uploaded in {t_create:.2f}s, "
         f"layout k={s.layout()}, eval kernel {s.eval_kernel()}, exchange {exchange_impl}")
@@ -436,7 +493,7 @@ def main():
         t = torch.tensor([1], dtype=torch.int64)
         dist.all_reduce(t)
         ranks_seen = int(t.item())
-        if ranks_seen != world or n_comm != world:
+        if ranks_seen != world or n_comm != (1 if plan == "replicate" else world):
             raise SystemExit(f"rank {rank}: {ranks_seen} ranks answered, communicator holds {n_comm}, "
                              f"expected {world}")
 
@@ -510,7 +567,7 @@ def main():
             "metric": "clause-evals/sec + resample iters/sec, random 3-SAT 10M clauses, 1/2/4/8 GPUs",
             "value": value,
             "unit": "clause-evals/s",
-            "n_gpus": n_comm,
+            "n_gpus": ranks_seen,
             "ranks_seen": ranks_seen,
             "steps": args.steps,
             "steps_done": steps_done,
@@ -524,7 +581,9 @@ def main():
             "config": {"workload": f"{args.config}: {desc}", "n_vars": n, "n_clauses": m, "k": k,
                        "solve_seed": args.seed,
                        "exchange": f"{args.exchange}/{exchange_impl}" if world > 1 or comm_id else "none",
-                       "parallelism": f"clause-shard x{world}"},
+                       "parallelism": (f"replicated x{world}" if plan == "replicate" else
+                                       f"clause-shard x{world}" if world > 1 else "one GPU")},
+            "multi_gpu_plan": dict(mplan, chosen=plan, requested=args.plan) if world > 1 else None,
             "value_kind": vkind,
             "trajectory_check": traj,
             "graphs": graphs,
@@ -571,6 +630,13 @@ def main():
             },
         }
     s.close()
+    if world > 1 and plan == "replicate" and not args.no_shard_line:
+        # the clause-sharded path (exchange every iteration) on the same instance, so that a
+        # multi-GPU run still exercises and checks it: its own rate and trajectory check
+        sh = shard_line(args, n, offs, lits, kw, rank, world, exchange_impl, comm_id, dist, barrier, torch)
+        del offs, lits
+        if rank == 0:
+            out["shard_line"] = sh
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not args.no_rr_line:
         # the CPU baseline runs the reference's -p T path, whose MIS is the T-set round robin
         # (SATInstance.h:414-447), not the one-set LFMIS timed above: the same workload with that
@@ -600,7 +666,8 @@ def main():
         dist.destroy_process_group()
     rr = (out or {}).get("gpu_same_mis_as_cpu_baseline") or {}
     bad = [name for name, t in (("T=1 loop", traj), ("round robin", rr.get("trajectory_check")),
-                                ("streaming solve", ((out or {}).get("stream_line") or {}).get("check")))
+                                ("streaming solve", ((out or {}).get("stream_line") or {}).get("check")),
+                                ("sharded path", ((out or {}).get("shard_line") or {}).get("trajectory_check")))
            if t and t.get("match") is False]
     if rank == 0 and bad:
         log(f"[rank 0] FAIL: the {' and '.join(bad)} left a state that differs from the committed oracle trajectory")

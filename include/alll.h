@@ -249,6 +249,30 @@ int alll_dimacs_read(const char* path, uint32_t* n_vars, uint64_t* n_clauses, ui
 int alll_shard_plan(uint64_t n_clauses, int world, int rank, uint64_t* clause_begin,
                     uint64_t* clause_end, uint64_t* mask_words_per_rank);
 
+/* Multi-GPU plan for one instance on `world` GPUs of one node.  The exact
+ * LFMIS and the resample run on every rank whatever the plan (their per-round minima over all
+ * clauses would cost ~2 collectives per round), so only the evaluation can shard, and the
+ * sharded plan (alll_shard_plan + the RCCL all-gather of the violated bitmask) pays an exchange
+ * every iteration.  From the instance's size, the model predicts the evaluation time on one GPU,
+ * what sharding saves of it, and the exchange's cost (marking, all-gather, collection of the
+ * other shards' violated clauses, the round-0 scatter and reduce the exchange path cannot fuse),
+ * with rates measured on one MI355X; `plan` is ALLL_PLAN_SHARD when the saving
+ * exceeds the exchange, else ALLL_PLAN_REPLICATE: every rank runs the whole one-GPU loop (no
+ * exchange; the trajectories are identical by construction, Philox keyed by seed, iteration
+ * and word).  k_avg = literals / clauses. */
+#define ALLL_PLAN_REPLICATE 0
+#define ALLL_PLAN_SHARD 1
+typedef struct {
+    double eval_us_1gpu;   /* evaluation of the whole instance on one GPU */
+    double eval_saved_us;  /* eval_us_1gpu * (1 - 1/world) */
+    double exchange_us;    /* the sharded plan's per-iteration exchange */
+    double violated_est;   /* violated clauses per iteration assumed: n_clauses * 2^-k_avg */
+    int plan;              /* ALLL_PLAN_REPLICATE or ALLL_PLAN_SHARD */
+    int pad;
+} alll_multi_plan;
+int alll_plan_multi_gpu(uint64_t n_clauses, uint64_t n_literals, uint32_t n_vars, int world,
+                        alll_multi_plan* out);
+
 /* The solver's initial assignment for `seed` as n_vars bytes of 0/1 (word w of the packed
  * form = Philox4x32-10(key=seed, ctr={w, 0, 0xFFFFFFFF, 0}).x); used by the compatibility
  * VariablesArray (replaces the random_device fill of VariablesArray.h:23-34). */

@@ -43,6 +43,28 @@ def test_struct_layout(native):
     assert ctypes.sizeof(native.PhaseTimes) == 6 * 8
 
 
+def test_multi_gpu_plan(native):
+    """alll_plan_multi_gpu: the bench instance M and C2/C5 (10M clauses or fewer,
+    3-SAT) replicate at every node size -- sharding their ~28 us evaluation saves less than the
+    exchange costs; C4 (128M clauses) shards from 4 GPUs on; one GPU is never sharded."""
+    from alllsatisfiabilitysolver_amd import plan_multi_gpu
+
+    cfg = {"M": (2_500_000, 10_000_000, 3), "C2": (1_000_000, 4_000_000, 3), "C5": (2_500_000, 10_000_000, 3),
+           "C4": (32_000_000, 128_000_000, 3)}
+    for name, (n, m, k) in cfg.items():
+        p1 = plan_multi_gpu(m, m * k, n, 1)
+        assert p1["plan"] == "replicate" and p1["exchange_us"] == 0.0 and p1["eval_saved_us"] == 0.0
+        for G in (2, 4, 8):
+            p = plan_multi_gpu(m, m * k, n, G)
+            assert p["eval_saved_us"] == pytest.approx(p["eval_us_1gpu"] * (1 - 1 / G))
+            want = "shard" if name == "C4" and G >= 4 else "replicate"
+            assert p["plan"] == want, (name, G, p)
+            assert (p["eval_saved_us"] > p["exchange_us"]) == (want == "shard")
+    # the evaluation model at M: 121.6 MB at 4.3 TB/s
+    assert plan_multi_gpu(10_000_000, 30_000_000, 2_500_000, 8)["eval_us_1gpu"] == pytest.approx(28.3, abs=0.5)
+    assert native.lib().alll_plan_multi_gpu(1, 3, 1, 0, None) != 0  # bad arguments
+
+
 def test_create_fails_loudly_without_gpu(native):
     from alllsatisfiabilitysolver_amd import Solver, AlllError
 

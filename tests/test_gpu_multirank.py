@@ -215,16 +215,30 @@ def _bench_stdout(args, env_extra=None):
     return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("mode", ["rccl_self", "host_n2"])
+@pytest.mark.parametrize("mode", ["rccl_self", "host_n2", "host_n2_shard"])
 def test_bench_prints_one_json_line(mode):
     """The driver reads one JSON line from bench.py's stdout: RCCL's banner at communicator
     init and the rank processes' output must not reach it (N=1 over a one-rank RCCL
-    communicator; N=2 self-launched ranks over the host exchange on this one GPU)."""
+    communicator; N=2 self-launched ranks over the host exchange on this one GPU).  With N=2 the
+    planner replicates C2 and the sharded path runs as the checked secondary
+    line; --plan shard makes the sharded path the headline."""
     common = ["--config", "C2", "--steps", "4", "--warmup", "1", "--no-cpu-baseline", "--event-iters", "0"]
     if mode == "rccl_self":
         d = _bench_stdout(common + ["--rccl-self"])
         assert d["n_gpus"] == 1 and d["config"]["exchange"] == "allgather/rccl-self"
     else:
-        d = _bench_stdout(common + ["--gpus", "2", "--exchange-impl", "host"], {"ALLL_BENCH_SAME_DEVICE": "1"})
+        extra = ["--plan", "shard"] if mode == "host_n2_shard" else []
+        d = _bench_stdout(common + ["--gpus", "2", "--exchange-impl", "host"] + extra, {"ALLL_BENCH_SAME_DEVICE": "1"})
         assert d["n_gpus"] == 2 and d["ranks_seen"] == 2
+        mp = d["multi_gpu_plan"]
+        assert mp["plan"] == "replicate" and mp["requested"] == ("shard" if extra else "auto")
+        if extra:
+            assert mp["chosen"] == "shard" and d["config"]["parallelism"] == "clause-shard x2"
+            assert "shard_line" not in d
+        else:
+            assert mp["chosen"] == "replicate" and d["config"]["parallelism"] == "replicated x2"
+            sl = d["shard_line"]
+            assert sl["n_comm"] == 2 and sl["steps"] == 20 and sl["value"] > 0
+            assert sl["trajectory_check"]["match"] is True, sl["trajectory_check"]
+        assert d["trajectory_check"]["match"] is True, d["trajectory_check"]
     assert d["steps_done"] == 4 and d["value"] > 0

@@ -67,6 +67,78 @@ uint32_t orc_resample_bit(uint64_t seed, uint64_t iter, uint32_t v) {
 }
 
 /* ------------------------------------------------------------------------- */
+/* The reference's own RNG, for the reference-RNG mode:       */
+/* RBG<default_random_engine> (RandomBoolGenerator.h:29-52) over libstdc++'s   */
+/* (GCC 11, the toolchain here; unpinned by the reference) default_random_    */
+/* engine = minstd_rand0 = linear_congruential_engine<uint_fast32_t, 16807, 0, */
+/* 2147483647> and uniform_int_distribution<unsigned long long> (bits/         */
+/* uniform_int_dist.h: downscaling by rejection, upscaling by recursion), each */
+/* engine seeded with one std::random_device{}() value (VariablesArray.h:24,   */
+/* SATInstance.h:346).  random_device is the reference's only nondeterminism:  */
+/* the probe (oracle/ref_probe.cpp) replaces it with a 64-bit LCG, restated     */
+/* here, so the reference's whole T = 1 trajectory is reproducible.            */
+/* ------------------------------------------------------------------------- */
+uint32_t orc_refrng_rd_next(uint64_t* state) {
+    *state = *state * 6364136223846793005ull + 1442695040888963407ull;
+    return (uint32_t)(*state >> 33);
+}
+
+#define MINSTD_M 2147483647ull
+#define MINSTD_MIN 1ull
+#define MINSTD_RANGE (MINSTD_M - 1ull - MINSTD_MIN) /* max() - min() */
+
+static void minstd_seed(uint64_t* x, uint64_t s) {
+    const uint64_t r = s % MINSTD_M;
+    *x = r ? r : 1ull;
+}
+static uint64_t minstd_next(uint64_t* x) {
+    *x = (*x * 16807ull) % MINSTD_M;
+    return *x;
+}
+
+/* uniform_int_distribution<unsigned long long>(0, urange)(engine) */
+static uint64_t uid_u64(uint64_t* x, uint64_t urange) {
+    uint64_t ret;
+    if (MINSTD_RANGE > urange) {
+        const uint64_t uerange = urange + 1, scaling = MINSTD_RANGE / uerange, past = uerange * scaling;
+        do ret = minstd_next(x) - MINSTD_MIN;
+        while (ret >= past);
+        ret /= scaling;
+    } else if (MINSTD_RANGE < urange) {
+        uint64_t tmp;
+        do {
+            const uint64_t uerngrange = MINSTD_RANGE + 1;
+            tmp = uerngrange * uid_u64(x, urange / uerngrange);
+            ret = tmp + (minstd_next(x) - MINSTD_MIN);
+        } while (ret > urange || ret < tmp);
+    } else {
+        ret = minstd_next(x) - MINSTD_MIN;
+    }
+    return ret;
+}
+
+void orc_rbg_seed(orc_rbg* g, uint32_t seed) {
+    minstd_seed(&g->x, seed);
+    g->m = 1;
+}
+/* RBG::sample: a 64-bit draw | bit 63 serves 63 bits, lowest first */
+uint32_t orc_rbg_sample(orc_rbg* g) {
+    if (g->m == 1) g->m = uid_u64(&g->x, ~0ull) | (1ull << 63);
+    const uint32_t b = (uint32_t)(g->m & 1u);
+    g->m >>= 1;
+    return b;
+}
+
+/* VariablesArray(n) (VariablesArray.h:23-34): one random_device value seeds the engine, then
+ * one RBG bit per variable in index order */
+void orc_refrng_init(uint64_t* rd_state, uint32_t n_vars, uint32_t* A) {
+    orc_rbg g;
+    orc_rbg_seed(&g, orc_refrng_rd_next(rd_state));
+    memset(A, 0, sizeof(uint32_t) * ((n_vars + 31) / 32));
+    for (uint32_t v = 0; v < n_vars; ++v) A[v >> 5] |= orc_rbg_sample(&g) << (v & 31);
+}
+
+/* ------------------------------------------------------------------------- */
 /* Synthetic instance generator (shared specification with the product's      */
 /* generator; both are checked equal in tests).  Counter-based per clause.     */
 /* ------------------------------------------------------------------------- */
@@ -237,9 +309,12 @@ uint64_t orc_rr_mis(uint32_t n_vars, const uint64_t* offs, const uint32_t* lits,
 /* floor(sum|M| / n_iterations).                                               */
 /* max_iters (0 = unlimited) caps eval passes; a capped pass does not resample. */
 /* ------------------------------------------------------------------------- */
+/* rd_state != NULL: the reference-RNG mode -- every resample round draws from a fresh
+ * RBG<default_random_engine> seeded by the next random_device value (resample_clauses,
+ * SATInstance.h:340-365, with T = 1: bits in MIS pick order, literal order) instead of Philox */
 static int solve_sets(uint32_t n_vars, uint64_t m, const uint64_t* offs, const uint32_t* lits,
                       uint64_t seed, uint64_t max_iters, uint32_t T, const uint64_t* chunk_starts,
-                      uint32_t* A, orc_stats* st, orc_iter_cb cb, void* cb_user) {
+                      uint32_t* A, orc_stats* st, orc_iter_cb cb, void* cb_user, uint64_t* rd_state) {
     uint64_t nw = (m + 63) / 64;
     uint64_t* vmask = (uint64_t*)calloc(nw ? nw : 1, sizeof(uint64_t));
     uint32_t* U = (uint32_t*)malloc(sizeof(uint32_t) * (m ? m : 1));
@@ -259,11 +334,13 @@ static int solve_sets(uint32_t n_vars, uint64_t m, const uint64_t* offs, const u
                             : orc_lfmis(n_vars, offs, lits, U, nu, M, used);
         sum_mis += nm;
         uint64_t dres = 0, iter = st->n_iterations - 1;
+        orc_rbg g;
+        if (rd_state) orc_rbg_seed(&g, orc_refrng_rd_next(rd_state));
         for (uint64_t i = 0; i < nm; ++i) {
             uint32_t c = M[i];
             for (uint64_t j = offs[c]; j < offs[c + 1]; ++j) {
                 uint32_t v = lits[j] >> 1;
-                uint32_t b = orc_resample_bit(seed, iter, v);
+                uint32_t b = rd_state ? orc_rbg_sample(&g) : orc_resample_bit(seed, iter, v);
                 A[v >> 5] = (A[v >> 5] & ~(1u << (v & 31))) | (b << (v & 31));
             }
             dres += offs[c + 1] - offs[c];
@@ -281,7 +358,17 @@ static int solve_sets(uint32_t n_vars, uint64_t m, const uint64_t* offs, const u
 int orc_solve(uint32_t n_vars, uint64_t m, const uint64_t* offs, const uint32_t* lits,
               uint64_t seed, uint64_t max_iters, uint32_t* A, orc_stats* st,
               orc_iter_cb cb, void* cb_user) {
-    return solve_sets(n_vars, m, offs, lits, seed, max_iters, 1, 0, A, st, cb, cb_user);
+    return solve_sets(n_vars, m, offs, lits, seed, max_iters, 1, 0, A, st, cb, cb_user, NULL);
+}
+
+/* orc_solve in the reference-RNG mode: A is initialised here (orc_refrng_init) from the
+ * random_device stand-in seeded with rd_seed, then every resample round takes the next value */
+int orc_solve_refrng(uint32_t n_vars, uint64_t m, const uint64_t* offs, const uint32_t* lits,
+                     uint64_t rd_seed, uint64_t max_iters, uint32_t* A, orc_stats* st,
+                     orc_iter_cb cb, void* cb_user) {
+    uint64_t rd = rd_seed;
+    orc_refrng_init(&rd, n_vars, A);
+    return solve_sets(n_vars, m, offs, lits, 0, max_iters, 1, 0, A, st, cb, cb_user, &rd);
 }
 
 /* parallel_solve with T > 1 clause chunks (chunk q = clauses [chunk_starts[q],
@@ -290,7 +377,7 @@ int orc_solve(uint32_t n_vars, uint64_t m, const uint64_t* offs, const uint32_t*
 int orc_solve_rr(uint32_t n_vars, uint64_t m, const uint64_t* offs, const uint32_t* lits,
                  uint64_t seed, uint64_t max_iters, uint32_t T, const uint64_t* chunk_starts,
                  uint32_t* A, orc_stats* st, orc_iter_cb cb, void* cb_user) {
-    return solve_sets(n_vars, m, offs, lits, seed, max_iters, T, chunk_starts, A, st, cb, cb_user);
+    return solve_sets(n_vars, m, offs, lits, seed, max_iters, T, chunk_starts, A, st, cb, cb_user, NULL);
 }
 
 /* ------------------------------------------------------------------------- */

@@ -35,6 +35,15 @@ void orc_chunk_bounds(uint64_t m, uint32_t T, uint64_t* starts);
 uint64_t orc_rr_mis(uint32_t n_vars, const uint64_t* offs, const uint32_t* lits, const uint32_t* U,
                     uint64_t nu, uint32_t T, const uint64_t* chunk_starts, uint32_t* M,
                     uint8_t* scratch_used);
+/* the reference's own RNG (reference-RNG mode): random_device stand-in, RBG<minstd_rand0> */
+typedef struct { uint64_t x, m; } orc_rbg;
+uint32_t orc_refrng_rd_next(uint64_t* state);
+void orc_rbg_seed(orc_rbg* g, uint32_t seed);
+uint32_t orc_rbg_sample(orc_rbg* g);
+void orc_refrng_init(uint64_t* rd_state, uint32_t n_vars, uint32_t* A);
+int orc_solve_refrng(uint32_t n_vars, uint64_t m, const uint64_t* offs, const uint32_t* lits,
+                     uint64_t rd_seed, uint64_t max_iters, uint32_t* A, orc_stats* st,
+                     orc_iter_cb cb, void* cb_user);
 int orc_solve(uint32_t n_vars, uint64_t m, const uint64_t* offs, const uint32_t* lits, uint64_t seed,
               uint64_t max_iters, uint32_t* A, orc_stats* st, orc_iter_cb cb, void* cb_user);
 int orc_solve_rr(uint32_t n_vars, uint64_t m, const uint64_t* offs, const uint32_t* lits, uint64_t seed,

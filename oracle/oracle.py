@@ -86,6 +86,11 @@ def lib():
                                           ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
                                           _u32p, ctypes.POINTER(OrcStats), ITER_CB, ctypes.c_void_p]
         L.orc_solve_stream_rr.restype = ctypes.c_int
+        L.orc_solve_refrng.argtypes = [ctypes.c_uint32, ctypes.c_uint64, _u64p, _u32p, ctypes.c_uint64,
+                                       ctypes.c_uint64, _u32p, ctypes.POINTER(OrcStats), ITER_CB, ctypes.c_void_p]
+        L.orc_solve_refrng.restype = ctypes.c_int
+        L.orc_refrng_init.argtypes = [_u64p, ctypes.c_uint32, _u32p]
+        L.orc_refrng_init.restype = None
         L.orc_dimacs_parse.argtypes = [ctypes.c_char_p, ctypes.c_uint64, _u32p, _u64p, _u64p,
                                        _u32p, _u64p]
         L.orc_dimacs_parse.restype = ctypes.c_int
@@ -315,6 +320,36 @@ def solve_stream_rr(n_vars, offs, lits, seed, batch, T, max_iters=0, A0=None, tr
                                    step_cap, _p(A, _u32p), ctypes.byref(st), cbf, None)
     stats = {k: int(getattr(st, k)) for k, _ in OrcStats._fields_ if k != "pad"}
     return int(rc), stats, A, rows
+
+
+def refrng_init(rd_seed, n_vars):
+    """The reference's VariablesArray fill (VariablesArray.h:23-34) under the probe's random_device
+    stand-in seeded with rd_seed: packed words, and the stand-in's state after the draw."""
+    A = np.zeros(max(1, (n_vars + 31) // 32), np.uint32)
+    st = ctypes.c_uint64(rd_seed)
+    lib().orc_refrng_init(ctypes.byref(st), n_vars, _p(A, _u32p))
+    return A, int(st.value)
+
+
+def solve_refrng(n_vars, offs, lits, rd_seed, max_iters=0, trace=False):
+    """orc_solve in the reference-RNG mode (orc_solve_refrng): the reference's own RBG /
+    minstd_rand0 / uniform_int_distribution stream, engines seeded from the random_device
+    stand-in.  Returns (stats dict, final A words, per-iteration rows (it, |U|, |M|, dres, A))."""
+    m = len(offs) - 1
+    A = np.zeros(max(1, (n_vars + 31) // 32), np.uint32)
+    st = OrcStats()
+    rows = []
+
+    def cb(user, it, nu, nm, dres, Ap):
+        if trace:
+            rows.append((int(it), int(nu), int(nm), int(dres),
+                         np.ctypeslib.as_array(Ap, shape=(A.size,)).copy()))
+
+    cbf = ITER_CB(cb)
+    lib().orc_solve_refrng(n_vars, m, _p(offs, _u64p), _p(lits, _u32p), rd_seed, max_iters, _p(A, _u32p),
+                           ctypes.byref(st), cbf, None)
+    stats = {k: int(getattr(st, k)) for k, _ in OrcStats._fields_ if k != "pad"}
+    return stats, A, rows
 
 
 # Pure-Python restatement of one streaming iteration with T threads (small cases; the maps the

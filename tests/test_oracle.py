@@ -478,3 +478,31 @@ def test_bench_trajectory_check_logic():
     finally:
         S.assignment_digest = orig
         pkg.assignment_digest = orig
+
+
+REFRNG_FIXTURES = [p for p in FIXTURES if p.endswith("_T1.npz")]
+
+
+@pytest.mark.parametrize("path", REFRNG_FIXTURES, ids=lambda p: os.path.basename(p)[:-4])
+def test_oracle_reference_rng_reproduces_reference_trajectory(path, oracle_mod):
+    """The reference-RNG mode (orc_solve_refrng): with the probe's random_device stand-in
+    (rd_seed = 7, tests/golden/manifest.json), the restated RBG<minstd_rand0> /
+    uniform_int_distribution<unsigned long long> stream reproduces the reference's whole T = 1
+    trajectory -- the initial VariablesArray fill, the assignment after every iteration, the
+    final statistics -- as recorded by the reference's own code (oracle/ref_probe.cpp trace)."""
+    o = oracle_mod
+    f = load(path)
+    man = {d["fixture"]: d for d in json.load(open(os.path.join(GOLDEN, "manifest.json")))["fixtures"]}
+    name = os.path.basename(path)[:-4]
+    n, offs, lits = int(f["n_vars"]), f["offs"], f["lits"]
+    rd_seed = json.load(open(os.path.join(GOLDEN, "manifest.json")))["rd_seed"]
+    A0, _ = o.refrng_init(rd_seed, n)
+    np.testing.assert_array_equal(A0, f["A"][0], err_msg="initial fill")
+    its = f["A"].shape[0]
+    st, A, rows = o.solve_refrng(n, offs, lits, rd_seed, max_iters=man[name].get("max_iters") or its + 5, trace=True)
+    assert len(rows) >= its - 1
+    for i in range(its - 1):
+        np.testing.assert_array_equal(rows[i][4], f["A"][i + 1], err_msg=f"A after iteration {i + 1}")
+        assert rows[i][3] == int(f["dres"][i])
+    np.testing.assert_array_equal(A, f["A_final"])
+    assert [st["n_iterations"], st["n_resamples"], st["avg_mis_size"]] == [int(x) for x in f["stats"]]

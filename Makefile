@@ -11,7 +11,7 @@ SRC := $(PKG)/csrc
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-result \
             -Iinclude -I$(SRC) -I$(ROCM)/include $(EXTRA)
 LIB := $(PKG)/liballl.so
-OBJS := $(SRC)/alll_kernels.o $(SRC)/alll_stream.o $(SRC)/alll_runtime.o $(SRC)/alll_host.o
+OBJS := $(SRC)/alll_kernels.o $(SRC)/alll_stream.o $(SRC)/alll_refrng.o $(SRC)/alll_runtime.o $(SRC)/alll_host.o
 
 all: $(LIB)
 
@@ -19,6 +19,9 @@ $(SRC)/alll_kernels.o: $(SRC)/alll_kernels.hip $(SRC)/alll_internal.h
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
 $(SRC)/alll_stream.o: $(SRC)/alll_stream.hip $(SRC)/alll_internal.h
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(SRC)/alll_refrng.o: $(SRC)/alll_refrng.hip $(SRC)/alll_internal.h
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
 $(SRC)/alll_runtime.o: $(SRC)/alll_runtime.cpp $(SRC)/alll_internal.h include/alll.h

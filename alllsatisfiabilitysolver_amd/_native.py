@@ -34,6 +34,7 @@ FLAG_NO_RANGED = 1 << 3
 FLAG_KERNEL_TIMING = 1 << 4
 FLAG_ATOMIC_CLAIMS = 1 << 5
 FLAG_LFMIS = 1 << 6
+FLAG_REFERENCE_RNG = 1 << 7
 
 MAX_GPU_STATS = 64
 

@@ -175,6 +175,8 @@ struct DevState {
     uint32_t tmis_cnt;     // MIS entries decided by the tail kernel (list b.tmis)
     uint64_t win_start;    // streaming solve: generator steps taken before this iteration
     uint64_t win_len;      // streaming solve: steps (clauses yielded) in this iteration
+    uint64_t rd_state;     // reference-RNG mode: state of the random_device stand-in (alll_refrng.hip)
+    uint64_t rd_bits;      // reference-RNG mode: bits the current resample round draws
 };
 
 // Clause storage on the device.
@@ -349,6 +351,12 @@ struct LoopBuffers {
     uint32_t* srr_ent;          // violated walk steps of every generator in walk order (SRR_ENT_WORDS each)
     uint32_t* srr_step;         // (steps + 1) x srr_T: first entry of generator t's batch at step s; row
                                 // `steps` = the ends of the lists
+    // reference-RNG mode (ALLL_FLAG_REFERENCE_RNG, alll_refrng.hip; nullptr otherwise)
+    unsigned long long* rrng_mask;   // ceil(m/64) words: this round's MIS clauses, clause order
+    uint32_t* rrng_woff;             // per mask word: its clauses' literal count, then their bit offset in the block
+    uint32_t* rrng_bsum;             // per 1024-word block: bit total, then the block's bit offset
+    unsigned long long* rrng_stream; // the round's RBG draws (63 bits each)
+    uint64_t rrng_cap;               // draws rrng_stream holds
     uint32_t n_vars;
     uint32_t n_words;
     uint32_t n_tiles;       // tiles covering [0, m)
@@ -400,6 +408,9 @@ hipError_t launch_apply_delta(const LoopBuffers& b, hipStream_t s);
 hipError_t fp_repair_occupancy(const ClauseView& cv, const LoopBuffers& b, int* blocks_per_cu);
 // streaming solve with T > 1 threads (alll_stream.hip): the check's first violated offset of every
 // generator (gated on the loop state), then the iteration's lists and round robins (b.srr_plan)
+// reference-RNG mode (alll_refrng.hip): the initial fill and the resample round
+hipError_t launch_refrng_init(const LoopBuffers& b, hipStream_t s);
+hipError_t launch_refrng_resample(const ClauseView& cv, const LoopBuffers& b, hipStream_t s);
 hipError_t launch_srr_first(const LoopBuffers& b, hipStream_t s);
 hipError_t launch_srr_lists(const ClauseView& cv, const LoopBuffers& b, uint32_t nblk, hipStream_t s);
 hipError_t launch_srr_mis(const ClauseView& cv, const LoopBuffers& b, hipStream_t s);

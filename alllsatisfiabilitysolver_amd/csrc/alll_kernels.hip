@@ -5021,6 +5021,7 @@ __global__ __launch_bounds__(FP_TURN_THREADS) void k_fp_turn(ClauseView cv, Loop
 // ------------------------------------------------------------------------------------
 // Launchers.
 hipError_t launch_init_assignment(const LoopBuffers& b, hipStream_t s) {
+    if (b.rrng_mask) return launch_refrng_init(b, s);  // (reference-RNG mode)
     if (b.n_words == 0) return hipSuccess;
     k_init_assignment<<<(b.n_words + 255) / 256, 256, 0, s>>>(b.A, b.n_words, b.n_vars, b.seed);
     return hipGetLastError();
@@ -5375,6 +5376,7 @@ hipError_t launch_resample(const ClauseView& cv, const LoopBuffers& b, uint32_t 
         ALLL_DISPATCH_K(cv.k, (k_resample_delta<K><<<b.n_tiles + 1, ROUND_THREADS, 0, s>>>(cv, b, own_begin, own_end)));
         return hipGetLastError();
     }
+    if (b.rrng_mask) return launch_refrng_resample(cv, b, s);  // (reference-RNG mode)
     if (b.n_vars == 0) return hipSuccess;
     const uint64_t blocks = ((uint64_t)b.n_words * 2 + 255) / 256;  // a thread per 16 variables
     if (blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;

@@ -324,6 +324,8 @@ int read_state(alll_ctx* c) {
                                   "were not all resident)", c->b.rr_mw);
     if (c->h_state->error == 5)
         return fail(ALLL_ERR_HIP, "round-robin MIS: an incremental-pass kernel ran without its buffers (DESIGN.md §10)");
+    if (c->h_state->error == 7)
+        return fail(ALLL_ERR_HIP, "reference-RNG mode: a resample round needed more draws than its buffer holds");
     if (c->h_state->error == 6)
         return fail(ALLL_ERR_HIP, "streaming round robin: k_srr_mis made no progress (DESIGN.md §4.2.1)");
     if (c->h_state->error)
@@ -939,6 +941,20 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
                 return fail(ALLL_ERR_UNSUPPORTED, "streaming solve with n_threads > 1: clause %llu is empty",
                             (unsigned long long)c);
     }
+    // the reference's own random stream (ALLL_FLAG_REFERENCE_RNG, alll_refrng.hip): defined for the
+    // one-thread loop on one GPU (the reference's T > 1 resample draws from T engines inside a
+    // schedule(dynamic) loop, so its bits follow the thread timing)
+    const bool refrng = (opt.flags & ALLL_FLAG_REFERENCE_RNG) != 0;
+    if (refrng) {
+        bool zid = true;
+        for (int i = 0; i < 128; ++i) zid &= opt.comm_id[i] == 0;
+        if (opt.n_threads > 1)
+            return fail(ALLL_ERR_UNSUPPORTED, "reference-RNG mode: n_threads must be 1 (the reference's T > 1 "
+                                              "resample draws from T engines in a schedule(dynamic) loop)");
+        if (opt.stream_batch) return fail(ALLL_ERR_UNSUPPORTED, "reference-RNG mode: not with the streaming solve");
+        if (opt.world > 1 || !zid || (opt.flags & ALLL_FLAG_EXCHANGE_ALLREDUCE))
+            return fail(ALLL_ERR_UNSUPPORTED, "reference-RNG mode runs on one GPU without the exchange path");
+    }
     std::vector<uint32_t> rr_sets;
     if (rr_T) {
         rr_sets.resize(rr_T + 1);
@@ -1226,6 +1242,17 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     if ((rc = dalloc(c, &b.mis, (size_t)n_tiles * TILE))) return bail(rc);
     if ((rc = dalloc(c, &b.left, (size_t)n_tiles * TILE * ent_words))) return bail(rc);
     if ((rc = dalloc(c, &b.tmis, (size_t)n_tiles * TILE))) return bail(rc);
+    if (refrng && m) {
+        const uint64_t nmw = (m + 63) / 64, nblk = (nmw + 1023) / 1024;
+        if ((rc = dalloc(c, &b.rrng_mask, (size_t)nmw)) || (rc = dalloc(c, &b.rrng_woff, (size_t)nmw)) ||
+            (rc = dalloc(c, &b.rrng_bsum, (size_t)nblk + 1)))
+            return bail(rc);
+        b.rrng_cap = L / 63 + 2;  // a round draws ceil(bits / 63), bits <= every literal
+        if ((rc = dalloc(c, &b.rrng_stream, (size_t)b.rrng_cap))) return bail(rc);
+    } else if (refrng) {
+        // (no clauses: the initial fill still draws; the mask pointer marks the mode)
+        if ((rc = dalloc(c, &b.rrng_mask, 1))) return bail(rc);
+    }
     // skewed instances (hot variables): owner slots and round-0 buckets by vmix (alll_internal.h)
     b.vmix_mul = 1u;
     b.vmix_mask = 0xFFFFFFFFu;
@@ -1574,6 +1601,7 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
     c->h_state->limit_eval = ~0ull;
     c->h_state->limit_nores = ~0ull;
     c->h_state->round_next = 1;
+    if (refrng) c->h_state->rd_state = opt.seed;  // (the random_device stand-in's state)
     if (hipMemcpyAsync(b.state, c->h_state, sizeof(DevState), hipMemcpyHostToDevice, c->stream) != hipSuccess)
         return bail(fail(ALLL_ERR_HIP, "state upload failed"));
     if (launch_init_assignment(b, c->stream) != hipSuccess)

@@ -61,6 +61,20 @@ typedef struct alll_problem {
 #define ALLL_FLAG_LFMIS             (1u << 6) /* n_threads > 1: keep the one-set MIS (the
                                                  lexicographically-first MIS in clause order, fast)
                                                  instead of the reference's T-set round robin */
+#define ALLL_FLAG_REFERENCE_RNG     (1u << 7) /* the reference's own random stream instead of Philox:
+                                                 RBG<default_random_engine> (RandomBoolGenerator.h,
+                                                 libstdc++ minstd_rand0 + uniform_int_distribution
+                                                 <unsigned long long>), every engine seeded with the
+                                                 next value of std::random_device, for which `seed`
+                                                 is the state of the 64-bit LCG stand-in of
+                                                 oracle/ref_probe.cpp (x = x*6364136223846793005 +
+                                                 1442695040888963407, value x >> 33): the initial
+                                                 fill (VariablesArray.h:23-34) and every resample
+                                                 round (SATInstance.h:340-365, T = 1) then equal the
+                                                 reference's, bit for bit.  One thread generates each
+                                                 round's draws (a verification mode, not the fast
+                                                 path).  n_threads = 1, no streaming, one GPU:
+                                                 ALLL_ERR_UNSUPPORTED otherwise */
 
 typedef struct alll_options {
     uint64_t seed;          /* Philox4x32-10 key; replaces std::random_device (SATInstance.h:346) */

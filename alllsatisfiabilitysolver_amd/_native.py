@@ -45,7 +45,7 @@ EXPORTED = [
     "alll_get_stats", "alll_verify", "alll_get_assignment", "alll_set_assignment",
     "alll_get_assignment_words", "alll_set_assignment_words", "alll_get_violated_mask",
     "alll_get_mis", "alll_bench_eval", "alll_profile", "alll_loop_times", "alll_synchronize", "alll_eval_bytes",
-    "alll_layout", "alll_eval_kernel", "alll_comm_size", "alll_uses_graphs", "alll_rr_pass_log", "alll_rr_barrier_timeouts", "alll_initial_assignment", "alll_shard_plan", "alll_plan_multi_gpu", "alll_dimacs_parse", "alll_dimacs_read", "alll_generate_ksat",
+    "alll_layout", "alll_eval_kernel", "alll_comm_size", "alll_uses_graphs", "alll_rr_pass_log", "alll_rr_barrier_timeouts", "alll_initial_assignment", "alll_reference_initial_assignment", "alll_shard_plan", "alll_plan_multi_gpu", "alll_dimacs_parse", "alll_dimacs_read", "alll_generate_ksat",
 ]
 
 
@@ -156,6 +156,7 @@ _SIGS = {
     "alll_rr_pass_log": ([_vp, _u32p, ctypes.c_uint32], ctypes.c_int),
     "alll_rr_barrier_timeouts": ([_vp], ctypes.c_int64),
     "alll_shard_plan": ([ctypes.c_uint64, ctypes.c_int, ctypes.c_int, _u64p, _u64p, _u64p], ctypes.c_int),
+    "alll_reference_initial_assignment": ([ctypes.c_uint64, ctypes.c_uint32, _u8p], ctypes.c_int),
     "alll_plan_multi_gpu": ([ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p],
                             ctypes.c_int),
     "alll_initial_assignment": ([ctypes.c_uint64, ctypes.c_uint32, _u8p], ctypes.c_int),

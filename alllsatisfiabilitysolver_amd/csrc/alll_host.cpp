@@ -418,9 +418,60 @@ uint32_t philox_x_host(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint3
     return c0;
 }
 
+// The reference's VariablesArray fill (VariablesArray.h:23-34) in the reference-RNG mode: the
+// same stream as k_rrng_init (alll_refrng.hip) -- the random_device stand-in's
+// next value seeds minstd_rand0, libstdc++'s uniform_int_distribution<unsigned long long> upscales
+// its values to 64 bits, RBG serves 63 bits of each, lowest first.
+struct RefRbg {
+    static constexpr uint64_t M = 2147483647ull, MIN = 1ull, RANGE = M - 1ull - MIN, UR = RANGE + 1ull;
+    static constexpr uint64_t Q1 = ~0ull / UR, Q2 = Q1 / UR, UE = Q2 + 1ull, SC = RANGE / UE, PAST = UE * SC;
+    uint64_t x;
+    uint64_t next() {
+        x = (x * 16807ull) % M;
+        return x;
+    }
+    uint64_t inner() {
+        uint64_t r;
+        do r = next() - MIN;
+        while (r >= PAST);
+        return r / SC;
+    }
+    uint64_t middle() {
+        uint64_t ret, tmp;
+        do {
+            tmp = UR * inner();
+            ret = tmp + (next() - MIN);
+        } while (ret > Q1 || ret < tmp);
+        return ret;
+    }
+    uint64_t draw() {
+        uint64_t ret, tmp;
+        do {
+            tmp = UR * middle();
+            ret = tmp + (next() - MIN);
+        } while (ret < tmp);
+        return ret;
+    }
+};
+
 }  // namespace
 
 extern "C" {
+
+int alll_reference_initial_assignment(uint64_t rd_state, uint32_t n_vars, uint8_t* out) {
+    if (!out && n_vars) return ALLL_ERR_INVALID_ARG;
+    rd_state = rd_state * 6364136223846793005ull + 1442695040888963407ull;
+    const uint32_t seed = (uint32_t)(rd_state >> 33);
+    RefRbg g{(uint64_t)seed % RefRbg::M};
+    if (!g.x) g.x = 1;
+    uint64_t m = 1;
+    for (uint32_t v = 0; v < n_vars; ++v) {
+        if (m == 1) m = g.draw() | (1ull << 63);
+        out[v] = (uint8_t)(m & 1u);
+        m >>= 1;
+    }
+    return ALLL_OK;
+}
 
 int alll_initial_assignment(uint64_t seed, uint32_t n_vars, uint8_t* out) {
     if (!out && n_vars) return ALLL_ERR_INVALID_ARG;

@@ -292,6 +292,12 @@ int alll_plan_multi_gpu(uint64_t n_clauses, uint64_t n_literals, uint32_t n_vars
  * VariablesArray (replaces the random_device fill of VariablesArray.h:23-34). */
 int alll_initial_assignment(uint64_t seed, uint32_t n_vars, uint8_t* out);
 
+/* The reference's own initial assignment (VariablesArray.h:23-34) in the reference-RNG mode
+ * (ALLL_FLAG_REFERENCE_RNG): `rd_state` is the random_device stand-in's state
+ * before the fill draws its one value; the bytes equal the device fill of a context created
+ * with that seed and the flag.  Used by the compatibility VariablesArray (env ALLL_REFERENCE_RNG). */
+int alll_reference_initial_assignment(uint64_t rd_state, uint32_t n_vars, uint8_t* out);
+
 /* Synthetic random k-SAT with k distinct variables per clause (kind 0 uniform, kind 1
  * power-law P(v) ~ (v+1)^-0.8); clauses [c_begin, c_end) of the instance, fixed width k. */
 int alll_generate_ksat(uint64_t gen_seed, uint32_t n_vars, uint64_t n_clauses, uint32_t k,

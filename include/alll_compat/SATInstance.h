@@ -138,6 +138,15 @@ class SATInstance {
         // ALLL_MIS=lfmis: keep the one-set MIS for n_threads > 1 (faster, a different valid MIS)
         if (const char* e = std::getenv("ALLL_MIS"))
             if (std::string(e) == "lfmis") o.flags |= ALLL_FLAG_LFMIS;
+        // ALLL_REFERENCE_RNG=<state>: the reference's own random stream; the
+        // context's fill draws the same first value as VariablesArray did, so the resample rounds
+        // take the stand-in's next values, as the reference's do (one VariablesArray and one solve
+        // per process, as in example/main.cpp)
+        if (const char* e = std::getenv("ALLL_REFERENCE_RNG"))
+            if (*e) {
+                o.flags |= ALLL_FLAG_REFERENCE_RNG;
+                o.seed = alll_compat::env_u64("ALLL_REFERENCE_RNG", 0);
+            }
         alll_ctx* ctx = nullptr;
         check(alll_create(&p, &o, &ctx));
         vector<uint8_t> a(n_vars > 0 ? n_vars : 1);

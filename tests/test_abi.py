@@ -65,6 +65,19 @@ def test_multi_gpu_plan(native):
     assert native.lib().alll_plan_multi_gpu(1, 3, 1, 0, None) != 0  # bad arguments
 
 
+@pytest.mark.parametrize("name", ["c1_3sat_200_800_T1", "u3sat_2500_10000_T1", "k8_4000_6000_T1", "edge_T1"])
+def test_reference_initial_assignment_matches_reference(native, name):
+    """alll_reference_initial_assignment (the compatibility VariablesArray under
+    ALLL_REFERENCE_RNG): the reference's own VariablesArray fill recorded by its trace (rd_seed 7)."""
+    f = dict(np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False))
+    n = int(f["n_vars"])
+    rd = json.load(open(os.path.join(GOLDEN, "manifest.json")))["rd_seed"]
+    out = np.zeros(n, np.uint8)
+    assert native.lib().alll_reference_initial_assignment(rd, n, out.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))) == 0
+    want = np.array([(int(f["A"][0][v >> 5]) >> (v & 31)) & 1 for v in range(n)], np.uint8)
+    np.testing.assert_array_equal(out, want)
+
+
 def test_create_fails_loudly_without_gpu(native):
     from alllsatisfiabilitysolver_amd import Solver, AlllError
 

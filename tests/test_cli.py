@@ -65,6 +65,32 @@ def test_cli_solves_and_matches_oracle(oracle_mod, native, tmp_path, threads):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("name", ["r2_3sat_200_400_T1", "k8_4000_6000_T1", "edge_T1"])
+def test_cli_reproduces_reference_run(oracle_mod, native, tmp_path, name):
+    """--reference-rng (ALLL_REFERENCE_RNG through the compatibility headers): the
+    CLI's whole run equals the reference's own SATInstance::solve() with the same random_device
+    stand-in state (ref_probe `solve`, recorded in the fixture): statistics and final assignment."""
+    from conftest import GOLDEN
+
+    f = dict(np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False))
+    n, offs, lits = int(f["n_vars"]), f["offs"], f["lits"]
+    rd = json.load(open(os.path.join(GOLDEN, "manifest.json")))["rd_seed"]
+    it, res, avg, valid = (int(x) for x in f["solve_stats"])
+    path = tmp_path / "inst.cnf"
+    path.write_text(oracle_mod.to_dimacs(n, offs, lits, comments=["reference run"]))
+    r = subprocess.run([CLI, "-o", "-p", "1", "--reference-rng", str(rd), "--sat", str(path)],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == (0 if valid else 1), r.stdout + r.stderr
+    out = r.stdout
+    assert f"# Iterations\t= {it}" in out
+    assert f"# Resamples\t= {res}" in out
+    assert f"Avg. UNSAT MIS Size = {avg}" in out
+    dump = (tmp_path / "inst.out").read_text()
+    vals = [int(line.split("= ")[1]) for line in dump.splitlines() if line.startswith("Variable ")]
+    np.testing.assert_array_equal(np.array(vals, np.uint8), oracle_mod.unpack_words(f["solve_A"], n))
+
+
+@pytest.mark.gpu
 def test_cli_unsolvable_cap_exit_code(native, tmp_path):
     path = tmp_path / "u.cnf"
     path.write_text("p cnf 2 4\n1 2 0\n1 -2 0\n-1 2 0\n-1 -2 0\n")  # UNSAT

@@ -1,7 +1,7 @@
 // alll_main.cpp -- command-line driver with the flags and output of the reference's
 // example/main.cpp (-h, -o, -p N, --sat PATH; main.cpp:48-93) without Boost, over the
 // compatibility SATInstance API (include/alll_compat) and the MI355X solver.
-// Additive flags: --seed S, --max-iters K, --device D.
+// Additive flags: --seed S, --max-iters K, --device D, --reference-rng STATE.
 //
 // Output parity with main.cpp: the INFORMATION block (n_clauses printed before solve, so 0:
 // main.cpp:192-194), STATISTICS with one line per thread (:236-247), SATISFIABLE / ERROR
@@ -42,6 +42,7 @@ static void usage() {
             "  -p [ --parallel ] arg (=0) Use parallel solver\n"
             "  --sat arg                 Path to SAT instance in DIMACS-CNF format\n"
             "  --seed arg (=1)           Philox seed (MI355X solver)\n"
+            "  --reference-rng arg       the reference's own random stream, random_device stand-in state (MI355X solver)\n"
             "  --max-iters arg (=0)      Cap on eval passes, 0 = unlimited (MI355X solver)\n"
             "  --device arg (=-1)        HIP device (MI355X solver)\n";
 }
@@ -69,6 +70,7 @@ int main(int argc, char* argv[]) {
             else n_threads = 1;
         } else if (a == "--sat") cnf_fpath = need("--sat");
         else if (a == "--seed") setenv("ALLL_SEED", need("--seed").c_str(), 1);
+        else if (a == "--reference-rng") setenv("ALLL_REFERENCE_RNG", need("--reference-rng").c_str(), 1);
         else if (a == "--max-iters") setenv("ALLL_MAX_ITERS", need("--max-iters").c_str(), 1);
         else if (a == "--device") setenv("ALLL_DEVICE", need("--device").c_str(), 1);
         else { cerr << "unrecognised option '" << a << "'" << endl; return 1; }

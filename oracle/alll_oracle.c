@@ -10,9 +10,12 @@
  * Parity pinning: every deterministic function here (eval, LFMIS, round-robin
  * MIS, chunking, statistics arithmetic, DIMACS semantics) is checked against
  * golden vectors produced by the reference's own code (oracle/ref_probe.cpp
- * compiled from /root/reference sources, fixtures in tests/golden/).  The RNG is
- * not pinned: the reference draws from std::random_device, so the build replaces
- * it with Philox4x32-10 (pinned against the Random123 known-answer vectors).
+ * compiled from /root/reference sources, fixtures in tests/golden/).  The product
+ * RNG is Philox4x32-10 (pinned against the Random123 known-answer vectors) in place
+ * of std::random_device; the reference's own stream (RBG over libstdc++'s
+ * minstd_rand0 and uniform_int_distribution, engines seeded from the probe's
+ * random_device stand-in) is restated too (orc_solve_refrng) and pinned to the
+ * reference's recorded T = 1 trajectories.
  *
  * Citations are to files under the reference repository.
  */

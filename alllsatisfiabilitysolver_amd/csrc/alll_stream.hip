@@ -275,6 +275,34 @@ __device__ __forceinline__ void srr_cover_test(const ClauseView& cv, const LoopB
     }
 }
 
+// the first sequence position recorded for variable v, or SRR_NONE
+__device__ __forceinline__ uint32_t srr_hget(const uint32_t* key, const uint32_t* pos, uint32_t v) {
+    uint32_t h = srr_hslot(v);
+    for (;;) {
+        const uint32_t k = key[h];
+        if (k == v) return pos[h];
+        if (k == SRR_NONE) return SRR_NONE;
+        h = (h + 1) & (SRR_HASH - 1);
+    }
+}
+
+// workgroup exclusive scan of one value per thread (SRR_THREADS)
+__device__ __forceinline__ uint32_t srr_block_excl(uint32_t x, uint32_t* s_w) {
+    const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    uint32_t incl = x;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(incl, o, 64);
+        if ((int)lane >= o) incl += y;
+    }
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    uint32_t before = 0;
+    for (uint32_t w = 0; w < wave; ++w) before += s_w[w];
+    __syncthreads();
+    return before + incl - x;
+}
+
 __device__ __forceinline__ uint32_t srr_wave_min(uint32_t x) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) x = min(x, (uint32_t)__shfl_xor((int)x, o, 64));
@@ -315,6 +343,8 @@ __global__ __launch_bounds__(SRR_THREADS) void k_srr_mis(ClauseView cv, LoopBuff
     __shared__ uint32_t s_gcur[SRR_WAVES], s_gcnt[SRR_WAVES], s_gst[SRR_WAVES];
     __shared__ uint32_t s_wc[SRR_WAVES], s_wwide[SRR_WAVES];
     __shared__ uint32_t s_red[4], s_wide, s_tot[2];  // (s_red: {E, q*} by segment parity)
+    __shared__ uint32_t s_slotset[SRR_CAND], s_rank[SRR_CAND], s_kc[SRR_CAND];  // (compaction)
+    __shared__ uint32_t s_scan[SRR_WAVES];
     __shared__ unsigned long long s_lits;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const unsigned long long lt_mask = (1ull << lane) - 1ull;
@@ -329,7 +359,7 @@ __global__ __launch_bounds__(SRR_THREADS) void k_srr_mis(ClauseView cv, LoopBuff
     unsigned long long weighted = 0, lits = 0;
 #ifdef SRR_PROFILE  // (development: phase clocks of thread 0, printed at the end)
     unsigned long long p_t0 = __builtin_amdgcn_s_memrealtime(), p_g = 0, p_x;
-    uint32_t p_segs = 0, p_conf = 0, p_wit = 0;
+    uint32_t p_segs = 0, p_conf = 0, p_wit = 0, p_cmp = 0;
     unsigned long long p_a = 0, p_b = 0, p_y, p_ph[5] = {0, 0, 0, 0, 0}, p_z;
 #define SRR_PH(k) { const unsigned long long z_ = __builtin_amdgcn_s_memrealtime(); p_ph[k] += z_ - p_z; p_z = z_; }
 #else
@@ -369,6 +399,7 @@ __global__ __launch_bounds__(SRR_THREADS) void k_srr_mis(ClauseView cv, LoopBuff
                 s_base[g] = d * K;
                 s_cnt[g] = 0;
                 s_use[seg & 1][g] = 0;
+                if (d < nsl) s_slotset[d] = g;
             }
             for (uint32_t h = tid; h < SRR_HASH; h += SRR_THREADS) { s_hkey[h] = SRR_NONE; s_hpos[h] = SRR_NONE; }
             if (tid == 0) s_wide = 0;
@@ -552,7 +583,57 @@ __global__ __launch_bounds__(SRR_THREADS) void k_srr_mis(ClauseView cv, LoopBuff
                 p_conf += A < E;
 #endif
                 if (A > 0) tt = (ts + A - 1) % sz;
-                if (A < E) break;  // a covered candidate: new gather
+                if (A < E) {
+                    // a covered candidate (the turn at q* re-runs): instead of a new gather, the
+                    // sets' unconsumed candidates minus those an accepted pick of this cycle covers
+                    // (a variable with a position below qb in the hash) become their lists, and the
+                    // hash starts afresh.  Every candidate left was uncovered at the gather and
+                    // shares nothing with the picks since; the candidate at q* is dropped.
+                    if (s_wide) break;  // (a wide first candidate's cycle: new gather)
+                    uint32_t* use2 = s_use[seg & 1];
+                    const uint32_t ns = nsl * K;
+                    bool keep = false;
+                    uint32_t d = 0, kent = 0, kid = 0, kw = 0, kv[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+                    if (tid < ns) {
+                        d = tid / K;
+                        const uint32_t r = tid - d * K, g = s_slotset[d];
+                        if (r >= use2[g] && r < (s_cnt[g] & ~SRR_COMPLETE)) {
+                            kent = s_cent[tid];
+                            kid = s_cid[tid];
+                            kw = s_cw[tid];
+#pragma unroll
+                            for (int q = 0; q < 8; ++q) kv[q] = s_cv[tid * 8 + q];
+                            keep = true;
+                            for (uint32_t q = 0; q < kw && q < 8; ++q) keep &= srr_hget(s_hkey, s_hpos, kv[q]) >= qb;
+                        }
+                    }
+                    if (tid < nsl) s_kc[tid] = 0;
+                    const uint32_t ex = srr_block_excl(keep ? 1u : 0u, s_scan);
+                    if (tid < ns) s_rank[tid] = ex;
+                    __syncthreads();
+                    if (keep) {
+                        const uint32_t slot = d * K + (ex - s_rank[d * K]);
+                        s_cent[slot] = kent;
+                        s_cid[slot] = kid;
+                        s_cw[slot] = kw;
+#pragma unroll
+                        for (int q = 0; q < 8; ++q) s_cv[slot * 8 + q] = kv[q];
+                        atomicAdd(&s_kc[d], 1u);
+                    }
+                    for (uint32_t hh = tid; hh < SRR_HASH; hh += SRR_THREADS) { s_hkey[hh] = SRR_NONE; s_hpos[hh] = SRR_NONE; }
+                    __syncthreads();
+                    if (tid < nsl) {
+                        const uint32_t g = s_slotset[tid];
+                        s_cnt[g] = s_kc[tid] | (s_cnt[g] & SRR_COMPLETE);
+                        use2[g] = 0;
+                    }
+                    __syncthreads();
+                    qb = 0;
+#ifdef SRR_PROFILE
+                    ++p_cmp;
+#endif
+                    continue;
+                }
                 const uint32_t te = (tt + 1) % sz, ge = s_live[te];
                 if (!(s_cnt[ge] & SRR_COMPLETE)) break;  // out of gathered candidates: new gather
                 // the set has no uncovered entry left: erase live[te]
@@ -574,8 +655,8 @@ __global__ __launch_bounds__(SRR_THREADS) void k_srr_mis(ClauseView cv, LoopBuff
     }
 #ifdef SRR_PROFILE
     if (tid == 0)
-        printf("srr_prof T %u steps %llu picks %u gathers %u window_iters %u segs %u conflicts %u ticks total %llu gather %llu reset %llu firstbar %llu seg E %llu ins %llu det %llu com %llu erase %llu\n",
-               T, (unsigned long long)pl.steps, nm, all_gathers, p_wit, p_segs, p_conf,
+        printf("srr_prof T %u steps %llu picks %u gathers %u window_iters %u segs %u conflicts %u compactions %u ticks total %llu gather %llu reset %llu firstbar %llu seg E %llu ins %llu det %llu com %llu erase %llu\n",
+               T, (unsigned long long)pl.steps, nm, all_gathers, p_wit, p_segs, p_conf, p_cmp,
                __builtin_amdgcn_s_memrealtime() - p_t0, p_g, p_a, p_b, p_ph[0], p_ph[1], p_ph[2], p_ph[3], p_ph[4]);
 #endif
     weighted += (unsigned long long)nm * pl.extra;

@@ -356,6 +356,7 @@ struct LoopBuffers {
     uint32_t* rrng_woff;             // per mask word: its clauses' literal count, then their bit offset in the block
     uint32_t* rrng_bsum;             // per 1024-word block: bit total, then the block's bit offset
     unsigned long long* rrng_stream; // the round's RBG draws (63 bits each)
+    uint32_t* rrng_map;              // streaming solve: pick position -> clause id (the mask is by position)
     uint64_t rrng_cap;               // draws rrng_stream holds
     uint32_t n_vars;
     uint32_t n_words;

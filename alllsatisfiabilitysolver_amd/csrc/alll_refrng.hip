@@ -9,13 +9,14 @@
 // every level redrawn when it overflows its range.  Each engine is seeded with one
 // std::random_device value: one for the initial fill (VariablesArray.h:23-34), one per resample
 // round with T = 1 (SATInstance.h:340-365), whose bits go to the MIS clauses' literals in pick
-// order -- ascending clause index for the one-set MIS.  random_device is replaced by the 64-bit
+// order -- ascending clause index for the one-set MIS, yield order in the streaming solve.  random_device is replaced by the 64-bit
 // LCG of oracle/ref_probe.cpp, so a run here equals the reference run the probe records, bit for
 // bit (oracle: orc_solve_refrng; tests/test_gpu_refrng.py).
 //
 // Per resample round:
-//   k_rrng_mark   the MIS (per-tile lists and the tail's list) as a clause-order bitmask, and per
-//                 64-clause word the literal count of its MIS clauses;
+//   k_rrng_mark   the MIS (per-tile lists and the tail's list) as a bitmask in pick order (clause
+//                 index; streaming: window offset, with the clause of every position), and per
+//                 64-position word the literal count of its MIS clauses;
 //   k_rrng_scan1  per 1024-word block: exclusive offsets of the words, the block total;
 //   k_rrng_scan2  one workgroup: the blocks' offsets, the round's bit count, and -- one thread, the
 //                 draws are a sequential chain of engine values with data-dependent rejections --
@@ -117,6 +118,17 @@ __global__ void k_rrng_init(LoopBuffers b) {
     }
 }
 
+// Pick position of MIS clause c: its clause index, or in the streaming solve its offset in the
+// iteration's window of generator steps (the LFMIS key - 1, alll_kernels.hip prio(): the clause
+// generator yields clause j*P mod m at step j, ClauseGenerator.h:47)
+__device__ __forceinline__ uint32_t pick_pos(const LoopBuffers& b, const DevState* st, uint32_t c) {
+    if (!b.stream_batch) return c;
+    const uint64_t m = b.m;
+    uint64_t pos = ((uint64_t)c * b.stream_pinv) % m;
+    if (pos == 0) pos = m;
+    return (uint32_t)((pos - 1 + m - st->win_start % m) % m);
+}
+
 __global__ __launch_bounds__(256) void k_rrng_mark(ClauseView cv, LoopBuffers b) {
     const DevState* st = b.state;
     if (!st->active) return;
@@ -124,9 +136,10 @@ __global__ __launch_bounds__(256) void k_rrng_mark(ClauseView cv, LoopBuffers b)
     const uint32_t* list = t < b.n_tiles ? b.mis + (uint64_t)t * TILE : b.tmis;
     const uint32_t cnt = t < b.n_tiles ? b.mis_cnt[t] : st->tmis_cnt;
     for (uint32_t i = threadIdx.x; i < cnt; i += blockDim.x) {
-        const uint32_t c = list[i];
-        atomicOr(&b.rrng_mask[c >> 6], 1ull << (c & 63));
-        atomicAdd(&b.rrng_woff[c >> 6], clause_len(cv, c));
+        const uint32_t c = list[i], p = pick_pos(b, st, c);
+        atomicOr(&b.rrng_mask[p >> 6], 1ull << (p & 63));
+        atomicAdd(&b.rrng_woff[p >> 6], clause_len(cv, c));
+        if (b.rrng_map) b.rrng_map[p] = c;
     }
 }
 
@@ -208,7 +221,8 @@ __global__ __launch_bounds__(RRNG_BLOCK) void k_rrng_apply(ClauseView cv, LoopBu
     b.rrng_woff[w] = 0u;  // (every word: the scan wrote them all; for the next round)
     if (!bits) return;
     while (bits) {
-        const uint32_t c = 64u * w + (uint32_t)__builtin_ctzll(bits);
+        const uint32_t p = 64u * w + (uint32_t)__builtin_ctzll(bits);
+        const uint32_t c = b.rrng_map ? b.rrng_map[p] : p;  // (the clause picked p-th)
         bits &= bits - 1ull;
         const uint64_t lb = clause_start(cv, c);
         const uint32_t len = clause_len(cv, c);

@@ -951,7 +951,7 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
         if (opt.n_threads > 1)
             return fail(ALLL_ERR_UNSUPPORTED, "reference-RNG mode: n_threads must be 1 (the reference's T > 1 "
                                               "resample draws from T engines in a schedule(dynamic) loop)");
-        if (opt.stream_batch) return fail(ALLL_ERR_UNSUPPORTED, "reference-RNG mode: not with the streaming solve");
+
         if (opt.world > 1 || !zid || (opt.flags & ALLL_FLAG_EXCHANGE_ALLREDUCE))
             return fail(ALLL_ERR_UNSUPPORTED, "reference-RNG mode runs on one GPU without the exchange path");
     }
@@ -1249,6 +1249,7 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
             return bail(rc);
         b.rrng_cap = L / 63 + 2;  // a round draws ceil(bits / 63), bits <= every literal
         if ((rc = dalloc(c, &b.rrng_stream, (size_t)b.rrng_cap))) return bail(rc);
+        if (opt.stream_batch && (rc = dalloc(c, &b.rrng_map, (size_t)m))) return bail(rc);
     } else if (refrng) {
         // (no clauses: the initial fill still draws; the mask pointer marks the mode)
         if ((rc = dalloc(c, &b.rrng_mask, 1))) return bail(rc);

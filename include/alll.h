@@ -73,7 +73,8 @@ typedef struct alll_problem {
                                                  round (SATInstance.h:340-365, T = 1) then equal the
                                                  reference's, bit for bit.  One thread generates each
                                                  round's draws (a verification mode, not the fast
-                                                 path).  n_threads = 1, no streaming, one GPU:
+                                                 path).  n_threads = 1 (also for the streaming
+                                                 solve: bits in yield order), one GPU:
                                                  ALLL_ERR_UNSUPPORTED otherwise */
 
 typedef struct alll_options {

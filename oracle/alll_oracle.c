@@ -418,9 +418,11 @@ void orc_stream_order(uint64_t m, uint32_t* order) {
     }
 }
 
-int orc_solve_stream(uint32_t n_vars, uint64_t m, const uint64_t* offs, const uint32_t* lits, uint64_t seed,
-                     uint64_t max_iters, uint64_t batch, uint32_t* A, orc_stats* st, orc_iter_cb cb,
-                     void* cb_user) {
+/* rd_state != NULL: the reference-RNG mode (a fresh RBG per iteration, seeded by the next
+ * random_device value; bits in pick order, SATInstance.h:340-365 with T = 1) */
+static int stream_impl(uint32_t n_vars, uint64_t m, const uint64_t* offs, const uint32_t* lits, uint64_t seed,
+                       uint64_t max_iters, uint64_t batch, uint32_t* A, orc_stats* st, orc_iter_cb cb,
+                       void* cb_user, uint64_t* rd_state) {
     uint32_t* M = (uint32_t*)malloc(sizeof(uint32_t) * (m ? m : 1));
     uint8_t* used = (uint8_t*)calloc(n_vars ? n_vars : 1, 1);
     uint64_t nw = (m + 63) / 64;
@@ -449,11 +451,13 @@ int orc_solve_stream(uint32_t n_vars, uint64_t m, const uint64_t* offs, const ui
         }
         uint64_t dres = 0;
         const uint64_t iter = st->n_iterations - 1;
+        orc_rbg g;
+        if (rd_state) orc_rbg_seed(&g, orc_refrng_rd_next(rd_state));
         for (uint64_t i = 0; i < nm; ++i) {
             const uint32_t cl = M[i];
             for (uint64_t j = offs[cl]; j < offs[cl + 1]; ++j) {
                 const uint32_t v = lits[j] >> 1;
-                const uint32_t b = orc_resample_bit(seed, iter, v);
+                const uint32_t b = rd_state ? orc_rbg_sample(&g) : orc_resample_bit(seed, iter, v);
                 A[v >> 5] = (A[v >> 5] & ~(1u << (v & 31))) | (b << (v & 31));
                 used[v] = 0;
             }
@@ -473,6 +477,22 @@ int orc_solve_stream(uint32_t n_vars, uint64_t m, const uint64_t* offs, const ui
     st->solved = solved;
     free(M); free(used); free(vmask);
     return solved ? 0 : 1;
+}
+
+int orc_solve_stream(uint32_t n_vars, uint64_t m, const uint64_t* offs, const uint32_t* lits, uint64_t seed,
+                     uint64_t max_iters, uint64_t batch, uint32_t* A, orc_stats* st, orc_iter_cb cb,
+                     void* cb_user) {
+    return stream_impl(n_vars, m, offs, lits, seed, max_iters, batch, A, st, cb, cb_user, NULL);
+}
+
+/* orc_solve_stream in the reference-RNG mode: A initialised here from the random_device stand-in
+ * seeded with rd_seed, every iteration's resample from the stand-in's next value */
+int orc_solve_stream_refrng(uint32_t n_vars, uint64_t m, const uint64_t* offs, const uint32_t* lits,
+                            uint64_t rd_seed, uint64_t max_iters, uint64_t batch, uint32_t* A, orc_stats* st,
+                            orc_iter_cb cb, void* cb_user) {
+    uint64_t rd = rd_seed;
+    orc_refrng_init(&rd, n_vars, A);
+    return stream_impl(n_vars, m, offs, lits, 0, max_iters, batch, A, st, cb, cb_user, &rd);
 }
 
 /* ------------------------------------------------------------------------- */

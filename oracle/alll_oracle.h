@@ -44,6 +44,9 @@ void orc_refrng_init(uint64_t* rd_state, uint32_t n_vars, uint32_t* A);
 int orc_solve_refrng(uint32_t n_vars, uint64_t m, const uint64_t* offs, const uint32_t* lits,
                      uint64_t rd_seed, uint64_t max_iters, uint32_t* A, orc_stats* st,
                      orc_iter_cb cb, void* cb_user);
+int orc_solve_stream_refrng(uint32_t n_vars, uint64_t m, const uint64_t* offs, const uint32_t* lits,
+                            uint64_t rd_seed, uint64_t max_iters, uint64_t batch, uint32_t* A, orc_stats* st,
+                            orc_iter_cb cb, void* cb_user);
 int orc_solve(uint32_t n_vars, uint64_t m, const uint64_t* offs, const uint32_t* lits, uint64_t seed,
               uint64_t max_iters, uint32_t* A, orc_stats* st, orc_iter_cb cb, void* cb_user);
 int orc_solve_rr(uint32_t n_vars, uint64_t m, const uint64_t* offs, const uint32_t* lits, uint64_t seed,

@@ -89,6 +89,10 @@ def lib():
         L.orc_solve_refrng.argtypes = [ctypes.c_uint32, ctypes.c_uint64, _u64p, _u32p, ctypes.c_uint64,
                                        ctypes.c_uint64, _u32p, ctypes.POINTER(OrcStats), ITER_CB, ctypes.c_void_p]
         L.orc_solve_refrng.restype = ctypes.c_int
+        L.orc_solve_stream_refrng.argtypes = [ctypes.c_uint32, ctypes.c_uint64, _u64p, _u32p, ctypes.c_uint64,
+                                              ctypes.c_uint64, ctypes.c_uint64, _u32p, ctypes.POINTER(OrcStats),
+                                              ITER_CB, ctypes.c_void_p]
+        L.orc_solve_stream_refrng.restype = ctypes.c_int
         L.orc_refrng_init.argtypes = [_u64p, ctypes.c_uint32, _u32p]
         L.orc_refrng_init.restype = None
         L.orc_dimacs_parse.argtypes = [ctypes.c_char_p, ctypes.c_uint64, _u32p, _u64p, _u64p,
@@ -348,6 +352,26 @@ def solve_refrng(n_vars, offs, lits, rd_seed, max_iters=0, trace=False):
     cbf = ITER_CB(cb)
     lib().orc_solve_refrng(n_vars, m, _p(offs, _u64p), _p(lits, _u32p), rd_seed, max_iters, _p(A, _u32p),
                            ctypes.byref(st), cbf, None)
+    stats = {k: int(getattr(st, k)) for k, _ in OrcStats._fields_ if k != "pad"}
+    return stats, A, rows
+
+
+def solve_stream_refrng(n_vars, offs, lits, rd_seed, batch, max_iters=0, trace=False):
+    """orc_solve_stream in the reference-RNG mode (one thread).  Returns (stats dict, final A
+    words, per-iteration rows (it, |U|, |M|, dres, A after))."""
+    m = len(offs) - 1
+    A = np.zeros(max(1, (n_vars + 31) // 32), np.uint32)
+    st = OrcStats()
+    rows = []
+
+    def cb(user, it, nu, nm, dres, Ap):
+        if trace:
+            rows.append((int(it), int(nu), int(nm), int(dres),
+                         np.ctypeslib.as_array(Ap, shape=(A.size,)).copy()))
+
+    cbf = ITER_CB(cb)
+    lib().orc_solve_stream_refrng(n_vars, m, _p(offs, _u64p), _p(lits, _u32p), rd_seed, max_iters, batch,
+                                  _p(A, _u32p), ctypes.byref(st), cbf, None)
     stats = {k: int(getattr(st, k)) for k, _ in OrcStats._fields_ if k != "pad"}
     return stats, A, rows
 

@@ -118,11 +118,53 @@ def test_reference_rng_matches_oracle(gpu, native, oracle_mod, name):
             assert st[key] == st_o[key], key
 
 
+STREAM_FIXTURES = sorted(glob.glob(os.path.join(GOLDEN, "stream_*.npz")))
+
+
+@pytest.mark.parametrize("path", STREAM_FIXTURES, ids=lambda p: os.path.basename(p)[:-4])
+def test_reference_stream_trajectory_on_gpu(gpu, native, path):
+    """The streaming overload (one thread) with the reference's own stream: the reference's runs
+    (ref_probe `stream`, rd_seed 7) -- every iteration's assignment, the statistics, and the real
+    solve(getEnumeratedClause, ...)'s final assignment and statistics."""
+    from alllsatisfiabilitysolver_amd import Solver
+
+    f = load(path)
+    n, offs, lits, bs = int(f["n_vars"]), f["offs"], f["lits"], int(f["batch"])
+    its = f["A"].shape[0]
+    with Solver(n, offs, lits, seed=RD_SEED, flags=native.FLAG_REFERENCE_RNG, stream_batch=bs) as s:
+        np.testing.assert_array_equal(s.assignment_words(), f["A"][0], err_msg="initial fill")
+        for i in range(its - 1):
+            s.run(1)
+            np.testing.assert_array_equal(s.assignment_words(), f["A"][i + 1], err_msg=f"A after iteration {i + 1}")
+    with Solver(n, offs, lits, seed=RD_SEED, flags=native.FLAG_REFERENCE_RNG, stream_batch=bs) as s:
+        st = s.solve()
+        np.testing.assert_array_equal(s.assignment_words(), f["solve_A"])
+        assert [st["n_iterations"], st["n_resamples"], st["avg_mis_size"]] == [int(x) for x in f["solve_stats"]]
+
+
+@pytest.mark.parametrize("bs", [1000, 40000])
+def test_reference_rng_stream_matches_oracle(gpu, native, oracle_mod, bs):
+    from alllsatisfiabilitysolver_amd import Solver, generate_ksat
+
+    n, m, rd = 20000, 80000, 21
+    offs, lits = generate_ksat(1, n, m, 3, 0)
+    st_o, A_o, rows = oracle_mod.solve_stream_refrng(n, offs, lits, rd, bs, max_iters=12, trace=True)
+    with Solver(n, offs, lits, seed=rd, flags=native.FLAG_REFERENCE_RNG, stream_batch=bs) as s:
+        for it, nu, nm, dres, A_after in rows:
+            s.run(1)
+            np.testing.assert_array_equal(s.assignment_words(), A_after, err_msg=f"A after iteration {it}")
+    with Solver(n, offs, lits, seed=rd, flags=native.FLAG_REFERENCE_RNG, stream_batch=bs, max_iters=12) as s:
+        st = s.solve()
+        np.testing.assert_array_equal(s.assignment_words(), A_o)
+        for key in ("n_iterations", "n_resamples", "avg_mis_size", "solved"):
+            assert st[key] == st_o[key], key
+
+
 def test_reference_rng_refusals(gpu, native):
     from alllsatisfiabilitysolver_amd import AlllError, Solver, generate_ksat
 
     offs, lits = generate_ksat(1, 200, 800, 3, 0)
-    for kw in (dict(n_threads=2), dict(stream_batch=64)):
+    for kw in (dict(n_threads=2), dict(n_threads=2, stream_batch=64)):
         with pytest.raises(AlllError) as ei:
             Solver(200, offs, lits, seed=1, flags=native.FLAG_REFERENCE_RNG, **kw)
         assert ei.value.code == native.ALLL_ERR_UNSUPPORTED, kw

@@ -506,3 +506,22 @@ def test_oracle_reference_rng_reproduces_reference_trajectory(path, oracle_mod):
         assert rows[i][3] == int(f["dres"][i])
     np.testing.assert_array_equal(A, f["A_final"])
     assert [st["n_iterations"], st["n_resamples"], st["avg_mis_size"]] == [int(x) for x in f["stats"]]
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "stream_*.npz"))),
+                         ids=lambda p: os.path.basename(p)[:-4])
+def test_oracle_reference_rng_reproduces_reference_stream(path, oracle_mod):
+    """The streaming overload (one thread) in the reference-RNG mode (orc_solve_stream_refrng)
+    reproduces the reference's streaming runs (ref_probe `stream`, rd_seed 7): every iteration's
+    assignment, the statistics, and the real solve(getEnumeratedClause, ...)'s result."""
+    o = oracle_mod
+    f = load(path)
+    n, offs, lits, bs = int(f["n_vars"]), f["offs"], f["lits"], int(f["batch"])
+    rd = json.load(open(os.path.join(GOLDEN, "manifest.json")))["rd_seed"]
+    its = f["A"].shape[0]
+    st, A, rows = o.solve_stream_refrng(n, offs, lits, rd, bs, max_iters=its + 5, trace=True)
+    assert len(rows) >= its - 1
+    for i in range(its - 1):
+        np.testing.assert_array_equal(rows[i][4], f["A"][i + 1], err_msg=f"A after iteration {i + 1}")
+    np.testing.assert_array_equal(A, f["solve_A"])
+    assert [st["n_iterations"], st["n_resamples"], st["avg_mis_size"]] == [int(x) for x in f["solve_stats"]]

@@ -177,6 +177,11 @@ struct DevState {
     uint64_t win_len;      // streaming solve: steps (clauses yielded) in this iteration
     uint64_t rd_state;     // reference-RNG mode: state of the random_device stand-in (alll_refrng.hip)
     uint64_t rd_bits;      // reference-RNG mode: bits the current resample round draws
+    uint64_t rd_x0;        // reference-RNG mode: the round's engine state after seeding
+    uint32_t rd_draws;     // reference-RNG mode: the round's draws
+    uint32_t rd_n;         // reference-RNG mode: engine positions the parallel draws consider
+    uint32_t rd_fail;      // reference-RNG mode: the parallel draws ran past rd_n (sequential redo)
+    uint32_t rd_pad;
 };
 
 // Clause storage on the device.
@@ -358,6 +363,10 @@ struct LoopBuffers {
     unsigned long long* rrng_stream; // the round's RBG draws (63 bits each)
     uint32_t* rrng_map;              // streaming solve: pick position -> clause id (the mask is by position)
     uint64_t rrng_cap;               // draws rrng_stream holds
+    uint32_t* rrng_jump;             // rrng_levels x (rrng_nmax + 2): successor draw start, 2^t draws on
+    unsigned long long* rrng_val;    // rrng_nmax + 2: the draw a start at each engine position yields
+    uint32_t rrng_nmax;              // engine positions the parallel draws can consider
+    uint32_t rrng_levels;            // jump levels: 2^levels > rrng_cap
     uint32_t n_vars;
     uint32_t n_words;
     uint32_t n_tiles;       // tiles covering [0, m)
@@ -412,6 +421,7 @@ hipError_t fp_repair_occupancy(const ClauseView& cv, const LoopBuffers& b, int* 
 // reference-RNG mode (alll_refrng.hip): the initial fill and the resample round
 hipError_t launch_refrng_init(const LoopBuffers& b, hipStream_t s);
 hipError_t launch_refrng_resample(const ClauseView& cv, const LoopBuffers& b, hipStream_t s);
+constexpr uint32_t RRNG_POS_PER_DRAW = 4;  // engine positions per draw the parallel draws allow (3.5 on average)
 hipError_t launch_srr_first(const LoopBuffers& b, hipStream_t s);
 hipError_t launch_srr_lists(const ClauseView& cv, const LoopBuffers& b, uint32_t nblk, hipStream_t s);
 hipError_t launch_srr_mis(const ClauseView& cv, const LoopBuffers& b, hipStream_t s);

@@ -18,9 +18,9 @@
 //                 index; streaming: window offset, with the clause of every position), and per
 //                 64-position word the literal count of its MIS clauses;
 //   k_rrng_scan1  per 1024-word block: exclusive offsets of the words, the block total;
-//   k_rrng_scan2  one workgroup: the blocks' offsets, the round's bit count, and -- one thread, the
-//                 draws are a sequential chain of engine values with data-dependent rejections --
-//                 the round's ceil(bits / 63) RBG draws;
+//   k_rrng_scan2  one workgroup: the blocks' offsets, the round's bit count, the engine's seed;
+//   k_rrng_pos / k_rrng_lift / k_rrng_collect
+//                 the round's ceil(bits / 63) RBG draws in parallel (below);
 //   k_rrng_apply  a thread per mask word: its MIS clauses in order, each literal's variable set to
 //                 the next bit (a repeated variable keeps the last, as in the reference).
 // Integer work, latency bound: no MFMA.
@@ -81,6 +81,45 @@ __device__ __forceinline__ uint64_t uid_u64(uint64_t& x) {
         tmp = UR * uid_middle(x);
         ret = tmp + (ms_next(x) - MS_MIN);
     } while (ret < tmp);  // (ret > 2^64 - 1 cannot happen)
+    return ret;
+}
+
+// (x * y) mod (2^31 - 1) for x, y < 2^31
+__device__ __forceinline__ uint64_t ms_mul(uint64_t x, uint64_t y) {
+    const uint64_t p = x * y;
+    uint64_t r = (p & MS_M) + (p >> 31);
+    r = (r & MS_M) + (r >> 31);
+    return r >= MS_M ? r - MS_M : r;
+}
+// 16807^e mod (2^31 - 1): the engine e steps ahead (jump-ahead of the LCG)
+__device__ __forceinline__ uint64_t ms_pow(uint64_t e) {
+    uint64_t r = 1, base = 16807ull;
+    while (e) {
+        if (e & 1ull) r = ms_mul(r, base);
+        base = ms_mul(base, base);
+        e >>= 1;
+    }
+    return r;
+}
+// uid_u64 counting the engine values it takes
+__device__ __forceinline__ uint64_t ms_next_cnt(uint64_t& x, uint32_t& n) {
+    ++n;
+    return ms_next(x);
+}
+__device__ __forceinline__ uint64_t uid_u64_cnt(uint64_t& x, uint32_t& n) {
+    uint64_t ret, tmp;
+    do {
+        uint64_t mid, mtmp;
+        do {
+            uint64_t r;
+            do r = ms_next_cnt(x, n) - MS_MIN;
+            while (r >= C_PAST);
+            mtmp = UR * (r / C_SCALING);
+            mid = mtmp + (ms_next_cnt(x, n) - MS_MIN);
+        } while (mid > Q1 || mid < mtmp);
+        tmp = UR * mid;
+        ret = tmp + (ms_next_cnt(x, n) - MS_MIN);
+    } while (ret < tmp);
     return ret;
 }
 
@@ -195,11 +234,11 @@ __global__ __launch_bounds__(RRNG_BLOCK) void k_rrng_scan2(LoopBuffers b, uint32
         __syncthreads();
     }
     if (threadIdx.x != 0) return;
-    // the round's draws: one engine seeded by the next random_device value (resample_clauses,
+    // the round's engine: seeded by the next random_device value (resample_clauses,
     // SATInstance.h:343-350, T = 1); ceil(bits / 63) 64-bit draws serve every bit
     const uint64_t bits = s_carry;
     uint64_t rd = st->rd_state;
-    uint64_t x = ms_seed(rd_next(rd));
+    st->rd_x0 = ms_seed(rd_next(rd));
     st->rd_state = rd;
     st->rd_bits = bits;
     const uint64_t draws = (bits + 62) / 63;
@@ -208,7 +247,72 @@ __global__ __launch_bounds__(RRNG_BLOCK) void k_rrng_scan2(LoopBuffers b, uint32
         st->done = 3;
         return;
     }
-    for (uint64_t d = 0; d < draws; ++d) b.rrng_stream[d] = uid_u64(x);
+    st->rd_draws = (uint32_t)draws;
+    st->rd_n = (uint32_t)min<uint64_t>(draws * RRNG_POS_PER_DRAW + 64, b.rrng_nmax);
+    st->rd_fail = 0;
+}
+
+// The round's draws in parallel.  Engine position i (1-based: the i-th value the seeded engine
+// returns) holds x0 * 16807^i mod (2^31 - 1), so every position's value is known without the
+// ones before it; a draw that starts at position i takes n(i) values (3, plus 2 per redrawn
+// middle level, ~1 in 5) and yields v(i), both functions of the values from i on:
+//   k_rrng_pos      a thread per position: jump[0][i] = i + n(i) (the next draw's start), val[i];
+//   k_rrng_lift(t)  jump[t + 1][i] = jump[t][jump[t][i]]: 2^(t+1) draws on;
+//   k_rrng_collect  a thread per draw k: its start = position 1 advanced by the bits of k, its
+//                   value val[start];
+//   k_rrng_seq      the one-thread chain, only when the draws ran past the positions considered
+//                   (more than RRNG_POS_PER_DRAW values per draw on average: not seen).
+__global__ __launch_bounds__(256) void k_rrng_pos(LoopBuffers b) {
+    const DevState* st = b.state;
+    if (!st->active || st->done == 3) return;
+    const uint32_t n = st->rd_n;
+    const uint64_t x0 = st->rd_x0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x + 1; i <= (uint64_t)n + 1; i += stride) {
+        if (i == (uint64_t)n + 1) {
+            b.rrng_jump[i] = n + 1;  // (the sentinel past the positions)
+            continue;
+        }
+        uint64_t x = ms_mul(x0, ms_pow(i - 1));  // the state whose next value is position i's
+        uint32_t used = 0;
+        b.rrng_val[i] = uid_u64_cnt(x, used);
+        b.rrng_jump[i] = (uint32_t)min<uint64_t>(i + used, (uint64_t)n + 1);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_rrng_lift(LoopBuffers b, uint32_t t) {
+    const DevState* st = b.state;
+    if (!st->active || st->done == 3) return;
+    const uint32_t d = st->rd_draws;
+    if (d < 2 || (uint64_t)(d - 1) >> (t + 1) == 0) return;  // (level t + 1 is not needed for k < d)
+    const uint32_t n = st->rd_n, w = b.rrng_nmax + 2;
+    const uint32_t* j0 = b.rrng_jump + (uint64_t)t * w;
+    uint32_t* j1 = b.rrng_jump + (uint64_t)(t + 1) * w;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x + 1; i <= (uint64_t)n + 1; i += stride)
+        j1[i] = j0[j0[i]];
+}
+
+__global__ __launch_bounds__(256) void k_rrng_collect(LoopBuffers b) {
+    DevState* st = b.state;
+    if (!st->active || st->done == 3) return;
+    const uint32_t d = st->rd_draws, n = st->rd_n, w = b.rrng_nmax + 2;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < d; k += stride) {
+        uint32_t pos = 1;
+        for (uint32_t t = 0; (k >> t) != 0; ++t)
+            if ((k >> t) & 1ull) pos = b.rrng_jump[(uint64_t)t * w + pos];
+        if (pos > n) st->rd_fail = 1u;
+        else b.rrng_stream[k] = b.rrng_val[pos];
+    }
+}
+
+__global__ void k_rrng_seq(LoopBuffers b) {
+    const DevState* st = b.state;
+    if (threadIdx.x != 0 || !st->active || st->done == 3 || !st->rd_fail) return;
+    uint64_t x = st->rd_x0;
+    const uint32_t d = st->rd_draws;
+    for (uint32_t k = 0; k < d; ++k) b.rrng_stream[k] = uid_u64(x);
 }
 
 __global__ __launch_bounds__(RRNG_BLOCK) void k_rrng_apply(ClauseView cv, LoopBuffers b, uint32_t n_mask_words) {
@@ -252,6 +356,11 @@ hipError_t launch_refrng_resample(const ClauseView& cv, const LoopBuffers& b, hi
     k_rrng_mark<<<b.n_tiles + 1, 256, 0, s>>>(cv, b);
     k_rrng_scan1<<<nblk, RRNG_BLOCK, 0, s>>>(b, (uint32_t)nmw);
     k_rrng_scan2<<<1, RRNG_BLOCK, 0, s>>>(b, nblk);
+    const uint32_t gp = (uint32_t)std::min<uint64_t>(((uint64_t)b.rrng_nmax + 2 + 255) / 256, 2048);
+    k_rrng_pos<<<gp, 256, 0, s>>>(b);
+    for (uint32_t t = 0; t + 1 < b.rrng_levels; ++t) k_rrng_lift<<<gp, 256, 0, s>>>(b, t);
+    k_rrng_collect<<<(uint32_t)std::min<uint64_t>((b.rrng_cap + 255) / 256, 2048), 256, 0, s>>>(b);
+    k_rrng_seq<<<1, 64, 0, s>>>(b);
     k_rrng_apply<<<nblk, RRNG_BLOCK, 0, s>>>(cv, b, (uint32_t)nmw);
     return hipGetLastError();
 }

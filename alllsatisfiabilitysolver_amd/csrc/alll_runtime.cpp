@@ -1249,6 +1249,19 @@ int alll_create(const alll_problem* prob, const alll_options* opt_in, alll_ctx**
             return bail(rc);
         b.rrng_cap = L / 63 + 2;  // a round draws ceil(bits / 63), bits <= every literal
         if ((rc = dalloc(c, &b.rrng_stream, (size_t)b.rrng_cap))) return bail(rc);
+        // the parallel draws (alll_refrng.hip): engine positions for RRNG_POS_PER_DRAW per draw,
+        // jump levels until 2^levels exceeds the most draws a round can take
+        uint64_t nmax = std::min<uint64_t>(b.rrng_cap * RRNG_POS_PER_DRAW + 64, 0xFFFFFFF0ull);
+        // (test knob: fewer positions, so that the parallel draws run past them and the
+        // one-thread chain redoes the round)
+        if (const char* e = getenv("ALLL_RRNG_NMAX"))
+            if (*e) nmax = std::max<uint64_t>(8, std::min<uint64_t>(nmax, strtoull(e, nullptr, 10)));
+        b.rrng_nmax = (uint32_t)nmax;
+        b.rrng_levels = 1;
+        while ((1ull << b.rrng_levels) <= b.rrng_cap) ++b.rrng_levels;
+        if ((rc = dalloc(c, &b.rrng_jump, (size_t)b.rrng_levels * (nmax + 2))) ||
+            (rc = dalloc(c, &b.rrng_val, (size_t)nmax + 2)))
+            return bail(rc);
         if (opt.stream_batch && (rc = dalloc(c, &b.rrng_map, (size_t)m))) return bail(rc);
     } else if (refrng) {
         // (no clauses: the initial fill still draws; the mask pointer marks the mode)

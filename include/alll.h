@@ -71,9 +71,9 @@ typedef struct alll_problem {
                                                  1442695040888963407, value x >> 33): the initial
                                                  fill (VariablesArray.h:23-34) and every resample
                                                  round (SATInstance.h:340-365, T = 1) then equal the
-                                                 reference's, bit for bit.  One thread generates each
-                                                 round's draws (a verification mode, not the fast
-                                                 path).  n_threads = 1 (also for the streaming
+                                                 reference's, bit for bit (the draws in parallel by
+                                                 jump-ahead; about half the Philox loop's rate at
+                                                 10M clauses).  n_threads = 1 (also for the streaming
                                                  solve: bits in yield order), one GPU:
                                                  ALLL_ERR_UNSUPPORTED otherwise */
 

@@ -160,6 +160,21 @@ def test_reference_rng_stream_matches_oracle(gpu, native, oracle_mod, bs):
             assert st[key] == st_o[key], key
 
 
+def test_reference_rng_sequential_fallback(gpu, native, oracle_mod, monkeypatch):
+    """ALLL_RRNG_NMAX caps the engine positions the parallel draws consider, so every round runs
+    past them and the one-thread chain (k_rrng_seq) redoes it: the same trajectory."""
+    from alllsatisfiabilitysolver_amd import Solver, generate_ksat
+
+    n, m, rd = 20000, 80000, 23
+    offs, lits = generate_ksat(1, n, m, 3, 0)
+    st_o, A_o, rows = oracle_mod.solve_refrng(n, offs, lits, rd, max_iters=6, trace=True)
+    monkeypatch.setenv("ALLL_RRNG_NMAX", "40")
+    with Solver(n, offs, lits, seed=rd, flags=native.FLAG_REFERENCE_RNG) as s:
+        for it, nu, nm, dres, A_after in rows:
+            s.run(1)
+            np.testing.assert_array_equal(s.assignment_words(), A_after, err_msg=f"A after iteration {it}")
+
+
 def test_reference_rng_refusals(gpu, native):
     from alllsatisfiabilitysolver_amd import AlllError, Solver, generate_ksat
 

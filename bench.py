@@ -380,6 +380,8 @@ def main():
                          "one-GPU loop; auto = alll_plan_multi_gpu's cost model (DESIGN.md §5.2)")
     ap.add_argument("--no-shard-line", action="store_true",
                     help="N>1 with the replicated plan: skip the secondary run of the sharded (exchange) path")
+    ap.add_argument("--shard-line-timeout", type=float, default=180.0,
+                    help="seconds the secondary sharded run may take before the line is written without it")
     ap.add_argument("--stream-line", default="4:100000",
                     help="T:BATCH -- also run the streaming solve with T generators of BATCH clauses "
                          "(GPU rate, and the oracle's first iterations as its CPU baseline and check); "
@@ -630,10 +632,37 @@ def main():
             },
         }
     s.close()
+    run_done = __import__("threading").Event()  # (set once the line is out and the ranks are torn down)
+    emitted = []
+
+    def emit(o):
+        if not emitted:
+            emitted.append(True)
+            result_out.write(json.dumps(o) + "\n")
+            result_out.flush()
+
     if world > 1 and plan == "replicate" and not args.no_shard_line:
         # the clause-sharded path (exchange every iteration) on the same instance, so that a
         # multi-GPU run still exercises and checks it: its own rate and trajectory check
-        sh = shard_line(args, n, offs, lits, kw, rank, world, exchange_impl, comm_id, dist, barrier, torch)
+        # (a watchdog keeps the headline: if the sharded run and the teardown after it have not
+        # finished in time -- a collective that never completes -- rank 0 writes the line as it
+        # stands and every rank exits; an error inside the sharded run is reported, not fatal)
+        import threading
+
+        def _watchdog():
+            if not run_done.wait(args.shard_line_timeout):
+                if rank == 0:
+                    out.setdefault("shard_line", {"value": None,
+                                                  "error": f"did not finish within {args.shard_line_timeout:.0f} s"})
+                    emit(out)
+                log(f"[rank {rank}] sharded line timed out; exiting")
+                os._exit(0)
+
+        threading.Thread(target=_watchdog, daemon=True).start()
+        try:
+            sh = shard_line(args, n, offs, lits, kw, rank, world, exchange_impl, comm_id, dist, barrier, torch)
+        except Exception as e:
+            sh = {"value": None, "error": f"{type(e).__name__}: {e}"}
         del offs, lits
         if rank == 0:
             out["shard_line"] = sh
@@ -659,11 +688,11 @@ def main():
         except Exception as e:  # reported, never fatal for the GPU number
             out["cpu_baseline"] = {"value": None, "error": str(e)}
     if rank == 0:
-        result_out.write(json.dumps(out) + "\n")
-        result_out.flush()
+        emit(out)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
+    run_done.set()
     rr = (out or {}).get("gpu_same_mis_as_cpu_baseline") or {}
     bad = [name for name, t in (("T=1 loop", traj), ("round robin", rr.get("trajectory_check")),
                                 ("streaming solve", ((out or {}).get("stream_line") or {}).get("check")),

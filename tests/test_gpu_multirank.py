@@ -215,7 +215,7 @@ def _bench_stdout(args, env_extra=None):
     return json.loads(lines[0])
 
 
-@pytest.mark.parametrize("mode", ["rccl_self", "host_n2", "host_n2_shard"])
+@pytest.mark.parametrize("mode", ["rccl_self", "host_n2", "host_n2_shard", "host_n2_watchdog"])
 def test_bench_prints_one_json_line(mode):
     """The driver reads one JSON line from bench.py's stdout: RCCL's banner at communicator
     init and the rank processes' output must not reach it (N=1 over a one-rank RCCL
@@ -227,14 +227,18 @@ def test_bench_prints_one_json_line(mode):
         d = _bench_stdout(common + ["--rccl-self"])
         assert d["n_gpus"] == 1 and d["config"]["exchange"] == "allgather/rccl-self"
     else:
-        extra = ["--plan", "shard"] if mode == "host_n2_shard" else []
+        extra = (["--plan", "shard"] if mode == "host_n2_shard" else
+                 ["--shard-line-timeout", "0.01"] if mode == "host_n2_watchdog" else [])
         d = _bench_stdout(common + ["--gpus", "2", "--exchange-impl", "host"] + extra, {"ALLL_BENCH_SAME_DEVICE": "1"})
         assert d["n_gpus"] == 2 and d["ranks_seen"] == 2
         mp = d["multi_gpu_plan"]
-        assert mp["plan"] == "replicate" and mp["requested"] == ("shard" if extra else "auto")
-        if extra:
+        assert mp["plan"] == "replicate" and mp["requested"] == ("shard" if mode == "host_n2_shard" else "auto")
+        if mode == "host_n2_shard":
             assert mp["chosen"] == "shard" and d["config"]["parallelism"] == "clause-shard x2"
             assert "shard_line" not in d
+        elif mode == "host_n2_watchdog":
+            # the sharded run cannot finish in 10 ms: the headline is written without it
+            assert mp["chosen"] == "replicate" and "did not finish" in d["shard_line"]["error"]
         else:
             assert mp["chosen"] == "replicate" and d["config"]["parallelism"] == "replicated x2"
             sl = d["shard_line"]

@@ -7,7 +7,7 @@ cd "$(dirname "$0")/.."
 NAME=$1; FLAGS=$2
 D=$(mktemp -d /tmp/abv.XXXX)
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -Iinclude -Ialllsatisfiabilitysolver_amd/csrc -I/opt/rocm/include $FLAGS"
-for f in alll_kernels.hip alll_runtime.cpp alll_host.cpp; do
+for f in $(cd alllsatisfiabilitysolver_amd/csrc && ls *.hip *.cpp); do
   /opt/rocm/bin/hipcc $F -c -o $D/${f%.*}.o alllsatisfiabilitysolver_amd/csrc/$f &
 done
 wait

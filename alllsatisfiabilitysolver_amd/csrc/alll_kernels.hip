@@ -439,6 +439,9 @@ __device__ __forceinline__ void eval_hybrid_body(const ClauseView& cv, const Loo
     const uint32_t wbits = __popc(cv.lit_mask) - 6u;  // word-index bits of a literal
     const auto rsV = __builtin_amdgcn_make_buffer_rsrc(
         (void*)b.vmask, (short)0, (int)__builtin_amdgcn_readfirstlane(b.n_tiles * (TILE_WORDS * 8u)), 0x00020000);
+    // (EV_FLAGS: the clause-order flag bytes)
+    const auto rsF = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)b.rr_flag, (short)0, (int)__builtin_amdgcn_readfirstlane(MODE == EV_FLAGS ? b.n_tiles * TILE : 0u), 0x00020000);
     // The four lookups of one literal slot (the lane's four clauses): the assignment word of
     // literal xs[q]'s variable, from LDS when the window holds it, else from L2.  Branch-free
     // per lane: a word a lane does not need from LDS (outside the window, or need[q] == false:
@@ -589,19 +592,38 @@ __device__ __forceinline__ void eval_hybrid_body(const ClauseView& cv, const Loo
             if constexpr (MODE == EV_FLAGS) {
                 const uint32_t tile = (uint32_t)(g / (TILE / CHUNK));
                 if (lane == 0 && tot) atomicAdd(&s_tcnt[tile - pt], tot);
+                if (cv.id_bits) {
+                    // Packed ids: four byte stores per chunk without branches (the satisfied
+                    // clauses' to an out-of-range offset), so that, as for the bitmask above, the
+                    // wait for the next chunk's literals need not wait for these scattered
+                    // stores (with a branch per store the count varies: 51.8 -> 48.9 us at M,
+                    // T = 16, profiles/r6_checks/rr/eval_flags_branchfree_ab.txt).
+                    const uint32_t fm = ((1u << cv.id_bits) - 1u) << cv.id_shift;
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    if (!v[q]) continue;
-                    Ent<K> e;
-                    uint32_t t[K];
+                    for (int q = 0; q < 4; ++q) {
+                        uint32_t id = 0;
 #pragma unroll
-                    for (int j = 0; j < K; ++j) {
-                        const uint32_t xs[4] = {x[j].x, x[j].y, x[j].z, x[j].w};
-                        t[j] = xs[q];
+                        for (int j = 0; j < K; ++j) {
+                            const uint32_t xs[4] = {x[j].x, x[j].y, x[j].z, x[j].w};
+                            id |= ((xs[q] & fm) >> cv.id_shift) << (j * cv.id_bits);
+                        }
+                        __builtin_amdgcn_raw_buffer_store_b8((uint8_t)1u, rsF, v[q] ? id : 0x80000000u, 0, 0);
                     }
-                    make_ent<K>(e, c0 + q, t);
-                    ent_unpack<K>(cv, e);
-                    b.rr_flag[e.w[0]] = 1u;
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        if (!v[q]) continue;
+                        Ent<K> e;
+                        uint32_t t[K];
+#pragma unroll
+                        for (int j = 0; j < K; ++j) {
+                            const uint32_t xs[4] = {x[j].x, x[j].y, x[j].z, x[j].w};
+                            t[j] = xs[q];
+                        }
+                        make_ent<K>(e, c0 + q, t);
+                        ent_unpack<K>(cv, e);
+                        b.rr_flag[e.w[0]] = 1u;
+                    }
                 }
             } else if (K <= 4 || tot) {
                 const uint32_t tile = (uint32_t)(g / (TILE / CHUNK));
